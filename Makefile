@@ -1,0 +1,38 @@
+# libgfslam (HIP, gfx950) + the CPU oracle (test infrastructure).
+HIPCC   ?= /opt/rocm/bin/hipcc
+CXX     ?= g++
+ARCH    ?= gfx950
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+           -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function
+ORCFLAGS = -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+
+CSRC    = gf_orb_slam_amd/csrc
+HIPSRCS = $(wildcard $(CSRC)/*.hip)
+HIPOBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIPSRCS))
+HDRS    = $(wildcard $(CSRC)/*.h) include/gfslam/abi.h
+LIB     = gf_orb_slam_amd/libgfslam.so
+
+ORCSRCS = $(wildcard oracle/*.cpp)
+ORCLIB  = oracle/liboracle.so
+
+all: $(LIB) $(ORCLIB)
+
+build/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIPOBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+
+$(ORCLIB): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h include/gfslam/abi.h
+	$(CXX) $(ORCFLAGS) -shared $(ORCSRCS) -o $@
+
+clean:
+	rm -rf build $(LIB) $(ORCLIB)
+
+.PHONY: all clean
+
+SELCHECK = tests/helpers/libselcheck.so
+all: $(SELCHECK)
+$(SELCHECK): tests/helpers/select_check.cpp $(CSRC)/select.h
+	$(CXX) -O2 -std=c++17 -fPIC -shared $< -o $@

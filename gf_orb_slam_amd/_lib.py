@@ -1,0 +1,102 @@
+"""ctypes binding of libgfslam.so (the C-ABI declared in include/gfslam/abi.h).
+
+The product path always goes through this library: if libgfslam.so is missing
+or no HIP device is present, every operator raises instead of falling back to
+any CPU implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgfslam.so")
+ABI_HEADER = os.path.join(os.path.dirname(_HERE), "include", "gfslam", "abi.h")
+
+GF_OK = 0
+ERRORS = {-1: "GF_ERR_ARG", -2: "GF_ERR_HIP", -3: "GF_ERR_CAP", -4: "GF_ERR_UNSUPPORTED", -5: "GF_ERR_NODEV"}
+
+
+class GFError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class KeyPoint(ctypes.Structure):
+    """cv::KeyPoint layout (28 bytes)."""
+
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float),
+                ("angle", ctypes.c_float), ("response", ctypes.c_float),
+                ("octave", ctypes.c_int32), ("class_id", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        # torch bundles its own libamdhip64.so.7; load it first so that this
+        # process has exactly one HIP runtime (libgfslam binds to the loaded
+        # soname) and torch device buffers / streams can be handed to the ABI.
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional plumbing
+            pass
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.gf_last_error.restype = ctypes.c_char_p
+        _declare(_lib)
+    return _lib
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_D = ctypes.c_double
+_S = ctypes.c_size_t
+_PROTOS = {
+    "gf_device_count": [_P],
+    "gf_ctx_create": [_I, _P],
+    "gf_ctx_destroy": [_P],
+    "gf_ctx_stream": [_P, _P],
+    "gf_ctx_sync": [_P],
+    "gf_extractor_create": [_P, _I, _F, _I, _I, _I, _I, _I, _I, _P],
+    "gf_extractor_destroy": [_P],
+    "gf_extractor_info": [_P, _P, _P, _P],
+    "gf_extractor_capacity": [_P, _P],
+    "gf_orb_extract": [_P, _P, _I, _P, _P, _I, _P],
+    "gf_orb_extract_batch_dev": [_P, _I, _P, _S, _I, _P, _P, _P, _I, _P],
+    "gf_extractor_debug_level": [_P, _I, _I, _I, _P, _P, _P],
+}
+
+
+def _declare(l) -> None:
+    for name, args in _PROTOS.items():
+        fn = getattr(l, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+
+
+def check(rc: int) -> None:
+    if rc != GF_OK:
+        raise GFError(rc, lib().gf_last_error().decode(errors="replace"))
+
+
+def declared_symbols() -> list[str]:
+    """Every function the ABI header declares (for the export test)."""
+    src = open(ABI_HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gf_[a-z0-9_]+)\s*\(", src)))
+
+
+def ptr(a):
+    """Host numpy array or torch tensor -> c_void_p."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    return ctypes.c_void_p(a.ctypes.data)

@@ -1,0 +1,50 @@
+// Shared runtime pieces of libgfslam: error capture, context, device helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/gfslam/abi.h"
+
+namespace gf {
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define GF_HIP(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return ::gf::fail(GF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define GF_CHECK(cond, code, msg)                     \
+    do {                                              \
+        if (!(cond)) return ::gf::fail((code), (msg)); \
+    } while (0)
+
+}  // namespace gf
+
+struct gf_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+};
+
+// Device-side helpers ------------------------------------------------------
+namespace gfd {
+
+__device__ __forceinline__ int reflect101(int p, int len) {
+    // BORDER_REFLECT_101 for the <= 18 px excursions the kernels make.
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - p - 2;
+    return p;
+}
+
+__device__ __forceinline__ int warp_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace gfd

@@ -1,0 +1,921 @@
+// ORB extraction on gfx950 — SURVEY.md §8a rows E1-E7.
+//
+// Replaces ORB_SLAM::ORBextractor (src/ORBextractor.cc:464-998) for a batch
+// of independent frames. Pipeline per batch (all kernels batched over frames,
+// one HIP stream, no host round trip):
+//
+//   k_resize  x (nlevels-1)  level l from level l-1 (cv::resize INTER_LINEAR,
+//                            11-bit fixed point; ComputePyramid :922-998)
+//   k_blur                   7x7 sigma-2 Gaussian of every level (:842)
+//   k_fast                   one workgroup per (frame, grid cell): FAST-9 +
+//                            score + in-cell NMS, threshold fallback 20 -> 7,
+//                            row-major compaction (ComputeKeyPoints :575-689)
+//   k_select                 one workgroup per (frame, level): quota
+//                            redistribution (:695-721) + retainBest per cell
+//                            and per level (:734-752)
+//   k_describe               one wave per keypoint: IC_Angle (:131-158) on
+//                            the unblurred level, rBRIEF (:162-201) on the
+//                            blurred level, scale to level 0 (:865-871)
+//
+// Levels are stored without the 16-px border frame: every border read the
+// reference makes is reflect-101 of the level interior, so it is addressed on
+// the fly (reflect101) instead of materialised.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "orb_pattern.h"
+#include "select.h"
+
+#define GF_MAX_LEVELS 12
+
+namespace {
+
+__constant__ int c_pattern[256 * 4];
+__constant__ int c_umax[16];
+
+struct LevelGeom {
+    int nlevels;
+    int w[GF_MAX_LEVELS], h[GF_MAX_LEVELS];
+    long long off[GF_MAX_LEVELS];   // pyramid slab offset (levels >= 1)
+    long long boff[GF_MAX_LEVELS];  // blurred slab offset (all levels)
+    long long slab, bslab;          // bytes per frame
+    float scale[GF_MAX_LEVELS];
+    // cells
+    int cell_begin[GF_MAX_LEVELS + 1];
+    int ncells;
+    int nfcell[GF_MAX_LEVELS], ndesired[GF_MAX_LEVELS];
+    long long lvl_off[GF_MAX_LEVELS + 1];  // level list offsets (entries)
+    // blur tiling
+    int tile_begin[GF_MAX_LEVELS + 1];
+    int tiles_x[GF_MAX_LEVELS];
+};
+
+struct CellInfo {
+    int level, x0, y0, w, h, valid;
+    long long cap_off;
+    int cap, pad;
+};
+
+struct Planes {
+    const uint8_t* img0;
+    long long fstride0;
+    int stride0;
+    uint8_t* pyr;
+    uint8_t* blur;
+};
+
+__device__ __forceinline__ const uint8_t* level_plane(const Planes& P, const LevelGeom& g, int f, int l,
+                                                      int& stride) {
+    if (l == 0) {
+        stride = P.stride0;
+        return P.img0 + (long long)f * P.fstride0;
+    }
+    stride = g.w[l];
+    return P.pyr + (long long)f * g.slab + g.off[l];
+}
+
+// -------------------------------------------------------------- k_resize
+// One thread per destination pixel. xtab[dx] = (sx, a0 | a1<<16),
+// ytab[dy] = (sy, b0 | b1<<16) precomputed on the host with OpenCV's float
+// coefficient arithmetic.
+__global__ void k_resize(Planes P, LevelGeom g, int l, const int2* __restrict__ xtab,
+                         const int2* __restrict__ ytab) {
+    const int f = blockIdx.z;
+    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int dy = blockIdx.y * blockDim.y + threadIdx.y;
+    const int dw = g.w[l], dh = g.h[l], sw = g.w[l - 1], sh = g.h[l - 1];
+    if (dx >= dw || dy >= dh) return;
+    int sstride;
+    const uint8_t* S = level_plane(P, g, f, l - 1, sstride);
+    uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l];
+    int2 xt = xtab[dx], yt = ytab[dy];
+    int sx = xt.x, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
+    int sy0 = min(max(yt.x, 0), sh - 1), sy1 = min(max(yt.x + 1, 0), sh - 1);
+    int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
+    const uint8_t* r0 = S + (long long)sy0 * sstride;
+    const uint8_t* r1 = S + (long long)sy1 * sstride;
+    int t0, t1;
+    if (sx + 1 < sw) {
+        t0 = r0[sx] * a0 + r0[sx + 1] * a1;
+        t1 = r1[sx] * a0 + r1[sx + 1] * a1;
+    } else {
+        t0 = r0[sx] * 2048;
+        t1 = r1[sx] * 2048;
+    }
+    int v = (((b0 * (t0 >> 4)) >> 16) + ((b1 * (t1 >> 4)) >> 16) + 2) >> 2;
+    D[(long long)dy * dw + dx] = (uint8_t)min(max(v, 0), 255);
+}
+
+// -------------------------------------------------------------- k_blur
+// 64x16 output tile per 256-thread workgroup; reflect-101 halo of 3 px staged
+// in LDS; integer row pass then column pass with the (s + 2^15) >> 16 cast.
+#define BT_W 64
+#define BT_H 16
+__global__ __launch_bounds__(256) void k_blur(Planes P, LevelGeom g) {
+    __shared__ uint8_t src[BT_H + 6][BT_W + 6 + 2];
+    __shared__ int rows[BT_H + 6][BT_W];
+    const int f = blockIdx.y;
+    int t = blockIdx.x, l = 0;
+    while (l + 1 < g.nlevels && t >= g.tile_begin[l + 1]) l++;
+    t -= g.tile_begin[l];
+    const int tx = t % g.tiles_x[l], ty = t / g.tiles_x[l];
+    const int w = g.w[l], h = g.h[l];
+    const int X0 = tx * BT_W, Y0 = ty * BT_H;
+    int stride;
+    const uint8_t* S = level_plane(P, g, f, l, stride);
+    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l];
+    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
+        int ry = i / (BT_W + 6), rx = i % (BT_W + 6);
+        int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+        int xx = gfd::reflect101(min(X0 + rx - 3, w + 2), w);
+        src[ry][rx] = S[(long long)yy * stride + xx];
+    }
+    __syncthreads();
+    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;  // round(256 * gaussian(7, sigma 2))
+    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
+        int ry = i / BT_W, rx = i % BT_W;
+        const uint8_t* p = &src[ry][rx];
+        rows[ry][rx] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
+        int ry = i / BT_W, rx = i % BT_W;
+        int y = Y0 + ry, x = X0 + rx;
+        if (y >= h || x >= w) continue;
+        int s = k0 * (rows[ry][rx] + rows[ry + 6][rx]) + k1 * (rows[ry + 1][rx] + rows[ry + 5][rx]) +
+                k2 * (rows[ry + 2][rx] + rows[ry + 4][rx]) + k3 * rows[ry + 3][rx];
+        int v = (s + (1 << 15)) >> 16;
+        D[(long long)y * w + x] = (uint8_t)min(max(v, 0), 255);
+    }
+}
+
+// -------------------------------------------------------------- FAST-9
+__device__ __forceinline__ void circle_vals(const uint8_t* roi, int rw, int px, int py, int c[16]) {
+    const uint8_t* p = roi + py * rw + px;
+    c[0] = p[3 * rw];
+    c[1] = p[3 * rw + 1];
+    c[2] = p[2 * rw + 2];
+    c[3] = p[rw + 3];
+    c[4] = p[3];
+    c[5] = p[-rw + 3];
+    c[6] = p[-2 * rw + 2];
+    c[7] = p[-3 * rw + 1];
+    c[8] = p[-3 * rw];
+    c[9] = p[-3 * rw - 1];
+    c[10] = p[-2 * rw - 2];
+    c[11] = p[-rw - 3];
+    c[12] = p[-3];
+    c[13] = p[rw - 3];
+    c[14] = p[2 * rw - 2];
+    c[15] = p[3 * rw - 1];
+}
+
+// Segment test (>= 9 contiguous darker/brighter by more than th) and, for a
+// corner, OpenCV cornerScore<16>. Returns 0x100 | score, or 0.
+__device__ int fast_score(int v, const int c[16], int th) {
+    unsigned dark = 0, bright = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        dark |= (unsigned)(c[k] < v - th) << k;
+        bright |= (unsigned)(c[k] > v + th) << k;
+    }
+    // 9 contiguous set bits on the 16-ring: AND of 9 rotations.
+    unsigned d2 = dark | (dark << 16), b2 = bright | (bright << 16);
+    unsigned dm = d2, bm = b2;
+#pragma unroll
+    for (int s = 1; s < 9; s++) {
+        dm &= d2 >> s;
+        bm &= b2 >> s;
+    }
+    if (((dm | bm) & 0xffff) == 0) return 0;
+    int d[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) d[k] = v - c[k & 15];
+    int a0 = th;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(min(d[k + 1], d[k + 2]), d[k + 3]);
+        if (a <= a0) continue;
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(max(d[k + 1], d[k + 2]), d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        if (b >= b0) continue;
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return 0x100 | ((-b0 - 1) & 0xff);
+}
+
+// Exclusive scan of one int per thread across a 256-thread workgroup.
+__device__ int block_scan_256(int v, int* tmp, int& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) tmp[wid] = x;
+    __syncthreads();
+    int base = 0;
+    for (int i = 0; i < wid; i++) base += tmp[i];
+    total = tmp[0] + tmp[1] + tmp[2] + tmp[3];
+    __syncthreads();
+    return base + x - v;
+}
+
+// One workgroup per (grid cell, frame). LDS holds the cell ROI (w x h u8, the
+// 3-px FAST margin included) and the per-pixel score map of the detection
+// window ((w-6) x (h-6), u16: 0x100 flags a corner).
+__global__ __launch_bounds__(256) void k_fast(Planes P, LevelGeom g, const CellInfo* __restrict__ cells,
+                                              uint32_t* __restrict__ lists, long long list_stride,
+                                              int* __restrict__ counts, int fast_th, int min_th) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ int scan_tmp[4];
+    const int f = blockIdx.y, cid = blockIdx.x;
+    const CellInfo ci = cells[cid];
+    if (!ci.valid) {
+        if (threadIdx.x == 0) counts[(long long)f * g.ncells + cid] = 0;
+        return;
+    }
+    const int rw = ci.w, rh = ci.h, dw = rw - 6, dh = rh - 6;
+    const int n = (dw > 0 && dh > 0) ? dw * dh : 0;  // degenerate ROI: FAST finds nothing
+    uint8_t* roi = smem;
+    uint16_t* sc = (uint16_t*)(smem + ((rw * rh + 15) & ~15));
+    int stride;
+    const uint8_t* S = level_plane(P, g, f, ci.level, stride);
+    for (int i = threadIdx.x; i < rw * rh; i += 256) {
+        int ry = i / rw, rx = i - ry * rw;
+        roi[i] = S[(long long)(ci.y0 + ry) * stride + ci.x0 + rx];
+    }
+    __syncthreads();
+    uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
+    const int chunk = (n + 255) / 256;
+    const int p0 = min(threadIdx.x * chunk, n), p1 = min(p0 + chunk, n);
+    for (int pass = 0; pass < 2; pass++) {
+        const int th = pass == 0 ? fast_th : min_th;
+        for (int p = threadIdx.x; p < n; p += 256) {
+            int py = p / dw + 3, px = p - (p / dw) * dw + 3;
+            int c[16];
+            circle_vals(roi, rw, px, py, c);
+            sc[p] = (uint16_t)fast_score(roi[py * rw + px], c, th);
+        }
+        __syncthreads();
+        int cnt = 0;
+        for (int p = p0; p < p1; p++) {
+            int s = sc[p];
+            if (!(s & 0x100)) continue;
+            int y = p / dw, x = p - y * dw, sv = s & 0xff;
+            bool keep = true;
+            for (int dy = -1; dy <= 1 && keep; dy++) {
+                int yy = y + dy;
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (!dx && !dy) continue;
+                    int xx = x + dx;
+                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? (sc[yy * dw + xx] & 0xff) : 0;
+                    if (!(sv > nb)) {
+                        keep = false;
+                        break;
+                    }
+                }
+            }
+            cnt += keep;
+        }
+        int total;
+        int off = block_scan_256(cnt, scan_tmp, total);
+        if (pass == 0 && total <= 3) {
+            __syncthreads();
+            continue;  // ORBextractor.cc:623-628: retry the cell with the minimum threshold
+        }
+        for (int p = p0; p < p1 && cnt > 0; p++) {
+            int s = sc[p];
+            if (!(s & 0x100)) continue;
+            int y = p / dw, x = p - y * dw, sv = s & 0xff;
+            bool keep = true;
+            for (int dy = -1; dy <= 1 && keep; dy++) {
+                int yy = y + dy;
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (!dx && !dy) continue;
+                    int xx = x + dx;
+                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? (sc[yy * dw + xx] & 0xff) : 0;
+                    if (!(sv > nb)) {
+                        keep = false;
+                        break;
+                    }
+                }
+            }
+            if (keep) {
+                out[off++] = ((uint32_t)sv << 24) | ((uint32_t)(ci.y0 + y + 3) << 12) | (uint32_t)(ci.x0 + x + 3);
+            }
+        }
+        if (threadIdx.x == 0) counts[(long long)f * g.ncells + cid] = total;
+        break;
+    }
+}
+
+// -------------------------------------------------------------- k_select
+// One workgroup per (level, frame).
+#define SEL_MAX_CELLS 1024
+__global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
+                                                uint32_t* __restrict__ lists, long long list_stride,
+                                                const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
+                                                long long lvl_stride, int* __restrict__ lvl_counts) {
+    __shared__ int cnt[SEL_MAX_CELLS], keep[SEL_MAX_CELLS], off[SEL_MAX_CELLS + 1];
+    __shared__ char valid[SEL_MAX_CELLS];
+    const int l = blockIdx.x, f = blockIdx.y;
+    const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        cnt[c] = counts[(long long)f * g.ncells + cb + c];
+        valid[c] = (char)cells[cb + c].valid;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // Quota redistribution, ORBextractor.cc:673-721. Cells skipped by the
+        // ROI loop (valid == 0) keep nTotal = 0, nToRetain = 0, bNoMore = false.
+        const int nf = g.nfcell[l];
+        int nNoMore = 0, nToDistribute = 0;
+        for (int c = 0; c < nc; c++) {
+            off[c] = 0;  // used as the noMore flag during redistribution
+            if (!valid[c]) {
+                keep[c] = 0;
+                continue;
+            }
+            if (cnt[c] > nf) {
+                keep[c] = nf;
+            } else {
+                keep[c] = cnt[c];
+                nToDistribute += nf - cnt[c];
+                off[c] = 1;
+                nNoMore++;
+            }
+        }
+        while (nToDistribute > 0 && nNoMore < nc) {
+            int nNew = nf + (int)ceilf((float)nToDistribute / (float)(nc - nNoMore));
+            nToDistribute = 0;
+            for (int c = 0; c < nc; c++) {
+                if (off[c]) continue;
+                if (cnt[c] > nNew) {
+                    keep[c] = nNew;
+                } else {
+                    keep[c] = cnt[c];
+                    nToDistribute += nNew - cnt[c];
+                    off[c] = 1;
+                    nNoMore++;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        if (!valid[c]) continue;
+        uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        keep[c] = gfsel::retain_best_truncate(a, cnt[c], keep[c], gfsel::RespGreater());
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int c = 0; c < nc; c++) {
+            off[c] = s;
+            s += valid[c] ? keep[c] : 0;
+        }
+        off[nc] = s;
+    }
+    __syncthreads();
+    uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+        if (!valid[c]) continue;
+        const uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        for (int i = 0; i < keep[c]; i++) L[off[c] + i] = a[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int total = off[nc];
+        total = gfsel::retain_best_truncate(L, total, g.ndesired[l], gfsel::RespGreater());
+        lvl_counts[(long long)f * g.nlevels + l] = total;
+    }
+}
+
+// -------------------------------------------------------------- k_describe
+__device__ float fast_atan2f(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// One wave per keypoint, 4 per workgroup.
+__global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const uint32_t* __restrict__ lvl_lists,
+                                                  long long lvl_stride, const int* __restrict__ lvl_counts,
+                                                  gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
+                                                  int* __restrict__ out_counts, int cap) {
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x & 63;
+    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    int total = 0, l = -1, idx = 0;
+    for (int i = 0; i < g.nlevels; i++) {
+        int c = lvl_counts[(long long)f * g.nlevels + i];
+        if (l < 0 && k < total + c) {
+            l = i;
+            idx = k - total;
+        }
+        total += c;
+    }
+    if (k == 0 && lane == 0) out_counts[f] = total;
+    if (l < 0) return;
+    const uint32_t e = lvl_lists[(long long)f * lvl_stride + g.lvl_off[l] + idx];
+    const int x = e & 0xfff, y = (e >> 12) & 0xfff, score = e >> 24;
+    const int w = g.w[l], h = g.h[l];
+    int stride;
+    const uint8_t* Pl = level_plane(P, g, f, l, stride);
+    const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[l];
+
+    // IC_Angle: lane r < 31 owns row v = r - 15 of the circular patch.
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        int v = lane - 15, d = c_umax[v < 0 ? -v : v], s = 0;
+        const uint8_t* row = Pl + (long long)(y + v) * stride + x;
+        for (int u = -d; u <= d; u++) {
+            int p = row[u];
+            s += p;
+            m10 += u * p;
+        }
+        m01 = v * s;
+    }
+    m10 = gfd::warp_sum(m10);
+    m01 = gfd::warp_sum(m01);
+    const float angle = fast_atan2f((float)m01, (float)m10);
+
+    // rBRIEF: lane b < 32 computes descriptor byte b.
+    if (lane < 32) {
+        const float factorPI = (float)(M_PI / 180.f);
+        const float ang = angle * factorPI;
+        const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+        int val = 0;
+#pragma unroll
+        for (int bit = 0; bit < 8; bit++) {
+            int t[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                int pi = lane * 16 + bit * 2 + q;
+                float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
+                int ry = __float2int_rn(px * b + py * a);
+                int rx = __float2int_rn(px * a - py * b);
+                int xx = x + rx, yy = y + ry;
+                if (xx >= 0 && xx < w && yy >= 0 && yy < h)
+                    t[q] = B[(long long)yy * w + xx];
+                else
+                    t[q] = Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
+            }
+            val |= (t[0] < t[1]) << bit;
+        }
+        desc[((long long)f * cap + k) * 32 + lane] = (uint8_t)val;
+    }
+    if (lane == 0) {
+        gf_keypoint kp;
+        float s = g.scale[l];
+        kp.x = l ? (float)x * s : (float)x;
+        kp.y = l ? (float)y * s : (float)y;
+        kp.size = (float)(int)(31 * s);
+        kp.angle = angle;
+        kp.response = (float)score;
+        kp.octave = l;
+        kp.class_id = -1;
+        kps[(long long)f * cap + k] = kp;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== host
+struct gf_extractor {
+    gf_ctx* ctx = nullptr;
+    int nfeatures = 0, nlevels = 0, fast_th = 20, min_th = 7, width = 0, height = 0, max_batch = 0;
+    float scale_factor = 1.2f;
+    LevelGeom g{};
+    std::vector<CellInfo> cells;
+    std::vector<int> feat_per_level;
+    int capacity = 0;
+    long long list_stride = 0, lvl_stride = 0;
+    size_t fast_lds = 0;
+    int max_tiles = 0;
+    // device buffers
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+    int2 *d_xtab = nullptr, *d_ytab = nullptr;
+    std::vector<long long> xtab_off, ytab_off;
+    CellInfo* d_cells = nullptr;
+    uint32_t *d_lists = nullptr, *d_lvl = nullptr;
+    int *d_counts = nullptr, *d_lvl_counts = nullptr;
+    // host-family staging
+    uint8_t* d_img = nullptr;
+    gf_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_nout = nullptr;
+    // last batch (debug hook)
+    Planes last{};
+};
+
+static int cv_round_f(float v) { return (int)std::lrintf(v); }
+static int cv_floor_f(float v) {
+    int i = (int)v;
+    return i - (i > v);
+}
+
+static int plan_extractor(gf_extractor* ex) {
+    const int nl = ex->nlevels;
+    LevelGeom& g = ex->g;
+    memset(&g, 0, sizeof(g));
+    g.nlevels = nl;
+    // ORBextractor::ORBextractor (:464-494): scale tables and level quotas.
+    const double sf = ex->scale_factor;
+    std::vector<float> scale(nl), inv(nl);
+    scale[0] = 1.f;
+    for (int i = 1; i < nl; i++) scale[i] = (float)((double)scale[i - 1] * sf);
+    float invs = (float)(1.0f / sf);
+    inv[0] = 1.f;
+    for (int i = 1; i < nl; i++) inv[i] = inv[i - 1] * invs;
+    ex->feat_per_level.assign(nl, 0);
+    float factor = (float)(1.0 / sf);
+    float nd = ex->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    int sum = 0;
+    for (int l = 0; l < nl - 1; l++) {
+        ex->feat_per_level[l] = cv_round_f(nd);
+        sum += ex->feat_per_level[l];
+        nd *= factor;
+    }
+    ex->feat_per_level[nl - 1] = std::max(ex->nfeatures - sum, 0);
+
+    long long off = 0, boff = 0;
+    for (int l = 0; l < nl; l++) {
+        g.w[l] = cv_round_f((float)ex->width * inv[l]);
+        g.h[l] = cv_round_f((float)ex->height * inv[l]);
+        g.scale[l] = scale[l];
+        GF_CHECK(g.w[l] >= 40 && g.h[l] >= 40 && g.w[l] < 4096 && g.h[l] < 4096, GF_ERR_ARG,
+                 "level size out of supported range");
+        if (l > 0) {
+            g.off[l] = off;
+            off += ((long long)g.w[l] * g.h[l] + 255) & ~255LL;
+        }
+        g.boff[l] = boff;
+        boff += ((long long)g.w[l] * g.h[l] + 255) & ~255LL;
+    }
+    g.slab = off;
+    g.bslab = boff;
+    // blur tiles
+    int t = 0;
+    for (int l = 0; l < nl; l++) {
+        g.tile_begin[l] = t;
+        g.tiles_x[l] = (g.w[l] + BT_W - 1) / BT_W;
+        t += g.tiles_x[l] * ((g.h[l] + BT_H - 1) / BT_H);
+    }
+    g.tile_begin[nl] = t;
+    ex->max_tiles = t;
+
+    // ComputeKeyPoints cell grids (:540-618).
+    ex->cells.clear();
+    long long cap_off = 0, lvl_off = 0;
+    size_t max_lds = 0;
+    const float imageRatio = (float)g.w[0] / g.h[0];
+    for (int l = 0; l < nl; l++) {
+        const int nDesired = ex->feat_per_level[l];
+        const int levelCols = (int)std::sqrt((float)nDesired / (5 * imageRatio));
+        const int levelRows = (int)(imageRatio * levelCols);
+        GF_CHECK(levelCols > 0 && levelRows > 0, GF_ERR_UNSUPPORTED, "level with an empty cell grid");
+        const int minB = 16, maxBX = g.w[l] - 16, maxBY = g.h[l] - 16;
+        const int W = maxBX - minB, H = maxBY - minB;
+        const int cellW = (int)std::ceil((float)W / levelCols);
+        const int cellH = (int)std::ceil((float)H / levelRows);
+        const int nCells = levelRows * levelCols;
+        GF_CHECK(nCells <= SEL_MAX_CELLS, GF_ERR_UNSUPPORTED, "too many cells per level");
+        g.nfcell[l] = (int)std::ceil((float)nDesired / nCells);
+        g.ndesired[l] = nDesired;
+        g.cell_begin[l] = (int)ex->cells.size();
+        g.lvl_off[l] = lvl_off;
+        std::vector<int> iniXCol(levelCols, 0);
+        float hY = cellH + 6;
+        long long lvl_cap = 0;
+        for (int i = 0; i < levelRows; i++) {
+            const float iniY = minB + i * cellH - 3;
+            bool rowSkip = false;
+            if (i == levelRows - 1) {
+                hY = maxBY + 3 - iniY;
+                if (hY <= 0) rowSkip = true;
+            }
+            float hX = cellW + 6;
+            for (int j = 0; j < levelCols; j++) {
+                float iniX;
+                if (i == 0) {
+                    iniX = minB + j * cellW - 3;
+                    iniXCol[j] = (int)iniX;
+                } else
+                    iniX = iniXCol[j];
+                CellInfo ci{};
+                ci.level = l;
+                ci.valid = 0;
+                if (!rowSkip) {
+                    bool skip = false;
+                    if (j == levelCols - 1) {
+                        hX = maxBX + 3 - iniX;
+                        if (hX <= 0) skip = true;
+                    }
+                    if (!skip) {
+                        ci.x0 = (int)iniX;
+                        ci.y0 = (int)iniY;
+                        ci.w = (int)hX;
+                        ci.h = (int)hY;
+                        // a degenerate ROI (< 7 px) is processed and detects nothing, as FAST does
+                        ci.valid = 1;
+                        int dw = std::max(ci.w - 6, 0), dh = std::max(ci.h - 6, 0);
+                        ci.cap = ((dw + 1) / 2) * ((dh + 1) / 2);
+                        ci.cap_off = cap_off;
+                        cap_off += ci.cap;
+                        lvl_cap += ci.cap;
+                        size_t lds = (((size_t)ci.w * ci.h + 15) & ~(size_t)15) + (size_t)dw * dh * 2;
+                        max_lds = std::max(max_lds, lds);
+                        GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
+                                 GF_ERR_ARG, "cell ROI outside level");
+                    }
+                }
+                ex->cells.push_back(ci);
+            }
+        }
+        lvl_off += std::max(lvl_cap, (long long)nDesired);
+    }
+    g.cell_begin[nl] = (int)ex->cells.size();
+    g.lvl_off[nl] = lvl_off;
+    g.ncells = (int)ex->cells.size();
+    ex->list_stride = cap_off;
+    ex->lvl_stride = lvl_off;
+    ex->fast_lds = max_lds;
+    GF_CHECK(max_lds <= 64 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
+    ex->capacity = 0;
+    for (int l = 0; l < nl; l++) ex->capacity += ex->feat_per_level[l];
+    return GF_OK;
+}
+
+static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt, std::vector<int2>& yt) {
+    // cv::resize INTER_LINEAR coefficient set-up (fixed point, 2048 = 1.0).
+    const int ONE = 2048;
+    double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    xt.resize(dw);
+    yt.resize(dh);
+    for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor_f(fx);
+        fx -= sx;
+        if (sx < 0) fx = 0, sx = 0;
+        if (sx >= sw - 1) fx = 0, sx = sw - 1;
+        int a0 = (short)cv_round_f((1.f - fx) * ONE), a1 = (short)cv_round_f(fx * ONE);
+        xt[dx] = make_int2(sx, (a0 & 0xffff) | (a1 << 16));
+    }
+    for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor_f(fy);
+        fy -= sy;
+        int b0 = (short)cv_round_f((1.f - fy) * ONE), b1 = (short)cv_round_f(fy * ONE);
+        yt[dy] = make_int2(sy, (b0 & 0xffff) | (b1 << 16));
+    }
+}
+
+static void free_extractor(gf_extractor* ex) {
+    (void)hipFree(ex->d_pyr);
+    (void)hipFree(ex->d_blur);
+    (void)hipFree(ex->d_xtab);
+    (void)hipFree(ex->d_ytab);
+    (void)hipFree(ex->d_cells);
+    (void)hipFree(ex->d_lists);
+    (void)hipFree(ex->d_lvl);
+    (void)hipFree(ex->d_counts);
+    (void)hipFree(ex->d_lvl_counts);
+    (void)hipFree(ex->d_img);
+    (void)hipFree(ex->d_kps);
+    (void)hipFree(ex->d_desc);
+    (void)hipFree(ex->d_nout);
+}
+
+static int upload_constants(int device) {
+    static unsigned long long done_mask = 0;
+    if (done_mask & (1ull << device)) return GF_OK;
+    GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, sizeof(kOrbPattern31)));
+    // umax of the circular patch (ORBextractor.cc:500-517)
+    int umax[16];
+    const int hp = 15;
+    int vmax = cv_floor_f(hp * std::sqrt(2.f) / 2 + 1);
+    float vminf = hp * std::sqrt(2.f) / 2;
+    int vmin = (int)vminf + ((int)vminf < vminf);
+    const double hp2 = hp * hp;
+    for (int v = 0; v <= vmax; ++v) umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+    for (int v = hp, v0 = 0; v >= vmin; --v) {
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
+        ++v0;
+    }
+    GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax)));
+    done_mask |= 1ull << device;
+    return GF_OK;
+}
+
+extern "C" {
+
+int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlevels, int score_type, int fast_th,
+                        int width, int height, int max_batch, gf_extractor** out) {
+    GF_CHECK(ctx && out, GF_ERR_ARG, "null arg");
+    GF_CHECK(score_type == 1, GF_ERR_UNSUPPORTED, "only FAST_SCORE (1) is implemented");
+    GF_CHECK(nlevels >= 1 && nlevels <= GF_MAX_LEVELS, GF_ERR_ARG, "nlevels out of range");
+    GF_CHECK(nfeatures > 0 && scale_factor > 1.f && width > 0 && height > 0 && max_batch > 0, GF_ERR_ARG,
+             "bad extractor parameters");
+    GF_CHECK(fast_th >= 0 && fast_th < 255, GF_ERR_ARG, "bad FAST threshold");
+    GF_HIP(hipSetDevice(ctx->device));
+    int rc = upload_constants(ctx->device);
+    if (rc) return rc;
+    gf_extractor* ex = new gf_extractor();
+    ex->ctx = ctx;
+    ex->nfeatures = nfeatures;
+    ex->scale_factor = scale_factor;
+    ex->nlevels = nlevels;
+    ex->fast_th = fast_th;
+    ex->width = width;
+    ex->height = height;
+    ex->max_batch = max_batch;
+    rc = plan_extractor(ex);
+    if (rc) {
+        delete ex;
+        return rc;
+    }
+    const LevelGeom& g = ex->g;
+    auto cleanup = [&](hipError_t e) {
+        free_extractor(ex);
+        delete ex;
+        return gf::fail(GF_ERR_HIP, std::string("extractor alloc: ") + hipGetErrorString(e));
+    };
+    hipError_t e;
+#define ALLOC(p, bytes)                              \
+    if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return cleanup(e);
+    ALLOC(ex->d_pyr, std::max<long long>(g.slab, 256) * max_batch);
+    ALLOC(ex->d_blur, g.bslab * max_batch);
+    ALLOC(ex->d_cells, sizeof(CellInfo) * ex->cells.size());
+    ALLOC(ex->d_lists, sizeof(uint32_t) * ex->list_stride * max_batch);
+    ALLOC(ex->d_lvl, sizeof(uint32_t) * ex->lvl_stride * max_batch);
+    ALLOC(ex->d_counts, sizeof(int) * g.ncells * max_batch);
+    ALLOC(ex->d_lvl_counts, sizeof(int) * nlevels * max_batch);
+    ALLOC(ex->d_img, (size_t)width * height);
+    ALLOC(ex->d_kps, sizeof(gf_keypoint) * ex->capacity);
+    ALLOC(ex->d_desc, 32 * (size_t)ex->capacity);
+    ALLOC(ex->d_nout, sizeof(int));
+    // resize tables for levels 1..nl-1
+    std::vector<int2> xall, yall, xt, yt;
+    ex->xtab_off.assign(nlevels, 0);
+    ex->ytab_off.assign(nlevels, 0);
+    for (int l = 1; l < nlevels; l++) {
+        resize_tables(g.w[l - 1], g.h[l - 1], g.w[l], g.h[l], xt, yt);
+        ex->xtab_off[l] = (long long)xall.size();
+        ex->ytab_off[l] = (long long)yall.size();
+        xall.insert(xall.end(), xt.begin(), xt.end());
+        yall.insert(yall.end(), yt.begin(), yt.end());
+    }
+    ALLOC(ex->d_xtab, sizeof(int2) * std::max<size_t>(xall.size(), 1));
+    ALLOC(ex->d_ytab, sizeof(int2) * std::max<size_t>(yall.size(), 1));
+#undef ALLOC
+    if (!xall.empty()) {
+        GF_HIP(hipMemcpy(ex->d_xtab, xall.data(), sizeof(int2) * xall.size(), hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy(ex->d_ytab, yall.data(), sizeof(int2) * yall.size(), hipMemcpyHostToDevice));
+    }
+    GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
+    GF_HIP(hipFuncSetAttribute((const void*)k_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)ex->fast_lds));
+    *out = ex;
+    return GF_OK;
+}
+
+int gf_extractor_destroy(gf_extractor* ex) {
+    if (!ex) return GF_OK;
+    (void)hipSetDevice(ex->ctx->device);
+    free_extractor(ex);
+    delete ex;
+    return GF_OK;
+}
+
+int gf_extractor_info(gf_extractor* ex, int* nlevels, float* scale_factor, int* features_per_level) {
+    GF_CHECK(ex, GF_ERR_ARG, "null extractor");
+    if (nlevels) *nlevels = ex->nlevels;
+    if (scale_factor) *scale_factor = ex->scale_factor;
+    if (features_per_level)
+        for (int l = 0; l < ex->nlevels; l++) features_per_level[l] = ex->feat_per_level[l];
+    return GF_OK;
+}
+
+int gf_extractor_capacity(gf_extractor* ex, int* cap) {
+    GF_CHECK(ex && cap, GF_ERR_ARG, "null arg");
+    *cap = ex->capacity;
+    return GF_OK;
+}
+
+int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_imgs, size_t frame_stride, int stride,
+                             gf_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, void* stream) {
+    GF_CHECK(ex && d_imgs && d_kps && d_desc && d_counts, GF_ERR_ARG, "null arg");
+    GF_CHECK(nframes >= 0 && nframes <= ex->max_batch, GF_ERR_ARG, "nframes exceeds max_batch");
+    GF_CHECK(cap >= ex->capacity, GF_ERR_CAP, "cap below extractor capacity");
+    GF_CHECK(stride >= ex->width, GF_ERR_ARG,
+             "row stride " + std::to_string(stride) + " below width " + std::to_string(ex->width));
+    if (nframes == 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const LevelGeom& g = ex->g;
+    Planes P{d_imgs, (long long)frame_stride, stride, ex->d_pyr, ex->d_blur};
+    ex->last = P;
+    for (int l = 1; l < ex->nlevels; l++) {
+        dim3 blk(64, 4), grd((g.w[l] + 63) / 64, (g.h[l] + 3) / 4, nframes);
+        k_resize<<<grd, blk, 0, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l], ex->d_ytab + ex->ytab_off[l]);
+    }
+    k_blur<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g);
+    k_fast<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(P, g, ex->d_cells, ex->d_lists, ex->list_stride,
+                                                              ex->d_counts, ex->fast_th, ex->min_th);
+    k_select<<<dim3(ex->nlevels, nframes), 256, 0, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts,
+                                                        ex->d_lvl, ex->lvl_stride, ex->d_lvl_counts);
+    k_describe<<<dim3((ex->capacity + 3) / 4, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
+                                                                      ex->d_lvl_counts, d_kps, d_desc, d_counts, cap);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_orb_extract(gf_extractor* ex, const uint8_t* img, int stride, gf_keypoint* kps, uint8_t* desc, int cap,
+                   int* n_out) {
+    GF_CHECK(ex && n_out, GF_ERR_ARG, "null arg");
+    *n_out = 0;
+    if (!img) return GF_OK;  // empty image (ORBextractor.cc:772)
+    GF_CHECK(kps && desc, GF_ERR_ARG, "null output");
+    GF_HIP(hipSetDevice(ex->ctx->device));
+    hipStream_t s = ex->ctx->stream;
+    GF_HIP(hipMemcpy2DAsync(ex->d_img, ex->width, img, stride, ex->width, ex->height, hipMemcpyHostToDevice, s));
+    int rc = gf_orb_extract_batch_dev(ex, 1, ex->d_img, (size_t)ex->width * ex->height, ex->width, ex->d_kps,
+                                      ex->d_desc, ex->d_nout, ex->capacity, s);
+    if (rc) return rc;
+    int n = 0;
+    GF_HIP(hipMemcpyAsync(&n, ex->d_nout, sizeof(int), hipMemcpyDeviceToHost, s));
+    GF_HIP(hipStreamSynchronize(s));
+    *n_out = n;
+    GF_CHECK(n <= cap, GF_ERR_CAP, "keypoint capacity too small");
+    if (n) {
+        GF_HIP(hipMemcpyAsync(kps, ex->d_kps, sizeof(gf_keypoint) * n, hipMemcpyDeviceToHost, s));
+        GF_HIP(hipMemcpyAsync(desc, ex->d_desc, 32 * (size_t)n, hipMemcpyDeviceToHost, s));
+        GF_HIP(hipStreamSynchronize(s));
+    }
+    return GF_OK;
+}
+
+int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, uint8_t* out, int* w, int* h) {
+    GF_CHECK(ex && w && h, GF_ERR_ARG, "null arg");
+    GF_CHECK(level >= 0 && level < ex->nlevels && frame >= 0 && frame < ex->max_batch, GF_ERR_ARG, "bad index");
+    const LevelGeom& g = ex->g;
+    *w = g.w[level];
+    *h = g.h[level];
+    if (!out) return GF_OK;
+    GF_HIP(hipSetDevice(ex->ctx->device));
+    GF_HIP(hipStreamSynchronize(ex->ctx->stream));
+    if (which == 1) {
+        GF_HIP(hipMemcpy(out, ex->d_blur + (long long)frame * g.bslab + g.boff[level], (size_t)g.w[level] * g.h[level],
+                         hipMemcpyDeviceToHost));
+    } else if (level == 0) {
+        GF_CHECK(ex->last.img0, GF_ERR_ARG, "no batch run yet");
+        GF_HIP(hipMemcpy2D(out, g.w[0], ex->last.img0 + (long long)frame * ex->last.fstride0, ex->last.stride0, g.w[0],
+                           g.h[0], hipMemcpyDeviceToHost));
+    } else {
+        GF_HIP(hipMemcpy(out, ex->d_pyr + (long long)frame * g.slab + g.off[level], (size_t)g.w[level] * g.h[level],
+                         hipMemcpyDeviceToHost));
+    }
+    return GF_OK;
+}
+
+}  // extern "C"

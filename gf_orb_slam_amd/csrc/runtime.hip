@@ -1,0 +1,67 @@
+// libgfslam runtime: error reporting and per-thread contexts (one HIP stream each).
+#include <string>
+
+#include "common.h"
+
+namespace gf {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace gf
+
+extern "C" {
+
+int gf_version(void) { return 1; }
+
+const char* gf_last_error(void) { return gf::g_err.c_str(); }
+
+int gf_device_count(int* n) {
+    GF_CHECK(n, GF_ERR_ARG, "null n");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = (e == hipSuccess) ? c : 0;
+    return GF_OK;
+}
+
+int gf_ctx_create(int hip_device, gf_ctx** out) {
+    GF_CHECK(out, GF_ERR_ARG, "null out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return gf::fail(GF_ERR_NODEV, "no HIP device");
+    GF_CHECK(hip_device >= 0 && hip_device < n, GF_ERR_ARG, "bad device index");
+    GF_HIP(hipSetDevice(hip_device));
+    gf_ctx* c = new gf_ctx();
+    c->device = hip_device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return gf::fail(GF_ERR_HIP, hipGetErrorString(e));
+    }
+    *out = c;
+    return GF_OK;
+}
+
+int gf_ctx_destroy(gf_ctx* ctx) {
+    if (!ctx) return GF_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return GF_OK;
+}
+
+int gf_ctx_stream(gf_ctx* ctx, void** stream) {
+    GF_CHECK(ctx && stream, GF_ERR_ARG, "null arg");
+    *stream = (void*)ctx->stream;
+    return GF_OK;
+}
+
+int gf_ctx_sync(gf_ctx* ctx) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    GF_HIP(hipSetDevice(ctx->device));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+}  // extern "C"
