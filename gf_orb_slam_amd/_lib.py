@@ -71,6 +71,14 @@ _PROTOS = {
     "gf_orb_extract": [_P, _P, _I, _P, _P, _I, _P],
     "gf_orb_extract_batch_dev": [_P, _I, _P, _S, _I, _P, _P, _P, _I, _P],
     "gf_extractor_debug_level": [_P, _I, _I, _I, _P, _P, _P],
+    "gf_frustum": [_P, _P, _P, _P, _I, _F, _P, _P],
+    "gf_match_project": [_P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P, _P],
+    "gf_match_lastframe": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P],
+    "gf_descriptor_distance": [_P, _P, _P, _I, _P],
+    "gf_frustum_dev": [_P, _P, _I, _P, _P, _P, _I, _F, _P, _P, _P],
+    "gf_match_project_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _I, _F, _F, _P, _P, _P, _P],
+    "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
+                               _P, _P],
 }
 
 

@@ -29,7 +29,18 @@ int fail(int code, const std::string& msg);
 struct gf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // grow-only device scratch for the host-family wrappers (one slot per use)
+    static const int kSlots = 32;
+    void* ws[kSlots] = {};
+    size_t ws_size[kSlots] = {};
 };
+
+namespace gf {
+// Device scratch buffer `slot` of at least `bytes` (grow-only, owned by ctx).
+int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out);
+// Host-family helper: copy host -> scratch slot (returns device pointer).
+int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out);
+}  // namespace gf
 
 // Device-side helpers ------------------------------------------------------
 namespace gfd {

@@ -1,0 +1,672 @@
+// Projection matching on gfx950 — SURVEY.md §8a rows E8, M1-M3, M7.
+//
+// ORBmatcher's projection searches are order dependent: map point k may only
+// take keypoints that no earlier map point claimed (F.mvpMapPoints[idx] is
+// tested before the distance, ORBmatcher.cc:426-427 / :2136). The kernel
+// resolves that sequential semantics exactly, in parallel rounds:
+//
+//   round: every unresolved query k marks, for each unclaimed candidate
+//          keypoint c in its window, minU[c] = min(minU[c], k);
+//          a query whose unclaimed candidates all have minU == k has no
+//          earlier unresolved competitor, so its sequential outcome is
+//          already determined: it walks its candidates in the reference
+//          order (grid cells ix-major, iy, keypoint index), takes best /
+//          second best exactly as the CPU loop does, and claims.
+//
+// Queries resolved in the same round have disjoint unclaimed candidate sets,
+// the lowest unresolved query is always resolvable, and claims are
+// monotone, so the result equals the sequential loop bit for bit. One
+// workgroup per frame (frames are independent streams), the 64x48 grid CSR,
+// claims and the round state live in LDS.
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+
+#define GRID_COLS 64
+#define GRID_ROWS 48
+#define NCELLS (GRID_COLS * GRID_ROWS)
+#define KP_MAX 4096
+#define Q_MAX 8192
+#define MATCH_THREADS 1024
+#define TH_HIGH 100
+#define HISTO_LENGTH 30
+
+namespace {
+
+struct FrameConst {
+    int min_x, max_x, min_y, max_y;
+    float fx, fy, cx, cy;
+    int nlevels;
+    float invW, invH;
+    float scales[16];
+};
+
+enum { MODE_PROJECT = 0, MODE_LAST = 1 };
+
+struct MatchArgs {
+    int mode;
+    // current frame
+    const gf_keypoint* kps;
+    const uint8_t* desc;
+    const int32_t* n;
+    int kp_cap;
+    // MODE_PROJECT queries
+    const gf_mp_view* views;
+    const uint8_t* qdesc;
+    const int32_t* m;
+    int q_cap;
+    // MODE_LAST queries
+    const gf_keypoint* last_kps;
+    const int32_t* last_kp2mp;
+    const uint8_t* last_outlier;
+    const float* last_pos;
+    const float* Tcw;  // [F][16]
+    float th, nnratio;
+    int check_ori;
+    // in/out
+    int32_t* kp2mp;
+    int32_t* score;
+    int32_t* nmatches;
+    int32_t* qres;  // [F][q_cap] scratch: matched kp per query (MODE_LAST)
+    int32_t* err;   // [F] round-limit flag
+};
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+    const uint4* pa = (const uint4*)a;
+    const uint4* pb = (const uint4*)b;
+    uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+struct Query {
+    bool valid;
+    float x, y, r;
+    int minL, maxL;
+    int cx0, cx1, cy0, cy1;  // grid window (empty if cx0 > cx1)
+    const uint8_t* d;
+    int id;  // value written into kp2mp
+};
+
+__device__ __forceinline__ void transform3(const float* T, const float* P, float* Pc) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        float a = T[4 * r + 0] * P[0];
+        float b = T[4 * r + 1] * P[1];
+        float c = T[4 * r + 2] * P[2];
+        Pc[r] = ((a + b) + c) + T[4 * r + 3];
+    }
+}
+
+__device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int k) {
+    Query q;
+    q.valid = false;
+    q.cx0 = 1;
+    q.cx1 = 0;
+    if (A.mode == MODE_PROJECT) {
+        const gf_mp_view v = A.views[(long long)f * A.q_cap + k];
+        if (!v.in_view) return q;
+        const int pl = min(max(v.level, 0), fc.nlevels - 1);
+        float r = v.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
+        if (A.th != 1.0) r *= A.th;
+        q.r = r * fc.scales[pl];
+        q.x = v.u;
+        q.y = v.v;
+        q.minL = pl - 1;
+        q.maxL = pl;
+        q.d = A.qdesc + ((long long)f * A.q_cap + k) * 32;
+        q.id = k;
+    } else {
+        const long long li = (long long)f * A.q_cap + k;
+        const int mp = A.last_kp2mp[li];
+        if (mp < 0 || A.last_outlier[li]) return q;
+        float Pc[3];
+        transform3(A.Tcw + 16 * f, A.last_pos + 3 * li, Pc);
+        const float invzc = (float)(1.0 / (double)Pc[2]);
+        const float u = fc.fx * Pc[0] * invzc + fc.cx;
+        const float v = fc.fy * Pc[1] * invzc + fc.cy;
+        if (u < fc.min_x || u > fc.max_x) return q;
+        if (v < fc.min_y || v > fc.max_y) return q;
+        const int oct = A.last_kps[li].octave;
+        q.r = A.th * fc.scales[oct];
+        q.x = u;
+        q.y = v;
+        q.minL = oct - 1;
+        q.maxL = oct + 1;
+        q.d = A.qdesc + li * 32;
+        q.id = mp;
+    }
+    q.valid = true;
+    // Frame::GetFeaturesInArea window (Frame.cc:305-327)
+    int nMinCellX = max(0, (int)floorf((q.x - fc.min_x - q.r) * fc.invW));
+    int nMaxCellX = min(GRID_COLS - 1, (int)ceilf((q.x - fc.min_x + q.r) * fc.invW));
+    int nMinCellY = max(0, (int)floorf((q.y - fc.min_y - q.r) * fc.invH));
+    int nMaxCellY = min(GRID_ROWS - 1, (int)ceilf((q.y - fc.min_y + q.r) * fc.invH));
+    if (nMinCellX >= GRID_COLS || nMaxCellX < 0 || nMinCellY >= GRID_ROWS || nMaxCellY < 0) return q;
+    q.cx0 = nMinCellX;
+    q.cx1 = nMaxCellX;
+    q.cy0 = nMinCellY;
+    q.cy1 = nMaxCellY;
+    return q;
+}
+
+__device__ __forceinline__ bool level_ok(int oct, int minL, int maxL) {
+    const bool check = !(minL == -1 && maxL == -1);
+    const bool same = check && minL == maxL;
+    if (check && !same) return !(oct < minL || oct > maxL);
+    if (same) return oct == minL;
+    return true;
+}
+
+__global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
+    extern __shared__ __align__(16) int lds[];
+    int* cell_start = lds;                  // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;  // NCELLS
+    int* items = cursor + NCELLS;           // KP_MAX
+    int* claim = items + KP_MAX;            // KP_MAX
+    int* minU = claim + KP_MAX;             // KP_MAX
+    uint8_t* done = (uint8_t*)(minU + KP_MAX);  // Q_MAX
+    __shared__ int s_any, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
+
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = min(A.n[f], KP_MAX);
+    const int nq = min(A.m[f], Q_MAX);
+    const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
+    const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
+    int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
+    int32_t* score = A.score + (long long)f * A.kp_cap;
+
+    // ---- 64x48 grid CSR (Frame.cc:114-131, PosInGrid :367-377), cells ix-major
+    for (int c = tid; c < NCELLS + 1; c += MATCH_THREADS) cell_start[c] = 0;
+    if (tid == 0) {
+        s_nm = 0;
+        for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += MATCH_THREADS) {
+        const gf_keypoint kp = K[i];
+        int px = (int)roundf((kp.x - fc.min_x) * fc.invW);
+        int py = (int)roundf((kp.y - fc.min_y) * fc.invH);
+        int c = (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
+        minU[i] = c;
+        if (c >= 0) atomicAdd(&cell_start[c + 1], 1);
+        claim[i] = kp2mp[i];
+    }
+    __syncthreads();
+    if (tid < 64) {  // one wave scans the 3072 counts
+        int carry = 0;
+        for (int base = 0; base < NCELLS; base += 64) {
+            int v = cell_start[base + 1 + tid], x = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                int y = __shfl_up(x, o, 64);
+                if (tid >= o) x += y;
+            }
+            cell_start[base + 1 + tid] = carry + x;
+            carry += __shfl(x, 63, 64);
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < NCELLS; c += MATCH_THREADS) cursor[c] = cell_start[c];
+    __syncthreads();
+    for (int i = tid; i < n; i += MATCH_THREADS) {
+        int c = minU[i];
+        if (c >= 0) items[atomicAdd(&cursor[c], 1)] = i;
+    }
+    __syncthreads();
+    for (int c = tid; c < NCELLS; c += MATCH_THREADS) {  // ascending index inside a cell
+        int s = cell_start[c], e = cell_start[c + 1];
+        for (int a = s + 1; a < e; a++) {
+            int v = items[a], b = a - 1;
+            while (b >= s && items[b] > v) {
+                items[b + 1] = items[b];
+                b--;
+            }
+            items[b + 1] = v;
+        }
+    }
+    for (int k = tid; k < nq; k += MATCH_THREADS) done[k] = 0;
+    __syncthreads();
+
+    // ---- claim-resolution rounds
+    int rounds = 0;
+    while (true) {
+        for (int i = tid; i < n; i += MATCH_THREADS) minU[i] = INT_MAX;
+        if (tid == 0) s_any = 0;
+        __syncthreads();
+        for (int k = tid; k < nq; k += MATCH_THREADS) {
+            if (done[k]) continue;
+            const Query q = make_query(A, fc, f, k);
+            if (!q.valid) continue;
+            for (int ix = q.cx0; ix <= q.cx1; ix++) {
+                const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
+                for (int t = s; t < e; t++) {
+                    const int idx = items[t];
+                    if (claim[idx] >= 0) continue;
+                    const gf_keypoint kp = K[idx];
+                    if (!level_ok(kp.octave, q.minL, q.maxL)) continue;
+                    if (fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
+                    atomicMin(&minU[idx], k);
+                }
+            }
+        }
+        __syncthreads();
+        for (int k = tid; k < nq; k += MATCH_THREADS) {
+            if (done[k]) continue;
+            const Query q = make_query(A, fc, f, k);
+            int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+            bool ok = true;
+            if (q.valid) {
+                for (int ix = q.cx0; ix <= q.cx1 && ok; ix++) {
+                    const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
+                    for (int t = s; t < e; t++) {
+                        const int idx = items[t];
+                        const gf_keypoint kp = K[idx];
+                        if (!level_ok(kp.octave, q.minL, q.maxL)) continue;
+                        if (fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
+                        if (__hip_atomic_load(&claim[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
+                            continue;
+                        if (minU[idx] != k) {
+                            ok = false;
+                            break;
+                        }
+                        const int dist = hamming32(q.d, D + (long long)idx * 32);
+                        if (dist < bestDist) {
+                            bestDist2 = bestDist;
+                            bestDist = dist;
+                            bestLevel2 = bestLevel;
+                            bestLevel = kp.octave;
+                            bestIdx = idx;
+                        } else if (dist < bestDist2) {
+                            bestLevel2 = kp.octave;
+                            bestDist2 = dist;
+                        }
+                    }
+                }
+            }
+            if (!ok) {
+                s_any = 1;
+                continue;
+            }
+            done[k] = 1;
+            int res = -1;
+            if (q.valid && bestDist <= TH_HIGH) {
+                bool reject = A.mode == MODE_PROJECT && bestLevel == bestLevel2 &&
+                              (float)bestDist > A.nnratio * (float)bestDist2;
+                if (!reject) {
+                    __hip_atomic_store(&claim[bestIdx], q.id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    score[bestIdx] = bestDist;
+                    atomicAdd(&s_nm, 1);
+                    res = bestIdx;
+                }
+            }
+            if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = res;
+        }
+        __syncthreads();
+        if (!s_any) break;
+        if (++rounds > nq + 2) {
+            if (tid == 0) A.err[f] = 1;
+            break;
+        }
+        __syncthreads();
+    }
+
+    // ---- rotation consistency (ORBmatcher.cc:2146-2190)
+    if (A.mode == MODE_LAST && A.check_ori) {
+        const float factor = 1.0f / HISTO_LENGTH;
+        for (int k = tid; k < nq; k += MATCH_THREADS) {
+            const int j = A.qres[(long long)f * A.q_cap + k];
+            if (j < 0) continue;
+            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            atomicAdd(&s_hist[bin], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int s = s_hist[i];
+                if (s > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = s;
+                    ind3 = ind2;
+                    ind2 = ind1;
+                    ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2;
+                    max2 = s;
+                    ind3 = ind2;
+                    ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1;
+                ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            s_keep[0] = ind1;
+            s_keep[1] = ind2;
+            s_keep[2] = ind3;
+        }
+        __syncthreads();
+        for (int k = tid; k < nq; k += MATCH_THREADS) {
+            const int j = A.qres[(long long)f * A.q_cap + k];
+            if (j < 0) continue;
+            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            if (bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2]) continue;
+            claim[j] = -1;
+            score[j] = 999;
+            atomicSub(&s_nm, 1);
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += MATCH_THREADS) kp2mp[i] = claim[i];
+    if (tid == 0) A.nmatches[f] = s_nm;
+}
+
+// ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
+__global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
+                          const int32_t* __restrict__ m, int cap, float viewCosLimit, gf_mp_view* __restrict__ views,
+                          int32_t* __restrict__ nview) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const float* T = Tcw + 16 * f;
+    int in = 0;
+    if (i < m[f]) {
+        gf_mp_view v;
+        v.in_view = 0;
+        v.u = v.v = v.view_cos = 0.f;
+        v.level = 0;
+        const gf_map_point mp = mps[(long long)f * cap + i];
+        float Ow[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float a = T[0 * 4 + c] * T[3], b = T[1 * 4 + c] * T[7], d = T[2 * 4 + c] * T[11];
+            Ow[c] = -((a + b) + d);
+        }
+        float Pc[3];
+        transform3(T, mp.pos, Pc);
+        do {
+            if (Pc[2] < 0.0) break;
+            const float invz = (float)(1.0 / (double)Pc[2]);
+            const float u = fc.fx * Pc[0] * invz + fc.cx;
+            const float vv = fc.fy * Pc[1] * invz + fc.cy;
+            if (u < fc.min_x || u > fc.max_x) break;
+            if (vv < fc.min_y || vv > fc.max_y) break;
+            const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
+            const float dist =
+                (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+            if (dist < mp.min_dist || dist > mp.max_dist) break;
+            double dot = (double)PO[0] * mp.normal[0] + (double)PO[1] * mp.normal[1] + (double)PO[2] * mp.normal[2];
+            const float viewCos = (float)(dot / dist);
+            if (viewCos < viewCosLimit) break;
+            const float ratio = dist / mp.min_dist;
+            int lvl = 0;
+            while (lvl < fc.nlevels && fc.scales[lvl] < ratio) lvl++;
+            if (lvl >= fc.nlevels) lvl = fc.nlevels - 1;
+            v.in_view = 1;
+            v.u = u;
+            v.v = vv;
+            v.level = lvl;
+            v.view_cos = viewCos;
+            in = 1;
+        } while (0);
+        views[(long long)f * cap + i] = v;
+    }
+    // count in-view points
+    int s = gfd::warp_sum(in);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(&nview[f], s);
+}
+
+__global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* dist) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dist[i] = hamming32(a + 32LL * i, b + 32LL * i);
+}
+
+size_t match_lds_bytes() { return sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX; }
+
+}  // namespace
+
+namespace gf {
+FrameConst make_frame_const(const gf_frame_info* fi) {
+    FrameConst fc{};
+    fc.min_x = fi->min_x;
+    fc.max_x = fi->max_x;
+    fc.min_y = fi->min_y;
+    fc.max_y = fi->max_y;
+    fc.fx = fi->fx;
+    fc.fy = fi->fy;
+    fc.cx = fi->cx;
+    fc.cy = fi->cy;
+    fc.nlevels = fi->nlevels;
+    fc.invW = (float)GRID_COLS / (float)(fi->max_x - fi->min_x);
+    fc.invH = (float)GRID_ROWS / (float)(fi->max_y - fi->min_y);
+    fc.scales[0] = 1.f;
+    for (int i = 1; i < fi->nlevels && i < 16; i++) fc.scales[i] = fc.scales[i - 1] * fi->scale_factor;
+    return fc;
+}
+}  // namespace gf
+
+static int check_fi(const gf_frame_info* fi) {
+    GF_CHECK(fi, GF_ERR_ARG, "null frame info");
+    GF_CHECK(fi->nlevels >= 1 && fi->nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
+    GF_CHECK(fi->max_x > fi->min_x && fi->max_y > fi->min_y, GF_ERR_ARG, "empty image bounds");
+    return GF_OK;
+}
+
+static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, int nframes, hipStream_t s) {
+    static unsigned long long attr_mask = 0;
+    if (!(attr_mask & (1ull << ctx->device))) {
+        GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)match_lds_bytes()));
+        attr_mask |= 1ull << ctx->device;
+    }
+    k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+extern "C" {
+
+int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw, const gf_map_point* d_mps,
+                   const int32_t* d_m, int mp_cap, float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview,
+                   void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    if (nframes <= 0 || mp_cap <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    FrameConst fc = gf::make_frame_const(fi);
+    GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
+    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
+                                                                   d_views, d_nview);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                         const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                         const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, float th, float nnratio,
+                         int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    GF_CHECK(kp_cap <= KP_MAX && mp_cap <= Q_MAX, GF_ERR_UNSUPPORTED, "frame exceeds matcher limits (4096 kps, 8192 mps)");
+    if (nframes <= 0) return GF_OK;
+    MatchArgs A{};
+    A.mode = MODE_PROJECT;
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.kp_cap = kp_cap;
+    A.views = d_views;
+    A.qdesc = d_mp_desc;
+    A.m = d_m;
+    A.q_cap = mp_cap;
+    A.th = th;
+    A.nnratio = nnratio;
+    A.kp2mp = d_kp2mp;
+    A.score = d_score;
+    A.nmatches = d_nmatches;
+    void* err;
+    rc = gf::ws_get(ctx, 31, sizeof(int32_t) * nframes, &err);
+    if (rc) return rc;
+    A.err = (int32_t*)err;
+    return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
+}
+
+int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                           const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const float* d_Tcw,
+                           const gf_keypoint* d_last_kps, const uint8_t* d_last_desc, const int32_t* d_last_kp2mp,
+                           const uint8_t* d_last_outlier, const float* d_last_pos, const int32_t* d_n_last,
+                           int last_cap, float th, int check_ori, int32_t* d_kp2mp, int32_t* d_score,
+                           int32_t* d_nmatches, int32_t* d_scratch, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    GF_CHECK(kp_cap <= KP_MAX && last_cap <= Q_MAX, GF_ERR_UNSUPPORTED, "frame exceeds matcher limits");
+    if (nframes <= 0) return GF_OK;
+    MatchArgs A{};
+    A.mode = MODE_LAST;
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.kp_cap = kp_cap;
+    A.qdesc = d_last_desc;
+    A.m = d_n_last;
+    A.q_cap = last_cap;
+    A.last_kps = d_last_kps;
+    A.last_kp2mp = d_last_kp2mp;
+    A.last_outlier = d_last_outlier;
+    A.last_pos = d_last_pos;
+    A.Tcw = d_Tcw;
+    A.th = th;
+    A.check_ori = check_ori;
+    A.kp2mp = d_kp2mp;
+    A.score = d_score;
+    A.nmatches = d_nmatches;
+    A.qres = d_scratch;
+    void* err;
+    rc = gf::ws_get(ctx, 31, sizeof(int32_t) * nframes, &err);
+    if (rc) return rc;
+    A.err = (int32_t*)err;
+    return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------ host family
+int gf_frustum(gf_ctx* ctx, const gf_frame_info* fi, const float* Tcw, const gf_map_point* mps, int m,
+               float view_cos_limit, gf_mp_view* views, int* n_in_view) {
+    GF_CHECK(ctx && Tcw && n_in_view, GF_ERR_ARG, "null arg");
+    *n_in_view = 0;
+    if (m <= 0) return GF_OK;
+    GF_CHECK(mps && views, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dT, *dM, *dm, *dV, *dn;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, Tcw, 64, &dT)) || (rc = gf::ws_upload(ctx, 1, mps, sizeof(gf_map_point) * m, &dM)) ||
+        (rc = gf::ws_upload(ctx, 2, &m, 4, &dm)) || (rc = gf::ws_get(ctx, 3, sizeof(gf_mp_view) * m, &dV)) ||
+        (rc = gf::ws_get(ctx, 4, 4, &dn)))
+        return rc;
+    rc = gf_frustum_dev(ctx, fi, 1, (const float*)dT, (const gf_map_point*)dM, (const int32_t*)dm, m, view_cos_limit,
+                        (gf_mp_view*)dV, (int32_t*)dn, ctx->stream);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(views, dV, sizeof(gf_mp_view) * m, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(n_in_view, dn, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+int gf_match_project(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                     const gf_mp_view* views, const uint8_t* mp_desc, int m, float th, float nnratio, int32_t* kp2mp,
+                     int32_t* score, int* nmatches) {
+    GF_CHECK(ctx && nmatches, GF_ERR_ARG, "null arg");
+    *nmatches = 0;
+    if (n <= 0 || m <= 0) return GF_OK;
+    GF_CHECK(kps && desc && views && mp_desc && kp2mp && score, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dK, *dD, *dn, *dV, *dQ, *dm, *dC, *dS, *dN;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, kps, sizeof(gf_keypoint) * n, &dK)) ||
+        (rc = gf::ws_upload(ctx, 1, desc, 32 * (size_t)n, &dD)) || (rc = gf::ws_upload(ctx, 2, &n, 4, &dn)) ||
+        (rc = gf::ws_upload(ctx, 3, views, sizeof(gf_mp_view) * m, &dV)) ||
+        (rc = gf::ws_upload(ctx, 4, mp_desc, 32 * (size_t)m, &dQ)) || (rc = gf::ws_upload(ctx, 5, &m, 4, &dm)) ||
+        (rc = gf::ws_upload(ctx, 6, kp2mp, 4 * (size_t)n, &dC)) || (rc = gf::ws_upload(ctx, 7, score, 4 * (size_t)n, &dS)) ||
+        (rc = gf::ws_get(ctx, 8, 4, &dN)))
+        return rc;
+    rc = gf_match_project_dev(ctx, fi, 1, (const gf_keypoint*)dK, (const uint8_t*)dD, (const int32_t*)dn, n,
+                              (const gf_mp_view*)dV, (const uint8_t*)dQ, (const int32_t*)dm, m, th, nnratio,
+                              (int32_t*)dC, (int32_t*)dS, (int32_t*)dN, ctx->stream);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(kp2mp, dC, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(score, dS, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(nmatches, dN, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+int gf_match_lastframe(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                       const float* Tcw, const gf_keypoint* last_kps, const uint8_t* last_desc,
+                       const int32_t* last_kp2mp, const uint8_t* last_outlier, const float* last_pos, int n_last,
+                       float th, int check_ori, int32_t* kp2mp, int32_t* score, int* nmatches) {
+    GF_CHECK(ctx && nmatches, GF_ERR_ARG, "null arg");
+    *nmatches = 0;
+    if (n <= 0 || n_last <= 0) return GF_OK;
+    GF_CHECK(kps && desc && Tcw && last_kps && last_desc && last_kp2mp && last_outlier && last_pos && kp2mp && score,
+             GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dK, *dD, *dn, *dT, *dLK, *dLD, *dLM, *dLO, *dLP, *dnl, *dC, *dS, *dN, *dR;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, kps, sizeof(gf_keypoint) * n, &dK)) ||
+        (rc = gf::ws_upload(ctx, 1, desc, 32 * (size_t)n, &dD)) || (rc = gf::ws_upload(ctx, 2, &n, 4, &dn)) ||
+        (rc = gf::ws_upload(ctx, 3, Tcw, 64, &dT)) ||
+        (rc = gf::ws_upload(ctx, 4, last_kps, sizeof(gf_keypoint) * n_last, &dLK)) ||
+        (rc = gf::ws_upload(ctx, 5, last_desc, 32 * (size_t)n_last, &dLD)) ||
+        (rc = gf::ws_upload(ctx, 6, last_kp2mp, 4 * (size_t)n_last, &dLM)) ||
+        (rc = gf::ws_upload(ctx, 7, last_outlier, (size_t)n_last, &dLO)) ||
+        (rc = gf::ws_upload(ctx, 8, last_pos, 12 * (size_t)n_last, &dLP)) ||
+        (rc = gf::ws_upload(ctx, 9, &n_last, 4, &dnl)) || (rc = gf::ws_upload(ctx, 10, kp2mp, 4 * (size_t)n, &dC)) ||
+        (rc = gf::ws_upload(ctx, 11, score, 4 * (size_t)n, &dS)) || (rc = gf::ws_get(ctx, 12, 4, &dN)) ||
+        (rc = gf::ws_get(ctx, 13, 4 * (size_t)n_last, &dR)))
+        return rc;
+    rc = gf_match_lastframe_dev(ctx, fi, 1, (const gf_keypoint*)dK, (const uint8_t*)dD, (const int32_t*)dn, n,
+                                (const float*)dT, (const gf_keypoint*)dLK, (const uint8_t*)dLD, (const int32_t*)dLM,
+                                (const uint8_t*)dLO, (const float*)dLP, (const int32_t*)dnl, n_last, th, check_ori,
+                                (int32_t*)dC, (int32_t*)dS, (int32_t*)dN, (int32_t*)dR, ctx->stream);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(kp2mp, dC, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(score, dS, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(nmatches, dN, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+int gf_descriptor_distance(gf_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int32_t* dist) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (n <= 0) return GF_OK;
+    GF_CHECK(a && b && dist, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dA, *dB, *dO;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, a, 32 * (size_t)n, &dA)) || (rc = gf::ws_upload(ctx, 1, b, 32 * (size_t)n, &dB)) ||
+        (rc = gf::ws_get(ctx, 2, 4 * (size_t)n, &dO)))
+        return rc;
+    k_hamming<<<(n + 255) / 256, 256, 0, ctx->stream>>>((const uint8_t*)dA, (const uint8_t*)dB, n, (int32_t*)dO);
+    GF_HIP(hipGetLastError());
+    GF_HIP(hipMemcpyAsync(dist, dO, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+}  // extern "C"

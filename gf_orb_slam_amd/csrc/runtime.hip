@@ -10,6 +10,28 @@ int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+
+int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out) {
+    GF_CHECK(slot >= 0 && slot < gf_ctx::kSlots, GF_ERR_ARG, "bad scratch slot");
+    if (bytes == 0) bytes = 16;
+    if (ctx->ws_size[slot] < bytes) {
+        if (ctx->ws[slot]) GF_HIP(hipFree(ctx->ws[slot]));
+        ctx->ws[slot] = nullptr;
+        ctx->ws_size[slot] = 0;
+        size_t sz = bytes + bytes / 2;
+        GF_HIP(hipMalloc(&ctx->ws[slot], sz));
+        ctx->ws_size[slot] = sz;
+    }
+    *out = ctx->ws[slot];
+    return GF_OK;
+}
+
+int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out) {
+    int rc = ws_get(ctx, slot, bytes, out);
+    if (rc) return rc;
+    if (host && bytes) GF_HIP(hipMemcpyAsync(*out, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return GF_OK;
+}
 }  // namespace gf
 
 extern "C" {
@@ -46,6 +68,9 @@ int gf_ctx_create(int hip_device, gf_ctx** out) {
 int gf_ctx_destroy(gf_ctx* ctx) {
     if (!ctx) return GF_OK;
     (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int i = 0; i < gf_ctx::kSlots; i++)
+        if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return GF_OK;

@@ -132,6 +132,8 @@ class ORBextractor:
         """Device family: imgs uint8 [F, H, W] (torch, on GPU), kps int8-viewable
         [F, cap, 28] bytes, desc uint8 [F, cap, 32], counts int32 [F]."""
         f, hgt, wid = imgs.shape
+        if imgs.stride(2) != 1:
+            raise ValueError("image rows must be contiguous (stride(2) == 1)")
         self._bind(wid, hgt)
         check(lib().gf_orb_extract_batch_dev(self._h, int(f), ptr(imgs), ctypes.c_size_t(int(imgs.stride(0))),
                                              int(imgs.stride(1)), ptr(kps), ptr(desc), ptr(counts),

@@ -63,9 +63,107 @@ def synth_frame(width: int, height: int, seed: int, n_shapes: int = 400) -> np.n
     img = np.apply_along_axis(lambda r: np.convolve(r, k, mode="same"), 1, img)
     img = np.apply_along_axis(lambda c: np.convolve(c, k, mode="same"), 0, img)
     img += rng.uniform(-3, 3, img.shape)
-    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
 
 
 def synth_sequence(camera: str, nframes: int, stream: int = 0) -> np.ndarray:
     w, h = CAMERAS[camera][:2]
     return np.stack([synth_frame(w, h, frame_seed(stream, f)) for f in range(nframes)])
+
+
+# ----------------------------------------------------------------- scenes
+def look_pose(rng, trans_sigma=0.0, rot_deg=0.0) -> np.ndarray:
+    """Tcw near identity (camera at the origin looking along +z)."""
+    T = np.eye(4)
+    if rot_deg:
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = np.radians(rot_deg)
+        K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+        T[:3, :3] = np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+    T[:3, 3] = rng.normal(scale=trans_sigma, size=3) if trans_sigma else 0
+    return T.astype(np.float32)
+
+
+def project(T, X, cam):
+    w, h, fx, fy, cx, cy = cam
+    Pc = X @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+    u = fx * Pc[:, 0] / Pc[:, 2] + cx
+    v = fy * Pc[:, 1] / Pc[:, 2] + cy
+    return u, v, Pc[:, 2]
+
+
+def flip_bits(rng, desc, kmax):
+    out = desc.copy()
+    for i in range(len(out)):
+        k = int(rng.integers(0, kmax + 1))
+        if k:
+            bits = rng.choice(256, k, replace=False)
+            for b in bits:
+                out[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    return out
+
+
+def synth_scene(camera: str, n_mp: int, n_kp: int, seed: int, nlevels: int = 8, scale: float = 1.2,
+                max_flip: int = 40, outlier_frac: float = 0.1):
+    """Map points + a frame that observes them.
+
+    Returns dict with map (MAP_POINT_DTYPE), mp_desc, Tcw, keypoints
+    (KEYPOINT_DTYPE), descriptors and kp_mp (ground-truth map point per
+    keypoint, -1 for distractors)."""
+    from .matcher import MAP_POINT_DTYPE
+    from .orb import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    cam = CAMERAS[camera]
+    w, h = cam[:2]
+    X = np.stack([rng.uniform(-4, 4, n_mp), rng.uniform(-3, 3, n_mp), rng.uniform(2, 8, n_mp)], 1)
+    Tcw = look_pose(rng, 0.02, 0.5)
+    Ow = -(Tcw[:3, :3].T @ Tcw[:3, 3])
+    dist = np.linalg.norm(X - Ow, axis=1)
+    level = rng.integers(0, nlevels, n_mp)
+    sf = np.array([np.float32(scale) ** i for i in range(nlevels)], np.float64)
+    mp = np.zeros(n_mp, MAP_POINT_DTYPE)
+    mp["pos"] = X
+    nrm = (X - Ow) / dist[:, None]
+    nrm += rng.normal(scale=0.02, size=nrm.shape)
+    mp["normal"] = nrm / np.linalg.norm(nrm, axis=1, keepdims=True)
+    # choose min distance so that the predicted level is `level`
+    mp["min_dist"] = dist / (sf[level] * 0.97)
+    mp["max_dist"] = mp["min_dist"] * sf[-1] * 1.2
+    mp_desc = rng.integers(0, 256, (n_mp, 32), dtype=np.uint8)
+    u, v, z = project(Tcw, X, cam)
+    vis = np.nonzero((z > 0) & (u >= 0) & (u < w) & (v >= 0) & (v < h))[0]
+    vis = vis[: n_kp]
+    nvis = len(vis)
+    kps = np.zeros(n_kp, KEYPOINT_DTYPE)
+    kp_mp = np.full(n_kp, -1, np.int32)
+    ku = u[vis] + rng.uniform(-1, 1, nvis)
+    kv = v[vis] + rng.uniform(-1, 1, nvis)
+    nout = int(outlier_frac * nvis)
+    sel = rng.choice(nvis, nout, replace=False) if nout else np.zeros(0, int)
+    ang = rng.uniform(0, 2 * np.pi, nout)
+    rad = rng.uniform(3, 6, nout)
+    ku[sel] += rad * np.cos(ang)
+    kv[sel] += rad * np.sin(ang)
+    kps["x"][:nvis], kps["y"][:nvis] = np.clip(ku, 0, w - 1), np.clip(kv, 0, h - 1)
+    lvl = level[vis] - (rng.uniform(size=nvis) < 0.3)
+    kps["octave"][:nvis] = np.clip(lvl, 0, nlevels - 1)
+    kp_mp[:nvis] = vis
+    desc = np.zeros((n_kp, 32), np.uint8)
+    desc[:nvis] = flip_bits(rng, mp_desc[vis], max_flip)
+    nd = n_kp - nvis
+    kps["x"][nvis:] = rng.uniform(0, w - 1, nd)
+    kps["y"][nvis:] = rng.uniform(0, h - 1, nd)
+    kps["octave"][nvis:] = rng.integers(0, nlevels, nd)
+    desc[nvis:] = rng.integers(0, 256, (nd, 32), dtype=np.uint8)
+    kps["angle"] = rng.uniform(0, 360, n_kp)
+    kps["size"] = 31 * sf[kps["octave"]]
+    kps["response"] = rng.integers(7, 80, n_kp)
+    kps["class_id"] = -1
+    perm = rng.permutation(n_kp)
+    kps, desc, kp_mp = kps[perm], desc[perm], kp_mp[perm]
+    # level-major order like the extractor output
+    order = np.argsort(kps["octave"], kind="stable")
+    kps, desc, kp_mp = kps[order], desc[order], kp_mp[order]
+    return {"map": mp, "mp_desc": mp_desc, "Tcw": Tcw, "keypoints": np.ascontiguousarray(kps),
+            "descriptors": np.ascontiguousarray(desc), "kp_mp": kp_mp, "camera": cam}

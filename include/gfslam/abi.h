@@ -93,6 +93,87 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
 int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, uint8_t* out,
                              int* w, int* h);
 
+/* ------------------------------------------------------ matching (E8, M1-M5, M7)
+ * Frame view (include/Frame.h:44-150): keypoints mvKeysUn (== mvKeys when
+ * k1 == 0, Frame.cc:391-395), descriptors, undistorted image bounds
+ * mnMinX..mnMaxY (Frame.cc:470-476), intrinsics, scale pyramid. The 64x48
+ * keypoint grid (Frame.cc:100-131) is built on the device per call. */
+typedef struct gf_frame_info {
+    int32_t min_x, max_x, min_y, max_y;
+    float fx, fy, cx, cy;
+    int32_t nlevels;
+    float scale_factor; /* mvScaleFactors[l] = scale_factor^l (float products) */
+} gf_frame_info;
+
+/* MapPoint state used by the tracker (include/MapPoint.h): world position,
+ * mean viewing direction, scale-invariance distances mfMinDistance /
+ * mfMaxDistance (MapPoint.cc:326-336). Descriptors travel separately (32 B). */
+typedef struct gf_map_point {
+    float pos[3];
+    float normal[3];
+    float min_dist, max_dist;
+} gf_map_point;
+
+/* Projection state Frame::isInFrustum writes into a MapPoint
+ * (Frame.cc:216-222): mTrackProjX/Y, mTrackViewCos, mnTrackScaleLevel,
+ * mbTrackInView (in_view = mbTrackInView && !isBad()). */
+typedef struct gf_mp_view {
+    float u, v, view_cos;
+    int32_t level;
+    int32_t in_view;
+} gf_mp_view;
+
+/* Frame::isInFrustum(pMP, viewingCosLimit), Frame.cc:166-227, for m map
+ * points at pose Tcw (row-major 4x4 float). */
+int gf_frustum(gf_ctx* ctx, const gf_frame_info* fi, const float* Tcw, const gf_map_point* mps, int m,
+               float view_cos_limit, gf_mp_view* views, int* n_in_view);
+
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, th),
+ * ORBmatcher.cc:384-465 (M2; with RadiusByViewingCos :696-702,
+ * Frame::GetFeaturesInArea Frame.cc:300-365). Map points are processed in
+ * list order; a keypoint already claimed (kp2mp[i] >= 0 on entry, or by an
+ * earlier map point) is skipped, exactly as F.mvpMapPoints[idx] != NULL.
+ * kp2mp/score are in/out (mvpMapPoints / mvpMatchScore, index of the map
+ * point in `views`); nmatches = new matches. */
+int gf_match_project(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                     const gf_mp_view* views, const uint8_t* mp_desc, int m, float th, float nnratio,
+                     int32_t* kp2mp, int32_t* score, int* nmatches);
+
+/* ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th),
+ * ORBmatcher.cc:2081-2202, with the rotation-consistency histogram
+ * (ComputeThreeMaxima :2338-2379) when check_ori != 0 (M3). Last-frame
+ * keypoint i carries map point last_kp2mp[i] (-1: none) at world position
+ * last_pos[3i..3i+2] and outlier flag last_outlier[i]. Matches write
+ * kp2mp[j] = last_kp2mp[i] and score[j]; rejected rotations reset score to
+ * 999 (:2183-2186). */
+int gf_match_lastframe(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                       const float* Tcw, const gf_keypoint* last_kps, const uint8_t* last_desc,
+                       const int32_t* last_kp2mp, const uint8_t* last_outlier, const float* last_pos, int n_last,
+                       float th, int check_ori, int32_t* kp2mp, int32_t* score, int* nmatches);
+
+/* Device family of the three above, batched over nframes independent frames.
+ * Per-frame arrays are strided by their capacity (kp_cap keypoints, mp_cap /
+ * last_cap queries); counts live on the device (d_n, d_m, d_n_last). Limits:
+ * kp_cap <= 4096, mp_cap/last_cap <= 8192. gf_match_lastframe_dev needs
+ * d_scratch of nframes*last_cap int32. */
+int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw, const gf_map_point* d_mps,
+                   const int32_t* d_m, int mp_cap, float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview,
+                   void* stream);
+int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                         const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                         const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, float th, float nnratio,
+                         int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream);
+int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                           const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const float* d_Tcw,
+                           const gf_keypoint* d_last_kps, const uint8_t* d_last_desc, const int32_t* d_last_kp2mp,
+                           const uint8_t* d_last_outlier, const float* d_last_pos, const int32_t* d_n_last,
+                           int last_cap, float th, int check_ori, int32_t* d_kp2mp, int32_t* d_score,
+                           int32_t* d_nmatches, int32_t* d_scratch, void* stream);
+
+/* ORBmatcher::DescriptorDistance (ORBmatcher.cc:2384-2400) over n pairs of
+ * 32-byte rows: dist[i] = popcount(a[i] ^ b[i]). */
+int gf_descriptor_distance(gf_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int32_t* dist);
+
 #ifdef __cplusplus
 }
 #endif

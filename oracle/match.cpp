@@ -1,0 +1,290 @@
+// CPU ORACLE (test infrastructure) — matching rows E8, M1-M3, M7 of
+// SURVEY.md §8a, restated sequentially from src/ORBmatcher.cc and src/Frame.cc.
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "oracle_common.h"
+
+namespace orc {
+
+static const int kGridCols = 64, kGridRows = 48;  // Frame.h:35-36
+static const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+
+struct FrameGrid {
+    const gf_frame_info* fi;
+    const gf_keypoint* kps;
+    int n;
+    float invW, invH;
+    std::vector<float> scales;
+    std::vector<int> grid[kGridCols][kGridRows];
+
+    FrameGrid(const gf_frame_info* f, const gf_keypoint* k, int nk) : fi(f), kps(k), n(nk) {
+        // Frame.cc:91-92 and :114-131
+        invW = (float)kGridCols / (float)(fi->max_x - fi->min_x);
+        invH = (float)kGridRows / (float)(fi->max_y - fi->min_y);
+        scales.resize(fi->nlevels);
+        scales[0] = 1.f;
+        for (int i = 1; i < fi->nlevels; i++) scales[i] = scales[i - 1] * fi->scale_factor;
+        for (int i = 0; i < n; i++) {
+            int px = (int)std::round((kps[i].x - fi->min_x) * invW);
+            int py = (int)std::round((kps[i].y - fi->min_y) * invH);
+            if (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) continue;
+            grid[px][py].push_back(i);
+        }
+    }
+
+    // Frame::GetFeaturesInArea, Frame.cc:300-365
+    std::vector<int> area(float x, float y, float r, int minLevel, int maxLevel) const {
+        std::vector<int> out;
+        int nMinCellX = (int)std::floor((x - fi->min_x - r) * invW);
+        nMinCellX = std::max(0, nMinCellX);
+        if (nMinCellX >= kGridCols) return out;
+        int nMaxCellX = (int)std::ceil((x - fi->min_x + r) * invW);
+        nMaxCellX = std::min(kGridCols - 1, nMaxCellX);
+        if (nMaxCellX < 0) return out;
+        int nMinCellY = (int)std::floor((y - fi->min_y - r) * invH);
+        nMinCellY = std::max(0, nMinCellY);
+        if (nMinCellY >= kGridRows) return out;
+        int nMaxCellY = (int)std::ceil((y - fi->min_y + r) * invH);
+        nMaxCellY = std::min(kGridRows - 1, nMaxCellY);
+        if (nMaxCellY < 0) return out;
+        bool check = !(minLevel == -1 && maxLevel == -1);
+        bool same = check && minLevel == maxLevel;
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+                for (int idx : grid[ix][iy]) {
+                    const gf_keypoint& k = kps[idx];
+                    if (check && !same) {
+                        if (k.octave < minLevel || k.octave > maxLevel) continue;
+                    } else if (same) {
+                        if (k.octave != minLevel) continue;
+                    }
+                    if (std::fabs(k.x - x) > r || std::fabs(k.y - y) > r) continue;
+                    out.push_back(idx);
+                }
+        return out;
+    }
+};
+
+// ORBmatcher::DescriptorDistance, ORBmatcher.cc:2384-2400
+int descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    int dist = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t va, vb;
+        std::memcpy(&va, a + 4 * i, 4);
+        std::memcpy(&vb, b + 4 * i, 4);
+        uint32_t v = va ^ vb;
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return dist;
+}
+
+// ORBmatcher::RadiusByViewingCos, ORBmatcher.cc:696-702
+static float radius_by_viewing_cos(float c) { return c > 0.998 ? 2.5f : 4.0f; }
+
+// ORBmatcher::ComputeThreeMaxima, ORBmatcher.cc:2338-2379
+void three_maxima(const int* histo, int L, int& ind1, int& ind2, int& ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    ind1 = ind2 = ind3 = -1;
+    for (int i = 0; i < L; i++) {
+        const int s = histo[i];
+        if (s > max1) {
+            max3 = max2;
+            max2 = max1;
+            max1 = s;
+            ind3 = ind2;
+            ind2 = ind1;
+            ind1 = i;
+        } else if (s > max2) {
+            max3 = max2;
+            max2 = s;
+            ind3 = ind2;
+            ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1;
+        ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+}
+
+// Pc = R * P + t, float, left-to-right, no contraction (cv::Mat
+// float gemm restated).
+static inline void transform(const float* T, const float* P, float* Pc) {
+    for (int r = 0; r < 3; r++) {
+        float a = T[4 * r + 0] * P[0];
+        float b = T[4 * r + 1] * P[1];
+        float c = T[4 * r + 2] * P[2];
+        Pc[r] = ((a + b) + c) + T[4 * r + 3];
+    }
+}
+
+}  // namespace orc
+
+extern "C" {
+
+int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return orc::descriptor_distance(a, b); }
+
+// Frame::isInFrustum, Frame.cc:166-227
+int orc_frustum(const gf_frame_info* fi, const float* Tcw, const gf_map_point* mps, int m, float viewCosLimit,
+                gf_mp_view* views, int* n_in_view) {
+    std::vector<float> scales(fi->nlevels);
+    scales[0] = 1.f;
+    for (int i = 1; i < fi->nlevels; i++) scales[i] = scales[i - 1] * fi->scale_factor;
+    // Ow = -Rcw^T * tcw (Frame::UpdatePoseMatrices :143-148)
+    float Ow[3];
+    for (int c = 0; c < 3; c++) {
+        float a = Tcw[0 * 4 + c] * Tcw[3], b = Tcw[1 * 4 + c] * Tcw[7], d = Tcw[2 * 4 + c] * Tcw[11];
+        Ow[c] = -((a + b) + d);
+    }
+    int cnt = 0;
+    for (int i = 0; i < m; i++) {
+        gf_mp_view& v = views[i];
+        v.in_view = 0;
+        v.u = v.v = v.view_cos = 0.f;
+        v.level = 0;
+        const float* P = mps[i].pos;
+        float Pc[3];
+        orc::transform(Tcw, P, Pc);
+        if (Pc[2] < 0.0) continue;
+        const float invz = (float)(1.0 / (double)Pc[2]);
+        const float u = fi->fx * Pc[0] * invz + fi->cx;
+        const float vv = fi->fy * Pc[1] * invz + fi->cy;
+        if (u < fi->min_x || u > fi->max_x) continue;
+        if (vv < fi->min_y || vv > fi->max_y) continue;
+        const float maxD = mps[i].max_dist, minD = mps[i].min_dist;
+        const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+        const float dist = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist < minD || dist > maxD) continue;
+        const float* Pn = mps[i].normal;
+        double dot = (double)PO[0] * Pn[0] + (double)PO[1] * Pn[1] + (double)PO[2] * Pn[2];
+        float viewCos = (float)(dot / dist);
+        if (viewCos < viewCosLimit) continue;
+        float ratio = dist / minD;
+        int lvl = 0;
+        while (lvl < fi->nlevels && scales[lvl] < ratio) lvl++;  // lower_bound
+        if (lvl >= fi->nlevels) lvl = fi->nlevels - 1;
+        v.in_view = 1;
+        v.u = u;
+        v.v = vv;
+        v.level = lvl;
+        v.view_cos = viewCos;
+        cnt++;
+    }
+    *n_in_view = cnt;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th), :384-465
+int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                      const gf_mp_view* views, const uint8_t* mp_desc, int m, float th, float nnratio,
+                      int32_t* kp2mp, int32_t* score, int* nmatches) {
+    orc::FrameGrid G(fi, kps, n);
+    int nm = 0;
+    const bool bFactor = th != 1.0;
+    for (int k = 0; k < m; k++) {
+        const gf_mp_view& v = views[k];
+        if (!v.in_view) continue;
+        const int pl = v.level;
+        float r = orc::radius_by_viewing_cos(v.view_cos);
+        if (bFactor) r *= th;
+        std::vector<int> near = G.area(v.u, v.v, r * G.scales[pl], pl - 1, pl);
+        if (near.empty()) continue;
+        int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+        for (int idx : near) {
+            if (kp2mp[idx] >= 0) continue;
+            const int dist = orc::descriptor_distance(mp_desc + 32 * (size_t)k, desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = kps[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kps[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= orc::TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            kp2mp[bestIdx] = k;
+            score[bestIdx] = bestDist;
+            nm++;
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th), :2081-2202
+int orc_match_lastframe(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n, const float* Tcw,
+                        const gf_keypoint* last_kps, const uint8_t* last_desc, const int32_t* last_kp2mp,
+                        const uint8_t* last_outlier, const float* last_pos, int n_last, float th, int check_ori,
+                        int32_t* kp2mp, int32_t* score, int* nmatches) {
+    orc::FrameGrid G(fi, kps, n);
+    std::vector<int> rotHist[orc::HISTO_LENGTH];
+    const float factor = 1.0f / orc::HISTO_LENGTH;
+    int nm = 0;
+    for (int i = 0; i < n_last; i++) {
+        if (last_kp2mp[i] < 0 || last_outlier[i]) continue;
+        float Pc[3];
+        orc::transform(Tcw, last_pos + 3 * (size_t)i, Pc);
+        const float xc = Pc[0], yc = Pc[1];
+        const float invzc = (float)(1.0 / (double)Pc[2]);
+        float u = fi->fx * xc * invzc + fi->cx;
+        float v = fi->fy * yc * invzc + fi->cy;
+        if (u < fi->min_x || u > fi->max_x) continue;
+        if (v < fi->min_y || v > fi->max_y) continue;
+        int oct = last_kps[i].octave;
+        float radius = th * G.scales[oct];
+        std::vector<int> idx2 = G.area(u, v, radius, oct - 1, oct + 1);
+        if (idx2.empty()) continue;
+        int bestDist = INT_MAX, bestIdx2 = -1;
+        for (int i2 : idx2) {
+            if (kp2mp[i2] >= 0) continue;
+            int dist = orc::descriptor_distance(last_desc + 32 * (size_t)i, desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= orc::TH_HIGH) {
+            kp2mp[bestIdx2] = last_kp2mp[i];
+            score[bestIdx2] = bestDist;
+            nm++;
+            if (check_ori) {
+                float rot = last_kps[i].angle - kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == orc::HISTO_LENGTH) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    if (check_ori) {
+        int sizes[orc::HISTO_LENGTH], i1, i2, i3;
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) sizes[b] = (int)rotHist[b].size();
+        orc::three_maxima(sizes, orc::HISTO_LENGTH, i1, i2, i3);
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int j : rotHist[b]) {
+                kp2mp[j] = -1;
+                score[j] = 999;
+                nm--;
+            }
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+}  // extern "C"

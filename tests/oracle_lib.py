@@ -63,3 +63,31 @@ def plan(w, h, nfeatures=1000, scale=1.2, nlevels=8):
     orc().orc_extractor_plan(w, h, nfeatures, ctypes.c_float(scale), nlevels, _p(lw), _p(lh), _p(fpl), _p(sc),
                              _p(um))
     return lw, lh, fpl, sc, um
+
+
+def frustum(info, Tcw, mps, view_cos=0.5):
+    from gf_orb_slam_amd.matcher import MP_VIEW_DTYPE
+    mps = np.ascontiguousarray(mps)
+    views = np.zeros(len(mps), MP_VIEW_DTYPE)
+    n = ctypes.c_int()
+    orc().orc_frustum(ctypes.byref(info), _p(np.ascontiguousarray(Tcw, np.float32)), _p(mps), len(mps),
+                      ctypes.c_float(view_cos), _p(views), ctypes.byref(n))
+    return views, n.value
+
+
+def match_project(info, kps, desc, views, mp_desc, th, nnratio, kp2mp, score):
+    n = ctypes.c_int()
+    orc().orc_match_project(ctypes.byref(info), _p(kps), _p(desc), len(kps), _p(views), _p(mp_desc), len(views),
+                            ctypes.c_float(th), ctypes.c_float(nnratio), _p(kp2mp), _p(score), ctypes.byref(n))
+    return n.value
+
+
+def match_lastframe(info, kps, desc, Tcw, last_kps, last_desc, last_kp2mp, last_outlier, last_pos, th, check_ori,
+                    kp2mp, score):
+    n = ctypes.c_int()
+    orc().orc_match_lastframe(ctypes.byref(info), _p(kps), _p(desc), len(kps),
+                              _p(np.ascontiguousarray(Tcw, np.float32)), _p(last_kps), _p(last_desc),
+                              _p(last_kp2mp), _p(last_outlier), _p(np.ascontiguousarray(last_pos, np.float32)),
+                              len(last_kps), ctypes.c_float(th), int(check_ori), _p(kp2mp), _p(score),
+                              ctypes.byref(n))
+    return n.value
