@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""GF-ORB-SLAM front-end benchmark (BASELINE.json metric).
+
+Metric: front-end fps (extract + match + GF-select) @ 752x480 / 1000 feats
+(config 2: EuRoC-geometry synthetic frames, one MI355X per rank). One step =
+one frame of each of B independent streams through the device-resident hot
+path (gf_orb_slam_amd.pipeline.FrontEnd); value = frames of all ranks / wall
+time. Multi-GPU: one process per GPU (torchrun), streams shard across ranks
+with no data-path collective ("weak" scaling); rank 0 broadcasts the shared
+vocabulary/map blob over RCCL once before timing.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# Algorithmic bytes per frame for the extraction kernels,
+# computed from the level sizes: P = sum of pyramid pixels.
+LEVELS = {"euroc": [(752, 480), (627, 400), (522, 333), (435, 278), (363, 231), (302, 193), (252, 161), (210, 134)],
+          "tum": [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231), (257, 193), (214, 161), (179, 134)]}
+
+
+def kernel_bytes(camera: str, nfeat: int) -> dict:
+    px = [w * h for w, h in LEVELS[camera]]
+    P, P0, P7 = sum(px), px[0], px[-1]
+    return {
+        "k_resize": (P - P7) + (P - P0),  # read level l-1, write level l
+        "k_blur": 2 * P,                  # read + write every level
+        "k_fast": P,                      # FAST reads every pyramid pixel once
+        "k_describe": 60 * nfeat,         # 32 B descriptor + 28 B keypoint out
+        "extract_total": (P - P7) + (P - P0) + P + 2 * P + 60 * nfeat,
+    }
+
+
+def cpu_baseline(camera: str, nfeat: int, budget_s: float = 12.0) -> dict:
+    """Oracle (CPU restatement, 1 thread) on a bounded sample of the same
+    workload: extraction + frustum + SearchByProjection per frame."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+
+    from gf_orb_slam_amd import synth
+    from gf_orb_slam_amd.matcher import FrameInfo
+    from gf_orb_slam_amd.pipeline import build_local_map
+
+    cam = synth.CAMERAS[camera]
+    info = FrameInfo.make(*cam)
+    frames = [synth.synth_frame(cam[0], cam[1], synth.frame_seed(99, i)) for i in range(4)]
+    prep = []
+    for i, img in enumerate(frames):
+        rng = np.random.default_rng(1000 + i)
+        k, d = O.extract(img, nfeatures=nfeat)
+        mp, md = build_local_map(k, d, cam, rng, 2000)
+        T = synth.look_pose(rng, 0.002, 0.05)
+        prep.append((img, mp, md, T))
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        img, mp, md, T = prep[n % len(prep)]
+        k, d = O.extract(img, nfeatures=nfeat)
+        views, _ = O.frustum(info, T, mp)
+        kp2mp = np.full(len(k), -1, np.int32)
+        score = np.full(len(k), 999, np.int32)
+        O.match_project(info, k, d, views, md, 1.0, 0.8, kp2mp, score)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames ({camera} {nfeat} feats: extract + isInFrustum + SearchByProjection, "
+                      f"2000-point local map), 1 thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="independent streams per GPU")
+    ap.add_argument("--camera", default="euroc")
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from gf_orb_slam_amd import synth
+    from gf_orb_slam_amd.pipeline import FrontEnd
+
+    cam = args.camera
+    w, h = synth.CAMERAS[cam][:2]
+    B = args.batch
+    fe = FrontEnd(cam, args.nfeatures, B, 2000, seed=rank)
+    frames = np.stack([synth.synth_frame(w, h, synth.frame_seed(rank * B + b, 0)) for b in range(min(B, 8))])
+    frames = frames[np.arange(B) % len(frames)]
+    fe.load_frames(frames)
+    fe.build_maps()
+
+    # one-off exchange: rank 0 broadcasts the shared vocabulary/map blob (RCCL over xGMI)
+    if world > 1:
+        blob = torch.zeros(45 * 1024 * 1024 // 4, dtype=torch.int32, device="cuda")
+        if rank == 0:
+            blob.copy_(torch.arange(blob.numel(), dtype=torch.int32, device="cuda"))
+        dist.broadcast(blob, src=0)
+        dist.broadcast(fe.mps, src=0)
+        dist.broadcast(fe.mp_desc, src=0)
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        fe.step()
+    fe.sync()
+    torch.cuda.synchronize()
+    fe.prof_enable(True)
+    fe.prof_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fe.step()
+    fe.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    prof = fe.prof_report()
+    fe.prof_enable(False)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+
+    nm = fe.nmatch.float().mean().item()
+    nk = fe.nkp.float().mean().item()
+    frames_total = world * B * args.steps
+    fps = frames_total / dt
+
+    # roofline of the dominant kernel (HIP events on the launch stream)
+    kb = kernel_bytes(cam, args.nfeatures)
+    per_kernel = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1]} for k, v in prof.items()}
+    dom = max(prof, key=lambda k: prof[k][0])
+    roof = None
+    if dom in kb:
+        avg_s = prof[dom][0] / prof[dom][1] / 1e3
+        achieved = kb[dom] * B / avg_s / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(achieved / 8000.0, 5), "traffic": None,
+                "bytes_per_frame": kb[dom], "frames_per_launch": B}
+    else:
+        roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
+                "traffic": None}
+    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur", "k_fast", "k_select", "k_describe") if k in prof)
+    ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
+
+    out = {
+        "metric": "front-end fps (extract+match+GF-select) @ 752x480/1000 feats; pose-opt ms/iter",
+        "value": round(fps, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int32 (f32 projection)",
+        "data": "synthetic (seeded 752x480 frames + synthetic 2000-point local maps; no dataset reachable)",
+        "config": {"workload": f"config 2: {cam} {w}x{h}, {args.nfeatures} feats, {B} streams/GPU, "
+                               f"stages: extract + isInFrustum + SearchByProjection",
+                   "streams_per_gpu": B, "parallelism": f"streams x {world} ranks"},
+        "roofline": roof,
+        "extraction_stage": {"ms_per_frame": round(ext_ms / (B * args.steps), 5),
+                             "algorithmic_GBps": round(ext_bw, 2) if ext_bw else None},
+        "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"]} for k, v in per_kernel.items()},
+        "avg_keypoints": nk,
+        "avg_matches": nm,
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -64,6 +64,9 @@ _PROTOS = {
     "gf_ctx_destroy": [_P],
     "gf_ctx_stream": [_P, _P],
     "gf_ctx_sync": [_P],
+    "gf_prof_enable": [_P, _I],
+    "gf_prof_reset": [_P],
+    "gf_prof_report": [_P, _I, _P, _I, _P, _P],
     "gf_extractor_create": [_P, _I, _F, _I, _I, _I, _I, _I, _I, _P],
     "gf_extractor_destroy": [_P],
     "gf_extractor_info": [_P, _P, _P, _P],

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/gfslam/abi.h"
 
@@ -26,9 +27,21 @@ int fail(int code, const std::string& msg);
 
 }  // namespace gf
 
+namespace gf {
+// Per-kernel HIP-event timing (enabled by gf_prof_enable): every launch site
+// brackets its kernel with an event pair on the launch stream.
+struct ProfEntry {
+    std::string name;
+    std::vector<hipEvent_t> start, stop;  // pairs, recorded in order
+};
+}  // namespace gf
+
 struct gf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool prof = false;
+    std::vector<gf::ProfEntry> prof_entries;
+    std::vector<hipEvent_t> event_pool;
     // grow-only device scratch for the host-family wrappers (one slot per use)
     static const int kSlots = 32;
     void* ws[kSlots] = {};
@@ -40,7 +53,18 @@ namespace gf {
 int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out);
 // Host-family helper: copy host -> scratch slot (returns device pointer).
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out);
+
+// RAII bracket for one kernel launch when profiling is on.
+struct ProfScope {
+    gf_ctx* ctx;
+    hipStream_t s;
+    int idx = -1;
+    ProfScope(gf_ctx* c, hipStream_t st, const char* name);
+    ~ProfScope();
+};
 }  // namespace gf
+
+#define GF_PROF(ctx, stream, name) ::gf::ProfScope _gf_prof_scope((ctx), (stream), (name))
 
 // Device-side helpers ------------------------------------------------------
 namespace gfd {

@@ -855,17 +855,35 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     const LevelGeom& g = ex->g;
     Planes P{d_imgs, (long long)frame_stride, stride, ex->d_pyr, ex->d_blur};
     ex->last = P;
-    for (int l = 1; l < ex->nlevels; l++) {
-        dim3 blk(64, 4), grd((g.w[l] + 63) / 64, (g.h[l] + 3) / 4, nframes);
-        k_resize<<<grd, blk, 0, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l], ex->d_ytab + ex->ytab_off[l]);
+    gf_ctx* ctx = ex->ctx;
+    {
+        GF_PROF(ctx, s, "k_resize");
+        for (int l = 1; l < ex->nlevels; l++) {
+            dim3 blk(64, 4), grd((g.w[l] + 63) / 64, (g.h[l] + 3) / 4, nframes);
+            k_resize<<<grd, blk, 0, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l], ex->d_ytab + ex->ytab_off[l]);
+        }
     }
-    k_blur<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g);
-    k_fast<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(P, g, ex->d_cells, ex->d_lists, ex->list_stride,
-                                                              ex->d_counts, ex->fast_th, ex->min_th);
-    k_select<<<dim3(ex->nlevels, nframes), 256, 0, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts,
-                                                        ex->d_lvl, ex->lvl_stride, ex->d_lvl_counts);
-    k_describe<<<dim3((ex->capacity + 3) / 4, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
-                                                                      ex->d_lvl_counts, d_kps, d_desc, d_counts, cap);
+    {
+        GF_PROF(ctx, s, "k_blur");
+        k_blur<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g);
+    }
+    {
+        GF_PROF(ctx, s, "k_fast");
+        k_fast<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(P, g, ex->d_cells, ex->d_lists, ex->list_stride,
+                                                                  ex->d_counts, ex->fast_th, ex->min_th);
+    }
+    {
+        GF_PROF(ctx, s, "k_select");
+        k_select<<<dim3(ex->nlevels, nframes), 256, 0, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+                                                            ex->d_counts, ex->d_lvl, ex->lvl_stride,
+                                                            ex->d_lvl_counts);
+    }
+    {
+        GF_PROF(ctx, s, "k_describe");
+        k_describe<<<dim3((ex->capacity + 3) / 4, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
+                                                                          ex->d_lvl_counts, d_kps, d_desc, d_counts,
+                                                                          cap);
+    }
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

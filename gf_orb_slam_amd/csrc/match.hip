@@ -473,6 +473,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
                                    (int)match_lds_bytes()));
         attr_mask |= 1ull << ctx->device;
     }
+    GF_PROF(ctx, s, A.mode == MODE_PROJECT ? "k_match_project" : "k_match_lastframe");
     k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -490,6 +491,7 @@ int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const floa
     hipStream_t s = (hipStream_t)stream;
     FrameConst fc = gf::make_frame_const(fi);
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
+    GF_PROF(ctx, s, "k_frustum");
     k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
                                                                    d_views, d_nview);
     GF_HIP(hipGetLastError());

@@ -1,4 +1,7 @@
 // libgfslam runtime: error reporting and per-thread contexts (one HIP stream each).
+#include <string.h>
+
+#include <algorithm>
 #include <string>
 
 #include "common.h"
@@ -24,6 +27,42 @@ int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out) {
     }
     *out = ctx->ws[slot];
     return GF_OK;
+}
+
+static hipEvent_t pool_event(gf_ctx* ctx) {
+    hipEvent_t e = nullptr;
+    if (!ctx->event_pool.empty()) {
+        e = ctx->event_pool.back();
+        ctx->event_pool.pop_back();
+    } else if (hipEventCreate(&e) != hipSuccess) {
+        e = nullptr;
+    }
+    return e;
+}
+
+ProfScope::ProfScope(gf_ctx* c, hipStream_t st, const char* name) : ctx(c), s(st) {
+    if (!ctx || !ctx->prof) return;
+    for (size_t i = 0; i < ctx->prof_entries.size(); i++)
+        if (ctx->prof_entries[i].name == name) idx = (int)i;
+    if (idx < 0) {
+        ctx->prof_entries.push_back(ProfEntry{name, {}, {}});
+        idx = (int)ctx->prof_entries.size() - 1;
+    }
+    hipEvent_t e = pool_event(ctx);
+    if (!e) {
+        idx = -1;
+        return;
+    }
+    (void)hipEventRecord(e, s);
+    ctx->prof_entries[idx].start.push_back(e);
+}
+
+ProfScope::~ProfScope() {
+    if (idx < 0) return;
+    hipEvent_t e = pool_event(ctx);
+    if (!e) return;
+    (void)hipEventRecord(e, s);
+    ctx->prof_entries[idx].stop.push_back(e);
 }
 
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out) {
@@ -71,6 +110,11 @@ int gf_ctx_destroy(gf_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int i = 0; i < gf_ctx::kSlots; i++)
         if (ctx->ws[i]) (void)hipFree(ctx->ws[i]);
+    for (auto& e : ctx->prof_entries) {
+        for (auto ev : e.start) (void)hipEventDestroy(ev);
+        for (auto ev : e.stop) (void)hipEventDestroy(ev);
+    }
+    for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return GF_OK;
@@ -79,6 +123,47 @@ int gf_ctx_destroy(gf_ctx* ctx) {
 int gf_ctx_stream(gf_ctx* ctx, void** stream) {
     GF_CHECK(ctx && stream, GF_ERR_ARG, "null arg");
     *stream = (void*)ctx->stream;
+    return GF_OK;
+}
+
+int gf_prof_enable(gf_ctx* ctx, int on) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    ctx->prof = on != 0;
+    return GF_OK;
+}
+
+int gf_prof_reset(gf_ctx* ctx) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    GF_HIP(hipSetDevice(ctx->device));
+    GF_HIP(hipDeviceSynchronize());
+    for (auto& e : ctx->prof_entries) {
+        for (auto ev : e.start) ctx->event_pool.push_back(ev);
+        for (auto ev : e.stop) ctx->event_pool.push_back(ev);
+    }
+    ctx->prof_entries.clear();
+    return GF_OK;
+}
+
+int gf_prof_report(gf_ctx* ctx, int idx, char* name, int name_cap, double* total_ms, int* launches) {
+    GF_CHECK(ctx && total_ms && launches, GF_ERR_ARG, "null arg");
+    GF_CHECK(idx >= 0 && idx < (int)ctx->prof_entries.size(), GF_ERR_ARG, "no such profile entry");
+    GF_HIP(hipSetDevice(ctx->device));
+    const gf::ProfEntry& e = ctx->prof_entries[idx];
+    double tot = 0;
+    size_t n = std::min(e.start.size(), e.stop.size());
+    for (size_t i = 0; i < n; i++) {
+        GF_HIP(hipEventSynchronize(e.stop[i]));
+        float ms = 0;
+        GF_HIP(hipEventElapsedTime(&ms, e.start[i], e.stop[i]));
+        tot += ms;
+    }
+    *total_ms = tot;
+    *launches = (int)n;
+    if (name && name_cap > 0) {
+        size_t k = std::min((size_t)name_cap - 1, e.name.size());
+        memcpy(name, e.name.data(), k);
+        name[k] = 0;
+    }
     return GF_OK;
 }
 

@@ -53,6 +53,12 @@ int gf_ctx_create(int hip_device, gf_ctx** out);
 int gf_ctx_destroy(gf_ctx* ctx);
 int gf_ctx_stream(gf_ctx* ctx, void** stream);
 int gf_ctx_sync(gf_ctx* ctx);
+/* Per-kernel timing with HIP events recorded on each launch's own stream
+ * (what bench.py reports the roofline from). gf_prof_report returns, for
+ * entry idx, the kernel name, summed device time and launch count. */
+int gf_prof_enable(gf_ctx* ctx, int on);
+int gf_prof_reset(gf_ctx* ctx);
+int gf_prof_report(gf_ctx* ctx, int idx, char* name, int name_cap, double* total_ms, int* launches);
 
 /* ------------------------------------------------------- ORB extraction (E1-E8)
  * Replaces ORB_SLAM::ORBextractor (include/ORBextractor.h:57-70,
