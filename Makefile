@@ -9,6 +9,8 @@ ORCFLAGS = -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 CSRC    = gf_orb_slam_amd/csrc
 HIPSRCS = $(wildcard $(CSRC)/*.hip)
 HIPOBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIPSRCS))
+CPPSRCS = $(wildcard $(CSRC)/*.cpp)
+CPPOBJS = $(patsubst $(CSRC)/%.cpp,build/%.cpp.o,$(CPPSRCS))
 HDRS    = $(wildcard $(CSRC)/*.h) include/gfslam/abi.h
 LIB     = gf_orb_slam_amd/libgfslam.so
 
@@ -21,7 +23,11 @@ build/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(HIPOBJS)
+build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p build
+	$(CXX) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
+
+$(LIB): $(HIPOBJS) $(CPPOBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 $(ORCLIB): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h include/gfslam/abi.h

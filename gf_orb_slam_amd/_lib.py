@@ -80,6 +80,20 @@ _PROTOS = {
     "gf_descriptor_distance": [_P, _P, _P, _I, _P],
     "gf_frustum_dev": [_P, _P, _I, _P, _P, _P, _I, _F, _P, _P, _P],
     "gf_match_project_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _I, _F, _F, _P, _P, _P, _P],
+    "gf_rng_seed": [_P, ctypes.c_uint32],
+    "gf_rng_next": [_P, _P, _I],
+    "gf_obs_update": [_D, _P, _D, _P, _P],
+    "gf_obs_predict": [_P, _D, _I, _P],
+    "gf_obs_build_info": [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
+    "gf_logdet": [_P, _P, _I, _P],
+    "gf_obs_active_match": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _F, _F, _P, _P, _P, _P, _P,
+                            _P],
+    "gf_maxvol_select": [_P, _P, _P, _I, _I, _D, _I, _P, _P, _P],
+    "gf_obs_build_info_dev": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
+    "gf_obs_accumulate_dev": [_P, _I, _P, _P, _P, _I, _D, _P, _P],
+    "gf_obs_active_match_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _F, _P,
+                                _P, _P, _P, _P, _P, _P],
+    "gf_maxvol_select_dev": [_P, _I, _P, _P, _P, _I, _I, _D, _I, _P, _P, _P, _P],
     "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
                                _P, _P],
 }

@@ -1,0 +1,947 @@
+// Good-feature selection on gfx950 — SURVEY.md §8a rows G2-G7 (f64).
+//
+//   k_obs_info     one thread per landmark: measurement Jacobian H (2x7) and
+//                  information block H_rw^T H_rw (compute_H_subblock_simplied
+//                  Observability.h:460-515, reWeightInfoMat :517-596,
+//                  batchInfoMat_Map/_Frame Observability.cc:386-644)
+//   k_logdet       Util.hpp:714-731 (Cholesky, LU fallback)
+//   k_active_match one workgroup per frame: runActiveMapMatching
+//                  (Observability.cc:1249-1524). The lazier-greedy rounds are
+//                  sequential in the reference (std::rand draws, a max-heap,
+//                  one-point matches that claim keypoints); the workgroup keeps
+//                  that order exactly — draws and heap on one lane, the
+//                  log-dets of each batch of random samples across the
+//                  workgroup, grid/claims/pool/heap in LDS.
+//   k_maxvol       one workgroup per pool: maxVolSelection_BaselineGreedy /
+//                  _LazierGreedy / maxVolDeletion_LazierGreedy
+//                  (Observability.cc:2339-3155).
+#include <cfloat>
+#include <climits>
+#include <cmath>
+
+#include "common.h"
+#include "match_common.h"
+#include "rng.h"
+#include "select.h"
+
+#define POOL_MAX 4096
+#define GF_THREADS 256
+#define MAX_RANDOM_QUERY_TIME 2000
+
+namespace {
+
+// ------------------------------------------------------------- math helpers
+__device__ __forceinline__ void q2r(const double* q, double R[3][3]) {
+    const double x = q[1], y = q[2], z = q[3], r = q[0];
+    R[0][0] = r * r + x * x - y * y - z * z;
+    R[0][1] = 2.0 * (x * y - r * z);
+    R[0][2] = 2.0 * (z * x + r * y);
+    R[1][0] = 2.0 * (x * y + r * z);
+    R[1][1] = r * r - x * x + y * y - z * z;
+    R[1][2] = 2.0 * (y * z - r * x);
+    R[2][0] = 2.0 * (z * x - r * y);
+    R[2][1] = 2.0 * (y * z + r * x);
+    R[2][2] = r * r - x * x - y * y + z * z;
+}
+
+// arma::inv of a 3x3 (cofactors / determinant)
+__device__ __forceinline__ bool inv3(const double X[3][3], double O[3][3]) {
+    const double v1 = X[0][0] * (X[2][2] * X[1][1] - X[1][2] * X[2][1]);
+    const double v2 = X[0][1] * (X[2][2] * X[1][0] - X[1][2] * X[2][0]);
+    const double v3 = X[0][2] * (X[2][1] * X[1][0] - X[1][1] * X[2][0]);
+    const double det = v1 - v2 + v3;
+    if (fabs(det) < DBL_EPSILON) return false;
+    O[0][0] = (X[2][2] * X[1][1] - X[1][2] * X[2][1]) / det;
+    O[1][0] = -(X[2][2] * X[1][0] - X[2][0] * X[1][2]) / det;
+    O[2][0] = (X[2][1] * X[1][0] - X[2][0] * X[1][1]) / det;
+    O[0][1] = -(X[2][2] * X[0][1] - X[2][1] * X[0][2]) / det;
+    O[1][1] = (X[2][2] * X[0][0] - X[2][0] * X[0][2]) / det;
+    O[2][1] = -(X[2][1] * X[0][0] - X[2][0] * X[0][1]) / det;
+    O[0][2] = (X[1][2] * X[0][1] - X[1][1] * X[0][2]) / det;
+    O[1][2] = -(X[1][2] * X[0][0] - X[1][0] * X[0][2]) / det;
+    O[2][2] = (X[1][1] * X[0][0] - X[1][0] * X[0][1]) / det;
+    return true;
+}
+
+// H = [H13 H47] (2x7 row-major) and the projected pixel; false when the
+// visibility check rejects the landmark.
+__device__ bool landmark_jacobian(const gf_obs_camera& cam, const double* Xv, const double* y, bool check_viz,
+                                  double* H, float* uv) {
+    const double* q = Xv + 3;
+    double Rq[3][3], R[3][3];
+    q2r(q, Rq);
+    if (!inv3(Rq, R))
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[i][j] = 0;
+    const double t[3] = {y[0] - Xv[0], y[1] - Xv[1], y[2] - Xv[2]};
+    double h[3];
+    for (int i = 0; i < 3; i++) h[i] = R[i][0] * t[0] + R[i][1] * t[1] + R[i][2] * t[2];
+    float u = FLT_MAX, v = FLT_MAX;
+    if (h[2] > 0) {
+        u = (float)((double)(float)cam.fu * h[0] / h[2] + (double)(float)cam.cx);
+        v = (float)((double)(float)cam.fv * h[1] / h[2] + (double)(float)cam.cy);
+    }
+    uv[0] = u;
+    uv[1] = v;
+    if (check_viz) {
+        if (h[2] < 0.0 + cam.bound_depth) return false;
+        if (u < cam.min_x - cam.bound_x || u > cam.max_x + cam.bound_x) return false;
+        if (v < cam.min_y - cam.bound_y || v > cam.max_y + cam.bound_y) return false;
+    }
+    double dh[2][3] = {{0, 0, 0}, {0, 0, 0}};
+    if (!(fabs(h[2]) < 1e-6)) {
+        const double z2 = h[2] * h[2];
+        dh[0][0] = cam.fu / h[2];
+        dh[0][2] = -h[0] * cam.fu / z2;
+        dh[1][1] = cam.fv / h[2];
+        dh[1][2] = -h[1] * cam.fv / z2;
+    }
+    // dRq_times_a_by_dq(qconj(q), t) * diag(1,-1,-1,-1), Util.hpp:391-438
+    const double q0 = q[0], qx = -1.0 * q[1], qy = -1.0 * q[2], qz = -1.0 * q[3];
+    const double D[4][3][3] = {
+        {{2.0 * q0, -2.0 * qz, 2.0 * qy}, {2.0 * qz, 2.0 * q0, -2.0 * qx}, {-2.0 * qy, 2.0 * qx, 2.0 * q0}},
+        {{2.0 * qx, 2.0 * qy, 2.0 * qz}, {2.0 * qy, -2.0 * qx, -2.0 * q0}, {2.0 * qz, 2.0 * q0, -2.0 * qx}},
+        {{-2.0 * qy, 2.0 * qx, 2.0 * q0}, {2.0 * qx, 2.0 * qy, 2.0 * qz}, {-2.0 * q0, 2.0 * qz, -2.0 * qy}},
+        {{-2.0 * qz, -2.0 * q0, 2.0 * qx}, {2.0 * q0, -2.0 * qz, 2.0 * qy}, {2.0 * qx, 2.0 * qy, 2.0 * qz}}};
+    double dR[3][4];
+    for (int c = 0; c < 4; c++)
+        for (int r = 0; r < 3; r++) {
+            double e = D[c][r][0] * t[0] + D[c][r][1] * t[1] + D[c][r][2] * t[2];
+            dR[r][c] = c ? -e : e;
+        }
+    for (int i = 0; i < 2; i++) {
+        for (int j = 0; j < 3; j++) H[7 * i + j] = -1.0 * (dh[i][0] * R[0][j] + dh[i][1] * R[1][j] + dh[i][2] * R[2][j]);
+        for (int j = 0; j < 4; j++) H[7 * i + 3 + j] = dh[i][0] * dR[0][j] + dh[i][1] * dR[1][j] + dh[i][2] * dR[2][j];
+    }
+    return true;
+}
+
+// information block of H / sigma (reWeightInfoMat + H_rw^T H_rw)
+__device__ __forceinline__ void add_info_block(const double* H, double sigma2, double* M) {
+    const double s = sqrt(sigma2);
+    const double w = s / (s * s);
+    double Hw[14];
+    for (int i = 0; i < 14; i++) Hw[i] = w * H[i];
+    for (int i = 0; i < 7; i++)
+        for (int j = 0; j < 7; j++) M[7 * i + j] = M[7 * i + j] + (Hw[i] * Hw[j] + Hw[7 + i] * Hw[7 + j]);
+}
+
+__device__ __noinline__ double logdet_lu(const double* M) {
+    double A[49];
+    for (int i = 0; i < 49; i++) A[i] = M[i];
+    double acc = 0;
+    for (int c = 0; c < 7; c++) {
+        int p = c;
+        double best = fabs(A[7 * c + c]);
+        for (int r = c + 1; r < 7; r++)
+            if (fabs(A[7 * r + c]) > best) best = fabs(A[7 * r + c]), p = r;
+        if (p != c)
+            for (int k = 0; k < 7; k++) {
+                double t = A[7 * c + k];
+                A[7 * c + k] = A[7 * p + k];
+                A[7 * p + k] = t;
+            }
+        const double piv = A[7 * c + c];
+        if (piv != 0)
+            for (int r = c + 1; r < 7; r++) {
+                const double f = A[7 * r + c] / piv;
+                A[7 * r + c] = f;
+                for (int k = c + 1; k < 7; k++) A[7 * r + k] -= f * A[7 * c + k];
+            }
+        acc += log(fabs(piv));
+    }
+    return acc;
+}
+
+// logDet(a + sign*b), Util.hpp:714-731: 2 log prod diag chol, else LU.
+__device__ double logdet_sum(const double* a, const double* b, double sign) {
+    double M[49];
+#pragma unroll
+    for (int i = 0; i < 49; i++) M[i] = sign > 0 ? a[i] + b[i] : a[i] - b[i];
+    double L[28];  // packed lower triangle, row-major
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        double s = M[8 * j];
+#pragma unroll
+        for (int k = 0; k < j; k++) s -= L[j * (j + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+        if (!(s > 0)) {
+            ok = false;
+            break;
+        }
+        const double d = sqrt(s);
+        L[j * (j + 1) / 2 + j] = d;
+        const double rd = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 7; i++) {
+            double t = M[7 * i + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) t -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+            L[i * (i + 1) / 2 + j] = t * rd;
+        }
+    }
+    if (!ok) return logdet_lu(M);
+    double v1 = 1, v2 = 1;  // Armadillo's two-accumulator product of the diagonal
+    v1 *= L[0];
+    v2 *= L[2];
+    v1 *= L[5];
+    v2 *= L[9];
+    v1 *= L[14];
+    v2 *= L[20];
+    v1 *= L[27];
+    return 2 * log(v1 * v2);
+}
+
+// ------------------------------------------------------------- k_obs_info
+__global__ void k_obs_info(gf_obs_camera cam, const double* __restrict__ Xv, const float* __restrict__ pos,
+                           const float* __restrict__ sigma2, const int32_t* __restrict__ n, int cap, int check_viz,
+                           double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
+                           uint8_t* __restrict__ valid) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n[f]) return;
+    const long long g = (long long)f * cap + i;
+    const double y[3] = {pos[3 * g], pos[3 * g + 1], pos[3 * g + 2]};
+    double H[14];
+    float p[2];
+    const bool ok = landmark_jacobian(cam, Xv + 13 * f, y, check_viz != 0, H, p);
+    uv[2 * g] = p[0];
+    uv[2 * g + 1] = p[1];
+    valid[g] = ok;
+    double M[49];
+    for (int k = 0; k < 49; k++) M[k] = 0;
+    if (ok) add_info_block(H, sigma2 ? (double)sigma2[g] : 1.0, M);
+    for (int k = 0; k < 14; k++) Hout[14 * g + k] = ok ? H[k] : 0.0;
+    for (int k = 0; k < 49; k++) info[49 * g + k] = M[k];
+}
+
+__global__ void k_logdet(const double* __restrict__ M, int n, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double z[49];
+    for (int k = 0; k < 49; k++) z[k] = 0;
+    out[i] = logdet_sum(M + 49LL * i, z, 1.0);
+}
+
+// Sum of information blocks of flagged entries: out[f] = base + sum info[i].
+__global__ void k_obs_accumulate(const double* __restrict__ info, const uint8_t* __restrict__ flag,
+                                 const int32_t* __restrict__ n, int cap, double diag, double* __restrict__ out) {
+    const int f = blockIdx.x;
+    const int e = threadIdx.x;  // 49 entries
+    if (e >= 49) return;
+    double s = (e % 8 == 0) ? diag : 0.0;
+    for (int i = 0; i < n[f]; i++) {
+        const long long g = (long long)f * cap + i;
+        if (flag[g]) s = s + info[49 * g + e];
+    }
+    out[49LL * f + e] = s;
+}
+
+// ------------------------------------------------------------- active matching
+struct HeapEntry {
+    double s;
+    int idx;
+    int pad;
+};
+struct HeapLess {  // std::priority_queue<SimplePoint>: SimplePoint::operator< on score
+    __device__ bool operator()(const HeapEntry& a, const HeapEntry& b) const { return a.s < b.s; }
+};
+
+struct ActiveArgs {
+    FrameConst fc;
+    const gf_keypoint* kps;
+    const uint8_t* desc;
+    const int32_t* n;
+    int kp_cap;
+    const gf_mp_view* views;
+    const uint8_t* mp_desc;
+    const uint8_t* updated;
+    const double* info;
+    const double* H;
+    const int32_t* m;
+    int mp_cap;
+    const double* base;  // [F][49]
+    float sigma2[16];
+    const int32_t* num_to_match;  // [F]
+    float th, nnratio;
+    gf_rng* rng;  // [F]
+    int32_t* kp2mp;
+    int32_t* score;
+    int32_t* left;
+    int32_t* nleft;
+    int32_t* nmatched;
+    int32_t* err;
+};
+
+// ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) on one lane.
+__device__ int one_point_match(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
+                               const int* items, int* claim, const gf_keypoint* K, const uint8_t* D) {
+    const gf_mp_view v = A.views[(long long)f * A.mp_cap + mpi];
+    if (!v.in_view) return -1;
+    const int pl = min(max(v.level, 0), fc.nlevels - 1);
+    float r = v.view_cos > 0.998 ? 2.5f : 4.0f;
+    if (A.th != 1.0) r *= A.th;
+    r = r * fc.scales[pl];
+    int cx0, cx1, cy0, cy1;
+    if (!grid_window(fc, v.u, v.v, r, cx0, cx1, cy0, cy1)) return -1;
+    const uint8_t* qd = A.mp_desc + ((long long)f * A.mp_cap + mpi) * 32;
+    int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+    for (int ix = cx0; ix <= cx1; ix++) {
+        const int s = cell_start[ix * GRID_ROWS + cy0], e = cell_start[ix * GRID_ROWS + cy1 + 1];
+        for (int t = s; t < e; t++) {
+            const int idx = items[t];
+            const gf_keypoint kp = K[idx];
+            if (!level_ok(kp.octave, pl - 1, pl)) continue;
+            if (fabsf(kp.x - v.u) > r || fabsf(kp.y - v.v) > r) continue;
+            if (claim[idx] >= 0) continue;
+            const int dist = hamming32(qd, D + (long long)idx * 32);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = kp.octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kp.octave;
+                bestDist2 = dist;
+            }
+        }
+    }
+    if (bestDist <= TH_HIGH) {
+        if (bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2) return -1;
+        claim[bestIdx] = mpi;
+        A.score[(long long)f * A.kp_cap + bestIdx] = bestDist;
+        return bestIdx;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int draw_sample(int32_t* st, int32_t* rf, int32_t* rr, const int16_t* dummy, int16_t* vis,
+                                           int N, int round) {
+    for (int q = 0; q < MAX_RANDOM_QUERY_TIME; q++) {
+        const int j = (int)((uint32_t)gfrng::next(st, rf, rr) % (uint32_t)N);
+        if (vis[j] < round) {
+            vis[j] = (int16_t)round;
+            return j;
+        }
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(GF_THREADS) void k_active_match(ActiveArgs A) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    HeapEntry* heap = (HeapEntry*)smem;                          // POOL_MAX
+    int* cell_start = (int*)(heap + POOL_MAX);                   // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;                       // NCELLS
+    int* items = cursor + NCELLS;                                // KP_MAX
+    int* claim = items + KP_MAX;                                 // KP_MAX
+    int16_t* lmk = (int16_t*)(claim + KP_MAX);                   // POOL_MAX
+    int16_t* vis = lmk + POOL_MAX;                               // POOL_MAX
+    int16_t* rem = vis + POOL_MAX;                               // POOL_MAX
+    __shared__ double cur[49];
+    __shared__ int32_t s_st[31], s_rf, s_rr;
+    __shared__ int s_N, s_cnt, s_rem, s_exh, s_term, s_nm, s_scan[GF_THREADS / 64];
+
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const FrameConst& fc = A.fc;
+    const int n = min(A.n[f], KP_MAX);
+    const int m = min(A.m[f], 32767);
+    const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
+    const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
+    int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
+    int32_t* left = A.left + (long long)f * A.mp_cap;
+    const int num_to_match = A.num_to_match[f];
+    // pool scratch doubles as the grid-build scratch (rem region >= n shorts is too small; use heap)
+    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, (int*)heap, GF_THREADS);
+
+    // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
+    const bool early = (m == 0 || num_to_match <= 0);
+    {
+        const int chunk = (m + GF_THREADS - 1) / GF_THREADS;
+        const int p0 = min(tid * chunk, m), p1 = min(p0 + chunk, m);
+        int c = 0;
+        for (int i = p0; i < p1; i++) {
+            const long long g = (long long)f * A.mp_cap + i;
+            c += A.views[g].in_view && (early || A.updated[g]);
+        }
+        // block exclusive scan
+        const int lane = tid & 63, wid = tid >> 6;
+        int x = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_scan[wid] = x;
+        __syncthreads();
+        int base = 0, tot = 0;
+        for (int w = 0; w < GF_THREADS / 64; w++) {
+            if (w < wid) base += s_scan[w];
+            tot += s_scan[w];
+        }
+        int o = base + x - c;
+        if (early) {
+            for (int i = p0; i < p1; i++)
+                if (A.views[(long long)f * A.mp_cap + i].in_view) left[o++] = i;
+            if (tid == 0) {
+                A.nleft[f] = tot;
+                A.nmatched[f] = 0;
+            }
+            return;
+        }
+        if (tot > POOL_MAX) {
+            if (tid == 0) A.err[f] = 2;
+            return;
+        }
+        for (int i = p0; i < p1; i++) {
+            const long long g = (long long)f * A.mp_cap + i;
+            if (A.views[g].in_view && A.updated[g]) {
+                lmk[o] = (int16_t)i;
+                vis[o] = -1;
+                o++;
+            }
+        }
+        if (tid == 0) s_N = tot;
+        if (tid < 49) cur[tid] = A.base[49LL * f + tid];
+        if (tid < 31) s_st[tid] = A.rng[f].state[tid];
+        if (tid == 0) {
+            s_rf = A.rng[f].f;
+            s_rr = A.rng[f].r;
+            s_nm = 0;
+        }
+        __syncthreads();
+    }
+    const int S = (int)((float)s_N / (float)num_to_match * 1.0);
+    const double* info = A.info + (long long)f * A.mp_cap * 49;
+    const double* Hm = A.H + (long long)f * A.mp_cap * 14;
+
+    for (int round = 0; round < num_to_match; ++round) {
+        // -- initial batch of random samples (lane 0, exact std::rand order)
+        if (tid == 0) {
+            const int N = s_N, szActual = min(S, N);
+            int cnt = 0, exh = 0;
+            while (cnt < szActual) {
+                const int j = draw_sample(s_st, &s_rf, &s_rr, nullptr, vis, N, round);
+                if (j < 0) {
+                    exh = 1;
+                    break;
+                }
+                heap[cnt].idx = lmk[j];
+                cnt++;
+            }
+            s_cnt = cnt;
+            s_exh = exh;
+            s_rem = 0;
+            s_term = 0;
+        }
+        __syncthreads();
+        // -- their log-dets across the workgroup
+        for (int t = tid; t < s_cnt; t += GF_THREADS) heap[t].s = logdet_sum(cur, info + 49LL * heap[t].idx, 1.0);
+        __syncthreads();
+        // -- heap, one-point matches, replacement draws (lane 0)
+        if (tid == 0) {
+            const int N = s_N, szActual = min(S, N);
+            int hn = 0;
+            for (int t = 0; t < s_cnt; t++) gfsel::push_heap(heap, ++hn, HeapLess());
+            int numHit = s_cnt, nrem = 0;
+            bool exh = s_exh != 0;
+            while (!exh && szActual > 0 && numHit >= szActual) {
+                const HeapEntry top = heap[0];
+                const int b = one_point_match(A, fc, f, top.idx, cell_start, items, claim, K, D);
+                rem[nrem++] = (int16_t)top.idx;
+                if (b >= 0) {
+                    add_info_block(Hm + 14LL * top.idx, (double)A.sigma2[K[b].octave], cur);
+                    s_nm++;
+                    break;
+                }
+                gfsel::pop_heap(heap, hn, HeapLess());
+                hn--;
+                numHit--;
+                const int j = draw_sample(s_st, &s_rf, &s_rr, nullptr, vis, N, round);
+                if (j < 0) {
+                    exh = true;
+                    break;
+                }
+                const int q = lmk[j];
+                heap[hn].idx = q;
+                heap[hn].s = logdet_sum(cur, info + 49LL * q, 1.0);
+                gfsel::push_heap(heap, ++hn, HeapLess());
+                numHit++;
+            }
+            int term = exh || hn == 0 || nrem == 0;
+            if (!term && nrem == N) term = 2;  // went through all map points: keep the pool as left-overs
+            if (!term) {                       // sort removeIdx (map point ids) ascending
+                for (int a = 1; a < nrem; a++) {
+                    int16_t v = rem[a];
+                    int b = a - 1;
+                    while (b >= 0 && rem[b] > v) {
+                        rem[b + 1] = rem[b];
+                        b--;
+                    }
+                    rem[b + 1] = v;
+                }
+            }
+            s_rem = nrem;
+            s_term = term;
+        }
+        __syncthreads();
+        if (s_term) break;
+        // -- drop tried entries from the pool (order-preserving compaction)
+        {
+            const int N = s_N, nrem = s_rem;
+            const int chunk = (N + GF_THREADS - 1) / GF_THREADS;
+            const int p0 = min(tid * chunk, N), p1 = min(p0 + chunk, N);
+            int16_t kl[POOL_MAX / GF_THREADS], kv[POOL_MAX / GF_THREADS];
+            int c = 0;
+            for (int p = p0; p < p1; p++) {
+                const int16_t id = lmk[p];
+                bool removed = false;
+                for (int r = 0; r < nrem; r++) removed |= rem[r] == id;
+                if (!removed) {
+                    kl[c] = id;
+                    kv[c] = vis[p];
+                    c++;
+                }
+            }
+            const int lane = tid & 63, wid = tid >> 6;
+            int x = c;
+            for (int o = 1; o < 64; o <<= 1) {
+                int y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) s_scan[wid] = x;
+            __syncthreads();
+            int base = 0, tot = 0;
+            for (int w = 0; w < GF_THREADS / 64; w++) {
+                if (w < wid) base += s_scan[w];
+                tot += s_scan[w];
+            }
+            const int o = base + x - c;
+            for (int k = 0; k < c; k++) {
+                lmk[o + k] = kl[k];
+                vis[o + k] = kv[k];
+            }
+            __syncthreads();
+            if (tid == 0) s_N = tot;
+            __syncthreads();
+        }
+    }
+    // ---- outputs: claims, left-over pool, RNG state
+    for (int i = tid; i < n; i += GF_THREADS) kp2mp[i] = claim[i];
+    for (int i = tid; i < s_N; i += GF_THREADS) left[i] = lmk[i];
+    if (tid < 31) A.rng[f].state[tid] = s_st[tid];
+    if (tid == 0) {
+        A.rng[f].f = s_rf;
+        A.rng[f].r = s_rr;
+        A.nleft[f] = s_N;
+        A.nmatched[f] = s_nm;
+    }
+}
+
+size_t active_lds_bytes() {
+    return sizeof(HeapEntry) * POOL_MAX + sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX) + sizeof(int16_t) * 3 * POOL_MAX;
+}
+
+// ------------------------------------------------------------- max-volume selection
+struct MaxvolArgs {
+    const double* info;   // [P][cap][49]
+    const double* score;  // [P][cap]
+    const int32_t* n;     // [P]
+    int cap, k, mode;
+    double sample_scale;
+    gf_rng* rng;
+    int32_t* out;   // [P][cap]
+    int32_t* nout;  // [P]
+    int32_t* err;
+};
+
+__global__ __launch_bounds__(GF_THREADS) void k_maxvol(MaxvolArgs A) {
+    __shared__ double cur[49];
+    __shared__ int16_t lmk[POOL_MAX], vis[POOL_MAX], samp[POOL_MAX];
+    __shared__ uint8_t sel[POOL_MAX];
+    __shared__ double s_best[GF_THREADS];
+    __shared__ double s_ub[GF_THREADS];
+    __shared__ int s_bi[GF_THREADS];
+    __shared__ int32_t s_st[31], s_rf, s_rr;
+    __shared__ int s_N, s_cnt, s_nout, s_stop;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int n = A.n[p], k = A.k;
+    const double* info = A.info + (long long)p * A.cap * 49;
+    const double* score = A.score + (long long)p * A.cap;
+    int32_t* out = A.out + (long long)p * A.cap;
+    if (n > POOL_MAX) {
+        if (tid == 0) A.err[p] = 2;
+        return;
+    }
+    if (k >= n) {  // every landmark is selected
+        for (int i = tid; i < n; i += GF_THREADS) out[i] = i;
+        if (tid == 0) A.nout[p] = n;
+        return;
+    }
+    const bool deletion = A.mode == 3 && 2LL * k > n;
+    for (int i = tid; i < n; i += GF_THREADS) {
+        lmk[i] = (int16_t)i;
+        vis[i] = -1;
+        sel[i] = deletion ? 1 : 0;
+    }
+    if (tid < 49) {
+        double c = (tid % 8 == 0) ? 0.00001 : 0.0;
+        if (deletion)
+            for (int i = 0; i < n; i++) c = c + info[49LL * i + tid];
+        cur[tid] = c;
+    }
+    if (tid < 31) s_st[tid] = A.rng[p].state[tid];
+    if (tid == 0) {
+        s_rf = A.rng[p].f;
+        s_rr = A.rng[p].r;
+        s_N = n;
+        s_nout = 0;
+        s_stop = 0;
+    }
+    __syncthreads();
+    const int rounds = deletion ? n - k : k;
+    const size_t szLazier = (size_t)((double)n / (double)k * A.sample_scale);
+    const double sign = deletion ? -1.0 : 1.0;
+    for (int it = 0; it < rounds; it++) {
+        double best = -DBL_MAX, bub = -DBL_MAX;
+        int bi = INT_MAX;
+        if (A.mode == 1) {
+            // baseline greedy: exact argmax of log det(cur + A_j) over the pool;
+            // ties keep the larger diagonal upper bound, then the lower index.
+            for (int j = tid; j < n; j += GF_THREADS) {
+                if (sel[j] || score[j] < 0) continue;
+                const double* b = info + 49LL * j;
+                double ub = 0;
+                for (int q = 0; q < 7; q++) ub += log(cur[8 * q] + b[8 * q]);
+                const double d = logdet_sum(cur, b, 1.0);
+                if (d > best || (d == best && (ub > bub || (ub == bub && j < bi)))) {
+                    best = d;
+                    bub = ub;
+                    bi = j;
+                }
+            }
+        } else {
+            if (tid == 0) {  // random samples in exact std::rand order
+                const int N = s_N;
+                const int szActual = (int)min(szLazier, (size_t)N);
+                int hit = 0, cnt = 0;
+                while (hit < szActual) {
+                    int j = -1;
+                    for (int q = 0; q < MAX_RANDOM_QUERY_TIME; q++) {
+                        const int jj = (int)((uint32_t)gfrng::next(s_st, &s_rf, &s_rr) % (uint32_t)N);
+                        if (vis[jj] < it) {
+                            vis[jj] = (int16_t)it;
+                            j = jj;
+                            break;
+                        }
+                    }
+                    if (j < 0) break;
+                    const int qi = lmk[j];
+                    hit++;
+                    const bool valid = deletion ? (sel[qi] && score[qi] >= 0) : (!sel[qi] && score[qi] >= 0);
+                    if (!valid) {
+                        hit--;
+                        continue;
+                    }
+                    samp[cnt++] = (int16_t)qi;
+                }
+                s_cnt = cnt;
+            }
+            __syncthreads();
+            for (int t = tid; t < s_cnt; t += GF_THREADS) {
+                const double d = logdet_sum(cur, info + 49LL * samp[t], sign);
+                if (d > best || (d == best && t < bi)) {  // first sample wins ties (strict '>')
+                    best = d;
+                    bi = t;
+                }
+            }
+        }
+        s_best[tid] = best;
+        s_ub[tid] = bub;
+        s_bi[tid] = bi;
+        __syncthreads();
+        if (tid == 0) {
+            double B = -DBL_MAX, U = -DBL_MAX;
+            int I = INT_MAX;
+            for (int t = 0; t < GF_THREADS; t++) {
+                const double d = s_best[t];
+                if (s_bi[t] == INT_MAX) continue;
+                bool better;
+                if (A.mode == 1)
+                    better = d > B || (d == B && (s_ub[t] > U || (s_ub[t] == U && s_bi[t] < I)));
+                else
+                    better = d > B || (d == B && s_bi[t] < I);
+                if (better) {
+                    B = d;
+                    U = s_ub[t];
+                    I = s_bi[t];
+                }
+            }
+            if (I == INT_MAX) {
+                s_stop = 1;  // early termination (no valid candidate)
+            } else {
+                const int chosen = A.mode == 1 ? I : samp[I];
+                for (int q = 0; q < 49; q++) cur[q] = deletion ? cur[q] - info[49LL * chosen + q] : cur[q] + info[49LL * chosen + q];
+                sel[chosen] = deletion ? 0 : 1;
+                if (!deletion) out[s_nout++] = chosen;
+                if (A.mode != 1) {  // drop the chosen entry from the index pool
+                    int w = 0;
+                    for (int r = 0; r < s_N; r++)
+                        if (lmk[r] != chosen) {
+                            lmk[w] = lmk[r];
+                            vis[w] = vis[r];
+                            w++;
+                        }
+                    s_N = w;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_stop) break;
+    }
+    if (deletion && tid == 0) {
+        for (int i = 0; i < n; i++)
+            if (sel[i]) out[s_nout++] = i;
+    }
+    __syncthreads();
+    if (tid < 31) A.rng[p].state[tid] = s_st[tid];
+    if (tid == 0) {
+        A.rng[p].f = s_rf;
+        A.rng[p].r = s_rr;
+        A.nout[p] = s_nout;
+    }
+}
+
+}  // namespace
+
+// ============================================================== ABI
+static int set_lds_attr(gf_ctx* ctx, const void* fn, size_t bytes, unsigned long long* mask) {
+    if (!(*mask & (1ull << ctx->device))) {
+        GF_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        *mask |= 1ull << ctx->device;
+    }
+    return GF_OK;
+}
+
+extern "C" {
+
+int gf_obs_build_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_pos,
+                          const float* d_sigma2, const int32_t* d_n, int cap, int check_viz, double* d_H,
+                          double* d_info, float* d_uv, uint8_t* d_valid, void* stream) {
+    GF_CHECK(ctx && cam, GF_ERR_ARG, "null arg");
+    if (nframes <= 0 || cap <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_info");
+    k_obs_info<<<dim3((cap + 127) / 128, nframes), 128, 0, s>>>(*cam, d_Xv, d_pos, d_sigma2, d_n, cap, check_viz, d_H,
+                                                                 d_info, d_uv, d_valid);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_obs_accumulate_dev(gf_ctx* ctx, int nframes, const double* d_info, const uint8_t* d_flag, const int32_t* d_n,
+                          int cap, double diag, double* d_out, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (nframes <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_accumulate");
+    k_obs_accumulate<<<nframes, 64, 0, s>>>(d_info, d_flag, d_n, cap, diag, d_out);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                            const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                            const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info,
+                            const double* d_H, const int32_t* d_m, int mp_cap, const double* d_base,
+                            const float* level_sigma2, const int32_t* d_num_to_match, float th, float nnratio,
+                            gf_rng* d_rng, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_left, int32_t* d_nleft,
+                            int32_t* d_nmatched, void* stream) {
+    GF_CHECK(ctx && fi && level_sigma2, GF_ERR_ARG, "null arg");
+    GF_CHECK(kp_cap <= KP_MAX && mp_cap <= 32767, GF_ERR_UNSUPPORTED, "frame exceeds active-matching limits");
+    GF_CHECK(fi->nlevels >= 1 && fi->nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
+    if (nframes <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    ActiveArgs A{};
+    A.fc = gf::make_frame_const(fi);
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.kp_cap = kp_cap;
+    A.views = d_views;
+    A.mp_desc = d_mp_desc;
+    A.updated = d_updated;
+    A.info = d_info;
+    A.H = d_H;
+    A.m = d_m;
+    A.mp_cap = mp_cap;
+    A.base = d_base;
+    for (int i = 0; i < fi->nlevels; i++) A.sigma2[i] = level_sigma2[i];
+    A.num_to_match = d_num_to_match;
+    A.th = th;
+    A.nnratio = nnratio;
+    A.rng = d_rng;
+    A.kp2mp = d_kp2mp;
+    A.score = d_score;
+    A.left = d_left;
+    A.nleft = d_nleft;
+    A.nmatched = d_nmatched;
+    void* err;
+    int rc = gf::ws_get(ctx, 30, sizeof(int32_t) * nframes, &err);
+    if (rc) return rc;
+    A.err = (int32_t*)err;
+    static unsigned long long mask = 0;
+    rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(), &mask);
+    if (rc) return rc;
+    GF_PROF(ctx, s, "k_active_match");
+    k_active_match<<<nframes, GF_THREADS, active_lds_bytes(), s>>>(A);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const double* d_score, const int32_t* d_n,
+                         int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
+                         int32_t* d_nout, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    GF_CHECK(mode >= 1 && mode <= 3, GF_ERR_ARG, "mode must be 1, 2 or 3");
+    GF_CHECK(cap <= POOL_MAX, GF_ERR_UNSUPPORTED, "pool exceeds 4096 landmarks");
+    if (npools <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    MaxvolArgs A{d_info, d_score, d_n, cap, k, mode, sample_scale, d_rng, d_out, d_nout, nullptr};
+    void* err;
+    int rc = gf::ws_get(ctx, 29, sizeof(int32_t) * npools, &err);
+    if (rc) return rc;
+    A.err = (int32_t*)err;
+    GF_PROF(ctx, s, "k_maxvol");
+    k_maxvol<<<npools, GF_THREADS, 0, s>>>(A);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+// ------------------------------------------------------------ host family
+int gf_obs_build_info(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv, const float* pos, const float* sigma2,
+                      int n, int check_viz, double* H, double* info, float* uv, uint8_t* valid) {
+    GF_CHECK(ctx && cam && Xv, GF_ERR_ARG, "null arg");
+    if (n <= 0) return GF_OK;
+    GF_CHECK(pos && H && info && uv && valid, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dX, *dP, *dS = nullptr, *dn, *dH, *dI, *dU, *dV;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, Xv, 13 * sizeof(double), &dX)) ||
+        (rc = gf::ws_upload(ctx, 1, pos, 12 * (size_t)n, &dP)) || (rc = gf::ws_upload(ctx, 2, &n, 4, &dn)) ||
+        (rc = gf::ws_get(ctx, 3, 14 * 8 * (size_t)n, &dH)) || (rc = gf::ws_get(ctx, 4, 49 * 8 * (size_t)n, &dI)) ||
+        (rc = gf::ws_get(ctx, 5, 8 * (size_t)n, &dU)) || (rc = gf::ws_get(ctx, 6, (size_t)n, &dV)))
+        return rc;
+    if (sigma2 && (rc = gf::ws_upload(ctx, 7, sigma2, 4 * (size_t)n, &dS))) return rc;
+    rc = gf_obs_build_info_dev(ctx, cam, 1, (const double*)dX, (const float*)dP, (const float*)dS, (const int32_t*)dn,
+                               n, check_viz, (double*)dH, (double*)dI, (float*)dU, (uint8_t*)dV, ctx->stream);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(H, dH, 14 * 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(info, dI, 49 * 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(uv, dU, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(valid, dV, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+int gf_logdet(gf_ctx* ctx, const double* M, int n, double* out) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (n <= 0) return GF_OK;
+    GF_CHECK(M && out, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dM, *dO;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, M, 49 * 8 * (size_t)n, &dM)) || (rc = gf::ws_get(ctx, 1, 8 * (size_t)n, &dO)))
+        return rc;
+    {
+        GF_PROF(ctx, ctx->stream, "k_logdet");
+        k_logdet<<<(n + 127) / 128, 128, 0, ctx->stream>>>((const double*)dM, n, (double*)dO);
+    }
+    GF_HIP(hipGetLastError());
+    GF_HIP(hipMemcpyAsync(out, dO, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+}
+
+int gf_obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                        const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
+                        const double* H, const float* uv, int m, const double* base, const float* level_sigma2,
+                        int num_to_match, float th, float nnratio, gf_rng* rng, int32_t* kp2mp, int32_t* score,
+                        int32_t* left, int* nleft, int* nmatched) {
+    GF_CHECK(ctx && fi && nleft && nmatched && rng && base && level_sigma2, GF_ERR_ARG, "null arg");
+    (void)uv;  // u_proj/v_proj feed only reWeightInfoMat's residual terms, which are compiled out
+    *nleft = 0;
+    *nmatched = 0;
+    GF_CHECK(n >= 0 && m >= 0, GF_ERR_ARG, "negative size");
+    GF_CHECK(m == 0 || (views && mp_desc && updated && info && H && left), GF_ERR_ARG, "null arg");
+    GF_CHECK(n == 0 || (kps && desc && kp2mp && score), GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    const int nn = n > 0 ? n : 1, mm = m > 0 ? m : 1;
+    void *dK, *dD, *dn, *dV, *dQ, *dU, *dI, *dH, *dm, *dB, *dT, *dR, *dC, *dS, *dL, *dNL, *dNM;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, kps, sizeof(gf_keypoint) * n, &dK)) ||
+        (rc = gf::ws_upload(ctx, 1, desc, 32 * (size_t)n, &dD)) || (rc = gf::ws_upload(ctx, 2, &n, 4, &dn)) ||
+        (rc = gf::ws_upload(ctx, 3, views, sizeof(gf_mp_view) * m, &dV)) ||
+        (rc = gf::ws_upload(ctx, 4, mp_desc, 32 * (size_t)m, &dQ)) ||
+        (rc = gf::ws_upload(ctx, 5, updated, (size_t)m, &dU)) ||
+        (rc = gf::ws_upload(ctx, 6, info, 49 * 8 * (size_t)m, &dI)) ||
+        (rc = gf::ws_upload(ctx, 7, H, 14 * 8 * (size_t)m, &dH)) || (rc = gf::ws_upload(ctx, 8, &m, 4, &dm)) ||
+        (rc = gf::ws_upload(ctx, 9, base, 49 * 8, &dB)) ||
+        (rc = gf::ws_upload(ctx, 10, &num_to_match, 4, &dT)) ||
+        (rc = gf::ws_upload(ctx, 11, rng, sizeof(gf_rng), &dR)) ||
+        (rc = gf::ws_upload(ctx, 12, kp2mp, 4 * (size_t)n, &dC)) ||
+        (rc = gf::ws_upload(ctx, 13, score, 4 * (size_t)n, &dS)) || (rc = gf::ws_get(ctx, 14, 4 * (size_t)mm, &dL)) ||
+        (rc = gf::ws_get(ctx, 15, 4, &dNL)) || (rc = gf::ws_get(ctx, 16, 4, &dNM)))
+        return rc;
+    (void)nn;
+    void* err;
+    if ((rc = gf::ws_get(ctx, 30, 4, &err))) return rc;
+    GF_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+    rc = gf_obs_active_match_dev(ctx, fi, 1, (const gf_keypoint*)dK, (const uint8_t*)dD, (const int32_t*)dn, n > 0 ? n : 1,
+                                 (const gf_mp_view*)dV, (const uint8_t*)dQ, (const uint8_t*)dU, (const double*)dI,
+                                 (const double*)dH, (const int32_t*)dm, mm, (const double*)dB, level_sigma2,
+                                 (const int32_t*)dT, th, nnratio, (gf_rng*)dR, (int32_t*)dC, (int32_t*)dS,
+                                 (int32_t*)dL, (int32_t*)dNL, (int32_t*)dNM, ctx->stream);
+    if (rc) return rc;
+    int e = 0;
+    GF_HIP(hipMemcpyAsync(&e, err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(nleft, dNL, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(nmatched, dNM, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(rng, dR, sizeof(gf_rng), hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    GF_CHECK(e == 0, GF_ERR_UNSUPPORTED, "active-matching pool exceeds 4096 map points");
+    if (n > 0) {
+        GF_HIP(hipMemcpy(kp2mp, dC, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        GF_HIP(hipMemcpy(score, dS, 4 * (size_t)n, hipMemcpyDeviceToHost));
+    }
+    if (*nleft > 0) GF_HIP(hipMemcpy(left, dL, 4 * (size_t)*nleft, hipMemcpyDeviceToHost));
+    return GF_OK;
+}
+
+int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n, int k, double sample_scale, int mode,
+                     gf_rng* rng, int32_t* out_idx, int* nout) {
+    GF_CHECK(ctx && nout && rng, GF_ERR_ARG, "null arg");
+    *nout = 0;
+    if (n <= 0) return GF_OK;
+    GF_CHECK(info && score && out_idx, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    void *dI, *dS, *dn, *dR, *dO, *dN, *err;
+    int rc;
+    if ((rc = gf::ws_upload(ctx, 0, info, 49 * 8 * (size_t)n, &dI)) ||
+        (rc = gf::ws_upload(ctx, 1, score, 8 * (size_t)n, &dS)) || (rc = gf::ws_upload(ctx, 2, &n, 4, &dn)) ||
+        (rc = gf::ws_upload(ctx, 3, rng, sizeof(gf_rng), &dR)) || (rc = gf::ws_get(ctx, 4, 4 * (size_t)n, &dO)) ||
+        (rc = gf::ws_get(ctx, 5, 4, &dN)) || (rc = gf::ws_get(ctx, 29, 4, &err)))
+        return rc;
+    GF_HIP(hipMemsetAsync(err, 0, 4, ctx->stream));
+    rc = gf_maxvol_select_dev(ctx, 1, (const double*)dI, (const double*)dS, (const int32_t*)dn, n, k, sample_scale,
+                              mode, (gf_rng*)dR, (int32_t*)dO, (int32_t*)dN, ctx->stream);
+    if (rc) return rc;
+    int e = 0;
+    GF_HIP(hipMemcpyAsync(&e, err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(nout, dN, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(rng, dR, sizeof(gf_rng), hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    GF_CHECK(e == 0, GF_ERR_UNSUPPORTED, "pool exceeds 4096 landmarks");
+    if (*nout > 0) GF_HIP(hipMemcpy(out_idx, dO, 4 * (size_t)*nout, hipMemcpyDeviceToHost));
+    return GF_OK;
+}
+
+}  // extern "C"

@@ -24,24 +24,9 @@
 
 #include "common.h"
 
-#define GRID_COLS 64
-#define GRID_ROWS 48
-#define NCELLS (GRID_COLS * GRID_ROWS)
-#define KP_MAX 4096
-#define Q_MAX 8192
-#define MATCH_THREADS 1024
-#define TH_HIGH 100
-#define HISTO_LENGTH 30
+#include "match_common.h"
 
 namespace {
-
-struct FrameConst {
-    int min_x, max_x, min_y, max_y;
-    float fx, fy, cx, cy;
-    int nlevels;
-    float invW, invH;
-    float scales[16];
-};
 
 enum { MODE_PROJECT = 0, MODE_LAST = 1 };
 
@@ -73,13 +58,6 @@ struct MatchArgs {
     int32_t* err;   // [F] round-limit flag
 };
 
-__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
-    const uint4* pa = (const uint4*)a;
-    const uint4* pb = (const uint4*)b;
-    uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
-    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
-}
 
 struct Query {
     bool valid;
@@ -90,15 +68,6 @@ struct Query {
     int id;  // value written into kp2mp
 };
 
-__device__ __forceinline__ void transform3(const float* T, const float* P, float* Pc) {
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        float a = T[4 * r + 0] * P[0];
-        float b = T[4 * r + 1] * P[1];
-        float c = T[4 * r + 2] * P[2];
-        Pc[r] = ((a + b) + c) + T[4 * r + 3];
-    }
-}
 
 __device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int k) {
     Query q;
@@ -152,13 +121,6 @@ __device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int
     return q;
 }
 
-__device__ __forceinline__ bool level_ok(int oct, int minL, int maxL) {
-    const bool check = !(minL == -1 && maxL == -1);
-    const bool same = check && minL == maxL;
-    if (check && !same) return !(oct < minL || oct > maxL);
-    if (same) return oct == minL;
-    return true;
-}
 
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
@@ -178,55 +140,11 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* score = A.score + (long long)f * A.kp_cap;
 
-    // ---- 64x48 grid CSR (Frame.cc:114-131, PosInGrid :367-377), cells ix-major
-    for (int c = tid; c < NCELLS + 1; c += MATCH_THREADS) cell_start[c] = 0;
     if (tid == 0) {
         s_nm = 0;
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
-    __syncthreads();
-    for (int i = tid; i < n; i += MATCH_THREADS) {
-        const gf_keypoint kp = K[i];
-        int px = (int)roundf((kp.x - fc.min_x) * fc.invW);
-        int py = (int)roundf((kp.y - fc.min_y) * fc.invH);
-        int c = (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
-        minU[i] = c;
-        if (c >= 0) atomicAdd(&cell_start[c + 1], 1);
-        claim[i] = kp2mp[i];
-    }
-    __syncthreads();
-    if (tid < 64) {  // one wave scans the 3072 counts
-        int carry = 0;
-        for (int base = 0; base < NCELLS; base += 64) {
-            int v = cell_start[base + 1 + tid], x = v;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                int y = __shfl_up(x, o, 64);
-                if (tid >= o) x += y;
-            }
-            cell_start[base + 1 + tid] = carry + x;
-            carry += __shfl(x, 63, 64);
-        }
-    }
-    __syncthreads();
-    for (int c = tid; c < NCELLS; c += MATCH_THREADS) cursor[c] = cell_start[c];
-    __syncthreads();
-    for (int i = tid; i < n; i += MATCH_THREADS) {
-        int c = minU[i];
-        if (c >= 0) items[atomicAdd(&cursor[c], 1)] = i;
-    }
-    __syncthreads();
-    for (int c = tid; c < NCELLS; c += MATCH_THREADS) {  // ascending index inside a cell
-        int s = cell_start[c], e = cell_start[c + 1];
-        for (int a = s + 1; a < e; a++) {
-            int v = items[a], b = a - 1;
-            while (b >= s && items[b] > v) {
-                items[b + 1] = items[b];
-                b--;
-            }
-            items[b + 1] = v;
-        }
-    }
+    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, minU, MATCH_THREADS);
     for (int k = tid; k < nq; k += MATCH_THREADS) done[k] = 0;
     __syncthreads();
 

@@ -180,6 +180,112 @@ int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, co
  * 32-byte rows: dist[i] = popcount(a[i] ^ b[i]). */
 int gf_descriptor_distance(gf_ctx* ctx, const uint8_t* a, const uint8_t* b, int n, int32_t* dist);
 
+/* ------------------------------------------------- good-feature selection (G1-G7)
+ * f64 throughout, as the reference's Armadillo matrices. */
+
+/* glibc rand() state (TYPE_3 additive feedback, 31 words): the reference draws
+ * its lazier-greedy samples with std::rand() % n (Observability.cc:1348,
+ * :2895). Callers keep one state per sequence across frames. */
+typedef struct gf_rng {
+    int32_t state[31];
+    int32_t f, r;
+} gf_rng;
+/* std::srand(seed) */
+int gf_rng_seed(gf_rng* rng, uint32_t seed);
+/* n successive std::rand() values (host; for checking the device port). */
+int gf_rng_next(gf_rng* rng, int32_t* out, int n);
+
+/* Observability camera (PinHoleCamera, include/Util.hpp:136-178) and the
+ * visibility margins mBoundX/YInFrame, mBoundDepth (Observability.h:727-728)
+ * with Frame::mnMinX..mnMaxY. */
+typedef struct gf_obs_camera {
+    double fu, fv, cx, cy;
+    int32_t nrows, ncols;
+    int32_t min_x, max_x, min_y, max_y;
+    int32_t bound_x, bound_y;
+    float bound_depth;
+} gf_obs_camera;
+
+/* One predicted segment of the constant-velocity PWLS motion model
+ * (KineStruct, Util.hpp:170-177): state Xv = [twc(3) q_wc(4) v(3) w(3)], the
+ * quaternion/angular-rate blocks of F for the full segment and one of 13
+ * sub-segments, and the predicted Tcw (float, row-major). */
+typedef struct gf_kine {
+    double dt, dt_inseg;
+    double Xv[13];
+    double F_Q[16], F_Omg[12], F_Q_inSeg[16], F_Omg_inSeg[12]; /* row-major */
+    float Tcw[16];
+} gf_kine;
+
+/* Observability::updatePWLSVec (Observability.h:222-259): Xv from the last
+ * frame pose Tcw_prev and the current Twc (float row-major), times in s. */
+int gf_obs_update(double t_prev, const float* Tcw_prev, double t_cur, const float* Twc_cur, double* Xv);
+/* Observability::predictPWLSVec(dt, nseg) (Observability.h:261-295). */
+int gf_obs_predict(const double* Xv, double dt, int nseg, gf_kine* out);
+
+/* Measurement Jacobian + information block per landmark
+ * (compute_H_subblock_simplied Observability.h:460-515, reWeightInfoMat
+ * :517-596, batchInfoMat_Map / batchInfoMat_Frame Observability.cc:386-644).
+ * For each of n landmarks at world position pos[3i..]: H (2x7 row-major,
+ * n x 14) and info = H_rw^T H_rw (7x7 row-major, n x 49) at state Xv, where
+ * H_rw = H / sigma, sigma^2 = sigma2[i] (frame path: level sigma^2 of the
+ * matched keypoint octave) or 1 when sigma2 == NULL (map path). uv = the
+ * projected pixel (u_proj, v_proj). valid[i] = 0 when check_viz rejects the
+ * landmark (ObsScore = -1). */
+int gf_obs_build_info(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv, const float* pos,
+                      const float* sigma2, int n, int check_viz, double* H, double* info, float* uv,
+                      uint8_t* valid);
+
+/* Util.hpp:714-731 logDet: 2 log prod diag chol(M), LU log|det| fallback;
+ * n 7x7 row-major matrices. */
+int gf_logdet(gf_ctx* ctx, const double* M, int n, double* out);
+
+/* Observability::runActiveMapMatching with FRAME_INFO_MATRIX
+ * (Observability.cc:1249-1524): lazier-greedy active matching of
+ * num_to_match map points into frame F using SearchByProjection_OnePoint
+ * (ORBmatcher.h:71-145). Pool = map points with views[i].in_view and
+ * updated[i] (updateAtFrameId == frame id), in list order; info/H are their
+ * map information blocks and Jacobians (gf_obs_build_info map path), uv their
+ * projections. base = mCurrentInfoMat (7x7). level_sigma2 = Frame
+ * mvLevelSigma2. Writes claims into kp2mp/score (in/out), the left-over pool
+ * (mLeftMapPoints) into left[0..nleft), advances rng; nmatched = matches. */
+int gf_obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                        const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
+                        const double* info, const double* H, const float* uv, int m, const double* base,
+                        const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
+                        int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
+
+/* Max-volume subset selection over a pool of 7x7 information blocks
+ * (Observability.cc): mode 1 = maxVolSelection_BaselineGreedy (:3031-3139),
+ * 2 = maxVolSelection_LazierGreedy (:2815-3029), 3 =
+ * maxVolAutomatic_LazierGreedy (:3141-3155, deletion when 2k > n).
+ * score[i] < 0 excludes block i (obs_score). sample_scale as
+ * setSelction_Number computes it (:823). out_idx receives pool indices in
+ * selection order (deletion: pool order). rng used by modes 2-3. */
+int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n, int k, double sample_scale,
+                     int mode, gf_rng* rng, int32_t* out_idx, int* nout);
+
+/* Device family of the GF rows, batched over frames (per-frame arrays strided
+ * by cap / mp_cap; d_Xv is [F][13], d_base [F][49], d_rng [F]). Pool limit
+ * for active matching and max-volume selection: 4096 landmarks.
+ * gf_obs_accumulate_dev: d_out[f] = diag*I + sum of d_info rows with d_flag
+ * set (mCurrentInfoMat accumulation, Tracking.cc:3161 and :3195-3219). */
+int gf_obs_build_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_pos,
+                          const float* d_sigma2, const int32_t* d_n, int cap, int check_viz, double* d_H,
+                          double* d_info, float* d_uv, uint8_t* d_valid, void* stream);
+int gf_obs_accumulate_dev(gf_ctx* ctx, int nframes, const double* d_info, const uint8_t* d_flag, const int32_t* d_n,
+                          int cap, double diag, double* d_out, void* stream);
+int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                            const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                            const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info,
+                            const double* d_H, const int32_t* d_m, int mp_cap, const double* d_base,
+                            const float* level_sigma2, const int32_t* d_num_to_match, float th, float nnratio,
+                            gf_rng* d_rng, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_left, int32_t* d_nleft,
+                            int32_t* d_nmatched, void* stream);
+int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const double* d_score, const int32_t* d_n,
+                         int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
+                         int32_t* d_nout, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,3 +91,75 @@ def match_lastframe(info, kps, desc, Tcw, last_kps, last_desc, last_kp2mp, last_
                               len(last_kps), ctypes.c_float(th), int(check_ori), _p(kp2mp), _p(score),
                               ctypes.byref(n))
     return n.value
+
+
+# ----------------------------------------------------------------- GF (G1-G7)
+class Kine(ctypes.Structure):
+    _fields_ = [("dt", ctypes.c_double), ("dt_inseg", ctypes.c_double), ("Xv", ctypes.c_double * 13),
+                ("F_Q", ctypes.c_double * 16), ("F_Omg", ctypes.c_double * 12), ("F_Q_inSeg", ctypes.c_double * 16),
+                ("F_Omg_inSeg", ctypes.c_double * 12), ("Tcw", ctypes.c_float * 16)]
+
+
+def obs_predict(Xv, dt, nseg):
+    out = (Kine * nseg)()
+    xv = np.ascontiguousarray(Xv, np.float64)
+    orc().orc_obs_predict(_p(xv), ctypes.c_double(dt), nseg, out)
+    return list(out)
+
+
+def obs_update(t0, Tcw0, t1, Twc1):
+    xv = np.zeros(13)
+    orc().orc_obs_update(ctypes.c_double(t0), _p(np.ascontiguousarray(Tcw0, np.float32)), ctypes.c_double(t1),
+                         _p(np.ascontiguousarray(Twc1, np.float32)), _p(xv))
+    return xv
+
+
+def obs_build_info(cam, Xv, pos, sigma2, check_viz):
+    pos = np.ascontiguousarray(pos, np.float32)
+    n = len(pos)
+    H = np.zeros((n, 14))
+    info = np.zeros((n, 49))
+    uv = np.zeros((n, 2), np.float32)
+    valid = np.zeros(n, np.uint8)
+    s2 = None if sigma2 is None else np.ascontiguousarray(sigma2, np.float32)
+    orc().orc_obs_build_info(ctypes.byref(cam), _p(np.ascontiguousarray(Xv, np.float64)), _p(pos), _p(s2), n,
+                             int(check_viz), _p(H), _p(info), _p(uv), _p(valid))
+    return H, info, uv, valid
+
+
+def logdet(M):
+    M = np.ascontiguousarray(M, np.float64).reshape(-1, 49)
+    out = np.zeros(len(M))
+    orc().orc_logdet(_p(M), len(M), _p(out))
+    return out
+
+
+def rand_sequence(seed, n):
+    out = np.zeros(n, np.int32)
+    orc().orc_rand_sequence(ctypes.c_uint(seed), n, _p(out))
+    return out
+
+
+def active_match(info_fi, kps, desc, views, mp_desc, updated, info, H, uv, base, level_sigma2, num_to_match, th,
+                 nnratio, seed, kp2mp, score):
+    m = len(views)
+    left = np.zeros(m, np.int32)
+    nleft, nmatched = ctypes.c_int(), ctypes.c_int()
+    orc().orc_obs_active_match(ctypes.byref(info_fi), _p(kps), _p(desc), len(kps), _p(views), _p(mp_desc),
+                               _p(np.ascontiguousarray(updated, np.uint8)), _p(np.ascontiguousarray(info)),
+                               _p(np.ascontiguousarray(H)), _p(np.ascontiguousarray(uv, np.float32)), m,
+                               _p(np.ascontiguousarray(base, np.float64)),
+                               _p(np.ascontiguousarray(level_sigma2, np.float32)), num_to_match, ctypes.c_float(th),
+                               ctypes.c_float(nnratio), ctypes.c_uint(seed), _p(kp2mp), _p(score), _p(left),
+                               ctypes.byref(nleft), ctypes.byref(nmatched))
+    return nmatched.value, left[:nleft.value].copy()
+
+
+def maxvol_select(info, score, k, sample_scale, mode, seed):
+    info = np.ascontiguousarray(info, np.float64).reshape(-1, 49)
+    n = len(info)
+    out = np.zeros(n, np.int32)
+    nout = ctypes.c_int()
+    orc().orc_maxvol_select(_p(info), _p(np.ascontiguousarray(score, np.float64)), n, k, ctypes.c_double(sample_scale),
+                            mode, ctypes.c_uint(seed), _p(out), ctypes.byref(nout))
+    return out[:nout.value].copy()

@@ -1,0 +1,132 @@
+"""GPU parity of the good-feature rows (G2-G7) with the CPU oracle:
+Jacobians/information blocks bit-exact, log-dets to 1e-12, active map
+matching (claims, scores, left-overs, RNG state) and max-volume subsets
+identical for the same seed; plus the reference's own KATs on the device."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gf_orb_slam_amd import synth
+from gf_orb_slam_amd.matcher import Frame, FrameInfo
+from gf_orb_slam_amd.observability import Observability, ObsCamera, Rng
+from test_oracle_gf import KAT, greedy_world, infnorm
+
+pytestmark = pytest.mark.gpu
+
+
+def test_jacobian_kat_gpu():
+    c = KAT["jacobian"]
+    cc = c["camera"]
+    cam = ObsCamera.from_focal(cc["f"], cc["nrows"], cc["ncols"], cc["cx"], cc["cy"], cc["dx"], cc["dy"])
+    ob = Observability(cam)
+    ob.Xv = np.array(c["Xv"])
+    ob.predictPWLSVec(c["dt"], 1)
+    H, info, uv, valid = ob.build_info(c["landmarks"])
+    for j in range(5):
+        h = H[j].reshape(2, 7)
+        assert infnorm(h[:, :3] - c["H13"][j]) < 0.25 and infnorm(h[:, 3:] - c["H47"][j]) < 0.25
+
+
+@pytest.mark.parametrize("check_viz,frame_path", [(False, False), (True, False), (False, True)])
+def test_build_info_bit_exact(check_viz, frame_path):
+    sc = synth.synth_scene("euroc", 3000, 10, 21)
+    cam = ObsCamera.from_intrinsics(457.3, 457.3, 367.215, 248.375, 752, 480, bound=75)
+    ob = Observability(cam)
+    T = sc["Tcw"]
+    Twc = np.linalg.inv(T.astype(np.float64)).astype(np.float32)
+    ob.updatePWLSVec(0.0, T, 0.05, Twc)
+    ob.predictPWLSVec(0.05, 2)
+    rng = np.random.default_rng(2)
+    s2 = np.float32(1.2) ** (2 * rng.integers(0, 8, 3000)).astype(np.float32) if frame_path else None
+    if s2 is not None:
+        s2 = s2.astype(np.float32)
+    Hg, Ig, Ug, Vg = ob.build_info(sc["map"]["pos"], s2, check_viz, kine_idx=1)
+    Ho, Io, Uo, Vo = O.obs_build_info(cam, np.array(ob.kinematic[1].Xv[:]), sc["map"]["pos"], s2, check_viz)
+    np.testing.assert_array_equal(Vg, Vo)
+    np.testing.assert_array_equal(Ug, Uo)
+    np.testing.assert_array_equal(Hg, Ho)
+    np.testing.assert_array_equal(Ig, Io)
+    if check_viz:
+        assert 0 < Vg.sum() < len(Vg)
+
+
+def test_logdet_gpu():
+    rng = np.random.default_rng(0)
+    A = rng.normal(size=(500, 7, 7))
+    M = A @ A.transpose(0, 2, 1) + 1e-4 * np.eye(7)
+    M[:20] = rng.normal(size=(20, 7, 7))  # non-PD: LU fallback
+    g = Observability(ObsCamera()).logDet(M)
+    o = O.logdet(M)
+    np.testing.assert_allclose(g, o, rtol=1e-12, atol=1e-12)
+
+
+def _active_case(seed, nmp=2500, nkp=1000, num_to_match=40, frac_updated=0.9):
+    sc = synth.synth_scene("euroc", nmp, nkp, seed)
+    info_fi = FrameInfo.make(*sc["camera"])
+    F = Frame(sc["keypoints"], sc["descriptors"], info_fi, sc["Tcw"])
+    views = F.isInFrustum(sc["map"], 0.5)
+    cam = ObsCamera.from_intrinsics(*sc["camera"][2:], sc["camera"][0], sc["camera"][1])
+    ob = Observability(cam)
+    T = sc["Tcw"]
+    ob.updatePWLSVec(0.0, T, 0.05, np.linalg.inv(T.astype(np.float64)).astype(np.float32))
+    ob.predictPWLSVec(0.05, 1)
+    H, info, uv, valid = ob.build_info(sc["map"]["pos"])
+    rng = np.random.default_rng(seed)
+    updated = (rng.uniform(size=nmp) < frac_updated).astype(np.uint8)
+    # motion-model matches already claimed
+    pre = rng.choice(nkp, 60, replace=False)
+    F.mvpMapPoints[pre] = 100000 + pre
+    F.mvpMatchScore[pre] = 11
+    base = np.eye(7).reshape(-1) * 1e-5
+    return sc, info_fi, F, views, ob, H, info, uv, updated, base, num_to_match
+
+
+@pytest.mark.parametrize("seed,ntm", [(1, 40), (2, 100), (3, 7), (4, 400), (5, 0)])
+def test_active_matching_bit_exact(seed, ntm):
+    sc, info_fi, F, views, ob, H, info, uv, updated, base, _ = _active_case(seed, num_to_match=ntm)
+    kp2mp, score = F.mvpMapPoints.copy(), F.mvpMatchScore.copy()
+    sig2 = (info_fi.scale_factors() ** 2).astype(np.float32)
+    ob.rng = Rng.seeded(seed)
+    ng = ob.runActiveMapMatching(F, views, sc["mp_desc"], updated, info, H, uv, base, ntm)
+    no, left_o = O.active_match(info_fi, sc["keypoints"], sc["descriptors"], views, sc["mp_desc"], updated, info, H,
+                                uv, base, sig2, ntm, 1.0, 0.8, seed, kp2mp, score)
+    assert ng == no
+    np.testing.assert_array_equal(F.mvpMapPoints, kp2mp)
+    np.testing.assert_array_equal(F.mvpMatchScore, score)
+    np.testing.assert_array_equal(ob.mLeftMapPoints, left_o)
+    if ntm:
+        assert ng > 0
+        # the RNG advanced exactly as std::rand would have
+        ref = Rng.seeded(seed)
+        ref_seq = O.rand_sequence(seed, 200000)
+        nxt = ob.rng.next(1)[0]
+        assert nxt in ref_seq
+
+
+@pytest.mark.parametrize("k,mode", [(60, 1), (100, 1), (60, 2), (140, 2), (100, 3), (250, 3)])
+def test_maxvol_bit_exact(k, mode):
+    info, score = greedy_world()
+    n = len(score)
+    scale = float(int(np.float32(n) / np.float32(k) * math.log(10.0)))
+    ob = Observability(ObsCamera())
+    ob.rng = Rng.seeded(77)
+    g = ob.maxvol_select(info, score, k, scale, mode)
+    o = O.maxvol_select(info, score, k, scale, mode, 77)
+    np.testing.assert_array_equal(g, o)
+
+
+def test_greedy_property_gpu():
+    """test_Greedy.cpp:209-295 on the device: lazier vs baseline <= 20%."""
+    info, score = greedy_world()
+    n = len(score)
+    ob = Observability(ObsCamera())
+    for k in range(60, 141, 10):
+        base = set(ob.maxvol_select(info, score, k, 0, 1).tolist())
+        scale = float(int(np.float32(n) / np.float32(k) * math.log(10.0)))
+        for _ in range(20):
+            lazy = ob.maxvol_select(info, score, k, scale, 3)
+            assert len(base - set(lazy.tolist())) <= math.ceil(0.2 * len(base))
