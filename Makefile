@@ -4,7 +4,7 @@ CXX     ?= g++
 ARCH    ?= gfx950
 HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
            -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function
-ORCFLAGS = -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
+ORCFLAGS = -O3 -fno-tree-vectorize -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function
 
 CSRC    = gf_orb_slam_amd/csrc
 HIPSRCS = $(wildcard $(CSRC)/*.hip)
@@ -25,7 +25,7 @@ build/%.o: $(CSRC)/%.hip $(HDRS)
 
 build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 	@mkdir -p build
-	$(CXX) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
+	$(CXX) -O3 -fno-tree-vectorize -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
 
 $(LIB): $(HIPOBJS) $(CPPOBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
