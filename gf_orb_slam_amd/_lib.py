@@ -96,6 +96,9 @@ _PROTOS = {
     "gf_maxvol_select_dev": [_P, _I, _P, _P, _P, _I, _I, _D, _I, _P, _P, _P, _P],
     "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
                                _P, _P],
+    "gf_pose_opt": [_P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
+    "gf_pose_opt_batch_dev": [_P, _I, _P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
+    "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
 }
 
 

@@ -1,0 +1,441 @@
+// Motion-only pose optimisation on gfx950.
+//
+// One 64-lane wave per problem (frame). Per-edge work — projection, error,
+// Huber weight, the 2x6 pose Jacobian and its 27 contributions to the lower
+// triangle of H and to b — runs one edge per lane; the reductions over edges
+// keep the reference's order: lane k of the wave owns accumulator k (21 lower
+// H entries, 6 b entries, robust chi2) and adds the per-edge terms staged in
+// LDS in edge order, exactly as g2o's sequential loop over _activeEdges
+// (sparse_optimizer.cpp:100-114, block_solver.hpp:502-562). The scalar LM
+// logic (lambda schedule, LDLT, exp update, stop rules) runs redundantly on
+// every lane from the shared sums, so no broadcast is needed.
+//
+// Reference: Optimizer::PoseOptimization src/Optimizer.cc:279-413,
+// OptimizationAlgorithmLevenberg::solve core/optimization_algorithm_levenberg.cpp:61-189,
+// EdgeSE3ProjectXYZ types/sba/types_six_dof_expmap.cpp:384-428,
+// BaseBinaryEdge::constructQuadraticForm core/base_binary_edge.hpp:55-122.
+#include "common.h"
+#include "se3.h"
+
+namespace {
+
+constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
+constexpr int PO_CHI = 27;
+constexpr int PO_STRIDE_MAX = 8192;
+
+struct PoseArgs {
+    const gf_pose_edge* edges;
+    const int32_t* nedges;
+    int stride;
+    float* Tcw;
+    uint8_t* outl;
+    int32_t* ninl;
+    int32_t* iters;
+    double* work;  // per problem: err0[stride], err1[stride], info[stride]
+    double fx, fy, cx, cy;
+    // optional scatter of the outlier flags to keypoint slots
+    const int32_t* edge_kp;
+    uint8_t* kp_outl;
+    int kp_stride;
+};
+
+struct Lane {
+    const gf_pose_edge* E;
+    double *e0, *e1, *info;
+    int n, l;
+    double fx, fy, cx, cy, delta, dsqr;
+};
+
+__device__ __forceinline__ void robustify(double e, double delta, double dsqr, double& rho0, double& rho1) {
+    if (e <= dsqr) {
+        rho0 = e;
+        rho1 = 1.;
+    } else {
+        const double s = sqrt(e);
+        rho0 = 2 * s * delta - dsqr;
+        rho1 = delta / s;
+    }
+}
+
+__device__ __forceinline__ void edge_error(const Lane& L, const gfse3::SE3& T, int e, double* pc, double& r0,
+                                           double& r1) {
+    const gf_pose_edge g = L.E[e];
+    const double X[3] = {(double)g.X[0], (double)g.X[1], (double)g.X[2]};
+    gfse3::map(T, X, pc);
+    const double px = pc[0] / pc[2], py = pc[1] / pc[2];
+    r0 = (double)g.z[0] - (px * L.fx + L.cx);
+    r1 = (double)g.z[1] - (py * L.fy + L.cy);
+}
+
+// computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
+// Returns the sums in sh_sum: [0,21) lower H row-major-packed, [21,27) b, 27 chi2.
+__device__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[65], double* sh_sum) {
+    double acc = 0.0;
+    for (int base = 0; base < L.n; base += 64) {
+        const int e = base + L.l;
+        if (e < L.n) {
+            double pc[3], r0, r1;
+            edge_error(L, T, e, pc, r0, r1);
+            L.e0[e] = r0;
+            L.e1[e] = r1;
+            const double info = L.info[e];
+            const double chi2 = r0 * (info * r0) + r1 * (info * r1);
+            double rho0, rho1;
+            robustify(chi2, L.delta, L.dsqr, rho0, rho1);
+            term[PO_CHI][L.l] = rho0;
+            if (build) {
+                const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
+                double J0[6], J1[6];
+                J0[0] = x * y / z2 * L.fx;
+                J0[1] = -(1 + (x * x / z2)) * L.fx;
+                J0[2] = y / z * L.fx;
+                J0[3] = -1. / z * L.fx;
+                J0[4] = 0;
+                J0[5] = x / z2 * L.fx;
+                J1[0] = (1 + y * y / z2) * L.fy;
+                J1[1] = -x * y / z2 * L.fy;
+                J1[2] = -x / z * L.fy;
+                J1[3] = 0;
+                J1[4] = -1. / z * L.fy;
+                J1[5] = y / z2 * L.fy;
+                const double w = rho1 * info;
+                const double o0 = -(info * r0) * rho1, o1 = -(info * r1) * rho1;
+                int k = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = 0; b <= a; b++) term[k++][L.l] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
+#pragma unroll
+                for (int a = 0; a < 6; a++) term[21 + a][L.l] = J0[a] * o0 + J1[a] * o1;
+            }
+        }
+        __syncthreads();
+        const int m = min(64, L.n - base);
+        if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
+            for (int j = 0; j < m; j++) acc += term[L.l][j];
+        }
+        __syncthreads();
+    }
+    if ((build && L.l < PO_NACC) || L.l == PO_CHI) sh_sum[L.l] = acc;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
+    __shared__ double term[PO_NACC][65];
+    __shared__ double sh_sum[PO_NACC];
+    const int p = blockIdx.x;
+    Lane L;
+    L.l = threadIdx.x;
+    L.n = min(max(A.nedges[p], 0), A.stride);
+    L.E = A.edges + (size_t)p * A.stride;
+    L.e0 = A.work + (size_t)p * A.stride * 3;
+    L.e1 = L.e0 + A.stride;
+    L.info = L.e1 + A.stride;
+    L.fx = A.fx;
+    L.fy = A.fy;
+    L.cx = A.cx;
+    L.cy = A.cy;
+    L.delta = (double)(float)sqrt(5.991);  // const float delta = sqrt(5.991)
+    L.dsqr = L.delta * L.delta;
+    uint8_t* ou = A.outl + (size_t)p * A.stride;
+    float* Tp = A.Tcw + (size_t)p * 16;
+
+    // Converter::toSE3Quat: float Tcw -> Matrix3d -> Quaterniond -> normalizeRotation
+    gfse3::SE3 T;
+    {
+        double R[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[3 * i + j] = (double)Tp[4 * i + j];
+        T.r = gfse3::from_R(R);
+        for (int i = 0; i < 3; i++) T.t[i] = (double)Tp[4 * i + 3];
+        gfse3::normalize(T.r);
+    }
+    for (int e = L.l; e < L.n; e += 64) {
+        L.info[e] = (double)L.E[e].inv_sigma2;
+        L.e0[e] = L.e1[e] = 0.0;
+        ou[e] = 0;
+    }
+    __syncthreads();
+
+    const double chi2t[4] = {(double)9.210f, (double)7.378f, (double)5.991f, (double)5.991f};
+    const int its[4] = {10, 10, 7, 5};
+    int nBadEdges = 0, total_it = 0;
+    double xs[6] = {0, 0, 0, 0, 0, 0};
+    for (int round = 0; round < 4 && L.n > 0; round++) {
+        // SparseOptimizer::optimize(its[round]) with the Levenberg algorithm
+        double lambda = 0, ni = 2;
+        int nBad = 0;
+        for (int iter = 0; iter < its[round]; iter++) {
+            total_it++;
+            pass(L, T, true, term, sh_sum);
+            double H[36], b[6];
+            for (int a = 0, k = 0; a < 6; a++)
+                for (int c = 0; c <= a; c++, k++) H[6 * a + c] = H[6 * c + a] = sh_sum[k];
+            for (int a = 0; a < 6; a++) b[a] = sh_sum[21 + a];
+            double currentChi = sh_sum[PO_CHI];
+            const double iniChi = currentChi;
+            if (iter == 0) {
+                double md = 0;
+                for (int j = 0; j < 6; j++) md = fmax(fabs(H[7 * j]), md);
+                lambda = 1e-5 * md;
+                ni = 2;
+                nBad = 0;
+            }
+            double rho = 0;
+            int q = 0;
+            do {
+                double Hl[36];
+                for (int i = 0; i < 36; i++) Hl[i] = H[i];
+                for (int j = 0; j < 6; j++) Hl[7 * j] += lambda;
+                double xn[6];
+                const bool ok = gfse3::ldlt6(Hl, b, xn);
+                if (ok)
+                    for (int j = 0; j < 6; j++) xs[j] = xn[j];
+                const gfse3::SE3 trial = gfse3::exp_mul(xs, T);
+                pass(L, trial, false, term, sh_sum);
+                double tempChi = sh_sum[PO_CHI];
+                if (!ok) tempChi = DBL_MAX;
+                rho = currentChi - tempChi;
+                double scale = 0;
+                for (int j = 0; j < 6; j++) scale += xs[j] * (lambda * xs[j] + b[j]);
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && isfinite(tempChi)) {
+                    double alpha = 1. - pow((2 * rho - 1), 3.0);
+                    alpha = fmin(alpha, 2. / 3.);
+                    const double sf = fmax(1. / 3., alpha);
+                    lambda *= sf;
+                    ni = 2;
+                    currentChi = tempChi;
+                    T = trial;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                }
+                q++;
+            } while (rho < 0 && q < 10);
+            if (q == 10 || rho == 0) break;
+            if ((iniChi - currentChi) * 1e3 < iniChi)
+                nBad++;
+            else
+                nBad = 0;
+            if (nBad >= 3) break;
+        }
+        // outlier classification (Optimizer.cc:373-395); errors are those of
+        // the last evaluated estimate, recomputed only for flagged edges.
+        int nb = 0;
+        for (int base = 0; base < L.n; base += 64) {
+            const int e = base + L.l;
+            bool bad = false;
+            if (e < L.n) {
+                if (ou[e]) {
+                    L.info[e] = (double)L.E[e].inv_sigma2;
+                    double pc[3], r0, r1;
+                    edge_error(L, T, e, pc, r0, r1);
+                    L.e0[e] = r0;
+                    L.e1[e] = r1;
+                }
+                const double r0 = L.e0[e], r1 = L.e1[e], info = L.info[e];
+                const double c2 = r0 * (info * r0) + r1 * (info * r1);
+                if (c2 > chi2t[round]) {
+                    ou[e] = 1;
+                    L.info[e] = 1e-10;
+                    bad = true;
+                } else if (c2 <= chi2t[round]) {
+                    ou[e] = 0;
+                }
+            }
+            nb += __popcll(__ballot(bad));
+        }
+        nBadEdges = nb;
+        __syncthreads();
+        if (L.n < 10) break;
+    }
+
+    // Converter::toCvMat(SE3Quat): float pose out
+    __syncthreads();
+    if (L.l == 0) {
+        double R[9];
+        gfse3::to_R(T.r, R);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) Tp[4 * i + j] = (float)R[3 * i + j];
+            Tp[4 * i + 3] = (float)T.t[i];
+        }
+        Tp[12] = Tp[13] = Tp[14] = 0.f;
+        Tp[15] = 1.f;
+        A.ninl[p] = L.n - nBadEdges;
+        if (A.iters) A.iters[p] = total_it;
+    }
+    if (A.kp_outl)
+        for (int e = L.l; e < L.n; e += 64)
+            A.kp_outl[(size_t)p * A.kp_stride + A.edge_kp[(size_t)p * A.stride + e]] = ou[e];
+}
+
+struct GatherArgs {
+    const gf_keypoint* kps;
+    const int32_t* nkps;
+    int kp_stride;
+    const int32_t* kp2mp;
+    const gf_map_point* map;
+    int map_stride;
+    float inv_sigma2[16];
+    int nlevels;
+    gf_pose_edge* edges;
+    int32_t* edge_kp;
+    int32_t* nedges;
+};
+
+// Ordered compaction of the matched keypoints of one frame (one wave).
+__global__ __launch_bounds__(64) void k_pose_gather(GatherArgs G) {
+    const int f = blockIdx.x, l = threadIdx.x;
+    const int n = G.nkps[f];
+    const size_t kb = (size_t)f * G.kp_stride;
+    int cnt = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + l;
+        int mp = -1;
+        if (i < n) mp = G.kp2mp[kb + i];
+        const bool on = mp >= 0;
+        const unsigned long long m = __ballot(on);
+        const int pos = cnt + __popcll(m & ((1ull << l) - 1ull));
+        if (on) {
+            const gf_keypoint k = G.kps[kb + i];
+            const gf_map_point& P = G.map[(size_t)f * G.map_stride + mp];
+            gf_pose_edge e;
+            e.X[0] = P.pos[0];
+            e.X[1] = P.pos[1];
+            e.X[2] = P.pos[2];
+            e.z[0] = k.x;
+            e.z[1] = k.y;
+            const int oc = min(max(k.octave, 0), G.nlevels - 1);
+            e.inv_sigma2 = G.inv_sigma2[oc];
+            G.edges[kb + pos] = e;
+            G.edge_kp[kb + pos] = i;
+        }
+        cnt += __popcll(m);
+    }
+    if (l == 0) G.nedges[f] = cnt;
+}
+
+int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
+    GF_PROF(ctx, s, "k_pose_opt");
+    k_pose_opt<<<nprob, 64, 0, s>>>(A);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gf_pose_opt_batch_dev(gf_ctx* ctx, int nprob, float* d_Tcw, const gf_pose_edge* d_edges, const int32_t* d_nedges,
+                          int edge_stride, float fx, float fy, float cx, float cy, uint8_t* d_outlier,
+                          int32_t* d_ninliers, int32_t* d_iterations, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (nprob <= 0) return GF_OK;
+    GF_CHECK(d_Tcw && d_edges && d_nedges && d_outlier && d_ninliers, GF_ERR_ARG, "null arg");
+    GF_CHECK(edge_stride > 0 && edge_stride <= PO_STRIDE_MAX, GF_ERR_UNSUPPORTED, "edge_stride out of range");
+    void* work;
+    int rc = gf::ws_get(ctx, 40, (size_t)nprob * edge_stride * 3 * sizeof(double), &work);
+    if (rc) return rc;
+    PoseArgs A{};
+    A.edges = d_edges;
+    A.nedges = d_nedges;
+    A.stride = edge_stride;
+    A.Tcw = d_Tcw;
+    A.outl = d_outlier;
+    A.ninl = d_ninliers;
+    A.iters = d_iterations;
+    A.work = (double*)work;
+    A.fx = fx;
+    A.fy = fy;
+    A.cx = cx;
+    A.cy = cy;
+    return launch_pose(ctx, nprob, A, (hipStream_t)stream);
+}
+
+int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keypoint* d_kps, const int32_t* d_nkps,
+                           int kp_stride, const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
+                           const float* inv_sigma2, int nlevels, float fx, float fy, float cx, float cy,
+                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (nframes <= 0) return GF_OK;
+    GF_CHECK(d_Tcw && d_kps && d_nkps && d_kp2mp && d_map && inv_sigma2 && d_outlier && d_ninliers, GF_ERR_ARG,
+             "null arg");
+    GF_CHECK(kp_stride > 0 && kp_stride <= PO_STRIDE_MAX, GF_ERR_UNSUPPORTED, "kp_stride out of range");
+    GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
+    hipStream_t s = (hipStream_t)stream;
+    void *edges, *ekp, *ne, *eout, *work;
+    int rc;
+    const size_t ne_tot = (size_t)nframes * kp_stride;
+    if ((rc = gf::ws_get(ctx, 41, ne_tot * sizeof(gf_pose_edge), &edges)) ||
+        (rc = gf::ws_get(ctx, 42, ne_tot * sizeof(int32_t), &ekp)) ||
+        (rc = gf::ws_get(ctx, 43, (size_t)nframes * sizeof(int32_t), &ne)) ||
+        (rc = gf::ws_get(ctx, 44, ne_tot, &eout)) ||
+        (rc = gf::ws_get(ctx, 40, ne_tot * 3 * sizeof(double), &work)))
+        return rc;
+    GatherArgs G{};
+    G.kps = d_kps;
+    G.nkps = d_nkps;
+    G.kp_stride = kp_stride;
+    G.kp2mp = d_kp2mp;
+    G.map = d_map;
+    G.map_stride = map_stride;
+    for (int i = 0; i < nlevels; i++) G.inv_sigma2[i] = inv_sigma2[i];
+    G.nlevels = nlevels;
+    G.edges = (gf_pose_edge*)edges;
+    G.edge_kp = (int32_t*)ekp;
+    G.nedges = (int32_t*)ne;
+    {
+        GF_PROF(ctx, s, "k_pose_gather");
+        k_pose_gather<<<nframes, 64, 0, s>>>(G);
+        GF_HIP(hipGetLastError());
+    }
+    PoseArgs A{};
+    A.edges = G.edges;
+    A.nedges = G.nedges;
+    A.stride = kp_stride;
+    A.Tcw = d_Tcw;
+    A.outl = (uint8_t*)eout;
+    A.ninl = d_ninliers;
+    A.iters = d_iterations;
+    A.work = (double*)work;
+    A.fx = fx;
+    A.fy = fy;
+    A.cx = cx;
+    A.cy = cy;
+    A.edge_kp = G.edge_kp;
+    A.kp_outl = d_outlier;
+    A.kp_stride = kp_stride;
+    return launch_pose(ctx, nframes, A, s);
+}
+
+int gf_pose_opt(gf_ctx* ctx, const float* Tcw_in, const gf_pose_edge* edges, int n, float fx, float fy, float cx,
+                float cy, float* Tcw_out, uint8_t* outlier, int32_t* ninliers, int32_t* iterations) {
+    GF_CHECK(ctx && Tcw_in && Tcw_out && ninliers, GF_ERR_ARG, "null arg");
+    GF_CHECK(n >= 0 && (n == 0 || (edges && outlier)), GF_ERR_ARG, "bad edge list");
+    GF_CHECK(n <= PO_STRIDE_MAX, GF_ERR_UNSUPPORTED, "too many edges");
+    GF_HIP(hipSetDevice(ctx->device));
+    const int stride = n > 0 ? n : 1;
+    void *dT, *dE, *dN, *dO, *dI, *dIt;
+    int rc;
+    const int32_t nn = n;
+    if ((rc = gf::ws_upload(ctx, 0, Tcw_in, 64, &dT)) || (rc = gf::ws_get(ctx, 1, sizeof(gf_pose_edge) * stride, &dE)) ||
+        (rc = gf::ws_upload(ctx, 2, &nn, 4, &dN)) || (rc = gf::ws_get(ctx, 3, stride, &dO)) ||
+        (rc = gf::ws_get(ctx, 4, 4, &dI)) || (rc = gf::ws_get(ctx, 5, 4, &dIt)))
+        return rc;
+    if (n > 0) GF_HIP(hipMemcpyAsync(dE, edges, sizeof(gf_pose_edge) * n, hipMemcpyHostToDevice, ctx->stream));
+    rc = gf_pose_opt_batch_dev(ctx, 1, (float*)dT, (const gf_pose_edge*)dE, (const int32_t*)dN, stride, fx, fy, cx, cy,
+                               (uint8_t*)dO, (int32_t*)dI, (int32_t*)dIt, ctx->stream);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(Tcw_out, dT, 64, hipMemcpyDeviceToHost, ctx->stream));
+    if (n > 0) GF_HIP(hipMemcpyAsync(outlier, dO, n, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(ninliers, dI, 4, hipMemcpyDeviceToHost, ctx->stream));
+    int32_t it = 0;
+    GF_HIP(hipMemcpyAsync(&it, dIt, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    if (iterations) *iterations = it;
+    return GF_OK;
+}
+
+}  // extern "C"

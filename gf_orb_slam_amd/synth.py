@@ -167,3 +167,49 @@ def synth_scene(camera: str, n_mp: int, n_kp: int, seed: int, nlevels: int = 8, 
     kps, desc, kp_mp = kps[order], desc[order], kp_mp[order]
     return {"map": mp, "mp_desc": mp_desc, "Tcw": Tcw, "keypoints": np.ascontiguousarray(kps),
             "descriptors": np.ascontiguousarray(desc), "kp_mp": kp_mp, "camera": cam}
+
+
+POSE_EDGE_DTYPE = np.dtype([("X", "<f4", 3), ("z", "<f4", 2), ("inv_sigma2", "<f4")])
+
+
+def synth_pose_problem(seed: int, n: int, camera: str = "euroc", noise_px: float = 1.0, outlier_frac: float = 0.1,
+                       rot_deg: float = 0.5, trans: float = 0.01, nlevels: int = 8, scale: float = 1.2):
+    """One PoseOptimization problem (SURVEY.md §8d config 4 noise model).
+
+    Map points X ~ U([-4,4]x[-4,4]x[2,8]) seen from a random Tcw_true; keypoint
+    z = projection + N(0, noise_px), octave U{0..nlevels-1}; outlier_frac of the
+    edges displaced 3-6 px (test_RANSAC.cpp:186-188 style). The initial pose is
+    Tcw_true perturbed by rot_deg / trans. Returns (Tcw_true, Tcw_init, edges, cam).
+    """
+    rng = np.random.default_rng(seed)
+    cam = CAMERAS[camera]
+    w, h, fx, fy, cx, cy = cam
+    T_true = look_pose(rng, trans_sigma=0.3, rot_deg=5.0).astype(np.float64)
+    Xs, zs = [], []
+    while sum(len(x) for x in Xs) < n:
+        Pc = np.c_[rng.uniform(-4, 4, 4 * n), rng.uniform(-4, 4, 4 * n), rng.uniform(2, 8, 4 * n)]
+        X = (Pc - T_true[:3, 3]) @ T_true[:3, :3]  # world = R^T (Pc - t)
+        u, v, d = project(T_true, X, cam)
+        ok = (d > 0.1) & (u >= 0) & (u < w) & (v >= 0) & (v < h)
+        Xs.append(X[ok])
+        zs.append(np.c_[u[ok], v[ok]])
+    X = np.concatenate(Xs)[:n]
+    z = np.concatenate(zs)[:n] + rng.normal(0, noise_px, (n, 2))
+    nout = int(round(outlier_frac * n))
+    if nout:
+        idx = rng.choice(n, nout, replace=False)
+        ang = rng.uniform(0, 2 * np.pi, nout)
+        r = rng.uniform(3, 6, nout)
+        z[idx] += np.c_[r * np.cos(ang), r * np.sin(ang)]
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(s[-1] * np.float32(scale)))
+    s = np.array(s, np.float32)
+    invs = (np.float32(1.0) / (s * s)).astype(np.float32)
+    edges = np.zeros(n, POSE_EDGE_DTYPE)
+    edges["X"] = X
+    edges["z"] = z
+    edges["inv_sigma2"] = invs[rng.integers(0, nlevels, n)]
+    dT = look_pose(rng, trans_sigma=trans, rot_deg=rot_deg).astype(np.float64)
+    T_init = (dT @ T_true).astype(np.float32)
+    return T_true.astype(np.float32), T_init, edges, cam

@@ -286,6 +286,45 @@ int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const do
                          int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
                          int32_t* d_nout, void* stream);
 
+/* ------------------------------------------------ pose optimisation (P1-P4)
+ * Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:279-413) on g2o's
+ * Levenberg-Marquardt (core/optimization_algorithm_levenberg.cpp:61-189),
+ * EdgeSE3ProjectXYZ with a fixed map point (types_six_dof_expmap.cpp:384-428),
+ * Huber delta^2 = 5.991 (robust_kernel_impl.cpp:78-88) and the dense LDLT
+ * solver (linear_solver_dense.h:65-113). One edge per matched keypoint, in
+ * keypoint order; f64 internally, float pose in and out (Converter.cc:38-72).
+ * Outlier flags follow the reference: 4 rounds of {10,10,7,5} iterations with
+ * chi2 thresholds {9.210,7.378,5.991,5.991}; outliers keep their edge with
+ * information 1e-10. ninliers = n - nBad of the last round. */
+typedef struct gf_pose_edge {
+    float X[3];       /* MapPoint::GetWorldPos() */
+    float z[2];       /* mvKeysUn[i].pt */
+    float inv_sigma2; /* mvInvLevelSigma2[octave] */
+} gf_pose_edge;
+
+/* Host family: one problem of n edges. iterations (may be NULL) = LM
+ * iterations run over the 4 rounds. */
+int gf_pose_opt(gf_ctx* ctx, const float* Tcw_in, const gf_pose_edge* edges, int n, float fx, float fy, float cx,
+                float cy, float* Tcw_out, uint8_t* outlier, int32_t* ninliers, int32_t* iterations);
+
+/* Device family, nprob independent problems (one workgroup each). d_Tcw is
+ * nprob x 16 floats, updated in place; problem p owns edges
+ * [p*edge_stride, p*edge_stride + d_nedges[p]) and the same outlier slots.
+ * d_iterations may be NULL. edge_stride <= 8192. */
+int gf_pose_opt_batch_dev(gf_ctx* ctx, int nprob, float* d_Tcw, const gf_pose_edge* d_edges, const int32_t* d_nedges,
+                          int edge_stride, float fx, float fy, float cx, float cy, uint8_t* d_outlier,
+                          int32_t* d_ninliers, int32_t* d_iterations, void* stream);
+
+/* Device family over Frames: gathers the edges of every keypoint with
+ * d_kp2mp >= 0 (X = d_map[kp2mp].pos of that frame's map, z = keypoint,
+ * inv_sigma2[octave]), optimises d_Tcw in place and writes mvbOutlier for the
+ * matched keypoints (others untouched). inv_sigma2 is a host array of nlevels
+ * (<= 16) floats. kp_stride <= 8192. */
+int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keypoint* d_kps, const int32_t* d_nkps,
+                           int kp_stride, const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
+                           const float* inv_sigma2, int nlevels, float fx, float fy, float cx, float cy,
+                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

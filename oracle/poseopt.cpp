@@ -1,0 +1,433 @@
+// CPU ORACLE (test infrastructure) — pose optimisation rows P1-P4 of
+// Optimizer::PoseOptimization (src/Optimizer.cc:279-413) on the
+// vendored g2o arithmetic it runs: OptimizationAlgorithmLevenberg::solve
+// (core/optimization_algorithm_levenberg.cpp:61-189), BaseBinaryEdge
+// constructQuadraticForm (core/base_binary_edge.hpp:55-122) with the Huber
+// kernel (core/robust_kernel_impl.cpp:78-88), EdgeSE3ProjectXYZ
+// (types/sba/types_six_dof_expmap.cpp:384-428), SE3Quat::exp / map
+// (types/slam3d/se3quat.h), Converter::toSE3Quat / toCvMat, and Eigen's
+// LDLT (diagonal pivoting) for LinearSolverDense. Sums run in edge order.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "oracle_common.h"
+
+namespace orc {
+
+struct Quat {
+    double w, x, y, z;
+};
+
+static Quat quat_from_R(const double m[3][3]) {  // Eigen quaternionbase_assign_impl
+    Quat q;
+    double t = m[0][0] + (m[1][1] + m[2][2]);  // diagonal().sum(): unrolled a0 + (a1 + a2)
+    if (t > 0) {
+        t = std::sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (m[2][1] - m[1][2]) * t;
+        q.y = (m[0][2] - m[2][0]) * t;
+        q.z = (m[1][0] - m[0][1]) * t;
+    } else {
+        int i = 0;
+        if (m[1][1] > m[0][0]) i = 1;
+        if (m[2][2] > m[i][i]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (m[k][j] - m[j][k]) * t;
+        c[j] = (m[j][i] + m[i][j]) * t;
+        c[k] = (m[k][i] + m[i][k]) * t;
+        q.x = c[0];
+        q.y = c[1];
+        q.z = c[2];
+    }
+    return q;
+}
+
+static void normalize_rotation(Quat& q) {  // SE3Quat::normalizeRotation
+    if (q.w < 0) {
+        q.w *= -1;
+        q.x *= -1;
+        q.y *= -1;
+        q.z *= -1;
+    }
+    // coeffs() = (x, y, z, w) reduced as two packets: (x^2 + z^2) + (y^2 + w^2)
+    double n = std::sqrt((q.x * q.x + q.z * q.z) + (q.y * q.y + q.w * q.w));
+    q.x /= n;
+    q.y /= n;
+    q.z /= n;
+    q.w /= n;
+}
+
+static void quat_to_R(const Quat& q, double R[3][3]) {  // Eigen toRotationMatrix
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    R[0][0] = 1 - (tyy + tzz);
+    R[0][1] = txy - twz;
+    R[0][2] = txz + twy;
+    R[1][0] = txy + twz;
+    R[1][1] = 1 - (txx + tzz);
+    R[1][2] = tyz - twx;
+    R[2][0] = txz - twy;
+    R[2][1] = tyz + twx;
+    R[2][2] = 1 - (txx + tyy);
+}
+
+static void rotate(const Quat& q, const double* v, double* o) {  // Eigen _transformVector
+    double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+    for (int i = 0; i < 3; i++) uv[i] += uv[i];
+    const double cx = q.y * uv[2] - q.z * uv[1], cy = q.z * uv[0] - q.x * uv[2], cz = q.x * uv[1] - q.y * uv[0];
+    o[0] = v[0] + q.w * uv[0] + cx;
+    o[1] = v[1] + q.w * uv[1] + cy;
+    o[2] = v[2] + q.w * uv[2] + cz;
+}
+
+static Quat qmul(const Quat& a, const Quat& b) {
+    Quat r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z;
+    r.z = a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x;
+    return r;
+}
+
+struct SE3 {
+    Quat r;
+    double t[3];
+    void map(const double* p, double* o) const {
+        rotate(r, p, o);
+        for (int i = 0; i < 3; i++) o[i] += t[i];
+    }
+};
+
+static SE3 se3_exp(const double* u) {  // SE3Quat::exp, se3quat.h:223-258
+    const double w[3] = {u[0], u[1], u[2]}, up[3] = {u[3], u[4], u[5]};
+    const double theta = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+    const double O[3][3] = {{0, -w[2], w[1]}, {w[2], 0, -w[0]}, {-w[1], w[0], 0}};
+    double O2[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) O2[i][j] = O[i][0] * O[0][j] + O[i][1] * O[1][j] + O[i][2] * O[2][j];
+    double R[3][3], V[3][3];
+    if (theta < 0.00001) {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[i][j] = ((i == j ? 1.0 : 0.0) + O[i][j]) + O2[i][j];
+        std::memcpy(V, R, sizeof(R));
+    } else {
+        const double a = std::sin(theta) / theta, b = (1 - std::cos(theta)) / (theta * theta);
+        const double c = (theta - std::sin(theta)) / std::pow(theta, 3);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                R[i][j] = ((i == j ? 1.0 : 0.0) + a * O[i][j]) + b * O2[i][j];
+                V[i][j] = ((i == j ? 1.0 : 0.0) + b * O[i][j]) + c * O2[i][j];
+            }
+    }
+    SE3 s;
+    s.r = quat_from_R(R);
+    for (int i = 0; i < 3; i++) s.t[i] = V[i][0] * up[0] + V[i][1] * up[1] + V[i][2] * up[2];
+    normalize_rotation(s.r);
+    return s;
+}
+
+static SE3 se3_mul(const SE3& a, const SE3& b) {  // SE3Quat::operator*
+    SE3 r = a;
+    double rt[3];
+    rotate(a.r, b.t, rt);
+    for (int i = 0; i < 3; i++) r.t[i] += rt[i];
+    r.r = qmul(a.r, b.r);
+    normalize_rotation(r.r);
+    return r;
+}
+
+// Eigen::LDLT<MatrixXd> (diagonal pivoting) solve of H x = b, n = 6.
+// Returns false when the factorisation is not positive (isPositive()).
+bool ldlt_solve(const double* Hin, const double* b, double* x, int n) {
+    double A[36];
+    std::memcpy(A, Hin, sizeof(double) * n * n);
+    int perm[6];
+    bool found_zero = false, ok = true;
+    int sign = 0;  // 0 zero, 1 psd, 2 nsd, 3 indefinite
+    double temp[6];
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = std::fabs(A[k * n + k]);
+        for (int i = k + 1; i < n; i++)
+            if (std::fabs(A[i * n + i]) > bv) bv = std::fabs(A[i * n + i]), big = i;
+        perm[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; j++) std::swap(A[k * n + j], A[big * n + j]);
+            for (int i = big + 1; i < n; i++) std::swap(A[i * n + k], A[i * n + big]);
+            std::swap(A[k * n + k], A[big * n + big]);
+            for (int i = k + 1; i < big; i++) {
+                double t = A[i * n + k];
+                A[i * n + k] = A[big * n + i];
+                A[big * n + i] = t;
+            }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; j++) temp[j] = A[j * n + j] * A[k * n + j];
+            double s = 0;
+            for (int j = 0; j < k; j++) s += A[k * n + j] * temp[j];
+            A[k * n + k] -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += A[i * n + j] * temp[j];
+                A[i * n + k] -= t;
+            }
+        }
+        const double akk = A[k * n + k];
+        const bool valid = std::fabs(akk) > 0;
+        if (k == 0 && !valid) {
+            sign = 0;
+            ok = false;
+            for (int j = 0; j < n; j++) perm[j] = j;
+            break;
+        }
+        if (valid)
+            for (int i = k + 1; i < n; i++) A[i * n + k] /= akk;
+        if (found_zero && valid)
+            ok = false;
+        else if (!valid)
+            found_zero = true;
+        if (sign == 1) {
+            if (akk < 0) sign = 3;
+        } else if (sign == 2) {
+            if (akk > 0) sign = 3;
+        } else if (sign == 0) {
+            if (akk > 0)
+                sign = 1;
+            else if (akk < 0)
+                sign = 2;
+        }
+    }
+    (void)ok;
+    if (!(sign == 1 || sign == 0)) return false;
+    // x = P b
+    for (int i = 0; i < n; i++) x[i] = b[i];
+    for (int k = 0; k < n; k++) std::swap(x[k], x[perm[k]]);
+    for (int j = 0; j < n; j++)  // L^-1 (unit lower, column axpy order)
+        for (int i = j + 1; i < n; i++) x[i] -= A[i * n + j] * x[j];
+    const double tol = DBL_MIN;  // numeric_limits<double>::min()
+    for (int i = 0; i < n; i++) x[i] = std::fabs(A[i * n + i]) > tol ? x[i] / A[i * n + i] : 0.0;
+    for (int i = n - 1; i >= 0; i--) {  // L^-T
+        double s = 0;
+        for (int k = i + 1; k < n; k++) s += A[k * n + i] * x[k];
+        x[i] -= s;
+    }
+    for (int k = n - 1; k >= 0; k--) std::swap(x[k], x[perm[k]]);
+    return true;
+}
+
+struct Edge {
+    double X[3], z[2], info, delta;
+    double err[2];
+};
+
+struct PoseProblem {
+    std::vector<Edge> e;
+    double fx, fy, cx, cy;
+    SE3 T;
+    // Solver::_x persists across optimize() calls and keeps its last value when
+    // the LDLT is not positive (g2o leaves it uninitialised; zero here).
+    double x[6] = {0, 0, 0, 0, 0, 0};
+
+    void compute_error(Edge& g, const SE3& P) const {
+        double pc[3];
+        P.map(g.X, pc);
+        const double px = pc[0] / pc[2], py = pc[1] / pc[2];
+        g.err[0] = g.z[0] - (px * fx + cx);
+        g.err[1] = g.z[1] - (py * fy + cy);
+    }
+    static double chi2(const Edge& g) { return g.err[0] * (g.info * g.err[0]) + g.err[1] * (g.info * g.err[1]); }
+    static void robustify(const Edge& g, double e, double* rho) {
+        const double dsqr = g.delta * g.delta;
+        if (e <= dsqr) {
+            rho[0] = e;
+            rho[1] = 1.;
+        } else {
+            const double s = std::sqrt(e);
+            rho[0] = 2 * s * g.delta - dsqr;
+            rho[1] = g.delta / s;
+        }
+    }
+    double robust_chi2_all(const SE3& P) {
+        double chi = 0;
+        for (auto& g : e) {
+            compute_error(g, P);
+            double rho[2];
+            robustify(g, chi2(g), rho);
+            chi += rho[0];
+        }
+        return chi;
+    }
+    void build(double* H, double* b) {
+        std::memset(H, 0, 36 * sizeof(double));
+        std::memset(b, 0, 6 * sizeof(double));
+        for (auto& g : e) {
+            double pc[3];
+            T.map(g.X, pc);
+            const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
+            double J[2][6];
+            J[0][0] = x * y / z2 * fx;
+            J[0][1] = -(1 + (x * x / z2)) * fx;
+            J[0][2] = y / z * fx;
+            J[0][3] = -1. / z * fx;
+            J[0][4] = 0;
+            J[0][5] = x / z2 * fx;
+            J[1][0] = (1 + y * y / z2) * fy;
+            J[1][1] = -x * y / z2 * fy;
+            J[1][2] = -x / z * fy;
+            J[1][3] = 0;
+            J[1][4] = -1. / z * fy;
+            J[1][5] = y / z2 * fy;
+            double rho[2];
+            robustify(g, chi2(g), rho);
+            const double w = rho[1] * g.info;
+            const double orr[2] = {-(g.info * g.err[0]) * rho[1], -(g.info * g.err[1]) * rho[1]};
+            for (int i = 0; i < 6; i++) {
+                b[i] += J[0][i] * orr[0] + J[1][i] * orr[1];
+                for (int j = 0; j < 6; j++) H[6 * i + j] += (J[0][i] * w) * J[0][j] + (J[1][i] * w) * J[1][j];
+            }
+        }
+    }
+
+    // SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg.
+    int optimize(int iterations) {
+        double lambda = 0, ni = 2;
+        int nBad = 0, it_done = 0;
+        for (int iter = 0; iter < iterations; iter++) {
+            it_done++;
+            double currentChi = robust_chi2_all(T);
+            double iniChi = currentChi;
+            double H[36], b[6];
+            build(H, b);
+            if (iter == 0) {
+                double md = 0;
+                for (int j = 0; j < 6; j++) md = std::max(std::fabs(H[7 * j]), md);
+                lambda = 1e-5 * md;
+                ni = 2;
+                nBad = 0;
+            }
+            double rho = 0;
+            int q = 0;
+            do {
+                double Hl[36];
+                std::memcpy(Hl, H, sizeof(H));
+                for (int j = 0; j < 6; j++) Hl[7 * j] += lambda;
+                double xs[6];
+                bool ok = ldlt_solve(Hl, b, xs, 6);
+                if (ok) std::memcpy(x, xs, sizeof(x));
+                SE3 trial = se3_mul(se3_exp(x), T);
+                double tempChi = robust_chi2_all(trial);
+                if (!ok) tempChi = DBL_MAX;
+                rho = currentChi - tempChi;
+                double scale = 0;
+                for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + b[j]);
+                scale += 1e-3;
+                rho /= scale;
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    double sf = std::max(1. / 3., alpha);
+                    lambda *= sf;
+                    ni = 2;
+                    currentChi = tempChi;
+                    T = trial;
+                } else {
+                    lambda *= ni;
+                    ni *= 2;
+                    // estimate restored; edge errors keep the trial values (g2o pops only the state)
+                }
+                q++;
+            } while (rho < 0 && q < 10);
+            if (q == 10 || rho == 0) break;
+            if ((iniChi - currentChi) * 1e3 < iniChi)
+                nBad++;
+            else
+                nBad = 0;
+            if (nBad >= 3) break;
+        }
+        return it_done;
+    }
+};
+
+}  // namespace orc
+
+extern "C" {
+
+// Optimizer::PoseOptimization for one frame. Edges in keypoint order: X (MP
+// world position, float as cv::Mat), z (keypoint), octave; inv_sigma2 per level.
+int orc_pose_opt(const float* Tcw_in, const float* X, const float* z, const int32_t* octave,
+                 const float* inv_sigma2_levels, int n, float fx, float fy, float cx, float cy, float* Tcw_out,
+                 uint8_t* outlier, int* ninliers, int* iterations) {
+    orc::PoseProblem P;
+    P.fx = fx;
+    P.fy = fy;
+    P.cx = cx;
+    P.cy = cy;
+    double R[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R[i][j] = Tcw_in[4 * i + j];
+    P.T.r = orc::quat_from_R(R);
+    for (int i = 0; i < 3; i++) P.T.t[i] = Tcw_in[4 * i + 3];
+    orc::normalize_rotation(P.T.r);
+    const float delta = std::sqrt(5.991);
+    std::vector<float> invs(n);
+    for (int i = 0; i < n; i++) {
+        orc::Edge g;
+        for (int k = 0; k < 3; k++) g.X[k] = X[3 * i + k];
+        g.z[0] = z[2 * i];
+        g.z[1] = z[2 * i + 1];
+        invs[i] = inv_sigma2_levels[octave[i]];
+        g.info = invs[i];
+        g.delta = delta;
+        g.err[0] = g.err[1] = 0;
+        P.e.push_back(g);
+        outlier[i] = 0;
+    }
+    const float chi2t[4] = {9.210f, 7.378f, 5.991f, 5.991f};
+    const int its[4] = {10, 10, 7, 5};
+    int nBad = 0, total_it = 0;
+    for (int it = 0; it < 4 && n > 0; it++) {  // empty graph: optimize() returns -1, nothing moves
+        total_it += P.optimize(its[it]);
+        nBad = 0;
+        for (int i = 0; i < n; i++) {
+            orc::Edge& g = P.e[i];
+            if (outlier[i]) {
+                g.info = invs[i];
+                P.compute_error(g, P.T);
+            }
+            const double c2 = orc::PoseProblem::chi2(g);
+            if (c2 > chi2t[it]) {
+                outlier[i] = 1;
+                g.info = 1e-10;
+                nBad++;
+            } else if (c2 <= chi2t[it]) {
+                outlier[i] = 0;
+            }
+        }
+        if (n < 10) break;
+    }
+    double Rr[3][3];
+    orc::quat_to_R(P.T.r, Rr);
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) Tcw_out[4 * i + j] = (float)Rr[i][j];
+        Tcw_out[4 * i + 3] = (float)P.T.t[i];
+    }
+    Tcw_out[12] = Tcw_out[13] = Tcw_out[14] = 0.f;
+    Tcw_out[15] = 1.f;
+    *ninliers = n - nBad;
+    if (iterations) *iterations = total_it;
+    return GF_OK;
+}
+
+int orc_ldlt_solve(const double* H, const double* b, double* x) { return orc::ldlt_solve(H, b, x, 6) ? 1 : 0; }
+
+}  // extern "C"

@@ -163,3 +163,29 @@ def maxvol_select(info, score, k, sample_scale, mode, seed):
     orc().orc_maxvol_select(_p(info), _p(np.ascontiguousarray(score, np.float64)), n, k, ctypes.c_double(sample_scale),
                             mode, ctypes.c_uint(seed), _p(out), ctypes.byref(nout))
     return out[:nout.value].copy()
+
+
+def pose_opt(Tcw, X, z, octave, inv_sigma2, fx, fy, cx, cy):
+    """Optimizer::PoseOptimization on the CPU oracle; returns (Tcw, outlier, ninliers, iterations)."""
+    Tcw = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+    X = np.ascontiguousarray(X, np.float32).reshape(-1, 3)
+    z = np.ascontiguousarray(z, np.float32).reshape(-1, 2)
+    octave = np.ascontiguousarray(octave, np.int32)
+    invs = np.ascontiguousarray(inv_sigma2, np.float32)
+    n = len(X)
+    out = np.zeros(16, np.float32)
+    outl = np.zeros(max(n, 1), np.uint8)
+    ninl, iters = ctypes.c_int(), ctypes.c_int()
+    f = ctypes.c_float
+    rc = orc().orc_pose_opt(_p(Tcw), _p(X), _p(z), _p(octave), _p(invs), n, f(fx), f(fy), f(cx), f(cy), _p(out),
+                            _p(outl), ctypes.byref(ninl), ctypes.byref(iters))
+    assert rc == 0, rc
+    return out.reshape(4, 4), outl[:n].copy(), ninl.value, iters.value
+
+
+def ldlt_solve(H, b):
+    H = np.ascontiguousarray(H, np.float64).reshape(6, 6)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.zeros(6)
+    ok = orc().orc_ldlt_solve(_p(H), _p(b), _p(x))
+    return bool(ok), x

@@ -23,6 +23,22 @@ def test_every_declared_symbol_is_exported():
     assert not missing, missing
 
 
+def test_every_declared_symbol_has_ctypes_prototype():
+    """Without argtypes ctypes truncates pointers to int: every entry point the
+    Python mirror can call must carry a prototype matching the header's arity."""
+    import re
+
+    src = re.sub(r"/\*.*?\*/", "", open(_lib.ABI_HEADER).read(), flags=re.S)
+    protos = dict(re.findall(r"\bint\s+(gf_[a-z0-9_]+)\s*\(([^)]*)\)", src))
+    _lib.lib()
+    missing = sorted(set(protos) - set(_lib._PROTOS) - {"gf_version"})
+    assert not missing, missing
+    for name, args in protos.items():
+        if name in _lib._PROTOS:
+            n = 0 if args.strip() in ("", "void") else args.count(",") + 1
+            assert len(_lib._PROTOS[name]) == n, (name, len(_lib._PROTOS[name]), n)
+
+
 def test_error_codes_without_device():
     lib = _lib.lib()
     n = ctypes.c_int(-1)
