@@ -96,9 +96,14 @@ _PROTOS = {
     "gf_maxvol_select_dev": [_P, _I, _P, _P, _P, _I, _I, _D, _I, _P, _P, _P, _P],
     "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
                                _P, _P],
+    "gf_obs_update_dev": [_P, _I, _P, _P, _P, _P, _P, _P],
+    "gf_motion_predict_dev": [_P, _I, _P, _P, _P, _P],
+    "gf_discard_outliers_dev": [_P, _I, _P, _P, _P, _I, _I, _P, _P, _P],
+    "gf_matched_gather_dev": [_P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P],
+    "gf_views_exclude_matched_dev": [_P, _I, _P, _P, _I, _P, _P, _I, _P],
     "gf_pose_opt": [_P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
     "gf_pose_opt_batch_dev": [_P, _I, _P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
-    "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
+    "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P, _P],
 }
 
 

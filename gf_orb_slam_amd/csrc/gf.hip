@@ -945,3 +945,32 @@ int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n
 }
 
 }  // extern "C"
+
+// G1 on the device: Observability::updatePWLSVec(mLastFrame.mTimeStamp,
+// mLastFrame.mTcw, mCurrentFrame.mTimeStamp, mCurrentFrame.getTwc())
+// (Tracking.cc:3168-3169) for every frame, one thread each.
+#include "kine.h"
+
+namespace {
+__global__ void k_obs_update(int nframes, const double* __restrict__ t_prev, const float* __restrict__ Tcw_prev,
+                             const double* __restrict__ t_cur, const float* __restrict__ Tcw_cur,
+                             double* __restrict__ Xv) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nframes) return;
+    float Twc[16];
+    gfkine::get_Twc(Tcw_cur + 16 * f, Twc);
+    gfkine::obs_update(t_prev[f], Tcw_prev + 16 * f, t_cur[f], Twc, Xv + 13 * f);
+}
+}  // namespace
+
+extern "C" int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev,
+                                 const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (nframes <= 0) return GF_OK;
+    GF_CHECK(d_t_prev && d_Tcw_prev && d_t_cur && d_Tcw_cur && d_Xv, GF_ERR_ARG, "null arg");
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_update");
+    k_obs_update<<<(nframes + 63) / 64, 64, 0, s>>>(nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}

@@ -357,7 +357,8 @@ int gf_pose_opt_batch_dev(gf_ctx* ctx, int nprob, float* d_Tcw, const gf_pose_ed
 int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keypoint* d_kps, const int32_t* d_nkps,
                            int kp_stride, const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
                            const float* inv_sigma2, int nlevels, float fx, float fy, float cx, float cy,
-                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, void* stream) {
+                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, int32_t* d_nedges,
+                           void* stream) {
     GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
     if (nframes <= 0) return GF_OK;
     GF_CHECK(d_Tcw && d_kps && d_nkps && d_kp2mp && d_map && inv_sigma2 && d_outlier && d_ninliers, GF_ERR_ARG,
@@ -365,12 +366,12 @@ int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keyp
     GF_CHECK(kp_stride > 0 && kp_stride <= PO_STRIDE_MAX, GF_ERR_UNSUPPORTED, "kp_stride out of range");
     GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
     hipStream_t s = (hipStream_t)stream;
-    void *edges, *ekp, *ne, *eout, *work;
+    void *edges, *ekp, *ne = d_nedges, *eout, *work;
     int rc;
     const size_t ne_tot = (size_t)nframes * kp_stride;
     if ((rc = gf::ws_get(ctx, 41, ne_tot * sizeof(gf_pose_edge), &edges)) ||
         (rc = gf::ws_get(ctx, 42, ne_tot * sizeof(int32_t), &ekp)) ||
-        (rc = gf::ws_get(ctx, 43, (size_t)nframes * sizeof(int32_t), &ne)) ||
+        (!d_nedges && (rc = gf::ws_get(ctx, 43, (size_t)nframes * sizeof(int32_t), &ne))) ||
         (rc = gf::ws_get(ctx, 44, ne_tot, &eout)) ||
         (rc = gf::ws_get(ctx, 40, ne_tot * 3 * sizeof(double), &work)))
         return rc;

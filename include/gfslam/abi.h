@@ -286,6 +286,12 @@ int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const do
                          int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
                          int32_t* d_nout, void* stream);
 
+/* G1 on the device: Xv[f] = updatePWLSVec(t_prev[f], Tcw_prev[f], t_cur[f],
+ * getTwc(Tcw_cur[f])) (Tracking.cc:3168-3169, Frame.cc:152-163). Segment 0 of
+ * predictPWLSVec keeps this Xv, which is what the FRAME/MAP info builds use. */
+int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev,
+                      const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, void* stream);
+
 /* ------------------------------------------------ pose optimisation (P1-P4)
  * Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:279-413) on g2o's
  * Levenberg-Marquardt (core/optimization_algorithm_levenberg.cpp:61-189),
@@ -319,11 +325,37 @@ int gf_pose_opt_batch_dev(gf_ctx* ctx, int nprob, float* d_Tcw, const gf_pose_ed
  * d_kp2mp >= 0 (X = d_map[kp2mp].pos of that frame's map, z = keypoint,
  * inv_sigma2[octave]), optimises d_Tcw in place and writes mvbOutlier for the
  * matched keypoints (others untouched). inv_sigma2 is a host array of nlevels
- * (<= 16) floats. kp_stride <= 8192. */
+ * (<= 16) floats. kp_stride <= 8192. d_nedges (nInitialCorrespondences) and
+ * d_iterations may be NULL. */
 int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keypoint* d_kps, const int32_t* d_nkps,
                            int kp_stride, const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
                            const float* inv_sigma2, int nlevels, float fx, float fy, float cx, float cy,
-                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, void* stream);
+                           uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, int32_t* d_nedges,
+                           void* stream);
+
+/* ------------------------------------------------ tracking glue (device)
+ * Per-frame bookkeeping of Tracking between the stages above, so a front-end
+ * step stays on the device. One workgroup per frame.
+ * gf_motion_predict_dev: Tcw = velocity * Tcw_last (Tracking.cc:1511).
+ * gf_discard_outliers_dev: kp2mp = -1, outlier = 0 for flagged matches
+ *   (Tracking.cc:1550-1563); nmatches = remaining, num_to_match = budget -
+ *   nmatches (Tracking.cc:3228). Either output may be NULL.
+ * gf_matched_gather_dev: keypoint-ordered compaction of the matched points:
+ *   pos (map position), sigma2 (level sigma^2 of the octave), idx (keypoint),
+ *   n per frame; the FRAME_INFO_MATRIX input (Observability.cc:386-520).
+ * gf_views_exclude_matched_dev: views[kp2mp].in_view = 0, i.e.
+ *   mbTrackInView = false for points already matched (Tracking.cc:3205). */
+int gf_motion_predict_dev(gf_ctx* ctx, int nframes, const float* d_velocity, const float* d_Tcw_last, float* d_Tcw,
+                          void* stream);
+int gf_discard_outliers_dev(gf_ctx* ctx, int nframes, int32_t* d_kp2mp, uint8_t* d_outlier, const int32_t* d_nkps,
+                            int kp_stride, int budget, int32_t* d_nmatches, int32_t* d_num_to_match, void* stream);
+int gf_matched_gather_dev(gf_ctx* ctx, int nframes, const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride,
+                          const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
+                          const float* level_sigma2, int nlevels, float* d_pos, float* d_sigma2, int32_t* d_idx,
+                          int32_t* d_n, void* stream);
+int gf_views_exclude_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
+                                 int kp_stride, gf_mp_view* d_views, const int32_t* d_nmp, int mp_stride,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

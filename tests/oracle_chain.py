@@ -1,0 +1,101 @@
+"""One front-end step of the reference path on the CPU oracle (test
+infrastructure: bench.py's cpu_baseline and the pipeline tests only).
+
+Mirrors pipeline.FrontEnd.step stage by stage for a single stream:
+extract -> motion model -> SearchByProjection(last frame) -> PoseOptimization
+-> discard outliers -> updatePWLSVec -> FRAME_INFO_MATRIX -> mCurrentInfoMat
+-> isInFrustum -> MAP_INFO_MATRIX -> runActiveMapMatching -> PoseOptimization
+-> discard outliers.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle_lib as O
+from gf_orb_slam_amd import synth
+from gf_orb_slam_amd.matcher import FrameInfo
+from gf_orb_slam_amd.observability import ObsCamera
+from gf_orb_slam_amd.optimizer import inv_level_sigma2
+from gf_orb_slam_amd.pipeline import build_local_map
+
+
+class Prepared:
+    pass
+
+
+def prepare(camera: str, nfeat: int, img: np.ndarray, seed: int, map_size: int = 2000, last_matches: int = 60,
+            rot_deg: float = 0.3, trans: float = 0.01, fps: float = 20.0) -> Prepared:
+    """Same set-up as FrontEnd.build_maps for one stream (camera at identity)."""
+    P = Prepared()
+    P.cam = synth.CAMERAS[camera]
+    w, h, fx, fy, cx, cy = P.cam
+    P.nfeat, P.img, P.fps = nfeat, img, fps
+    P.info = FrameInfo.make(*P.cam)
+    P.obs_cam = ObsCamera.from_intrinsics(fx, fy, cx, cy, w, h, bound=int(0.1 * w))
+    P.inv_sigma2 = inv_level_sigma2()
+    sf = P.info.scale_factors()
+    P.level_sigma2 = (sf * sf).astype(np.float32)
+    rng = np.random.default_rng(seed)
+    k, d = O.extract(img, nfeatures=nfeat)
+    P.mps, P.mdesc, assoc = build_local_map(k, d, P.cam, rng, map_size, return_assoc=True)
+    cand = np.nonzero(assoc >= 0)[0]
+    keep = np.sort(rng.choice(cand, min(last_matches, len(cand)), replace=False))
+    P.last_kps, P.last_desc = k, d
+    P.last_kp2mp = np.full(len(k), -1, np.int32)
+    P.last_kp2mp[keep] = assoc[keep]
+    P.last_pos = np.zeros((len(k), 3), np.float32)
+    P.last_pos[keep] = P.mps["pos"][assoc[keep]]
+    P.V = synth.look_pose(rng, trans, rot_deg)
+    P.Tlast = np.eye(4, dtype=np.float32)
+    P.seed = seed
+    return P
+
+
+def _pose(P, T0, kps, kp2mp):
+    idx = np.nonzero(kp2mp >= 0)[0]
+    X = P.mps["pos"][kp2mp[idx]]
+    z = np.c_[kps["x"][idx], kps["y"][idx]]
+    T, outl, ninl, iters = O.pose_opt(T0, X, z, kps["octave"][idx].astype(np.int32), P.inv_sigma2, *P.cam[2:])
+    kp2mp[idx[outl == 1]] = -1  # Tracking.cc:1550-1563
+    return T, ninl, iters
+
+
+def _matmul_f32(A, B):
+    out = np.zeros((4, 4), np.float32)
+    for i in range(4):
+        for j in range(4):
+            s = np.float32(A[i, 0] * B[0, j])
+            for k in range(1, 4):
+                s = np.float32(s + np.float32(A[i, k] * B[k, j]))
+            out[i, j] = s
+    return out
+
+
+def step(P: Prepared, budget: int = 100) -> dict:
+    kps, desc = O.extract(P.img, nfeatures=P.nfeat)
+    n = len(kps)
+    T = _matmul_f32(P.V, P.Tlast)
+    kp2mp = np.full(n, -1, np.int32)
+    score = np.full(n, 999, np.int32)
+    O.match_lastframe(P.info, kps, desc, T, P.last_kps, P.last_desc, P.last_kp2mp.copy(),
+                      np.zeros(len(P.last_kps), np.uint8), P.last_pos, 15.0, 1, kp2mp, score)
+    T, _, it1 = _pose(P, T, kps, kp2mp)
+    nmatch = int((kp2mp >= 0).sum())
+    Twc = np.eye(4, dtype=np.float32)
+    Twc[:3, :3] = T[:3, :3].T
+    Twc[:3, 3] = ((-T[0, :3] * T[0, 3]) + (-T[1, :3] * T[1, 3])) + (-T[2, :3] * T[2, 3])
+    xv = O.obs_update(0.0, P.Tlast, 1.0 / P.fps, Twc)
+    idx = np.nonzero(kp2mp >= 0)[0]
+    _, finfo, _, fvalid = O.obs_build_info(P.obs_cam, xv, P.mps["pos"][kp2mp[idx]],
+                                           P.level_sigma2[kps["octave"][idx]], 0)
+    base = np.eye(7).reshape(-1) * 1e-5
+    for j in range(len(idx)):
+        if fvalid[j]:
+            base = base + finfo[j]
+    views, _ = O.frustum(P.info, T, P.mps)
+    views["in_view"][kp2mp[idx]] = 0
+    H2, info2, uv2, valid2 = O.obs_build_info(P.obs_cam, xv, P.mps["pos"], None, 0)
+    nact, _ = O.active_match(P.info, kps, desc, views, P.mdesc, valid2, info2, H2, uv2, base, P.level_sigma2,
+                             budget - nmatch, 1.0, 0.8, P.seed, kp2mp, score)
+    T, ninl, it2 = _pose(P, T, kps, kp2mp)
+    return {"Tcw": T, "kp2mp": kp2mp, "ninliers": ninl, "iterations": (it1, it2), "n_active": nact}

@@ -160,7 +160,8 @@ def test_pose_opt_frames_dev_matches_oracle():
     ctx = default_context()
     check(lib().gf_pose_opt_frames_dev(ctx.handle, F, ptr(dT), ptr(dK), ptr(dNK), kp_stride, ptr(dKM), ptr(dM),
                                        map_stride, ptr(invs), len(invs), ctypes.c_float(fx), ctypes.c_float(fy),
-                                       ctypes.c_float(cx), ctypes.c_float(cy), ptr(dO), ptr(dI), None, ctx.stream))
+                                       ctypes.c_float(cx), ctypes.c_float(cy), ptr(dO), ptr(dI), None, None,
+                                       ctx.stream))
     check(lib().gf_ctx_sync(ctx.handle))
     Tg, og, ng = dT.cpu().numpy(), dO.cpu().numpy().reshape(F, kp_stride), dI.cpu().numpy()
     for f, (T0, ordered, kp_idx, _c) in enumerate(probs):
