@@ -96,7 +96,10 @@ _PROTOS = {
     "gf_maxvol_select_dev": [_P, _I, _P, _P, _P, _I, _I, _D, _I, _P, _P, _P, _P],
     "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
                                _P, _P],
-    "gf_obs_update_dev": [_P, _I, _P, _P, _P, _P, _P, _P],
+    "gf_obs_update_dev": [_P, _I, _P, _P, _P, _P, _P, _P, _P],
+    "gf_obs_frame_info_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P],
+    "gf_obs_map_info_dev": [_P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P],
+    "gf_obs_accumulate_matched_dev": [_P, _I, _P, _P, _I, _P, _P, _P, _I, _I, _D, _P, _P],
     "gf_motion_predict_dev": [_P, _I, _P, _P, _P, _P],
     "gf_discard_outliers_dev": [_P, _I, _P, _P, _P, _I, _I, _P, _P, _P],
     "gf_matched_gather_dev": [_P, _I, _P, _P, _I, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P],

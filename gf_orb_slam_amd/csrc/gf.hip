@@ -954,23 +954,181 @@ int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n
 namespace {
 __global__ void k_obs_update(int nframes, const double* __restrict__ t_prev, const float* __restrict__ Tcw_prev,
                              const double* __restrict__ t_cur, const float* __restrict__ Tcw_cur,
-                             double* __restrict__ Xv) {
+                             double* __restrict__ Xv, double* __restrict__ Xv_next) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
     float Twc[16];
     gfkine::get_Twc(Tcw_cur + 16 * f, Twc);
     gfkine::obs_update(t_prev[f], Tcw_prev + 16 * f, t_cur[f], Twc, Xv + 13 * f);
+    if (Xv_next) {  // predictPWLSVec(dt, 2): kinematic[1].Xv = propagate_PWLS(Xv, float(dt))
+        const double dt = (double)(float)(t_cur[f] - t_prev[f]);
+        gfkine::propagate_state(Xv + 13 * f, dt, Xv_next + 13 * f);
+    }
 }
 }  // namespace
 
 extern "C" int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev,
-                                 const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, void* stream) {
+                                 const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, double* d_Xv_next,
+                                 void* stream) {
     GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
     if (nframes <= 0) return GF_OK;
     GF_CHECK(d_t_prev && d_Tcw_prev && d_t_cur && d_Tcw_cur && d_Xv, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_update");
-    k_obs_update<<<(nframes + 63) / 64, 64, 0, s>>>(nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv);
+    k_obs_update<<<(nframes + 63) / 64, 64, 0, s>>>(nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv,
+                                                    d_Xv_next);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Map-resident observability state (MapPoint::ObsMat / H_meas / u_proj /
+// updateAtFrameId, MapPoint.h) and the three per-frame passes over it.
+namespace {
+
+struct LevelTab {
+    float v[16];
+};
+
+// batchInfoMat_Frame (Observability.cc:386-554): every matched, non-outlier
+// keypoint writes H/ObsMat/u_proj of its map point with the keypoint level
+// sigma^2 (WITH_OCT_LEVELED_NOISE); updateAtFrameId is left alone (:498-503).
+__global__ void k_obs_frame_info(gf_obs_camera cam, const double* __restrict__ Xv, const gf_keypoint* __restrict__ kps,
+                                 const int32_t* __restrict__ nkps, int kp_stride, const int32_t* __restrict__ kp2mp,
+                                 const uint8_t* __restrict__ outl, const float* __restrict__ mpos,
+                                 const int32_t* __restrict__ nmp, int map_stride, LevelTab sig, int nlevels,
+                                 double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkps[f]) return;
+    const long long k = (long long)f * kp_stride + i;
+    const int mp = kp2mp[k];
+    if (mp < 0 || mp >= nmp[f] || (outl && outl[k])) return;
+    const long long g = (long long)f * map_stride + mp;
+    const double y[3] = {mpos[3 * g], mpos[3 * g + 1], mpos[3 * g + 2]};
+    double H[14];
+    float p[2];
+    landmark_jacobian(cam, Xv + 13 * f, y, false, H, p);
+    const int oc = min(max(kps[k].octave, 0), nlevels - 1);
+    double M[49];
+    for (int e = 0; e < 49; e++) M[e] = 0;
+    add_info_block(H, (double)sig.v[oc], M);
+    uv[2 * g] = p[0];
+    uv[2 * g + 1] = p[1];
+    for (int e = 0; e < 14; e++) Hout[14 * g + e] = H[e];
+    for (int e = 0; e < 49; e++) info[49 * g + e] = M[e];
+}
+
+// batchInfoMat_Map (Observability.cc:556-644): skip points already updated
+// for this frame id, and (check_viz == false) points not mbTrackInView; on a
+// visible point write H/ObsMat/u_proj and updateAtFrameId = frame_id.
+// updated_out (optional) = (updateAtFrameId == frame_id) afterwards.
+__global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv, const float* __restrict__ mpos,
+                               const int32_t* __restrict__ nmp, int map_stride, int check_viz,
+                               const gf_mp_view* __restrict__ views, int32_t* __restrict__ upd_id, int frame_id,
+                               double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
+                               uint8_t* __restrict__ updated_out) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= map_stride) return;
+    const long long g = (long long)f * map_stride + i;
+    if (i >= nmp[f]) {
+        if (updated_out) updated_out[g] = 0;
+        return;
+    }
+    int u = upd_id[g];
+    const bool skip = (u == frame_id) || (!check_viz && views && !views[g].in_view);
+    if (!skip) {
+        const double y[3] = {mpos[3 * g], mpos[3 * g + 1], mpos[3 * g + 2]};
+        double H[14];
+        float p[2];
+        if (landmark_jacobian(cam, Xv + 13 * f, y, check_viz != 0, H, p)) {
+            double M[49];
+            for (int e = 0; e < 49; e++) M[e] = 0;
+            add_info_block(H, 1.0, M);
+            uv[2 * g] = p[0];
+            uv[2 * g + 1] = p[1];
+            for (int e = 0; e < 14; e++) Hout[14 * g + e] = H[e];
+            for (int e = 0; e < 49; e++) info[49 * g + e] = M[e];
+            u = frame_id;
+            upd_id[g] = u;
+        }
+    }
+    if (updated_out) updated_out[g] = (u == frame_id);
+}
+
+// mCurrentInfoMat = diag*I + sum over matched points (keypoint order) with
+// updateAtFrameId == frame_id of their ObsMat (Tracking.cc:3184, 3195-3213).
+__global__ void k_obs_accumulate_matched(const int32_t* __restrict__ kp2mp, const int32_t* __restrict__ nkps,
+                                         int kp_stride, const double* __restrict__ info,
+                                         const int32_t* __restrict__ upd_id, const int32_t* __restrict__ nmp,
+                                         int map_stride, int frame_id, double diag, double* __restrict__ out) {
+    const int f = blockIdx.x;
+    const int e = threadIdx.x;
+    if (e >= 49) return;
+    double s = (e % 8 == 0) ? diag : 0.0;
+    const int n = nkps[f], m = nmp[f];
+    for (int i = 0; i < n; i++) {
+        const int mp = kp2mp[(long long)f * kp_stride + i];
+        if (mp < 0 || mp >= m) continue;
+        const long long g = (long long)f * map_stride + mp;
+        if (upd_id[g] == frame_id) s = s + info[49 * g + e];
+    }
+    out[49LL * f + e] = s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gf_obs_frame_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv,
+                          const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
+                          const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
+                          const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
+                          void* stream) {
+    GF_CHECK(ctx && cam && level_sigma2, GF_ERR_ARG, "null arg");
+    if (nframes <= 0 || kp_stride <= 0) return GF_OK;
+    GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
+    GF_CHECK(d_Xv && d_kps && d_nkps && d_kp2mp && d_map_pos && d_nmp && d_H && d_info && d_uv, GF_ERR_ARG,
+             "null arg");
+    LevelTab t{};
+    for (int i = 0; i < nlevels; i++) t.v[i] = level_sigma2[i];
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_frame_info");
+    k_obs_frame_info<<<dim3((kp_stride + 127) / 128, nframes), 128, 0, s>>>(
+        *cam, d_Xv, d_kps, d_nkps, kp_stride, d_kp2mp, d_outlier, d_map_pos, d_nmp, map_stride, t, nlevels, d_H,
+        d_info, d_uv);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_obs_map_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
+                        const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
+                        int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv,
+                        uint8_t* d_updated, void* stream) {
+    GF_CHECK(ctx && cam, GF_ERR_ARG, "null arg");
+    if (nframes <= 0 || map_stride <= 0) return GF_OK;
+    GF_CHECK(d_Xv && d_map_pos && d_nmp && d_upd_id && d_H && d_info && d_uv, GF_ERR_ARG, "null arg");
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_map_info");
+    k_obs_map_info<<<dim3((map_stride + 127) / 128, nframes), 128, 0, s>>>(
+        *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
+                                  int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
+                                  int map_stride, int frame_id, double diag, double* d_out, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (nframes <= 0) return GF_OK;
+    GF_CHECK(d_kp2mp && d_nkps && d_info && d_upd_id && d_nmp && d_out, GF_ERR_ARG, "null arg");
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_obs_accumulate");
+    k_obs_accumulate_matched<<<nframes, 64, 0, s>>>(d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
+                                                    frame_id, diag, d_out);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+}  // extern "C"

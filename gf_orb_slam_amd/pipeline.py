@@ -139,21 +139,17 @@ class FrontEnd:
         self.nmp = torch.full((B,), M, dtype=i32, device=dev)
         self.views = z(B, M, MP_VIEW_DTYPE.itemsize)
         self.nview = z(B, dt=i32)
-        # good-feature state
+        # good-feature state: Xv of kinematic[0] / [1], mCurrentInfoMat, and the
+        # map-resident MapPoint::H_meas / ObsMat / u_proj / updateAtFrameId
         self.Xv = z(B, 13, dt=f64)
+        self.Xv_next = z(B, 13, dt=f64)
         self.base = z(B, 49, dt=f64)
-        self.m_pos = z(B, cap, 3, dt=f32)
-        self.m_sig = z(B, cap, dt=f32)
-        self.m_idx = z(B, cap, dt=i32)
-        self.m_n = z(B, dt=i32)
-        self.f_H = z(B, cap, 14, dt=f64)
-        self.f_info = z(B, cap, 49, dt=f64)
-        self.f_uv = z(B, cap, 2, dt=f32)
-        self.f_valid = z(B, cap)
         self.mp_H = z(B, M, 14, dt=f64)
         self.mp_info = z(B, M, 49, dt=f64)
         self.mp_uv = z(B, M, 2, dt=f32)
-        self.mp_valid = z(B, M)
+        self.mp_upd = torch.full((B, M), -1, dtype=i32, device=dev)
+        self.mp_updated = z(B, M)
+        self.frame_id = 1
         self.rng = z(B, ctypes.sizeof(Rng), dt=u8)
         self.left = z(B, M, dt=i32)
         self.nleft = z(B, dt=i32)
@@ -256,17 +252,18 @@ class FrontEnd:
                                             self._s))
 
     def frame_info(self) -> None:
-        """G1 + FRAME_INFO_MATRIX over the matched points + mCurrentInfoMat."""
+        """SearchReferencePointsInFrustum head (Tracking.cc:3160-3213): G1 at the
+        motion-model pose, FRAME_INFO_MATRIX over the matched points and
+        mCurrentInfoMat from the ones stamped for this frame."""
         check(lib().gf_obs_update_dev(self._h, self.B, ptr(self.t_prev), ptr(self.Tcw_last), ptr(self.t_cur),
-                                      ptr(self.Tcw), ptr(self.Xv), self._s))
-        check(lib().gf_matched_gather_dev(self._h, self.B, ptr(self.kps), ptr(self.nkp), self.cap, ptr(self.kp2mp),
-                                          ptr(self.mps), self.M, ptr(self.level_sigma2), len(self.level_sigma2),
-                                          ptr(self.m_pos), ptr(self.m_sig), ptr(self.m_idx), ptr(self.m_n), self._s))
-        check(lib().gf_obs_build_info_dev(self._h, ctypes.byref(self.obs_cam), self.B, ptr(self.Xv), ptr(self.m_pos),
-                                          ptr(self.m_sig), ptr(self.m_n), self.cap, 0, ptr(self.f_H),
-                                          ptr(self.f_info), ptr(self.f_uv), ptr(self.f_valid), self._s))
-        check(lib().gf_obs_accumulate_dev(self._h, self.B, ptr(self.f_info), ptr(self.f_valid), ptr(self.m_n),
-                                          self.cap, ctypes.c_double(1e-5), ptr(self.base), self._s))
+                                      ptr(self.Tcw), ptr(self.Xv), None, self._s))
+        check(lib().gf_obs_frame_info_dev(self._h, ctypes.byref(self.obs_cam), self.B, ptr(self.Xv), ptr(self.kps),
+                                          ptr(self.nkp), self.cap, ptr(self.kp2mp), ptr(self.outl), ptr(self.mp_pos),
+                                          ptr(self.nmp), self.M, ptr(self.level_sigma2), len(self.level_sigma2),
+                                          ptr(self.mp_H), ptr(self.mp_info), ptr(self.mp_uv), self._s))
+        check(lib().gf_obs_accumulate_matched_dev(self._h, self.B, ptr(self.kp2mp), ptr(self.nkp), self.cap,
+                                                  ptr(self.mp_info), ptr(self.mp_upd), ptr(self.nmp), self.M,
+                                                  self.frame_id, ctypes.c_double(1e-5), ptr(self.base), self._s))
 
     def frustum(self) -> None:
         check(lib().gf_frustum_dev(self._h, ctypes.byref(self.info), self.B, ptr(self.Tcw), ptr(self.mps),
@@ -276,14 +273,28 @@ class FrontEnd:
                                                  ptr(self.views), ptr(self.nmp), self.M, self._s))
 
     def map_info(self) -> None:
-        check(lib().gf_obs_build_info_dev(self._h, ctypes.byref(self.obs_cam), self.B, ptr(self.Xv), ptr(self.mp_pos),
-                                          None, ptr(self.nmp), self.M, 0, ptr(self.mp_H), ptr(self.mp_info),
-                                          ptr(self.mp_uv), ptr(self.mp_valid), self._s))
+        """MAP_INFO_MATRIX for the visible points not yet stamped this frame."""
+        check(lib().gf_obs_map_info_dev(self._h, ctypes.byref(self.obs_cam), self.B, ptr(self.Xv), ptr(self.mp_pos),
+                                        ptr(self.nmp), self.M, 0, ptr(self.views), ptr(self.mp_upd), self.frame_id,
+                                        ptr(self.mp_H), ptr(self.mp_info), ptr(self.mp_uv), ptr(self.mp_updated),
+                                        self._s))
+
+    def predict_next(self) -> None:
+        """After TrackLocalMap: updatePWLSVec at the final pose, predict 2
+        segments (Tracking.cc:795-800) and build the map information for the
+        next frame at kinematic[1] with the visibility check
+        (RunMapPointsSelection, Tracking.cc:1717-1772)."""
+        check(lib().gf_obs_update_dev(self._h, self.B, ptr(self.t_prev), ptr(self.Tcw_last), ptr(self.t_cur),
+                                      ptr(self.Tcw), ptr(self.Xv), ptr(self.Xv_next), self._s))
+        check(lib().gf_obs_map_info_dev(self._h, ctypes.byref(self.obs_cam), self.B, ptr(self.Xv_next),
+                                        ptr(self.mp_pos), ptr(self.nmp), self.M, 1, None, ptr(self.mp_upd),
+                                        self.frame_id + 1, ptr(self.mp_H), ptr(self.mp_info), ptr(self.mp_uv), None,
+                                        self._s))
 
     def active_match(self, th: float = 1.0, nnratio: float = 0.8) -> None:
         check(lib().gf_obs_active_match_dev(self._h, ctypes.byref(self.info), self.B, ptr(self.kps), ptr(self.desc),
                                             ptr(self.nkp), self.cap, ptr(self.views), ptr(self.mp_desc),
-                                            ptr(self.mp_valid), ptr(self.mp_info), ptr(self.mp_H), ptr(self.nmp),
+                                            ptr(self.mp_updated), ptr(self.mp_info), ptr(self.mp_H), ptr(self.nmp),
                                             self.M, ptr(self.base), ptr(self.level_sigma2), ptr(self.num_to_match),
                                             ctypes.c_float(th), ctypes.c_float(nnratio), ptr(self.rng),
                                             ptr(self.kp2mp), ptr(self.score), ptr(self.left), ptr(self.nleft),
@@ -305,7 +316,7 @@ class FrontEnd:
             self.match_last_frame()
             self.pose_optimization(0)
             self.discard_outliers()
-            # TrackLocalMap
+            # TrackLocalMap -> SearchReferencePointsInFrustum
             if self.gf:
                 self.frame_info()
             self.frustum()
@@ -316,6 +327,15 @@ class FrontEnd:
                 self.match_local_map()
             self.pose_optimization(1)
             self.discard_outliers()
+            if self.gf:
+                self.predict_next()
+        self.frame_id += 1
+
+    def reset_state(self) -> None:
+        """Back to the state right after build_maps (RNG, map stamps, frame id)."""
+        self.rng.copy_(self.rng0)
+        self.mp_upd.fill_(-1)
+        self.frame_id = 1
 
     def sync(self) -> None:
         self.stream.synchronize()

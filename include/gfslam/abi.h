@@ -287,10 +287,39 @@ int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const do
                          int32_t* d_nout, void* stream);
 
 /* G1 on the device: Xv[f] = updatePWLSVec(t_prev[f], Tcw_prev[f], t_cur[f],
- * getTwc(Tcw_cur[f])) (Tracking.cc:3168-3169, Frame.cc:152-163). Segment 0 of
- * predictPWLSVec keeps this Xv, which is what the FRAME/MAP info builds use. */
+ * getTwc(Tcw_cur[f])) (Tracking.cc:3168-3169, :797-799, Frame.cc:152-163).
+ * Segment 0 of predictPWLSVec keeps this Xv (the in-frame FRAME/MAP builds);
+ * d_Xv_next (optional) = kinematic[1].Xv = propagate_PWLS(Xv, float(dt)), the
+ * state the next-frame MAP build uses (Tracking.cc:1768, mKineIdx = 1). */
 int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev,
-                      const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, void* stream);
+                      const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, double* d_Xv_next,
+                      void* stream);
+
+/* Map-resident observability state, map-indexed per frame (stride
+ * map_stride): H [14], ObsMat [49], u/v_proj [2], updateAtFrameId (int32).
+ * gf_obs_frame_info_dev = batchInfoMat_Frame (Observability.cc:386-554):
+ *   matched non-outlier keypoints write their map point's H/ObsMat/uv with
+ *   the keypoint level sigma^2; updateAtFrameId untouched.
+ * gf_obs_map_info_dev = batchInfoMat_Map (Observability.cc:556-644): points
+ *   with updateAtFrameId == frame_id are skipped, and with check_viz == 0 so
+ *   are points whose view is not in_view (d_views may be NULL only with
+ *   check_viz); a valid point is written and stamped frame_id. d_updated
+ *   (optional) = (updateAtFrameId == frame_id) for every point afterwards.
+ * gf_obs_accumulate_matched_dev: mCurrentInfoMat = diag*I + sum, in keypoint
+ *   order, of the ObsMat of matched points stamped frame_id (Tracking.cc:3184,
+ *   3195-3213). */
+int gf_obs_frame_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv,
+                          const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
+                          const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
+                          const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
+                          void* stream);
+int gf_obs_map_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
+                        const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
+                        int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv,
+                        uint8_t* d_updated, void* stream);
+int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
+                                  int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
+                                  int map_stride, int frame_id, double diag, double* d_out, void* stream);
 
 /* ------------------------------------------------ pose optimisation (P1-P4)
  * Optimizer::PoseOptimization(Frame*) (src/Optimizer.cc:279-413) on g2o's

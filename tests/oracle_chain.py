@@ -5,7 +5,11 @@ Mirrors pipeline.FrontEnd.step stage by stage for a single stream:
 extract -> motion model -> SearchByProjection(last frame) -> PoseOptimization
 -> discard outliers -> updatePWLSVec -> FRAME_INFO_MATRIX -> mCurrentInfoMat
 -> isInFrustum -> MAP_INFO_MATRIX -> runActiveMapMatching -> PoseOptimization
--> discard outliers.
+-> discard outliers -> updatePWLSVec + 2-segment prediction -> next-frame
+MAP_INFO_MATRIX (check_viz) stamped frame_id + 1.
+
+The map-resident observability state (MapPoint::ObsMat, H_meas, u/v_proj,
+updateAtFrameId) lives in a MapState and carries over between steps.
 """
 from __future__ import annotations
 
@@ -21,6 +25,59 @@ from gf_orb_slam_amd.pipeline import build_local_map
 
 class Prepared:
     pass
+
+
+class MapState:
+    """MapPoint::H_meas / ObsMat / u,v_proj / updateAtFrameId for M points."""
+
+    def __init__(self, m: int):
+        self.H = np.zeros((m, 14))
+        self.info = np.zeros((m, 49))
+        self.uv = np.zeros((m, 2), np.float32)
+        self.upd = np.full(m, -1, np.int64)
+
+    def copy(self):
+        c = MapState(len(self.upd))
+        c.H, c.info, c.uv, c.upd = self.H.copy(), self.info.copy(), self.uv.copy(), self.upd.copy()
+        return c
+
+
+def frame_info_stage(P, xv, kps, kp2mp, outl, st: MapState) -> None:
+    """batchInfoMat_Frame (Observability.cc:386-554) over the matched keypoints."""
+    idx = np.nonzero((kp2mp >= 0) & (outl == 0))[0]
+    if len(idx) == 0:
+        return
+    mp = kp2mp[idx]
+    H, info, uv, _ = O.obs_build_info(P.obs_cam, xv, P.mps["pos"][mp], P.level_sigma2[kps["octave"][idx]], 0)
+    st.H[mp], st.info[mp], st.uv[mp] = H, info, uv  # later keypoints win, as the sequential loop
+
+
+def accumulate_stage(kp2mp, st: MapState, fid: int, diag: float = 1e-5) -> np.ndarray:
+    """mCurrentInfoMat (Tracking.cc:3184, 3195-3213)."""
+    acc = np.eye(7).reshape(-1) * diag
+    for mp in kp2mp:
+        if mp >= 0 and st.upd[mp] == fid:
+            acc = acc + st.info[mp]
+    return acc
+
+
+def map_info_stage(P, xv, views, check_viz: int, st: MapState, fid: int) -> np.ndarray:
+    """batchInfoMat_Map (Observability.cc:556-644); returns updateAtFrameId == fid."""
+    H, info, uv, valid = O.obs_build_info(P.obs_cam, xv, P.mps["pos"], None, check_viz)
+    sel = (st.upd != fid) & (valid != 0)
+    if not check_viz:
+        sel &= views["in_view"] != 0
+    st.H[sel], st.info[sel], st.uv[sel] = H[sel], info[sel], uv[sel]
+    st.upd[sel] = fid
+    return (st.upd == fid).astype(np.uint8)
+
+
+def twc_of(T: np.ndarray) -> np.ndarray:
+    """Frame::getTwc (Frame.cc:152-163) in float."""
+    Twc = np.eye(4, dtype=np.float32)
+    Twc[:3, :3] = T[:3, :3].T
+    Twc[:3, 3] = ((-T[0, :3] * T[0, 3]) + (-T[1, :3] * T[1, 3])) + (-T[2, :3] * T[2, 3])
+    return Twc
 
 
 def prepare(camera: str, nfeat: int, img: np.ndarray, seed: int, map_size: int = 2000, last_matches: int = 60,
@@ -48,6 +105,8 @@ def prepare(camera: str, nfeat: int, img: np.ndarray, seed: int, map_size: int =
     P.V = synth.look_pose(rng, trans, rot_deg)
     P.Tlast = np.eye(4, dtype=np.float32)
     P.seed = seed
+    P.state = MapState(map_size)
+    P.fid = 1
     return P
 
 
@@ -81,21 +140,19 @@ def step(P: Prepared, budget: int = 100) -> dict:
                       np.zeros(len(P.last_kps), np.uint8), P.last_pos, 15.0, 1, kp2mp, score)
     T, _, it1 = _pose(P, T, kps, kp2mp)
     nmatch = int((kp2mp >= 0).sum())
-    Twc = np.eye(4, dtype=np.float32)
-    Twc[:3, :3] = T[:3, :3].T
-    Twc[:3, 3] = ((-T[0, :3] * T[0, 3]) + (-T[1, :3] * T[1, 3])) + (-T[2, :3] * T[2, 3])
-    xv = O.obs_update(0.0, P.Tlast, 1.0 / P.fps, Twc)
-    idx = np.nonzero(kp2mp >= 0)[0]
-    _, finfo, _, fvalid = O.obs_build_info(P.obs_cam, xv, P.mps["pos"][kp2mp[idx]],
-                                           P.level_sigma2[kps["octave"][idx]], 0)
-    base = np.eye(7).reshape(-1) * 1e-5
-    for j in range(len(idx)):
-        if fvalid[j]:
-            base = base + finfo[j]
+    st, fid, dt = P.state, P.fid, 1.0 / P.fps
+    xv = O.obs_update(0.0, P.Tlast, dt, twc_of(T))
+    outl = np.zeros(n, np.uint8)
+    frame_info_stage(P, xv, kps, kp2mp, outl, st)
+    base = accumulate_stage(kp2mp, st, fid)
     views, _ = O.frustum(P.info, T, P.mps)
-    views["in_view"][kp2mp[idx]] = 0
-    H2, info2, uv2, valid2 = O.obs_build_info(P.obs_cam, xv, P.mps["pos"], None, 0)
-    nact, _ = O.active_match(P.info, kps, desc, views, P.mdesc, valid2, info2, H2, uv2, base, P.level_sigma2,
-                             budget - nmatch, 1.0, 0.8, P.seed, kp2mp, score)
+    views["in_view"][kp2mp[kp2mp >= 0]] = 0
+    updated = map_info_stage(P, xv, views, 0, st, fid)
+    nact, _ = O.active_match(P.info, kps, desc, views, P.mdesc, updated, st.info, st.H, st.uv, base,
+                             P.level_sigma2, budget - nmatch, 1.0, 0.8, P.seed, kp2mp, score)
     T, ninl, it2 = _pose(P, T, kps, kp2mp)
+    xv = O.obs_update(0.0, P.Tlast, dt, twc_of(T))
+    xv1 = np.array(O.obs_predict(xv, dt, 2)[1].Xv)
+    map_info_stage(P, xv1, None, 1, st, fid + 1)
+    P.fid += 1
     return {"Tcw": T, "kp2mp": kp2mp, "ninliers": ninl, "iterations": (it1, it2), "n_active": nact}

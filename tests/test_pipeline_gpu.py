@@ -1,38 +1,64 @@
 """The composed device front end (pipeline.FrontEnd) against the oracle chain.
 
-Each stage of one step is run on the device for B streams, its inputs and
-outputs are snapshotted, and the oracle runs the same stage on the same
-inputs: keypoint/match indices and information blocks bit-exact, poses within
-1e-5 relative (north_star), the active-matching claims and RNG-driven pool
-identical. This is what makes the bench step a valid measurement of the
-reference path rather than of a look-alike.
+After one warm-up step (so the map carries observability state stamped by the
+previous frame's prediction pass), every stage of the next step runs on the
+device for B streams; its inputs and outputs are snapshotted and the oracle
+runs the same stage on the same inputs (tests/oracle_chain.py): keypoint and
+match indices, information blocks and frame stamps bit-exact, poses within
+1e-5 relative (north_star), active-matching claims identical. This is what
+makes the bench step a measurement of the reference path and not of a
+look-alike.
 """
-import ctypes
-
 import numpy as np
 import pytest
 
+import oracle_chain as C
 import oracle_lib as O
 from gf_orb_slam_amd import synth
 from gf_orb_slam_amd.matcher import MAP_POINT_DTYPE, MP_VIEW_DTYPE
 from gf_orb_slam_amd.orb import KEYPOINT_DTYPE
 
-pytestmark = pytest.mark.gpu
 B = 3
+
+
+def _np(t):
+    return t.cpu().numpy().copy()
 
 
 def _kp(t, b, n):
     return t[b].cpu().numpy().view(KEYPOINT_DTYPE).reshape(-1)[:n].copy()
 
 
-def _pose_edges(kps, kp2mp, mps, invs):
-    idx = np.nonzero(kp2mp >= 0)[0]
-    return idx, mps["pos"][kp2mp[idx]], np.c_[kps["x"][idx], kps["y"][idx]], invs[kps["octave"][idx]]
+class _P:  # the oracle_chain.Prepared fields the stage helpers read
+    pass
 
 
-def _check_pose(fe, b, T0, kps, kp2mp_before, mps, Tg, outl_g, ninl_g):
-    idx, X, z, invs = _pose_edges(kps, kp2mp_before, mps, fe.inv_sigma2)
-    To, oo, no, _ = O.pose_opt(T0, X, z, np.arange(len(idx), dtype=np.int32), invs, *fe.cam[2:])
+def _prep(fe, mps_b):
+    P = _P()
+    P.obs_cam, P.level_sigma2, P.mps, P.info = fe.obs_cam, fe.level_sigma2, mps_b, fe.info
+    return P
+
+
+def _state(fe, b):
+    st = C.MapState(fe.M)
+    st.H = _np(fe.mp_H[b]).reshape(-1, 14)
+    st.info = _np(fe.mp_info[b]).reshape(-1, 49)
+    st.uv = _np(fe.mp_uv[b]).reshape(-1, 2)
+    st.upd = _np(fe.mp_upd[b]).astype(np.int64)
+    return st
+
+
+def _same_state(fe, b, st):
+    assert np.array_equal(_np(fe.mp_upd[b]), st.upd)
+    assert np.array_equal(_np(fe.mp_info[b]).reshape(-1, 49), st.info)
+    assert np.array_equal(_np(fe.mp_H[b]).reshape(-1, 14), st.H)
+    assert np.array_equal(_np(fe.mp_uv[b]).reshape(-1, 2), st.uv)
+
+
+def _check_pose(fe, T0, kps, kp2mp_before, mps, Tg, outl_g, ninl_g):
+    idx = np.nonzero(kp2mp_before >= 0)[0]
+    To, oo, no, _ = O.pose_opt(T0, mps["pos"][kp2mp_before[idx]], np.c_[kps["x"][idx], kps["y"][idx]],
+                               kps["octave"][idx].astype(np.int32), fe.inv_sigma2, *fe.cam[2:])
     assert ninl_g == no
     assert np.array_equal(outl_g[idx], oo)
     assert np.all(np.abs(Tg.reshape(4, 4).astype(np.float64) - To) <= 1e-5 * np.maximum(1, np.abs(To)))
@@ -49,8 +75,16 @@ def fe():
     return fe
 
 
+@pytest.mark.gpu
 def test_pipeline_stages_match_oracle(fe):
     import torch
+
+    fe.reset_state()
+    fe.step()  # warm: leaves next-frame stamps in the map
+    fe.sync()
+    fid = fe.frame_id
+    states = [_state(fe, b) for b in range(B)]
+    assert all((s.upd == fid).sum() > 100 for s in states)  # predicted-visible points carry the stamp
 
     s = fe.stream
     with torch.cuda.stream(s):
@@ -59,14 +93,12 @@ def test_pipeline_stages_match_oracle(fe):
         fe.reset_matches()
         fe.match_last_frame()
     fe.sync()
-    nk = fe.nkp.cpu().numpy()
-    T_pred = fe.Tcw.cpu().numpy()
+    nk = _np(fe.nkp)
+    T_pred = _np(fe.Tcw)
     mps = fe.mps.cpu().numpy().view(MAP_POINT_DTYPE).reshape(B, -1)
-    mdesc = fe.mp_desc.cpu().numpy()
-    last_kp2mp = fe.last_kp2mp.cpu().numpy()
-    last_pos = fe.last_pos.cpu().numpy()
-    kp2mp_m3 = fe.kp2mp.cpu().numpy().copy()
-    score_m3 = fe.score.cpu().numpy().copy()
+    mdesc = _np(fe.mp_desc)
+    last_kp2mp, last_pos = _np(fe.last_kp2mp), _np(fe.last_pos)
+    kp2mp_m3, score_m3 = _np(fe.kp2mp), _np(fe.score)
     kps = [_kp(fe.kps, b, nk[b]) for b in range(B)]
     desc = [fe.desc[b, :nk[b]].cpu().numpy() for b in range(B)]
     for b in range(B):
@@ -82,11 +114,9 @@ def test_pipeline_stages_match_oracle(fe):
     with torch.cuda.stream(s):
         fe.pose_optimization(0)
     fe.sync()
-    T1 = fe.Tcw.cpu().numpy()
-    outl = fe.outl.cpu().numpy()
-    ninl = fe.ninl.cpu().numpy()
+    T1, outl, ninl = _np(fe.Tcw), _np(fe.outl), _np(fe.ninl)
     for b in range(B):
-        _check_pose(fe, b, T_pred[b], kps[b], kp2mp_m3[b, :nk[b]], mps[b], T1[b], outl[b, :nk[b]], ninl[b])
+        _check_pose(fe, T_pred[b], kps[b], kp2mp_m3[b, :nk[b]], mps[b], T1[b], outl[b, :nk[b]], ninl[b])
 
     with torch.cuda.stream(s):
         fe.discard_outliers()
@@ -94,93 +124,87 @@ def test_pipeline_stages_match_oracle(fe):
         fe.frustum()
         fe.map_info()
     fe.sync()
-    kp2mp_d = fe.kp2mp.cpu().numpy().copy()
-    nmatch = fe.nmatch.cpu().numpy()
-    ntm = fe.num_to_match.cpu().numpy()
-    Xv = fe.Xv.cpu().numpy()
-    base = fe.base.cpu().numpy()
-    f_info = fe.f_info.cpu().numpy()
-    m_n = fe.m_n.cpu().numpy()
+    kp2mp_d, score_d = _np(fe.kp2mp), _np(fe.score)
+    nmatch, ntm = _np(fe.nmatch), _np(fe.num_to_match)
+    Xv, base = _np(fe.Xv), _np(fe.base)
     views = fe.views.cpu().numpy().view(MP_VIEW_DTYPE).reshape(B, -1)
-    map_info = fe.mp_info.cpu().numpy()
-    map_H = fe.mp_H.cpu().numpy()
-    map_uv = fe.mp_uv.cpu().numpy()
-    map_valid = fe.mp_valid.cpu().numpy()
-    score_d = fe.score.cpu().numpy().copy()
+    updated = _np(fe.mp_updated)
     for b in range(B):
         k = kp2mp_m3[b, :nk[b]].copy()
         k[outl[b, :nk[b]] == 1] = -1
         assert np.array_equal(k, kp2mp_d[b, :nk[b]])
         assert nmatch[b] == (k >= 0).sum() and ntm[b] == fe.budget - nmatch[b]
-        # G1 on the device vs the host port
-        Twc = np.eye(4, dtype=np.float32)
         T = T1[b].reshape(4, 4)
-        Twc[:3, :3] = T[:3, :3].T
-        Twc[:3, 3] = ((-T[0, :3] * T[0, 3]) + (-T[1, :3] * T[1, 3])) + (-T[2, :3] * T[2, 3])
-        xv = O.obs_update(0.0, np.eye(4, dtype=np.float32), 1.0 / fe.fps, Twc)
+        xv = O.obs_update(0.0, np.eye(4, dtype=np.float32), 1.0 / fe.fps, C.twc_of(T))
         np.testing.assert_allclose(Xv[b], xv, rtol=1e-12, atol=1e-12)
-        # FRAME_INFO_MATRIX over the matched points, in keypoint order
-        idx = np.nonzero(k >= 0)[0]
-        assert m_n[b] == len(idx)
-        pos = mps[b]["pos"][k[idx]]
-        s2 = fe.level_sigma2[kps[b]["octave"][idx]]
-        H, info, uv, valid = O.obs_build_info(fe.obs_cam, Xv[b], pos, s2, 0)
-        assert np.array_equal(info, f_info[b, :len(idx)])
-        acc = np.eye(7).reshape(-1) * 1e-5
-        for j in range(len(idx)):
-            if valid[j]:
-                acc = acc + info[j]
-        np.testing.assert_allclose(base[b], acc, rtol=1e-12, atol=1e-15)
-        # isInFrustum + exclusion of matched points
+        P, st = _prep(fe, mps[b]), states[b]
+        C.frame_info_stage(P, Xv[b], kps[b], k, np.zeros(nk[b], np.uint8), st)
+        acc = C.accumulate_stage(k, st, fid)
+        np.testing.assert_allclose(base[b], acc, rtol=1e-13, atol=1e-18)
+        assert np.abs(acc - np.eye(7).reshape(-1) * 1e-5).max() > 0  # stamped matches contribute
         v, _ = O.frustum(fe.info, T, mps[b])
-        v["in_view"][k[idx]] = 0
+        v["in_view"][k[k >= 0]] = 0
         assert np.array_equal(v, views[b])
-        # MAP_INFO_MATRIX
-        H2, info2, uv2, valid2 = O.obs_build_info(fe.obs_cam, Xv[b], mps[b]["pos"], None, 0)
-        assert np.array_equal(info2, map_info[b]) and np.array_equal(H2, map_H[b].reshape(-1, 14))
-        assert np.array_equal(valid2, map_valid[b])
+        upd = C.map_info_stage(P, Xv[b], v, 0, st, fid)
+        assert np.array_equal(upd, updated[b])
+        _same_state(fe, b, st)
 
+    fe.rng.copy_(fe.rng0)
     with torch.cuda.stream(s):
         fe.active_match()
     fe.sync()
-    kp2mp_a = fe.kp2mp.cpu().numpy()
-    score_a = fe.score.cpu().numpy()
-    n_act = fe.n_active.cpu().numpy()
+    kp2mp_a, score_a, n_act = _np(fe.kp2mp), _np(fe.score), _np(fe.n_active)
     for b in range(B):
         k2 = kp2mp_d[b, :nk[b]].copy()
         sc = score_d[b, :nk[b]].copy()
-        seed = 1 + fe.seed * 1000 + b
-        nm, left = O.active_match(fe.info, kps[b], desc[b], views[b], mdesc[b], map_valid[b], map_info[b],
-                                  map_H[b].reshape(-1, 14), map_uv[b].reshape(-1, 2), base[b], fe.level_sigma2,
-                                  int(ntm[b]), 1.0, 0.8, seed, k2, sc)
-        assert nm == n_act[b]
+        st = states[b]
+        nm, _ = O.active_match(fe.info, kps[b], desc[b], views[b], mdesc[b], updated[b], st.info, st.H, st.uv,
+                               base[b], fe.level_sigma2, int(ntm[b]), 1.0, 0.8, 1 + fe.seed * 1000 + b, k2, sc)
+        assert nm == n_act[b] and nm > 0
         assert np.array_equal(k2, kp2mp_a[b, :nk[b]])
         assert np.array_equal(sc, score_a[b, :nk[b]])
-        assert nm > 0
 
     with torch.cuda.stream(s):
         fe.pose_optimization(1)
         fe.discard_outliers()
+        fe.predict_next()
     fe.sync()
-    T2 = fe.Tcw.cpu().numpy()
-    outl2 = fe.outl.cpu().numpy()
-    ninl2 = fe.ninl.cpu().numpy()
+    T2, outl2, ninl2 = _np(fe.Tcw), _np(fe.outl), _np(fe.ninl)
+    Xv2, Xn = _np(fe.Xv), _np(fe.Xv_next)
     for b in range(B):
-        _check_pose(fe, b, T1[b], kps[b], kp2mp_a[b, :nk[b]], mps[b], T2[b], outl2[b, :nk[b]], ninl2[b])
-        # the synthetic map was built from the identity camera: the pose is recovered
-        assert np.abs(T2[b].reshape(4, 4) - np.eye(4)).max() < 2e-2
+        _check_pose(fe, T1[b], kps[b], kp2mp_a[b, :nk[b]], mps[b], T2[b], outl2[b, :nk[b]], ninl2[b])
+        assert np.abs(T2[b].reshape(4, 4) - np.eye(4)).max() < 2e-2  # map built from the identity camera
+        xv = O.obs_update(0.0, np.eye(4, dtype=np.float32), 1.0 / fe.fps, C.twc_of(T2[b].reshape(4, 4)))
+        np.testing.assert_allclose(Xv2[b], xv, rtol=1e-12, atol=1e-12)
+        xn = np.array(O.obs_predict(Xv2[b], 1.0 / fe.fps, 2)[1].Xv)
+        np.testing.assert_allclose(Xn[b], xn, rtol=1e-12, atol=1e-13)
+        st = states[b]
+        C.map_info_stage(_prep(fe, mps[b]), Xn[b], None, 1, st, fid + 1)
+        _same_state(fe, b, st)
 
 
+@pytest.mark.gpu
 def test_pipeline_step_repeatable(fe):
-    """A full step is deterministic given the RNG state."""
-    import torch
+    """A full step is deterministic given the RNG state and the map stamps."""
+    fe.reset_state()
+    fe.step()
+    fe.step()
+    fe.sync()
+    a = (_np(fe.Tcw), _np(fe.kp2mp), _np(fe.mp_info))
+    fe.reset_state()
+    fe.step()
+    fe.step()
+    fe.sync()
+    assert np.array_equal(a[0], _np(fe.Tcw)) and np.array_equal(a[1], _np(fe.kp2mp))
+    assert np.array_equal(a[2], _np(fe.mp_info))
 
-    fe.rng.copy_(fe.rng0)
-    fe.step()
-    fe.sync()
-    a = (fe.Tcw.cpu().numpy().copy(), fe.kp2mp.cpu().numpy().copy())
-    fe.rng.copy_(fe.rng0)
-    fe.step()
-    fe.sync()
-    assert np.array_equal(a[0], fe.Tcw.cpu().numpy()) and np.array_equal(a[1], fe.kp2mp.cpu().numpy())
-    del torch
+
+def test_oracle_chain_tracks_pose():
+    """CPU chain sanity (also what bench.py times as cpu_baseline)."""
+    P = C.prepare("euroc", 1000, synth.synth_frame(752, 480, synth.frame_seed(77, 0)), 7)
+    r1 = C.step(P)
+    r2 = C.step(P)
+    for r in (r1, r2):
+        assert r["ninliers"] >= 80 and r["n_active"] > 0
+        assert np.abs(r["Tcw"] - np.eye(4)).max() < 2e-2
+    assert (P.state.upd == P.fid).sum() > 100
