@@ -11,7 +11,7 @@ HIPSRCS = $(wildcard $(CSRC)/*.hip)
 HIPOBJS = $(patsubst $(CSRC)/%.hip,build/%.o,$(HIPSRCS))
 CPPSRCS = $(wildcard $(CSRC)/*.cpp)
 CPPOBJS = $(patsubst $(CSRC)/%.cpp,build/%.cpp.o,$(CPPSRCS))
-HDRS    = $(wildcard $(CSRC)/*.h) include/gfslam/abi.h
+HDRS    = $(wildcard $(CSRC)/*.h) include/gfslam/abi.h include/gfslam/orbslam.h
 LIB     = gf_orb_slam_amd/libgfslam.so
 
 ORCSRCS = $(wildcard oracle/*.cpp)
@@ -42,3 +42,9 @@ SELCHECK = tests/helpers/libselcheck.so
 all: $(SELCHECK)
 $(SELCHECK): tests/helpers/select_check.cpp $(CSRC)/select.h
 	$(CXX) -O2 -std=c++17 -fPIC -shared $< -o $@
+
+# C++ drop-in layer driver (tests/test_dropin_gpu.py runs it on the GPU box)
+DROPIN = tests/cpp/dropin_frontend
+all: $(DROPIN)
+$(DROPIN): tests/cpp/dropin_frontend.cpp include/gfslam/orbslam.h include/gfslam/abi.h $(LIB)
+	$(CXX) -O2 -std=c++17 -Iinclude $< -Lgf_orb_slam_amd -lgfslam -Wl,-rpath,'$$ORIGIN/../../gf_orb_slam_amd' -o $@

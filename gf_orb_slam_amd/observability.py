@@ -26,8 +26,15 @@ class ObsCamera(ctypes.Structure):
                    bound_depth)
 
     @classmethod
-    def from_intrinsics(cls, fu, fv, cx, cy, ncols, nrows, bound=20, bound_depth=0.0):
-        return cls(fu, fv, cx, cy, int(nrows), int(ncols), 0, int(ncols), 0, int(nrows), bound, bound, bound_depth)
+    def from_intrinsics(cls, fu, fv, cx, cy, ncols, nrows, bound=20, bound_depth=0.0, bound_y=None):
+        by = bound if bound_y is None else bound_y
+        return cls(fu, fv, cx, cy, int(nrows), int(ncols), 0, int(ncols), 0, int(nrows), bound, by, bound_depth)
+
+    @classmethod
+    def for_tracking(cls, fu, fv, cx, cy, ncols, nrows):
+        """The margins Tracking sets: mBoundX/YInFrame = 0.1 * image extent
+        (int), mBoundDepth = 0 (Tracking.cc:875-877)."""
+        return cls.from_intrinsics(fu, fv, cx, cy, ncols, nrows, bound=int(0.1 * ncols), bound_y=int(0.1 * nrows))
 
 
 class Kine(ctypes.Structure):

@@ -96,7 +96,7 @@ class FrontEnd:
                                ctx=self.ctx)
         self.cap = self.ex.capacity
         self.info = FrameInfo.make(*self.cam, nlevels=nlevels, scale_factor=scale)
-        self.obs_cam = ObsCamera.from_intrinsics(fx, fy, cx, cy, w, h, bound=int(0.1 * w))
+        self.obs_cam = ObsCamera.for_tracking(fx, fy, cx, cy, w, h)
         self.inv_sigma2 = inv_level_sigma2(nlevels, scale)
         sf = self.info.scale_factors()
         self.level_sigma2 = (sf * sf).astype(np.float32)  # Frame::mvLevelSigma2

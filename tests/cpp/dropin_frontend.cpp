@@ -1,0 +1,131 @@
+// Drives the C++ drop-in layer (include/gfslam/orbslam.h) the way Tracking
+// does for one frame, from files written by tests/test_dropin_gpu.py, and
+// dumps every result for the test to compare with the CPU oracle.
+//   dropin_frontend <dir>
+// <dir>/params.txt : w h fx fy cx cy M  then 16 floats Tcw
+// <dir>/img.u8     : h*w bytes
+// <dir>/map.bin    : M x (gf_map_point 32 B + descriptor 32 B)
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "gfslam/orbslam.h"
+
+using namespace ORB_SLAM;
+
+template <typename T>
+static void dump(const std::string& path, const T* p, size_t n) {
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(p), sizeof(T) * n);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    const std::string dir = argv[1];
+    int w, h, M;
+    float K[4], T0[16];
+    {
+        std::ifstream p(dir + "/params.txt");
+        p >> w >> h >> K[0] >> K[1] >> K[2] >> K[3] >> M;
+        for (float& t : T0) p >> t;
+    }
+    std::vector<uint8_t> img((size_t)w * h);
+    std::ifstream(dir + "/img.u8", std::ios::binary).read(reinterpret_cast<char*>(img.data()), img.size());
+    std::vector<MapPoint> mps(M);
+    {
+        std::ifstream f(dir + "/map.bin", std::ios::binary);
+        for (int i = 0; i < M; i++) {
+            gf_map_point g;
+            f.read(reinterpret_cast<char*>(&g), sizeof(g));
+            f.read(reinterpret_cast<char*>(mps[i].mDescriptor), 32);
+            for (int k = 0; k < 3; k++) {
+                mps[i].mWorldPos[k] = g.pos[k];
+                mps[i].mNormalVector[k] = g.normal[k];
+            }
+            mps[i].mfMinDistance = g.min_dist;
+            mps[i].mfMaxDistance = g.max_dist;
+        }
+    }
+    std::vector<MapPoint*> local(M);
+    for (int i = 0; i < M; i++) local[i] = &mps[i];
+
+    try {
+        // Frame::Frame -> ORBextractor (E1-E8)
+        ORBextractor extractor(1000, 1.2f, 8, ORBextractor::FAST_SCORE, 20);
+        ImageView im{img.data(), w, h, (size_t)w};
+        Frame F(im, 0.0, &extractor, K);
+        dump(dir + "/kps.bin", F.mvKeys.data(), F.N);
+        dump(dir + "/desc.bin", F.mDescriptors.data.data(), F.mDescriptors.data.size());
+
+        // SearchLocalPoints: isInFrustum (M7) + SearchByProjection(F, local, 1) (M2)
+        F.SetPose(T0);
+        const int nview = F.isInFrustum(local, 0.5f);
+        ORBmatcher matcher(0.8f);
+        const int nm = matcher.SearchByProjection(F, local, 1.0f);
+        std::vector<int32_t> kp2mp(F.N);
+        for (int i = 0; i < F.N; i++) kp2mp[i] = F.mvpMapPoints[i] ? (int32_t)(F.mvpMapPoints[i] - mps.data()) : -1;
+        dump(dir + "/kp2mp_m2.i32", kp2mp.data(), F.N);
+
+        // PoseOptimization (P1-P4)
+        const int ninl = Optimizer::PoseOptimization(&F);
+        dump(dir + "/pose.f32", F.mTcw, 16);
+        std::vector<uint8_t> outl(F.N);
+        for (int i = 0; i < F.N; i++) outl[i] = F.mvbOutlier[i];
+        dump(dir + "/outl.u8", outl.data(), F.N);
+
+        // SearchByProjection(Cur, Last, 15) (M3): the same image as the next frame
+        Frame F2(im, 0.05, &extractor, K);
+        F2.SetPose(F.mTcw);
+        ORBmatcher m3(0.9f, true);
+        const int n3 = m3.SearchByProjection(F2, F, 15.0f);
+        std::vector<int32_t> kp2mp3(F2.N);
+        for (int i = 0; i < F2.N; i++)
+            kp2mp3[i] = F2.mvpMapPoints[i] ? (int32_t)(F2.mvpMapPoints[i] - mps.data()) : -1;
+        dump(dir + "/kp2mp_m3.i32", kp2mp3.data(), F2.N);
+
+        // GF: kinematics + MAP_INFO_MATRIX + active matching (G1-G7)
+        Observability obs(K[0], K[1], h, w, K[2], K[3], 0, 0);
+        obs.mBoundXInFrame = (int)(0.1 * w);
+        obs.mBoundYInFrame = (int)(0.1 * h);
+        float Twc[16];
+        F2.getTwc(Twc);
+        obs.updatePWLSVec(0.0, F.mTcw, 0.05, Twc);
+        obs.predictPWLSVec(0.05, 1);
+        obs.mKineIdx = 0;
+        obs.mnFrameId = F2.mnId;
+        obs.pFrame = &F2;
+        for (int i = 0; i < F2.N; i++) {
+            if (F2.mvpMapPoints[i]) F2.mvpMapPoints[i]->mbTrackInView = false;
+        }
+        std::vector<MapPoint*> rest;
+        for (MapPoint* p : local) {
+            bool matched = false;
+            for (MapPoint* q : F2.mvpMapPoints) matched |= q == p;
+            if (!matched) rest.push_back(p);
+        }
+        F2.isInFrustum(rest, 0.5f);
+        obs.mMapPoints = &local;
+        obs.runMatrixBuilding(MAP_INFO_MATRIX, 1.0, true, false);
+        double base[49] = {};
+        for (int i = 0; i < 7; i++) base[8 * i] = 1e-5;
+        obs.srand(5);
+        const int nact = obs.runActiveMapMatching(&F2, FRAME_INFO_MATRIX, base, 1.0f, matcher, 40, 1.0);
+        std::vector<int32_t> kp2mp_a(F2.N);
+        for (int i = 0; i < F2.N; i++)
+            kp2mp_a[i] = F2.mvpMapPoints[i] ? (int32_t)(F2.mvpMapPoints[i] - mps.data()) : -1;
+        dump(dir + "/kp2mp_act.i32", kp2mp_a.data(), F2.N);
+        std::vector<double> Xv(obs.kinematic[0].Xv, obs.kinematic[0].Xv + 13);
+        dump(dir + "/xv.f64", Xv.data(), 13);
+
+        FILE* s = std::fopen((dir + "/summary.txt").c_str(), "w");
+        std::fprintf(s, "%d %d %d %d %d %d %d %d\n", F.N, nview, nm, ninl, F2.N, n3, nact,
+                     ORBmatcher::DescriptorDistance(F.mDescriptors.ptr(0), F.mDescriptors.ptr(1)));
+        std::fclose(s);
+    } catch (const GpuError& e) {
+        std::fprintf(stderr, "GpuError %d: %s\n", e.code, e.what());
+        return 1;
+    }
+    return 0;
+}

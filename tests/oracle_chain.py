@@ -88,7 +88,7 @@ def prepare(camera: str, nfeat: int, img: np.ndarray, seed: int, map_size: int =
     w, h, fx, fy, cx, cy = P.cam
     P.nfeat, P.img, P.fps = nfeat, img, fps
     P.info = FrameInfo.make(*P.cam)
-    P.obs_cam = ObsCamera.from_intrinsics(fx, fy, cx, cy, w, h, bound=int(0.1 * w))
+    P.obs_cam = ObsCamera.for_tracking(fx, fy, cx, cy, w, h)
     P.inv_sigma2 = inv_level_sigma2()
     sf = P.info.scale_factors()
     P.level_sigma2 = (sf * sf).astype(np.float32)

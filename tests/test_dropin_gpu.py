@@ -1,0 +1,97 @@
+"""The C++ drop-in layer (include/gfslam/orbslam.h) driven the way Tracking
+drives the reference classes (tests/cpp/dropin_frontend.cpp), compared with
+the CPU oracle: keypoints/descriptors and match indices bit-exact, pose within
+1e-5 relative, outlier flags and active-matching claims identical."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from gf_orb_slam_amd import synth
+from gf_orb_slam_amd.matcher import FrameInfo
+from gf_orb_slam_amd.observability import ObsCamera
+from gf_orb_slam_amd.optimizer import inv_level_sigma2
+from gf_orb_slam_amd.orb import KEYPOINT_DTYPE
+from gf_orb_slam_amd.pipeline import build_local_map
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "dropin_frontend")
+
+
+def test_dropin_binary_built():
+    assert os.path.exists(BIN), "run make (or __graft_entry__.build())"
+
+
+@pytest.mark.gpu
+def test_dropin_frontend_matches_oracle(tmp_path):
+    cam = synth.CAMERAS["euroc"]
+    w, h, fx, fy, cx, cy = cam
+    img = synth.synth_frame(w, h, synth.frame_seed(3, 7))
+    k, d = O.extract(img)
+    rng = np.random.default_rng(12)
+    mps, mdesc = build_local_map(k, d, cam, rng, 1500)
+    T0 = synth.look_pose(rng, 0.005, 0.2)
+    with open(tmp_path / "params.txt", "w") as f:
+        f.write(f"{w} {h} {fx} {fy} {cx} {cy} {len(mps)}\n" + " ".join(repr(float(x)) for x in T0.reshape(-1)))
+    img.tofile(tmp_path / "img.u8")
+    rec = np.zeros((len(mps), 64), np.uint8)
+    rec[:, :32] = mps.view(np.uint8).reshape(-1, 32)
+    rec[:, 32:] = mdesc
+    rec.tofile(tmp_path / "map.bin")
+    r = subprocess.run([BIN, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    N, nview, nm, ninl, N2, n3, nact, dd = map(int, open(tmp_path / "summary.txt").read().split())
+    rd = lambda name, dt: np.fromfile(tmp_path / name, dt)
+
+    # extraction (E1-E8)
+    kg = rd("kps.bin", KEYPOINT_DTYPE)
+    assert N == len(k) and kg.tobytes() == k.tobytes()
+    assert np.array_equal(rd("desc.bin", np.uint8).reshape(-1, 32), d)
+    assert dd == int(np.unpackbits(d[0] ^ d[1]).sum())
+
+    # isInFrustum + SearchByProjection(F, local, 1), nnratio 0.8 (M7, M2)
+    info = FrameInfo.make(*cam)
+    views, nv = O.frustum(info, T0, mps)
+    assert nv == nview
+    k2 = np.full(N, -1, np.int32)
+    sc = np.full(N, 999, np.int32)
+    no = O.match_project(info, k, d, views, mdesc, 1.0, 0.8, k2, sc)
+    assert no == nm and np.array_equal(k2, rd("kp2mp_m2.i32", np.int32))
+
+    # PoseOptimization (P1-P4)
+    idx = np.nonzero(k2 >= 0)[0]
+    To, oo, no_, _ = O.pose_opt(T0, mps["pos"][k2[idx]], np.c_[k["x"][idx], k["y"][idx]],
+                                k["octave"][idx].astype(np.int32), inv_level_sigma2(), fx, fy, cx, cy)
+    Tg = rd("pose.f32", np.float32).reshape(4, 4)
+    assert ninl == no_
+    assert np.all(np.abs(Tg.astype(np.float64) - To) <= 1e-5 * np.maximum(1, np.abs(To)))
+    og = rd("outl.u8", np.uint8)
+    assert np.array_equal(og[idx], oo) and og[k2 < 0].sum() == 0
+
+    # SearchByProjection(Cur, Last, 15) with the rotation check (M3)
+    pos = np.zeros((N, 3), np.float32)
+    pos[idx] = mps["pos"][k2[idx]]
+    k3 = np.full(N, -1, np.int32)
+    s3 = np.full(N, 999, np.int32)
+    n3o = O.match_lastframe(info, k, d, Tg, k, d, k2.copy(), og.copy(), pos, 15.0, 1, k3, s3)
+    assert N2 == N and n3o == n3 and np.array_equal(k3, rd("kp2mp_m3.i32", np.int32))
+
+    # Observability: PWLS state, MAP_INFO_MATRIX, runActiveMapMatching (G1-G7)
+    Twc = np.eye(4, dtype=np.float32)
+    Twc[:3, :3] = Tg[:3, :3].T
+    Twc[:3, 3] = ((-Tg[0, :3] * Tg[0, 3]) + (-Tg[1, :3] * Tg[1, 3])) + (-Tg[2, :3] * Tg[2, 3])
+    xv = O.obs_update(0.0, Tg, 0.05, Twc)
+    assert np.array_equal(xv, rd("xv.f64", np.float64))
+    v2, _ = O.frustum(info, Tg, mps)
+    v2["in_view"][k3[k3 >= 0]] = 0
+    ocam = ObsCamera.for_tracking(fx, fy, cx, cy, w, h)
+    H, inf, uv, valid = O.obs_build_info(ocam, xv, mps["pos"], None, 0)
+    upd = ((v2["in_view"] != 0) & (valid != 0)).astype(np.uint8)
+    sig2 = (info.scale_factors() ** 2).astype(np.float32)
+    ka = k3.copy()
+    nao, _ = O.active_match(info, k, d, v2, mdesc, upd, inf, H, uv, np.eye(7).reshape(-1) * 1e-5, sig2, 40, 1.0,
+                            0.8, 5, ka, s3.copy())
+    assert nao == nact and nact > 0
+    assert np.array_equal(ka, rd("kp2mp_act.i32", np.int32))
