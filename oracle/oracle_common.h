@@ -17,8 +17,12 @@
 // pose-optimisation rows are "parity unpinned" against the original binaries:
 // they are pinned against this restatement only.
 //
-// Compile with -O3 -ffp-contract=off: no FMA contraction anywhere, so float
-// arithmetic matches the device kernels (which are built the same way).
+// Compile with -O3 -fno-tree-vectorize -ffp-contract=off: no FMA contraction
+// and no auto-vectorised float conversions (GCC's vectorizer changed an
+// f64->f32 rounding), so float arithmetic matches the device kernels, which
+// are built with -ffp-contract=off and correctly rounded f32 div/sqrt.
+// Pose LM (oracle/poseopt.cpp): parity unpinned (no PoseOptimization test
+// upstream); checked by recovery/outlier properties in tests/test_oracle_pose.py.
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
