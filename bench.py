@@ -65,6 +65,53 @@ def cpu_baseline(camera: str, nfeat: int, budget_s: float = 12.0) -> dict:
                       f"PoseOptimization, 1 thread, {dt:.1f} s"}
 
 
+def single_stream(camera: str, nfeat: int, budget: int, steps: int) -> dict:
+    """Per-frame latency of ONE sequence (B = 1) through the same device path."""
+    import torch
+
+    from gf_orb_slam_amd import synth
+    from gf_orb_slam_amd.pipeline import FrontEnd
+
+    w, h = synth.CAMERAS[camera][:2]
+    fe = FrontEnd(camera, nfeat, 1, 2000, gf_budget=budget, seed=99)
+    fe.load_frames(synth.synth_frame(w, h, synth.frame_seed(99, 0))[None])
+    fe.build_maps()
+    for _ in range(3):
+        fe.step()
+    fe.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fe.step()
+    fe.sync()
+    dt = (time.perf_counter() - t0) / steps
+    return {"ms_per_frame": round(dt * 1e3, 3), "fps": round(1.0 / dt, 2), "steps": steps}
+
+
+def share_startup_state(dist, device, world: int, rank: int, nbytes: int = 45 * 1024 * 1024):
+    """The one exchange step: rank 0 broadcasts the shared
+    vocabulary/map blob to every rank (RCCL over xGMI on the GPU box, gloo in
+    the CPU tests). Returns a checksum every rank must agree on."""
+    import torch
+
+    blob = torch.zeros(nbytes // 4, dtype=torch.int32, device=device)
+    if rank == 0:
+        blob.copy_(torch.arange(blob.numel(), dtype=torch.int32, device=device) * 7 + 3)
+    if world > 1:
+        dist.broadcast(blob, src=0)
+    return int(blob[:: max(1, blob.numel() // 1024)].sum().item())
+
+
+def max_over_ranks(dist, device, world: int, seconds: float) -> float:
+    """The timed region's wall time: max over ranks (bench contract)."""
+    import torch
+
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -75,6 +122,8 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-stream-steps", type=int, default=20,
+                    help="also time one stream alone (per-frame latency of a single sequence)")
     args = ap.parse_args()
 
     import torch
@@ -101,10 +150,7 @@ def main():
 
     # one-off exchange: rank 0 broadcasts the shared vocabulary/map blob (RCCL over xGMI)
     if world > 1:
-        blob = torch.zeros(45 * 1024 * 1024 // 4, dtype=torch.int32, device="cuda")
-        if rank == 0:
-            blob.copy_(torch.arange(blob.numel(), dtype=torch.int32, device="cuda"))
-        dist.broadcast(blob, src=0)
+        share_startup_state(dist, "cuda", world, rank)
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -126,10 +172,7 @@ def main():
     dt = time.perf_counter() - t0
     prof = fe.prof_report()
     fe.prof_enable(False)
-    dt_t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+    dt = max_over_ranks(dist, "cuda", world, dt)
 
     frames_total = world * B * args.steps
     fps = frames_total / dt
@@ -194,6 +237,8 @@ def main():
         "avg_active_matches": n_active,
         "avg_inliers": ninl,
     }
+    if rank == 0 and args.single_stream_steps > 0:
+        out["single_stream"] = single_stream(cam, args.nfeatures, args.gf_budget, args.single_stream_steps)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures)
     if rank == 0:
