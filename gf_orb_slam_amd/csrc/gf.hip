@@ -126,9 +126,10 @@ __device__ __forceinline__ void add_info_block(const double* H, double sigma2, d
         for (int j = 0; j < 7; j++) M[7 * i + j] = M[7 * i + j] + (Hw[i] * Hw[j] + Hw[7 + i] * Hw[7 + j]);
 }
 
-__device__ __noinline__ double logdet_lu(const double* M) {
+// rebuilds a + sign*b itself so the caller's matrix can stay in registers
+__device__ __noinline__ double logdet_lu(const double* a, const double* b, double sign) {
     double A[49];
-    for (int i = 0; i < 49; i++) A[i] = M[i];
+    for (int i = 0; i < 49; i++) A[i] = sign > 0 ? a[i] + b[i] : a[i] - b[i];
     double acc = 0;
     for (int c = 0; c < 7; c++) {
         int p = c;
@@ -180,7 +181,7 @@ __device__ double logdet_sum(const double* a, const double* b, double sign) {
             L[i * (i + 1) / 2 + j] = t * rd;
         }
     }
-    if (!ok) return logdet_lu(M);
+    if (!ok) return logdet_lu(a, b, sign);
     double v1 = 1, v2 = 1;  // Armadillo's two-accumulator product of the diagonal
     v1 *= L[0];
     v2 *= L[2];
@@ -273,17 +274,115 @@ struct ActiveArgs {
     int32_t* err;
 };
 
-// ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) on one lane.
-__device__ int one_point_match(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
-                               const int* items, int* claim, const gf_keypoint* K, const uint8_t* D) {
+// ---------------------------------------------------------------------------
+// runActiveMapMatching on ONE wave per frame. Everything that is sequential in
+// the reference stays sequential and in its order (std::rand draws, heap
+// tops, one-point matches, claims), but each sequential step is wave-wide:
+//   * the glibc random_r state lives in lanes 0..30 of a VGPR and advances
+//     with readlane/writelane;
+//   * the heap top is a wave arg-max over the live candidates; when the
+//     maximum is tied or a score is NaN the std::priority_queue order is
+//     ambiguous, and the exact heap is rebuilt by replaying the round's
+//     push/pop log with the libstdc++ heap port (select.h);
+//   * SearchByProjection_OnePoint scans its grid window with 64 lanes and
+//     merges (distance, candidate order) top-2 lists, which is what the
+//     sequential best / second-best loop keeps.
+constexpr int AW = 64;
+
+// glibc random_r TYPE_3 as a linear recurrence: with the ring read oldest
+// first, s_j = st[(f + j) % 31] = o_{n-31+j}, every later word is
+// o_{n+k} = o_{n+k-3} + o_{n+k-31} (mod 2^32), hence a fixed integer
+// combination sum_j C[k][j] s_j. One wave produces the next 64 words at once
+// (lane k: 31 multiply-adds); rand() = word >> 1.
+__constant__ uint32_t c_rng_coef[64][31];
+
+__device__ __forceinline__ uint32_t rng_word(uint32_t s) {
+    const int k = threadIdx.x;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 31; j++) acc += c_rng_coef[k][j] * (uint32_t)__builtin_amdgcn_readlane((int)s, j);
+    return acc;
+}
+
+// history after consuming c (<= 64) words: s'_j = h_{c+j}, h = s ++ o
+__device__ __forceinline__ uint32_t rng_advance(uint32_t s, uint32_t o, int c) {
+    const int j = threadIdx.x, src = c + j;
+    const uint32_t a = (uint32_t)__shfl((int)s, min(src, 30), 64);
+    const uint32_t b = (uint32_t)__shfl((int)o, max(src - 31, 0), 64);
+    return j < 31 ? (src < 31 ? a : b) : 0u;
+}
+
+struct IdxLess {  // SimplePoint::operator< (score only), on candidate indices
+    const double* sc;
+    __device__ bool operator()(int16_t a, int16_t b) const { return sc[a] < sc[b]; }
+};
+
+__device__ __forceinline__ void top2_insert(unsigned long long key, unsigned long long& k1, unsigned long long& k2) {
+    if (key < k1) {
+        k2 = k1;
+        k1 = key;
+    } else if (key < k2) {
+        k2 = key;
+    }
+}
+
+// Pool = lmkIdx columns: alive slots of the original in-view list, in slot
+// order; bits + per-word prefix counts give the j-th column in O(log).
+struct Pool {
+    unsigned long long* bits;  // [64]
+    int* pre;                  // [65]
+};
+
+__device__ __forceinline__ int pool_select(const Pool& P, int j) {
+    int lo = 0, hi = 64;  // largest w with pre[w] <= j
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (P.pre[mid] <= j) lo = mid;
+        else hi = mid;
+    }
+    unsigned long long w = P.bits[lo];
+    int r = j - P.pre[lo], pos = 0;
+#pragma unroll
+    for (int half = 32; half >= 1; half >>= 1) {
+        const int c = __popcll(w & ((1ull << half) - 1ull));
+        if (r >= c) {
+            r -= c;
+            w >>= half;
+            pos += half;
+        }
+    }
+    return lo * 64 + pos;
+}
+
+__device__ __forceinline__ void pool_prefix(const Pool& P) {
+    const int lane = threadIdx.x;
+    int c = __popcll(P.bits[lane]), x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    P.pre[lane] = x - c;
+    if (lane == 63) P.pre[64] = x;
+}
+
+// ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) on one lane,
+// without claiming: returns the keypoint it would claim (or -1) and its
+// distance. Within a round every candidate sees the same claims (only the
+// round's final success claims), so all candidates are evaluated at once.
+__device__ void lane_one_point(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
+                               const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D,
+                               int& outIdx, int& outDist) {
+    outIdx = -1;
+    outDist = INT_MAX;
     const gf_mp_view v = A.views[(long long)f * A.mp_cap + mpi];
-    if (!v.in_view) return -1;
+    if (!v.in_view) return;
     const int pl = min(max(v.level, 0), fc.nlevels - 1);
     float r = v.view_cos > 0.998 ? 2.5f : 4.0f;
     if (A.th != 1.0) r *= A.th;
     r = r * fc.scales[pl];
     int cx0, cx1, cy0, cy1;
-    if (!grid_window(fc, v.u, v.v, r, cx0, cx1, cy0, cy1)) return -1;
+    if (!grid_window(fc, v.u, v.v, r, cx0, cx1, cy0, cy1)) return;
     const uint8_t* qd = A.mp_desc + ((long long)f * A.mp_cap + mpi) * 32;
     int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
     for (int ix = cx0; ix <= cx1; ix++) {
@@ -308,41 +407,150 @@ __device__ int one_point_match(const ActiveArgs& A, const FrameConst& fc, int f,
         }
     }
     if (bestDist <= TH_HIGH) {
-        if (bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2) return -1;
-        claim[bestIdx] = mpi;
-        A.score[(long long)f * A.kp_cap + bestIdx] = bestDist;
-        return bestIdx;
+        if (bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2) return;
+        outIdx = bestIdx;
+        outDist = bestDist;
     }
-    return -1;
 }
 
-__device__ __forceinline__ int draw_sample(int32_t* st, int32_t* rf, int32_t* rr, const int16_t* dummy, int16_t* vis,
-                                           int N, int round) {
-    for (int q = 0; q < MAX_RANDOM_QUERY_TIME; q++) {
-        const int j = (int)((uint32_t)gfrng::next(st, rf, rr) % (uint32_t)N);
-        if (vis[j] < round) {
-            vis[j] = (int16_t)round;
-            return j;
+// Per-round candidate list: the draws of the sequential loop in order (the
+// initial random subset, then one replacement per failed top), produced 64
+// tries at a time ahead of need.
+struct Cands {
+    int16_t* slot;   // pool slot drawn
+    int32_t* tries;  // rand() calls from the round start up to this acceptance
+    double* score;   // logDet(curMat + ObsMat)
+    int16_t* match;  // keypoint OnePoint would claim, -1
+    int16_t* dist;
+    uint8_t* alive;  // still in the heap
+};
+
+// One batch of 64 tries: tries are accepted in order when their column was not
+// visited this round and not drawn earlier in the batch; accepted columns are
+// marked visited at once (unused ones are unmarked at the round end). A draw
+// fails after MAX_RANDOM_QUERY_TIME rejected tries: *exh_at = tries count then.
+__device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, const Pool& P, int16_t* vis,
+                          const Cands& C, int nc, int* exh_at) {
+    const int lane = threadIdx.x;
+    const uint32_t o = rng_word(s);
+    const int j = (int)((o >> 1) % (uint32_t)N);
+    const int sl = pool_select(P, j);
+    bool acc = vis[sl] < round;
+    for (int k = 0; k < 63; k++) {
+        const int jk = __builtin_amdgcn_readlane(j, k);
+        acc = acc && !(k < lane && jk == j);
+    }
+    const unsigned long long m = __ballot(acc);
+    const int a0 = m ? __ffsll((long long)m) - 1 : 64;
+    int got = 0;
+    if (run + a0 >= MAX_RANDOM_QUERY_TIME) {  // the next draw gives up inside this batch
+        *exh_at = tries + (MAX_RANDOM_QUERY_TIME - run);
+    } else {
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        if (acc) {
+            C.slot[nc + rank] = (int16_t)sl;
+            C.tries[nc + rank] = tries + lane + 1;
+            vis[sl] = (int16_t)round;
+        }
+        got = __popcll(m);
+        if (m) {
+            run = __clzll((long long)m);  // rejected tries after the last acceptance
+        } else {
+            run += 64;
         }
     }
-    return -1;
+    s = rng_advance(s, o, 64);
+    tries += 64;
+    __syncthreads();
+    return got;
 }
 
-__global__ __launch_bounds__(GF_THREADS) void k_active_match(ActiveArgs A) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    HeapEntry* heap = (HeapEntry*)smem;                          // POOL_MAX
-    int* cell_start = (int*)(heap + POOL_MAX);                   // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;                       // NCELLS
-    int* items = cursor + NCELLS;                                // KP_MAX
-    int* claim = items + KP_MAX;                                 // KP_MAX
-    int16_t* lmk = (int16_t*)(claim + KP_MAX);                   // POOL_MAX
-    int16_t* vis = lmk + POOL_MAX;                               // POOL_MAX
-    int16_t* rem = vis + POOL_MAX;                               // POOL_MAX
-    __shared__ double cur[49];
-    __shared__ int32_t s_st[31], s_rf, s_rr;
-    __shared__ int s_N, s_cnt, s_rem, s_exh, s_term, s_nm, s_scan[GF_THREADS / 64];
+__device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
+                           const int16_t* lmk, const double* cur, const double* info, const int* cell_start,
+                           const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D) {
+    for (int c = c0 + threadIdx.x; c < c1; c += AW) {
+        const int q = lmk[C.slot[c]];
+        C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
+        int mi, md;
+        lane_one_point(A, fc, f, q, cell_start, items, claim, K, D, mi, md);
+        C.match[c] = (int16_t)mi;
+        C.dist[c] = (int16_t)(mi >= 0 ? md : 0);
+        C.alive[c] = 0;
+    }
+    __syncthreads();
+}
 
-    const int f = blockIdx.x, tid = threadIdx.x;
+// Heap top of the live candidates: the arg-max, unless the maximum is tied
+// or a score is NaN, when std::priority_queue's order is reproduced by
+// replaying its push/pop history (sz pushes, then pop/push pairs) exactly.
+__device__ int wave_top(const Cands& C, int ncand, int sz, int npop, int16_t* rheap, int* s_res) {
+    const int lane = threadIdx.x;
+    double best = -INFINITY;
+    int bi = -1, nan = 0;
+    for (int c = lane; c < ncand; c += AW) {
+        if (!C.alive[c]) continue;
+        const double sc = C.score[c];
+        if (sc != sc) {
+            nan = 1;
+        } else if (bi < 0 || sc > best) {
+            best = sc;
+            bi = c;
+        }
+    }
+    double gb = best;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) gb = fmax(gb, __shfl_xor(gb, o, 64));
+    int cnt = 0;
+    for (int c = lane; c < ncand; c += AW) cnt += C.alive[c] && C.score[c] == gb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+        nan |= __shfl_xor(nan, o, 64);
+    }
+    if (!nan && cnt == 1) {
+        const unsigned long long m = __ballot(bi >= 0 && best == gb);
+        return __shfl(bi, __ffsll((long long)m) - 1, 64);
+    }
+    if (lane == 0) {
+        int hn = 0;
+        const IdxLess cmp{C.score};
+        for (int c = 0; c < sz; c++) {
+            rheap[hn++] = (int16_t)c;
+            gfsel::push_heap(rheap, hn, cmp);
+        }
+        for (int p = 0; p < npop; p++) {
+            gfsel::pop_heap(rheap, hn, cmp);
+            hn--;
+            rheap[hn++] = (int16_t)(sz + p);
+            gfsel::push_heap(rheap, hn, cmp);
+        }
+        *s_res = rheap[0];
+    }
+    __syncthreads();
+    return *s_res;
+}
+
+__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    double* c_score = (double*)smem;                                       // POOL_MAX
+    unsigned long long* pbits = (unsigned long long*)(c_score + POOL_MAX);  // 64
+    int* cell_start = (int*)(pbits + 64);                                  // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;                                 // NCELLS (later: replay heap)
+    int* items = cursor + NCELLS;                                          // KP_MAX
+    int* claim = items + KP_MAX;                                           // KP_MAX
+    int* ppre = claim + KP_MAX;                                            // 65 (+3 pad)
+    int32_t* c_tries = ppre + 68;                                          // POOL_MAX
+    int16_t* lmk = (int16_t*)(c_tries + POOL_MAX);                         // POOL_MAX: map point of each slot
+    int16_t* vis = lmk + POOL_MAX;                                         // POOL_MAX: lmkVisited per slot
+    int16_t* c_slot = vis + POOL_MAX;                                      // POOL_MAX
+    int16_t* c_match = c_slot + POOL_MAX;                                  // POOL_MAX
+    int16_t* c_dist = c_match + POOL_MAX;                                  // POOL_MAX
+    uint8_t* c_alive = (uint8_t*)(c_dist + POOL_MAX);                      // POOL_MAX
+    int16_t* rheap = (int16_t*)cursor;
+    __shared__ double cur[49];
+    __shared__ int s_res, s_exh;
+
+    const int f = blockIdx.x, lane = threadIdx.x;
     const FrameConst& fc = A.fc;
     const int n = min(A.n[f], KP_MAX);
     const int m = min(A.m[f], 32767);
@@ -351,194 +559,175 @@ __global__ __launch_bounds__(GF_THREADS) void k_active_match(ActiveArgs A) {
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* left = A.left + (long long)f * A.mp_cap;
     const int num_to_match = A.num_to_match[f];
-    // pool scratch doubles as the grid-build scratch (rem region >= n shorts is too small; use heap)
-    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, (int*)heap, GF_THREADS);
+    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, (int*)c_score, AW);
 
     // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
     const bool early = (m == 0 || num_to_match <= 0);
-    {
-        const int chunk = (m + GF_THREADS - 1) / GF_THREADS;
-        const int p0 = min(tid * chunk, m), p1 = min(p0 + chunk, m);
-        int c = 0;
-        for (int i = p0; i < p1; i++) {
+    int N = 0;
+    for (int base = 0; base < m; base += AW) {
+        const int i = base + lane;
+        bool in = false, upd = false;
+        if (i < m) {
             const long long g = (long long)f * A.mp_cap + i;
-            c += A.views[g].in_view && (early || A.updated[g]);
+            in = A.views[g].in_view;
+            upd = A.updated[g];
         }
-        // block exclusive scan
-        const int lane = tid & 63, wid = tid >> 6;
-        int x = c;
-        for (int o = 1; o < 64; o <<= 1) {
-            int y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_scan[wid] = x;
-        __syncthreads();
-        int base = 0, tot = 0;
-        for (int w = 0; w < GF_THREADS / 64; w++) {
-            if (w < wid) base += s_scan[w];
-            tot += s_scan[w];
-        }
-        int o = base + x - c;
-        if (early) {
-            for (int i = p0; i < p1; i++)
-                if (A.views[(long long)f * A.mp_cap + i].in_view) left[o++] = i;
-            if (tid == 0) {
-                A.nleft[f] = tot;
-                A.nmatched[f] = 0;
-            }
-            return;
-        }
-        if (tot > POOL_MAX) {
-            if (tid == 0) A.err[f] = 2;
-            return;
-        }
-        for (int i = p0; i < p1; i++) {
-            const long long g = (long long)f * A.mp_cap + i;
-            if (A.views[g].in_view && A.updated[g]) {
+        const bool take = in && (early || upd);
+        const unsigned long long msk = __ballot(take);
+        const int o = N + __popcll(msk & ((1ull << lane) - 1ull));
+        if (take) {
+            if (early) {
+                left[o] = i;
+            } else if (o < POOL_MAX) {
                 lmk[o] = (int16_t)i;
                 vis[o] = -1;
-                o++;
             }
         }
-        if (tid == 0) s_N = tot;
-        if (tid < 49) cur[tid] = A.base[49LL * f + tid];
-        if (tid < 31) s_st[tid] = A.rng[f].state[tid];
-        if (tid == 0) {
-            s_rf = A.rng[f].f;
-            s_rr = A.rng[f].r;
-            s_nm = 0;
-        }
-        __syncthreads();
+        N += __popcll(msk);
     }
-    const int S = (int)((float)s_N / (float)num_to_match * 1.0);
+    if (early) {
+        if (lane == 0) {
+            A.nleft[f] = N;
+            A.nmatched[f] = 0;
+        }
+        return;
+    }
+    if (N > POOL_MAX) {
+        if (lane == 0) A.err[f] = 2;
+        return;
+    }
+    const Pool P{pbits, ppre};
+    {
+        const int lo = lane * 64;
+        pbits[lane] = N >= lo + 64 ? ~0ull : (N > lo ? ((1ull << (N - lo)) - 1ull) : 0ull);
+        __syncthreads();
+        pool_prefix(P);
+    }
+    if (lane < 49) cur[lane] = A.base[49LL * f + lane];
+    uint32_t rs;  // RNG history (oldest first) at the last committed rand() call
+    {
+        const int f0 = A.rng[f].f;
+        rs = lane < 31 ? (uint32_t)A.rng[f].state[(f0 + lane) % 31] : 0u;
+    }
+    int used = 0, nm = 0;
+    __syncthreads();
+
+    const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
+    const int S = (int)((float)N / (float)num_to_match * 1.0);
     const double* info = A.info + (long long)f * A.mp_cap * 49;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
 
     for (int round = 0; round < num_to_match; ++round) {
-        // -- initial batch of random samples (lane 0, exact std::rand order)
-        if (tid == 0) {
-            const int N = s_N, szActual = min(S, N);
-            int cnt = 0, exh = 0;
-            while (cnt < szActual) {
-                const int j = draw_sample(s_st, &s_rf, &s_rr, nullptr, vis, N, round);
-                if (j < 0) {
-                    exh = 1;
-                    break;
-                }
-                heap[cnt].idx = lmk[j];
-                cnt++;
-            }
-            s_cnt = cnt;
-            s_exh = exh;
-            s_rem = 0;
-            s_term = 0;
-        }
-        __syncthreads();
-        // -- their log-dets across the workgroup
-        for (int t = tid; t < s_cnt; t += GF_THREADS) heap[t].s = logdet_sum(cur, info + 49LL * heap[t].idx, 1.0);
-        __syncthreads();
-        // -- heap, one-point matches, replacement draws (lane 0)
-        if (tid == 0) {
-            const int N = s_N, szActual = min(S, N);
-            int hn = 0;
-            for (int t = 0; t < s_cnt; t++) gfsel::push_heap(heap, ++hn, HeapLess());
-            int numHit = s_cnt, nrem = 0;
-            bool exh = s_exh != 0;
-            while (!exh && szActual > 0 && numHit >= szActual) {
-                const HeapEntry top = heap[0];
-                const int b = one_point_match(A, fc, f, top.idx, cell_start, items, claim, K, D);
-                rem[nrem++] = (int16_t)top.idx;
-                if (b >= 0) {
-                    add_info_block(Hm + 14LL * top.idx, (double)A.sigma2[K[b].octave], cur);
-                    s_nm++;
-                    break;
-                }
-                gfsel::pop_heap(heap, hn, HeapLess());
-                hn--;
-                numHit--;
-                const int j = draw_sample(s_st, &s_rf, &s_rr, nullptr, vis, N, round);
-                if (j < 0) {
-                    exh = true;
-                    break;
-                }
-                const int q = lmk[j];
-                heap[hn].idx = q;
-                heap[hn].s = logdet_sum(cur, info + 49LL * q, 1.0);
-                gfsel::push_heap(heap, ++hn, HeapLess());
-                numHit++;
-            }
-            int term = exh || hn == 0 || nrem == 0;
-            if (!term && nrem == N) term = 2;  // went through all map points: keep the pool as left-overs
-            if (!term) {                       // sort removeIdx (map point ids) ascending
-                for (int a = 1; a < nrem; a++) {
-                    int16_t v = rem[a];
-                    int b = a - 1;
-                    while (b >= 0 && rem[b] > v) {
-                        rem[b + 1] = rem[b];
-                        b--;
-                    }
-                    rem[b + 1] = v;
-                }
-            }
-            s_rem = nrem;
-            s_term = term;
-        }
-        __syncthreads();
-        if (s_term) break;
-        // -- drop tried entries from the pool (order-preserving compaction)
-        {
-            const int N = s_N, nrem = s_rem;
-            const int chunk = (N + GF_THREADS - 1) / GF_THREADS;
-            const int p0 = min(tid * chunk, N), p1 = min(p0 + chunk, N);
-            int16_t kl[POOL_MAX / GF_THREADS], kv[POOL_MAX / GF_THREADS];
-            int c = 0;
-            for (int p = p0; p < p1; p++) {
-                const int16_t id = lmk[p];
-                bool removed = false;
-                for (int r = 0; r < nrem; r++) removed |= rem[r] == id;
-                if (!removed) {
-                    kl[c] = id;
-                    kv[c] = vis[p];
-                    c++;
-                }
-            }
-            const int lane = tid & 63, wid = tid >> 6;
-            int x = c;
-            for (int o = 1; o < 64; o <<= 1) {
-                int y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (lane == 63) s_scan[wid] = x;
+        const int sz = min(S, N);
+        if (sz == 0) break;  // empty heap: early termination
+        // -- draws, ahead of need
+        uint32_t sd = rs;
+        int tries = 0, run = 0, nc = 0, evald = 0, exh_at = -1;
+        while (nc < sz && exh_at < 0) {
+            if (lane == 0) s_exh = -1;
             __syncthreads();
-            int base = 0, tot = 0;
-            for (int w = 0; w < GF_THREADS / 64; w++) {
-                if (w < wid) base += s_scan[w];
-                tot += s_scan[w];
+            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh);
+            exh_at = s_exh;
+        }
+        if (nc < sz) {  // the initial subset could not be completed
+            for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
+            used += exh_at;
+            for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs), min(T, 64));
+            break;
+        }
+        eval_cands(A, fc, f, C, 0, nc, lmk, cur, info, cell_start, items, claim, K, D);
+        evald = nc;
+        for (int c = lane; c < sz; c += AW) C.alive[c] = 1;
+        __syncthreads();
+        // -- the sequential heap loop, now over known scores and match results
+        int npop = 0, top = -1;
+        bool exh = false, success = false;
+        while (true) {
+            top = wave_top(C, sz + npop, sz, npop, rheap, &s_res);
+            if (C.match[top] >= 0) {
+                success = true;
+                break;
             }
-            const int o = base + x - c;
-            for (int k = 0; k < c; k++) {
-                lmk[o + k] = kl[k];
-                vis[o + k] = kv[k];
+            if (lane == 0) C.alive[top] = 0;  // heapSubset.pop()
+            const int rep = sz + npop;       // the replacement draw
+            while (rep >= nc && exh_at < 0) {
+                if (lane == 0) s_exh = -1;
+                __syncthreads();
+                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh);
+                exh_at = s_exh;
             }
-            __syncthreads();
-            if (tid == 0) s_N = tot;
+            if (rep >= nc) {
+                exh = true;
+                break;
+            }
+            if (rep >= evald) {
+                eval_cands(A, fc, f, C, evald, nc, lmk, cur, info, cell_start, items, claim, K, D);
+                evald = nc;
+            }
+            if (lane == 0) C.alive[rep] = 1;
+            npop++;
             __syncthreads();
         }
+        // -- commit: RNG calls actually made, visited marks of the used draws only
+        const int nused = sz + npop;  // draws that happened
+        const int T = exh ? exh_at : C.tries[nused - 1];
+        for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
+        used += T;
+        for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs), min(t, 64));
+        __syncthreads();
+        if (exh) break;
+        const int nrem = npop + 1;  // removeIdx: every top tried
+        const int q = lmk[C.slot[top]];
+        const int b = C.match[top];
+        if (lane == 0) {  // OnePoint's claim
+            claim[b] = q;
+            A.score[(long long)f * A.kp_cap + b] = C.dist[top];
+        }
+        if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
+            const double* H = Hm + 14LL * q;
+            const double s2 = sqrt((double)A.sigma2[K[b].octave]);
+            const double w = s2 / (s2 * s2);
+            const int i = lane / 7, jj = lane % 7;
+            const double a0 = w * H[i], a1 = w * H[jj], b0 = w * H[7 + i], b1 = w * H[7 + jj];
+            cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
+        }
+        nm++;
+        (void)success;
+        __syncthreads();
+        if (nrem == N) break;  // went through all map points: the pool stays as left-overs
+        // drop the tried columns: popped candidates and the successful top
+        for (int c = lane; c < nused; c += AW)
+            if (!C.alive[c] || c == top) atomicAnd(&pbits[C.slot[c] >> 6], ~(1ull << (C.slot[c] & 63)));
+        __syncthreads();
+        pool_prefix(P);
+        N -= nrem;
+        __syncthreads();
     }
-    // ---- outputs: claims, left-over pool, RNG state
-    for (int i = tid; i < n; i += GF_THREADS) kp2mp[i] = claim[i];
-    for (int i = tid; i < s_N; i += GF_THREADS) left[i] = lmk[i];
-    if (tid < 31) A.rng[f].state[tid] = s_st[tid];
-    if (tid == 0) {
-        A.rng[f].f = s_rf;
-        A.rng[f].r = s_rr;
-        A.nleft[f] = s_N;
-        A.nmatched[f] = s_nm;
+    // ---- outputs: claims, left-over pool (alive slots in order), RNG state
+    for (int i = lane; i < n; i += AW) kp2mp[i] = claim[i];
+    for (int w = 0; w < 64; w++) {
+        const unsigned long long bits = pbits[w];
+        if (((bits >> lane) & 1ull) && w * 64 + lane < POOL_MAX)
+            left[ppre[w] + __popcll(bits & ((1ull << lane) - 1ull))] = lmk[w * 64 + lane];
+    }
+    {  // back to the glibc ring: f advanced by the calls made, oldest word at f
+        const int f1 = (A.rng[f].f + used) % 31;
+        __syncthreads();
+        if (lane < 31) A.rng[f].state[(f1 + lane) % 31] = (int32_t)rs;
+        __syncthreads();
+        if (lane == 0) {
+            A.rng[f].f = f1;
+            A.rng[f].r = (f1 + 28) % 31;
+            A.nleft[f] = N;
+            A.nmatched[f] = nm;
+        }
     }
 }
 
+
 size_t active_lds_bytes() {
-    return sizeof(HeapEntry) * POOL_MAX + sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX) + sizeof(int16_t) * 3 * POOL_MAX;
+    return sizeof(double) * POOL_MAX + 8 * 64 + sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX + 68) +
+           sizeof(int32_t) * POOL_MAX + sizeof(int16_t) * 5 * POOL_MAX + POOL_MAX;
 }
 
 // ------------------------------------------------------------- max-volume selection
@@ -789,10 +978,17 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
     if (rc) return rc;
     A.err = (int32_t*)err;
     static unsigned long long mask = 0;
+    if (!(mask & (1ull << ctx->device))) {  // rand() as a linear combination of the 31-word history
+        uint32_t h[31 + 64][31] = {};
+        for (int j = 0; j < 31; j++) h[j][j] = 1u;
+        for (int k = 0; k < 64; k++)
+            for (int j = 0; j < 31; j++) h[31 + k][j] = h[28 + k][j] + h[k][j];
+        GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_rng_coef), &h[31][0], sizeof(uint32_t) * 64 * 31));
+    }
     rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(), &mask);
     if (rc) return rc;
     GF_PROF(ctx, s, "k_active_match");
-    k_active_match<<<nframes, GF_THREADS, active_lds_bytes(), s>>>(A);
+    k_active_match<<<nframes, AW, active_lds_bytes(), s>>>(A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

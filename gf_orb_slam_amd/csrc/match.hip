@@ -122,6 +122,69 @@ __device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int
 }
 
 
+// Rotation-consistency histogram of SearchByProjection(Cur, Last)
+// (ORBmatcher.cc:2146-2190, ComputeThreeMaxima :2338-2379) over qres.
+__device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keypoint* K, int* claim, int32_t* score,
+                                int* s_nm, int* s_hist, int* s_keep, int nthreads) {
+    const int tid = threadIdx.x;
+        const float factor = 1.0f / HISTO_LENGTH;
+        for (int k = tid; k < nq; k += nthreads) {
+            const int j = A.qres[(long long)f * A.q_cap + k];
+            if (j < 0) continue;
+            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            atomicAdd(&s_hist[bin], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO_LENGTH; i++) {
+                const int s = s_hist[i];
+                if (s > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = s;
+                    ind3 = ind2;
+                    ind2 = ind1;
+                    ind1 = i;
+                } else if (s > max2) {
+                    max3 = max2;
+                    max2 = s;
+                    ind3 = ind2;
+                    ind2 = i;
+                } else if (s > max3) {
+                    max3 = s;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1;
+                ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            s_keep[0] = ind1;
+            s_keep[1] = ind2;
+            s_keep[2] = ind3;
+        }
+        __syncthreads();
+        for (int k = tid; k < nq; k += nthreads) {
+            const int j = A.qres[(long long)f * A.q_cap + k];
+            if (j < 0) continue;
+            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)roundf(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            if (bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2]) continue;
+            claim[j] = -1;
+            score[j] = 999;
+            atomicSub(s_nm, 1);
+        }
+        __syncthreads();
+}
+
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
     int* cell_start = lds;                  // NCELLS + 1
@@ -232,67 +295,133 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     }
 
     // ---- rotation consistency (ORBmatcher.cc:2146-2190)
-    if (A.mode == MODE_LAST && A.check_ori) {
-        const float factor = 1.0f / HISTO_LENGTH;
-        for (int k = tid; k < nq; k += MATCH_THREADS) {
-            const int j = A.qres[(long long)f * A.q_cap + k];
-            if (j < 0) continue;
-            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
-            if (rot < 0.0) rot += 360.0f;
-            int bin = (int)roundf(rot * factor);
-            if (bin == HISTO_LENGTH) bin = 0;
-            atomicAdd(&s_hist[bin], 1);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < HISTO_LENGTH; i++) {
-                const int s = s_hist[i];
-                if (s > max1) {
-                    max3 = max2;
-                    max2 = max1;
-                    max1 = s;
-                    ind3 = ind2;
-                    ind2 = ind1;
-                    ind1 = i;
-                } else if (s > max2) {
-                    max3 = max2;
-                    max2 = s;
-                    ind3 = ind2;
-                    ind2 = i;
-                } else if (s > max3) {
-                    max3 = s;
-                    ind3 = i;
-                }
-            }
-            if (max2 < 0.1f * (float)max1) {
-                ind2 = -1;
-                ind3 = -1;
-            } else if (max3 < 0.1f * (float)max1) {
-                ind3 = -1;
-            }
-            s_keep[0] = ind1;
-            s_keep[1] = ind2;
-            s_keep[2] = ind3;
-        }
-        __syncthreads();
-        for (int k = tid; k < nq; k += MATCH_THREADS) {
-            const int j = A.qres[(long long)f * A.q_cap + k];
-            if (j < 0) continue;
-            float rot = A.last_kps[(long long)f * A.q_cap + k].angle - K[j].angle;
-            if (rot < 0.0) rot += 360.0f;
-            int bin = (int)roundf(rot * factor);
-            if (bin == HISTO_LENGTH) bin = 0;
-            if (bin == s_keep[0] || bin == s_keep[1] || bin == s_keep[2]) continue;
-            claim[j] = -1;
-            score[j] = 999;
-            atomicSub(&s_nm, 1);
-        }
-        __syncthreads();
-    }
+    if (A.mode == MODE_LAST && A.check_ori) rotation_filter(A, f, nq, K, claim, score, &s_nm, s_hist, s_keep, MATCH_THREADS);
     for (int i = tid; i < n; i += MATCH_THREADS) kp2mp[i] = claim[i];
     if (tid == 0) A.nmatches[f] = s_nm;
 }
+
+// ---- Wave-sequential variant for few, wide queries (SearchByProjection(Cur,
+// Last, th), th = 15 px x scale): the queries run in the reference order, one
+// after the other, and each query's candidate window is scanned by the 64
+// lanes of one wave. Each lane keeps the two smallest (distance, candidate
+// order) pairs of its candidates; a butterfly merge gives the global best
+// and second best, which is exactly what the sequential `dist < bestDist /
+// dist < bestDist2` loop keeps (ties go to the earlier candidate).
+constexpr int SEQ_THREADS = 64;
+
+__device__ __forceinline__ void top2_insert(unsigned long long key, unsigned long long& k1, unsigned long long& k2) {
+    if (key < k1) {
+        k2 = k1;
+        k1 = key;
+    } else if (key < k2) {
+        k2 = key;
+    }
+}
+
+__global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameConst fc) {
+    extern __shared__ __align__(16) int lds[];
+    int* cell_start = lds;                  // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;  // NCELLS
+    int* items = cursor + NCELLS;           // KP_MAX
+    int* claim = items + KP_MAX;            // KP_MAX
+    int* qlist = claim + KP_MAX;            // Q_MAX (also the grid-build scratch)
+    __shared__ int s_nm, s_hist[HISTO_LENGTH], s_keep[3];
+
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int n = min(A.n[f], KP_MAX);
+    const int nq = min(A.m[f], Q_MAX);
+    const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
+    const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
+    int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
+    int32_t* score = A.score + (long long)f * A.kp_cap;
+    if (lane == 0) {
+        s_nm = 0;
+        for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
+    }
+    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, qlist, SEQ_THREADS);
+
+    // ordered list of the queries that project into the image
+    int nvalid = 0;
+    for (int base = 0; base < nq; base += SEQ_THREADS) {
+        const int k = base + lane;
+        bool ok = false;
+        if (k < nq) {
+            if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = -1;
+            ok = make_query(A, fc, f, k).valid;
+        }
+        const unsigned long long m = __ballot(ok);
+        if (ok) qlist[nvalid + __popcll(m & ((1ull << lane) - 1ull))] = k;
+        nvalid += __popcll(m);
+    }
+    __syncthreads();
+
+    const unsigned long long NONE = ~0ull;
+    for (int qi = 0; qi < nvalid; qi++) {
+        const int k = qlist[qi];
+        const Query q = make_query(A, fc, f, k);
+        unsigned long long k1 = NONE, k2 = NONE;
+        // walk the window's columns; candidate order t runs ix-major, then the CSR
+        int col = q.cx0, colStart = 0;
+        int cs = cell_start[col * GRID_ROWS + q.cy0], ce = cell_start[col * GRID_ROWS + q.cy1 + 1];
+        int t = lane;
+        while (col <= q.cx1) {
+            if (t - colStart >= ce - cs) {  // next column
+                colStart += ce - cs;
+                col++;
+                if (col > q.cx1) break;
+                cs = cell_start[col * GRID_ROWS + q.cy0];
+                ce = cell_start[col * GRID_ROWS + q.cy1 + 1];
+                continue;
+            }
+            const int idx = items[cs + (t - colStart)];
+            const gf_keypoint kp = K[idx];
+            if (level_ok(kp.octave, q.minL, q.maxL) && !(fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) &&
+                claim[idx] < 0) {
+                const int dist = hamming32(q.d, D + (long long)idx * 32);
+                top2_insert(((unsigned long long)dist << 40) | ((unsigned long long)t << 8) |
+                                (unsigned long long)(kp.octave & 0xff),
+                            k1, k2);
+            }
+            t += SEQ_THREADS;
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long o1 = __shfl_xor(k1, o, 64), o2 = __shfl_xor(k2, o, 64);
+            top2_insert(o1, k1, k2);
+            top2_insert(o2, k1, k2);
+        }
+        if (lane == 0 && k1 != NONE) {
+            const int bestDist = (int)(k1 >> 40);
+            const int bestLevel = (int)(k1 & 0xff);
+            const int bestDist2 = k2 == NONE ? INT_MAX : (int)(k2 >> 40);
+            const int bestLevel2 = k2 == NONE ? -1 : (int)(k2 & 0xff);
+            if (bestDist <= TH_HIGH) {
+                const bool reject = A.mode == MODE_PROJECT && bestLevel == bestLevel2 &&
+                                    (float)bestDist > A.nnratio * (float)bestDist2;
+                if (!reject) {
+                    // candidate order -> keypoint index
+                    int tt = (int)((k1 >> 8) & 0xffffffffull), c = q.cx0;
+                    for (;; c++) {
+                        const int len = cell_start[c * GRID_ROWS + q.cy1 + 1] - cell_start[c * GRID_ROWS + q.cy0];
+                        if (tt < len) break;
+                        tt -= len;
+                    }
+                    const int bestIdx = items[cell_start[c * GRID_ROWS + q.cy0] + tt];
+                    claim[bestIdx] = q.id;
+                    score[bestIdx] = bestDist;
+                    s_nm++;
+                    if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = bestIdx;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (A.mode == MODE_LAST && A.check_ori) rotation_filter(A, f, nq, K, claim, score, &s_nm, s_hist, s_keep, SEQ_THREADS);
+    for (int i = lane; i < n; i += SEQ_THREADS) kp2mp[i] = claim[i];
+    if (lane == 0) A.nmatches[f] = s_nm;
+}
+
+size_t seq_lds_bytes() { return sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX + Q_MAX); }
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
@@ -389,10 +518,17 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
     if (!(attr_mask & (1ull << ctx->device))) {
         GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)match_lds_bytes()));
+        GF_HIP(hipFuncSetAttribute((const void*)k_match_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)seq_lds_bytes()));
         attr_mask |= 1ull << ctx->device;
     }
-    GF_PROF(ctx, s, A.mode == MODE_PROJECT ? "k_match_project" : "k_match_lastframe");
-    k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
+    if (A.mode == MODE_LAST) {  // few queries, wide windows: wave-sequential in the reference order
+        GF_PROF(ctx, s, "k_match_lastframe");
+        k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(), s>>>(A, fc);
+    } else {  // many queries, narrow windows: claim-resolution rounds
+        GF_PROF(ctx, s, "k_match_project");
+        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
+    }
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

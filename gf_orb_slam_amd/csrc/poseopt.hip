@@ -69,7 +69,7 @@ __device__ __forceinline__ void edge_error(const Lane& L, const gfse3::SE3& T, i
 
 // computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
 // Returns the sums in sh_sum: [0,21) lower H row-major-packed, [21,27) b, 27 chi2.
-__device__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[65], double* sh_sum) {
+__device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[65], double* sh_sum) {
     double acc = 0.0;
     for (int base = 0; base < L.n; base += 64) {
         const int e = base + L.l;
@@ -112,7 +112,17 @@ __device__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*te
         __syncthreads();
         const int m = min(64, L.n - base);
         if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
-            for (int j = 0; j < m; j++) acc += term[L.l][j];
+            // edge order, one dependent add per edge; loads batched ahead of the chain
+            const double* row = term[L.l];
+            int j = 0;
+            for (; j + 8 <= m; j += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = row[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) acc += v[u];
+            }
+            for (; j < m; j++) acc += row[j];
         }
         __syncthreads();
     }
@@ -157,15 +167,16 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
     }
     __syncthreads();
 
-    const double chi2t[4] = {(double)9.210f, (double)7.378f, (double)5.991f, (double)5.991f};
-    const int its[4] = {10, 10, 7, 5};
+    // chi2 thresholds {9.210, 7.378, 5.991, 5.991} (float) and iterations {10, 10, 7, 5}
     int nBadEdges = 0, total_it = 0;
     double xs[6] = {0, 0, 0, 0, 0, 0};
     for (int round = 0; round < 4 && L.n > 0; round++) {
-        // SparseOptimizer::optimize(its[round]) with the Levenberg algorithm
+        const double chi2th = round == 0 ? (double)9.210f : round == 1 ? (double)7.378f : (double)5.991f;
+        const int its = round < 2 ? 10 : round == 2 ? 7 : 5;
+        // SparseOptimizer::optimize(its) with the Levenberg algorithm
         double lambda = 0, ni = 2;
         int nBad = 0;
-        for (int iter = 0; iter < its[round]; iter++) {
+        for (int iter = 0; iter < its; iter++) {
             total_it++;
             pass(L, T, true, term, sh_sum);
             double H[36], b[6];
@@ -237,11 +248,11 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                 }
                 const double r0 = L.e0[e], r1 = L.e1[e], info = L.info[e];
                 const double c2 = r0 * (info * r0) + r1 * (info * r1);
-                if (c2 > chi2t[round]) {
+                if (c2 > chi2th) {
                     ou[e] = 1;
                     L.info[e] = 1e-10;
                     bad = true;
-                } else if (c2 <= chi2t[round]) {
+                } else if (c2 <= chi2th) {
                     ou[e] = 0;
                 }
             }

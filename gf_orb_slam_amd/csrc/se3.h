@@ -120,15 +120,20 @@ SE3_HD SE3 exp_mul(const double* u, const SE3& T) {
     const double theta = sqrt((w0 * w0 + w1 * w1) + w2 * w2);
     const double O[9] = {0, -w2, w1, w2, 0, -w0, -w1, w0, 0};
     double O2[9];
+#pragma unroll
     for (int i = 0; i < 3; i++)
+#pragma unroll
         for (int j = 0; j < 3; j++) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
     double R[9], V[9];
     if (theta < 0.00001) {
+#pragma unroll
         for (int i = 0; i < 9; i++) R[i] = ((i % 4 == 0 ? 1.0 : 0.0) + O[i]) + O2[i];
+#pragma unroll
         for (int i = 0; i < 9; i++) V[i] = R[i];
     } else {
         const double s = sin(theta), c = cos(theta);
         const double a = s / theta, b = (1 - c) / (theta * theta), cc = (theta - s) / pow(theta, 3.0);  // libm pow(double, double)
+#pragma unroll
         for (int i = 0; i < 9; i++) {
             const double I = i % 4 == 0 ? 1.0 : 0.0;
             R[i] = (I + a * O[i]) + b * O2[i];
@@ -151,62 +156,87 @@ SE3_HD SE3 exp_mul(const double* u, const SE3& T) {
 
 // Eigen::LDLT (lower, diagonal pivoting) factor + solve of the 6x6 system
 // A x = b; A row-major, only its lower triangle is read. Returns isPositive().
-// x is written only when the factorisation is positive.
-SE3_HD bool ldlt6(const double* Ain, const double* b, double* x) {
-    const int n = 6;
-    double A[36];
-    for (int i = 0; i < 36; i++) A[i] = Ain[i];
-    int perm[6];
-    bool found_zero = false;
-    int sign = 0;  // 0 zero, 1 psd, 2 nsd, 3 indefinite
-    double temp[6];
-    for (int k = 0; k < n; ++k) {
-        int big = k;
-        double bv = fabs(A[k * n + k]);
-        for (int i = k + 1; i < n; i++)
-            if (fabs(A[i * n + i]) > bv) bv = fabs(A[i * n + i]), big = i;
-        perm[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; j++) {
-                double t = A[k * n + j];
-                A[k * n + j] = A[big * n + j];
-                A[big * n + j] = t;
-            }
-            for (int i = big + 1; i < n; i++) {
-                double t = A[i * n + k];
-                A[i * n + k] = A[i * n + big];
-                A[i * n + big] = t;
-            }
-            double t = A[k * n + k];
-            A[k * n + k] = A[big * n + big];
-            A[big * n + big] = t;
-            for (int i = k + 1; i < big; i++) {
-                double t2 = A[i * n + k];
-                A[i * n + k] = A[big * n + i];
-                A[big * n + i] = t2;
-            }
-        }
-        if (k > 0) {
-            for (int j = 0; j < k; j++) temp[j] = A[j * n + j] * A[k * n + j];
+// x is written only when the factorisation is positive. Every array index is
+// a compile-time constant (template recursion over the pivot step, pivot
+// swaps selected by comparison), so A stays in registers on the device; the
+// arithmetic and its order are those of Eigen's ldlt_inplace<Lower>::unblocked
+// and LDLT::_solve_impl.
+namespace ldlt_detail {
+
+// conditional exchange as two selects (no branch, no address arithmetic)
+SE3_HD void csw(bool c, double& a, double& b) {
+    const double ta = c ? b : a, tb = c ? a : b;
+    a = ta;
+    b = tb;
+}
+
+// symmetric swap of row/column K and B (K < B) within the lower triangle, if c
+template <int K, int B>
+SE3_HD void sym_swap(double (&A)[36], bool c) {
+#pragma unroll
+    for (int j = 0; j < K; j++) csw(c, A[K * 6 + j], A[B * 6 + j]);
+#pragma unroll
+    for (int i = B + 1; i < 6; i++) csw(c, A[i * 6 + K], A[i * 6 + B]);
+    csw(c, A[K * 7], A[B * 7]);
+#pragma unroll
+    for (int i = K + 1; i < B; i++) csw(c, A[i * 6 + K], A[B * 6 + i]);
+}
+
+template <int K, int B>
+SE3_HD void pivot(double (&A)[36], int big) {
+    if constexpr (B < 6) {
+        sym_swap<K, B>(A, big == B);
+        pivot<K, B + 1>(A, big);
+    }
+}
+
+template <int K, int B>
+SE3_HD void perm_vec(double (&y)[6], int p) {
+    if constexpr (B < 6) {
+        csw(p == B, y[K], y[B]);
+        perm_vec<K, B + 1>(y, p);
+    }
+}
+
+template <int K>
+SE3_HD void step(double (&A)[36], int (&perm)[6], int& sign, bool& stop) {
+    if constexpr (K < 6) {
+        int big = K;
+        double bv = fabs(A[K * 7]);
+#pragma unroll
+        for (int i = K + 1; i < 6; i++)
+            if (fabs(A[i * 7]) > bv) bv = fabs(A[i * 7]), big = i;
+        perm[K] = big;
+        pivot<K, K + 1>(A, big);
+        if constexpr (K > 0) {
+            double temp[K];
+#pragma unroll
+            for (int j = 0; j < K; j++) temp[j] = A[j * 7] * A[K * 6 + j];
             double s = 0;
-            for (int j = 0; j < k; j++) s += A[k * n + j] * temp[j];
-            A[k * n + k] -= s;
-            for (int i = k + 1; i < n; i++) {
+#pragma unroll
+            for (int j = 0; j < K; j++) s += A[K * 6 + j] * temp[j];
+            A[K * 7] -= s;
+#pragma unroll
+            for (int i = K + 1; i < 6; i++) {
                 double t = 0;
-                for (int j = 0; j < k; j++) t += A[i * n + j] * temp[j];
-                A[i * n + k] -= t;
+#pragma unroll
+                for (int j = 0; j < K; j++) t += A[i * 6 + j] * temp[j];
+                A[i * 6 + K] -= t;
             }
         }
-        const double akk = A[k * n + k];
+        const double akk = A[K * 7];
         const bool valid = fabs(akk) > 0;
-        if (k == 0 && !valid) {
+        if (K == 0 && !valid) {  // zero matrix: identity transpositions, ZeroSign
             sign = 0;
-            for (int j = 0; j < n; j++) perm[j] = j;
-            break;
+#pragma unroll
+            for (int j = 0; j < 6; j++) perm[j] = j;
+            stop = true;
+            return;
         }
-        if (valid)
-            for (int i = k + 1; i < n; i++) A[i * n + k] /= akk;
-        if (!valid) found_zero = true;
+        if (valid) {
+#pragma unroll
+            for (int i = K + 1; i < 6; i++) A[i * 6 + K] /= akk;
+        }
         if (sign == 1) {
             if (akk < 0) sign = 3;
         } else if (sign == 2) {
@@ -217,30 +247,54 @@ SE3_HD bool ldlt6(const double* Ain, const double* b, double* x) {
             else if (akk < 0)
                 sign = 2;
         }
+        step<K + 1>(A, perm, sign, stop);
     }
-    (void)found_zero;
+}
+
+}  // namespace ldlt_detail
+
+SE3_HD bool ldlt6(const double* Ain, const double* b, double* x) {
+    double A[36];
+#pragma unroll
+    for (int i = 0; i < 36; i++) A[i] = Ain[i];
+    int perm[6];
+    int sign = 0;  // 0 zero, 1 psd, 2 nsd, 3 indefinite
+    bool stop = false;
+    ldlt_detail::step<0>(A, perm, sign, stop);
     if (!(sign == 1 || sign == 0)) return false;
     double y[6];
-    for (int i = 0; i < n; i++) y[i] = b[i];
-    for (int k = 0; k < n; k++) {
-        double t = y[k];
-        y[k] = y[perm[k]];
-        y[perm[k]] = t;
-    }
-    for (int j = 0; j < n; j++)
-        for (int i = j + 1; i < n; i++) y[i] -= A[i * n + j] * y[j];
-    for (int i = 0; i < n; i++) y[i] = fabs(A[i * n + i]) > DBL_MIN ? y[i] / A[i * n + i] : 0.0;
-    for (int i = n - 1; i >= 0; i--) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] = b[i];
+    // y = P b
+    ldlt_detail::perm_vec<0, 1>(y, perm[0]);
+    ldlt_detail::perm_vec<1, 2>(y, perm[1]);
+    ldlt_detail::perm_vec<2, 3>(y, perm[2]);
+    ldlt_detail::perm_vec<3, 4>(y, perm[3]);
+    ldlt_detail::perm_vec<4, 5>(y, perm[4]);
+    // L^-1 (unit lower, column axpy order)
+#pragma unroll
+    for (int j = 0; j < 6; j++)
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) y[i] -= A[i * 6 + j] * y[j];
+    // D^+ (pseudo-inverse below numeric_limits<double>::min())
+#pragma unroll
+    for (int i = 0; i < 6; i++) y[i] = fabs(A[i * 7]) > DBL_MIN ? y[i] / A[i * 7] : 0.0;
+    // L^-T
+#pragma unroll
+    for (int i = 5; i >= 0; i--) {
         double s = 0;
-        for (int k = i + 1; k < n; k++) s += A[k * n + i] * y[k];
+#pragma unroll
+        for (int k = i + 1; k < 6; k++) s += A[k * 6 + i] * y[k];
         y[i] -= s;
     }
-    for (int k = n - 1; k >= 0; k--) {
-        double t = y[k];
-        y[k] = y[perm[k]];
-        y[perm[k]] = t;
-    }
-    for (int i = 0; i < n; i++) x[i] = y[i];
+    // P^-1
+    ldlt_detail::perm_vec<4, 5>(y, perm[4]);
+    ldlt_detail::perm_vec<3, 4>(y, perm[3]);
+    ldlt_detail::perm_vec<2, 3>(y, perm[2]);
+    ldlt_detail::perm_vec<1, 2>(y, perm[1]);
+    ldlt_detail::perm_vec<0, 1>(y, perm[0]);
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = y[i];
     return true;
 }
 
