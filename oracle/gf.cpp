@@ -384,9 +384,13 @@ double logdet7(const double* M) {
 }
 
 // ------------------------------------------------------------ RNG
+static int g_rand_calls = 0;  // rand() calls of the last active-match / max-vol call
+
 struct Rand {  // glibc random_r TYPE_3 (the generator behind std::rand)
     struct random_data rd;
     char state[128];
+    ~Rand() { g_rand_calls = calls; }
+    int calls = 0;
     void seed(unsigned s) {
         std::memset(&rd, 0, sizeof(rd));
         initstate_r(s, state, sizeof(state), &rd);
@@ -394,6 +398,7 @@ struct Rand {  // glibc random_r TYPE_3 (the generator behind std::rand)
     int next() {
         int32_t r;
         random_r(&rd, &r);
+        calls++;
         return r;
     }
 };
@@ -725,5 +730,8 @@ int orc_maxvol_select(const double* info, const double* score, int n, int k, dou
         if (pool[i].selected) out_idx[(*nout)++] = i;
     return GF_OK;
 }
+
+// rand() calls made by the last orc_obs_active_match / orc_maxvol_select
+int orc_last_rand_calls(void) { return orc::g_rand_calls; }
 
 }  // extern "C"

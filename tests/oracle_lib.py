@@ -155,6 +155,11 @@ def active_match(info_fi, kps, desc, views, mp_desc, updated, info, H, uv, base,
     return nmatched.value, left[:nleft.value].copy()
 
 
+def last_rand_calls():
+    """std::rand() calls made by the last active_match / maxvol_select."""
+    return orc().orc_last_rand_calls()
+
+
 def maxvol_select(info, score, k, sample_scale, mode, seed):
     info = np.ascontiguousarray(info, np.float64).reshape(-1, 49)
     n = len(info)

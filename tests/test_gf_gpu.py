@@ -85,26 +85,57 @@ def _active_case(seed, nmp=2500, nkp=1000, num_to_match=40, frac_updated=0.9):
     return sc, info_fi, F, views, ob, H, info, uv, updated, base, num_to_match
 
 
-@pytest.mark.parametrize("seed,ntm", [(1, 40), (2, 100), (3, 7), (4, 400), (5, 0)])
-def test_active_matching_bit_exact(seed, ntm):
-    sc, info_fi, F, views, ob, H, info, uv, updated, base, _ = _active_case(seed, num_to_match=ntm)
+def _check_active(sc, info_fi, F, views, ob, H, info, uv, updated, base, ntm, seed, mp_desc=None):
+    mp_desc = sc["mp_desc"] if mp_desc is None else mp_desc
     kp2mp, score = F.mvpMapPoints.copy(), F.mvpMatchScore.copy()
     sig2 = (info_fi.scale_factors() ** 2).astype(np.float32)
     ob.rng = Rng.seeded(seed)
-    ng = ob.runActiveMapMatching(F, views, sc["mp_desc"], updated, info, H, uv, base, ntm)
-    no, left_o = O.active_match(info_fi, sc["keypoints"], sc["descriptors"], views, sc["mp_desc"], updated, info, H,
+    ng = ob.runActiveMapMatching(F, views, mp_desc, updated, info, H, uv, base, ntm)
+    no, left_o = O.active_match(info_fi, sc["keypoints"], sc["descriptors"], views, mp_desc, updated, info, H,
                                 uv, base, sig2, ntm, 1.0, 0.8, seed, kp2mp, score)
+    calls = O.last_rand_calls()
     assert ng == no
     np.testing.assert_array_equal(F.mvpMapPoints, kp2mp)
     np.testing.assert_array_equal(F.mvpMatchScore, score)
     np.testing.assert_array_equal(ob.mLeftMapPoints, left_o)
-    if ntm:
-        assert ng > 0
-        # the RNG advanced exactly as std::rand would have
-        ref = Rng.seeded(seed)
-        ref_seq = O.rand_sequence(seed, 200000)
-        nxt = ob.rng.next(1)[0]
-        assert nxt in ref_seq
+    # the RNG advanced exactly as std::rand would have: same ring, same position
+    ref = Rng.seeded(seed)
+    if calls:
+        ref.next(calls)
+    assert bytes(ob.rng) == bytes(ref)
+    return ng, calls
+
+
+@pytest.mark.parametrize("seed,ntm", [(1, 40), (2, 100), (3, 7), (4, 400), (5, 0), (6, 1), (7, 3000)])
+def test_active_matching_bit_exact(seed, ntm):
+    case = _active_case(seed, num_to_match=ntm)
+    ng, calls = _check_active(*case[:-1], ntm, seed)
+    if 1 < ntm < 1000:  # S = N (ntm 1) exhausts after one failure; ntm > N gives S = 0 (reference quirks)
+        assert ng > 0 and calls > 0
+
+
+def test_active_matching_tied_and_nan_scores():
+    """Equal log-dets (duplicated information blocks) and NaN scores make the
+    std::priority_queue order depend on its history: the device must replay it."""
+    sc, info_fi, F, views, ob, H, info, uv, updated, base, _ = _active_case(11, num_to_match=40)
+    info = info.copy()
+    idx = np.nonzero(views["in_view"] & updated)[0]
+    info[idx[::3]] = info[idx[0]]            # many exact ties
+    info[idx[1::17]] = np.nan                # NaN log-dets
+    _check_active(sc, info_fi, F, views, ob, H, info, uv, updated, base, 40, 11)
+
+
+def test_active_matching_exhausted_draws():
+    """A tiny pool whose points never match: every column gets visited, the
+    next draw gives up after MAX_RANDOM_QUERY_TIME tries (early termination)."""
+    sc, info_fi, F, views, ob, H, info, uv, updated, base, _ = _active_case(12, num_to_match=1)
+    upd = np.zeros_like(updated)
+    idx = np.nonzero(views["in_view"])[0][:5]
+    upd[idx] = 1
+    mp_desc = sc["mp_desc"].copy()
+    mp_desc[idx] = np.random.default_rng(5).integers(0, 256, (len(idx), 32), dtype=np.uint8) * 0 + 0xFF
+    ng, calls = _check_active(sc, info_fi, F, views, ob, H, info, uv, upd, base, 1, 12, mp_desc=mp_desc)
+    assert ng == 0 and calls >= 2000
 
 
 @pytest.mark.parametrize("k,mode", [(60, 1), (100, 1), (60, 2), (140, 2), (100, 3), (250, 3)])
