@@ -107,6 +107,11 @@ _PROTOS = {
     "gf_pose_opt": [_P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
     "gf_pose_opt_batch_dev": [_P, _I, _P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
     "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P, _P],
+    "gf_local_ba": [_P, _P, _P],
+    "gf_ba_plan_create": [_P, _I, _P, _P],
+    "gf_ba_plan_solve": [_P, _P, _P],
+    "gf_ba_plan_results": [_P, _P],
+    "gf_ba_plan_destroy": [_P],
 }
 
 

@@ -1,0 +1,1170 @@
+// Local bundle adjustment on gfx950.
+//
+// Optimizer::LocalBundleAdjustment (src/Optimizer.cc:1515-1764) builds a g2o
+// graph — local keyframe poses (SE3; mnId 0 fixed), fixed observer cameras,
+// marginalised map points, one Huber EdgeSE3ProjectXYZ per observation — and
+// runs optimize(5), removes the edges with chi2 > 5.991 or negative depth,
+// runs optimize(10) and flags the outliers again. The device keeps g2o's
+// Levenberg-Marquardt (core/optimization_algorithm_levenberg.cpp:61-189) and
+// its Schur solve (BlockSolver::solve, core/block_solver.hpp:354-486) as a
+// state machine per problem in device memory. One host-enqueued step is one
+// LM trial of every problem of the batch:
+//
+//   k_ba_linearize  computeActiveErrors + the point half of buildSystem, one
+//                   thread per map point: Hll, b_l, the 6x3 Hpl block of every
+//                   edge (also written into the dense K-major panel Ht), robust
+//                   chi2 partial sums
+//   k_ba_poses      the pose half: Hpp, b_p, one wave per free pose over its
+//                   edge list
+//   k_ba_schur_pts  lambda init, Dinv = (Hll + lambda I)^-1, db = Dinv b_l and
+//                   W = Hpl Dinv into the panel Wt, db as Wt's column n
+//   k_ba_gemm       C = Ht^T Wt on v_mfma_f64_16x16x4 (split-K, fixed order):
+//                   the Schur product Hpl Dinv Hpl^T and the coefficient
+//                   vector Hpl db in one pass — the J^T J-shaped contraction
+//   k_ba_solve      S = Hpp + lambda I - C, b_s = b_p - C[:, n]; dense LL^T
+//                   and the triangular solves in LDS; trial poses exp(x) * T
+//   k_ba_update     landmark back-substitution, trial points, trial errors
+//   k_ba_decide     rho, lambda schedule and stop rules (levenberg.cpp:99-163);
+//                   at the end of optimize(5) / optimize(10) the outlier pass
+//                   (Optimizer.cc:1680-1698, 1724-1743)
+//
+// Every kernel reads the problem's state first and returns at once when the
+// step does not concern it, so the host enqueues steps blindly and polls the
+// done flags every few steps. Floating-point parity with the oracle is a
+// tolerance (the reference's CHOLMOD is unpinned, and the Schur sums run in
+// MFMA order); the LL^T itself and the triangular solves use the oracle's
+// exact operation order.
+#include <float.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "se3.h"
+
+namespace {
+
+constexpr int BA_T = 256;     // threads of the point kernels
+constexpr int BA_NSPLIT = 8;  // split-K of the Schur GEMM
+constexpr int BA_MAXFREE = 32;
+constexpr int BA_MAXN = 6 * BA_MAXFREE;  // LDS of k_ba_solve
+constexpr int BA_MAXPTS = 65536;
+constexpr int BA_MAXSTEPS = 400;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+struct BADesc {
+    int nkf, npts, nedges, nfree;
+    int n, npad, K, sps;  // 6 * nfree; panel width; panel rows; MFMA k-steps per split
+    int ntiles, nwg;      // Schur GEMM tiles; point workgroups
+    int kf0, pt0, e0, f0, fe0, pl0, tile0, wg0;
+    long long panel0;  // Ht at panel0, Wt at panel0 + K * npad (doubles)
+};
+
+struct BAState {
+    int round;     // 0: optimize(5), 1: optimize(10), 2: done
+    int iter, q;   // outer iteration of the round, trial of the iteration
+    int need_lin;  // next step starts an iteration (errors + buildSystem)
+    int cur;       // estimate buffer holding the current state
+    int chol_ok, nbad, pad;
+    int iters[2];
+    double lambda, ni, currentChi, iniChi, scale_p;
+};
+
+struct BAArena {
+    const BADesc* desc;
+    BAState* st;
+    int nkf_tot, npt_tot;
+    // keyframes: [2][nkf_tot][8] = q(w,x,y,z), t(3), pad
+    double* kfT;
+    const float* kf_Tcw0;
+    const uint8_t* kf_kind;
+    const int32_t* kf_col;  // free pose index or -1
+    // points: [2][npt_tot][4]
+    double* ptX;
+    const float* pt_pos0;
+    const int32_t* pt_eb;  // problem-local edge range [eb, ee)
+    const int32_t* pt_ee;
+    double *Hll, *bl, *Dinv, *xl;  // 9, 3, 9, 3 per point
+    uint8_t* pt_act;
+    // edges
+    const int32_t* e_pt;   // problem-local
+    const int32_t* e_kf;   // problem-local
+    const double* e_meas;  // 8: z0, z1, info, fx, fy, cx, cy, 0
+    double* e_err;         // 2: errors of the last evaluated estimate
+    uint8_t* e_act;
+    uint8_t* e_out;
+    double* Hpl;  // 18 per edge (6x3 row-major)
+    // free poses
+    const int32_t* f_kf;
+    const int32_t* f_eptr;   // nfree + 1 per problem, into f_elist (problem-local)
+    const int32_t* f_elist;  // problem-local edge indices, point order
+    double *Hpp, *bp, *xp;   // 36, 6, 6 per free pose
+    uint8_t* f_act;
+    // dense panels, GEMM tiles, per-workgroup partial sums
+    double* panel;
+    double* tiles;
+    double *wg_chi, *wg_chi_t, *wg_maxd, *wg_scale;
+    // outputs
+    float* out_T;
+    float* out_X;
+};
+
+__device__ __forceinline__ gfse3::SE3 load_T(const BAArena& A, int buf, int gk) {
+    const double* p = A.kfT + ((size_t)buf * A.nkf_tot + gk) * 8;
+    gfse3::SE3 s;
+    s.r.w = p[0];
+    s.r.x = p[1];
+    s.r.y = p[2];
+    s.r.z = p[3];
+    s.t[0] = p[4];
+    s.t[1] = p[5];
+    s.t[2] = p[6];
+    return s;
+}
+
+__device__ __forceinline__ void store_T(const BAArena& A, int buf, int gk, const gfse3::SE3& s) {
+    double* p = A.kfT + ((size_t)buf * A.nkf_tot + gk) * 8;
+    p[0] = s.r.w;
+    p[1] = s.r.x;
+    p[2] = s.r.y;
+    p[3] = s.r.z;
+    p[4] = s.t[0];
+    p[5] = s.t[1];
+    p[6] = s.t[2];
+}
+
+__device__ __forceinline__ double* ptX_at(const BAArena& A, int buf, int gp) {
+    return A.ptX + ((size_t)buf * A.npt_tot + gp) * 4;
+}
+
+__device__ __forceinline__ void huber(double e, double& rho0, double& rho1) {
+    const double delta = (double)(float)sqrt(5.991);  // const float thHuber = sqrt(5.991)
+    const double dsqr = delta * delta;
+    if (e <= dsqr) {
+        rho0 = e;
+        rho1 = 1.;
+    } else {
+        const double s = sqrt(e);
+        rho0 = 2 * s * delta - dsqr;
+        rho1 = delta / s;
+    }
+}
+
+// EdgeSE3ProjectXYZ::computeError; pc = T.map(X)
+__device__ __forceinline__ void edge_error(const double* m, const gfse3::SE3& T, const double* X, double* pc,
+                                           double& e0, double& e1) {
+    gfse3::map(T, X, pc);
+    const double px = pc[0] / pc[2], py = pc[1] / pc[2];
+    e0 = m[0] - (px * m[3] + m[5]);
+    e1 = m[1] - (py * m[4] + m[6]);
+}
+
+// EdgeSE3ProjectXYZ::linearizeOplus: point (2x3) and pose (2x6) Jacobians.
+__device__ __forceinline__ void edge_jac(const double* m, const gfse3::SE3& T, const double* pc, double (*Jp)[3],
+                                         double (*Jc)[6], bool want_point) {
+    const double fx = m[3], fy = m[4];
+    const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
+    if (want_point) {
+        double R[9];
+        gfse3::to_R(T.r, R);
+        const double s = -1. / z;
+        const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                Jp[i][j] = ((s * tmp[i][0]) * R[j] + (s * tmp[i][1]) * R[3 + j]) + (s * tmp[i][2]) * R[6 + j];
+    }
+    Jc[0][0] = x * y / z2 * fx;
+    Jc[0][1] = -(1 + (x * x / z2)) * fx;
+    Jc[0][2] = y / z * fx;
+    Jc[0][3] = -1. / z * fx;
+    Jc[0][4] = 0;
+    Jc[0][5] = x / z2 * fx;
+    Jc[1][0] = (1 + y * y / z2) * fy;
+    Jc[1][1] = -x * y / z2 * fy;
+    Jc[1][2] = -x / z * fy;
+    Jc[1][3] = 0;
+    Jc[1][4] = -1. / z * fy;
+    Jc[1][5] = y / z2 * fy;
+}
+
+// Workgroup sum / max of one double per thread in a fixed order.
+__device__ double block_reduce(double v, double* sh, bool is_max) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double u = __shfl_xor(v, o, 64);
+        v = is_max ? fmax(v, u) : v + u;
+    }
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double r = sh[0];
+    for (int i = 1; i < nw; i++) r = is_max ? fmax(r, sh[i]) : r + sh[i];
+    __syncthreads();
+    return r;
+}
+
+// Eigen compute_inverse<Matrix3d> (oracle/lba.cpp inverse3).
+__device__ __forceinline__ void inverse3(const double* m, double* r) {
+    const double c0 = m[4] * m[8] - m[5] * m[7];
+    const double c1 = m[7] * m[2] - m[8] * m[1];
+    const double c2 = m[1] * m[5] - m[2] * m[4];
+    const double det = (c0 * m[0] + c1 * m[3]) + c2 * m[6];
+    const double inv = 1.0 / det;
+    r[0] = c0 * inv;
+    r[1] = c1 * inv;
+    r[2] = c2 * inv;
+    r[3] = (m[5] * m[6] - m[3] * m[8]) * inv;
+    r[4] = (m[8] * m[0] - m[6] * m[2]) * inv;
+    r[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+    r[6] = (m[3] * m[7] - m[4] * m[6]) * inv;
+    r[7] = (m[6] * m[1] - m[7] * m[0]) * inv;
+    r[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
+}
+
+// ------------------------------------------------------------------ init
+__global__ __launch_bounds__(256) void k_ba_init(BAArena A) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const BADesc d = A.desc[p];
+    for (int k = tid; k < d.nkf; k += 256) {  // Converter::toSE3Quat
+        const float* T = A.kf_Tcw0 + (size_t)(d.kf0 + k) * 16;
+        double R[9];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R[3 * i + j] = (double)T[4 * i + j];
+        gfse3::SE3 s;
+        s.r = gfse3::from_R(R);
+        for (int i = 0; i < 3; i++) s.t[i] = (double)T[4 * i + 3];
+        gfse3::normalize(s.r);
+        store_T(A, 0, d.kf0 + k, s);
+    }
+    for (int i = tid; i < d.npts; i += 256) {
+        double* X = ptX_at(A, 0, d.pt0 + i);
+        for (int c = 0; c < 3; c++) X[c] = (double)A.pt_pos0[(size_t)(d.pt0 + i) * 3 + c];
+        for (int c = 0; c < 3; c++) A.xl[(size_t)(d.pt0 + i) * 3 + c] = 0.0;
+    }
+    for (int e = tid; e < d.nedges; e += 256) {
+        A.e_act[d.e0 + e] = 1;
+        A.e_out[d.e0 + e] = 0;
+    }
+    for (int i = tid; i < 6 * d.nfree; i += 256) A.xp[(size_t)d.f0 * 6 + i] = 0.0;
+    if (tid == 0) {
+        BAState s{};
+        s.round = d.nedges > 0 ? 0 : 2;
+        s.iters[0] = d.nedges > 0 ? 0 : -1;
+        s.iters[1] = d.nedges > 0 ? 0 : -1;
+        s.need_lin = 1;
+        s.ni = 2;
+        A.st[p] = s;
+    }
+}
+
+// ------------------------------------------------------------------ buildSystem, point half
+__global__ __launch_bounds__(BA_T) void k_ba_linearize(BAArena A) {
+    __shared__ double sh[BA_T / 64];
+    const int p = blockIdx.y;
+    const BADesc d = A.desc[p];
+    if (blockIdx.x >= d.nwg) return;
+    const BAState st = A.st[p];
+    if (st.round >= 2 || !st.need_lin) return;
+    const int i = blockIdx.x * BA_T + threadIdx.x;
+    double chi = 0.0, maxd = 0.0;
+    if (i < d.npts) {
+        const int gp = d.pt0 + i, cur = st.cur;
+        const double* Xp = ptX_at(A, cur, gp);
+        const double X[3] = {Xp[0], Xp[1], Xp[2]};
+        double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+        int nact = 0;
+        const int eb = A.pt_eb[gp], ee = A.pt_ee[gp];
+        for (int le = eb; le < ee; le++) {
+            const int ge = d.e0 + le;
+            if (!A.e_act[ge]) continue;
+            nact++;
+            const int kf = A.e_kf[ge];
+            const double* m = A.e_meas + (size_t)ge * 8;
+            const gfse3::SE3 T = load_T(A, cur, d.kf0 + kf);
+            double pc[3], e0, e1;
+            edge_error(m, T, X, pc, e0, e1);
+            const double info = m[2];
+            double rho0, rho1;
+            huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
+            chi += rho0;
+            double Jp[2][3], Jc[2][6];
+            edge_jac(m, T, pc, Jp, Jc, true);
+            const double w = rho1 * info;
+            const double o0 = -(info * e0) * rho1, o1 = -(info * e1) * rho1;
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                b[r] += Jp[0][r] * o0 + Jp[1][r] * o1;
+#pragma unroll
+                for (int c = 0; c < 3; c++) H[3 * r + c] += (Jp[0][r] * w) * Jp[0][c] + (Jp[1][r] * w) * Jp[1][c];
+            }
+            const int col = A.kf_col[d.kf0 + kf];
+            if (col >= 0) {  // Hpl = B^T W A, also the panel Ht[3 i + c][6 col + r]
+                double* hp = A.Hpl + (size_t)ge * 18;
+                double* Ht = A.panel + d.panel0;
+#pragma unroll
+                for (int r = 0; r < 6; r++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const double v = (Jc[0][r] * w) * Jp[0][c] + (Jc[1][r] * w) * Jp[1][c];
+                        hp[3 * r + c] = v;
+                        Ht[(size_t)(3 * i + c) * d.npad + 6 * col + r] = v;
+                    }
+            }
+        }
+        double* Hg = A.Hll + (size_t)gp * 9;
+        for (int k = 0; k < 9; k++) Hg[k] = H[k];
+        for (int k = 0; k < 3; k++) A.bl[(size_t)gp * 3 + k] = b[k];
+        A.pt_act[gp] = nact > 0;
+        if (nact) maxd = fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+    }
+    const double cs = block_reduce(chi, sh, false);
+    const double mx = block_reduce(maxd, sh, true);
+    if (threadIdx.x == 0) {
+        A.wg_chi[d.wg0 + blockIdx.x] = cs;
+        A.wg_maxd[d.wg0 + blockIdx.x] = mx;
+    }
+}
+
+// ------------------------------------------------------------------ buildSystem, pose half
+__global__ __launch_bounds__(64) void k_ba_poses(BAArena A) {
+    const int p = blockIdx.y, a = blockIdx.x, lane = threadIdx.x;
+    const BADesc d = A.desc[p];
+    if (a >= d.nfree) return;
+    const BAState st = A.st[p];
+    if (st.round >= 2 || !st.need_lin) return;
+    const int cur = st.cur;
+    const int kf = A.f_kf[d.f0 + a];
+    const gfse3::SE3 T = load_T(A, cur, d.kf0 + kf);
+    double acc[27];
+#pragma unroll
+    for (int k = 0; k < 27; k++) acc[k] = 0.0;
+    int cnt = 0;
+    const int j0 = A.f_eptr[d.fe0 + a], j1 = A.f_eptr[d.fe0 + a + 1];
+    for (int j = j0 + lane; j < j1; j += 64) {
+        const int ge = d.e0 + A.f_elist[d.pl0 + j];
+        if (!A.e_act[ge]) continue;
+        cnt++;
+        const double* m = A.e_meas + (size_t)ge * 8;
+        const double* Xp = ptX_at(A, cur, d.pt0 + A.e_pt[ge]);
+        const double X[3] = {Xp[0], Xp[1], Xp[2]};
+        double pc[3], e0, e1;
+        edge_error(m, T, X, pc, e0, e1);
+        const double info = m[2];
+        double rho0, rho1;
+        huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
+        double Jc[2][6];
+        edge_jac(m, T, pc, nullptr, Jc, false);
+        const double w = rho1 * info;
+        const double o0 = -(info * e0) * rho1, o1 = -(info * e1) * rho1;
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c <= r; c++) acc[k++] += (Jc[0][r] * w) * Jc[0][c] + (Jc[1][r] * w) * Jc[1][c];
+#pragma unroll
+        for (int r = 0; r < 6; r++) acc[21 + r] += Jc[0][r] * o0 + Jc[1][r] * o1;
+    }
+#pragma unroll
+    for (int k = 0; k < 27; k++)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 64);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (lane == 0) {
+        double* H = A.Hpp + (size_t)(d.f0 + a) * 36;
+        int k = 0;
+        for (int r = 0; r < 6; r++)
+            for (int c = 0; c <= r; c++, k++) H[6 * r + c] = H[6 * c + r] = acc[k];
+        for (int r = 0; r < 6; r++) A.bp[(size_t)(d.f0 + a) * 6 + r] = acc[21 + r];
+        A.f_act[d.f0 + a] = cnt > 0;
+    }
+}
+
+// lambda of this trial: computeLambdaInit at the first trial of a round
+// (max |diag| over the active poses and points), else the state's.
+__device__ double trial_lambda(const BAArena& A, const BADesc& d, const BAState& st) {
+    if (!(st.iter == 0 && st.q == 0)) return st.lambda;
+    double m = 0.0;
+    for (int w = 0; w < d.nwg; w++) m = fmax(m, A.wg_maxd[d.wg0 + w]);
+    for (int a = 0; a < d.nfree; a++)
+        if (A.f_act[d.f0 + a])
+            for (int j = 0; j < 6; j++) m = fmax(m, fabs(A.Hpp[(size_t)(d.f0 + a) * 36 + 7 * j]));
+    return 1e-5 * m;
+}
+
+// ------------------------------------------------------------------ Schur, per point
+__global__ __launch_bounds__(BA_T) void k_ba_schur_pts(BAArena A) {
+    __shared__ double s_lam;
+    const int p = blockIdx.y;
+    const BADesc d = A.desc[p];
+    if (blockIdx.x >= d.nwg) return;
+    const BAState st = A.st[p];
+    if (st.round >= 2) return;
+    if (threadIdx.x == 0) {
+        s_lam = trial_lambda(A, d, st);
+        if (blockIdx.x == 0 && st.iter == 0 && st.q == 0) A.st[p].lambda = s_lam;
+    }
+    __syncthreads();
+    const double lam = s_lam;
+    const int i = blockIdx.x * BA_T + threadIdx.x;
+    if (i >= d.npts) return;
+    const int gp = d.pt0 + i;
+    double* Wt = A.panel + d.panel0 + (size_t)d.K * d.npad;
+    if (!A.pt_act[gp]) {
+        for (int c = 0; c < 3; c++) Wt[(size_t)(3 * i + c) * d.npad + d.n] = 0.0;
+        return;
+    }
+    double D[9], Di[9];
+    const double* Hg = A.Hll + (size_t)gp * 9;
+    for (int k = 0; k < 9; k++) D[k] = Hg[k] + (k % 4 == 0 ? lam : 0.0);
+    inverse3(D, Di);
+    for (int k = 0; k < 9; k++) A.Dinv[(size_t)gp * 9 + k] = Di[k];
+    const double* b = A.bl + (size_t)gp * 3;
+    for (int r = 0; r < 3; r++)
+        Wt[(size_t)(3 * i + r) * d.npad + d.n] = (Di[3 * r] * b[0] + Di[3 * r + 1] * b[1]) + Di[3 * r + 2] * b[2];
+    const int eb = A.pt_eb[gp], ee = A.pt_ee[gp];
+    for (int le = eb; le < ee; le++) {
+        const int ge = d.e0 + le;
+        if (!A.e_act[ge]) continue;
+        const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
+        if (col < 0) continue;
+        const double* H = A.Hpl + (size_t)ge * 18;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                Wt[(size_t)(3 * i + c) * d.npad + 6 * col + r] =
+                    (H[3 * r] * Di[c] + H[3 * r + 1] * Di[3 + c]) + H[3 * r + 2] * Di[6 + c];
+    }
+}
+
+// ------------------------------------------------------------------ Schur product on MFMA
+// C[i][j] = sum_k Ht[k][i] Wt[k][j] for the lower-triangle 16x16 tiles of the
+// reduced camera system plus the tiles of column n (the coefficient vector).
+// Workgroup = (tile, split): 4 waves interleave the split's k-steps, then sum
+// their accumulators in wave order.
+__global__ __launch_bounds__(256) void k_ba_gemm(BAArena A) {
+    __shared__ double red[4][4][64];
+    const int p = blockIdx.z, t = blockIdx.x, s = blockIdx.y;
+    const BADesc d = A.desc[p];
+    if (t >= d.ntiles) return;
+    if (A.st[p].round >= 2) return;
+    const int nt = d.npad >> 4, lower = nt * (nt + 1) / 2;
+    int ti, tj;
+    if (t < lower) {
+        ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+        tj = t - ti * (ti + 1) / 2;
+    } else {
+        tj = d.n >> 4;
+        ti = t - lower;
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const double* Ht = A.panel + d.panel0;
+    const double* Wt = Ht + (size_t)d.K * d.npad;
+    const int ca = 16 * ti + (l & 15), cb = 16 * tj + (l & 15), kr = l >> 4;
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const int j1 = (s + 1) * d.sps;
+#pragma unroll 4
+    for (int j = s * d.sps + w; j < j1; j += 4) {
+        const size_t row = (size_t)(4 * j + kr) * d.npad;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ht[row + ca], Wt[row + cb], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) red[w][r][l] = acc[r];
+    __syncthreads();
+    if (w == 0) {
+        double* out = A.tiles + ((size_t)d.tile0 + (size_t)s * d.ntiles + t) * 256;
+#pragma unroll
+        for (int r = 0; r < 4; r++)  // f64 16x16x4 C/D: col = lane & 15, row = (lane >> 4) + 4 r
+            out[((l >> 4) + 4 * r) * 16 + (l & 15)] = ((red[0][r][l] + red[1][r][l]) + red[2][r][l]) + red[3][r][l];
+    }
+}
+
+__device__ __forceinline__ int tri(int i) { return i * (i + 1) / 2; }
+
+// ------------------------------------------------------------------ reduced camera system
+__global__ __launch_bounds__(1024) void k_ba_solve(BAArena A) {
+    __shared__ double sL[BA_MAXN * (BA_MAXN + 1) / 2];
+    __shared__ double sb[BA_MAXN];
+    __shared__ uint8_t sact[BA_MAXFREE];
+    __shared__ int s_fail;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const BADesc d = A.desc[p];
+    const BAState st = A.st[p];
+    if (st.round >= 2) return;
+    const int n = d.n, nt = d.npad >> 4, lower = nt * (nt + 1) / 2, tdb = n >> 4;
+    const double lam = st.lambda;
+    const double* tiles = A.tiles + (size_t)d.tile0 * 256;
+    for (int a = tid; a < d.nfree; a += 1024) sact[a] = A.f_act[d.f0 + a];
+    if (tid == 0) s_fail = 0;
+    __syncthreads();
+    // S = Hpp + lambda I - sum_split C (lower, packed); inactive poses decouple (x = 0)
+    for (int i = (tid >> 6); i < n; i += 16) {
+        const int a = i / 6;
+        for (int j = tid & 63; j <= i; j += 64) {
+            const int c = j / 6;
+            double v;
+            if (!sact[a] || !sact[c]) {
+                v = (i == j) ? 1.0 : 0.0;
+            } else {
+                v = 0.0;
+                if (a == c) v = A.Hpp[(size_t)(d.f0 + a) * 36 + (i % 6) * 6 + (j % 6)] + (i == j ? lam : 0.0);
+                const int t = tri(i >> 4) + (j >> 4), e = (i & 15) * 16 + (j & 15);
+                double g = 0.0;
+                for (int s = 0; s < BA_NSPLIT; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
+                v = v - g;
+            }
+            sL[tri(i) + j] = v;
+        }
+    }
+    for (int i = tid; i < n; i += 1024) {
+        const int a = i / 6;
+        double v = 0.0;
+        if (sact[a]) {
+            const int ti = i >> 4;
+            const int t = ti >= tdb ? tri(ti) + tdb : lower + ti;
+            const int e = (i & 15) * 16 + (n & 15);
+            double g = 0.0;
+            for (int s = 0; s < BA_NSPLIT; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
+            v = A.bp[(size_t)(d.f0 + a) * 6 + i % 6] - g;
+        }
+        sb[i] = v;
+    }
+    __syncthreads();
+    // LL^T, right-looking; per element the oracle's left-looking order
+    bool fail = false;
+    for (int k = 0; k < n; k++) {
+        const double dkk = sL[tri(k) + k];
+        if (!(dkk > 0.0)) {
+            fail = true;
+            break;
+        }
+        const double lkk = sqrt(dkk);
+        __syncthreads();
+        if (tid == 0) sL[tri(k) + k] = lkk;
+        for (int i = k + 1 + tid; i < n; i += 1024) sL[tri(i) + k] /= lkk;
+        __syncthreads();
+        for (int i = k + 1 + (tid >> 6); i < n; i += 16) {
+            const double lik = sL[tri(i) + k];
+            for (int j = k + 1 + (tid & 63); j <= i; j += 64) sL[tri(i) + j] -= lik * sL[tri(j) + k];
+        }
+        __syncthreads();
+    }
+    if (!fail && tid < 64) {  // one wave: values in registers, broadcast per step
+        double r[3];
+        for (int u = 0; u < 3; u++) r[u] = (tid + 64 * u < n) ? sb[tid + 64 * u] : 0.0;
+        for (int k = 0; k < n; k++) {  // forward: y_k = r_k / L_kk, r_i -= L_ik y_k
+            const int reg = k >> 6;
+            const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
+            const double yk = __shfl(mine, k & 63, 64) / sL[tri(k) + k];
+            for (int u = 0; u < 3; u++) {
+                const int i = tid + 64 * u;
+                if (i == k) r[u] = yk;
+                else if (i > k && i < n) r[u] -= sL[tri(i) + k] * yk;
+            }
+        }
+        for (int k = n - 1; k >= 0; k--) {  // backward: x_k = r_k / L_kk, r_i -= L_ki x_k (descending k)
+            const int reg = k >> 6;
+            const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
+            const double xk = __shfl(mine, k & 63, 64) / sL[tri(k) + k];
+            for (int u = 0; u < 3; u++) {
+                const int i = tid + 64 * u;
+                if (i == k) r[u] = xk;
+                else if (i < k) r[u] -= sL[tri(k) + i] * xk;
+            }
+        }
+        for (int u = 0; u < 3; u++)
+            if (tid + 64 * u < n) sb[tid + 64 * u] = r[u];
+    }
+    if (fail && tid == 0) s_fail = 1;
+    __syncthreads();
+    const bool ok = !s_fail;
+    if (ok)
+        for (int i = tid; i < n; i += 1024) A.xp[(size_t)d.f0 * 6 + i] = sb[i];
+    __syncthreads();
+    // trial poses: exp(x) * T for the active free poses (stale x when the solve failed)
+    const int cur = st.cur;
+    for (int k = tid; k < d.nkf; k += 1024) {
+        gfse3::SE3 T = load_T(A, cur, d.kf0 + k);
+        const int col = A.kf_col[d.kf0 + k];
+        if (col >= 0 && sact[col]) T = gfse3::exp_mul(A.xp + (size_t)(d.f0 + col) * 6, T);
+        store_T(A, 1 - cur, d.kf0 + k, T);
+    }
+    if (tid == 0) {  // computeScale, pose part (index order)
+        double sc = 0.0;
+        for (int i = 0; i < n; i++) {
+            const double xi = A.xp[(size_t)d.f0 * 6 + i];
+            sc += xi * (lam * xi + A.bp[(size_t)d.f0 * 6 + i]);
+        }
+        A.st[p].scale_p = sc;
+        A.st[p].chol_ok = ok ? 1 : 0;
+    }
+}
+
+// ------------------------------------------------------------------ landmarks, trial errors
+__global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
+    __shared__ double sh[BA_T / 64];
+    const int p = blockIdx.y;
+    const BADesc d = A.desc[p];
+    if (blockIdx.x >= d.nwg) return;
+    const BAState st = A.st[p];
+    if (st.round >= 2) return;
+    const int i = blockIdx.x * BA_T + threadIdx.x;
+    double chi = 0.0, sc = 0.0;
+    if (i < d.npts) {
+        const int gp = d.pt0 + i, cur = st.cur, nxt = 1 - st.cur;
+        const double lam = st.lambda;
+        const double* Xc = ptX_at(A, cur, gp);
+        double X[3] = {Xc[0], Xc[1], Xc[2]};
+        const int eb = A.pt_eb[gp], ee = A.pt_ee[gp];
+        if (A.pt_act[gp]) {
+            double* xl = A.xl + (size_t)gp * 3;
+            const double* b = A.bl + (size_t)gp * 3;
+            if (st.chol_ok) {  // cl = b_l + Hpl^T (-x_p), x_l = Dinv cl
+                double cl[3] = {b[0], b[1], b[2]};
+                for (int le = eb; le < ee; le++) {
+                    const int ge = d.e0 + le;
+                    if (!A.e_act[ge]) continue;
+                    const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
+                    if (col < 0) continue;
+                    const double* H = A.Hpl + (size_t)ge * 18;
+                    const double* xa = A.xp + (size_t)(d.f0 + col) * 6;
+                    for (int c = 0; c < 3; c++) {
+                        double t = H[c] * (-xa[0]);
+                        for (int r = 1; r < 6; r++) t += H[3 * r + c] * (-xa[r]);
+                        cl[c] += t;
+                    }
+                }
+                const double* Di = A.Dinv + (size_t)gp * 9;
+                for (int r = 0; r < 3; r++) xl[r] = (Di[3 * r] * cl[0] + Di[3 * r + 1] * cl[1]) + Di[3 * r + 2] * cl[2];
+            }
+            for (int c = 0; c < 3; c++) {
+                X[c] += xl[c];
+                sc += xl[c] * (lam * xl[c] + b[c]);
+            }
+        }
+        double* Xn = ptX_at(A, nxt, gp);
+        Xn[0] = X[0];
+        Xn[1] = X[1];
+        Xn[2] = X[2];
+        for (int le = eb; le < ee; le++) {  // errors at the trial estimate
+            const int ge = d.e0 + le;
+            if (!A.e_act[ge]) continue;
+            const double* m = A.e_meas + (size_t)ge * 8;
+            const gfse3::SE3 T = load_T(A, nxt, d.kf0 + A.e_kf[ge]);
+            double pc[3], e0, e1;
+            edge_error(m, T, X, pc, e0, e1);
+            A.e_err[(size_t)ge * 2] = e0;
+            A.e_err[(size_t)ge * 2 + 1] = e1;
+            const double info = m[2];
+            double rho0, rho1;
+            huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
+            chi += rho0;
+        }
+    }
+    const double cs = block_reduce(chi, sh, false);
+    const double ss = block_reduce(sc, sh, false);
+    if (threadIdx.x == 0) {
+        A.wg_chi_t[d.wg0 + blockIdx.x] = cs;
+        A.wg_scale[d.wg0 + blockIdx.x] = ss;
+    }
+}
+
+// ------------------------------------------------------------------ LM decision + outlier pass
+__global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
+    __shared__ int s_end, s_cnt;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const BADesc d = A.desc[p];
+    if (A.st[p].round >= 2) return;
+    if (tid == 0) {
+        BAState st = A.st[p];
+        if (st.q == 0) {  // activeRobustChi2 at the iteration start
+            double c = 0.0;
+            for (int w = 0; w < d.nwg; w++) c += A.wg_chi[d.wg0 + w];
+            st.currentChi = c;
+            st.iniChi = c;
+        }
+        double tempChi = 0.0;
+        for (int w = 0; w < d.nwg; w++) tempChi += A.wg_chi_t[d.wg0 + w];
+        if (!st.chol_ok) tempChi = DBL_MAX;
+        double scale = st.scale_p;
+        for (int w = 0; w < d.nwg; w++) scale += A.wg_scale[d.wg0 + w];
+        scale += 1e-3;
+        const double rho = (st.currentChi - tempChi) / scale;
+        if (rho > 0 && isfinite(tempChi)) {
+            double alpha = 1. - pow((2 * rho - 1), 3.0);
+            alpha = fmin(alpha, 2. / 3.);
+            const double sf = fmax(1. / 3., alpha);
+            st.lambda *= sf;
+            st.ni = 2;
+            st.currentChi = tempChi;
+            st.cur ^= 1;  // the trial estimate becomes the current one
+        } else {
+            st.lambda *= st.ni;
+            st.ni *= 2;
+        }
+        st.q++;
+        int end = 0;
+        if (rho < 0 && st.q < 10) {
+            st.need_lin = 0;  // another trial on the same system
+        } else {
+            st.iters[st.round]++;
+            bool term = (st.q == 10 || rho == 0);
+            if (!term) {
+                if ((st.iniChi - st.currentChi) * 1e3 < st.iniChi)
+                    st.nbad++;
+                else
+                    st.nbad = 0;
+                term = st.nbad >= 3;
+            }
+            st.iter++;
+            if (term || st.iter >= (st.round == 0 ? 5 : 10)) {
+                end = 1;
+            } else {
+                st.need_lin = 1;
+                st.q = 0;
+            }
+        }
+        A.st[p] = st;
+        s_end = end;
+        s_cnt = 0;
+    }
+    __syncthreads();
+    if (!s_end) return;
+    const BAState st = A.st[p];
+    const int round = st.round, cur = st.cur;
+    double* Ht = A.panel + d.panel0;
+    double* Wt = Ht + (size_t)d.K * d.npad;
+    int cnt = 0;
+    for (int e = tid; e < d.nedges; e += 1024) {
+        const int ge = d.e0 + e;
+        if (!A.e_act[ge]) continue;
+        const double* m = A.e_meas + (size_t)ge * 8;
+        const double e0 = A.e_err[(size_t)ge * 2], e1 = A.e_err[(size_t)ge * 2 + 1], info = m[2];
+        const int pt = A.e_pt[ge], kf = A.e_kf[ge];
+        const double* Xp = ptX_at(A, cur, d.pt0 + pt);
+        const double X[3] = {Xp[0], Xp[1], Xp[2]};
+        double pc[3];
+        gfse3::map(load_T(A, cur, d.kf0 + kf), X, pc);
+        if (e0 * (info * e0) + e1 * (info * e1) > 5.991 || !(pc[2] > 0.0)) {
+            A.e_out[ge] = (uint8_t)(round + 1);
+            if (round == 0) {  // removeEdge: out of the structure of optimize(10)
+                A.e_act[ge] = 0;
+                const int col = A.kf_col[d.kf0 + kf];
+                if (col >= 0)
+                    for (int c = 0; c < 3; c++)
+                        for (int r = 0; r < 6; r++) {
+                            Ht[(size_t)(3 * pt + c) * d.npad + 6 * col + r] = 0.0;
+                            Wt[(size_t)(3 * pt + c) * d.npad + 6 * col + r] = 0.0;
+                        }
+                continue;
+            }
+        }
+        cnt++;
+    }
+    for (int i = tid; i < 6 * d.nfree; i += 1024) A.xp[(size_t)d.f0 * 6 + i] = 0.0;  // new structure: fresh _x
+    for (int i = tid; i < 3 * d.npts; i += 1024) A.xl[(size_t)d.pt0 * 3 + i] = 0.0;
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (tid == 0) {
+        BAState s2 = A.st[p];
+        s2.round++;
+        if (s2.round == 1 && s_cnt == 0) {  // no edge left: optimize(10) does not run
+            s2.round = 2;
+            s2.iters[1] = -1;
+        }
+        s2.iter = 0;
+        s2.q = 0;
+        s2.need_lin = 1;
+        s2.ni = 2;
+        s2.nbad = 0;
+        A.st[p] = s2;
+    }
+}
+
+// ------------------------------------------------------------------ outputs
+__global__ __launch_bounds__(256) void k_ba_finish(BAArena A) {
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const BADesc d = A.desc[p];
+    const int cur = A.st[p].cur;
+    for (int k = tid; k < d.nkf; k += 256) {  // Converter::toCvMat for the local keyframes
+        float* o = A.out_T + (size_t)(d.kf0 + k) * 16;
+        if (A.kf_kind[d.kf0 + k] == 2) {
+            for (int q = 0; q < 16; q++) o[q] = A.kf_Tcw0[(size_t)(d.kf0 + k) * 16 + q];
+            continue;
+        }
+        const gfse3::SE3 T = load_T(A, cur, d.kf0 + k);
+        double R[9];
+        gfse3::to_R(T.r, R);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) o[4 * i + j] = (float)R[3 * i + j];
+            o[4 * i + 3] = (float)T.t[i];
+        }
+        o[12] = o[13] = o[14] = 0.f;
+        o[15] = 1.f;
+    }
+    for (int i = tid; i < d.npts; i += 256) {
+        const double* X = ptX_at(A, cur, d.pt0 + i);
+        for (int c = 0; c < 3; c++) A.out_X[(size_t)(d.pt0 + i) * 3 + c] = (float)X[c];
+    }
+}
+
+template <typename T>
+int dalloc(T** p, size_t n, std::vector<void*>& owned) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    GF_HIP(hipMalloc((void**)p, n * sizeof(T)));
+    owned.push_back((void*)*p);
+    return GF_OK;
+}
+
+}  // namespace
+
+// ====================================================================== host
+struct gf_ba_plan {
+    gf_ctx* ctx = nullptr;
+    int nprob = 0;
+    std::vector<BADesc> desc;
+    int max_nwg = 1, max_free = 1, max_tiles = 1;
+    size_t panel_doubles = 0;
+    BAArena A{};
+    std::vector<void*> owned;
+    BAState* h_state = nullptr;  // pinned
+    BADesc* d_desc = nullptr;
+    std::vector<uint8_t> h_out;  // scratch for results
+};
+
+namespace {
+
+int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
+    const BAArena& A = P->A;
+    const int B = P->nprob;
+    const dim3 gpt(P->max_nwg, B), gpose(P->max_free, B), ggemm(P->max_tiles, BA_NSPLIT, B);
+    {
+        GF_PROF(P->ctx, s, "k_ba_linearize");
+        k_ba_linearize<<<gpt, BA_T, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_poses");
+        k_ba_poses<<<gpose, 64, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_schur_pts");
+        k_ba_schur_pts<<<gpt, BA_T, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_gemm");
+        k_ba_gemm<<<ggemm, 256, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_solve");
+        k_ba_solve<<<B, 1024, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_update");
+        k_ba_update<<<gpt, BA_T, 0, s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_decide");
+        k_ba_decide<<<B, 1024, 0, s>>>(A);
+    }
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gf_ba_plan_destroy(gf_ba_plan* P) {
+    if (!P) return GF_OK;
+    if (P->ctx) (void)hipSetDevice(P->ctx->device);
+    for (void* q : P->owned) (void)hipFree(q);
+    if (P->h_state) (void)hipHostFree(P->h_state);
+    delete P;
+    return GF_OK;
+}
+
+int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_plan** out) {
+    GF_CHECK(ctx && out && (nprob == 0 || probs), GF_ERR_ARG, "null arg");
+    GF_CHECK(nprob >= 0, GF_ERR_ARG, "nprob < 0");
+    *out = nullptr;
+    // ---- validate and lay out (host): index mapping, edge ranges, pose edge lists
+    std::vector<BADesc> desc(nprob);
+    std::vector<int32_t> kf_col, pt_eb, pt_ee, e_pt, e_kf, f_kf, f_eptr, f_elist;
+    std::vector<double> e_meas;
+    std::vector<float> kf_T, pt_pos;
+    std::vector<uint8_t> kf_kind;
+    int nkf_tot = 0, npt_tot = 0, ne_tot = 0, nf_tot = 0, ntile_tot = 0, nwg_tot = 0;
+    long long panel = 0;
+    for (int p = 0; p < nprob; p++) {
+        const gf_ba_problem& Q = probs[p];
+        GF_CHECK(Q.nkf >= 0 && Q.npts >= 0 && Q.nedges >= 0, GF_ERR_ARG, "negative size");
+        GF_CHECK(Q.npts <= BA_MAXPTS, GF_ERR_UNSUPPORTED, "more than 65536 points");
+        GF_CHECK((Q.nkf == 0 || (Q.kf_Tcw && Q.kf_kind && Q.kf_cam)) && (Q.npts == 0 || Q.pt_pos) &&
+                     (Q.nedges == 0 || (Q.edge_pt && Q.edge_kf && Q.edge_z && Q.edge_inv_sigma2)),
+                 GF_ERR_ARG, "null array");
+        BADesc& d = desc[p];
+        d.nkf = Q.nkf;
+        d.npts = Q.npts;
+        d.nedges = Q.nedges;
+        d.kf0 = nkf_tot;
+        d.pt0 = npt_tot;
+        d.e0 = ne_tot;
+        d.f0 = nf_tot;
+        d.fe0 = (int)f_eptr.size();
+        d.pl0 = (int)f_elist.size();
+        int nfree = 0;
+        std::vector<int> col(Q.nkf, -1);
+        for (int k = 0; k < Q.nkf; k++) {
+            GF_CHECK(Q.kf_kind[k] <= 2, GF_ERR_ARG, "keyframe kind must be 0, 1 or 2");
+            if (Q.kf_kind[k] == 0) {
+                col[k] = nfree++;
+                f_kf.push_back(k);
+            }
+            kf_col.push_back(col[k]);
+            kf_kind.push_back(Q.kf_kind[k]);
+            for (int q = 0; q < 16; q++) kf_T.push_back(Q.kf_Tcw[16 * k + q]);
+        }
+        GF_CHECK(nfree <= BA_MAXFREE, GF_ERR_UNSUPPORTED, "more than 32 local (non-fixed) keyframes");
+        d.nfree = nfree;
+        // edges of a point contiguous, one edge per (point, keyframe)
+        std::vector<int> eb(Q.npts, 0), ee(Q.npts, 0), seen(Q.npts, 0);
+        for (int e = 0; e < Q.nedges; e++) {
+            const int pt = Q.edge_pt[e], kf = Q.edge_kf[e];
+            GF_CHECK(pt >= 0 && pt < Q.npts && kf >= 0 && kf < Q.nkf, GF_ERR_ARG, "edge index out of range");
+            if (!seen[pt]) {
+                seen[pt] = 1;
+                eb[pt] = e;
+            } else {
+                GF_CHECK(ee[pt] == e, GF_ERR_ARG, "edges of a map point must be contiguous");
+            }
+            ee[pt] = e + 1;
+        }
+        for (int i = 0; i < Q.npts; i++) {
+            for (int a = eb[i]; a < ee[i]; a++)
+                for (int b = a + 1; b < ee[i]; b++)
+                    GF_CHECK(Q.edge_kf[a] != Q.edge_kf[b], GF_ERR_ARG, "two edges between one point and one keyframe");
+            pt_eb.push_back(eb[i]);
+            pt_ee.push_back(ee[i]);
+            for (int c = 0; c < 3; c++) pt_pos.push_back(Q.pt_pos[3 * i + c]);
+        }
+        for (int e = 0; e < Q.nedges; e++) {
+            const float* K = Q.kf_cam + 4 * Q.edge_kf[e];
+            e_pt.push_back(Q.edge_pt[e]);
+            e_kf.push_back(Q.edge_kf[e]);
+            const double m[8] = {(double)Q.edge_z[2 * e], (double)Q.edge_z[2 * e + 1], (double)Q.edge_inv_sigma2[e],
+                                 (double)K[0], (double)K[1], (double)K[2], (double)K[3], 0.0};
+            e_meas.insert(e_meas.end(), m, m + 8);
+        }
+        // per free pose: its edges in point order
+        std::vector<std::vector<int>> lists(nfree);
+        for (int i = 0; i < Q.npts; i++)
+            for (int e = eb[i]; e < ee[i]; e++)
+                if (col[Q.edge_kf[e]] >= 0) lists[col[Q.edge_kf[e]]].push_back(e);
+        int acc = 0;
+        for (int a = 0; a < nfree; a++) {
+            f_eptr.push_back(acc);
+            for (int e : lists[a]) f_elist.push_back(e);
+            acc += (int)lists[a].size();
+        }
+        f_eptr.push_back(acc);
+        // Schur panel / GEMM geometry
+        d.n = 6 * nfree;
+        d.npad = ((d.n + 1 + 15) / 16) * 16;
+        const int steps = std::max(1, (3 * Q.npts + 3) / 4);
+        d.sps = (steps + BA_NSPLIT - 1) / BA_NSPLIT;
+        d.K = BA_NSPLIT * d.sps * 4;
+        const int nt = d.npad / 16;
+        d.ntiles = nt * (nt + 1) / 2 + (d.n >> 4);
+        d.nwg = std::max(1, (Q.npts + BA_T - 1) / BA_T);
+        d.tile0 = ntile_tot;
+        d.wg0 = nwg_tot;
+        d.panel0 = panel;
+        nkf_tot += Q.nkf;
+        npt_tot += Q.npts;
+        ne_tot += Q.nedges;
+        nf_tot += nfree;
+        ntile_tot += BA_NSPLIT * d.ntiles;
+        nwg_tot += d.nwg;
+        panel += 2LL * d.K * d.npad;
+    }
+    GF_HIP(hipSetDevice(ctx->device));
+    gf_ba_plan* P = new gf_ba_plan();
+    P->ctx = ctx;
+    P->nprob = nprob;
+    P->desc = desc;
+    for (const BADesc& d : desc) {
+        P->max_nwg = std::max(P->max_nwg, d.nwg);
+        P->max_free = std::max(P->max_free, d.nfree);
+        P->max_tiles = std::max(P->max_tiles, d.ntiles);
+    }
+    P->panel_doubles = (size_t)panel;
+    BAArena& A = P->A;
+    A.nkf_tot = nkf_tot;
+    A.npt_tot = npt_tot;
+    int rc = 0;
+    BADesc* dd;
+    BAState* ds;
+    double *kfT, *ptX, *Hll, *bl, *Dinv, *xl, *e_err, *Hpl, *Hpp, *bp, *xp, *pnl, *tiles, *w0, *w1, *w2, *w3;
+    float *kT0, *pX0, *oT, *oX;
+    uint8_t *kk, *pa, *ea, *eo, *fa;
+    int32_t *kc, *peb, *pee, *ept, *ekf, *fkf, *fep, *fel;
+    double* em;
+    auto& o = P->owned;
+    if ((rc = dalloc(&dd, nprob, o)) || (rc = dalloc(&ds, nprob, o)) || (rc = dalloc(&kfT, 16 * (size_t)nkf_tot, o)) ||
+        (rc = dalloc(&kT0, 16 * (size_t)nkf_tot, o)) || (rc = dalloc(&kk, nkf_tot, o)) ||
+        (rc = dalloc(&kc, nkf_tot, o)) || (rc = dalloc(&ptX, 8 * (size_t)npt_tot, o)) ||
+        (rc = dalloc(&pX0, 3 * (size_t)npt_tot, o)) || (rc = dalloc(&peb, npt_tot, o)) ||
+        (rc = dalloc(&pee, npt_tot, o)) || (rc = dalloc(&Hll, 9 * (size_t)npt_tot, o)) ||
+        (rc = dalloc(&bl, 3 * (size_t)npt_tot, o)) || (rc = dalloc(&Dinv, 9 * (size_t)npt_tot, o)) ||
+        (rc = dalloc(&xl, 3 * (size_t)npt_tot, o)) || (rc = dalloc(&pa, npt_tot, o)) ||
+        (rc = dalloc(&ept, ne_tot, o)) || (rc = dalloc(&ekf, ne_tot, o)) || (rc = dalloc(&em, 8 * (size_t)ne_tot, o)) ||
+        (rc = dalloc(&e_err, 2 * (size_t)ne_tot, o)) || (rc = dalloc(&ea, ne_tot, o)) || (rc = dalloc(&eo, ne_tot, o)) ||
+        (rc = dalloc(&Hpl, 18 * (size_t)ne_tot, o)) || (rc = dalloc(&fkf, nf_tot, o)) ||
+        (rc = dalloc(&fep, f_eptr.size(), o)) || (rc = dalloc(&fel, f_elist.size(), o)) ||
+        (rc = dalloc(&Hpp, 36 * (size_t)nf_tot, o)) || (rc = dalloc(&bp, 6 * (size_t)nf_tot, o)) ||
+        (rc = dalloc(&xp, 6 * (size_t)nf_tot, o)) || (rc = dalloc(&fa, nf_tot, o)) ||
+        (rc = dalloc(&pnl, P->panel_doubles, o)) || (rc = dalloc(&tiles, 256 * (size_t)ntile_tot, o)) ||
+        (rc = dalloc(&w0, nwg_tot, o)) || (rc = dalloc(&w1, nwg_tot, o)) || (rc = dalloc(&w2, nwg_tot, o)) ||
+        (rc = dalloc(&w3, nwg_tot, o)) || (rc = dalloc(&oT, 16 * (size_t)nkf_tot, o)) ||
+        (rc = dalloc(&oX, 3 * (size_t)npt_tot, o))) {
+        gf_ba_plan_destroy(P);
+        return rc;
+    }
+    hipError_t he = hipHostMalloc((void**)&P->h_state, sizeof(BAState) * std::max(nprob, 1));
+    if (he != hipSuccess) {
+        gf_ba_plan_destroy(P);
+        return gf::fail(GF_ERR_HIP, hipGetErrorString(he));
+    }
+    hipStream_t s = ctx->stream;
+    auto up = [&](void* dst, const void* src, size_t bytes) {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s) : hipSuccess;
+    };
+    if ((he = up(dd, desc.data(), sizeof(BADesc) * nprob)) || (he = up(kT0, kf_T.data(), 4 * kf_T.size())) ||
+        (he = up(kk, kf_kind.data(), kf_kind.size())) || (he = up(kc, kf_col.data(), 4 * kf_col.size())) ||
+        (he = up(pX0, pt_pos.data(), 4 * pt_pos.size())) || (he = up(peb, pt_eb.data(), 4 * pt_eb.size())) ||
+        (he = up(pee, pt_ee.data(), 4 * pt_ee.size())) || (he = up(ept, e_pt.data(), 4 * e_pt.size())) ||
+        (he = up(ekf, e_kf.data(), 4 * e_kf.size())) || (he = up(em, e_meas.data(), 8 * e_meas.size())) ||
+        (he = up(fkf, f_kf.data(), 4 * f_kf.size())) || (he = up(fep, f_eptr.data(), 4 * f_eptr.size())) ||
+        (he = up(fel, f_elist.data(), 4 * f_elist.size())) || (he = hipStreamSynchronize(s))) {
+        gf_ba_plan_destroy(P);
+        return gf::fail(GF_ERR_HIP, hipGetErrorString(he));
+    }
+    P->d_desc = dd;
+    A.desc = dd;
+    A.st = ds;
+    A.kfT = kfT;
+    A.kf_Tcw0 = kT0;
+    A.kf_kind = kk;
+    A.kf_col = kc;
+    A.ptX = ptX;
+    A.pt_pos0 = pX0;
+    A.pt_eb = peb;
+    A.pt_ee = pee;
+    A.Hll = Hll;
+    A.bl = bl;
+    A.Dinv = Dinv;
+    A.xl = xl;
+    A.pt_act = pa;
+    A.e_pt = ept;
+    A.e_kf = ekf;
+    A.e_meas = em;
+    A.e_err = e_err;
+    A.e_act = ea;
+    A.e_out = eo;
+    A.Hpl = Hpl;
+    A.f_kf = fkf;
+    A.f_eptr = fep;
+    A.f_elist = fel;
+    A.Hpp = Hpp;
+    A.bp = bp;
+    A.xp = xp;
+    A.f_act = fa;
+    A.panel = pnl;
+    A.tiles = tiles;
+    A.wg_chi = w0;
+    A.wg_chi_t = w1;
+    A.wg_maxd = w2;
+    A.wg_scale = w3;
+    A.out_T = oT;
+    A.out_X = oX;
+    *out = P;
+    return GF_OK;
+}
+
+int gf_ba_plan_solve(gf_ba_plan* P, void* stream, int* steps) {
+    GF_CHECK(P, GF_ERR_ARG, "null plan");
+    if (steps) *steps = 0;
+    if (P->nprob == 0) return GF_OK;
+    GF_HIP(hipSetDevice(P->ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : P->ctx->stream;
+    GF_HIP(hipMemsetAsync(P->A.panel, 0, P->panel_doubles * sizeof(double), s));
+    {
+        GF_PROF(P->ctx, s, "k_ba_init");
+        k_ba_init<<<P->nprob, 256, 0, s>>>(P->A);
+        GF_HIP(hipGetLastError());
+    }
+    int n = 0;
+    const int chunk = 4;
+    bool done = false;
+    while (!done) {
+        GF_CHECK(n < BA_MAXSTEPS, GF_ERR_HIP, "local BA did not terminate");
+        for (int c = 0; c < chunk; c++, n++) {
+            int rc = ba_launch_step(P, s);
+            if (rc) return rc;
+        }
+        GF_HIP(hipMemcpyAsync(P->h_state, P->A.st, sizeof(BAState) * P->nprob, hipMemcpyDeviceToHost, s));
+        GF_HIP(hipStreamSynchronize(s));
+        done = true;
+        for (int p = 0; p < P->nprob; p++) done = done && P->h_state[p].round >= 2;
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_finish");
+        k_ba_finish<<<P->nprob, 256, 0, s>>>(P->A);
+        GF_HIP(hipGetLastError());
+    }
+    GF_HIP(hipStreamSynchronize(s));
+    if (steps) *steps = n;
+    return GF_OK;
+}
+
+int gf_ba_plan_results(gf_ba_plan* P, gf_ba_result* res) {
+    GF_CHECK(P && (P->nprob == 0 || res), GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(P->ctx->device));
+    hipStream_t s = P->ctx->stream;
+    GF_HIP(hipMemcpyAsync(P->h_state, P->A.st, sizeof(BAState) * std::max(P->nprob, 1), hipMemcpyDeviceToHost, s));
+    for (int p = 0; p < P->nprob; p++) {
+        const BADesc& d = P->desc[p];
+        gf_ba_result& r = res[p];
+        if (d.nkf)
+            GF_HIP(hipMemcpyAsync(r.kf_Tcw, P->A.out_T + (size_t)d.kf0 * 16, 64 * (size_t)d.nkf, hipMemcpyDeviceToHost, s));
+        if (d.npts)
+            GF_HIP(hipMemcpyAsync(r.pt_pos, P->A.out_X + (size_t)d.pt0 * 3, 12 * (size_t)d.npts, hipMemcpyDeviceToHost, s));
+        if (d.nedges) GF_HIP(hipMemcpyAsync(r.edge_outlier, P->A.e_out + d.e0, d.nedges, hipMemcpyDeviceToHost, s));
+    }
+    GF_HIP(hipStreamSynchronize(s));
+    for (int p = 0; p < P->nprob; p++) {
+        res[p].iterations[0] = P->h_state[p].iters[0];
+        res[p].iterations[1] = P->h_state[p].iters[1];
+    }
+    return GF_OK;
+}
+
+int gf_local_ba(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res) {
+    GF_CHECK(ctx && prob && res, GF_ERR_ARG, "null arg");
+    gf_ba_plan* P = nullptr;
+    int rc = gf_ba_plan_create(ctx, 1, prob, &P);
+    if (rc) return rc;
+    rc = gf_ba_plan_solve(P, nullptr, nullptr);
+    if (!rc) rc = gf_ba_plan_results(P, res);
+    gf_ba_plan_destroy(P);
+    return rc;
+}
+
+}  // extern "C"

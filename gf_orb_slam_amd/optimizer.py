@@ -85,3 +85,91 @@ class Optimizer:
                                           int(edge_stride), ctypes.c_float(fx), ctypes.c_float(fy),
                                           ctypes.c_float(cx), ctypes.c_float(cy), ptr(d_outlier), ptr(d_ninliers),
                                           ptr(d_iterations), stream if stream is not None else ctx.stream))
+
+
+# ---------------------------------------------------------------- local BA (B1)
+BA_LOCAL, BA_LOCAL_FIXED, BA_FIXED = 0, 1, 2
+
+
+class BAProblem(ctypes.Structure):
+    """gf_ba_problem (include/gfslam/abi.h): the graph LocalBundleAdjustment builds."""
+
+    _fields_ = [("nkf", ctypes.c_int32), ("npts", ctypes.c_int32), ("nedges", ctypes.c_int32),
+                ("kf_Tcw", ctypes.c_void_p), ("kf_kind", ctypes.c_void_p), ("kf_cam", ctypes.c_void_p),
+                ("pt_pos", ctypes.c_void_p), ("edge_pt", ctypes.c_void_p), ("edge_kf", ctypes.c_void_p),
+                ("edge_z", ctypes.c_void_p), ("edge_inv_sigma2", ctypes.c_void_p)]
+
+
+class BAResult(ctypes.Structure):
+    _fields_ = [("kf_Tcw", ctypes.c_void_p), ("pt_pos", ctypes.c_void_p), ("edge_outlier", ctypes.c_void_p),
+                ("iterations", ctypes.c_int32 * 2)]
+
+
+_BA_FIELDS = (("kf_Tcw", np.float32), ("kf_kind", np.uint8), ("kf_cam", np.float32), ("pt_pos", np.float32),
+              ("edge_pt", np.int32), ("edge_kf", np.int32), ("edge_z", np.float32),
+              ("edge_inv_sigma2", np.float32))
+
+
+class BAArrays:
+    """Keeps the numpy arrays of one problem alive next to its ctypes views."""
+
+    def __init__(self, prob: dict):
+        self.a = {k: np.ascontiguousarray(prob[k], dt) for k, dt in _BA_FIELDS}
+        self.nkf, self.npts, self.nedges = len(self.a["kf_kind"]), len(self.a["pt_pos"]), len(self.a["edge_pt"])
+        self.problem = BAProblem(self.nkf, self.npts, self.nedges,
+                                 *[self.a[k].ctypes.data if self.a[k].size else None for k, _ in _BA_FIELDS])
+        self.kf_Tcw = np.zeros((self.nkf, 4, 4), np.float32)
+        self.pt_pos = np.zeros((self.npts, 3), np.float32)
+        self.outlier = np.zeros(max(self.nedges, 1), np.uint8)
+        self.result = BAResult(self.kf_Tcw.ctypes.data, self.pt_pos.ctypes.data, self.outlier.ctypes.data)
+
+    def out(self):
+        """(kf_Tcw [nkf,4,4], pt_pos [npts,3], edge_outlier [nedges], iterations (it5, it10))."""
+        return (self.kf_Tcw.copy(), self.pt_pos.copy(), self.outlier[:self.nedges].copy(),
+                tuple(int(i) for i in self.result.iterations))
+
+
+def local_bundle_adjustment(prob: dict, ctx=None):
+    """Optimizer::LocalBundleAdjustment (Optimizer.cc:1515-1764) on one local
+    window (dict with the gf_ba_problem arrays, e.g. synth.synth_lba_problem).
+    Returns (kf_Tcw, pt_pos, edge_outlier, iterations)."""
+    ctx = ctx or default_context()
+    arr = BAArrays(prob)
+    check(lib().gf_local_ba(ctx.handle, ctypes.byref(arr.problem), ctypes.byref(arr.result)))
+    return arr.out()
+
+
+class LocalBAPlan:
+    """Batched device path: nprob local windows uploaded once, solved together
+    (gf_ba_plan_create / _solve / _results)."""
+
+    def __init__(self, probs: list, ctx=None):
+        self.ctx = ctx or default_context()
+        self.arrs = [BAArrays(p) for p in probs]
+        ps = (BAProblem * len(probs))(*[a.problem for a in self.arrs])
+        self.handle = ctypes.c_void_p()
+        check(lib().gf_ba_plan_create(self.ctx.handle, len(probs), ps, ctypes.byref(self.handle)))
+
+    def solve(self, stream=None) -> int:
+        steps = ctypes.c_int()
+        check(lib().gf_ba_plan_solve(self.handle, stream if stream is not None else self.ctx.stream,
+                                     ctypes.byref(steps)))
+        return steps.value
+
+    def results(self) -> list:
+        rs = (BAResult * len(self.arrs))(*[a.result for a in self.arrs])
+        check(lib().gf_ba_plan_results(self.handle, rs))
+        for a, r in zip(self.arrs, rs):
+            a.result.iterations[:] = r.iterations[:]
+        return [a.out() for a in self.arrs]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().gf_ba_plan_destroy(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -213,3 +213,75 @@ def synth_pose_problem(seed: int, n: int, camera: str = "euroc", noise_px: float
     dT = look_pose(rng, trans_sigma=trans, rot_deg=rot_deg).astype(np.float64)
     T_init = (dT @ T_true).astype(np.float32)
     return T_true.astype(np.float32), T_init, edges, cam
+
+
+def synth_lba_problem(seed: int, nkf: int = 20, npts: int = 3000, nfixed: int = 2, camera: str = "euroc",
+                      noise_px: float = 1.0, outlier_frac: float = 0.05, rot_deg: float = 0.5, trans: float = 0.01,
+                      pt_noise: float = 0.02, min_obs: int = 2, max_obs: int = 8, nlevels: int = 8,
+                      scale: float = 1.2) -> dict:
+    """One LocalBundleAdjustment window.
+
+    nkf local keyframes on a 1 m arc (keyframe 0 is the fixed mnId == 0 one),
+    plus nfixed fixed observer cameras (lFixedCameras). npts map points with
+    X ~ U([-4,4] x [-4,4] x [2,8]), each observed by U{min_obs..max_obs} of the
+    keyframes that see it (observation order per point random, as the
+    reference's map<KeyFrame*, size_t> pointer order); z = projection +
+    N(0, noise_px), octave U{0..nlevels-1}; outlier_frac of the observations
+    displaced 3-6 px. Initial local poses perturbed by rot_deg / trans, points
+    by N(0, pt_noise). Arrays follow gf_ba_problem (include/gfslam/abi.h)."""
+    rng = np.random.default_rng(seed)
+    w, h, fx, fy, cx, cy = CAMERAS[camera]
+    K = nkf + nfixed
+    ang = np.linspace(-0.25, 0.25, K) + rng.normal(0, 0.01, K)
+    centers = np.c_[2 * np.sin(ang), rng.normal(0, 0.05, K), 2 - 2 * np.cos(ang)]
+    T_true = np.zeros((K, 4, 4))
+    for k in range(K):
+        c, s = np.cos(-ang[k] * 0.5), np.sin(-ang[k] * 0.5)
+        R = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+        T_true[k] = np.eye(4)
+        T_true[k, :3, :3] = R
+        T_true[k, :3, 3] = -R @ centers[k]
+    kind = np.zeros(K, np.uint8)  # vertex-id order; fixed cameras interleave with the local keyframes
+    kind[0] = 1
+    kind[rng.choice(np.arange(1, K), nfixed, replace=False)] = 2
+    X, obs = [], []
+    while len(X) < npts:
+        P = np.c_[rng.uniform(-4, 4, 4 * npts), rng.uniform(-4, 4, 4 * npts), rng.uniform(2, 8, 4 * npts)]
+        Pc = np.einsum("kij,nj->kni", T_true[:, :3, :3], P) + T_true[:, None, :3, 3]
+        u = fx * Pc[..., 0] / Pc[..., 2] + cx
+        v = fy * Pc[..., 1] / Pc[..., 2] + cy
+        vis = (Pc[..., 2] > 0.1) & (u >= 0) & (u < w) & (v >= 0) & (v < h)
+        for i in np.nonzero(vis.sum(0) >= min_obs)[0]:
+            ks = np.nonzero(vis[:, i])[0]
+            m = int(rng.integers(min_obs, min(max_obs, len(ks)) + 1))
+            sel = rng.permutation(rng.choice(ks, m, replace=False))
+            X.append(P[i])
+            obs.append([(int(k), u[k, i], v[k, i]) for k in sel])
+            if len(X) == npts:
+                break
+    X = np.array(X)
+    e_pt = np.array([i for i, o in enumerate(obs) for _ in o], np.int32)
+    e_kf = np.array([k for o in obs for (k, _, _) in o], np.int32)
+    z = np.array([(uu, vv) for o in obs for (_, uu, vv) in o]) + rng.normal(0, noise_px, (len(e_pt), 2))
+    nout = int(round(outlier_frac * len(e_pt)))
+    if nout:
+        idx = rng.choice(len(e_pt), nout, replace=False)
+        a = rng.uniform(0, 2 * np.pi, nout)
+        r = rng.uniform(3, 6, nout)
+        z[idx] += np.c_[r * np.cos(a), r * np.sin(a)]
+    s = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        s.append(np.float32(s[-1] * np.float32(scale)))
+    s = np.array(s, np.float32)
+    invs = (np.float32(1.0) / (s * s)).astype(np.float32)
+    T0 = T_true.copy()
+    for k in range(K):
+        if kind[k] == 0:
+            T0[k] = look_pose(rng, trans, rot_deg).astype(np.float64) @ T_true[k]
+    X0 = X + rng.normal(0, pt_noise, X.shape)
+    return {"kf_Tcw": np.ascontiguousarray(T0.reshape(K, 16), np.float32), "kf_kind": kind,
+            "kf_cam": np.tile(np.array([fx, fy, cx, cy], np.float32), (K, 1)),
+            "pt_pos": np.ascontiguousarray(X0, np.float32), "edge_pt": e_pt, "edge_kf": e_kf,
+            "edge_z": np.ascontiguousarray(z, np.float32),
+            "edge_inv_sigma2": invs[rng.integers(0, nlevels, len(e_pt))],
+            "T_true": T_true.astype(np.float32), "X_true": X.astype(np.float32)}

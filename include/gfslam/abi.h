@@ -362,6 +362,61 @@ int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keyp
                            uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, int32_t* d_nedges,
                            void* stream);
 
+/* ------------------------------------------------ local bundle adjustment (B1)
+ * Optimizer::LocalBundleAdjustment(KeyFrame*, bool*) (src/Optimizer.cc:1515-1764)
+ * on g2o's Levenberg-Marquardt with the Schur complement over the map points
+ * (core/block_solver.hpp:354-486): optimize(5), drop the edges with chi2 >
+ * 5.991 or negative depth, optimize(10), flag the outliers again.
+ *
+ * The caller passes the graph the reference builds (Optimizer.cc:1517-1675)
+ * as plain arrays, in the reference's orders:
+ *   keyframes in vertex-id order (mnId), kind 0 = local keyframe, 1 = local
+ *     keyframe that is fixed (mnId == 0; written back), 2 = fixed camera
+ *     (lFixedCameras: a fixed vertex, not written back);
+ *   map points in vertex-id order (mnId), their world positions;
+ *   edges in insertion order (lLocalMapPoints, then each point's
+ *     observations); the edges of one point are contiguous and a point has
+ *     at most one edge per keyframe (map<KeyFrame*, size_t>).
+ * Results: poses of kinds 0/1 (kind 2 copied through), point positions,
+ * per-edge outlier flags (1 = removed after optimize(5), 2 = flagged after
+ * optimize(10); the caller erases those observations, Optimizer.cc:1691-1696,
+ * 1739-1741) and the iterations of the two optimize() calls (-1 = not run).
+ * Limits: at most 32 keyframes of kind 0 per problem, 65536 points. */
+typedef struct gf_ba_problem {
+    int32_t nkf, npts, nedges;
+    const float* kf_Tcw;          /* nkf x 16, row-major KeyFrame::GetPose() */
+    const uint8_t* kf_kind;       /* nkf: 0 local, 1 local fixed, 2 fixed camera */
+    const float* kf_cam;          /* nkf x 4: fx, fy, cx, cy */
+    const float* pt_pos;          /* npts x 3: MapPoint::GetWorldPos() */
+    const int32_t* edge_pt;       /* nedges: point index */
+    const int32_t* edge_kf;       /* nedges: keyframe index */
+    const float* edge_z;          /* nedges x 2: GetKeyPointUn(idx).pt */
+    const float* edge_inv_sigma2; /* nedges: GetInvSigma2(octave) */
+} gf_ba_problem;
+
+typedef struct gf_ba_result {
+    float* kf_Tcw;          /* nkf x 16 */
+    float* pt_pos;          /* npts x 3 */
+    uint8_t* edge_outlier;  /* nedges */
+    int32_t iterations[2];  /* optimize(5), optimize(10) */
+} gf_ba_result;
+
+typedef struct gf_ba_plan gf_ba_plan;
+
+/* Host family: one problem, synchronous. */
+int gf_local_ba(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res);
+
+/* Batched device path: gf_ba_plan_create validates and uploads nprob
+ * problems and builds their structure (index mapping, per-pose edge lists,
+ * Schur panel layout) once; gf_ba_plan_solve runs every problem from its
+ * uploaded initial state to the end on `stream` (all problems advance one LM
+ * trial per step; the host polls a device done flag every few steps; *steps
+ * = steps run); gf_ba_plan_results copies res[0..nprob) out. */
+int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_plan** out);
+int gf_ba_plan_solve(gf_ba_plan* plan, void* stream, int* steps);
+int gf_ba_plan_results(gf_ba_plan* plan, gf_ba_result* res);
+int gf_ba_plan_destroy(gf_ba_plan* plan);
+
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end
  * step stays on the device. One workgroup per frame.

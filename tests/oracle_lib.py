@@ -194,3 +194,20 @@ def ldlt_solve(H, b):
     x = np.zeros(6)
     ok = orc().orc_ldlt_solve(_p(H), _p(b), _p(x))
     return bool(ok), x
+
+
+def local_ba(prob: dict):
+    """Optimizer::LocalBundleAdjustment on the CPU oracle; returns
+    (kf_Tcw [nkf,4,4], pt_pos [npts,3], edge_outlier, iterations)."""
+    from gf_orb_slam_amd.optimizer import BAArrays
+    arr = BAArrays(prob)
+    rc = orc().orc_local_ba(ctypes.byref(arr.problem), ctypes.byref(arr.result))
+    assert rc == 0, rc
+    return arr.out()
+
+
+def inverse3(m):
+    m = np.ascontiguousarray(m, np.float64).reshape(9)
+    r = np.zeros(9)
+    orc().orc_inverse3(_p(m), _p(r))
+    return r.reshape(3, 3)
