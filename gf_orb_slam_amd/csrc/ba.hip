@@ -46,7 +46,7 @@
 namespace {
 
 constexpr int BA_T = 256;     // threads of the point kernels
-constexpr int BA_NSPLIT = 8;  // split-K of the Schur GEMM
+constexpr int BA_MAXSPLIT = 64;  // split-K of the Schur GEMM (per plan: more splits for small batches)
 constexpr int BA_MAXFREE = 32;
 constexpr int BA_MAXN = 6 * BA_MAXFREE;  // LDS of k_ba_solve
 constexpr int BA_MAXPTS = 65536;
@@ -58,7 +58,8 @@ struct BADesc {
     int nkf, npts, nedges, nfree;
     int n, npad, K, sps;  // 6 * nfree; panel width; panel rows; MFMA k-steps per split
     int ntiles, nwg;      // Schur GEMM tiles; point workgroups
-    int kf0, pt0, e0, f0, fe0, pl0, tile0, wg0;
+    int nsplit, newg;     // GEMM k-splits; edge workgroups
+    int kf0, pt0, e0, f0, fe0, pl0, tile0, wg0, mask0, ss0;
     long long panel0;  // Ht at panel0, Wt at panel0 + K * npad (doubles)
 };
 
@@ -102,13 +103,18 @@ struct BAArena {
     const int32_t* f_elist;  // problem-local edge indices, point order
     double *Hpp, *bp, *xp;   // 36, 6, 6 per free pose
     uint8_t* f_act;
-    // dense panels, GEMM tiles, per-workgroup partial sums
+    // dense panels, their per-k-step column-tile masks, GEMM tiles and their
+    // split sums (S lower packed + the coefficient column), per-workgroup partials
     double* panel;
+    const uint16_t* kmask;
     double* tiles;
+    double* Ssum;
     double *wg_chi, *wg_chi_t, *wg_maxd, *wg_scale;
     // outputs
     float* out_T;
     float* out_X;
+    // diagnostics: phase stamps of k_ba_solve (s_memrealtime, 100 MHz) when non-null
+    unsigned long long* tstamp;
 };
 
 __device__ __forceinline__ gfse3::SE3 load_T(const BAArena& A, int buf, int gk) {
@@ -385,128 +391,221 @@ __global__ __launch_bounds__(64) void k_ba_poses(BAArena A) {
 }
 
 // lambda of this trial: computeLambdaInit at the first trial of a round
-// (max |diag| over the active poses and points), else the state's.
-__device__ double trial_lambda(const BAArena& A, const BADesc& d, const BAState& st) {
+// (max |diag| over the active poses and points), else the state's. Called by
+// every thread of a workgroup (block_reduce inside).
+__device__ double trial_lambda(const BAArena& A, const BADesc& d, const BAState& st, double* sh) {
     if (!(st.iter == 0 && st.q == 0)) return st.lambda;
     double m = 0.0;
-    for (int w = 0; w < d.nwg; w++) m = fmax(m, A.wg_maxd[d.wg0 + w]);
-    for (int a = 0; a < d.nfree; a++)
-        if (A.f_act[d.f0 + a])
-            for (int j = 0; j < 6; j++) m = fmax(m, fabs(A.Hpp[(size_t)(d.f0 + a) * 36 + 7 * j]));
-    return 1e-5 * m;
+    for (int w = threadIdx.x; w < d.nwg; w += blockDim.x) m = fmax(m, A.wg_maxd[d.wg0 + w]);
+    for (int u = threadIdx.x; u < 6 * d.nfree; u += blockDim.x)
+        if (A.f_act[d.f0 + u / 6]) m = fmax(m, fabs(A.Hpp[(size_t)(d.f0 + u / 6) * 36 + 7 * (u % 6)]));
+    return 1e-5 * block_reduce(m, sh, true);
 }
 
-// ------------------------------------------------------------------ Schur, per point
+// ------------------------------------------------------------------ Schur, per edge
+// One thread per edge: Dinv of its point (recomputed per edge; the same
+// arithmetic as the point's own), W = Hpl Dinv into the panel Wt. The first
+// active edge of a point also stores Dinv and writes db = Dinv b_l into Wt's
+// column n.
 __global__ __launch_bounds__(BA_T) void k_ba_schur_pts(BAArena A) {
-    __shared__ double s_lam;
+    __shared__ double sh[BA_T / 64];
     const int p = blockIdx.y;
     const BADesc d = A.desc[p];
-    if (blockIdx.x >= d.nwg) return;
+    if (blockIdx.x >= d.newg) return;
     const BAState st = A.st[p];
     if (st.round >= 2) return;
-    if (threadIdx.x == 0) {
-        s_lam = trial_lambda(A, d, st);
-        if (blockIdx.x == 0 && st.iter == 0 && st.q == 0) A.st[p].lambda = s_lam;
-    }
-    __syncthreads();
-    const double lam = s_lam;
-    const int i = blockIdx.x * BA_T + threadIdx.x;
-    if (i >= d.npts) return;
-    const int gp = d.pt0 + i;
-    double* Wt = A.panel + d.panel0 + (size_t)d.K * d.npad;
-    if (!A.pt_act[gp]) {
-        for (int c = 0; c < 3; c++) Wt[(size_t)(3 * i + c) * d.npad + d.n] = 0.0;
-        return;
-    }
+    const double lam = trial_lambda(A, d, st, sh);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && st.iter == 0 && st.q == 0) A.st[p].lambda = lam;
+    const int e = blockIdx.x * BA_T + threadIdx.x;
+    if (e >= d.nedges) return;
+    const int ge = d.e0 + e;
+    if (!A.e_act[ge]) return;
+    const int i = A.e_pt[ge], gp = d.pt0 + i;
+    const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
+    bool first = true;
+    for (int le = A.pt_eb[gp]; le < e; le++) first = first && !A.e_act[d.e0 + le];
+    if (col < 0 && !first) return;
     double D[9], Di[9];
     const double* Hg = A.Hll + (size_t)gp * 9;
+#pragma unroll
     for (int k = 0; k < 9; k++) D[k] = Hg[k] + (k % 4 == 0 ? lam : 0.0);
     inverse3(D, Di);
-    for (int k = 0; k < 9; k++) A.Dinv[(size_t)gp * 9 + k] = Di[k];
-    const double* b = A.bl + (size_t)gp * 3;
-    for (int r = 0; r < 3; r++)
-        Wt[(size_t)(3 * i + r) * d.npad + d.n] = (Di[3 * r] * b[0] + Di[3 * r + 1] * b[1]) + Di[3 * r + 2] * b[2];
-    const int eb = A.pt_eb[gp], ee = A.pt_ee[gp];
-    for (int le = eb; le < ee; le++) {
-        const int ge = d.e0 + le;
-        if (!A.e_act[ge]) continue;
-        const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
-        if (col < 0) continue;
-        const double* H = A.Hpl + (size_t)ge * 18;
+    double* Wt = A.panel + d.panel0 + (size_t)d.K * d.npad;
+    if (first) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) A.Dinv[(size_t)gp * 9 + k] = Di[k];
+        const double* b = A.bl + (size_t)gp * 3;
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            Wt[(size_t)(3 * i + r) * d.npad + d.n] = (Di[3 * r] * b[0] + Di[3 * r + 1] * b[1]) + Di[3 * r + 2] * b[2];
+    }
+    if (col < 0) return;
+    const double* H = A.Hpl + (size_t)ge * 18;
+    double h[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) h[k] = H[k];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
 #pragma unroll
         for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int c = 0; c < 3; c++)
-                Wt[(size_t)(3 * i + c) * d.npad + 6 * col + r] =
-                    (H[3 * r] * Di[c] + H[3 * r + 1] * Di[3 + c]) + H[3 * r + 2] * Di[6 + c];
-    }
+            Wt[(size_t)(3 * i + c) * d.npad + 6 * col + r] =
+                (h[3 * r] * Di[c] + h[3 * r + 1] * Di[3 + c]) + h[3 * r + 2] * Di[6 + c];
 }
 
 // ------------------------------------------------------------------ Schur product on MFMA
-// C[i][j] = sum_k Ht[k][i] Wt[k][j] for the lower-triangle 16x16 tiles of the
+// C[i][j] = sum_k Ht[k][i] Wt[k][j] over the lower-triangle 16x16 tiles of the
 // reduced camera system plus the tiles of column n (the coefficient vector).
-// Workgroup = (tile, split): 4 waves interleave the split's k-steps, then sum
-// their accumulators in wave order.
-__global__ __launch_bounds__(256) void k_ba_gemm(BAArena A) {
-    __shared__ double red[4][4][64];
-    const int p = blockIdx.z, t = blockIdx.x, s = blockIdx.y;
+// Workgroup = (split, problem), 8 waves; wave w owns tiles w + 8u (u < 16)
+// with their accumulators in registers. The split's panel rows stream through
+// LDS in chunks of BA_GCH k-steps (4 rows each, both panels, full width,
+// 16-byte loads); a k-step issues the MFMA of tile (ti, tj) only when its
+// column-tile mask has ti (Ht) and tj (Wt): the panels are block sparse (a
+// map point is seen by a few keyframes) and the mask comes from the graph
+// structure (host, gf_ba_plan_create).
+constexpr int BA_GCH = 8;
+constexpr int BA_GW = 8;    // waves per GEMM workgroup
+constexpr int BA_GTPW = 16; // tiles per wave
+__global__ __launch_bounds__(64 * BA_GW) void k_ba_gemm(BAArena A) {
+    extern __shared__ __align__(16) double gs[];
+    __shared__ uint16_t smask[BA_GCH];
+    const int p = blockIdx.y, s = blockIdx.x;
     const BADesc d = A.desc[p];
-    if (t >= d.ntiles) return;
+    if (s >= d.nsplit) return;
     if (A.st[p].round >= 2) return;
-    const int nt = d.npad >> 4, lower = nt * (nt + 1) / 2;
-    int ti, tj;
-    if (t < lower) {
-        ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
-        tj = t - ti * (ti + 1) / 2;
-    } else {
-        tj = d.n >> 4;
-        ti = t - lower;
-    }
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int nt = d.npad >> 4, lower = nt * (nt + 1) / 2, tdb = d.n >> 4;
+    const int ld = d.npad + 2;  // padded LDS row: the 4 k-rows of an operand fall in different banks
+    double* sa = gs;
+    double* sw = gs + BA_GCH * 4 * ld;
     const double* Ht = A.panel + d.panel0;
     const double* Wt = Ht + (size_t)d.K * d.npad;
-    const int ca = 16 * ti + (l & 15), cb = 16 * tj + (l & 15), kr = l >> 4;
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-    const int j1 = (s + 1) * d.sps;
-#pragma unroll 4
-    for (int j = s * d.sps + w; j < j1; j += 4) {
-        const size_t row = (size_t)(4 * j + kr) * d.npad;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ht[row + ca], Wt[row + cb], acc, 0, 0, 0);
+    const uint16_t* km = A.kmask + d.mask0;
+    const int kr = l >> 4, cl = l & 15;
+    int ti[BA_GTPW], tj[BA_GTPW];
+#pragma unroll
+    for (int u = 0; u < BA_GTPW; u++) {
+        const int t = w + BA_GW * u;
+        if (t >= d.ntiles) {
+            ti[u] = tj[u] = -1;
+        } else if (t < lower) {
+            int a = 0;
+            while ((a + 1) * (a + 2) / 2 <= t) a++;
+            ti[u] = a;
+            tj[u] = t - a * (a + 1) / 2;
+        } else {
+            ti[u] = t - lower;
+            tj[u] = tdb;
+        }
+    }
+    d4 acc[BA_GTPW];
+#pragma unroll
+    for (int u = 0; u < BA_GTPW; u++) acc[u] = (d4){0.0, 0.0, 0.0, 0.0};
+    const int j0 = s * d.sps, j1 = j0 + d.sps, half = d.npad >> 1;
+    for (int c0 = j0; c0 < j1; c0 += BA_GCH) {
+        const int nstep = min(BA_GCH, j1 - c0), nrow = 4 * nstep;
+        if (threadIdx.x < nstep) smask[threadIdx.x] = km[c0 + threadIdx.x];
+        for (int q = threadIdx.x; q < nrow * half; q += 64 * BA_GW) {
+            const int r = q / half, c2 = 2 * (q - r * half);
+            const size_t g = (size_t)(4 * c0 + r) * d.npad + c2;
+            const double2 va = *(const double2*)(Ht + g), vw = *(const double2*)(Wt + g);
+            sa[r * ld + c2] = va.x;
+            sa[r * ld + c2 + 1] = va.y;
+            sw[r * ld + c2] = vw.x;
+            sw[r * ld + c2 + 1] = vw.y;
+        }
+        __syncthreads();
+        for (int js = 0; js < nstep; js++) {
+            const unsigned ma = smask[js], mb = ma | (1u << tdb);
+            if (!ma) continue;
+            const double* ra = sa + (4 * js + kr) * ld + cl;
+            const double* rw = sw + (4 * js + kr) * ld + cl;
+#pragma unroll
+            for (int u = 0; u < BA_GTPW; u++) {
+                if (ti[u] >= 0 && ((ma >> ti[u]) & (mb >> tj[u]) & 1u))
+                    acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra[16 * ti[u]], rw[16 * tj[u]], acc[u], 0, 0, 0);
+            }
+        }
+        __syncthreads();
     }
 #pragma unroll
-    for (int r = 0; r < 4; r++) red[w][r][l] = acc[r];
-    __syncthreads();
-    if (w == 0) {
-        double* out = A.tiles + ((size_t)d.tile0 + (size_t)s * d.ntiles + t) * 256;
+    for (int u = 0; u < BA_GTPW; u++) {
+        if (ti[u] < 0) continue;
+        double* out = A.tiles + ((size_t)d.tile0 + (size_t)s * d.ntiles + w + BA_GW * u) * 256;
 #pragma unroll
         for (int r = 0; r < 4; r++)  // f64 16x16x4 C/D: col = lane & 15, row = (lane >> 4) + 4 r
-            out[((l >> 4) + 4 * r) * 16 + (l & 15)] = ((red[0][r][l] + red[1][r][l]) + red[2][r][l]) + red[3][r][l];
+            out[(kr + 4 * r) * 16 + cl] = acc[u][r];
     }
 }
 
+size_t ba_gemm_lds(int npad) { return sizeof(double) * 2 * BA_GCH * 4 * (npad + 2); }
+
 __device__ __forceinline__ int tri(int i) { return i * (i + 1) / 2; }
 
+// Split sums in split order: Ssum = [S lower packed (n(n+1)/2) | column n (n)].
+__global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
+    const int p = blockIdx.y;
+    const BADesc d = A.desc[p];
+    const int n = d.n, npk = tri(n);
+    const int u = blockIdx.x * 256 + threadIdx.x;
+    if (u >= npk + n) return;
+    if (A.st[p].round >= 2) return;
+    int t, e;
+    if (u < npk) {
+        int i = (int)((sqrt(8.0 * u + 1.0) - 1.0) * 0.5);
+        while (tri(i) > u) i--;
+        while (tri(i + 1) <= u) i++;
+        const int j = u - tri(i);
+        t = tri(i >> 4) + (j >> 4);
+        e = (i & 15) * 16 + (j & 15);
+    } else {
+        const int i = u - npk, ti = i >> 4, tdb = n >> 4, nt = d.npad >> 4;
+        t = ti >= tdb ? tri(ti) + tdb : nt * (nt + 1) / 2 + ti;
+        e = (i & 15) * 16 + (n & 15);
+    }
+    const double* tiles = A.tiles + (size_t)d.tile0 * 256;
+    double g = 0.0;
+    for (int s = 0; s < d.nsplit; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
+    A.Ssum[(size_t)d.ss0 + u] = g;
+}
+
 // ------------------------------------------------------------------ reduced camera system
-__global__ __launch_bounds__(1024) void k_ba_solve(BAArena A) {
+// S = Hpp + lambda I - C (lower, packed in LDS), b_s = b_p - C[:, n]; inactive
+// poses decouple with x = 0. LL^T right-looking with one barrier per column:
+// at step k every thread takes r_k = 1 / sqrt(S_kk) itself and updates its
+// trailing elements with (S_ik r_k)(S_jk r_k) — bit for bit L_ik L_jk — so
+// the scaled column is never waited for; column k is written back, scaled,
+// at step k + 1 when nobody reads it any more. Per element this is the
+// oracle's left-looking order. Forward / back substitution on one wave with
+// the values in registers, broadcast by readlane, in the oracle's order.
+constexpr int BA_ST = 1024;
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffLL), l);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     __shared__ double sL[BA_MAXN * (BA_MAXN + 1) / 2];
-    __shared__ double sb[BA_MAXN];
+    __shared__ double sb[BA_MAXN], sbp[BA_MAXN], srinv[BA_MAXN];
     __shared__ uint8_t sact[BA_MAXFREE];
     __shared__ int s_fail;
-    const int p = blockIdx.x, tid = threadIdx.x;
+    const int p = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const BADesc d = A.desc[p];
     const BAState st = A.st[p];
     if (st.round >= 2) return;
-    const int n = d.n, nt = d.npad >> 4, lower = nt * (nt + 1) / 2, tdb = n >> 4;
+#define BA_STAMP(k)                                                                      \
+    if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+    BA_STAMP(0);
+    const int n = d.n, npk = tri(n);
     const double lam = st.lambda;
-    const double* tiles = A.tiles + (size_t)d.tile0 * 256;
-    for (int a = tid; a < d.nfree; a += 1024) sact[a] = A.f_act[d.f0 + a];
-    if (tid == 0) s_fail = 0;
+    for (int a = tid; a < d.nfree; a += BA_ST) sact[a] = A.f_act[d.f0 + a];
     __syncthreads();
-    // S = Hpp + lambda I - sum_split C (lower, packed); inactive poses decouple (x = 0)
-    for (int i = (tid >> 6); i < n; i += 16) {
+    const double* Sg = A.Ssum + d.ss0;
+    for (int i = w; i < n; i += BA_ST / 64) {
         const int a = i / 6;
-        for (int j = tid & 63; j <= i; j += 64) {
+        for (int j = lane; j <= i; j += 64) {
             const int c = j / 6;
             double v;
             if (!sact[a] || !sact[c]) {
@@ -514,96 +613,144 @@ __global__ __launch_bounds__(1024) void k_ba_solve(BAArena A) {
             } else {
                 v = 0.0;
                 if (a == c) v = A.Hpp[(size_t)(d.f0 + a) * 36 + (i % 6) * 6 + (j % 6)] + (i == j ? lam : 0.0);
-                const int t = tri(i >> 4) + (j >> 4), e = (i & 15) * 16 + (j & 15);
-                double g = 0.0;
-                for (int s = 0; s < BA_NSPLIT; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
-                v = v - g;
+                v = v - Sg[tri(i) + j];
             }
             sL[tri(i) + j] = v;
         }
     }
-    for (int i = tid; i < n; i += 1024) {
-        const int a = i / 6;
-        double v = 0.0;
-        if (sact[a]) {
-            const int ti = i >> 4;
-            const int t = ti >= tdb ? tri(ti) + tdb : lower + ti;
-            const int e = (i & 15) * 16 + (n & 15);
-            double g = 0.0;
-            for (int s = 0; s < BA_NSPLIT; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
-            v = A.bp[(size_t)(d.f0 + a) * 6 + i % 6] - g;
-        }
-        sb[i] = v;
+    for (int i = tid; i < n; i += BA_ST) {
+        const double bpi = A.bp[(size_t)d.f0 * 6 + i];
+        sbp[i] = bpi;
+        sb[i] = sact[i / 6] ? bpi - Sg[npk + i] : 0.0;
     }
     __syncthreads();
-    // LL^T, right-looking; per element the oracle's left-looking order
-    bool fail = false;
-    for (int k = 0; k < n; k++) {
-        const double dkk = sL[tri(k) + k];
-        if (!(dkk > 0.0)) {
-            fail = true;
-            break;
+    BA_STAMP(1);
+    // the owner of S_kk's last update publishes r_k = 1 / sqrt(S_kk) (or the
+    // failure) for step k; step 0's comes from thread 0
+    if (tid == 0) {
+        const double d0 = n > 0 ? sL[0] : 1.0;
+        s_fail = !(d0 > 0.0);
+        srinv[0] = 1.0 / sqrt(d0);
+    }
+    __syncthreads();
+    for (int k = 0; k < n && !s_fail; k++) {
+        const double rk = srinv[k];
+        if (k > 0) {  // write back column k-1, scaled
+            const double rp = srinv[k - 1];
+            for (int i = k + tid; i < n; i += BA_ST) sL[tri(i) + k - 1] *= rp;
         }
-        const double lkk = sqrt(dkk);
-        __syncthreads();
-        if (tid == 0) sL[tri(k) + k] = lkk;
-        for (int i = k + 1 + tid; i < n; i += 1024) sL[tri(i) + k] /= lkk;
-        __syncthreads();
-        for (int i = k + 1 + (tid >> 6); i < n; i += 16) {
-            const double lik = sL[tri(i) + k];
-            for (int j = k + 1 + (tid & 63); j <= i; j += 64) sL[tri(i) + j] -= lik * sL[tri(j) + k];
+        for (int i = k + 1 + w; i < n; i += BA_ST / 64) {  // trailing rows to waves, columns to lanes
+            const int ti = tri(i);
+            const double lik = sL[ti + k] * rk;
+            for (int j = k + 1 + lane; j <= i; j += 64) {
+                const double v = sL[ti + j] - lik * (sL[tri(j) + k] * rk);
+                sL[ti + j] = v;
+                if (j == k + 1 && i == k + 1) {  // S_{k+1,k+1} is final: publish step k+1's pivot
+                    if (!(v > 0.0)) s_fail = 1;
+                    srinv[k + 1] = 1.0 / sqrt(v);
+                }
+            }
         }
         __syncthreads();
     }
-    if (!fail && tid < 64) {  // one wave: values in registers, broadcast per step
+    const bool fail = s_fail;
+    __syncthreads();
+    BA_STAMP(2);
+    if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 5] = __builtin_amdgcn_s_memtime();
+    if (!fail && w == 0) {  // the scaled last column needs no write-back (no entries below its diagonal)
         double r[3];
-        for (int u = 0; u < 3; u++) r[u] = (tid + 64 * u < n) ? sb[tid + 64 * u] : 0.0;
-        for (int k = 0; k < n; k++) {  // forward: y_k = r_k / L_kk, r_i -= L_ik y_k
+        for (int u = 0; u < 3; u++) r[u] = (lane + 64 * u < n) ? sb[lane + 64 * u] : 0.0;
+        // forward: y_k = r_k / L_kk, r_i -= L_ik y_k; next step's L column and 1 / L_kk loaded ahead
+        double Ln[3], rn = n > 0 ? srinv[0] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = lane + 64 * u;
+            Ln[u] = (i > 0 && i < n) ? sL[tri(i)] : 0.0;
+        }
+        for (int k = 0; k < n; k++) {
+            double Lc[3];
+#pragma unroll
+            for (int u = 0; u < 3; u++) Lc[u] = Ln[u];
+            const double rc = rn;
+            if (k + 1 < n) {
+#pragma unroll
+                for (int u = 0; u < 3; u++) {
+                    const int i = lane + 64 * u;
+                    Ln[u] = (i > k + 1 && i < n) ? sL[tri(i) + k + 1] : 0.0;
+                }
+                rn = srinv[k + 1];
+            }
             const int reg = k >> 6;
             const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
-            const double yk = __shfl(mine, k & 63, 64) / sL[tri(k) + k];
-            for (int u = 0; u < 3; u++) {
-                const int i = tid + 64 * u;
-                if (i == k) r[u] = yk;
-                else if (i > k && i < n) r[u] -= sL[tri(i) + k] * yk;
+            const double yk = readlane_d(mine, k & 63) * rc;
+#pragma unroll
+            for (int u = 0; u < 3; u++) {  // Lc = 0 off the rows below k: r - 0 * y = r
+                const double upd = r[u] - Lc[u] * yk;
+                r[u] = (lane + 64 * u == k) ? yk : upd;
             }
         }
-        for (int k = n - 1; k >= 0; k--) {  // backward: x_k = r_k / L_kk, r_i -= L_ki x_k (descending k)
+        // backward: x_k = r_k / L_kk, r_i -= L_ki x_k (descending k); row k of L loaded ahead
+        rn = n > 0 ? srinv[n - 1] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = lane + 64 * u;
+            Ln[u] = (n > 0 && i < n - 1) ? sL[tri(n - 1) + i] : 0.0;
+        }
+        for (int k = n - 1; k >= 0; k--) {
+            double Lc[3];
+#pragma unroll
+            for (int u = 0; u < 3; u++) Lc[u] = Ln[u];
+            const double rc = rn;
+            if (k > 0) {
+#pragma unroll
+                for (int u = 0; u < 3; u++) {
+                    const int i = lane + 64 * u;
+                    Ln[u] = (i < k - 1) ? sL[tri(k - 1) + i] : 0.0;
+                }
+                rn = srinv[k - 1];
+            }
             const int reg = k >> 6;
             const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
-            const double xk = __shfl(mine, k & 63, 64) / sL[tri(k) + k];
-            for (int u = 0; u < 3; u++) {
-                const int i = tid + 64 * u;
-                if (i == k) r[u] = xk;
-                else if (i < k) r[u] -= sL[tri(k) + i] * xk;
+            const double xk = readlane_d(mine, k & 63) * rc;
+#pragma unroll
+            for (int u = 0; u < 3; u++) {  // Lc = 0 off the rows above k
+                const double upd = r[u] - Lc[u] * xk;
+                r[u] = (lane + 64 * u == k) ? xk : upd;
             }
         }
+#pragma unroll
         for (int u = 0; u < 3; u++)
-            if (tid + 64 * u < n) sb[tid + 64 * u] = r[u];
+            if (lane + 64 * u < n) sb[lane + 64 * u] = r[u];
     }
-    if (fail && tid == 0) s_fail = 1;
     __syncthreads();
-    const bool ok = !s_fail;
-    if (ok)
-        for (int i = tid; i < n; i += 1024) A.xp[(size_t)d.f0 * 6 + i] = sb[i];
+    BA_STAMP(3);
+    if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 6] = __builtin_amdgcn_s_memtime();
+    if (fail) {  // Solver::_x keeps its previous value
+        for (int i = tid; i < n; i += BA_ST) sb[i] = A.xp[(size_t)d.f0 * 6 + i];
+    } else {
+        for (int i = tid; i < n; i += BA_ST) A.xp[(size_t)d.f0 * 6 + i] = sb[i];
+    }
     __syncthreads();
-    // trial poses: exp(x) * T for the active free poses (stale x when the solve failed)
+    // trial poses: exp(x) * T for the active free poses
     const int cur = st.cur;
-    for (int k = tid; k < d.nkf; k += 1024) {
+    for (int k = tid; k < d.nkf; k += BA_ST) {
         gfse3::SE3 T = load_T(A, cur, d.kf0 + k);
         const int col = A.kf_col[d.kf0 + k];
-        if (col >= 0 && sact[col]) T = gfse3::exp_mul(A.xp + (size_t)(d.f0 + col) * 6, T);
+        if (col >= 0 && sact[col]) {
+            double x6[6];
+            for (int r = 0; r < 6; r++) x6[r] = sb[6 * col + r];
+            T = gfse3::exp_mul(x6, T);
+        }
         store_T(A, 1 - cur, d.kf0 + k, T);
     }
     if (tid == 0) {  // computeScale, pose part (index order)
         double sc = 0.0;
-        for (int i = 0; i < n; i++) {
-            const double xi = A.xp[(size_t)d.f0 * 6 + i];
-            sc += xi * (lam * xi + A.bp[(size_t)d.f0 * 6 + i]);
-        }
+        for (int i = 0; i < n; i++) sc += sb[i] * (lam * sb[i] + sbp[i]);
         A.st[p].scale_p = sc;
-        A.st[p].chol_ok = ok ? 1 : 0;
+        A.st[p].chol_ok = fail ? 0 : 1;
     }
+    BA_STAMP(4);
+#undef BA_STAMP
 }
 
 // ------------------------------------------------------------------ landmarks, trial errors
@@ -678,22 +825,29 @@ __global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
 // ------------------------------------------------------------------ LM decision + outlier pass
 __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
     __shared__ int s_end, s_cnt;
+    __shared__ double s_part[3][BA_MAXPTS / BA_T];
     const int p = blockIdx.x, tid = threadIdx.x;
     const BADesc d = A.desc[p];
     if (A.st[p].round >= 2) return;
+    for (int w = tid; w < d.nwg; w += 1024) {  // partial sums staged in LDS, summed in order by one thread
+        s_part[0][w] = A.wg_chi[d.wg0 + w];
+        s_part[1][w] = A.wg_chi_t[d.wg0 + w];
+        s_part[2][w] = A.wg_scale[d.wg0 + w];
+    }
+    __syncthreads();
     if (tid == 0) {
         BAState st = A.st[p];
         if (st.q == 0) {  // activeRobustChi2 at the iteration start
             double c = 0.0;
-            for (int w = 0; w < d.nwg; w++) c += A.wg_chi[d.wg0 + w];
+            for (int w = 0; w < d.nwg; w++) c += s_part[0][w];
             st.currentChi = c;
             st.iniChi = c;
         }
         double tempChi = 0.0;
-        for (int w = 0; w < d.nwg; w++) tempChi += A.wg_chi_t[d.wg0 + w];
+        for (int w = 0; w < d.nwg; w++) tempChi += s_part[1][w];
         if (!st.chol_ok) tempChi = DBL_MAX;
         double scale = st.scale_p;
-        for (int w = 0; w < d.nwg; w++) scale += A.wg_scale[d.wg0 + w];
+        for (int w = 0; w < d.nwg; w++) scale += s_part[2][w];
         scale += 1e-3;
         const double rho = (st.currentChi - tempChi) / scale;
         if (rho > 0 && isfinite(tempChi)) {
@@ -767,6 +921,7 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         }
         cnt++;
     }
+    for (int i = tid; i < 3 * d.npts; i += 1024) Wt[(size_t)i * d.npad + d.n] = 0.0;  // db column of dropped points
     for (int i = tid; i < 6 * d.nfree; i += 1024) A.xp[(size_t)d.f0 * 6 + i] = 0.0;  // new structure: fresh _x
     for (int i = tid; i < 3 * d.npts; i += 1024) A.xl[(size_t)d.pt0 * 3 + i] = 0.0;
     atomicAdd(&s_cnt, cnt);
@@ -830,7 +985,7 @@ struct gf_ba_plan {
     gf_ctx* ctx = nullptr;
     int nprob = 0;
     std::vector<BADesc> desc;
-    int max_nwg = 1, max_free = 1, max_tiles = 1;
+    int max_nwg = 1, max_free = 1, max_tiles = 1, max_newg = 1, max_split = 1, max_ss = 1, max_npad = 16;
     size_t panel_doubles = 0;
     BAArena A{};
     std::vector<void*> owned;
@@ -844,7 +999,8 @@ namespace {
 int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
     const BAArena& A = P->A;
     const int B = P->nprob;
-    const dim3 gpt(P->max_nwg, B), gpose(P->max_free, B), ggemm(P->max_tiles, BA_NSPLIT, B);
+    const dim3 gpt(P->max_nwg, B), gpose(P->max_free, B), gedge(P->max_newg, B), ggemm(P->max_split, B),
+        gred((P->max_ss + 255) / 256, B);
     {
         GF_PROF(P->ctx, s, "k_ba_linearize");
         k_ba_linearize<<<gpt, BA_T, 0, s>>>(A);
@@ -855,15 +1011,19 @@ int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
     }
     {
         GF_PROF(P->ctx, s, "k_ba_schur_pts");
-        k_ba_schur_pts<<<gpt, BA_T, 0, s>>>(A);
+        k_ba_schur_pts<<<gedge, BA_T, 0, s>>>(A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_gemm");
-        k_ba_gemm<<<ggemm, 256, 0, s>>>(A);
+        k_ba_gemm<<<ggemm, 64 * BA_GW, ba_gemm_lds(P->max_npad), s>>>(A);
+    }
+    {
+        GF_PROF(P->ctx, s, "k_ba_gemm_reduce");
+        k_ba_gemm_reduce<<<gred, 256, 0, s>>>(A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_solve");
-        k_ba_solve<<<B, 1024, 0, s>>>(A);
+        k_ba_solve<<<B, BA_ST, 0, s>>>(A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_update");
@@ -899,6 +1059,9 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     std::vector<int32_t> kf_col, pt_eb, pt_ee, e_pt, e_kf, f_kf, f_eptr, f_elist;
     std::vector<double> e_meas;
     std::vector<float> kf_T, pt_pos;
+    std::vector<uint16_t> kmask;
+    const int nsplit = std::max(1, std::min(BA_MAXSPLIT, (256 + std::max(nprob, 1) - 1) / std::max(nprob, 1)));
+    int ss_tot = 0;
     std::vector<uint8_t> kf_kind;
     int nkf_tot = 0, npt_tot = 0, ne_tot = 0, nf_tot = 0, ntile_tot = 0, nwg_tot = 0;
     long long panel = 0;
@@ -974,24 +1137,38 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
             acc += (int)lists[a].size();
         }
         f_eptr.push_back(acc);
-        // Schur panel / GEMM geometry
+        // Schur panel / GEMM geometry; per k-step (4 panel rows) the column tiles a point block touches
         d.n = 6 * nfree;
         d.npad = ((d.n + 1 + 15) / 16) * 16;
         const int steps = std::max(1, (3 * Q.npts + 3) / 4);
-        d.sps = (steps + BA_NSPLIT - 1) / BA_NSPLIT;
-        d.K = BA_NSPLIT * d.sps * 4;
+        d.nsplit = nsplit;
+        d.sps = (steps + nsplit - 1) / nsplit;
+        d.K = nsplit * d.sps * 4;
         const int nt = d.npad / 16;
         d.ntiles = nt * (nt + 1) / 2 + (d.n >> 4);
+        GF_CHECK(d.ntiles <= BA_GW * BA_GTPW, GF_ERR_UNSUPPORTED, "Schur GEMM tile count");
         d.nwg = std::max(1, (Q.npts + BA_T - 1) / BA_T);
+        d.newg = std::max(1, (Q.nedges + BA_T - 1) / BA_T);
         d.tile0 = ntile_tot;
         d.wg0 = nwg_tot;
         d.panel0 = panel;
+        d.mask0 = (int)kmask.size();
+        d.ss0 = ss_tot;
+        kmask.resize(kmask.size() + (size_t)nsplit * d.sps, 0);
+        for (int i = 0; i < Q.npts; i++)
+            for (int e = eb[i]; e < ee[i]; e++) {
+                const int c = col[Q.edge_kf[e]];
+                if (c < 0) continue;
+                const uint16_t bits = (uint16_t)((1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4)));
+                for (int r = 3 * i; r < 3 * i + 3; r++) kmask[d.mask0 + r / 4] |= bits;
+            }
         nkf_tot += Q.nkf;
         npt_tot += Q.npts;
         ne_tot += Q.nedges;
         nf_tot += nfree;
-        ntile_tot += BA_NSPLIT * d.ntiles;
+        ntile_tot += nsplit * d.ntiles;
         nwg_tot += d.nwg;
+        ss_tot += d.n * (d.n + 1) / 2 + d.n;
         panel += 2LL * d.K * d.npad;
     }
     GF_HIP(hipSetDevice(ctx->device));
@@ -1003,6 +1180,10 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         P->max_nwg = std::max(P->max_nwg, d.nwg);
         P->max_free = std::max(P->max_free, d.nfree);
         P->max_tiles = std::max(P->max_tiles, d.ntiles);
+        P->max_newg = std::max(P->max_newg, d.newg);
+        P->max_split = std::max(P->max_split, d.nsplit);
+        P->max_ss = std::max(P->max_ss, d.n * (d.n + 1) / 2 + d.n);
+        P->max_npad = std::max(P->max_npad, d.npad);
     }
     P->panel_doubles = (size_t)panel;
     BAArena& A = P->A;
@@ -1011,7 +1192,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     int rc = 0;
     BADesc* dd;
     BAState* ds;
-    double *kfT, *ptX, *Hll, *bl, *Dinv, *xl, *e_err, *Hpl, *Hpp, *bp, *xp, *pnl, *tiles, *w0, *w1, *w2, *w3;
+    double *kfT, *ptX, *Hll, *bl, *Dinv, *xl, *e_err, *Hpl, *Hpp, *bp, *xp, *pnl, *tiles, *w0, *w1, *w2, *w3, *ssum;
+    uint16_t* kmk;
     float *kT0, *pX0, *oT, *oX;
     uint8_t *kk, *pa, *ea, *eo, *fa;
     int32_t *kc, *peb, *pee, *ept, *ekf, *fkf, *fep, *fel;
@@ -1033,7 +1215,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         (rc = dalloc(&pnl, P->panel_doubles, o)) || (rc = dalloc(&tiles, 256 * (size_t)ntile_tot, o)) ||
         (rc = dalloc(&w0, nwg_tot, o)) || (rc = dalloc(&w1, nwg_tot, o)) || (rc = dalloc(&w2, nwg_tot, o)) ||
         (rc = dalloc(&w3, nwg_tot, o)) || (rc = dalloc(&oT, 16 * (size_t)nkf_tot, o)) ||
-        (rc = dalloc(&oX, 3 * (size_t)npt_tot, o))) {
+        (rc = dalloc(&oX, 3 * (size_t)npt_tot, o)) || (rc = dalloc(&kmk, kmask.size(), o)) ||
+        (rc = dalloc(&ssum, ss_tot, o))) {
         gf_ba_plan_destroy(P);
         return rc;
     }
@@ -1052,7 +1235,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         (he = up(pee, pt_ee.data(), 4 * pt_ee.size())) || (he = up(ept, e_pt.data(), 4 * e_pt.size())) ||
         (he = up(ekf, e_kf.data(), 4 * e_kf.size())) || (he = up(em, e_meas.data(), 8 * e_meas.size())) ||
         (he = up(fkf, f_kf.data(), 4 * f_kf.size())) || (he = up(fep, f_eptr.data(), 4 * f_eptr.size())) ||
-        (he = up(fel, f_elist.data(), 4 * f_elist.size())) || (he = hipStreamSynchronize(s))) {
+        (he = up(fel, f_elist.data(), 4 * f_elist.size())) || (he = up(kmk, kmask.data(), 2 * kmask.size())) ||
+        (he = hipStreamSynchronize(s))) {
         gf_ba_plan_destroy(P);
         return gf::fail(GF_ERR_HIP, hipGetErrorString(he));
     }
@@ -1088,6 +1272,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     A.f_act = fa;
     A.panel = pnl;
     A.tiles = tiles;
+    A.kmask = kmk;
+    A.Ssum = ssum;
     A.wg_chi = w0;
     A.wg_chi_t = w1;
     A.wg_maxd = w2;
@@ -1097,6 +1283,18 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     *out = P;
     return GF_OK;
 }
+
+}  // extern "C"
+
+// Diagnostics (not in the ABI header): device buffer of 8 stamps per problem
+// written by k_ba_solve, or nullptr.
+extern "C" int gf_ba_plan_debug_stamps(gf_ba_plan* P, unsigned long long* d_stamps) {
+    GF_CHECK(P, GF_ERR_ARG, "null plan");
+    P->A.tstamp = d_stamps;
+    return GF_OK;
+}
+
+extern "C" {
 
 int gf_ba_plan_solve(gf_ba_plan* P, void* stream, int* steps) {
     GF_CHECK(P, GF_ERR_ARG, "null plan");

@@ -19,8 +19,9 @@
 // Parity unpinned for the linear solve: the reference factors the reduced
 // camera system with CHOLMOD (solvers/cholmod/linear_solver_cholmod.h:115-154,
 // AMD ordering; CHOLMOD is not vendored). This restatement
-// factors the same matrix with a dense LL^T in natural order (forward
-// substitution with ascending, back substitution with descending sums) and
+// factors the same matrix with a dense LL^T in natural order (divisions by
+// L_jj as products with its reciprocal; forward substitution with ascending,
+// back substitution with descending sums) and
 // treats a non-positive pivot as CHOLMOD_NOT_POSDEF (solve() returns false,
 // Solver::_x keeps its previous value). Solver::_x is zeroed whenever the
 // structure is rebuilt (g2o leaves it uninitialised). Every other sum runs in
@@ -249,29 +250,31 @@ struct LBA {
                 }
             }
         }
-        // dense LL^T of the upper-stored S (CHOLMOD stand-in, see header)
-        std::vector<double> L((size_t)n * n, 0.0), y(n), xs(n);
+        // dense LL^T of the upper-stored S (CHOLMOD stand-in, see header);
+        // divisions by L_jj are multiplications by its reciprocal
+        std::vector<double> L((size_t)n * n, 0.0), rinv(n), y(n), xs(n);
         for (int j = 0; j < n; j++) {
             double s = S[(size_t)j * n + j];
             for (int k = 0; k < j; k++) s -= L[(size_t)j * n + k] * L[(size_t)j * n + k];
             if (!(s > 0.0)) return false;
             const double dj = std::sqrt(s);
             L[(size_t)j * n + j] = dj;
+            rinv[j] = 1.0 / dj;
             for (int i = j + 1; i < n; i++) {
                 double t = S[(size_t)j * n + i];
                 for (int k = 0; k < j; k++) t -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
-                L[(size_t)i * n + j] = t / dj;
+                L[(size_t)i * n + j] = t * rinv[j];
             }
         }
         for (int i = 0; i < n; i++) {
             double s = bp[i] - coef[i];  // _bschur = _b - coefficients
             for (int k = 0; k < i; k++) s -= L[(size_t)i * n + k] * y[k];
-            y[i] = s / L[(size_t)i * n + i];
+            y[i] = s * rinv[i];
         }
         for (int i = n - 1; i >= 0; i--) {
             double s = y[i];
             for (int k = n - 1; k > i; k--) s -= L[(size_t)k * n + i] * xs[k];
-            xs[i] = s / L[(size_t)i * n + i];
+            xs[i] = s * rinv[i];
         }
         for (int i = 0; i < n; i++) x[i] = xs[i];
         // landmarks: cl = bl + Hpl^T (-xp) (column blocks in pose order), xl = Dinv cl
