@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -88,6 +89,82 @@ def single_stream(camera: str, nfeat: int, budget: int, steps: int) -> dict:
     return {"ms_per_frame": round(dt * 1e3, 3), "fps": round(1.0 / dt, 2), "steps": steps}
 
 
+def schur_flops(prob: dict) -> float:
+    """Algorithmic flops of one Schur contraction (k_ba_gemm) for one LBA
+    window: per map point with k edges to local (free) keyframes, the k(k+1)/2
+    6x6 blocks W_i Hpl_j^T (3 products each) and the k 6-vectors Hpl_i db."""
+    free = prob["kf_kind"][prob["edge_kf"]] == 0
+    k = np.bincount(prob["edge_pt"][free], minlength=len(prob["pt_pos"])).astype(np.float64)
+    return float((k * (k + 1) / 2 * 36 * 3 * 2 + k * 6 * 3 * 2).sum())
+
+
+def lba_leg(batch: int, repeats: int = 3, cpu: bool = True) -> dict:
+    """Config 4: LocalBundleAdjustment on synthetic 20-keyframe x
+    3000-point windows, `batch` independent windows solved together on the
+    device (inputs resident), plus the single-window latency."""
+    import torch
+
+    from gf_orb_slam_amd._lib import check, lib
+    from gf_orb_slam_amd.optimizer import LocalBAPlan
+    from gf_orb_slam_amd.synth import synth_lba_problem
+
+    out = {"workload": "config 4: LocalBundleAdjustment, 20 keyframes (17-19 local) x 3000 map points, ~15k edges",
+           "dtype": "f64"}
+    for B in sorted({1, batch}):
+        probs = [synth_lba_problem(1000 + i, 20, 3000) for i in range(B)]
+        plan = LocalBAPlan(probs)
+        plan.solve()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(repeats):
+            steps = plan.solve()
+        dt = (time.perf_counter() - t0) / repeats
+        res = plan.results()
+        iters = np.array([r[3] for r in res], np.float64)
+        check(lib().gf_prof_enable(plan.ctx.handle, 1))
+        check(lib().gf_prof_reset(plan.ctx.handle))
+        plan.solve()
+        prof = {}
+        i = 0
+        name = ctypes.create_string_buffer(64)
+        while True:
+            ms, cnt = ctypes.c_double(), ctypes.c_int()
+            if lib().gf_prof_report(plan.ctx.handle, i, name, 64, ctypes.byref(ms), ctypes.byref(cnt)) != 0:
+                break
+            prof[name.value.decode()] = (ms.value, cnt.value)
+            i += 1
+        check(lib().gf_prof_enable(plan.ctx.handle, 0))
+        plan.close()
+        g_ms, g_n = prof.get("k_ba_gemm", (0.0, 1))
+        flops = sum(schur_flops(p) for p in probs)
+        entry = {"problems": B, "ms_per_batch": round(dt * 1e3, 3), "solves_per_s": round(B / dt, 2),
+                 "ms_per_solve_amortized": round(dt * 1e3 / B, 4), "steps": steps,
+                 "lm_iterations": [round(float(x), 2) for x in iters.mean(0)],
+                 "ms_per_lm_iteration": round(dt * 1e3 / float(iters.sum(1).mean()), 4),
+                 "kernels": {k: {"avg_us": round(v[0] / max(v[1], 1) * 1e3, 2), "launches": v[1]}
+                             for k, v in prof.items()}}
+        if g_ms > 0:
+            tf = flops / (g_ms / g_n / 1e3) / 1e12
+            entry["schur_gemm"] = {"bound": "mfma", "achieved": round(tf, 4), "peak": 78.6, "unit": "TFLOP/s",
+                                   "frac": round(tf / 78.6, 6), "algorithmic_flops_per_launch": flops,
+                                   "note": "f64 MFMA 16x16x4; peak = AMD spec FP64 matrix (not measured here)"}
+        out["batch_%d" % B] = entry
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+
+        p = synth_lba_problem(1000, 20, 3000)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 5.0:
+            oracle_lib.local_ba(p)
+            n += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n / dt, 3), "unit": "solves/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} solves of one config-4 window, 1 thread, {dt:.1f} s (dense LL^T in "
+                                         f"place of CHOLMOD)"}
+    return out
+
+
 def share_startup_state(dist, device, world: int, rank: int, nbytes: int = 45 * 1024 * 1024):
     """The one exchange step: rank 0 broadcasts the shared
     vocabulary/map blob to every rank (RCCL over xGMI on the GPU box, gloo in
@@ -122,6 +199,7 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lba-batch", type=int, default=64, help="local-BA windows solved together (0: skip)")
     ap.add_argument("--single-stream-steps", type=int, default=20,
                     help="also time one stream alone (per-frame latency of a single sequence)")
     args = ap.parse_args()
@@ -239,6 +317,8 @@ def main():
     }
     if rank == 0 and args.single_stream_steps > 0:
         out["single_stream"] = single_stream(cam, args.nfeatures, args.gf_budget, args.single_stream_steps)
+    if rank == 0 and args.lba_batch > 0:
+        out["local_ba"] = lba_leg(args.lba_batch, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures)
     if rank == 0:

@@ -107,6 +107,15 @@ _PROTOS = {
     "gf_pose_opt": [_P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
     "gf_pose_opt_batch_dev": [_P, _I, _P, _P, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P],
     "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P, _P],
+    "gf_vocab_read": [_P, _P],
+    "gf_vocab_create": [_P, _P, _P],
+    "gf_vocab_load": [_P, _P, _P],
+    "gf_vocab_info": [_P, _P, _P, _P, _P],
+    "gf_vocab_destroy": [_P],
+    "gf_bow_transform": [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "gf_bow_transform_dev": [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
+    "gf_match_bow": [_P, _I, _F, _I, _P, _P, _P, _P],
+    "gf_match_bow_dev": [_P, _I, _F, _I, _I, _P, _P, _P, _P, _P],
     "gf_local_ba": [_P, _P, _P],
     "gf_ba_plan_create": [_P, _I, _P, _P],
     "gf_ba_plan_solve": [_P, _P, _P],

@@ -43,7 +43,7 @@ struct gf_ctx {
     std::vector<gf::ProfEntry> prof_entries;
     std::vector<hipEvent_t> event_pool;
     // grow-only device scratch for the host-family wrappers (one slot per use)
-    static const int kSlots = 48;
+    static const int kSlots = 64;
     void* ws[kSlots] = {};
     size_t ws_size[kSlots] = {};
 };

@@ -285,3 +285,68 @@ def synth_lba_problem(seed: int, nkf: int = 20, npts: int = 3000, nfixed: int = 
             "edge_z": np.ascontiguousarray(z, np.float32),
             "edge_inv_sigma2": invs[rng.integers(0, nlevels, len(e_pt))],
             "T_true": T_true.astype(np.float32), "X_true": X.astype(np.float32)}
+
+
+def synth_vocabulary(seed: int = 7, k: int = 10, L: int = 3, flip: int = 40, stop_frac: float = 0.02,
+                     scoring: int = 0, weighting: int = 0) -> dict:
+    """A k-ary, L-level ORB vocabulary tree in the loaders' node order (SURVEY.md
+    §8d: random-descriptor tree, seed 7): breadth first, so a node's children
+    are consecutive records. Level-1 descriptors are random; a child is its
+    parent with `flip` random bits flipped, so descents are informative.
+    Leaves carry idf-like weights in [0.5, 5) with `stop_frac` stopped (0)."""
+    rng = np.random.default_rng(seed)
+    parent, desc, leaf = [-1], [np.zeros(32, np.uint8)], [0]
+    level = [0]
+    for lev in range(1, L + 1):
+        nxt = []
+        for p in level:
+            base = desc[p] if lev > 1 else None
+            for _ in range(k):
+                if base is None:
+                    d = rng.integers(0, 256, 32, dtype=np.uint8)
+                else:
+                    d = flip_bits(rng, base[None], flip)[0] if flip else base.copy()
+                parent.append(p)
+                desc.append(d)
+                leaf.append(1 if lev == L else 0)
+                nxt.append(len(parent) - 1)
+        level = nxt
+    n = len(parent)
+    weight = np.zeros(n)
+    lv = np.array(leaf, bool)
+    weight[lv] = rng.uniform(0.5, 5.0, lv.sum())
+    weight[lv & (rng.uniform(size=n) < stop_frac)] = 0.0
+    return {"k": k, "L": L, "scoring": scoring, "weighting": weighting, "parent": np.array(parent, np.int32),
+            "desc": np.ascontiguousarray(np.stack(desc), np.uint8), "weight": weight, "is_leaf": lv.astype(np.uint8)}
+
+
+def vocab_features(voc: dict, n: int, seed: int, flip: int = 20) -> np.ndarray:
+    """Descriptors drawn near random leaves of the vocabulary (a frame's ORB
+    features), so FeatureVector nodes hold several features."""
+    rng = np.random.default_rng(seed)
+    leaves = np.nonzero(voc["is_leaf"])[0]
+    src = voc["desc"][rng.choice(leaves, n)]
+    return np.ascontiguousarray(flip_bits(rng, src, flip))
+
+
+def write_vocab_binary(voc: dict, path: str) -> None:
+    """TemplatedVocabulary::saveToBinaryFile layout (TemplatedVocabulary.h:1516-1536)."""
+    n = len(voc["parent"])
+    rec = np.zeros(n - 1, np.dtype([("parent", "<i4"), ("desc", "u1", 32), ("weight", "<f4"), ("leaf", "u1")]))
+    rec["parent"] = voc["parent"][1:]
+    rec["desc"] = voc["desc"][1:]
+    rec["weight"] = voc["weight"][1:]
+    rec["leaf"] = voc["is_leaf"][1:]
+    with open(path, "wb") as f:
+        f.write(np.array([n, 41], "<u4").tobytes())
+        f.write(np.array([voc["k"], voc["L"], voc["scoring"], voc["weighting"]], "<i4").tobytes())
+        f.write(rec.tobytes())
+
+
+def write_vocab_text(voc: dict, path: str) -> None:
+    """TemplatedVocabulary::saveToTextFile layout (TemplatedVocabulary.h:1443-1462)."""
+    with open(path, "w") as f:
+        f.write(f"{voc['k']} {voc['L']}  {voc['scoring']} {voc['weighting']}\n")
+        for i in range(1, len(voc["parent"])):
+            d = " ".join(str(int(x)) for x in voc["desc"][i])
+            f.write(f"{voc['parent'][i]} {int(voc['is_leaf'][i])} {d}  {float(voc['weight'][i])!r}\n")

@@ -362,6 +362,78 @@ int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keyp
                            uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, int32_t* d_nedges,
                            void* stream);
 
+/* --------------------------------------- ORB vocabulary, BoW (D1), SearchByBoW (M6)
+ * A DBoW2 ORB vocabulary tree (TemplatedVocabulary<FORB::TDescriptor, FORB>,
+ * Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) as its loaders build it:
+ * node 0 is the root; nodes 1..nnodes-1 in file record order with their
+ * parent, 32-byte descriptor, weight and leaf flag; a node's children in
+ * record order; word ids in record order of the leaves. scoring is DBoW2's
+ * ScoringType (0 L1_NORM, 1 L2_NORM, 2 CHI_SQUARE, 3 KL, 4 BHATTACHARYYA,
+ * 5 DOT_PRODUCT), weighting its WeightingType (0 TF_IDF, 1 TF, 2 IDF, 3 BINARY). */
+typedef struct gf_vocab_arrays {
+    int32_t k, L, scoring, weighting, nnodes;
+    int32_t* parent;  /* nnodes; parent[0] = -1 */
+    uint8_t* desc;    /* nnodes x 32 */
+    double* weight;   /* nnodes */
+    uint8_t* is_leaf; /* nnodes */
+} gf_vocab_arrays;
+
+typedef struct gf_vocab gf_vocab;
+
+/* Host only: parse a vocabulary file — loadFromTextFile (TemplatedVocabulary.h:1352-1432)
+ * for a ".txt" path, loadFromBinaryFile (:1469-1510) otherwise. With out->parent
+ * == NULL only the header fields and nnodes are filled; call again with buffers
+ * of nnodes entries. */
+int gf_vocab_read(const char* path, gf_vocab_arrays* out);
+/* Upload a tree (device-resident, shared by every frame of the context). */
+int gf_vocab_create(gf_ctx* ctx, const gf_vocab_arrays* tree, gf_vocab** out);
+/* gf_vocab_read + gf_vocab_create (main.cc:92-106 picks the loader by suffix). */
+int gf_vocab_load(gf_ctx* ctx, const char* path, gf_vocab** out);
+int gf_vocab_info(gf_vocab* voc, int* k, int* L, int* nnodes, int* nwords);
+int gf_vocab_destroy(gf_vocab* voc);
+
+/* Frame::ComputeBoW (Frame.cc:380-387) = transform(descriptors, mBowVec,
+ * mFeatVec, levelsup) (TemplatedVocabulary.h:1141-1208, 1232-1273): the
+ * BowVector as words[0..nwords) ascending with values, the FeatureVector as
+ * fv_nodes[0..nfv) ascending with the feature indices of node i in
+ * fv_feats[fv_start[i] .. fv_start[i+1]). Capacities n (fv_start n + 1).
+ * At most 4096 descriptors per frame. */
+int gf_bow_transform(gf_vocab* voc, const uint8_t* desc, int n, int levelsup, int32_t* words, double* values,
+                     int* nwords, int32_t* fv_nodes, int32_t* fv_start, int32_t* fv_feats, int* nfv);
+/* Device family: nframes frames, descriptors and outputs strided by cap. */
+int gf_bow_transform_dev(gf_vocab* voc, int nframes, const uint8_t* d_desc, const int32_t* d_n, int cap, int levelsup,
+                         int32_t* d_words, double* d_values, int32_t* d_nwords, int32_t* d_fv_nodes,
+                         int32_t* d_fv_start, int32_t* d_fv_feats, int32_t* d_nfv, void* stream);
+
+/* One side of ORBmatcher::SearchByBoW: its FeatureVector, descriptors,
+ * keypoints (for the angle) and map point per feature (-1 = none or bad). */
+typedef struct gf_bow_side {
+    const int32_t* fv_nodes;
+    const int32_t* fv_start;
+    const int32_t* fv_feats;
+    int32_t nfv;
+    const uint8_t* desc;
+    const gf_keypoint* kps;
+    const int32_t* mp;
+    int32_t n;
+} gf_bow_side;
+
+/* mode 0: SearchByBoW(KeyFrame* a, Frame& b, vpMapPointMatches)
+ *   (ORBmatcher.cc:724-853): out has b.n entries, out[j] = a's map point
+ *   matched to b feature j or -1; a feature needs a map point, best <= TH_LOW.
+ * mode 1: SearchByBoW(KeyFrame* a, KeyFrame* b, vpMatches12) (:1289-1424):
+ *   out has a.n entries, out[i] = b's map point matched to a feature i; b
+ *   features need a map point, best < TH_LOW.
+ * Both: best < nnratio * second, rotation consistency (ComputeThreeMaxima
+ * :2338-2379) when check_ori. nmatches = the returned count. */
+int gf_match_bow(gf_ctx* ctx, int mode, float nnratio, int check_ori, const gf_bow_side* a, const gf_bow_side* b,
+                 int32_t* out, int* nmatches);
+/* Device family: npairs (a[p], b[p]) pairs whose pointers are device
+ * pointers; outs[p] device output of pair p, d_nmatches[p]. The host arrays a,
+ * b, outs are copied at the call. At most 4096 features per side. */
+int gf_match_bow_dev(gf_ctx* ctx, int mode, float nnratio, int check_ori, int npairs, const gf_bow_side* a,
+                     const gf_bow_side* b, int32_t* const* outs, int32_t* d_nmatches, void* stream);
+
 /* ------------------------------------------------ local bundle adjustment (B1)
  * Optimizer::LocalBundleAdjustment(KeyFrame*, bool*) (src/Optimizer.cc:1515-1764)
  * on g2o's Levenberg-Marquardt with the Schur complement over the map points

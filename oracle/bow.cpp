@@ -1,0 +1,247 @@
+// CPU ORACLE (test infrastructure) — rows D1 and M6 of SURVEY.md §8a:
+//   DBoW2 TemplatedVocabulary::transform(features, BowVector, FeatureVector,
+//     levelsup) and its per-descriptor descent
+//     (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1141-1208, 1232-1273),
+//   BowVector::addWeight / addIfNotExist / normalize (BowVector.cpp:34-84),
+//   FeatureVector::addFeature (FeatureVector.cpp:31-45),
+//   FORB::distance (FORB.cpp:81-101), the scoring objects' mustNormalize
+//     (ScoringObject.h:74-89);
+//   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (src/ORBmatcher.cc:724-853)
+//   and SearchByBoW(KeyFrame*, KeyFrame*, ...) (:1289-1424) with
+//   ComputeThreeMaxima (:2338-2379).
+// The vocabulary tree arrives as the loaders build it (node 0 = root, nodes
+// in record order, children in record order, word ids in record order of the
+// leaves). DBoW2 is vendored, so these rows restate vendored text; parity is
+// pinned against this restatement (no DBoW2 test or fixture exists upstream).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "oracle_common.h"
+
+namespace orc {
+namespace {
+
+int hamming(const uint8_t* a, const uint8_t* b) {  // FORB::distance: 8 x int32 SWAR popcount
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        uint32_t v = x ^ y;
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        d += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return d;
+}
+
+struct Vocab {
+    int k, L, scoring, weighting;
+    std::vector<std::vector<int>> children;
+    const uint8_t* desc;
+    const double* weight;
+    std::vector<int> word;
+    Vocab(int k_, int L_, int sc, int wt, int nnodes, const int32_t* parent, const uint8_t* d, const double* w,
+          const uint8_t* leaf)
+        : k(k_), L(L_), scoring(sc), weighting(wt), children(nnodes), desc(d), weight(w), word(nnodes, 0) {
+        int nw = 0;
+        for (int i = 1; i < nnodes; i++) {
+            children[parent[i]].push_back(i);
+            if (leaf[i]) word[i] = nw++;
+        }
+    }
+    // transform(feature, word_id, weight, &nid, levelsup)
+    void descend(const uint8_t* f, int levelsup, int& wid, double& w, int& nid) const {
+        const int nid_level = L - levelsup;
+        if (nid_level <= 0) nid = 0;
+        int final_id = 0, level = 0;
+        do {
+            ++level;
+            const std::vector<int>& nodes = children[final_id];
+            final_id = nodes[0];
+            int best = hamming(f, desc + 32 * (size_t)final_id);
+            for (size_t c = 1; c < nodes.size(); c++) {
+                const int d = hamming(f, desc + 32 * (size_t)nodes[c]);
+                if (d < best) {
+                    best = d;
+                    final_id = nodes[c];
+                }
+            }
+            if (level == nid_level) nid = final_id;
+        } while (!children[final_id].empty());
+        wid = word[final_id];
+        w = weight[final_id];
+    }
+};
+
+}  // namespace
+}  // namespace orc
+
+extern "C" {
+
+// TemplatedVocabulary::transform(features, v, fv, levelsup) for one frame.
+// Outputs the BowVector (word ids ascending, values) and the FeatureVector
+// (node ids ascending, CSR offsets, feature indices).
+int orc_bow_transform(int k, int L, int scoring, int weighting, int nnodes, const int32_t* parent,
+                      const uint8_t* desc, const double* weight, const uint8_t* is_leaf, const uint8_t* feats, int n,
+                      int levelsup, int32_t* words, double* values, int* nwords, int32_t* fv_nodes, int32_t* fv_start,
+                      int32_t* fv_feats, int* nfv) {
+    orc::Vocab V(k, L, scoring, weighting, nnodes, parent, desc, weight, is_leaf);
+    std::map<int, double> v;
+    std::map<int, std::vector<int>> fv;
+    const bool must = scoring != 5;  // DOT_PRODUCT does not normalise; the others: L2 for L2_NORM, else L1
+    if (nnodes > 1) {
+        for (int i = 0; i < n; i++) {
+            int wid, nid = 0;
+            double w;
+            V.descend(feats + 32 * (size_t)i, levelsup, wid, w, nid);
+            if (!(w > 0)) continue;  // stopped word
+            if (weighting == 0 || weighting == 1) {  // TF_IDF, TF: addWeight
+                auto it = v.lower_bound(wid);
+                if (it != v.end() && it->first == wid)
+                    it->second += w;
+                else
+                    v.insert(it, {wid, w});
+            } else {  // IDF, BINARY: addIfNotExist
+                if (!v.count(wid)) v[wid] = w;
+            }
+            fv[nid].push_back(i);
+        }
+        if ((weighting == 0 || weighting == 1) && !v.empty() && !must) {
+            const double nd = (double)v.size();
+            for (auto& e : v) e.second /= nd;
+        }
+        if (must) {
+            double norm = 0.0;
+            if (scoring == 1) {
+                for (auto& e : v) norm += e.second * e.second;
+                norm = std::sqrt(norm);
+            } else {
+                for (auto& e : v) norm += std::fabs(e.second);
+            }
+            if (norm > 0.0)
+                for (auto& e : v) e.second /= norm;
+        }
+    }
+    int c = 0;
+    for (auto& e : v) {
+        words[c] = e.first;
+        values[c++] = e.second;
+    }
+    *nwords = c;
+    c = 0;
+    int off = 0;
+    for (auto& e : fv) {
+        fv_nodes[c] = e.first;
+        fv_start[c++] = off;
+        for (int f : e.second) fv_feats[off++] = f;
+    }
+    fv_start[c] = off;
+    *nfv = c;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchByBoW. mode 0: (KeyFrame a, Frame b) — a feature i with
+// a_mp[i] >= 0 matches an unclaimed b feature, best <= TH_LOW(50) and best <
+// nnratio * second; out[b index] = a_mp[i] (vpMapPointMatches). mode 1:
+// (KeyFrame a, KeyFrame b) — b features need b_mp >= 0 and !vbMatched2, best <
+// TH_LOW; out[a index] = b_mp[j] (vpMatches12). Rotation consistency when
+// check_ori. Features of one FeatureVector node are walked in list order.
+int orc_match_bow(int mode, float nnratio, int check_ori, const int32_t* a_nodes, const int32_t* a_start,
+                  const int32_t* a_feats, int a_nn, const uint8_t* a_desc, const float* a_angle, const int32_t* a_mp,
+                  int a_n, const int32_t* b_nodes, const int32_t* b_start, const int32_t* b_feats, int b_nn,
+                  const uint8_t* b_desc, const float* b_angle, const int32_t* b_mp, int b_n, int32_t* out,
+                  int* nmatches) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    const int nout = mode == 0 ? b_n : a_n;
+    for (int i = 0; i < nout; i++) out[i] = -1;
+    std::vector<char> matched_b(b_n, 0);
+    std::vector<int> rotHist[30];
+    const float factor = 1.0f / HISTO_LENGTH;
+    int nm = 0, ia = 0, ib = 0;
+    while (ia < a_nn && ib < b_nn) {
+        if (a_nodes[ia] == b_nodes[ib]) {
+            for (int x = a_start[ia]; x < a_start[ia + 1]; x++) {
+                const int idxA = a_feats[x];
+                if (a_mp[idxA] < 0) continue;
+                int best1 = INT32_MAX, best2 = INT32_MAX, bestB = -1;
+                for (int y = b_start[ib]; y < b_start[ib + 1]; y++) {
+                    const int idxB = b_feats[y];
+                    if (mode == 0 ? out[idxB] >= 0 : (matched_b[idxB] || b_mp[idxB] < 0)) continue;
+                    const int dist = orc::hamming(a_desc + 32 * (size_t)idxA, b_desc + 32 * (size_t)idxB);
+                    if (dist < best1) {
+                        best2 = best1;
+                        best1 = dist;
+                        bestB = idxB;
+                    } else if (dist < best2) {
+                        best2 = dist;
+                    }
+                }
+                const bool ok = mode == 0 ? best1 <= TH_LOW : best1 < TH_LOW;
+                if (!ok || !(static_cast<float>(best1) < nnratio * static_cast<float>(best2))) continue;
+                if (mode == 0) {
+                    out[bestB] = a_mp[idxA];
+                } else {
+                    out[idxA] = b_mp[bestB];
+                    matched_b[bestB] = 1;
+                }
+                if (check_ori) {
+                    float rot = a_angle[idxA] - b_angle[bestB];
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)std::round(rot * factor);
+                    if (bin == HISTO_LENGTH) bin = 0;
+                    rotHist[bin].push_back(mode == 0 ? bestB : idxA);
+                }
+                nm++;
+            }
+            ia++;
+            ib++;
+        } else if (a_nodes[ia] < b_nodes[ib]) {
+            ia = (int)(std::lower_bound(a_nodes + ia, a_nodes + a_nn, b_nodes[ib]) - a_nodes);
+        } else {
+            ib = (int)(std::lower_bound(b_nodes + ib, b_nodes + b_nn, a_nodes[ia]) - b_nodes);
+        }
+    }
+    if (check_ori) {  // ComputeThreeMaxima
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = (int)rotHist[i].size();
+            if (s > max1) {
+                max3 = max2;
+                max2 = max1;
+                max1 = s;
+                ind3 = ind2;
+                ind2 = ind1;
+                ind1 = i;
+            } else if (s > max2) {
+                max3 = max2;
+                max2 = s;
+                ind3 = ind2;
+                ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (int j : rotHist[i]) {
+                out[j] = -1;
+                nm--;
+            }
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+}  // extern "C"

@@ -211,3 +211,36 @@ def inverse3(m):
     r = np.zeros(9)
     orc().orc_inverse3(_p(m), _p(r))
     return r.reshape(3, 3)
+
+
+def bow_transform(voc: dict, desc: np.ndarray, levelsup: int = 4):
+    """TemplatedVocabulary::transform on the CPU oracle -> (words, values, (nodes, start, feats))."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(d)
+    words, values = np.zeros(max(n, 1), np.int32), np.zeros(max(n, 1))
+    nodes, start, feats = np.zeros(max(n, 1), np.int32), np.zeros(n + 1, np.int32), np.zeros(max(n, 1), np.int32)
+    nw, nf = ctypes.c_int(), ctypes.c_int()
+    t = {k: np.ascontiguousarray(voc[k], dt) for k, dt in (("parent", np.int32), ("desc", np.uint8),
+                                                           ("weight", np.float64), ("is_leaf", np.uint8))}
+    orc().orc_bow_transform(voc["k"], voc["L"], voc["scoring"], voc["weighting"], len(t["parent"]), _p(t["parent"]),
+                            _p(t["desc"]), _p(t["weight"]), _p(t["is_leaf"]), _p(d), n, levelsup, _p(words),
+                            _p(values), ctypes.byref(nw), _p(nodes), _p(start), _p(feats), ctypes.byref(nf))
+    k = nf.value
+    return words[:nw.value].copy(), values[:nw.value].copy(), (nodes[:k].copy(), start[:k + 1].copy(),
+                                                                feats[:start[k]].copy())
+
+
+def match_bow(mode, nnratio, check_ori, a, b):
+    """ORBmatcher::SearchByBoW on the CPU oracle; a, b = ((nodes, start, feats), desc, kps, mp)."""
+    def side(s):
+        (nodes, start, feats), desc, kps, mp = s
+        return [np.ascontiguousarray(nodes, np.int32), np.ascontiguousarray(start, np.int32),
+                np.ascontiguousarray(feats, np.int32), np.ascontiguousarray(desc, np.uint8),
+                np.ascontiguousarray(kps["angle"], np.float32), np.ascontiguousarray(mp, np.int32)]
+    A, B = side(a), side(b)
+    out = np.zeros(max(len(B[3]) if mode == 0 else len(A[3]), 1), np.int32)
+    nm = ctypes.c_int()
+    orc().orc_match_bow(mode, ctypes.c_float(nnratio), int(check_ori), _p(A[0]), _p(A[1]), _p(A[2]), len(A[0]),
+                        _p(A[3]), _p(A[4]), _p(A[5]), len(A[3]), _p(B[0]), _p(B[1]), _p(B[2]), len(B[0]), _p(B[3]),
+                        _p(B[4]), _p(B[5]), len(B[3]), _p(out), ctypes.byref(nm))
+    return nm.value, out[:(len(B[3]) if mode == 0 else len(A[3]))].copy()
