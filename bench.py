@@ -37,8 +37,7 @@ def kernel_bytes(camera: str, nfeat: int) -> dict:
     P, P0, P7 = sum(px), px[0], px[-1]
     return {
         "k_resize": (P - P7) + (P - P0),  # read level l-1, write level l
-        "k_blur": 2 * P,                  # read + write every level
-        "k_fast": P,                      # FAST reads every pyramid pixel once
+        "k_blur_fast": 3 * P,             # blur read + write every level, FAST reads every pixel once
         "k_describe": 60 * nfeat,         # 32 B descriptor + 28 B keypoint out
         "extract_total": (P - P7) + (P - P0) + P + 2 * P + 60 * nfeat,
     }
@@ -262,7 +261,7 @@ def main():
 
     # algorithmic bytes per launch for the kernels with a §8(d) formula
     kb = kernel_bytes(cam, args.nfeatures)
-    per_launch_bytes = {k: kb[k] * B for k in ("k_resize", "k_blur", "k_fast", "k_describe")}
+    per_launch_bytes = {k: kb[k] * B for k in ("k_resize", "k_blur_fast", "k_describe")}
     # pose LM: N_e * 40 B per LM iteration per problem, summed over the launch
     per_launch_bytes["k_pose_opt"] = float((nedges * iters).sum(axis=1).mean() * 40.0)
     per_kernel = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "ms_per_step": v[0] / args.steps}
@@ -278,7 +277,7 @@ def main():
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
                 "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)}
-    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur", "k_fast", "k_select", "k_describe") if k in prof)
+    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe") if k in prof)
     ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
     pose_ms = prof.get("k_pose_opt", (0.0, 1))
     pose_avg_ms = pose_ms[0] / max(pose_ms[1], 1)

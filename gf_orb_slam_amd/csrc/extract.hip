@@ -6,10 +6,13 @@
 //
 //   k_resize  x (nlevels-1)  level l from level l-1 (cv::resize INTER_LINEAR,
 //                            11-bit fixed point; ComputePyramid :922-998)
-//   k_blur                   7x7 sigma-2 Gaussian of every level (:842)
-//   k_fast                   one workgroup per (frame, grid cell): FAST-9 +
-//                            score + in-cell NMS, threshold fallback 20 -> 7,
-//                            row-major compaction (ComputeKeyPoints :575-689)
+//   k_blur_fast              one 64x16 tile per workgroup: 7x7 sigma-2
+//                            Gaussian of every level (:842) and, from the same
+//                            LDS tile, the FAST-9 score map of the level
+//   k_fast_cells             one workgroup per (frame, grid cell): corners of
+//                            the cell window from the score map, in-cell NMS,
+//                            threshold fallback 20 -> 7, row-major compaction
+//                            (ComputeKeyPoints :575-689)
 //   k_select                 one workgroup per (frame, level): quota
 //                            redistribution (:695-721) + retainBest per cell
 //                            and per level (:734-752)
@@ -112,49 +115,6 @@ __global__ void k_resize(Planes P, LevelGeom g, int l, const int2* __restrict__ 
     D[(long long)dy * dw + dx] = (uint8_t)min(max(v, 0), 255);
 }
 
-// -------------------------------------------------------------- k_blur
-// 64x16 output tile per 256-thread workgroup; reflect-101 halo of 3 px staged
-// in LDS; integer row pass then column pass with the (s + 2^15) >> 16 cast.
-#define BT_W 64
-#define BT_H 16
-__global__ __launch_bounds__(256) void k_blur(Planes P, LevelGeom g) {
-    __shared__ uint8_t src[BT_H + 6][BT_W + 6 + 2];
-    __shared__ int rows[BT_H + 6][BT_W];
-    const int f = blockIdx.y;
-    int t = blockIdx.x, l = 0;
-    while (l + 1 < g.nlevels && t >= g.tile_begin[l + 1]) l++;
-    t -= g.tile_begin[l];
-    const int tx = t % g.tiles_x[l], ty = t / g.tiles_x[l];
-    const int w = g.w[l], h = g.h[l];
-    const int X0 = tx * BT_W, Y0 = ty * BT_H;
-    int stride;
-    const uint8_t* S = level_plane(P, g, f, l, stride);
-    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l];
-    for (int i = threadIdx.x; i < (BT_H + 6) * (BT_W + 6); i += 256) {
-        int ry = i / (BT_W + 6), rx = i % (BT_W + 6);
-        int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-        int xx = gfd::reflect101(min(X0 + rx - 3, w + 2), w);
-        src[ry][rx] = S[(long long)yy * stride + xx];
-    }
-    __syncthreads();
-    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;  // round(256 * gaussian(7, sigma 2))
-    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
-        int ry = i / BT_W, rx = i % BT_W;
-        const uint8_t* p = &src[ry][rx];
-        rows[ry][rx] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < BT_H * BT_W; i += 256) {
-        int ry = i / BT_W, rx = i % BT_W;
-        int y = Y0 + ry, x = X0 + rx;
-        if (y >= h || x >= w) continue;
-        int s = k0 * (rows[ry][rx] + rows[ry + 6][rx]) + k1 * (rows[ry + 1][rx] + rows[ry + 5][rx]) +
-                k2 * (rows[ry + 2][rx] + rows[ry + 4][rx]) + k3 * rows[ry + 3][rx];
-        int v = (s + (1 << 15)) >> 16;
-        D[(long long)y * w + x] = (uint8_t)min(max(v, 0), 255);
-    }
-}
-
 // -------------------------------------------------------------- FAST-9
 __device__ __forceinline__ void circle_vals(const uint8_t* roi, int rw, int px, int py, int c[16]) {
     const uint8_t* p = roi + py * rw + px;
@@ -244,93 +204,225 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
     return base + x - v;
 }
 
-// One workgroup per (grid cell, frame). LDS holds the cell ROI (w x h u8, the
-// 3-px FAST margin included) and the per-pixel score map of the detection
-// window ((w-6) x (h-6), u16: 0x100 flags a corner).
-__global__ __launch_bounds__(256) void k_fast(Planes P, LevelGeom g, const CellInfo* __restrict__ cells,
-                                              uint32_t* __restrict__ lists, long long list_stride,
-                                              int* __restrict__ counts, int fast_th, int min_th) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ int scan_tmp[4];
-    const int f = blockIdx.y, cid = blockIdx.x;
-    const CellInfo ci = cells[cid];
-    if (!ci.valid) {
-        if (threadIdx.x == 0) counts[(long long)f * g.ncells + cid] = 0;
-        return;
-    }
-    const int rw = ci.w, rh = ci.h, dw = rw - 6, dh = rh - 6;
-    const int n = (dw > 0 && dh > 0) ? dw * dh : 0;  // degenerate ROI: FAST finds nothing
-    uint8_t* roi = smem;
-    uint16_t* sc = (uint16_t*)(smem + ((rw * rh + 15) & ~15));
+// -------------------------------------------------------------- k_blur_fast
+// One 64x16 tile of one level per 256-thread workgroup, its 3-px halo staged
+// in LDS once and used twice:
+//   * GaussianBlur 7x7 sigma 2 (reflect-101 border; ORBextractor.cc:842):
+//     integer row pass, column pass with the (s + 2^15) >> 16 cast;
+//   * the FAST-9 score map of the unblurred level at the lower of the two
+//     thresholds (:621, :626): S + 1 (S = cornerScore<16> <= 254) for a
+//     pixel that passes the segment test, else 0 (and 0 within 3 px of the
+//     level border).
+//     cornerScore does not depend on the threshold once the test passes, and
+//     a pixel is a corner at th >= the map's threshold iff S >= th, so the
+//     cells run both the fast_th pass and the min_th retry, NMS included,
+//     from this one map (k_fast_cells). Every pixel gets the 4-point
+//     compass test only; the few that pass are compacted into an LDS list and
+//     the full segment test + cornerScore runs on that list, so whole waves do
+//     it (a divergent ~250-op branch per lane otherwise).
+// Thread t owns column t & 63 and rows 4 (t >> 6) .. +3 of the tile.
+#define BT_W 64
+#define BT_H 16
+#define BT_SW (BT_W + 8)  // LDS row of the source tile (70 used)
+
+// Necessary condition for a 9-arc: it covers two neighbouring compass points
+// of the ring (positions 0, 4, 8, 12), both darker or both brighter.
+__device__ __forceinline__ bool fast_compass(const uint8_t* p, int rw, int th) {
+    const int v = p[0], c0 = p[3 * rw], c4 = p[3], c8 = p[-3 * rw], c12 = p[-3];
+    const unsigned dark = (unsigned)(c0 < v - th) | (unsigned)(c4 < v - th) << 1 | (unsigned)(c8 < v - th) << 2 |
+                          (unsigned)(c12 < v - th) << 3;
+    const unsigned bright = (unsigned)(c0 > v + th) | (unsigned)(c4 > v + th) << 1 |
+                            (unsigned)(c8 > v + th) << 2 | (unsigned)(c12 > v + th) << 3;
+    const unsigned d2 = dark & (dark >> 1 | dark << 3), b2 = bright & (bright >> 1 | bright << 3);
+    return ((d2 | b2) & 0xf) != 0;
+}
+
+__global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
+    __shared__ uint8_t src[BT_H + 6][BT_SW];
+    __shared__ int rows[BT_H + 6][BT_W];
+    __shared__ uint16_t cand[BT_W * BT_H];
+    __shared__ int s_nc;
+    const int f = blockIdx.y;
+    int t = blockIdx.x, l = 0;
+    while (l + 1 < g.nlevels && t >= g.tile_begin[l + 1]) l++;
+    t -= g.tile_begin[l];
+    const int tx = t % g.tiles_x[l], ty = t / g.tiles_x[l];
+    const int w = g.w[l], h = g.h[l];
+    const int X0 = tx * BT_W, Y0 = ty * BT_H;
     int stride;
-    const uint8_t* S = level_plane(P, g, f, ci.level, stride);
-    for (int i = threadIdx.x; i < rw * rh; i += 256) {
-        int ry = i / rw, rx = i - ry * rw;
-        roi[i] = S[(long long)(ci.y0 + ry) * stride + ci.x0 + rx];
+    const uint8_t* S = level_plane(P, g, f, l, stride);
+    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l];
+    uint8_t* SC = score + (long long)f * g.bslab + g.boff[l];
+    const bool interior = X0 >= 3 && Y0 >= 3 && X0 + BT_W + 3 <= w && Y0 + BT_H + 3 <= h;
+    if (threadIdx.x == 0) s_nc = 0;
+    // all of a thread's loads issue before the first LDS write: one memory
+    // latency per tile instead of one per loop trip
+    constexpr int NSRC = (BT_H + 6) * (BT_W + 6), NLD = (NSRC + 255) / 256;
+    uint8_t v[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < NSRC) {
+            const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
+            int yy = Y0 + ry - 3, xx = X0 + rx - 3;
+            if (!interior) {
+                yy = gfd::reflect101(min(yy, h + 2), h);
+                xx = gfd::reflect101(min(xx, w + 2), w);
+            }
+            v[k] = S[(long long)yy * stride + xx];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NLD; k++) {
+        const int i = threadIdx.x + 256 * k;
+        if (i < NSRC) {
+            const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
+            src[ry][rx] = v[k];
+        }
     }
     __syncthreads();
-    uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
-    const int chunk = (n + 255) / 256;
-    const int p0 = min(threadIdx.x * chunk, n), p1 = min(p0 + chunk, n);
-    for (int pass = 0; pass < 2; pass++) {
-        const int th = pass == 0 ? fast_th : min_th;
-        for (int p = threadIdx.x; p < n; p += 256) {
-            int py = p / dw + 3, px = p - (p / dw) * dw + 3;
-            int c[16];
-            circle_vals(roi, rw, px, py, c);
-            sc[p] = (uint16_t)fast_score(roi[py * rw + px], c, th);
-        }
-        __syncthreads();
-        int cnt = 0;
-        for (int p = p0; p < p1; p++) {
-            int s = sc[p];
-            if (!(s & 0x100)) continue;
-            int y = p / dw, x = p - y * dw, sv = s & 0xff;
-            bool keep = true;
-            for (int dy = -1; dy <= 1 && keep; dy++) {
-                int yy = y + dy;
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (!dx && !dy) continue;
-                    int xx = x + dx;
-                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? (sc[yy * dw + xx] & 0xff) : 0;
-                    if (!(sv > nb)) {
-                        keep = false;
-                        break;
-                    }
-                }
-            }
-            cnt += keep;
-        }
-        int total;
-        int off = block_scan_256(cnt, scan_tmp, total);
-        if (pass == 0 && total <= 3) {
-            __syncthreads();
-            continue;  // ORBextractor.cc:623-628: retry the cell with the minimum threshold
-        }
-        for (int p = p0; p < p1 && cnt > 0; p++) {
-            int s = sc[p];
-            if (!(s & 0x100)) continue;
-            int y = p / dw, x = p - y * dw, sv = s & 0xff;
-            bool keep = true;
-            for (int dy = -1; dy <= 1 && keep; dy++) {
-                int yy = y + dy;
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (!dx && !dy) continue;
-                    int xx = x + dx;
-                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? (sc[yy * dw + xx] & 0xff) : 0;
-                    if (!(sv > nb)) {
-                        keep = false;
-                        break;
-                    }
-                }
-            }
-            if (keep) {
-                out[off++] = ((uint32_t)sv << 24) | ((uint32_t)(ci.y0 + y + 3) << 12) | (uint32_t)(ci.x0 + x + 3);
-            }
-        }
-        if (threadIdx.x == 0) counts[(long long)f * g.ncells + cid] = total;
-        break;
+    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;  // round(256 * gaussian(7, sigma 2))
+    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
+        const int ry = i >> 6, rx = i & 63;
+        const uint8_t* q = &src[ry][rx];
+        rows[ry][rx] = k0 * (q[0] + q[6]) + k1 * (q[1] + q[5]) + k2 * (q[2] + q[4]) + k3 * q[3];
     }
+    __syncthreads();
+    const int cx = threadIdx.x & 63, ry0 = (threadIdx.x >> 6) * 4, x = X0 + cx;
+    int rv[10];
+#pragma unroll
+    for (int k = 0; k < 10; k++) rv[k] = rows[ry0 + k][cx];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int y = Y0 + ry0 + r;
+        if (y >= h || x >= w) continue;
+        const int sum = k0 * (rv[r] + rv[r + 6]) + k1 * (rv[r + 1] + rv[r + 5]) + k2 * (rv[r + 2] + rv[r + 4]) +
+                        k3 * rv[r + 3];
+        D[(long long)y * w + x] = (uint8_t)min(max((sum + (1 << 15)) >> 16, 0), 255);
+        const bool cand_px = x >= 3 && x < w - 3 && y >= 3 && y < h - 3 &&
+                             fast_compass(&src[ry0 + r + 3][cx + 3], BT_SW, map_th);
+        if (cand_px)
+            cand[atomicAdd(&s_nc, 1)] = (uint16_t)((ry0 + r) * BT_W + cx);
+        else
+            SC[(long long)y * w + x] = 0;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < s_nc; i += 256) {
+        const int q = cand[i], py = q >> 6, px = q & 63;
+        int c[16];
+        circle_vals(&src[0][0], BT_SW, px + 3, py + 3, c);
+        const int fs = fast_score(src[py + 3][px + 3], c, map_th);
+        SC[(long long)(Y0 + py) * w + X0 + px] = (fs & 0x100) ? (uint8_t)((fs & 0xff) + 1) : 0;
+    }
+}
+
+// -------------------------------------------------------------- k_fast_cells
+// One wave per (grid cell, frame), four cells per workgroup, no block
+// barriers: the cell's detection window (the ROI minus its 3-px FAST margin,
+// :621) of the score map in the wave's LDS slice; corners at fast_th with
+// strict 3x3 non-maximum suppression inside the window (neighbours outside it
+// or not corners count 0, as in FAST's row buffer), 64 pixels a step,
+// compacted in row-major order with a ballot. When at most 3 survive
+// (:623-628) the list is rewritten from the same map at min_th.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// rows x cols bytes (row pitch `pitch`) into LDS (row pitch cols), 16 loads per
+// lane in flight before the LDS writes.
+__device__ __forceinline__ void wave_load_window(const uint8_t* __restrict__ G, long long pitch, int rows, int cols,
+                                                 uint8_t* L, int lane) {
+    const int n = rows * cols;
+    int y = lane / cols, x = lane - y * cols;
+    for (int p0 = 0; p0 < n; p0 += 64 * 16) {
+        uint8_t v[16];
+        int yy = y, xx = x;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (p0 + 64 * k + lane < n) v[k] = G[(long long)yy * pitch + xx];
+            xx += 64;
+            while (xx >= cols) {
+                xx -= cols;
+                yy++;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (p0 + 64 * k + lane < n) L[y * cols + x] = v[k];
+            x += 64;
+            while (x >= cols) {
+                x -= cols;
+                y++;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int cell_nms(const uint8_t* sc, int dw, int dh, int th, int lane, uint32_t* out, int x0,
+                                        int y0) {
+    const int n = dw * dh;
+    int y = lane / dw, x = lane - y * dw, base = 0;
+    for (int p0 = 0; p0 < n; p0 += 64) {
+        bool keep = false;
+        int sv = 0;
+        if (p0 + lane < n) {
+            // map entries are S + 1 for corners at the map threshold, 0 otherwise;
+            // a corner at th has S >= th, non-corners count 0 (FAST's buffers)
+            const int m = sc[y * dw + x];
+            sv = m - 1;
+            keep = m != 0 && sv >= th;
+#pragma unroll
+            for (int dy = -1; dy <= 1; dy++) {
+#pragma unroll
+                for (int dx = -1; dx <= 1; dx++) {
+                    if (!dx && !dy) continue;
+                    const int yy = y + dy, xx = x + dx;
+                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? sc[yy * dw + xx] - 1 : -1;
+                    if (nb < th) nb = 0;
+                    keep = keep && sv > nb;
+                }
+            }
+        }
+        const unsigned long long m = __ballot(keep);
+        if (keep)
+            out[base + __popcll(m & ((1ull << lane) - 1))] =
+                ((uint32_t)sv << 24) | ((uint32_t)(y0 + y) << 12) | (uint32_t)(x0 + x);
+        base += __popcll(m);
+        x += 64;
+        while (x >= dw) {
+            x -= dw;
+            y++;
+        }
+    }
+    return base;
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* __restrict__ score,
+                                                    const CellInfo* __restrict__ cells, uint32_t* __restrict__ lists,
+                                                    long long list_stride, int* __restrict__ counts, int fast_th,
+                                                    int min_th, int wave_lds) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int lane = threadIdx.x & 63, f = blockIdx.y;
+    const int cid = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (cid >= g.ncells) return;  // whole wave; nothing below waits on other waves
+    const CellInfo ci = cells[cid];
+    const int rw = ci.w, rh = ci.h, dw = rw - 6, dh = rh - 6;
+    if (!ci.valid || dw <= 0 || dh <= 0) {  // degenerate ROI: FAST finds nothing
+        if (lane == 0) counts[(long long)f * g.ncells + cid] = 0;
+        return;
+    }
+    uint8_t* sc = smem + (threadIdx.x >> 6) * wave_lds;  // dw x dh scores
+    const int l = ci.level, lw = g.w[l];
+    const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
+    wave_load_window(SC, lw, dh, dw, sc, lane);
+    wave_sync_lds();
+    uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
+    int total = cell_nms(sc, dw, dh, fast_th, lane, out, ci.x0 + 3, ci.y0 + 3);
+    if (total <= 3)  // ORBextractor.cc:623-628: retry with the minimum threshold
+        total = cell_nms(sc, dw, dh, min_th, lane, out, ci.x0 + 3, ci.y0 + 3);
+    if (lane == 0) counts[(long long)f * g.ncells + cid] = total;
 }
 
 // -------------------------------------------------------------- k_select
@@ -463,46 +555,57 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     const uint8_t* Pl = level_plane(P, g, f, l, stride);
     const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[l];
 
-    // IC_Angle: lane r < 31 owns row v = r - 15 of the circular patch.
+    // IC_Angle: the 31x31 square around the keypoint, 16 pixels per lane with
+    // every load in flight at once; pixels outside the circular patch
+    // (|u| > umax[|v|]) weigh 0. Integer moments, so the order is free.
     int m10 = 0, m01 = 0;
-    if (lane < 31) {
-        int v = lane - 15, d = c_umax[v < 0 ? -v : v], s = 0;
-        const uint8_t* row = Pl + (long long)(y + v) * stride + x;
-        for (int u = -d; u <= d; u++) {
-            int p = row[u];
-            s += p;
-            m10 += u * p;
+    {
+        int pv[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int j = lane + 64 * k;
+            const int v = j / 31 - 15, u = j - (j / 31) * 31 - 15;
+            const bool in = j < 961 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v];
+            pv[k] = in ? Pl[(long long)(y + v) * stride + x + u] : 0;
         }
-        m01 = v * s;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int j = lane + 64 * k;
+            const int v = j / 31 - 15, u = j - (j / 31) * 31 - 15;
+            m10 += u * pv[k];
+            m01 += v * pv[k];
+        }
     }
     m10 = gfd::warp_sum(m10);
     m01 = gfd::warp_sum(m01);
     const float angle = fast_atan2f((float)m01, (float)m10);
 
-    // rBRIEF: lane b < 32 computes descriptor byte b.
-    if (lane < 32) {
+    // rBRIEF: lane 2b + hi computes bits 4 hi .. 4 hi + 3 of descriptor byte b;
+    // addresses first (blurred interior or unblurred reflect-101 border), then
+    // the 8 loads together.
+    {
         const float factorPI = (float)(M_PI / 180.f);
         const float ang = angle * factorPI;
         const float a = (float)cos((double)ang), b = (float)sin((double)ang);
-        int val = 0;
+        const int byte = lane >> 1, hi = lane & 1;
+        int t[8];
 #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
-            int t[2];
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                int pi = lane * 16 + bit * 2 + q;
-                float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
-                int ry = __float2int_rn(px * b + py * a);
-                int rx = __float2int_rn(px * a - py * b);
-                int xx = x + rx, yy = y + ry;
-                if (xx >= 0 && xx < w && yy >= 0 && yy < h)
-                    t[q] = B[(long long)yy * w + xx];
-                else
-                    t[q] = Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
-            }
-            val |= (t[0] < t[1]) << bit;
+        for (int q = 0; q < 8; q++) {
+            const int pi = byte * 16 + hi * 8 + q;
+            const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
+            const int ry = __float2int_rn(px * b + py * a);
+            const int rx = __float2int_rn(px * a - py * b);
+            const int xx = x + rx, yy = y + ry;
+            const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
+            const uint8_t* src = inside ? B + (long long)yy * w + xx
+                                        : Pl + (long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w);
+            t[q] = *src;
         }
-        desc[((long long)f * cap + k) * 32 + lane] = (uint8_t)val;
+        int nib = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) nib |= (t[2 * q] < t[2 * q + 1]) << q;
+        const int other = __shfl_xor(nib, 1, 64);
+        if (!hi) desc[((long long)f * cap + k) * 32 + byte] = (uint8_t)(nib | other << 4);
     }
     if (lane == 0) {
         gf_keypoint kp;
@@ -533,7 +636,7 @@ struct gf_extractor {
     size_t fast_lds = 0;
     int max_tiles = 0;
     // device buffers
-    uint8_t *d_pyr = nullptr, *d_blur = nullptr;
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
     int2 *d_xtab = nullptr, *d_ytab = nullptr;
     std::vector<long long> xtab_off, ytab_off;
     CellInfo* d_cells = nullptr;
@@ -663,7 +766,7 @@ static int plan_extractor(gf_extractor* ex) {
                         ci.cap_off = cap_off;
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
-                        size_t lds = (((size_t)ci.w * ci.h + 15) & ~(size_t)15) + (size_t)dw * dh * 2;
+                        size_t lds = ((size_t)dw * dh + 15) & ~(size_t)15;
                         max_lds = std::max(max_lds, lds);
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
                                  GF_ERR_ARG, "cell ROI outside level");
@@ -679,8 +782,8 @@ static int plan_extractor(gf_extractor* ex) {
     g.ncells = (int)ex->cells.size();
     ex->list_stride = cap_off;
     ex->lvl_stride = lvl_off;
-    ex->fast_lds = max_lds;
-    GF_CHECK(max_lds <= 64 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
+    ex->fast_lds = max_lds;  // per wave; four cells per workgroup
+    GF_CHECK(4 * max_lds <= 160 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
     ex->capacity = 0;
     for (int l = 0; l < nl; l++) ex->capacity += ex->feat_per_level[l];
     return GF_OK;
@@ -713,6 +816,7 @@ static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt,
 static void free_extractor(gf_extractor* ex) {
     (void)hipFree(ex->d_pyr);
     (void)hipFree(ex->d_blur);
+    (void)hipFree(ex->d_score);
     (void)hipFree(ex->d_xtab);
     (void)hipFree(ex->d_ytab);
     (void)hipFree(ex->d_cells);
@@ -786,6 +890,7 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     if ((e = hipMalloc((void**)&(p), (bytes))) != hipSuccess) return cleanup(e);
     ALLOC(ex->d_pyr, std::max<long long>(g.slab, 256) * max_batch);
     ALLOC(ex->d_blur, g.bslab * max_batch);
+    ALLOC(ex->d_score, g.bslab * max_batch);
     ALLOC(ex->d_cells, sizeof(CellInfo) * ex->cells.size());
     ALLOC(ex->d_lists, sizeof(uint32_t) * ex->list_stride * max_batch);
     ALLOC(ex->d_lvl, sizeof(uint32_t) * ex->lvl_stride * max_batch);
@@ -814,8 +919,8 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
         GF_HIP(hipMemcpy(ex->d_ytab, yall.data(), sizeof(int2) * yall.size(), hipMemcpyHostToDevice));
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
-    GF_HIP(hipFuncSetAttribute((const void*)k_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)ex->fast_lds));
+    GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(4 * ex->fast_lds)));
     *out = ex;
     return GF_OK;
 }
@@ -864,13 +969,14 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
         }
     }
     {
-        GF_PROF(ctx, s, "k_blur");
-        k_blur<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g);
+        GF_PROF(ctx, s, "k_blur_fast");
+        k_blur_fast<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g, ex->d_score, std::min(ex->fast_th, ex->min_th));
     }
     {
-        GF_PROF(ctx, s, "k_fast");
-        k_fast<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(P, g, ex->d_cells, ex->d_lists, ex->list_stride,
-                                                                  ex->d_counts, ex->fast_th, ex->min_th);
+        GF_PROF(ctx, s, "k_fast_cells");
+        k_fast_cells<<<dim3((g.ncells + 3) / 4, nframes), 256, 4 * ex->fast_lds, s>>>(
+            g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th,
+            (int)ex->fast_lds);
     }
     {
         GF_PROF(ctx, s, "k_select");

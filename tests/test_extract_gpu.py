@@ -75,6 +75,17 @@ def test_low_texture_threshold_fallback():
     assert np.array_equal(dg, do)
 
 
+@pytest.mark.parametrize("fast_th", [0, 5, 7, 40])
+def test_fast_threshold_edges(fast_th):
+    """Thresholds at and below the minimum one (7): the score map is built at
+    min(fastTh, 7), where a threshold of 0 admits corners of score 0."""
+    img = _frame("euroc", 11)
+    kg, dg = ORBextractor(1000, 1.2, 8, 1, fast_th)(img)
+    ko, do = O.extract(img, nfeatures=1000, fast_th=fast_th)
+    assert kg.tobytes() == ko.tobytes(), _diff_report(kg, ko)
+    assert np.array_equal(dg, do)
+
+
 def test_flat_image_no_keypoints():
     img = np.full((480, 640), 77, np.uint8)
     kg, dg = ORBextractor(1000)(img)
