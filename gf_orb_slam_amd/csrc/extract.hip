@@ -317,112 +317,117 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 }
 
 // -------------------------------------------------------------- k_fast_cells
-// One wave per (grid cell, frame), four cells per workgroup, no block
-// barriers: the cell's detection window (the ROI minus its 3-px FAST margin,
-// :621) of the score map in the wave's LDS slice; corners at fast_th with
-// strict 3x3 non-maximum suppression inside the window (neighbours outside it
-// or not corners count 0, as in FAST's row buffer), 64 pixels a step,
-// compacted in row-major order with a ballot. When at most 3 survive
-// (:623-628) the list is rewritten from the same map at min_th.
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// One workgroup per (grid cell, frame). The cell's detection window (the ROI
+// minus its 3-px FAST margin, :621) of the score map goes to LDS; corners at
+// fast_th survive strict 3x3 non-maximum suppression inside the window
+// (neighbours outside it or not corners count 0, as in FAST's row buffers)
+// and are listed in row-major order. When at most 3 survive (:623-628) the
+// same map is suppressed again at min_th and the list rewritten.
+// NMS: wave w walks rows [w dh/4, (w+1) dh/4) of each 64-column strip, lane =
+// column, keeping the three rows it compares in registers (three LDS reads a
+// pixel); survivors set their bit in an LDS bit array (bit = row-major pixel
+// index). Listing: a workgroup scan over the popcounts of the bit words.
+__device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buffer value at th
+    const int S = m - 1;  // entries are S + 1 for corners at the map threshold, 0 otherwise
+    return S >= th ? S : 0;
 }
 
-// rows x cols bytes (row pitch `pitch`) into LDS (row pitch cols), 16 loads per
-// lane in flight before the LDS writes.
-__device__ __forceinline__ void wave_load_window(const uint8_t* __restrict__ G, long long pitch, int rows, int cols,
-                                                 uint8_t* L, int lane) {
-    const int n = rows * cols;
-    int y = lane / cols, x = lane - y * cols;
-    for (int p0 = 0; p0 < n; p0 += 64 * 16) {
-        uint8_t v[16];
-        int yy = y, xx = x;
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if (p0 + 64 * k + lane < n) v[k] = G[(long long)yy * pitch + xx];
-            xx += 64;
-            while (xx >= cols) {
-                xx -= cols;
-                yy++;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if (p0 + 64 * k + lane < n) L[y * cols + x] = v[k];
-            x += 64;
-            while (x >= cols) {
-                x -= cols;
-                y++;
-            }
+__device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, uint32_t* bits, int dw, int dh, int th) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ya = wv * dh / 4, yb = (wv + 1) * dh / 4;
+    int cnt = 0;
+    for (int x0 = 0; x0 < dw; x0 += 64) {
+        const int x = x0 + lane;
+        const bool col = x < dw;
+        auto rd = [&](int y, int xx) -> int {
+            return (col && y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * dw + xx], th) : 0;
+        };
+        int u0 = rd(ya - 1, x - 1), u1 = rd(ya - 1, x), u2 = rd(ya - 1, x + 1);
+        int c0 = rd(ya, x - 1), c1 = rd(ya, x), c2 = rd(ya, x + 1);
+        for (int y = ya; y < yb; y++) {
+            const int d0 = rd(y + 1, x - 1), d1 = rd(y + 1, x), d2 = rd(y + 1, x + 1);
+            const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
+            const bool keep = c1 != 0 && c1 > mx;
+            if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
+            cnt += __popcll(__ballot(keep));
+            u0 = c0, u1 = c1, u2 = c2;
+            c0 = d0, c1 = d1, c2 = d2;
         }
     }
-}
-
-__device__ __forceinline__ int cell_nms(const uint8_t* sc, int dw, int dh, int th, int lane, uint32_t* out, int x0,
-                                        int y0) {
-    const int n = dw * dh;
-    int y = lane / dw, x = lane - y * dw, base = 0;
-    for (int p0 = 0; p0 < n; p0 += 64) {
-        bool keep = false;
-        int sv = 0;
-        if (p0 + lane < n) {
-            // map entries are S + 1 for corners at the map threshold, 0 otherwise;
-            // a corner at th has S >= th, non-corners count 0 (FAST's buffers)
-            const int m = sc[y * dw + x];
-            sv = m - 1;
-            keep = m != 0 && sv >= th;
-#pragma unroll
-            for (int dy = -1; dy <= 1; dy++) {
-#pragma unroll
-                for (int dx = -1; dx <= 1; dx++) {
-                    if (!dx && !dy) continue;
-                    const int yy = y + dy, xx = x + dx;
-                    int nb = (yy >= 0 && yy < dh && xx >= 0 && xx < dw) ? sc[yy * dw + xx] - 1 : -1;
-                    if (nb < th) nb = 0;
-                    keep = keep && sv > nb;
-                }
-            }
-        }
-        const unsigned long long m = __ballot(keep);
-        if (keep)
-            out[base + __popcll(m & ((1ull << lane) - 1))] =
-                ((uint32_t)sv << 24) | ((uint32_t)(y0 + y) << 12) | (uint32_t)(x0 + x);
-        base += __popcll(m);
-        x += 64;
-        while (x >= dw) {
-            x -= dw;
-            y++;
-        }
-    }
-    return base;
+    return cnt;  // this wave's survivors
 }
 
 __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* __restrict__ score,
                                                     const CellInfo* __restrict__ cells, uint32_t* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
-                                                    int min_th, int wave_lds) {
+                                                    int min_th) {
     extern __shared__ __align__(16) uint8_t smem[];
-    const int lane = threadIdx.x & 63, f = blockIdx.y;
-    const int cid = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (cid >= g.ncells) return;  // whole wave; nothing below waits on other waves
+    __shared__ int s_cnt[2][4];
+    __shared__ int scan_tmp[4];
+    const int f = blockIdx.y, cid = blockIdx.x, tid = threadIdx.x;
     const CellInfo ci = cells[cid];
-    const int rw = ci.w, rh = ci.h, dw = rw - 6, dh = rh - 6;
+    const int dw = ci.w - 6, dh = ci.h - 6;
     if (!ci.valid || dw <= 0 || dh <= 0) {  // degenerate ROI: FAST finds nothing
-        if (lane == 0) counts[(long long)f * g.ncells + cid] = 0;
+        if (tid == 0) counts[(long long)f * g.ncells + cid] = 0;
         return;
     }
-    uint8_t* sc = smem + (threadIdx.x >> 6) * wave_lds;  // dw x dh scores
+    const int n = dw * dh, nwords = (n + 31) >> 5;
+    uint8_t* sc = smem;                                          // dw x dh map entries
+    uint32_t* bits = reinterpret_cast<uint32_t*>(smem + ((n + 15) & ~15));  // survivor bits
     const int l = ci.level, lw = g.w[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
-    wave_load_window(SC, lw, dh, dw, sc, lane);
-    wave_sync_lds();
+    // the window: every load of a 16-deep batch in flight before its LDS writes
+    {
+        int y = tid / dw, x = tid - y * dw;
+        for (int p0 = 0; p0 < n; p0 += 256 * 16) {
+            uint8_t v[16];
+            int yy = y, xx = x;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (p0 + 256 * k + tid < n) v[k] = SC[(long long)yy * lw + xx];
+                xx += 256;
+                while (xx >= dw) xx -= dw, yy++;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (p0 + 256 * k + tid < n) sc[y * dw + x] = v[k];
+                x += 256;
+                while (x >= dw) x -= dw, y++;
+            }
+        }
+    }
+    for (int i = tid; i < nwords; i += 256) bits[i] = 0;
+    __syncthreads();
+    int c = cell_nms_bits(sc, bits, dw, dh, fast_th);
+    if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
+    __syncthreads();
+    int total = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+    if (total <= 3) {  // ORBextractor.cc:623-628: retry with the minimum threshold
+        __syncthreads();
+        for (int i = tid; i < nwords; i += 256) bits[i] = 0;
+        __syncthreads();
+        c = cell_nms_bits(sc, bits, dw, dh, min_th);
+        if ((tid & 63) == 0) s_cnt[1][tid >> 6] = c;
+        __syncthreads();
+        total = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+    }
     uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
-    int total = cell_nms(sc, dw, dh, fast_th, lane, out, ci.x0 + 3, ci.y0 + 3);
-    if (total <= 3)  // ORBextractor.cc:623-628: retry with the minimum threshold
-        total = cell_nms(sc, dw, dh, min_th, lane, out, ci.x0 + 3, ci.y0 + 3);
-    if (lane == 0) counts[(long long)f * g.ncells + cid] = total;
+    const int X0 = ci.x0 + 3, Y0 = ci.y0 + 3;
+    int base = 0;
+    for (int w0 = 0; w0 < nwords; w0 += 256) {
+        const int i = w0 + tid;
+        uint32_t word = i < nwords ? bits[i] : 0u;
+        int tot;
+        int off = base + block_scan_256(__popc(word), scan_tmp, tot);
+        while (word) {
+            const int p = 32 * i + __ffs(word) - 1;
+            word &= word - 1;
+            const int y = p / dw, x = p - y * dw;
+            out[off++] = ((uint32_t)(sc[p] - 1) << 24) | ((uint32_t)(Y0 + y) << 12) | (uint32_t)(X0 + x);
+        }
+        base += tot;
+    }
+    if (tid == 0) counts[(long long)f * g.ncells + cid] = total;
 }
 
 // -------------------------------------------------------------- k_select
@@ -766,7 +771,7 @@ static int plan_extractor(gf_extractor* ex) {
                         ci.cap_off = cap_off;
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
-                        size_t lds = ((size_t)dw * dh + 15) & ~(size_t)15;
+                        size_t lds = (((size_t)dw * dh + 15) & ~(size_t)15) + 4 * (((size_t)dw * dh + 31) / 32);
                         max_lds = std::max(max_lds, lds);
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
                                  GF_ERR_ARG, "cell ROI outside level");
@@ -782,8 +787,8 @@ static int plan_extractor(gf_extractor* ex) {
     g.ncells = (int)ex->cells.size();
     ex->list_stride = cap_off;
     ex->lvl_stride = lvl_off;
-    ex->fast_lds = max_lds;  // per wave; four cells per workgroup
-    GF_CHECK(4 * max_lds <= 160 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
+    ex->fast_lds = max_lds;
+    GF_CHECK(max_lds <= 150 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
     ex->capacity = 0;
     for (int l = 0; l < nl; l++) ex->capacity += ex->feat_per_level[l];
     return GF_OK;
@@ -920,7 +925,7 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
     GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)(4 * ex->fast_lds)));
+                               (int)ex->fast_lds));
     *out = ex;
     return GF_OK;
 }
@@ -974,9 +979,8 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     }
     {
         GF_PROF(ctx, s, "k_fast_cells");
-        k_fast_cells<<<dim3((g.ncells + 3) / 4, nframes), 256, 4 * ex->fast_lds, s>>>(
-            g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th,
-            (int)ex->fast_lds);
+        k_fast_cells<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(
+            g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
     }
     {
         GF_PROF(ctx, s, "k_select");
