@@ -220,29 +220,34 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 //     compass test only; the few that pass are compacted into an LDS list and
 //     the full segment test + cornerScore runs on that list, so whole waves do
 //     it (a divergent ~250-op branch per lane otherwise).
-// Thread t owns column t & 63 and rows 4 (t >> 6) .. +3 of the tile.
+// LDS column j of the source tile holds x = X0 - 4 + j, so the tile's rows are
+// whole dwords: x-interior tiles load them as aligned global dwords realigned
+// with v_alignbyte (two loads per dword, all in flight together); border
+// tiles load bytes through reflect-101. The row pass makes four outputs from
+// three LDS dwords with v_dot4_u32_u8 (two per output: the 7 taps are bytes).
+// Thread t then owns column t & 63 and rows 4 (t >> 6) .. +3 of the tile for
+// the column pass, the compass test and the stores.
 #define BT_W 64
 #define BT_H 16
-#define BT_SW (BT_W + 8)  // LDS row of the source tile (70 used)
+#define BT_R (BT_H + 6)   // source rows
+#define BT_SW (BT_W + 8)  // source row: 72 bytes = 18 dwords, x = X0 - 4 .. X0 + 67
 
 // Necessary condition for a 9-arc: it covers two neighbouring compass points
 // of the ring (positions 0, 4, 8, 12), both darker or both brighter.
 __device__ __forceinline__ bool fast_compass(const uint8_t* p, int rw, int th) {
     const int v = p[0], c0 = p[3 * rw], c4 = p[3], c8 = p[-3 * rw], c12 = p[-3];
-    const unsigned dark = (unsigned)(c0 < v - th) | (unsigned)(c4 < v - th) << 1 | (unsigned)(c8 < v - th) << 2 |
-                          (unsigned)(c12 < v - th) << 3;
-    const unsigned bright = (unsigned)(c0 > v + th) | (unsigned)(c4 > v + th) << 1 |
-                            (unsigned)(c8 > v + th) << 2 | (unsigned)(c12 > v + th) << 3;
-    const unsigned d2 = dark & (dark >> 1 | dark << 3), b2 = bright & (bright >> 1 | bright << 3);
-    return ((d2 | b2) & 0xf) != 0;
+    const bool d0 = c0 < v - th, d4 = c4 < v - th, d8 = c8 < v - th, d12 = c12 < v - th;
+    const bool b0 = c0 > v + th, b4 = c4 > v + th, b8 = c8 > v + th, b12 = c12 > v + th;
+    return (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) || (b4 && b8) || (b8 && b12) ||
+           (b12 && b0);
 }
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
-    __shared__ uint8_t src[BT_H + 6][BT_SW];
-    __shared__ int rows[BT_H + 6][BT_W];
+    __shared__ __align__(16) uint8_t src[BT_R][BT_SW];
+    __shared__ int rows[BT_R][BT_W];
     __shared__ uint16_t cand[BT_W * BT_H];
     __shared__ int s_nc;
-    const int f = blockIdx.y;
+    const int f = blockIdx.y, tid = threadIdx.x;
     int t = blockIdx.x, l = 0;
     while (l + 1 < g.nlevels && t >= g.tile_begin[l + 1]) l++;
     t -= g.tile_begin[l];
@@ -253,42 +258,72 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     const uint8_t* S = level_plane(P, g, f, l, stride);
     uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l];
     uint8_t* SC = score + (long long)f * g.bslab + g.boff[l];
-    const bool interior = X0 >= 3 && Y0 >= 3 && X0 + BT_W + 3 <= w && Y0 + BT_H + 3 <= h;
-    if (threadIdx.x == 0) s_nc = 0;
-    // all of a thread's loads issue before the first LDS write: one memory
-    // latency per tile instead of one per loop trip
-    constexpr int NSRC = (BT_H + 6) * (BT_W + 6), NLD = (NSRC + 255) / 256;
-    uint8_t v[NLD];
+    if (tid == 0) s_nc = 0;
+    if (X0 >= 4 && X0 + BT_SW <= w) {
+        // 22 rows x 18 dwords; rows reflect-101 at the top and bottom
+        constexpr int NT = BT_R * (BT_SW / 4), NI = (NT + 255) / 256;
+        uint32_t lo[NI], hi[NI];
+        int sh[NI];
 #pragma unroll
-    for (int k = 0; k < NLD; k++) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < NSRC) {
-            const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
-            int yy = Y0 + ry - 3, xx = X0 + rx - 3;
-            if (!interior) {
-                yy = gfd::reflect101(min(yy, h + 2), h);
-                xx = gfd::reflect101(min(xx, w + 2), w);
+        for (int k = 0; k < NI; k++) {
+            const int i = tid + 256 * k;
+            if (i < NT) {
+                const int ry = i / (BT_SW / 4), q = i - ry * (BT_SW / 4);
+                const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+                const uintptr_t a = (uintptr_t)(S + (long long)yy * stride + X0 - 4 + 4 * q);
+                const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+                sh[k] = (int)(a & 3);
+                lo[k] = al[0];
+                hi[k] = sh[k] ? al[1] : 0u;  // al[1] holds needed bytes whenever sh != 0
             }
-            v[k] = S[(long long)yy * stride + xx];
         }
-    }
 #pragma unroll
-    for (int k = 0; k < NLD; k++) {
-        const int i = threadIdx.x + 256 * k;
-        if (i < NSRC) {
-            const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
-            src[ry][rx] = v[k];
+        for (int k = 0; k < NI; k++) {
+            const int i = tid + 256 * k;
+            if (i < NT) reinterpret_cast<uint32_t*>(&src[0][0])[i] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+        }
+    } else {
+        constexpr int NSRC = BT_R * (BT_W + 6), NLD = (NSRC + 255) / 256;
+        uint8_t v[NLD];
+#pragma unroll
+        for (int k = 0; k < NLD; k++) {
+            const int i = tid + 256 * k;
+            if (i < NSRC) {
+                const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
+                const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+                const int xx = gfd::reflect101(min(X0 + rx - 3, w + 2), w);
+                v[k] = S[(long long)yy * stride + xx];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NLD; k++) {
+            const int i = tid + 256 * k;
+            if (i < NSRC) {
+                const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
+                src[ry][rx + 1] = v[k];
+            }
         }
     }
     __syncthreads();
-    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;  // round(256 * gaussian(7, sigma 2))
-    for (int i = threadIdx.x; i < (BT_H + 6) * BT_W; i += 256) {
-        const int ry = i >> 6, rx = i & 63;
-        const uint8_t* q = &src[ry][rx];
-        rows[ry][rx] = k0 * (q[0] + q[6]) + k1 * (q[1] + q[5]) + k2 * (q[2] + q[4]) + k3 * q[3];
+    // taps round(256 * gaussian(7, sigma 2)) = 18 34 49 55 49 34 18
+    constexpr uint32_t KLO = 18u | 34u << 8 | 49u << 16 | 55u << 24, KHI = 49u | 34u << 8 | 18u << 16;
+    for (int i = tid; i < BT_R * (BT_W / 4); i += 256) {
+        const int ry = i >> 4, q = i & 15;
+        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(&src[ry][0]) + q;
+        const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2];
+        int4 o;  // output x = X0 + 4q + j reads LDS columns 4q + 1 + j .. 4q + 7 + j
+        o.x = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), KLO, 0u, false) +
+                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), KHI, 0u, false));
+        o.y = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), KLO, 0u, false) +
+                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), KHI, 0u, false));
+        o.z = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), KLO, 0u, false) +
+                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), KHI, 0u, false));
+        o.w = (int)(__builtin_amdgcn_udot4(w1, KLO, 0u, false) + __builtin_amdgcn_udot4(w2, KHI, 0u, false));
+        *reinterpret_cast<int4*>(&rows[ry][4 * q]) = o;
     }
     __syncthreads();
-    const int cx = threadIdx.x & 63, ry0 = (threadIdx.x >> 6) * 4, x = X0 + cx;
+    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
+    const int cx = tid & 63, ry0 = (tid >> 6) * 4, x = X0 + cx;
     int rv[10];
 #pragma unroll
     for (int k = 0; k < 10; k++) rv[k] = rows[ry0 + k][cx];
@@ -300,18 +335,18 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
                         k3 * rv[r + 3];
         D[(long long)y * w + x] = (uint8_t)min(max((sum + (1 << 15)) >> 16, 0), 255);
         const bool cand_px = x >= 3 && x < w - 3 && y >= 3 && y < h - 3 &&
-                             fast_compass(&src[ry0 + r + 3][cx + 3], BT_SW, map_th);
+                             fast_compass(&src[ry0 + r + 3][cx + 4], BT_SW, map_th);
         if (cand_px)
             cand[atomicAdd(&s_nc, 1)] = (uint16_t)((ry0 + r) * BT_W + cx);
         else
             SC[(long long)y * w + x] = 0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < s_nc; i += 256) {
+    for (int i = tid; i < s_nc; i += 256) {
         const int q = cand[i], py = q >> 6, px = q & 63;
         int c[16];
-        circle_vals(&src[0][0], BT_SW, px + 3, py + 3, c);
-        const int fs = fast_score(src[py + 3][px + 3], c, map_th);
+        circle_vals(&src[0][0], BT_SW, px + 4, py + 3, c);
+        const int fs = fast_score(src[py + 3][px + 4], c, map_th);
         SC[(long long)(Y0 + py) * w + X0 + px] = (fs & 0x100) ? (uint8_t)((fs & 0xff) + 1) : 0;
     }
 }
