@@ -272,6 +272,7 @@ struct ActiveArgs {
     int32_t* nleft;
     int32_t* nmatched;
     int32_t* err;
+    const struct OnePre* pre;  // [F][mp_cap] one-point results against the starting claims
 };
 
 // ---------------------------------------------------------------------------
@@ -366,15 +367,39 @@ __device__ __forceinline__ void pool_prefix(const Pool& P) {
     if (lane == 63) P.pre[64] = x;
 }
 
+// Keypoint sources for the one-point scan: the frame's arrays in HBM, or the
+// copy a precompute workgroup staged in LDS (x, y, octave as float4; the
+// descriptors behind a generic pointer, LDS or HBM).
+struct KpGlobal {
+    const gf_keypoint* K;
+    const uint8_t* D;
+    __device__ float4 xyo(int i) const {
+        const gf_keypoint kp = K[i];
+        return make_float4(kp.x, kp.y, __int_as_float(kp.octave), 0.f);
+    }
+    __device__ const uint8_t* desc(int i) const { return D + (long long)i * 32; }
+};
+struct KpStaged {
+    const float4* X;
+    const uint8_t* D;
+    __device__ float4 xyo(int i) const { return X[i]; }
+    __device__ const uint8_t* desc(int i) const { return D + (long long)i * 32; }
+};
+
 // ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) on one lane,
-// without claiming: returns the keypoint it would claim (or -1) and its
-// distance. Within a round every candidate sees the same claims (only the
-// round's final success claims), so all candidates are evaluated at once.
-__device__ void lane_one_point(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
-                               const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D,
-                               int& outIdx, int& outDist) {
+// without claiming: the keypoint it would claim (or -1) and its distance,
+// plus the keypoints holding first and second place in its best/second-best
+// loop. Claims only remove keypoints, and the loop's outcome is a function of
+// those two holders alone (the first keypoint at the minimum distance, the
+// first other one at the second smallest), so a result stays exact until one
+// of its two holders is claimed.
+template <class KP>
+__device__ void one_point_scan(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
+                               const int* items, const int* claim, const KP& kps, int& outIdx, int& outDist,
+                               int& holder1, int& holder2) {
     outIdx = -1;
     outDist = INT_MAX;
+    holder1 = holder2 = -1;
     const gf_mp_view v = A.views[(long long)f * A.mp_cap + mpi];
     if (!v.in_view) return;
     const int pl = min(max(v.level, 0), fc.nlevels - 1);
@@ -384,33 +409,85 @@ __device__ void lane_one_point(const ActiveArgs& A, const FrameConst& fc, int f,
     int cx0, cx1, cy0, cy1;
     if (!grid_window(fc, v.u, v.v, r, cx0, cx1, cy0, cy1)) return;
     const uint8_t* qd = A.mp_desc + ((long long)f * A.mp_cap + mpi) * 32;
-    int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+    int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1, secondIdx = -1;
     for (int ix = cx0; ix <= cx1; ix++) {
         const int s = cell_start[ix * GRID_ROWS + cy0], e = cell_start[ix * GRID_ROWS + cy1 + 1];
         for (int t = s; t < e; t++) {
             const int idx = items[t];
-            const gf_keypoint kp = K[idx];
-            if (!level_ok(kp.octave, pl - 1, pl)) continue;
+            const float4 kp = kps.xyo(idx);
+            const int oct = __float_as_int(kp.z);
+            if (!level_ok(oct, pl - 1, pl)) continue;
             if (fabsf(kp.x - v.u) > r || fabsf(kp.y - v.v) > r) continue;
             if (claim[idx] >= 0) continue;
-            const int dist = hamming32(qd, D + (long long)idx * 32);
+            const int dist = hamming32(qd, kps.desc(idx));
             if (dist < bestDist) {
                 bestDist2 = bestDist;
                 bestDist = dist;
                 bestLevel2 = bestLevel;
-                bestLevel = kp.octave;
+                bestLevel = oct;
+                secondIdx = bestIdx;
                 bestIdx = idx;
             } else if (dist < bestDist2) {
-                bestLevel2 = kp.octave;
+                bestLevel2 = oct;
                 bestDist2 = dist;
+                secondIdx = idx;
             }
         }
     }
+    holder1 = bestIdx;
+    holder2 = secondIdx;
     if (bestDist <= TH_HIGH) {
         if (bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2) return;
         outIdx = bestIdx;
         outDist = bestDist;
     }
+}
+
+struct OnePre {  // one-point result against the frame's starting claims
+    int16_t idx, dist, holder1, holder2;
+};
+
+// One 1024-thread workgroup per frame: the keypoint grid, the keypoints'
+// (x, y, octave) and (up to 2048 keypoints) their descriptors in LDS, then
+// one thread per in-view map point runs the one-point scan. The active
+// matcher takes these results until a claim hits one of their holders.
+#define PRE_THREADS 1024
+#define PRE_DESC_LDS_MAX 2048
+__global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OnePre* __restrict__ out) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = min(A.n[f], KP_MAX);
+    const int m = min(A.m[f], 32767);
+    float4* X = (float4*)smem;                  // kp_cap
+    int* cell_start = (int*)(X + A.kp_cap);     // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;      // NCELLS
+    int* items = cursor + NCELLS;               // kp_cap
+    int* claim = items + A.kp_cap;              // kp_cap
+    int* scratch = claim + A.kp_cap;            // kp_cap
+    uint8_t* Ds = (uint8_t*)(scratch + A.kp_cap);  // 32 x kp_cap when kp_cap <= PRE_DESC_LDS_MAX
+    const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
+    const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
+    const bool dl = A.kp_cap <= PRE_DESC_LDS_MAX;
+    for (int i = tid; i < n; i += PRE_THREADS) {
+        const gf_keypoint kp = K[i];
+        X[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), 0.f);
+    }
+    if (dl)
+        for (int i = tid; i < 2 * n; i += PRE_THREADS)
+            reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
+    build_grid(A.fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
+               PRE_THREADS);
+    const KpStaged src{X, dl ? (const uint8_t*)Ds : D};
+    for (int i = tid; i < m; i += PRE_THREADS) {
+        int mi, md, h1, h2;
+        one_point_scan(A, A.fc, f, i, cell_start, items, claim, src, mi, md, h1, h2);
+        out[(long long)f * A.mp_cap + i] = OnePre{(int16_t)mi, (int16_t)(mi >= 0 ? md : 0), (int16_t)h1, (int16_t)h2};
+    }
+}
+
+size_t onepoint_pre_lds_bytes(int kp_cap) {
+    return 16 * (size_t)kp_cap + sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kp_cap) +
+           (kp_cap <= PRE_DESC_LDS_MAX ? 32 * (size_t)kp_cap : 0);
 }
 
 // Per-round candidate list: the draws of the sequential loop in order (the
@@ -471,10 +548,15 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int q = lmk[C.slot[c]];
         C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
-        int mi, md;
-        lane_one_point(A, fc, f, q, cell_start, items, claim, K, D, mi, md);
+        const OnePre p = A.pre[(long long)f * A.mp_cap + q];
+        int mi = p.idx, md = p.dist;
+        if ((p.holder1 >= 0 && claim[p.holder1] >= 0) || (p.holder2 >= 0 && claim[p.holder2] >= 0)) {
+            int h1, h2;  // a holder was claimed this frame: scan again
+            one_point_scan(A, fc, f, q, cell_start, items, claim, KpGlobal{K, D}, mi, md, h1, h2);
+            if (mi < 0) md = 0;
+        }
         C.match[c] = (int16_t)mi;
-        C.dist[c] = (int16_t)(mi >= 0 ? md : 0);
+        C.dist[c] = (int16_t)md;
         C.alive[c] = 0;
     }
     __syncthreads();
@@ -530,7 +612,22 @@ __device__ int wave_top(const Cands& C, int ncand, int sz, int npop, int16_t* rh
     return *s_res;
 }
 
+#ifdef GF_AM_STAMP  // diagnostic build only: shader cycles per phase, summed over frames
+__device__ unsigned long long g_am_stamp[8];
+#define AM_T(k)                                                               \
+    do {                                                                      \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
+        if (threadIdx.x == 0) atomicAdd(&g_am_stamp[k], now_ - am_last_);     \
+        am_last_ = now_;                                                      \
+    } while (0)
+#else
+#define AM_T(k) (void)0
+#endif
+
 __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
+#ifdef GF_AM_STAMP
+    unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
+#endif
     extern __shared__ __align__(16) uint8_t smem[];
     double* c_score = (double*)smem;                                       // POOL_MAX
     unsigned long long* pbits = (unsigned long long*)(c_score + POOL_MAX);  // 64
@@ -560,6 +657,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     int32_t* left = A.left + (long long)f * A.mp_cap;
     const int num_to_match = A.num_to_match[f];
     build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, (int*)c_score, AW);
+    AM_T(0);
 
     // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
     const bool early = (m == 0 || num_to_match <= 0);
@@ -611,6 +709,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     }
     int used = 0, nm = 0;
     __syncthreads();
+    AM_T(1);
 
     const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
     const int S = (int)((float)N / (float)num_to_match * 1.0);
@@ -629,6 +728,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh);
             exh_at = s_exh;
         }
+        AM_T(2);
         if (nc < sz) {  // the initial subset could not be completed
             for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
             used += exh_at;
@@ -639,6 +739,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         evald = nc;
         for (int c = lane; c < sz; c += AW) C.alive[c] = 1;
         __syncthreads();
+        AM_T(3);
         // -- the sequential heap loop, now over known scores and match results
         int npop = 0, top = -1;
         bool exh = false, success = false;
@@ -668,6 +769,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             npop++;
             __syncthreads();
         }
+        AM_T(4);
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
         const int T = exh ? exh_at : C.tries[nused - 1];
@@ -676,6 +778,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs), min(t, 64));
         __syncthreads();
         if (exh) break;
+        AM_T(5);
         const int nrem = npop + 1;  // removeIdx: every top tried
         const int q = lmk[C.slot[top]];
         const int b = C.match[top];
@@ -702,6 +805,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         pool_prefix(P);
         N -= nrem;
         __syncthreads();
+        AM_T(6);
     }
     // ---- outputs: claims, left-over pool (alive slots in order), RNG state
     for (int i = lane; i < n; i += AW) kp2mp[i] = claim[i];
@@ -724,6 +828,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     }
 }
 
+
+#undef AM_T
 
 size_t active_lds_bytes() {
     return sizeof(double) * POOL_MAX + 8 * 64 + sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX + 68) +
@@ -984,6 +1090,23 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
         for (int k = 0; k < 64; k++)
             for (int j = 0; j < 31; j++) h[31 + k][j] = h[28 + k][j] + h[k][j];
         GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_rng_coef), &h[31][0], sizeof(uint32_t) * 64 * 31));
+    }
+    void* pre;
+    rc = gf::ws_get(ctx, 32, sizeof(OnePre) * (size_t)nframes * mp_cap, &pre);
+    if (rc) return rc;
+    A.pre = (const OnePre*)pre;
+    static unsigned long long pre_mask = 0;
+    const size_t pre_lds = onepoint_pre_lds_bytes(kp_cap);
+    GF_CHECK(pre_lds <= 160 * 1024, GF_ERR_UNSUPPORTED, "keypoint capacity too large for the one-point precompute");
+    if (!(pre_mask & (1ull << ctx->device))) {
+        GF_HIP(hipFuncSetAttribute((const void*)k_onepoint_pre, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)onepoint_pre_lds_bytes(KP_MAX)));
+        pre_mask |= 1ull << ctx->device;
+    }
+    {
+        GF_PROF(ctx, s, "k_onepoint_pre");
+        k_onepoint_pre<<<nframes, PRE_THREADS, pre_lds, s>>>(A, (OnePre*)pre);
+        GF_HIP(hipGetLastError());
     }
     rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(), &mask);
     if (rc) return rc;
@@ -1328,3 +1451,15 @@ int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2
 }
 
 }  // extern "C"
+
+#ifdef GF_AM_STAMP
+// Diagnostic build only (not in the header): phase cycles of k_active_match.
+extern "C" int gf_debug_am_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_stamp), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_am_stamp), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
