@@ -570,12 +570,31 @@ __device__ float fast_atan2f(float y, float x) {
 }
 
 // One wave per keypoint, 4 per workgroup.
+// Per wave: the 31x31 IC_Angle patch of the unblurred level and the 37x37
+// window of the blurred level that holds every rotated rBRIEF sample (the
+// pattern's points lie within 18.4 px of the keypoint), both fetched as
+// aligned dwords in one batch right after the keypoint entry, so a keypoint
+// costs two dependent memory round trips. A keypoint whose window leaves the
+// level reads its rBRIEF samples from HBM with the reflect-101 border instead.
+#define DS_IC 31
+#define DS_ICW 9    // dwords per IC row (31 bytes at any alignment)
+#define DS_BL 37
+#define DS_BLW 10   // dwords per window row (37 bytes at any alignment)
+#define DS_LOADS ((DS_IC * DS_ICW + DS_BL * DS_BLW + 63) / 64)
+struct DescLds {
+    uint32_t ic[DS_IC * DS_ICW];
+    uint32_t bl[DS_BL * DS_BLW];
+    uint8_t ic_sh[DS_IC], bl_sh[DS_BL];
+};
+
 __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const uint32_t* __restrict__ lvl_lists,
                                                   long long lvl_stride, const int* __restrict__ lvl_counts,
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
+    __shared__ DescLds sh_all[4];
     const int f = blockIdx.y;
     const int lane = threadIdx.x & 63;
+    DescLds& W = sh_all[threadIdx.x >> 6];
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
     int total = 0, l = -1, idx = 0;
     for (int i = 0; i < g.nlevels; i++) {
@@ -594,35 +613,58 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     int stride;
     const uint8_t* Pl = level_plane(P, g, f, l, stride);
     const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[l];
+    const bool win = x >= 18 && x + 18 < w && y >= 18 && y + 18 < h;
 
-    // IC_Angle: the 31x31 square around the keypoint, 16 pixels per lane with
-    // every load in flight at once; pixels outside the circular patch
-    // (|u| > umax[|v|]) weigh 0. Integer moments, so the order is free.
-    int m10 = 0, m01 = 0;
-    {
-        int pv[16];
+    {  // one batch: IC rows y-15..y+15 (cols x-15..), window rows y-18..y+18 (cols x-18..)
+        uint32_t v[DS_LOADS];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int j = lane + 64 * k;
-            const int v = j / 31 - 15, u = j - (j / 31) * 31 - 15;
-            const bool in = j < 961 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v];
-            pv[k] = in ? Pl[(long long)(y + v) * stride + x + u] : 0;
+        for (int t = 0; t < DS_LOADS; t++) {
+            const int i = lane + 64 * t;
+            v[t] = 0;
+            if (i < DS_IC * DS_ICW) {
+                const int r = i / DS_ICW, q = i - r * DS_ICW;
+                const uintptr_t a = (uintptr_t)(Pl + (long long)(y - 15 + r) * stride + x - 15);
+                v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+            } else if (win && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
+                const int j = i - DS_IC * DS_ICW, r = j / DS_BLW, q = j - r * DS_BLW;
+                const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * w + x - 18);
+                v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+            }
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const int j = lane + 64 * k;
-            const int v = j / 31 - 15, u = j - (j / 31) * 31 - 15;
-            m10 += u * pv[k];
-            m01 += v * pv[k];
+        for (int t = 0; t < DS_LOADS; t++) {
+            const int i = lane + 64 * t;
+            if (i < DS_IC * DS_ICW) W.ic[i] = v[t];
+            else if (i < DS_IC * DS_ICW + DS_BL * DS_BLW) W.bl[i - DS_IC * DS_ICW] = v[t];
+        }
+        if (lane < DS_IC) W.ic_sh[lane] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + lane) * stride + x - 15) & 3);
+        if (lane < DS_BL) W.bl_sh[lane] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + lane) * w + x - 18) & 3);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint8_t* ic8 = reinterpret_cast<const uint8_t*>(W.ic);
+    const uint8_t* bl8 = reinterpret_cast<const uint8_t*>(W.bl);
+
+    // IC_Angle: 16 pixels of the 31x31 square per lane; pixels outside the
+    // circular patch (|u| > umax[|v|]) weigh 0. Integer moments: order-free.
+    int m10 = 0, m01 = 0;
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const int j = lane + 64 * t;
+        const int r = j / 31, c = j - r * 31;
+        const int v = r - 15, u = c - 15;
+        if (j < 961 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v]) {
+            const int p = ic8[r * (4 * DS_ICW) + W.ic_sh[r] + c];
+            m10 += u * p;
+            m01 += v * p;
         }
     }
     m10 = gfd::warp_sum(m10);
     m01 = gfd::warp_sum(m01);
     const float angle = fast_atan2f((float)m01, (float)m10);
 
-    // rBRIEF: lane 2b + hi computes bits 4 hi .. 4 hi + 3 of descriptor byte b;
-    // addresses first (blurred interior or unblurred reflect-101 border), then
-    // the 8 loads together.
+    // rBRIEF: lane 2b + hi computes bits 4 hi .. 4 hi + 3 of descriptor byte b.
     {
         const float factorPI = (float)(M_PI / 180.f);
         const float ang = angle * factorPI;
@@ -635,11 +677,15 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
             const int ry = __float2int_rn(px * b + py * a);
             const int rx = __float2int_rn(px * a - py * b);
-            const int xx = x + rx, yy = y + ry;
-            const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
-            const uint8_t* src = inside ? B + (long long)yy * w + xx
-                                        : Pl + (long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w);
-            t[q] = *src;
+            if (win) {
+                const int r = ry + 18;
+                t[q] = bl8[r * (4 * DS_BLW) + W.bl_sh[r] + rx + 18];
+            } else {
+                const int xx = x + rx, yy = y + ry;
+                const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
+                t[q] = inside ? B[(long long)yy * w + xx]
+                              : Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
+            }
         }
         int nib = 0;
 #pragma unroll

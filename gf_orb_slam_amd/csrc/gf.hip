@@ -490,6 +490,10 @@ size_t onepoint_pre_lds_bytes(int kp_cap) {
            (kp_cap <= PRE_DESC_LDS_MAX ? 32 * (size_t)kp_cap : 0);
 }
 
+#ifdef GF_AM_STAMP
+__device__ unsigned long long g_am_stamp[8];
+#endif
+
 // Per-round candidate list: the draws of the sequential loop in order (the
 // initial random subset, then one replacement per failed top), produced 64
 // tries at a time ahead of need.
@@ -545,9 +549,19 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const double* cur, const double* info, const int* cell_start,
                            const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D) {
+#ifdef GF_AM_STAMP
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int q = lmk[C.slot[c]];
         C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
+    }
+#ifdef GF_AM_STAMP
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) atomicAdd(&g_am_stamp[7], t1 - t0);
+#endif
+    for (int c = c0 + threadIdx.x; c < c1; c += AW) {
+        const int q = lmk[C.slot[c]];
         const OnePre p = A.pre[(long long)f * A.mp_cap + q];
         int mi = p.idx, md = p.dist;
         if ((p.holder1 >= 0 && claim[p.holder1] >= 0) || (p.holder2 >= 0 && claim[p.holder2] >= 0)) {
@@ -613,7 +627,6 @@ __device__ int wave_top(const Cands& C, int ncand, int sz, int npop, int16_t* rh
 }
 
 #ifdef GF_AM_STAMP  // diagnostic build only: shader cycles per phase, summed over frames
-__device__ unsigned long long g_am_stamp[8];
 #define AM_T(k)                                                               \
     do {                                                                      \
         const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \

@@ -31,10 +31,10 @@ for _ in range(steps):
     fe.step()
 fe.sync()
 fn(buf, 1)
-names = ["grid", "pool", "draw", "eval0", "heaploop", "commit", "claim+pool"]
+names = ["grid", "pool", "draw", "eval0", "heaploop", "commit", "claim+pool", "(logdet)"]
 tot = sum(buf[i] for i in range(7))
 per = B * steps
 print(f"cycles per frame (B={B}, steps={steps}): total {tot / per:.0f}")
-for i, nme in enumerate(names):
+for i, nme in enumerate(names):  # (logdet) is inside eval0 + heaploop
     print(f"  {nme:12s} {buf[i] / per:10.0f}  {100.0 * buf[i] / max(tot, 1):5.1f}%")
 print("matched per frame", fe.n_active.float().mean().item())
