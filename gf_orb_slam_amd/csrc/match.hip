@@ -56,6 +56,7 @@ struct MatchArgs {
     int32_t* nmatches;
     int32_t* qres;  // [F][q_cap] scratch: matched kp per query (MODE_LAST)
     int32_t* err;   // [F] round-limit flag
+    const struct SeqPre* pre;  // [F][q_cap] MODE_LAST: each query against the starting claims
 };
 
 
@@ -300,6 +301,93 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     if (tid == 0) A.nmatches[f] = s_nm;
 }
 
+// ---- Per-query precompute for the wave-sequential matcher. Every valid query
+// runs its window scan at once (one thread each) against the frame's starting
+// claims, keeping the keypoints that end in first and second place of the
+// best / second-best loop. Claims only remove keypoints and the loop's outcome
+// depends on those two holders alone (the first keypoint at the minimum
+// distance, the first other one at the second smallest), so in the ordered
+// pass a query whose holders are both still unclaimed takes its precomputed
+// result as is; only the others scan again.
+struct SeqPre {
+    int32_t id;
+    int16_t res, dist, holder1, holder2;
+};
+
+#define SEQ_PRE_THREADS 1024
+#define SEQ_PRE_DESC_MAX 2048
+__global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,
+                                                                   SeqPre* __restrict__ out) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int n = min(A.n[f], KP_MAX);
+    const int nq = min(A.m[f], Q_MAX);
+    float4* X = (float4*)smem;                  // kp_cap: x, y, octave
+    int* cell_start = (int*)(X + A.kp_cap);     // NCELLS + 1
+    int* cursor = cell_start + NCELLS + 1;      // NCELLS
+    int* items = cursor + NCELLS;               // kp_cap
+    int* claim = items + A.kp_cap;              // kp_cap
+    int* scratch = claim + A.kp_cap;            // kp_cap
+    uint8_t* Ds = (uint8_t*)(scratch + A.kp_cap);  // 32 x kp_cap when kp_cap <= SEQ_PRE_DESC_MAX
+    const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
+    const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
+    const bool dl = A.kp_cap <= SEQ_PRE_DESC_MAX;
+    for (int i = tid; i < n; i += SEQ_PRE_THREADS) {
+        const gf_keypoint kp = K[i];
+        X[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), 0.f);
+    }
+    if (dl)
+        for (int i = tid; i < 2 * n; i += SEQ_PRE_THREADS)
+            reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
+    build_grid(fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
+               SEQ_PRE_THREADS);
+    const uint8_t* DD = dl ? (const uint8_t*)Ds : D;
+    for (int k = tid; k < nq; k += SEQ_PRE_THREADS) {
+        const Query q = make_query(A, fc, f, k);
+        SeqPre r{q.id, -1, 0, -1, -1};
+        if (q.valid) {
+            int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, h1 = -1, h2 = -1;
+            for (int ix = q.cx0; ix <= q.cx1; ix++) {
+                const int s0 = cell_start[ix * GRID_ROWS + q.cy0], s1 = cell_start[ix * GRID_ROWS + q.cy1 + 1];
+                for (int t = s0; t < s1; t++) {
+                    const int idx = items[t];
+                    const float4 kp = X[idx];
+                    const int oct = __float_as_int(kp.z);
+                    if (!level_ok(oct, q.minL, q.maxL) || fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r ||
+                        claim[idx] >= 0)
+                        continue;
+                    const int dist = hamming32(q.d, DD + (long long)idx * 32);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist;
+                        bestDist = dist;
+                        bestLevel2 = bestLevel;
+                        bestLevel = oct;
+                        h2 = h1;
+                        h1 = idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = oct;
+                        bestDist2 = dist;
+                        h2 = idx;
+                    }
+                }
+            }
+            r.holder1 = (int16_t)h1;
+            r.holder2 = (int16_t)h2;
+            if (h1 >= 0 && bestDist <= TH_HIGH &&
+                !(A.mode == MODE_PROJECT && bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2)) {
+                r.res = (int16_t)h1;
+                r.dist = (int16_t)bestDist;
+            }
+        }
+        out[(long long)f * A.q_cap + k] = r;
+    }
+}
+
+size_t seq_pre_lds_bytes(int kp_cap) {
+    return 16 * (size_t)kp_cap + sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kp_cap) +
+           (kp_cap <= SEQ_PRE_DESC_MAX ? 32 * (size_t)kp_cap : 0);
+}
+
 // ---- Wave-sequential variant for few, wide queries (SearchByProjection(Cur,
 // Last, th), th = 15 px x scale): the queries run in the reference order, one
 // after the other, and each query's candidate window is scanned by the 64
@@ -358,6 +446,17 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
     const unsigned long long NONE = ~0ull;
     for (int qi = 0; qi < nvalid; qi++) {
         const int k = qlist[qi];
+        const SeqPre pr = A.pre[(long long)f * A.q_cap + k];
+        if ((pr.holder1 < 0 || claim[pr.holder1] < 0) && (pr.holder2 < 0 || claim[pr.holder2] < 0)) {
+            if (lane == 0 && pr.res >= 0) {  // the precomputed outcome still holds
+                claim[pr.res] = pr.id;
+                score[pr.res] = pr.dist;
+                s_nm++;
+                if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = pr.res;
+            }
+            __syncthreads();
+            continue;
+        }
         const Query q = make_query(A, fc, f, k);
         unsigned long long k1 = NONE, k2 = NONE;
         // walk the window's columns; candidate order t runs ix-major, then the CSR
@@ -520,9 +619,16 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
                                    (int)match_lds_bytes()));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)seq_lds_bytes()));
+        GF_HIP(hipFuncSetAttribute((const void*)k_match_seq_pre, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)seq_pre_lds_bytes(KP_MAX)));
         attr_mask |= 1ull << ctx->device;
     }
     if (A.mode == MODE_LAST) {  // few queries, wide windows: wave-sequential in the reference order
+        {
+            GF_PROF(ctx, s, "k_match_seq_pre");
+            k_match_seq_pre<<<nframes, SEQ_PRE_THREADS, seq_pre_lds_bytes(A.kp_cap), s>>>(A, fc, (SeqPre*)A.pre);
+            GF_HIP(hipGetLastError());
+        }
         GF_PROF(ctx, s, "k_match_lastframe");
         k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(), s>>>(A, fc);
     } else {  // many queries, narrow windows: claim-resolution rounds
@@ -618,6 +724,11 @@ int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, co
     rc = gf::ws_get(ctx, 31, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
     A.err = (int32_t*)err;
+    void* pre;
+    rc = gf::ws_get(ctx, 33, sizeof(SeqPre) * (size_t)nframes * last_cap, &pre);
+    if (rc) return rc;
+    A.pre = (const SeqPre*)pre;
+    GF_CHECK(seq_pre_lds_bytes(kp_cap) <= 160 * 1024, GF_ERR_UNSUPPORTED, "keypoint capacity too large");
     return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
 }
 
