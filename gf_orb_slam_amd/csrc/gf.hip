@@ -273,6 +273,8 @@ struct ActiveArgs {
     int32_t* nmatched;
     int32_t* err;
     const struct OnePre* pre;  // [F][mp_cap] one-point results against the starting claims
+    int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
+    int* grid_items;           // [F][kp_cap]
 };
 
 // ---------------------------------------------------------------------------
@@ -297,11 +299,10 @@ constexpr int AW = 64;
 // (lane k: 31 multiply-adds); rand() = word >> 1.
 __constant__ uint32_t c_rng_coef[64][31];
 
-__device__ __forceinline__ uint32_t rng_word(uint32_t s) {
-    const int k = threadIdx.x;
+__device__ __forceinline__ uint32_t rng_word(uint32_t s, const uint32_t (&coef)[31]) {
     uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < 31; j++) acc += c_rng_coef[k][j] * (uint32_t)__builtin_amdgcn_readlane((int)s, j);
+    for (int j = 0; j < 31; j++) acc += coef[j] * (uint32_t)__builtin_amdgcn_readlane((int)s, j);
     return acc;
 }
 
@@ -477,6 +478,8 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
             reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
     build_grid(A.fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
                PRE_THREADS);
+    for (int c = tid; c < NCELLS + 1; c += PRE_THREADS) A.grid_cs[(long long)f * (NCELLS + 1) + c] = cell_start[c];
+    for (int i = tid; i < n; i += PRE_THREADS) A.grid_items[(long long)f * A.kp_cap + i] = items[i];
     const KpStaged src{X, dl ? (const uint8_t*)Ds : D};
     for (int i = tid; i < m; i += PRE_THREADS) {
         int mi, md, h1, h2;
@@ -511,16 +514,22 @@ struct Cands {
 // marked visited at once (unused ones are unmarked at the round end). A draw
 // fails after MAX_RANDOM_QUERY_TIME rejected tries: *exh_at = tries count then.
 __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, const Pool& P, int16_t* vis,
-                          const Cands& C, int nc, int* exh_at) {
+                          const Cands& C, int nc, int* exh_at, int* first, const uint32_t (&coef)[31]) {
     const int lane = threadIdx.x;
-    const uint32_t o = rng_word(s);
+    const uint32_t o = rng_word(s, coef);
     const int j = (int)((o >> 1) % (uint32_t)N);
     const int sl = pool_select(P, j);
-    bool acc = vis[sl] < round;
-    for (int k = 0; k < 63; k++) {
-        const int jk = __builtin_amdgcn_readlane(j, k);
-        acc = acc && !(k < lane && jk == j);
-    }
+    // an earlier try of this batch that drew the same column wins: the lowest
+    // lane per slot, through LDS marks reset right after
+    atomicMin(&first[sl], lane);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool acc = vis[sl] < round && first[sl] == lane;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    first[sl] = AW;
     const unsigned long long m = __ballot(acc);
     const int a0 = m ? __ffsll((long long)m) - 1 : 64;
     int got = 0;
@@ -644,10 +653,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     extern __shared__ __align__(16) uint8_t smem[];
     double* c_score = (double*)smem;                                       // POOL_MAX
     unsigned long long* pbits = (unsigned long long*)(c_score + POOL_MAX);  // 64
-    int* cell_start = (int*)(pbits + 64);                                  // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;                                 // NCELLS (later: replay heap)
-    int* items = cursor + NCELLS;                                          // KP_MAX
-    int* claim = items + KP_MAX;                                           // KP_MAX
+    int* first = (int*)(pbits + 64);                                       // POOL_MAX: draw-batch duplicate marks
+    int* claim = first + POOL_MAX;                                         // KP_MAX
     int* ppre = claim + KP_MAX;                                            // 65 (+3 pad)
     int32_t* c_tries = ppre + 68;                                          // POOL_MAX
     int16_t* lmk = (int16_t*)(c_tries + POOL_MAX);                         // POOL_MAX: map point of each slot
@@ -655,8 +662,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     int16_t* c_slot = vis + POOL_MAX;                                      // POOL_MAX
     int16_t* c_match = c_slot + POOL_MAX;                                  // POOL_MAX
     int16_t* c_dist = c_match + POOL_MAX;                                  // POOL_MAX
-    uint8_t* c_alive = (uint8_t*)(c_dist + POOL_MAX);                      // POOL_MAX
-    int16_t* rheap = (int16_t*)cursor;
+    int16_t* rheap = c_dist + POOL_MAX;                                    // POOL_MAX: replay heap
+    uint8_t* c_alive = (uint8_t*)(rheap + POOL_MAX);                       // POOL_MAX
     __shared__ double cur[49];
     __shared__ int s_res, s_exh;
 
@@ -669,7 +676,15 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* left = A.left + (long long)f * A.mp_cap;
     const int num_to_match = A.num_to_match[f];
-    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, (int*)c_score, AW);
+    // the keypoint grid comes from k_onepoint_pre (HBM; only rescans read it)
+    const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
+    const int* items = A.grid_items + (long long)f * A.kp_cap;
+    for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
+    for (int i = lane; i < POOL_MAX; i += AW) first[i] = AW;
+    uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
+#pragma unroll
+    for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
+    __syncthreads();
     AM_T(0);
 
     // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
@@ -738,14 +753,14 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         while (nc < sz && exh_at < 0) {
             if (lane == 0) s_exh = -1;
             __syncthreads();
-            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh);
+            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, first, rcoef);
             exh_at = s_exh;
         }
         AM_T(2);
         if (nc < sz) {  // the initial subset could not be completed
             for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
             used += exh_at;
-            for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs), min(T, 64));
+            for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
         eval_cands(A, fc, f, C, 0, nc, lmk, cur, info, cell_start, items, claim, K, D);
@@ -767,7 +782,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             while (rep >= nc && exh_at < 0) {
                 if (lane == 0) s_exh = -1;
                 __syncthreads();
-                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh);
+                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, first, rcoef);
                 exh_at = s_exh;
             }
             if (rep >= nc) {
@@ -788,7 +803,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         const int T = exh ? exh_at : C.tries[nused - 1];
         for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
         used += T;
-        for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs), min(t, 64));
+        for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
         __syncthreads();
         if (exh) break;
         AM_T(5);
@@ -845,8 +860,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
 #undef AM_T
 
 size_t active_lds_bytes() {
-    return sizeof(double) * POOL_MAX + 8 * 64 + sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX + 68) +
-           sizeof(int32_t) * POOL_MAX + sizeof(int16_t) * 5 * POOL_MAX + POOL_MAX;
+    return sizeof(double) * POOL_MAX + 8 * 64 + sizeof(int) * (POOL_MAX + KP_MAX + 68) +
+           sizeof(int32_t) * POOL_MAX + sizeof(int16_t) * 6 * POOL_MAX + POOL_MAX;
 }
 
 // ------------------------------------------------------------- max-volume selection
@@ -1108,6 +1123,12 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
     rc = gf::ws_get(ctx, 32, sizeof(OnePre) * (size_t)nframes * mp_cap, &pre);
     if (rc) return rc;
     A.pre = (const OnePre*)pre;
+    void *gcs, *gitems;
+    if ((rc = gf::ws_get(ctx, 34, sizeof(int) * (size_t)nframes * (NCELLS + 1), &gcs)) ||
+        (rc = gf::ws_get(ctx, 35, sizeof(int) * (size_t)nframes * kp_cap, &gitems)))
+        return rc;
+    A.grid_cs = (int*)gcs;
+    A.grid_items = (int*)gitems;
     static unsigned long long pre_mask = 0;
     const size_t pre_lds = onepoint_pre_lds_bytes(kp_cap);
     GF_CHECK(pre_lds <= 160 * 1024, GF_ERR_UNSUPPORTED, "keypoint capacity too large for the one-point precompute");
