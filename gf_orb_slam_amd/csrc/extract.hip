@@ -84,35 +84,82 @@ __device__ __forceinline__ const uint8_t* level_plane(const Planes& P, const Lev
 }
 
 // -------------------------------------------------------------- k_resize
-// One thread per destination pixel. xtab[dx] = (sx, a0 | a1<<16),
-// ytab[dy] = (sy, b0 | b1<<16) precomputed on the host with OpenCV's float
-// coefficient arithmetic.
-__global__ void k_resize(Planes P, LevelGeom g, int l, const int2* __restrict__ xtab,
-                         const int2* __restrict__ ytab) {
-    const int f = blockIdx.z;
-    const int dx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int dy = blockIdx.y * blockDim.y + threadIdx.y;
+// cv::resize INTER_LINEAR, level l from level l-1 (ORBextractor.cc:1063-1068).
+// xtab[dx] = (sx, a0 | a1<<16), ytab[dy] = (sy, b0 | b1<<16) precomputed on
+// the host with OpenCV's float coefficient arithmetic. One 256-thread
+// workgroup per 64x16 output tile: the source rows and columns the tile
+// reads go to LDS as aligned dwords (one batch of loads), then each thread
+// makes one column's outputs in 4 rows from LDS.
+#define RS_W 64
+#define RS_H 16
+__global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, const int2* __restrict__ xtab,
+                                                const int2* __restrict__ ytab, int tiles_x, int pitch, int max_rows) {
+    extern __shared__ __align__(16) uint32_t rs_lds[];
+    uint8_t* src = reinterpret_cast<uint8_t*>(rs_lds);
+    uint8_t* rsh = src + (size_t)pitch * max_rows;  // byte offset of each row's first needed column
+    const int f = blockIdx.y, tid = threadIdx.x;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
     const int dw = g.w[l], dh = g.h[l], sw = g.w[l - 1], sh = g.h[l - 1];
-    if (dx >= dw || dy >= dh) return;
+    const int X0 = tx * RS_W, Y0 = ty * RS_H;
+    const int xl = min(X0 + RS_W - 1, dw - 1), yl = min(Y0 + RS_H - 1, dh - 1);
+    const int cs = xtab[X0].x, ce = min(xtab[xl].x + 1, sw - 1);
+    const int rs = min(max(ytab[Y0].x, 0), sh - 1), re = min(max(ytab[yl].x + 1, 0), sh - 1);
+    const int nrows = re - rs + 1, span = ce - cs + 1;
+    const int ndw = pitch / 4;  // dwords per LDS row (covers 3 + span bytes)
     int sstride;
     const uint8_t* S = level_plane(P, g, f, l - 1, sstride);
     uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l];
-    int2 xt = xtab[dx], yt = ytab[dy];
-    int sx = xt.x, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
-    int sy0 = min(max(yt.x, 0), sh - 1), sy1 = min(max(yt.x + 1, 0), sh - 1);
-    int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
-    const uint8_t* r0 = S + (long long)sy0 * sstride;
-    const uint8_t* r1 = S + (long long)sy1 * sstride;
-    int t0, t1;
-    if (sx + 1 < sw) {
-        t0 = r0[sx] * a0 + r0[sx + 1] * a1;
-        t1 = r1[sx] * a0 + r1[sx + 1] * a1;
-    } else {
-        t0 = r0[sx] * 2048;
-        t1 = r1[sx] * 2048;
+    // this thread's table entries, fetched alongside the source rows
+    const int x = X0 + (tid & 63), yb = Y0 + 4 * (tid >> 6);
+    const int2 xt = xtab[min(x, xl)];
+    int2 yts[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) yts[i] = ytab[min(yb + i, yl)];
+    for (int i0 = 0; i0 < nrows * ndw; i0 += 256 * 4) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + 256 * k + tid;
+            const int r = i / ndw, q = i - r * ndw;
+            v[k] = 0;
+            if (r < nrows) {
+                const uintptr_t a = (uintptr_t)(S + (long long)(rs + r) * sstride + cs);
+                if (4 * q < (int)(a & 3) + span)  // only dwords that hold a needed byte
+                    v[k] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int i = i0 + 256 * k + tid;
+            if (i < nrows * ndw) rs_lds[i] = v[k];
+        }
     }
-    int v = (((b0 * (t0 >> 4)) >> 16) + ((b1 * (t1 >> 4)) >> 16) + 2) >> 2;
-    D[(long long)dy * dw + dx] = (uint8_t)min(max(v, 0), 255);
+    for (int r = tid; r < nrows; r += 256) rsh[r] = (uint8_t)((uintptr_t)(S + (long long)(rs + r) * sstride + cs) & 3);
+    __syncthreads();
+    // thread: column X0 + (tid & 63), rows Y0 + 4 (tid >> 6) .. +3 (a wave stores 64 consecutive bytes)
+    if (x > xl) return;
+    const int sx = xt.x, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
+    const bool two = sx + 1 < sw;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int y = yb + i;
+        if (y > yl) break;
+        const int2 yt = yts[i];
+        const int r0 = min(max(yt.x, 0), sh - 1) - rs, r1 = min(max(yt.x + 1, 0), sh - 1) - rs;
+        const int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
+        const uint8_t* s0 = src + r0 * pitch + rsh[r0] + (sx - cs);
+        const uint8_t* s1 = src + r1 * pitch + rsh[r1] + (sx - cs);
+        int t0, t1;
+        if (two) {
+            t0 = s0[0] * a0 + s0[1] * a1;
+            t1 = s1[0] * a0 + s1[1] * a1;
+        } else {
+            t0 = s0[0] * 2048;
+            t1 = s1[0] * 2048;
+        }
+        const int v = (((b0 * (t0 >> 4)) >> 16) + ((b1 * (t1 >> 4)) >> 16) + 2) >> 2;
+        D[(long long)y * dw + x] = (uint8_t)min(max(v, 0), 255);
+    }
 }
 
 // -------------------------------------------------------------- FAST-9
@@ -725,6 +772,7 @@ struct gf_extractor {
     uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
     int2 *d_xtab = nullptr, *d_ytab = nullptr;
     std::vector<long long> xtab_off, ytab_off;
+    std::vector<int> rs_pitch, rs_rows, rs_tiles_x, rs_tiles;
     CellInfo* d_cells = nullptr;
     uint32_t *d_lists = nullptr, *d_lvl = nullptr;
     int *d_counts = nullptr, *d_lvl_counts = nullptr;
@@ -990,8 +1038,35 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     std::vector<int2> xall, yall, xt, yt;
     ex->xtab_off.assign(nlevels, 0);
     ex->ytab_off.assign(nlevels, 0);
+    ex->rs_pitch.assign(nlevels, 0);
+    ex->rs_rows.assign(nlevels, 0);
+    ex->rs_tiles_x.assign(nlevels, 0);
+    ex->rs_tiles.assign(nlevels, 0);
     for (int l = 1; l < nlevels; l++) {
         resize_tables(g.w[l - 1], g.h[l - 1], g.w[l], g.h[l], xt, yt);
+        {  // LDS geometry of k_resize's tiles: widest column span, most source rows
+            const int sw = g.w[l - 1], sh = g.h[l - 1], dw = g.w[l], dh = g.h[l];
+            int maxspan = 1, maxrows = 1;
+            for (int X0 = 0; X0 < dw; X0 += RS_W) {
+                const int xl = std::min(X0 + RS_W - 1, dw - 1);
+                maxspan = std::max(maxspan, std::min(xt[xl].x + 1, sw - 1) - xt[X0].x + 1);
+            }
+            for (int Y0 = 0; Y0 < dh; Y0 += RS_H) {
+                const int yl = std::min(Y0 + RS_H - 1, dh - 1);
+                const int rs = std::min(std::max(yt[Y0].x, 0), sh - 1), re = std::min(std::max(yt[yl].x + 1, 0), sh - 1);
+                maxrows = std::max(maxrows, re - rs + 1);
+            }
+            ex->rs_pitch[l] = ((maxspan + 3) + 3) / 4 * 4;
+            ex->rs_rows[l] = maxrows;
+            ex->rs_tiles_x[l] = (dw + RS_W - 1) / RS_W;
+            ex->rs_tiles[l] = ex->rs_tiles_x[l] * ((dh + RS_H - 1) / RS_H);
+            const size_t lds = (size_t)ex->rs_pitch[l] * maxrows + maxrows;
+            if (lds > 64 * 1024) {
+                free_extractor(ex);
+                delete ex;
+                return gf::fail(GF_ERR_UNSUPPORTED, "scale factor too large for the resize tile");
+            }
+        }
         ex->xtab_off[l] = (long long)xall.size();
         ex->ytab_off[l] = (long long)yall.size();
         xall.insert(xall.end(), xt.begin(), xt.end());
@@ -1050,8 +1125,10 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     {
         GF_PROF(ctx, s, "k_resize");
         for (int l = 1; l < ex->nlevels; l++) {
-            dim3 blk(64, 4), grd((g.w[l] + 63) / 64, (g.h[l] + 3) / 4, nframes);
-            k_resize<<<grd, blk, 0, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l], ex->d_ytab + ex->ytab_off[l]);
+            const size_t lds = (size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l];
+            k_resize<<<dim3(ex->rs_tiles[l], nframes), 256, lds, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l],
+                                                                      ex->d_ytab + ex->ytab_off[l], ex->rs_tiles_x[l],
+                                                                      ex->rs_pitch[l], ex->rs_rows[l]);
         }
     }
     {
