@@ -193,7 +193,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="independent streams per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="independent streams per GPU")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
