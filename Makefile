@@ -30,7 +30,7 @@ build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 $(LIB): $(HIPOBJS) $(CPPOBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
-$(ORCLIB): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h include/gfslam/abi.h
+$(ORCLIB): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h $(CSRC)/libm_sincosf.h include/gfslam/abi.h
 	$(CXX) $(ORCFLAGS) -shared $(ORCSRCS) -o $@
 
 clean:

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "common.h"
+#include "libm_sincosf.h"
 #include "orb_pattern.h"
 #include "select.h"
 
@@ -715,7 +716,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     {
         const float factorPI = (float)(M_PI / 180.f);
         const float ang = angle * factorPI;
-        const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+        const float a = gflibm::cosf(ang), b = gflibm::sinf(ang);  // glibc cosf/sinf (ORBextractor.cc:167)
         const int byte = lane >> 1, hi = lane & 1;
         int t[8];
 #pragma unroll

@@ -304,14 +304,15 @@ static float ic_angle(const Image& im, int cx, int cy, const int* umax) {
 }
 
 // ---------------------------------------------------------------- E6 rBRIEF
-// computeOrbDescriptor, ORBextractor.cc:162-201. cos/sin are taken as
-// (float)cos((double)angle) (shared with the device). Pixels
+// computeOrbDescriptor, ORBextractor.cc:162-201. `(float)cos(angle)` of a
+// float under `using namespace std` (:75, :167) is the C library's cosf/sinf:
+// called here as such (glibc; the device restates its algorithm). Pixels
 // outside the level interior come from the unblurred reflect-101 border
 // (GaussianBlur writes only the ROI of the bordered level, :842).
 static void orb_descriptor(const KP& kp, const Image& blurred, const Image& level, uint8_t* desc) {
     const float factorPI = (float)(M_PI / 180.f);
     float angle = kp.angle * factorPI;
-    float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+    float a = ::cosf(angle), b = ::sinf(angle);
     int cx = cv_round(kp.x), cy = cv_round(kp.y);
     auto value = [&](int idx) -> int {
         float px = (float)kOrbPattern31[2 * idx], py = (float)kOrbPattern31[2 * idx + 1];

@@ -89,3 +89,17 @@ def test_golden_extraction_fixture():
         assert len(k) == case["n"]
         assert hashlib.sha256(k.tobytes()).hexdigest() == case["kps_sha256"]
         assert hashlib.sha256(d.tobytes()).hexdigest() == case["desc_sha256"]
+
+
+def test_device_sincosf_restatement_matches_libm():
+    """rBRIEF's cos/sin are glibc cosf/sinf (ORBextractor.cc:75, :167). The
+    device restatement (csrc/libm_sincosf.h) is compiled into the oracle
+    library for the host and compared with the C library on every float of
+    [0, 2pi], the range of keypoint angles in radians."""
+    import ctypes
+    ns, nc, n = ctypes.c_longlong(), ctypes.c_longlong(), ctypes.c_longlong()
+    fn = O.orc().orc_libm_sincosf_mismatches
+    fn.argtypes = [ctypes.c_float, ctypes.c_float] + [ctypes.POINTER(ctypes.c_longlong)] * 3
+    assert fn(0.0, 6.2832, ctypes.byref(ns), ctypes.byref(nc), ctypes.byref(n)) == 0
+    assert n.value > 1_000_000_000
+    assert ns.value == 0 and nc.value == 0, (ns.value, nc.value)
