@@ -320,6 +320,60 @@ def synth_vocabulary(seed: int = 7, k: int = 10, L: int = 3, flip: int = 40, sto
             "desc": np.ascontiguousarray(np.stack(desc), np.uint8), "weight": weight, "is_leaf": lv.astype(np.uint8)}
 
 
+def synth_vocabulary_fast(seed: int = 7, k: int = 10, L: int = 6, stop_frac: float = 0.02) -> dict:
+    """ORBvoc-sized tree (k = 10, L = 6: 1,111,111 nodes, ~50 MB) in the loaders'
+    breadth-first node order, vectorised level by level: a child is its parent
+    with each bit flipped with probability 1/8 (AND of three random bytes).
+    Used for the start-up vocabulary broadcast (bench.py); the tests use the
+    smaller synth_vocabulary."""
+    rng = np.random.default_rng(seed)
+    descs = [np.zeros((1, 32), np.uint8)]
+    parents = [np.array([-1], np.int32)]
+    first = 0  # node id of the first node of the previous level
+    for lev in range(1, L + 1):
+        prev = descs[-1]
+        n = len(prev) * k
+        if lev == 1:
+            d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+        else:
+            m = rng.integers(0, 256, (3, n, 32), dtype=np.uint8)
+            d = np.repeat(prev, k, axis=0) ^ (m[0] & m[1] & m[2])
+        descs.append(d)
+        parents.append((first + np.arange(len(prev), dtype=np.int32)).repeat(k))
+        first += len(prev)
+    parent = np.concatenate(parents)
+    nn = len(parent)
+    leaf = np.zeros(nn, np.uint8)
+    leaf[nn - k ** L:] = 1
+    weight = np.zeros(nn)
+    weight[nn - k ** L:] = rng.uniform(0.5, 5.0, k ** L)
+    weight[(leaf == 1) & (rng.uniform(size=nn) < stop_frac)] = 0.0
+    return {"k": k, "L": L, "scoring": 0, "weighting": 0, "parent": parent,
+            "desc": np.ascontiguousarray(np.concatenate(descs)), "weight": weight, "is_leaf": leaf}
+
+
+def pack_vocabulary(voc: dict) -> np.ndarray:
+    """One byte blob: int32 header (k, L, scoring, weighting, nnodes, 0), then
+    parent i32, descriptors 32 B, weights f64, is_leaf u8."""
+    n = len(voc["parent"])
+    hdr = np.array([voc["k"], voc["L"], voc["scoring"], voc["weighting"], n, 0], np.int32)
+    return np.concatenate([hdr.view(np.uint8), voc["parent"].astype(np.int32).view(np.uint8),
+                           voc["desc"].reshape(-1), voc["weight"].astype(np.float64).view(np.uint8),
+                           voc["is_leaf"].astype(np.uint8)])
+
+
+def unpack_vocabulary(blob: np.ndarray) -> dict:
+    hdr = blob[:24].view(np.int32)
+    n = int(hdr[4])
+    o = 24
+    parent = blob[o:o + 4 * n].view(np.int32); o += 4 * n
+    desc = blob[o:o + 32 * n].reshape(n, 32); o += 32 * n
+    weight = blob[o:o + 8 * n].view(np.float64); o += 8 * n
+    leaf = blob[o:o + n]
+    return {"k": int(hdr[0]), "L": int(hdr[1]), "scoring": int(hdr[2]), "weighting": int(hdr[3]),
+            "parent": parent.copy(), "desc": desc.copy(), "weight": weight.copy(), "is_leaf": leaf.copy()}
+
+
 def vocab_features(voc: dict, n: int, seed: int, flip: int = 20) -> np.ndarray:
     """Descriptors drawn near random leaves of the vocabulary (a frame's ORB
     features), so FeatureVector nodes hold several features."""

@@ -23,7 +23,8 @@ def _rank(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    ck = bench.share_startup_state(dist, "cpu", world, rank, nbytes=1 << 20)
+    voc, ck = bench.share_startup_state(dist, "cpu", world, rank, vocab_levels=3)
+    assert len(voc["parent"]) == 1111 and voc["desc"].shape == (1111, 32)
     t = bench.max_over_ranks(dist, "cpu", world, 1.0 + rank)
     dist.barrier()
     dist.destroy_process_group()
