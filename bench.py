@@ -286,10 +286,21 @@ def main():
                   for k, v in prof.items()}
     dom = max(prof, key=lambda k: prof[k][0])
     avg_s = prof[dom][0] / prof[dom][1] / 1e3
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of this code
+    # (profiles/r01/pmc_traffic.json, scripts/pmc_extract.sh), when taken at this batch
+    traffic = None
+    try:
+        pmc = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
+                                          "pmc_traffic.json")))
+        if pmc.get("batch") == B and dom in pmc.get("kernels", {}):
+            traffic = round(pmc["kernels"][dom]["traffic_bytes"])
+    except (OSError, ValueError, KeyError):
+        traffic = None
     if dom in per_launch_bytes:
         achieved = per_launch_bytes[dom] / avg_s / 1e9
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 5), "traffic": None,
+                "frac": round(achieved / 8000.0, 5), "traffic": traffic,
+                "traffic_source": "profiles/r01/pmc_traffic.json (FETCH_SIZE+WRITE_SIZE per launch)" if traffic else None,
                 "algorithmic_bytes_per_launch": per_launch_bytes[dom], "frames_per_launch": B,
                 "avg_launch_ms": round(avg_s * 1e3, 4)}
     else:
