@@ -234,6 +234,34 @@ __device__ int fast_score(int v, const int c[16], int th) {
     return 0x100 | ((-b0 - 1) & 0xff);
 }
 
+// The same test and score in closed form, branch-free on packed 16-bit pairs.
+// With d_k = v - c_k, OpenCV's cornerScore<16> returns
+// max(th, D, B) - 1 where D = max over the 16 arcs of 9 of min_arc d and
+// B = max over arcs of min_arc (-d) (its early-outs only skip arcs that cannot
+// raise the maximum), and the segment test at th passes exactly when
+// max(D, B) > th. So M = max(D, B) gives both: corner iff M > th, score
+// M - 1. (d, -d) share one register; the 9-wide circular minimum is
+// min(m8[k], d[k+8]) with m8 built by doubling (v_pk_min_i16 / v_pk_max_i16).
+typedef short gf_s2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int fast_max_arc(int v, const int c[16]) {
+    gf_s2 p[16], m2[16], m4[16], m8[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        p[k].x = (short)(v - c[k]);
+        p[k].y = (short)(c[k] - v);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(p[k], p[(k + 1) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) m8[k] = __builtin_elementwise_min(m4[k], m4[(k + 4) & 15]);
+    gf_s2 mx = __builtin_elementwise_min(m8[0], p[8]);
+#pragma unroll
+    for (int k = 1; k < 16; k++) mx = __builtin_elementwise_max(mx, __builtin_elementwise_min(m8[k], p[(k + 8) & 15]));
+    return max((int)mx.x, (int)mx.y);
+}
+
 // Exclusive scan of one int per thread across a 256-thread workgroup.
 __device__ int block_scan_256(int v, int* tmp, int& total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -297,7 +325,8 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     __shared__ int s_nc;
     const int f = blockIdx.y, tid = threadIdx.x;
     int t = blockIdx.x, l = 0;
-    while (l + 1 < g.nlevels && t >= g.tile_begin[l + 1]) l++;
+#pragma unroll
+    for (int i = 1; i < GF_MAX_LEVELS; i++) l += (i < g.nlevels && t >= g.tile_begin[i]) ? 1 : 0;
     t -= g.tile_begin[l];
     const int tx = t % g.tiles_x[l], ty = t / g.tiles_x[l];
     const int w = g.w[l], h = g.h[l];
@@ -394,8 +423,8 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         const int q = cand[i], py = q >> 6, px = q & 63;
         int c[16];
         circle_vals(&src[0][0], BT_SW, px + 4, py + 3, c);
-        const int fs = fast_score(src[py + 3][px + 4], c, map_th);
-        SC[(long long)(Y0 + py) * w + X0 + px] = (fs & 0x100) ? (uint8_t)((fs & 0xff) + 1) : 0;
+        const int M = fast_max_arc(src[py + 3][px + 4], c);  // corner iff M > th; map entry S + 1 = M
+        SC[(long long)(Y0 + py) * w + X0 + px] = M > map_th ? (uint8_t)M : 0;
     }
 }
 
@@ -644,14 +673,17 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     const int lane = threadIdx.x & 63;
     DescLds& W = sh_all[threadIdx.x >> 6];
     const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    int cnt[GF_MAX_LEVELS];  // all level counts in one batch of loads
+#pragma unroll
+    for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = i < g.nlevels ? lvl_counts[(long long)f * g.nlevels + i] : 0;
     int total = 0, l = -1, idx = 0;
-    for (int i = 0; i < g.nlevels; i++) {
-        int c = lvl_counts[(long long)f * g.nlevels + i];
-        if (l < 0 && k < total + c) {
+#pragma unroll
+    for (int i = 0; i < GF_MAX_LEVELS; i++) {
+        if (l < 0 && i < g.nlevels && k < total + cnt[i]) {
             l = i;
             idx = k - total;
         }
-        total += c;
+        total += cnt[i];
     }
     if (k == 0 && lane == 0) out_counts[f] = total;
     if (l < 0) return;
