@@ -6,7 +6,7 @@
 //
 //   k_resize  x (nlevels-1)  level l from level l-1 (cv::resize INTER_LINEAR,
 //                            11-bit fixed point; ComputePyramid :922-998)
-//   k_blur_fast              one 64x16 tile per workgroup: 7x7 sigma-2
+//   k_blur_fast              one 64x32 tile per workgroup: 7x7 sigma-2
 //                            Gaussian of every level (:842) and, from the same
 //                            LDS tile, the FAST-9 score map of the level
 //   k_fast_cells             one workgroup per (frame, grid cell): corners of
@@ -281,7 +281,7 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 }
 
 // -------------------------------------------------------------- k_blur_fast
-// One 64x16 tile of one level per 256-thread workgroup, its 3-px halo staged
+// One 64x32 tile of one level per 256-thread workgroup, its 3-px halo staged
 // in LDS once and used twice:
 //   * GaussianBlur 7x7 sigma 2 (reflect-101 border; ORBextractor.cc:842):
 //     integer row pass, column pass with the (s + 2^15) >> 16 cast;
@@ -301,10 +301,11 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 // with v_alignbyte (two loads per dword, all in flight together); border
 // tiles load bytes through reflect-101. The row pass makes four outputs from
 // three LDS dwords with v_dot4_u32_u8 (two per output: the 7 taps are bytes).
-// Thread t then owns column t & 63 and rows 4 (t >> 6) .. +3 of the tile for
+// Thread t then owns column t & 63 and rows BT_RPT (t >> 6) .. +BT_RPT-1 for
 // the column pass, the compass test and the stores.
 #define BT_W 64
-#define BT_H 16
+#define BT_H 32
+#define BT_RPT (BT_H / 4)  // rows per thread in the column pass
 #define BT_R (BT_H + 6)   // source rows
 #define BT_SW (BT_W + 8)  // source row: 72 bytes = 18 dwords, x = X0 - 4 .. X0 + 67
 
@@ -400,12 +401,12 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     }
     __syncthreads();
     const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
-    const int cx = tid & 63, ry0 = (tid >> 6) * 4, x = X0 + cx;
-    int rv[10];
+    const int cx = tid & 63, ry0 = (tid >> 6) * BT_RPT, x = X0 + cx;
+    int rv[BT_RPT + 6];
 #pragma unroll
-    for (int k = 0; k < 10; k++) rv[k] = rows[ry0 + k][cx];
+    for (int k = 0; k < BT_RPT + 6; k++) rv[k] = rows[ry0 + k][cx];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
+    for (int r = 0; r < BT_RPT; r++) {
         const int y = Y0 + ry0 + r;
         if (y >= h || x >= w) continue;
         const int sum = k0 * (rv[r] + rv[r + 6]) + k1 * (rv[r + 1] + rv[r + 5]) + k2 * (rv[r + 2] + rv[r + 4]) +
