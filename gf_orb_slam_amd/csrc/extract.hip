@@ -445,7 +445,9 @@ __device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buf
     return S >= th ? S : 0;
 }
 
-__device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, uint32_t* bits, int dw, int dh, int th) {
+// sc: the window rows as loaded (row y at byte y * pitch + rsh[y]).
+__device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* rsh, int pitch, uint32_t* bits, int dw,
+                                             int dh, int th) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ya = wv * dh / 4, yb = (wv + 1) * dh / 4;
     int cnt = 0;
@@ -453,18 +455,21 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, uint32_t* bits, 
         const int x = x0 + lane;
         const bool col = x < dw;
         auto rd = [&](int y, int xx) -> int {
-            return (col && y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * dw + xx], th) : 0;
+            return (col && y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * pitch + rsh[y] + xx], th) : 0;
         };
         int u0 = rd(ya - 1, x - 1), u1 = rd(ya - 1, x), u2 = rd(ya - 1, x + 1);
         int c0 = rd(ya, x - 1), c1 = rd(ya, x), c2 = rd(ya, x + 1);
+        int d0 = rd(ya + 1, x - 1), d1 = rd(ya + 1, x), d2 = rd(ya + 1, x + 1);
         for (int y = ya; y < yb; y++) {
-            const int d0 = rd(y + 1, x - 1), d1 = rd(y + 1, x), d2 = rd(y + 1, x + 1);
+            // row y + 2 is read one step ahead, so its LDS latency overlaps this step
+            const int e0 = rd(y + 2, x - 1), e1 = rd(y + 2, x), e2 = rd(y + 2, x + 1);
             const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
             const bool keep = c1 != 0 && c1 > mx;
             if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
             cnt += __popcll(__ballot(keep));
             u0 = c0, u1 = c1, u2 = c2;
             c0 = d0, c1 = d1, c2 = d2;
+            d0 = e0, d1 = e1, d2 = e2;
         }
     }
     return cnt;  // this wave's survivors
@@ -485,33 +490,35 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
         return;
     }
     const int n = dw * dh, nwords = (n + 31) >> 5;
-    uint8_t* sc = smem;                                          // dw x dh map entries
-    uint32_t* bits = reinterpret_cast<uint32_t*>(smem + ((n + 15) & ~15));  // survivor bits
+    const int ndw = (dw + 6) >> 2, pitch = 4 * ndw;  // dwords per row: dw bytes at any alignment
+    uint8_t* sc = smem;                                                   // dh x pitch
+    uint8_t* rsh = sc + dh * pitch;                                        // dh row shifts
+    uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 15) & ~15));  // survivor bits
     const int l = ci.level, lw = g.w[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
-    // the window: every load of a 16-deep batch in flight before its LDS writes
-    {
-        int y = tid / dw, x = tid - y * dw;
-        for (int p0 = 0; p0 < n; p0 += 256 * 16) {
-            uint8_t v[16];
-            int yy = y, xx = x;
+    // the window as aligned dwords, 16 loads per thread in flight before the LDS writes
+    for (int i0 = 0; i0 < dh * ndw; i0 += 256 * 16) {
+        uint32_t v[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (p0 + 256 * k + tid < n) v[k] = SC[(long long)yy * lw + xx];
-                xx += 256;
-                while (xx >= dw) xx -= dw, yy++;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (p0 + 256 * k + tid < n) sc[y * dw + x] = v[k];
-                x += 256;
-                while (x >= dw) x -= dw, y++;
+        for (int k = 0; k < 16; k++) {
+            const int i = i0 + 256 * k + tid;
+            const int r = i / ndw, q = i - r * ndw;
+            v[k] = 0;
+            if (r < dh) {
+                const uintptr_t a = (uintptr_t)(SC + (long long)r * lw);
+                if (4 * q < (int)(a & 3) + dw) v[k] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
             }
         }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int i = i0 + 256 * k + tid;
+            if (i < dh * ndw) reinterpret_cast<uint32_t*>(sc)[i] = v[k];
+        }
     }
+    for (int r = tid; r < dh; r += 256) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)r * lw) & 3);
     for (int i = tid; i < nwords; i += 256) bits[i] = 0;
     __syncthreads();
-    int c = cell_nms_bits(sc, bits, dw, dh, fast_th);
+    int c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, fast_th);
     if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
     __syncthreads();
     int total = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
@@ -519,7 +526,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
         __syncthreads();
         for (int i = tid; i < nwords; i += 256) bits[i] = 0;
         __syncthreads();
-        c = cell_nms_bits(sc, bits, dw, dh, min_th);
+        c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, min_th);
         if ((tid & 63) == 0) s_cnt[1][tid >> 6] = c;
         __syncthreads();
         total = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
@@ -536,7 +543,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
             const int p = 32 * i + __ffs(word) - 1;
             word &= word - 1;
             const int y = p / dw, x = p - y * dw;
-            out[off++] = ((uint32_t)(sc[p] - 1) << 24) | ((uint32_t)(Y0 + y) << 12) | (uint32_t)(X0 + x);
+            out[off++] = ((uint32_t)(sc[y * pitch + rsh[y] + x] - 1) << 24) | ((uint32_t)(Y0 + y) << 12) |
+                         (uint32_t)(X0 + x);
         }
         base += tot;
     }
@@ -934,7 +942,8 @@ static int plan_extractor(gf_extractor* ex) {
                         ci.cap_off = cap_off;
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
-                        size_t lds = (((size_t)dw * dh + 15) & ~(size_t)15) + 4 * (((size_t)dw * dh + 31) / 32);
+                        size_t lds = (size_t)dh * (4 * (size_t)((dw + 6) / 4)) + (((size_t)dh + 15) & ~(size_t)15) +
+                                     4 * (((size_t)dw * dh + 31) / 32);
                         max_lds = std::max(max_lds, lds);
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
                                  GF_ERR_ARG, "cell ROI outside level");
