@@ -22,6 +22,7 @@ namespace {
 constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
 constexpr int PO_CHI = 27;
 constexpr int PO_STRIDE_MAX = 8192;
+constexpr int PO_LDS_EDGES = 1024;  // problems up to this size keep edges and residuals in LDS
 
 struct PoseArgs {
     const gf_pose_edge* edges;
@@ -133,14 +134,28 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
 __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
     __shared__ double term[PO_NACC][65];
     __shared__ double sh_sum[PO_NACC];
+    // every pass re-reads each edge and its residuals: for problems up to
+    // PO_LDS_EDGES edges they live in LDS (generic pointers), else in HBM
+    __shared__ gf_pose_edge sh_edges[PO_LDS_EDGES];
+    __shared__ double sh_res[3][PO_LDS_EDGES];
     const int p = blockIdx.x;
     Lane L;
     L.l = threadIdx.x;
     L.n = min(max(A.nedges[p], 0), A.stride);
-    L.E = A.edges + (size_t)p * A.stride;
-    L.e0 = A.work + (size_t)p * A.stride * 3;
-    L.e1 = L.e0 + A.stride;
-    L.info = L.e1 + A.stride;
+    if (L.n <= PO_LDS_EDGES) {
+        const gf_pose_edge* src = A.edges + (size_t)p * A.stride;
+        for (int e = L.l; e < L.n; e += 64) sh_edges[e] = src[e];
+        L.E = sh_edges;
+        L.e0 = sh_res[0];
+        L.e1 = sh_res[1];
+        L.info = sh_res[2];
+        __syncthreads();
+    } else {
+        L.E = A.edges + (size_t)p * A.stride;
+        L.e0 = A.work + (size_t)p * A.stride * 3;
+        L.e1 = L.e0 + A.stride;
+        L.info = L.e1 + A.stride;
+    }
     L.fx = A.fx;
     L.fy = A.fy;
     L.cx = A.cx;
