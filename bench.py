@@ -206,7 +206,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="independent streams per GPU")
+    ap.add_argument("--batch", type=int, default=512, help="independent streams per GPU")
+    ap.add_argument("--groups", type=int, default=2,
+                    help="stream groups per GPU, each on its own HIP stream (their kernels overlap)")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
@@ -232,11 +234,21 @@ def main():
     cam = args.camera
     w, h = synth.CAMERAS[cam][:2]
     B = args.batch
-    fe = FrontEnd(cam, args.nfeatures, B, 2000, gf_budget=args.gf_budget, seed=rank)
-    frames = np.stack([synth.synth_frame(w, h, synth.frame_seed(rank * B + b, 0)) for b in range(min(B, 8))])
-    frames = frames[np.arange(B) % len(frames)]
-    fe.load_frames(frames)
-    fe.build_maps()
+    G = max(1, args.groups)
+    if B % G:
+        raise SystemExit(f"--batch {B} must be a multiple of --groups {G}")
+    Bg = B // G
+    # G groups of B/G streams, each a FrontEnd with its own context and HIP
+    # stream: their kernels overlap, so one group's latency-bound stages (pose
+    # LM, active matching) run beside another group's extraction
+    fes = []
+    for g in range(G):
+        fe = FrontEnd(cam, args.nfeatures, Bg, 2000, gf_budget=args.gf_budget, seed=rank * G + g)
+        base = rank * B + g * Bg
+        frames = np.stack([synth.synth_frame(w, h, synth.frame_seed(base + b, 0)) for b in range(min(Bg, 8))])
+        fe.load_frames(frames[np.arange(Bg) % len(frames)])
+        fe.build_maps()
+        fes.append(fe)
 
     # one-off exchange before timing: rank 0 broadcasts the ORB vocabulary (RCCL over xGMI)
     t_bc = time.perf_counter()
@@ -249,40 +261,57 @@ def main():
                "broadcast_s": round(t_bc, 3), "checksum": voc_ck}
 
     for _ in range(args.warmup):
-        fe.step()
-    fe.sync()
+        for fe in fes:
+            fe.step()
+    for fe in fes:
+        fe.sync()
     torch.cuda.synchronize()
-    fe.prof_enable(True)
-    fe.prof_reset()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        fe.step()
-    fe.sync()
+        for fe in fes:
+            fe.step()
+    for fe in fes:
+        fe.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    prof = fe.prof_report()
-    fe.prof_enable(False)
     dt = max_over_ranks(dist, "cuda", world, dt)
+
+    # per-kernel times from a separate pass with the groups serialised (HIP
+    # events on each launch's stream), so overlap does not stretch them
+    prof_steps = max(1, min(args.steps, 10))
+    prof = {}
+    for fe in fes:
+        fe.prof_enable(True)
+        fe.prof_reset()
+        for _ in range(prof_steps):
+            fe.step()
+        fe.sync()
+        for k, (ms, cnt) in fe.prof_report().items():
+            a = prof.setdefault(k, [0.0, 0])
+            a[0] += ms
+            a[1] += cnt
+        fe.prof_enable(False)
+    fe = fes[0]
 
     frames_total = world * B * args.steps
     fps = frames_total / dt
-    nk = fe.nkp.float().mean().item()
-    iters = fe.iters.cpu().numpy().astype(np.float64)      # [2][B] LM iterations (last step)
-    nedges = fe.nedges.cpu().numpy().astype(np.float64)    # [2][B] edges per problem
-    n_active = fe.n_active.float().mean().item()
-    ninl = fe.ninl.float().mean().item()
+    nk = float(np.mean([f.nkp.float().mean().item() for f in fes]))
+    iters = np.concatenate([f.iters.cpu().numpy() for f in fes], axis=1).astype(np.float64)   # [2][B] LM iterations
+    nedges = np.concatenate([f.nedges.cpu().numpy() for f in fes], axis=1).astype(np.float64)  # [2][B] edges
+    n_active = float(np.mean([f.n_active.float().mean().item() for f in fes]))
+    ninl = float(np.mean([f.ninl.float().mean().item() for f in fes]))
 
     # algorithmic bytes per launch for the kernels with a §8(d) formula
     kb = kernel_bytes(cam, args.nfeatures)
-    per_launch_bytes = {k: kb[k] * B for k in ("k_resize", "k_blur_fast", "k_describe")}
+    per_launch_bytes = {k: kb[k] * Bg for k in ("k_resize", "k_blur_fast", "k_describe")}
     # pose LM: N_e * 40 B per LM iteration per problem, summed over the launch
-    per_launch_bytes["k_pose_opt"] = float((nedges * iters).sum(axis=1).mean() * 40.0)
-    per_kernel = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "ms_per_step": v[0] / args.steps}
+    per_launch_bytes["k_pose_opt"] = float((nedges * iters).sum(axis=1).mean() * 40.0) / G
+    per_kernel = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "ms_per_step": v[0] / prof_steps}
                   for k, v in prof.items()}
     dom = max(prof, key=lambda k: prof[k][0])
     avg_s = prof[dom][0] / prof[dom][1] / 1e3
@@ -292,7 +321,7 @@ def main():
     try:
         pmc = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
                                           "pmc_traffic.json")))
-        if pmc.get("batch") == B and dom in pmc.get("kernels", {}):
+        if pmc.get("batch") == Bg and dom in pmc.get("kernels", {}):
             traffic = round(pmc["kernels"][dom]["traffic_bytes"])
     except (OSError, ValueError, KeyError):
         traffic = None
@@ -301,13 +330,13 @@ def main():
         roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(achieved / 8000.0, 5), "traffic": traffic,
                 "traffic_source": "profiles/r01/pmc_traffic.json (FETCH_SIZE+WRITE_SIZE per launch)" if traffic else None,
-                "algorithmic_bytes_per_launch": per_launch_bytes[dom], "frames_per_launch": B,
+                "algorithmic_bytes_per_launch": per_launch_bytes[dom], "frames_per_launch": Bg,
                 "avg_launch_ms": round(avg_s * 1e3, 4)}
     else:
         roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
                 "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)}
     ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe") if k in prof)
-    ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
+    ext_bw = kb["extract_total"] * B * prof_steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
     pose_ms = prof.get("k_pose_opt", (0.0, 1))
     pose_avg_ms = pose_ms[0] / max(pose_ms[1], 1)
     mean_iters = float(iters.mean())
@@ -326,18 +355,20 @@ def main():
         "dtype": "u8/int32 (extract, match), f64 (GF, pose LM)",
         "data": "synthetic (seeded 752x480 frames + synthetic 2000-point local maps; no dataset reachable)",
         "config": {"workload": f"config 2: {cam} {w}x{h}, {args.nfeatures} feats, GF budget {args.gf_budget}, "
-                               f"{B} streams/GPU; step = extract + motion model + SearchByProjection(last frame) + "
+                               f"{B} streams/GPU in {G} groups; step = extract + motion model + SearchByProjection(last frame) + "
                                f"PoseOptimization + G1-G7 active map matching + PoseOptimization",
-                   "streams_per_gpu": B, "parallelism": f"streams x {world} ranks"},
+                   "streams_per_gpu": B, "stream_groups": G, "parallelism": f"{B} streams x {world} ranks"},
         "startup": startup,
         "roofline": roof,
         "pose_opt": {"ms_per_iter": round(pose_avg_ms / max(mean_iters, 1e-9), 5),
-                     "ms_per_iter_per_problem": round(pose_avg_ms / max(mean_iters * B, 1e-9), 6),
+                     "ms_per_iter_per_problem": round(pose_avg_ms / max(mean_iters * Bg, 1e-9), 6),
                      "avg_launch_ms": round(pose_avg_ms, 4), "mean_iterations": round(mean_iters, 2),
                      "mean_edges": [round(float(x), 1) for x in nedges.mean(axis=1)],
                      "note": "ms_per_iter = launch time / mean LM iterations (all B problems run concurrently)"},
-        "extraction_stage": {"ms_per_frame": round(ext_ms / (B * args.steps), 5),
+        "extraction_stage": {"ms_per_frame": round(ext_ms / (B * prof_steps), 5),
                              "algorithmic_GBps": round(ext_bw, 2) if ext_bw else None},
+        "kernels_note": f"HIP events per launch in a separate pass of {prof_steps} steps with the groups serialised; "
+                        f"each launch covers one group ({Bg} streams)",
         "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
                         "ms_per_step": round(v["ms_per_step"], 4)} for k, v in per_kernel.items()},
         "avg_keypoints": nk,

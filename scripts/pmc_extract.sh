@@ -7,7 +7,7 @@ B=${B:-256}
 mkdir -p $R/gpurun_out/$TAG
 export TMPDIR=/tmp
 cd /tmp
-ARGS="$R/bench.py --batch $B --steps 5 --warmup 2 --no-cpu-baseline --lba-batch 0 --single-stream-steps 0"
+ARGS="$R/bench.py --batch $B --groups 1 --steps 5 --warmup 2 --no-cpu-baseline --lba-batch 0 --single-stream-steps 0"
 i=0
 for CTRS in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
             "FETCH_SIZE" "WRITE_SIZE" ${EXTRA_PASSES}; do
