@@ -673,15 +673,23 @@ struct DescLds {
     uint8_t ic_sh[DS_IC], bl_sh[DS_BL];
 };
 
+// Two keypoints per wave, one per 32-lane half: the halves' loads go out in
+// the same batch, so a wave covers two keypoints with the same two round trips.
+__device__ __forceinline__ int half_sum(int v) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);  // xor < 32 stays inside the half
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const uint32_t* __restrict__ lvl_lists,
                                                   long long lvl_stride, const int* __restrict__ lvl_counts,
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
-    __shared__ DescLds sh_all[4];
+    __shared__ DescLds sh_all[8];
     const int f = blockIdx.y;
-    const int lane = threadIdx.x & 63;
-    DescLds& W = sh_all[threadIdx.x >> 6];
-    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, hl = lane & 31, half = (threadIdx.x >> 5);  // half = slot 0..7
+    DescLds& W = sh_all[half];
+    const int k = blockIdx.x * 8 + half;
     int cnt[GF_MAX_LEVELS];  // all level counts in one batch of loads
 #pragma unroll
     for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = i < g.nlevels ? lvl_counts[(long long)f * g.nlevels + i] : 0;
@@ -694,40 +702,45 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
         }
         total += cnt[i];
     }
-    if (k == 0 && lane == 0) out_counts[f] = total;
-    if (l < 0) return;
-    const uint32_t e = lvl_lists[(long long)f * lvl_stride + g.lvl_off[l] + idx];
+    if (k == 0 && hl == 0) out_counts[f] = total;
+    if (__ballot(l >= 0) == 0) return;  // whole wave past the last keypoint
+    const bool live = l >= 0;
+    const int lv = live ? l : 0;
+    const uint32_t e = live ? lvl_lists[(long long)f * lvl_stride + g.lvl_off[lv] + idx] : 0u;
     const int x = e & 0xfff, y = (e >> 12) & 0xfff, score = e >> 24;
-    const int w = g.w[l], h = g.h[l];
+    const int w = g.w[lv], h = g.h[lv];
     int stride;
-    const uint8_t* Pl = level_plane(P, g, f, l, stride);
-    const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[l];
-    const bool win = x >= 18 && x + 18 < w && y >= 18 && y + 18 < h;
+    const uint8_t* Pl = level_plane(P, g, f, lv, stride);
+    const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[lv];
+    const bool win = live && x >= 18 && x + 18 < w && y >= 18 && y + 18 < h;
 
     {  // one batch: IC rows y-15..y+15 (cols x-15..), window rows y-18..y+18 (cols x-18..)
-        uint32_t v[DS_LOADS];
+        constexpr int NL = (DS_IC * DS_ICW + DS_BL * DS_BLW + 31) / 32;
+        uint32_t v[NL];
 #pragma unroll
-        for (int t = 0; t < DS_LOADS; t++) {
-            const int i = lane + 64 * t;
+        for (int t = 0; t < NL; t++) {
+            const int i = hl + 32 * t;
             v[t] = 0;
-            if (i < DS_IC * DS_ICW) {
+            if (live && i < DS_IC * DS_ICW) {
                 const int r = i / DS_ICW, q = i - r * DS_ICW;
                 const uintptr_t a = (uintptr_t)(Pl + (long long)(y - 15 + r) * stride + x - 15);
                 v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
-            } else if (win && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
+            } else if (win && i >= DS_IC * DS_ICW && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
                 const int j = i - DS_IC * DS_ICW, r = j / DS_BLW, q = j - r * DS_BLW;
                 const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * w + x - 18);
                 v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
             }
         }
 #pragma unroll
-        for (int t = 0; t < DS_LOADS; t++) {
-            const int i = lane + 64 * t;
+        for (int t = 0; t < NL; t++) {
+            const int i = hl + 32 * t;
             if (i < DS_IC * DS_ICW) W.ic[i] = v[t];
             else if (i < DS_IC * DS_ICW + DS_BL * DS_BLW) W.bl[i - DS_IC * DS_ICW] = v[t];
         }
-        if (lane < DS_IC) W.ic_sh[lane] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + lane) * stride + x - 15) & 3);
-        if (lane < DS_BL) W.bl_sh[lane] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + lane) * w + x - 18) & 3);
+        if (hl < DS_IC) W.ic_sh[hl] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + hl) * stride + x - 15) & 3);
+        W.bl_sh[hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + hl) * w + x - 18) & 3);
+        if (hl < DS_BL - 32)
+            W.bl_sh[32 + hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + 32 + hl) * w + x - 18) & 3);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -735,56 +748,58 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     const uint8_t* ic8 = reinterpret_cast<const uint8_t*>(W.ic);
     const uint8_t* bl8 = reinterpret_cast<const uint8_t*>(W.bl);
 
-    // IC_Angle: 16 pixels of the 31x31 square per lane; pixels outside the
-    // circular patch (|u| > umax[|v|]) weigh 0. Integer moments: order-free.
+    // IC_Angle: 31 pixels of the 31x31 square per lane (row hl); pixels outside
+    // the circular patch (|u| > umax[|v|]) weigh 0. Integer moments: order-free.
     int m10 = 0, m01 = 0;
+    if (hl < 31) {
+        const int v = hl - 15, d = c_umax[v < 0 ? -v : v];
+        const uint8_t* row = ic8 + hl * (4 * DS_ICW) + W.ic_sh[hl] + 15;
+        int sum = 0;
 #pragma unroll
-    for (int t = 0; t < 16; t++) {
-        const int j = lane + 64 * t;
-        const int r = j / 31, c = j - r * 31;
-        const int v = r - 15, u = c - 15;
-        if (j < 961 && (u < 0 ? -u : u) <= c_umax[v < 0 ? -v : v]) {
-            const int p = ic8[r * (4 * DS_ICW) + W.ic_sh[r] + c];
+        for (int u = -15; u <= 15; u++) {
+            const int p = (u >= -d && u <= d) ? row[u] : 0;
+            sum += p;
             m10 += u * p;
-            m01 += v * p;
         }
+        m01 = v * sum;
     }
-    m10 = gfd::warp_sum(m10);
-    m01 = gfd::warp_sum(m01);
+    m10 = half_sum(m10);
+    m01 = half_sum(m01);
     const float angle = fast_atan2f((float)m01, (float)m10);
 
-    // rBRIEF: lane 2b + hi computes bits 4 hi .. 4 hi + 3 of descriptor byte b.
+    // rBRIEF: lane hl of the half computes descriptor byte hl (16 tests).
     {
         const float factorPI = (float)(M_PI / 180.f);
         const float ang = angle * factorPI;
         const float a = gflibm::cosf(ang), b = gflibm::sinf(ang);  // glibc cosf/sinf (ORBextractor.cc:167)
-        const int byte = lane >> 1, hi = lane & 1;
-        int t[8];
+        int val = 0;
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int pi = byte * 16 + hi * 8 + q;
-            const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
-            const int ry = __float2int_rn(px * b + py * a);
-            const int rx = __float2int_rn(px * a - py * b);
-            if (win) {
-                const int r = ry + 18;
-                t[q] = bl8[r * (4 * DS_BLW) + W.bl_sh[r] + rx + 18];
-            } else {
-                const int xx = x + rx, yy = y + ry;
-                const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
-                t[q] = inside ? B[(long long)yy * w + xx]
-                              : Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
+        for (int bit = 0; bit < 8; bit++) {
+            int t[2];
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const int pi = hl * 16 + bit * 2 + q;
+                const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
+                const int ry = __float2int_rn(px * b + py * a);
+                const int rx = __float2int_rn(px * a - py * b);
+                if (win) {
+                    const int r = ry + 18;
+                    t[q] = bl8[r * (4 * DS_BLW) + W.bl_sh[r] + rx + 18];
+                } else {
+                    const int xx = x + rx, yy = y + ry;
+                    const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
+                    t[q] = !live ? 0
+                           : inside ? B[(long long)yy * w + xx]
+                                    : Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
+                }
             }
+            val |= (t[0] < t[1]) << bit;
         }
-        int nib = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) nib |= (t[2 * q] < t[2 * q + 1]) << q;
-        const int other = __shfl_xor(nib, 1, 64);
-        if (!hi) desc[((long long)f * cap + k) * 32 + byte] = (uint8_t)(nib | other << 4);
+        if (live) desc[((long long)f * cap + k) * 32 + hl] = (uint8_t)val;
     }
-    if (lane == 0) {
+    if (live && hl == 0) {
         gf_keypoint kp;
-        float s = g.scale[l];
+        const float s = g.scale[l];
         kp.x = l ? (float)x * s : (float)x;
         kp.y = l ? (float)y * s : (float)y;
         kp.size = (float)(int)(31 * s);
@@ -1191,7 +1206,7 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     }
     {
         GF_PROF(ctx, s, "k_describe");
-        k_describe<<<dim3((ex->capacity + 3) / 4, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
+        k_describe<<<dim3((ex->capacity + 7) / 8, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
                                                                           ex->d_lvl_counts, d_kps, d_desc, d_counts,
                                                                           cap);
     }
