@@ -400,24 +400,28 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         *reinterpret_cast<int4*>(&rows[ry][4 * q]) = o;
     }
     __syncthreads();
-    const int k0 = 18, k1 = 34, k2 = 49, k3 = 55;
     const int cx = tid & 63, ry0 = (tid >> 6) * BT_RPT, x = X0 + cx;
     int rv[BT_RPT + 6];
 #pragma unroll
     for (int k = 0; k < BT_RPT + 6; k++) rv[k] = rows[ry0 + k][cx];
+    // row pointers advanced by w per row (no 64-bit multiply per store); the
+    // taps fit 24-bit multiplies (row sums < 2^17), which issue at full rate
+    const long long o0 = (long long)(Y0 + ry0) * w + x;
+    uint8_t* dp = D + o0;
+    uint8_t* sp = SC + o0;
 #pragma unroll
-    for (int r = 0; r < BT_RPT; r++) {
+    for (int r = 0; r < BT_RPT; r++, dp += w, sp += w) {
         const int y = Y0 + ry0 + r;
         if (y >= h || x >= w) continue;
-        const int sum = k0 * (rv[r] + rv[r + 6]) + k1 * (rv[r + 1] + rv[r + 5]) + k2 * (rv[r + 2] + rv[r + 4]) +
-                        k3 * rv[r + 3];
-        D[(long long)y * w + x] = (uint8_t)min(max((sum + (1 << 15)) >> 16, 0), 255);
+        const unsigned sum = __umul24(18u, (unsigned)(rv[r] + rv[r + 6])) + __umul24(34u, (unsigned)(rv[r + 1] + rv[r + 5])) +
+                             __umul24(49u, (unsigned)(rv[r + 2] + rv[r + 4])) + __umul24(55u, (unsigned)rv[r + 3]);
+        *dp = (uint8_t)min((sum + (1u << 15)) >> 16, 255u);
         const bool cand_px = x >= 3 && x < w - 3 && y >= 3 && y < h - 3 &&
                              fast_compass(&src[ry0 + r + 3][cx + 4], BT_SW, map_th);
         if (cand_px)
             cand[atomicAdd(&s_nc, 1)] = (uint16_t)((ry0 + r) * BT_W + cx);
         else
-            SC[(long long)y * w + x] = 0;
+            *sp = 0;
     }
     __syncthreads();
     for (int i = tid; i < s_nc; i += 256) {
