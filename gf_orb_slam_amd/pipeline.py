@@ -149,7 +149,8 @@ class FrontEnd:
         self.mp_uv = z(B, M, 2, dt=f32)
         self.mp_upd = torch.full((B, M), -1, dtype=i32, device=dev)
         self.mp_updated = z(B, M)
-        self.frame_id = 1
+        self.frame_id = 1  # the current frame's stamp; stamps stay relative to it (see _step_body)
+        self.graph = None
         self.rng = z(B, ctypes.sizeof(Rng), dt=u8)
         self.left = z(B, M, dt=i32)
         self.nleft = z(B, dt=i32)
@@ -306,30 +307,56 @@ class FrontEnd:
                                          self.M, ctypes.c_float(th), ctypes.c_float(nnratio), ptr(self.kp2mp),
                                          ptr(self.score), ptr(self.n_active), self._s))
 
+    def _step_body(self) -> None:
+        self.extract()
+        # TrackWithMotionModel
+        self.predict_pose()
+        self.reset_matches()
+        self.match_last_frame()
+        self.pose_optimization(0)
+        self.discard_outliers()
+        # TrackLocalMap -> SearchReferencePointsInFrustum
+        if self.gf:
+            self.frame_info()
+        self.frustum()
+        if self.gf:
+            self.map_info()
+            self.active_match()
+        else:
+            self.match_local_map()
+        self.pose_optimization(1)
+        self.discard_outliers()
+        if self.gf:
+            self.predict_next()
+        # MapPoint::updateAtFrameId stamps are kept relative to the current
+        # frame: this frame is always frame_id (1) and the next frame_id + 1, so
+        # after a step every stamp moves down by one. The kernels only compare
+        # stamps for equality with the current / next id, so this is the
+        # reference's absolute mnId bookkeeping, and a step has no per-frame
+        # host arguments (it can be captured once as a HIP graph and replayed).
+        self.mp_upd.sub_(1)
+
     def step(self) -> None:
         torch = _torch()
+        if self.graph is not None:
+            self.graph.replay()
+            return
         with torch.cuda.stream(self.stream):
-            self.extract()
-            # TrackWithMotionModel
-            self.predict_pose()
-            self.reset_matches()
-            self.match_last_frame()
-            self.pose_optimization(0)
-            self.discard_outliers()
-            # TrackLocalMap -> SearchReferencePointsInFrustum
-            if self.gf:
-                self.frame_info()
-            self.frustum()
-            if self.gf:
-                self.map_info()
-                self.active_match()
-            else:
-                self.match_local_map()
-            self.pose_optimization(1)
-            self.discard_outliers()
-            if self.gf:
-                self.predict_next()
-        self.frame_id += 1
+            self._step_body()
+
+    def capture_graph(self) -> None:
+        """Capture one step as a HIP graph (after at least one eager step, so
+        every workspace is allocated); step() replays it from then on.
+        Measured on ROCm 7.2 (scripts/overlap_exp.py): replaying per-group
+        graphs is slower than eager launches on two streams (61.6k vs 73.4k
+        frames/s at 512 streams), because the replays do not overlap across
+        streams; the bench therefore launches eagerly."""
+        torch = _torch()
+        self.sync()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=self.stream):
+            self._step_body()
+        self.graph = g  # capturing records the step without running it
 
     def reset_state(self) -> None:
         """Back to the state right after build_maps (RNG, map stamps, frame id)."""

@@ -13,6 +13,7 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 
 B, G = int(sys.argv[1]), int(sys.argv[2])
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+graphs = len(sys.argv) > 4 and sys.argv[4] == "graph"
 torch.cuda.set_device(0)
 w, h = synth.CAMERAS["euroc"][:2]
 fes = []
@@ -27,6 +28,14 @@ for _ in range(3):
         fe.step()
 for fe in fes:
     fe.sync()
+if graphs:
+    for fe in fes:
+        fe.capture_graph()
+    for _ in range(2):
+        for fe in fes:
+            fe.step()
+    for fe in fes:
+        fe.sync()
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(steps):
@@ -36,4 +45,4 @@ for fe in fes:
     fe.sync()
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
-print(f"B={B} G={G}: {B * steps / dt:.0f} fps, {dt / steps * 1e3:.3f} ms/step")
+print(f"B={B} G={G} graphs={graphs}: {B * steps / dt:.0f} fps, {dt / steps * 1e3:.3f} ms/step")
