@@ -570,13 +570,10 @@ __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
 
 // ------------------------------------------------------------------ reduced camera system
 // S = Hpp + lambda I - C (lower, packed in LDS), b_s = b_p - C[:, n]; inactive
-// poses decouple with x = 0. LL^T right-looking with one barrier per column:
-// at step k every thread takes r_k = 1 / sqrt(S_kk) itself and updates its
-// trailing elements with (S_ik r_k)(S_jk r_k) — bit for bit L_ik L_jk — so
-// the scaled column is never waited for; column k is written back, scaled,
-// at step k + 1 when nobody reads it any more. Per element this is the
-// oracle's left-looking order. Forward / back substitution on one wave with
-// the values in registers, broadcast by readlane, in the oracle's order.
+// poses decouple with x = 0. LL^T right-looking with one barrier per column,
+// the trailing matrix in registers (6x6 pose blocks per thread, see below).
+// Forward / back substitution on one wave with the values in registers,
+// broadcast by readlane, in the oracle's order.
 constexpr int BA_ST = 1024;
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -589,6 +586,7 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     __shared__ double sL[BA_MAXN * (BA_MAXN + 1) / 2];
     __shared__ double sb[BA_MAXN], sbp[BA_MAXN], srinv[BA_MAXN];
+    __shared__ double scol[2][BA_MAXN];  // column k of the trailing matrix (unscaled), double-buffered
     __shared__ uint8_t sact[BA_MAXFREE];
     __shared__ int s_fail;
     const int p = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -625,34 +623,98 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     }
     __syncthreads();
     BA_STAMP(1);
-    // the owner of S_kk's last update publishes r_k = 1 / sqrt(S_kk) (or the
-    // failure) for step k; step 0's comes from thread 0
+    // Right-looking LL^T with the trailing matrix in registers: thread t owns
+    // the BS x BS block (bi, bj), bi >= bj, of the packed lower triangle
+    // (<= 2080 blocks of 3 for 32 free poses: at most two per thread). At step k every owner of a
+    // trailing element subtracts (S_ik r_k)(S_jk r_k) — bit for bit the
+    // oracle's L_ik L_jk in its left-looking order — with column k read from
+    // an LDS buffer its owners filled at step k - 1 (double-buffered), and
+    // r_k = 1 / sqrt(S_kk) published by the owner of S_kk. One barrier per
+    // column; no read-modify-write of the matrix in LDS.
+    constexpr int BS = 3;  // block edge (n is a multiple of 6)
+    constexpr int NBT = 2;  // blocks per thread: 2080 blocks of 3 at n = 192
+    const int nb = n / BS, nblk = nb * (nb + 1) / 2;
+    int I0[NBT], J0[NBT];
+    bool own[NBT];
+    double R[NBT][BS][BS];
+#pragma unroll
+    for (int q = 0; q < NBT; q++) {
+        const int t = tid + q * BA_ST;
+        own[q] = t < nblk;
+        int bi = 0, bj = 0;
+        if (own[q]) {  // t -> (bi, bj): row-major over the lower block triangle
+            bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+            while (tri(bi + 1) <= t) bi++;
+            while (tri(bi) > t) bi--;
+            bj = t - tri(bi);
+        }
+        I0[q] = BS * bi;
+        J0[q] = BS * bj;
+#pragma unroll
+        for (int a = 0; a < BS; a++)
+#pragma unroll
+            for (int c = 0; c < BS; c++)
+                R[q][a][c] = (own[q] && J0[q] + c <= I0[q] + a) ? sL[tri(I0[q] + a) + J0[q] + c] : 0.0;
+    }
+    if (tid < n) scol[0][tid] = sL[tri(tid)];  // column 0
     if (tid == 0) {
         const double d0 = n > 0 ? sL[0] : 1.0;
         s_fail = !(d0 > 0.0);
         srinv[0] = 1.0 / sqrt(d0);
     }
     __syncthreads();
-    for (int k = 0; k < n && !s_fail; k++) {
+    for (int k = 0; k < n; k++) {
+        if (s_fail) break;
         const double rk = srinv[k];
-        if (k > 0) {  // write back column k-1, scaled
-            const double rp = srinv[k - 1];
-            for (int i = k + tid; i < n; i += BA_ST) sL[tri(i) + k - 1] *= rp;
-        }
-        for (int i = k + 1 + w; i < n; i += BA_ST / 64) {  // trailing rows to waves, columns to lanes
-            const int ti = tri(i);
-            const double lik = sL[ti + k] * rk;
-            for (int j = k + 1 + lane; j <= i; j += 64) {
-                const double v = sL[ti + j] - lik * (sL[tri(j) + k] * rk);
-                sL[ti + j] = v;
-                if (j == k + 1 && i == k + 1) {  // S_{k+1,k+1} is final: publish step k+1's pivot
-                    if (!(v > 0.0)) s_fail = 1;
-                    srinv[k + 1] = 1.0 / sqrt(v);
+        const double* colk = scol[k & 1];
+        double* coln = scol[(k + 1) & 1];
+#pragma unroll
+        for (int q = 0; q < NBT; q++) {
+            const int i0 = I0[q], j0 = J0[q];
+            if (!own[q] || i0 + BS - 1 <= k || j0 + BS - 1 <= k) continue;  // no trailing elements
+            double li[BS], lj[BS];
+#pragma unroll
+            for (int a = 0; a < BS; a++) li[a] = (i0 + a > k) ? colk[i0 + a] * rk : 0.0;
+#pragma unroll
+            for (int c = 0; c < BS; c++) lj[c] = (j0 + c > k) ? colk[j0 + c] * rk : 0.0;
+#pragma unroll
+            for (int a = 0; a < BS; a++)
+#pragma unroll
+                for (int c = 0; c < BS; c++) {
+                    const int i = i0 + a, j = j0 + c;
+                    if (j > k && j <= i) R[q][a][c] = R[q][a][c] - li[a] * lj[c];
                 }
+            // column k + 1 is final now: publish it (and its pivot)
+            const int cc = k + 1 - j0;
+            if (cc >= 0 && cc < BS) {
+#pragma unroll
+                for (int a = 0; a < BS; a++)
+#pragma unroll
+                    for (int c = 0; c < BS; c++)
+                        if (c == cc && i0 + a >= k + 1) {
+                            coln[i0 + a] = R[q][a][c];
+                            if (i0 + a == k + 1) {
+                                if (!(R[q][a][c] > 0.0)) s_fail = 1;
+                                srinv[k + 1] = 1.0 / sqrt(R[q][a][c]);
+                            }
+                        }
             }
         }
         __syncthreads();
     }
+    // the factor back into sL, scaled: L_ij = S_ij r_j (the substitutions read it)
+    if (!s_fail) {
+#pragma unroll
+        for (int q = 0; q < NBT; q++)
+#pragma unroll
+            for (int a = 0; a < BS; a++)
+#pragma unroll
+                for (int c = 0; c < BS; c++) {
+                    const int i = I0[q] + a, j = J0[q] + c;
+                    if (own[q] && j < i) sL[tri(i) + j] = R[q][a][c] * srinv[j];
+                }
+    }
+    __syncthreads();
     const bool fail = s_fail;
     __syncthreads();
     BA_STAMP(2);
