@@ -21,6 +21,8 @@ namespace {
 
 constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
 constexpr int PO_CHI = 27;
+constexpr int PO_SPEC = 4;                     // LM trials evaluated together (see k_pose_opt)
+constexpr int PO_ROWS = PO_CHI + PO_SPEC;      // term rows: H, b, one chi2 row per speculative trial
 constexpr int PO_STRIDE_MAX = 8192;
 constexpr int PO_LDS_EDGES = 1024;  // problems up to this size keep edges and residuals in LDS
 
@@ -71,6 +73,7 @@ __device__ __forceinline__ void edge_error(const Lane& L, const gfse3::SE3& T, i
 // computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
 // Returns the sums in sh_sum: [0,21) lower H row-major-packed, [21,27) b, 27 chi2.
 __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[65], double* sh_sum) {
+    // (build: the H/b rows too; the chi2 row is PO_CHI)
     double acc = 0.0;
     for (int base = 0; base < L.n; base += 64) {
         const int e = base + L.l;
@@ -131,9 +134,66 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
     __syncthreads();
 }
 
+// computeActiveErrors + activeRobustChi2 at S trial estimates at once: lane
+// PO_CHI + s adds trial s's robust chi2 terms in edge order. The stored
+// residuals are not touched (the caller re-evaluates the estimate that was
+// evaluated last, as g2o's edges keep it, before the outlier pass).
+__device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[65],
+                                            double* sh_sum) {
+    double acc = 0.0;
+    for (int base = 0; base < L.n; base += 64) {
+        const int e = base + L.l;
+        if (e < L.n) {
+            const double info = L.info[e];
+#pragma unroll
+            for (int s = 0; s < PO_SPEC; s++) {
+                if (s >= S) break;
+                double pc[3], r0, r1;
+                edge_error(L, T[s], e, pc, r0, r1);
+                const double chi2 = r0 * (info * r0) + r1 * (info * r1);
+                double rho0, rho1;
+                robustify(chi2, L.delta, L.dsqr, rho0, rho1);
+                term[PO_CHI + s][L.l] = rho0;
+            }
+        }
+        __syncthreads();
+        const int m = min(64, L.n - base);
+        if (L.l >= PO_CHI && L.l < PO_CHI + S) {
+            const double* row = term[L.l];
+            int j = 0;
+            for (; j + 8 <= m; j += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = row[j + u];
+#pragma unroll
+                for (int u = 0; u < 8; u++) acc += v[u];
+            }
+            for (; j < m; j++) acc += row[j];
+        }
+        __syncthreads();
+    }
+    if (L.l >= PO_CHI && L.l < PO_CHI + S) sh_sum[L.l] = acc;
+    __syncthreads();
+}
+
+// residuals of the non-flagged edges at T (the estimate g2o evaluated last)
+__device__ __forceinline__ void store_errors(const Lane& L, const gfse3::SE3& T, const uint8_t* ou) {
+    for (int e = L.l; e < L.n; e += 64) {
+        if (ou[e]) continue;
+        double pc[3], r0, r1;
+        edge_error(L, T, e, pc, r0, r1);
+        L.e0[e] = r0;
+        L.e1[e] = r1;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
-    __shared__ double term[PO_NACC][65];
-    __shared__ double sh_sum[PO_NACC];
+    __shared__ double term[PO_ROWS][65];
+    __shared__ double sh_sum[PO_ROWS];
+    __shared__ double sh_x[PO_SPEC][6];       // each speculative trial's solution
+    __shared__ int sh_ok[PO_SPEC];
+    __shared__ gfse3::SE3 sh_T[PO_SPEC];      // and its trial estimate
     // every pass re-reads each edge and its residuals: for problems up to
     // PO_LDS_EDGES edges they live in LDS (generic pointers), else in HBM
     __shared__ gf_pose_edge sh_edges[PO_LDS_EDGES];
@@ -185,6 +245,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
     // chi2 thresholds {9.210, 7.378, 5.991, 5.991} (float) and iterations {10, 10, 7, 5}
     int nBadEdges = 0, total_it = 0;
     double xs[6] = {0, 0, 0, 0, 0, 0};
+    gfse3::SE3 last_eval = T;  // the estimate whose residuals the edges hold
     for (int round = 0; round < 4 && L.n > 0; round++) {
         const double chi2th = round == 0 ? (double)9.210f : round == 1 ? (double)7.378f : (double)5.991f;
         const int its = round < 2 ? 10 : round == 2 ? 7 : 5;
@@ -207,39 +268,89 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                 ni = 2;
                 nBad = 0;
             }
+            // g2o's trial loop (levenberg.cpp:99-163): on a rejection lambda *= ni,
+            // ni *= 2 and the next trial solves again. The next PO_SPEC trials'
+            // lambdas are therefore known in advance; they are solved (one
+            // 16-lane group per trial), their estimates built and their chi2
+            // evaluated together, and the sequential decision then walks them
+            // in order and stops at the first acceptance — the same trials, the
+            // same arithmetic and the same outcome as one trial at a time.
             double rho = 0;
             int q = 0;
-            do {
-                double Hl[36];
-                for (int i = 0; i < 36; i++) Hl[i] = H[i];
-                for (int j = 0; j < 6; j++) Hl[7 * j] += lambda;
-                double xn[6];
-                const bool ok = gfse3::ldlt6(Hl, b, xn);
-                if (ok)
-                    for (int j = 0; j < 6; j++) xs[j] = xn[j];
-                const gfse3::SE3 trial = gfse3::exp_mul(xs, T);
-                pass(L, trial, false, term, sh_sum);
-                double tempChi = sh_sum[PO_CHI];
-                if (!ok) tempChi = DBL_MAX;
-                rho = currentChi - tempChi;
-                double scale = 0;
-                for (int j = 0; j < 6; j++) scale += xs[j] * (lambda * xs[j] + b[j]);
-                scale += 1e-3;
-                rho /= scale;
-                if (rho > 0 && isfinite(tempChi)) {
-                    double alpha = 1. - pow((2 * rho - 1), 3.0);
-                    alpha = fmin(alpha, 2. / 3.);
-                    const double sf = fmax(1. / 3., alpha);
-                    lambda *= sf;
-                    ni = 2;
-                    currentChi = tempChi;
-                    T = trial;
-                } else {
-                    lambda *= ni;
-                    ni *= 2;
+            bool more = true;
+            while (more) {
+                const int S = min(PO_SPEC, 10 - q);
+                double lam_s[PO_SPEC], ni_s[PO_SPEC];
+                lam_s[0] = lambda;
+                ni_s[0] = ni;
+#pragma unroll
+                for (int s2 = 1; s2 < PO_SPEC; s2++) {
+                    lam_s[s2] = lam_s[s2 - 1] * ni_s[s2 - 1];
+                    ni_s[s2] = ni_s[s2 - 1] * 2;
                 }
-                q++;
-            } while (rho < 0 && q < 10);
+                {
+                    const int g = L.l >> 4;  // this lane's trial
+                    double lam_g = lam_s[0];
+#pragma unroll
+                    for (int s2 = 1; s2 < PO_SPEC; s2++)
+                        if (g == s2) lam_g = lam_s[s2];
+                    double Hl[36];
+                    for (int i = 0; i < 36; i++) Hl[i] = H[i];
+                    for (int j = 0; j < 6; j++) Hl[7 * j] += lam_g;
+                    double xn[6];
+                    const bool ok = gfse3::ldlt6(Hl, b, xn);
+                    if ((L.l & 15) == 0) {
+                        sh_ok[g] = ok;
+                        for (int j = 0; j < 6; j++) sh_x[g][j] = xn[j];
+                    }
+                }
+                __syncthreads();
+                // a failed factorisation keeps the previous solution (Solver::_x):
+                // trial g solves with the last successful x among trials <= g
+                {
+                    const int g = L.l >> 4;
+                    if ((L.l & 15) == 0 && g < S) {
+                        double xg[6];
+                        for (int j = 0; j < 6; j++) xg[j] = xs[j];
+                        for (int s2 = 0; s2 <= g; s2++)
+                            if (sh_ok[s2])
+                                for (int j = 0; j < 6; j++) xg[j] = sh_x[s2][j];
+                        sh_T[g] = gfse3::exp_mul(xg, T);
+                    }
+                }
+                __syncthreads();
+                pass_trials(L, sh_T, S, term, sh_sum);
+                for (int s2 = 0; s2 < S; s2++) {
+                    const bool ok = sh_ok[s2];
+                    if (ok)
+                        for (int j = 0; j < 6; j++) xs[j] = sh_x[s2][j];
+                    double tempChi = sh_sum[PO_CHI + s2];
+                    if (!ok) tempChi = DBL_MAX;
+                    rho = currentChi - tempChi;
+                    double scale = 0;
+                    for (int j = 0; j < 6; j++) scale += xs[j] * (lam_s[s2] * xs[j] + b[j]);
+                    scale += 1e-3;
+                    rho /= scale;
+                    last_eval = sh_T[s2];
+                    q++;
+                    if (rho > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - pow((2 * rho - 1), 3.0);
+                        alpha = fmin(alpha, 2. / 3.);
+                        const double sf = fmax(1. / 3., alpha);
+                        lambda = lam_s[s2] * sf;
+                        ni = 2;
+                        currentChi = tempChi;
+                        T = sh_T[s2];
+                    } else {
+                        lambda = lam_s[s2] * ni_s[s2];
+                        ni = ni_s[s2] * 2;
+                    }
+                    if (!(rho < 0 && q < 10)) {
+                        more = false;
+                        break;
+                    }
+                }
+            }
             if (q == 10 || rho == 0) break;
             if ((iniChi - currentChi) * 1e3 < iniChi)
                 nBad++;
@@ -248,7 +359,9 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
             if (nBad >= 3) break;
         }
         // outlier classification (Optimizer.cc:373-395); errors are those of
-        // the last evaluated estimate, recomputed only for flagged edges.
+        // the last evaluated estimate, recomputed at the current one for
+        // flagged edges.
+        store_errors(L, last_eval, ou);
         int nb = 0;
         for (int base = 0; base < L.n; base += 64) {
             const int e = base + L.l;
