@@ -558,20 +558,10 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const double* cur, const double* info, const int* cell_start,
                            const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D) {
-#ifdef GF_AM_STAMP
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-#endif
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int q = lmk[C.slot[c]];
+        const OnePre p = A.pre[(long long)f * A.mp_cap + q];  // in flight during the log-det
         C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
-    }
-#ifdef GF_AM_STAMP
-    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) atomicAdd(&g_am_stamp[7], t1 - t0);
-#endif
-    for (int c = c0 + threadIdx.x; c < c1; c += AW) {
-        const int q = lmk[C.slot[c]];
-        const OnePre p = A.pre[(long long)f * A.mp_cap + q];
         int mi = p.idx, md = p.dist;
         if ((p.holder1 >= 0 && claim[p.holder1] >= 0) || (p.holder2 >= 0 && claim[p.holder2] >= 0)) {
             int h1, h2;  // a holder was claimed this frame: scan again
@@ -798,6 +788,19 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             __syncthreads();
         }
         AM_T(4);
+        // the successful top's H row and its keypoint's octave, loaded now so
+        // that their latency overlaps the commit below
+        double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
+        int oct_b = 0;
+        if (!exh && lane < 49) {
+            const double* Hq = Hm + 14LL * lmk[C.slot[top]];
+            const int i = lane / 7, jj = lane % 7;
+            h_i = Hq[i];
+            h_j = Hq[jj];
+            h_7i = Hq[7 + i];
+            h_7j = Hq[7 + jj];
+            oct_b = K[C.match[top]].octave;
+        }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
         const int T = exh ? exh_at : C.tries[nused - 1];
@@ -815,11 +818,9 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             A.score[(long long)f * A.kp_cap + b] = C.dist[top];
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
-            const double* H = Hm + 14LL * q;
-            const double s2 = sqrt((double)A.sigma2[K[b].octave]);
+            const double s2 = sqrt((double)A.sigma2[oct_b]);
             const double w = s2 / (s2 * s2);
-            const int i = lane / 7, jj = lane % 7;
-            const double a0 = w * H[i], a1 = w * H[jj], b0 = w * H[7 + i], b1 = w * H[7 + jj];
+            const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
         }
         nm++;
