@@ -206,8 +206,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=512, help="independent streams per GPU")
-    ap.add_argument("--groups", type=int, default=2,
+    ap.add_argument("--batch", type=int, default=768, help="independent streams per GPU")
+    ap.add_argument("--groups", type=int, default=3,
                     help="stream groups per GPU, each on its own HIP stream (their kernels overlap)")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
