@@ -275,6 +275,7 @@ struct ActiveArgs {
     const struct OnePre* pre;  // [F][mp_cap] one-point results against the starting claims
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
     int* grid_items;           // [F][kp_cap]
+    int pool_cap;              // LDS pool capacity of this launch (<= POOL_MAX)
 };
 
 // ---------------------------------------------------------------------------
@@ -641,25 +642,28 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
 #endif
     extern __shared__ __align__(16) uint8_t smem[];
-    double* c_score = (double*)smem;                                       // POOL_MAX
-    unsigned long long* pbits = (unsigned long long*)(c_score + POOL_MAX);  // 64
-    int* first = (int*)(pbits + 64);                                       // POOL_MAX: draw-batch duplicate marks
-    int* claim = first + POOL_MAX;                                         // KP_MAX
-    int* ppre = claim + KP_MAX;                                            // 65 (+3 pad)
-    int32_t* c_tries = ppre + 68;                                          // POOL_MAX
-    int16_t* lmk = (int16_t*)(c_tries + POOL_MAX);                         // POOL_MAX: map point of each slot
-    int16_t* vis = lmk + POOL_MAX;                                         // POOL_MAX: lmkVisited per slot
-    int16_t* c_slot = vis + POOL_MAX;                                      // POOL_MAX
-    int16_t* c_match = c_slot + POOL_MAX;                                  // POOL_MAX
-    int16_t* c_dist = c_match + POOL_MAX;                                  // POOL_MAX
-    int16_t* rheap = c_dist + POOL_MAX;                                    // POOL_MAX: replay heap
-    uint8_t* c_alive = (uint8_t*)(rheap + POOL_MAX);                       // POOL_MAX
+    // sized for this launch: PC = pool capacity (map-list capacity rounded to 64,
+    // at most POOL_MAX), claims for kp_cap keypoints
+    const int PC = A.pool_cap;
+    double* c_score = (double*)smem;                                       // PC
+    unsigned long long* pbits = (unsigned long long*)(c_score + PC);       // 64
+    int* first = (int*)(pbits + 64);                                       // PC: draw-batch duplicate marks
+    int* claim = first + PC;                                               // kp_cap
+    int* ppre = claim + A.kp_cap;                                          // 65 (+3 pad)
+    int32_t* c_tries = ppre + 68;                                          // PC
+    int16_t* lmk = (int16_t*)(c_tries + PC);                               // PC: map point of each slot
+    int16_t* vis = lmk + PC;                                               // PC: lmkVisited per slot
+    int16_t* c_slot = vis + PC;                                            // PC
+    int16_t* c_match = c_slot + PC;                                        // PC
+    int16_t* c_dist = c_match + PC;                                        // PC
+    int16_t* rheap = c_dist + PC;                                          // PC: replay heap
+    uint8_t* c_alive = (uint8_t*)(rheap + PC);                             // PC
     __shared__ double cur[49];
     __shared__ int s_res, s_exh;
 
     const int f = blockIdx.x, lane = threadIdx.x;
     const FrameConst& fc = A.fc;
-    const int n = min(A.n[f], KP_MAX);
+    const int n = min(A.n[f], A.kp_cap);
     const int m = min(A.m[f], 32767);
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
@@ -670,7 +674,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
     for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
-    for (int i = lane; i < POOL_MAX; i += AW) first[i] = AW;
+    for (int i = lane; i < PC; i += AW) first[i] = AW;
     uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
 #pragma unroll
     for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         if (take) {
             if (early) {
                 left[o] = i;
-            } else if (o < POOL_MAX) {
+            } else if (o < PC) {
                 lmk[o] = (int16_t)i;
                 vis[o] = -1;
             }
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         }
         return;
     }
-    if (N > POOL_MAX) {
+    if (N > PC) {
         if (lane == 0) A.err[f] = 2;
         return;
     }
@@ -840,7 +844,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     for (int i = lane; i < n; i += AW) kp2mp[i] = claim[i];
     for (int w = 0; w < 64; w++) {
         const unsigned long long bits = pbits[w];
-        if (((bits >> lane) & 1ull) && w * 64 + lane < POOL_MAX)
+        if (((bits >> lane) & 1ull) && w * 64 + lane < PC)
             left[ppre[w] + __popcll(bits & ((1ull << lane) - 1ull))] = lmk[w * 64 + lane];
     }
     {  // back to the glibc ring: f advanced by the calls made, oldest word at f
@@ -860,9 +864,9 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
 
 #undef AM_T
 
-size_t active_lds_bytes() {
-    return sizeof(double) * POOL_MAX + 8 * 64 + sizeof(int) * (POOL_MAX + KP_MAX + 68) +
-           sizeof(int32_t) * POOL_MAX + sizeof(int16_t) * 6 * POOL_MAX + POOL_MAX;
+size_t active_lds_bytes(int pool_cap, int kp_cap) {
+    return sizeof(double) * pool_cap + 8 * 64 + sizeof(int) * ((size_t)pool_cap + kp_cap + 68) +
+           sizeof(int32_t) * pool_cap + sizeof(int16_t) * 6 * (size_t)pool_cap + pool_cap;
 }
 
 // ------------------------------------------------------------- max-volume selection
@@ -1143,10 +1147,12 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
         k_onepoint_pre<<<nframes, PRE_THREADS, pre_lds, s>>>(A, (OnePre*)pre);
         GF_HIP(hipGetLastError());
     }
-    rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(), &mask);
+    A.pool_cap = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
+    const size_t am_lds = active_lds_bytes(A.pool_cap, kp_cap);
+    rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, KP_MAX), &mask);
     if (rc) return rc;
     GF_PROF(ctx, s, "k_active_match");
-    k_active_match<<<nframes, AW, active_lds_bytes(), s>>>(A);
+    k_active_match<<<nframes, AW, am_lds, s>>>(A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
