@@ -57,6 +57,8 @@ struct MatchArgs {
     int32_t* qres;  // [F][q_cap] scratch: matched kp per query (MODE_LAST)
     int32_t* err;   // [F] round-limit flag
     const struct SeqPre* pre;  // [F][q_cap] MODE_LAST: each query against the starting claims
+    int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (k_match_seq_pre writes, rescans read)
+    int* grid_items;           // [F][kp_cap]
 };
 
 
@@ -341,6 +343,8 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
             reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
     build_grid(fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
                SEQ_PRE_THREADS);
+    for (int c = tid; c < NCELLS + 1; c += SEQ_PRE_THREADS) A.grid_cs[(long long)f * (NCELLS + 1) + c] = cell_start[c];
+    for (int i = tid; i < n; i += SEQ_PRE_THREADS) A.grid_items[(long long)f * A.kp_cap + i] = items[i];
     const uint8_t* DD = dl ? (const uint8_t*)Ds : D;
     for (int k = tid; k < nq; k += SEQ_PRE_THREADS) {
         const Query q = make_query(A, fc, f, k);
@@ -408,16 +412,16 @@ __device__ __forceinline__ void top2_insert(unsigned long long key, unsigned lon
 
 __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
-    int* cell_start = lds;                  // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;  // NCELLS
-    int* items = cursor + NCELLS;           // KP_MAX
-    int* claim = items + KP_MAX;            // KP_MAX
-    int* qlist = claim + KP_MAX;            // Q_MAX (also the grid-build scratch)
+    int* claim = lds;                // kp_cap
+    int* qlist = claim + A.kp_cap;   // q_cap
     __shared__ int s_nm, s_hist[HISTO_LENGTH], s_keep[3];
 
     const int f = blockIdx.x, lane = threadIdx.x;
-    const int n = min(A.n[f], KP_MAX);
-    const int nq = min(A.m[f], Q_MAX);
+    const int n = min(A.n[f], A.kp_cap);
+    const int nq = min(A.m[f], A.q_cap);
+    // the keypoint grid comes from k_match_seq_pre (HBM; only rescans read it)
+    const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
+    const int* items = A.grid_items + (long long)f * A.kp_cap;
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
@@ -426,7 +430,8 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
         s_nm = 0;
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
-    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, qlist, SEQ_THREADS);
+    for (int i = lane; i < n; i += SEQ_THREADS) claim[i] = kp2mp[i];
+    __syncthreads();
 
     // ordered list of the queries that project into the image
     int nvalid = 0;
@@ -520,7 +525,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
     if (lane == 0) A.nmatches[f] = s_nm;
 }
 
-size_t seq_lds_bytes() { return sizeof(int) * (2 * NCELLS + 1 + 2 * KP_MAX + Q_MAX); }
+size_t seq_lds_bytes(int kp_cap, int q_cap) { return sizeof(int) * ((size_t)kp_cap + q_cap); }
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
@@ -618,7 +623,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
         GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)match_lds_bytes()));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)seq_lds_bytes()));
+                                   (int)seq_lds_bytes(KP_MAX, Q_MAX)));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq_pre, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)seq_pre_lds_bytes(KP_MAX)));
         attr_mask |= 1ull << ctx->device;
@@ -630,7 +635,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
             GF_HIP(hipGetLastError());
         }
         GF_PROF(ctx, s, "k_match_lastframe");
-        k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(), s>>>(A, fc);
+        k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
     } else {  // many queries, narrow windows: claim-resolution rounds
         GF_PROF(ctx, s, "k_match_project");
         k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
@@ -728,6 +733,12 @@ int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, co
     rc = gf::ws_get(ctx, 33, sizeof(SeqPre) * (size_t)nframes * last_cap, &pre);
     if (rc) return rc;
     A.pre = (const SeqPre*)pre;
+    void *gcs, *gitems;
+    if ((rc = gf::ws_get(ctx, 36, sizeof(int) * (size_t)nframes * (NCELLS + 1), &gcs)) ||
+        (rc = gf::ws_get(ctx, 37, sizeof(int) * (size_t)nframes * kp_cap, &gitems)))
+        return rc;
+    A.grid_cs = (int*)gcs;
+    A.grid_items = (int*)gitems;
     GF_CHECK(seq_pre_lds_bytes(kp_cap) <= 160 * 1024, GF_ERR_UNSUPPORTED, "keypoint capacity too large");
     return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
 }
