@@ -24,7 +24,7 @@ constexpr int PO_CHI = 27;
 constexpr int PO_SPEC = 4;                     // LM trials evaluated together (see k_pose_opt)
 constexpr int PO_ROWS = PO_CHI + PO_SPEC;      // term rows: H, b, one chi2 row per speculative trial
 constexpr int PO_STRIDE_MAX = 8192;
-constexpr int PO_LDS_EDGES = 1024;  // problems up to this size keep edges and residuals in LDS
+constexpr int PO_LDS_EDGES = 512;  // problems up to this size keep edges and residuals in LDS (40 KB in all)
 
 struct PoseArgs {
     const gf_pose_edge* edges;
