@@ -455,25 +455,36 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ya = wv * dh / 4, yb = (wv + 1) * dh / 4;
     int cnt = 0;
-    for (int x0 = 0; x0 < dw; x0 += 64) {
-        const int x = x0 + lane;
-        const bool col = x < dw;
+    // two 64-column strips per pass, walked together: their LDS reads are
+    // independent, so each row step waits for one latency, not two
+    for (int x0 = 0; x0 < dw; x0 += 128) {
+        const int xa = x0 + lane, xb = x0 + 64 + lane;
         auto rd = [&](int y, int xx) -> int {
-            return (col && y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * pitch + rsh[y] + xx], th) : 0;
+            return (y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * pitch + rsh[y] + xx], th) : 0;
         };
-        int u0 = rd(ya - 1, x - 1), u1 = rd(ya - 1, x), u2 = rd(ya - 1, x + 1);
-        int c0 = rd(ya, x - 1), c1 = rd(ya, x), c2 = rd(ya, x + 1);
-        int d0 = rd(ya + 1, x - 1), d1 = rd(ya + 1, x), d2 = rd(ya + 1, x + 1);
+        int ua0 = rd(ya - 1, xa - 1), ua1 = rd(ya - 1, xa), ua2 = rd(ya - 1, xa + 1);
+        int ca0 = rd(ya, xa - 1), ca1 = rd(ya, xa), ca2 = rd(ya, xa + 1);
+        int da0 = rd(ya + 1, xa - 1), da1 = rd(ya + 1, xa), da2 = rd(ya + 1, xa + 1);
+        int ub0 = rd(ya - 1, xb - 1), ub1 = rd(ya - 1, xb), ub2 = rd(ya - 1, xb + 1);
+        int cb0 = rd(ya, xb - 1), cb1 = rd(ya, xb), cb2 = rd(ya, xb + 1);
+        int db0 = rd(ya + 1, xb - 1), db1 = rd(ya + 1, xb), db2 = rd(ya + 1, xb + 1);
         for (int y = ya; y < yb; y++) {
             // row y + 2 is read one step ahead, so its LDS latency overlaps this step
-            const int e0 = rd(y + 2, x - 1), e1 = rd(y + 2, x), e2 = rd(y + 2, x + 1);
-            const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
-            const bool keep = c1 != 0 && c1 > mx;
-            if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
-            cnt += __popcll(__ballot(keep));
-            u0 = c0, u1 = c1, u2 = c2;
-            c0 = d0, c1 = d1, c2 = d2;
-            d0 = e0, d1 = e1, d2 = e2;
+            const int ea0 = rd(y + 2, xa - 1), ea1 = rd(y + 2, xa), ea2 = rd(y + 2, xa + 1);
+            const int eb0 = rd(y + 2, xb - 1), eb1 = rd(y + 2, xb), eb2 = rd(y + 2, xb + 1);
+            const int mxa = max(max(max(ua0, ua1), max(ua2, ca0)), max(max(ca2, da0), max(da1, da2)));
+            const int mxb = max(max(max(ub0, ub1), max(ub2, cb0)), max(max(cb2, db0), max(db1, db2)));
+            const bool ka = xa < dw && ca1 != 0 && ca1 > mxa;
+            const bool kb = xb < dw && cb1 != 0 && cb1 > mxb;
+            if (ka) atomicOr(&bits[(y * dw + xa) >> 5], 1u << ((y * dw + xa) & 31));
+            if (kb) atomicOr(&bits[(y * dw + xb) >> 5], 1u << ((y * dw + xb) & 31));
+            cnt += __popcll(__ballot(ka)) + __popcll(__ballot(kb));
+            ua0 = ca0, ua1 = ca1, ua2 = ca2;
+            ca0 = da0, ca1 = da1, ca2 = da2;
+            da0 = ea0, da1 = ea1, da2 = ea2;
+            ub0 = cb0, ub1 = cb1, ub2 = cb2;
+            cb0 = db0, cb1 = db1, cb2 = db2;
+            db0 = eb0, db1 = eb1, db2 = eb2;
         }
     }
     return cnt;  // this wave's survivors
