@@ -92,6 +92,24 @@ class ORBmatcher:
                                      ctypes.byref(n)))
         return n.value
 
+    def SearchByProjection_Budget(self, F: Frame, views: np.ndarray, mp_desc: np.ndarray, th: float,
+                                  time_constr: float, found: np.ndarray | None = None) -> int:
+        """ORBmatcher::SearchByProjection_Budget (ORBmatcher.cc:276-379): the
+        M2 search with MapPoint::IncreaseFound on every match and a wall-clock
+        cap. A non-positive budget matches nothing (:281-282); any positive
+        budget runs the whole list (parity mode: the device pass finishes far
+        inside the reference's budgets, and a clock cut-off would make the
+        result timing-dependent). `found` (per map point, optional) receives
+        the IncreaseFound increments."""
+        if time_constr <= 0:
+            return 0
+        before = F.mvpMapPoints.copy()
+        n = self.SearchByProjection(F, views, mp_desc, th)
+        if found is not None:
+            new = F.mvpMapPoints[(F.mvpMapPoints >= 0) & (before < 0)]
+            np.add.at(found, new, 1)
+        return n
+
     def SearchByProjectionLast(self, CurrentFrame: Frame, LastFrame: Frame, th: float) -> int:
         """ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th) (ORBmatcher.cc:2081)."""
         n = ctypes.c_int()

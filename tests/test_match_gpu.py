@@ -50,6 +50,24 @@ def test_search_by_projection_bit_exact(cam, nmp, nkp, seed, th, ratio):
     assert ng > 0
 
 
+def test_search_by_projection_budget():
+    """M5 (ORBmatcher.cc:276-379): the M2 search with IncreaseFound; a
+    non-positive budget matches nothing, a positive one runs the full list."""
+    sc, info = _scene("euroc", 2000, 1000, 9)
+    F = Frame(sc["keypoints"], sc["descriptors"], info, sc["Tcw"])
+    views = F.isInFrustum(sc["map"], 0.5)
+    assert ORBmatcher(0.8).SearchByProjection_Budget(F, views, sc["mp_desc"], 1.0, 0.0) == 0
+    assert (F.mvpMapPoints < 0).all()
+    kp2mp, score = F.mvpMapPoints.copy(), F.mvpMatchScore.copy()
+    found = np.zeros(len(views), np.int32)
+    ng = ORBmatcher(0.8).SearchByProjection_Budget(F, views, sc["mp_desc"], 1.0, 5.0, found)
+    no = O.match_project(info, sc["keypoints"], sc["descriptors"], views, sc["mp_desc"], 1.0, 0.8, kp2mp, score)
+    assert ng == no and np.array_equal(F.mvpMapPoints, kp2mp) and np.array_equal(F.mvpMatchScore, score)
+    expect = np.zeros(len(views), np.int32)
+    np.add.at(expect, kp2mp[kp2mp >= 0], 1)
+    assert np.array_equal(found, expect) and found.sum() == ng
+
+
 def _two_frames(seed, nmp=2500, nkp=1500, rot_deg=0.3):
     sc, info = _scene("euroc", nmp, nkp, seed)
     rng = np.random.default_rng(seed + 100)
