@@ -64,11 +64,15 @@ def _check_pose(fe, T0, kps, kp2mp_before, mps, Tg, outl_g, ninl_g):
     assert np.all(np.abs(Tg.reshape(4, 4).astype(np.float64) - To) <= 1e-5 * np.maximum(1, np.abs(To)))
 
 
-@pytest.fixture(scope="module")
-def fe():
+# config 2 (EuRoC 752x480, 1000 feats, GF budget 100, 2000-point map) and
+# config 3 (TUM 640x480, 2000 feats, GF budget 160, 3000-point map)
+@pytest.fixture(scope="module", params=[("euroc", 1000, 2000, 100), ("tum", 2000, 3000, 160)],
+                ids=["config2", "config3"])
+def fe(request):
     from gf_orb_slam_amd.pipeline import FrontEnd
 
-    fe = FrontEnd("euroc", 1000, B, 2000, seed=3)
+    cam, nfeat, nmap, budget = request.param
+    fe = FrontEnd(cam, nfeat, B, nmap, gf_budget=budget, seed=3)
     w, h = fe.cam[:2]
     fe.load_frames(np.stack([synth.synth_frame(w, h, synth.frame_seed(40 + b, 0)) for b in range(B)]))
     fe.build_maps()
