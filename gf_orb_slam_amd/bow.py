@@ -40,6 +40,16 @@ def read_vocabulary(path: str) -> dict:
     return out
 
 
+def save_vocabulary_binary(tree: dict, path: str) -> None:
+    """TemplatedVocabulary::saveToBinaryFile (TemplatedVocabulary.h:1516-1536)
+    of tree arrays with the root at index 0 (as read_vocabulary returns them)."""
+    t = {k: np.ascontiguousarray(tree[k], dt) for k, dt in
+         (("parent", np.int32), ("desc", np.uint8), ("weight", np.float64), ("is_leaf", np.uint8))}
+    arr = VocabArrays(tree["k"], tree["L"], tree["scoring"], tree["weighting"], len(t["parent"]),
+                      *[t[k].ctypes.data for k in ("parent", "desc", "weight", "is_leaf")])
+    check(lib().gf_vocab_save_binary(ctypes.byref(arr), path.encode()))
+
+
 class FeatureVector:
     """DBoW2::FeatureVector as CSR: nodes ascending, feature indices per node."""
 

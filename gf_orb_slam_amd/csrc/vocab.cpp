@@ -131,3 +131,30 @@ extern "C" int gf_vocab_read(const char* path, gf_vocab_arrays* out) {
     out->nnodes = n;
     return GF_OK;
 }
+
+extern "C" int gf_vocab_save_binary(const gf_vocab_arrays* t, const char* path) {
+    if (!t || !path || !t->parent || !t->desc || !t->weight || t->nnodes < 1) return GF_ERR_ARG;
+    const int n = t->nnodes;
+    std::vector<uint8_t> has_child((size_t)n, 0);
+    for (int i = 1; i < n; i++) {
+        if (t->parent[i] < 0 || t->parent[i] >= n) return GF_ERR_ARG;
+        has_child[(size_t)t->parent[i]] = 1;
+    }
+    std::ofstream f(path, std::ios::out | std::ios::binary);
+    if (!f) return GF_ERR_ARG;
+    const uint32_t nb_nodes = (uint32_t)n, size_node = 4 + 32 + 4 + 1;
+    const int32_t hdr[4] = {t->k, t->L, t->scoring, t->weighting};
+    f.write((const char*)&nb_nodes, 4);
+    f.write((const char*)&size_node, 4);
+    f.write((const char*)hdr, 16);
+    for (int i = 1; i < n; i++) {
+        const uint32_t par = (uint32_t)t->parent[i];
+        const float w = (float)t->weight[i];
+        const uint8_t leaf = has_child[(size_t)i] ? 0 : 1;
+        f.write((const char*)&par, 4);
+        f.write((const char*)t->desc + 32 * (size_t)i, 32);
+        f.write((const char*)&w, 4);
+        f.write((const char*)&leaf, 1);
+    }
+    return f ? GF_OK : GF_ERR_ARG;
+}

@@ -385,6 +385,12 @@ typedef struct gf_vocab gf_vocab;
  * == NULL only the header fields and nnodes are filled; call again with buffers
  * of nnodes entries. */
 int gf_vocab_read(const char* path, gf_vocab_arrays* out);
+/* Host only: TemplatedVocabulary::saveToBinaryFile (TemplatedVocabulary.h:1516-1536;
+ * tools/bin_vocabulary.cc converts ORBvoc.txt with it): header {nb_nodes,
+ * size_node = 41, k, L, scoring, weighting}, then nodes 1..nnodes-1 as {uint32
+ * parent, 32 descriptor bytes, float weight, bool is_leaf}, is_leaf meaning "has
+ * no children" as Node::isLeaf. */
+int gf_vocab_save_binary(const gf_vocab_arrays* tree, const char* path);
 /* Upload a tree (device-resident, shared by every frame of the context). */
 int gf_vocab_create(gf_ctx* ctx, const gf_vocab_arrays* tree, gf_vocab** out);
 /* gf_vocab_read + gf_vocab_create (main.cc:92-106 picks the loader by suffix). */

@@ -73,3 +73,25 @@ def test_match_bow_recovers_correspondences():
     ok = out >= 0
     assert n == ok.sum() and n > 200
     assert np.all(out[ok] == mp[perm[ok]])  # every accepted match is the true one
+
+
+def test_bin_vocabulary_tool_matches_save_to_binary(tmp_path):
+    """tools/bin_vocabulary.cc: loadFromTextFile + saveToBinaryFile. The
+    converter's bytes equal the saveToBinaryFile layout written from the same
+    tree, and loading them back gives the text tree plus the binary loader's
+    duplicated last record."""
+    from gf_orb_slam_amd.bin_vocabulary import convert
+
+    voc = synth_vocabulary(13, k=6, L=3, stop_frac=0.1)
+    txt, out, ref = str(tmp_path / "v.txt"), str(tmp_path / "v.bin"), str(tmp_path / "ref.bin")
+    write_vocab_text(voc, txt)
+    r = convert(txt, out)
+    write_vocab_binary(voc, ref)
+    assert r["nodes"] == len(voc["parent"])
+    assert open(out, "rb").read() == open(ref, "rb").read()
+    tb, tt = read_vocabulary(out), read_vocabulary(txt)
+    n = len(tt["parent"])
+    assert len(tb["parent"]) == n + 1
+    for key in ("parent", "desc", "is_leaf"):
+        assert np.array_equal(tb[key][:n], tt[key])
+    assert np.array_equal(tb["weight"][:n], tt["weight"].astype(np.float32).astype(np.float64))
