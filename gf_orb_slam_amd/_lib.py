@@ -109,6 +109,8 @@ _PROTOS = {
     "gf_pose_opt_frames_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _I, _F, _F, _F, _F, _P, _P, _P, _P, _P],
     "gf_vocab_read": [_P, _P],
     "gf_vocab_save_binary": [_P, _P],
+    "gf_undistort_keypoints": [_P, _P, _P, _P, _I, _P],
+    "gf_undistort_keypoints_dev": [_P, _I, _P, _P, _P, _P, _I, _P, _P],
     "gf_vocab_create": [_P, _P, _P],
     "gf_vocab_load": [_P, _P, _P],
     "gf_vocab_info": [_P, _P, _P, _P, _P],

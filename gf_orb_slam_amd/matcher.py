@@ -121,3 +121,17 @@ class ORBmatcher:
                                        ptr(CurrentFrame.mvpMapPoints), ptr(CurrentFrame.mvpMatchScore),
                                        ctypes.byref(n)))
         return n.value
+
+
+def undistort_keypoints(kps: np.ndarray, K, dist, ctx=None) -> np.ndarray:
+    """Frame::UndistortKeyPoints (Frame.cc:389-423): mvKeysUn from mvKeys with
+    cv::undistortPoints(K, mDistCoef); a copy when k1 == 0. K = (fx, fy, cx,
+    cy); dist = (k1, k2, p1, p2[, k3])."""
+    ctx = ctx or default_context()
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = k.copy()
+    Kf = np.asarray(K, np.float32).reshape(4)
+    d = np.zeros(5, np.float32)
+    d[:len(dist)] = np.asarray(dist, np.float32)
+    check(lib().gf_undistort_keypoints(ctx.handle, ptr(Kf), ptr(d), ptr(k), len(k), ptr(out)))
+    return out

@@ -495,6 +495,16 @@ int gf_ba_plan_solve(gf_ba_plan* plan, void* stream, int* steps);
 int gf_ba_plan_results(gf_ba_plan* plan, gf_ba_result* res);
 int gf_ba_plan_destroy(gf_ba_plan* plan);
 
+/* ------------------------------------------------ keypoint undistortion
+ * Frame::UndistortKeyPoints (Frame.cc:389-423): cv::undistortPoints with
+ * K = {fx, fy, cx, cy} and dist = {k1, k2, p1, p2, k3} (k3 = 0 for the 4-term
+ * model); keypoints are copied unchanged when k1 == 0. Only x/y change. */
+int gf_undistort_keypoints(gf_ctx* ctx, const float K[4], const float dist[5], const gf_keypoint* kps, int n,
+                           gf_keypoint* out);
+/* Batched: d_in/d_out are [nframes][cap], d_n[nframes] keypoints each. */
+int gf_undistort_keypoints_dev(gf_ctx* ctx, int nframes, const float K[4], const float dist[5],
+                               const gf_keypoint* d_in, const int32_t* d_n, int cap, gf_keypoint* d_out, void* stream);
+
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end
  * step stays on the device. One workgroup per frame.

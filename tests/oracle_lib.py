@@ -244,3 +244,14 @@ def match_bow(mode, nnratio, check_ori, a, b):
                         _p(A[3]), _p(A[4]), _p(A[5]), len(A[3]), _p(B[0]), _p(B[1]), _p(B[2]), len(B[0]), _p(B[3]),
                         _p(B[4]), _p(B[5]), len(B[3]), _p(out), ctypes.byref(nm))
     return nm.value, out[:(len(B[3]) if mode == 0 else len(A[3]))].copy()
+
+
+def undistort_keypoints(kps, K, dist):
+    """Frame::UndistortKeyPoints on the CPU oracle (OpenCV undistortPoints restated)."""
+    k = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = k.copy()
+    Kf = np.asarray(K, np.float32).reshape(4)
+    d = np.zeros(5, np.float32)
+    d[:len(dist)] = np.asarray(dist, np.float32)
+    assert orc().orc_undistort_keypoints(_p(Kf), _p(d), _p(k), len(k), _p(out)) == 0
+    return out
