@@ -111,6 +111,12 @@ _PROTOS = {
     "gf_vocab_save_binary": [_P, _P],
     "gf_undistort_keypoints": [_P, _P, _P, _P, _I, _P],
     "gf_undistort_keypoints_dev": [_P, _I, _P, _P, _P, _P, _I, _P, _P],
+    "gf_distinctive_descriptors": [_P, _I, _P, _P, _P, _P],
+    "gf_distinctive_descriptors_dev": [_P, _I, _P, _P, _P, _P, _I, _P],
+    "gf_fuse": [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _F, _P, _P],
+    "gf_fuse_dev": [_P, _P, _I, _P, _P],
+    "gf_search_for_triangulation": [_P, _I, _P, _P, _P, _P, _I, _P, _P],
+    "gf_search_for_triangulation_dev": [_P, _I, _I, _P, _P, _P, _P, _I, _P, _P, _P],
     "gf_vocab_create": [_P, _P, _P],
     "gf_vocab_load": [_P, _P, _P],
     "gf_vocab_info": [_P, _P, _P, _P, _P],

@@ -218,6 +218,56 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __
     }
 }
 
+// ComputeThreeMaxima (ORBmatcher.cc:2338-2379) over the recorded matches' bins;
+// drops the matches outside the three dominant bins. All threads of the block.
+__device__ void rotation_filter(int nm, const uint8_t* rbin, const int* rec, int32_t* out, int* s_hist,
+                                int* s_keep, int* s_nm) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int r = tid; r < nm; r += nt) atomicAdd(&s_hist[rbin[r]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = s_hist[i];
+            if (s > max1) {
+                max3 = max2;
+                max2 = max1;
+                max1 = s;
+                ind3 = ind2;
+                ind2 = ind1;
+                ind1 = i;
+            } else if (s > max2) {
+                max3 = max2;
+                max2 = s;
+                ind3 = ind2;
+                ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        s_keep[0] = ind1;
+        s_keep[1] = ind2;
+        s_keep[2] = ind3;
+    }
+    __syncthreads();
+    int drop = 0;
+    for (int r = tid; r < nm; r += nt) {
+        const int b = rbin[r];
+        if (b == s_keep[0] || b == s_keep[1] || b == s_keep[2]) continue;
+        out[rec[r]] = -1;
+        drop++;
+    }
+    atomicSub(s_nm, drop);
+    __syncthreads();
+}
+
 struct BowPair {
     gf_bow_side a, b;
     int32_t* out;
@@ -314,51 +364,215 @@ __global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ p
     }
     __syncthreads();
     const int nm = s_nm;
-    if (check_ori) {  // ComputeThreeMaxima (ORBmatcher.cc:2338-2379)
-        for (int r = tid; r < nm; r += 256) atomicAdd(&s_hist[rbin[r]], 1);
-        __syncthreads();
-        if (tid == 0) {
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < HISTO_LENGTH; i++) {
-                const int s = s_hist[i];
-                if (s > max1) {
-                    max3 = max2;
-                    max2 = max1;
-                    max1 = s;
-                    ind3 = ind2;
-                    ind2 = ind1;
-                    ind1 = i;
-                } else if (s > max2) {
-                    max3 = max2;
-                    max2 = s;
-                    ind3 = ind2;
-                    ind2 = i;
-                } else if (s > max3) {
-                    max3 = s;
-                    ind3 = i;
+    if (check_ori) rotation_filter(nm, rbin, rec, P.out, s_hist, s_keep, &s_nm);
+    if (tid == 0) nmatches[blockIdx.x] = s_nm;
+}
+
+// SearchForTriangulation (ORBmatcher.cc:1426-1588): same node walk as
+// SearchByBoW, but over keypoints WITHOUT a map point. Per a feature: best =
+// min distance over unclaimed b candidates with d <= TH_LOW; the reference
+// sorts (dist, idx2) and takes the first within round(2 best) passing the
+// epipolar test, i.e. the (dist, idx2)-least passing candidate with
+// d <= min(TH_LOW, 2 best): two wave reductions.
+struct TriPair {
+    gf_bow_side a, b;
+    float F[9];
+    float sigma2[16];
+    int32_t nlevels;
+    int32_t* out;
+};
+
+__device__ __forceinline__ bool epipolar_ok(float a, float b, float c, const gf_keypoint& kp2, const TriPair& P) {
+    // CheckDistEpipolarLine (ORBmatcher.cc:705-722)
+    const float num = a * kp2.x + b * kp2.y + c;
+    const float den = a * a + b * b;
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    const int o = min(max(kp2.octave, 0), P.nlevels - 1);
+    return (double)dsqr < 3.84 * (double)P.sigma2[o];
+}
+
+#define TRI_THREADS 1024
+#define TRI_CT 4  // b candidates per lane held in registers (nodes of <= 256 b features)
+
+__device__ __forceinline__ int hamming_r(const uint4 a0, const uint4 a1, const uint8_t* b) {
+    const uint4 b0 = ((const uint4*)b)[0], b1 = ((const uint4*)b)[1];
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Match step of one a feature against the node's b candidates: best over the
+// unclaimed (d <= TH_LOW), then the (d, idx)-least epipolar-passing one with
+// d <= 2 best. Returns the b index or -1 (wave-uniform).
+__device__ __forceinline__ int tri_pick(const int* d, const int* idx, const bool* ok, int n, float la, float lb,
+                                        float lc, const gf_keypoint* kps, const TriPair& P) {
+    int best = INT_MAX;
+    for (int t = 0; t < n; t++)
+        if (ok[t] && d[t] <= 50) best = min(best, d[t]);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) best = min(best, __shfl_xor(best, o, 64));
+    if (best == INT_MAX) return -1;
+    const int dth = min(2 * best, 50);  // round(2 * BestDist) is exact
+    unsigned key = 0xffffffffu;
+    for (int t = 0; t < n; t++) {
+        if (!ok[t] || d[t] > dth) continue;
+        const unsigned k = ((unsigned)d[t] << 16) | (unsigned)idx[t];
+        if (k < key && epipolar_ok(la, lb, lc, kps[idx[t]], P)) key = k;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) key = min(key, (unsigned)__shfl_xor((int)key, o, 64));
+    return key == 0xffffffffu ? -1 : (int)(key & 0xffffu);
+}
+
+__global__ __launch_bounds__(TRI_THREADS) void k_search_tri(const TriPair* __restrict__ pairs, int check_ori,
+                                                            int32_t* __restrict__ nmatches) {
+    __shared__ uint8_t claimed[BOW_MAX];
+    __shared__ int2 common[BOW_MAX];
+    __shared__ int rec[BOW_MAX];
+    __shared__ uint8_t rbin[BOW_MAX];
+    __shared__ int s_nc, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
+    __shared__ int st_idx[TRI_THREADS / 64][64];
+    __shared__ uint4 st_desc[TRI_THREADS / 64][64][2];
+    __shared__ float3 st_kp[TRI_THREADS / 64][64];
+    const TriPair& P = pairs[blockIdx.x];
+    const gf_bow_side& A = P.a;
+    const gf_bow_side& B = P.b;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, nw = TRI_THREADS / 64;
+    for (int i = tid; i < A.n; i += TRI_THREADS) P.out[i] = -1;
+    for (int i = tid; i < B.n; i += TRI_THREADS) claimed[i] = 0;
+    if (tid == 0) s_nc = s_nm = 0;
+    if (tid < HISTO_LENGTH) s_hist[tid] = 0;
+    __syncthreads();
+    for (int ib = tid; ib < B.nfv; ib += TRI_THREADS) {
+        const int key = B.fv_nodes[ib];
+        int lo = 0, hi = A.nfv;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (A.fv_nodes[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo < A.nfv && A.fv_nodes[lo] == key) common[atomicAdd(&s_nc, 1)] = make_int2(lo, ib);
+    }
+    __syncthreads();
+    const int nc = s_nc;
+    const float factor = 1.0f / HISTO_LENGTH;
+    const float* F = P.F;
+    for (int c = w; c < nc; c += nw) {
+        const int ia = common[c].x, ib = common[c].y;
+        const int as = A.fv_start[ia], ae = A.fv_start[ia + 1], bs = B.fv_start[ib], be = B.fv_start[ib + 1];
+        // a b feature sits in exactly one node, so only this wave claims it:
+        // for nodes of <= 64 TRI_CT b features the candidates and their claim
+        // flags stay in registers for the whole walk
+        const bool regs = be - bs <= 64 * TRI_CT;
+        uint4 cd[TRI_CT][2];
+        int cidx[TRI_CT];
+        bool cok[TRI_CT];
+        if (regs) {
+#pragma unroll
+            for (int t = 0; t < TRI_CT; t++) {
+                const int y = bs + lane + 64 * t;
+                cok[t] = false;
+                cidx[t] = 0;
+                if (y < be) {
+                    cidx[t] = B.fv_feats[y];
+                    cok[t] = B.mp[cidx[t]] < 0;  // no MapPoint yet (:1484-1486)
+                    const uint4* q = (const uint4*)(B.desc + (size_t)cidx[t] * 32);
+                    cd[t][0] = q[0];
+                    cd[t][1] = q[1];
                 }
             }
-            if (max2 < 0.1f * (float)max1) {
-                ind2 = -1;
-                ind3 = -1;
-            } else if (max3 < 0.1f * (float)max1) {
-                ind3 = -1;
+        }
+        // the node's a features are staged into LDS 64 at a time (one parallel
+        // load), so the sequential walk reads LDS instead of chained global loads
+        for (int x0 = as; x0 < ae; x0 += 64) {
+        {
+            const int x = x0 + lane;
+            int idx = -1;
+            if (x < ae) {
+                idx = A.fv_feats[x];
+                if (A.mp[idx] >= 0) idx = -1;  // already has a MapPoint (:1466-1468)
             }
-            s_keep[0] = ind1;
-            s_keep[1] = ind2;
-            s_keep[2] = ind3;
+            st_idx[w][lane] = idx;
+            if (idx >= 0) {
+                const uint4* q = (const uint4*)(A.desc + (size_t)idx * 32);
+                st_desc[w][lane][0] = q[0];
+                st_desc[w][lane][1] = q[1];
+                const gf_keypoint k = A.kps[idx];
+                st_kp[w][lane] = make_float3(k.x, k.y, k.angle);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        __syncthreads();
-        int drop = 0;
-        for (int r = tid; r < nm; r += 256) {
-            const int b = rbin[r];
-            if (b == s_keep[0] || b == s_keep[1] || b == s_keep[2]) continue;
-            P.out[rec[r]] = -1;
-            drop++;
+        const int xn = min(64, ae - x0);
+        for (int xi = 0; xi < xn; xi++) {
+            const int idxA = st_idx[w][xi];
+            if (idxA < 0) continue;
+            const uint4 a0 = st_desc[w][xi][0], a1 = st_desc[w][xi][1];
+            const float3 kp1 = st_kp[w][xi];
+            // epipolar line l = x1' F12 (:708-710)
+            const float la = kp1.x * F[0] + kp1.y * F[3] + F[6];
+            const float lb = kp1.x * F[1] + kp1.y * F[4] + F[7];
+            const float lc = kp1.x * F[2] + kp1.y * F[5] + F[8];
+            int bestB;
+            if (regs) {
+                int d[TRI_CT];
+#pragma unroll
+                for (int t = 0; t < TRI_CT; t++)
+                    d[t] = __popc(a0.x ^ cd[t][0].x) + __popc(a0.y ^ cd[t][0].y) + __popc(a0.z ^ cd[t][0].z) +
+                           __popc(a0.w ^ cd[t][0].w) + __popc(a1.x ^ cd[t][1].x) + __popc(a1.y ^ cd[t][1].y) +
+                           __popc(a1.z ^ cd[t][1].z) + __popc(a1.w ^ cd[t][1].w);
+                bestB = tri_pick(d, cidx, cok, TRI_CT, la, lb, lc, B.kps, P);
+                if (bestB < 0) continue;
+#pragma unroll
+                for (int t = 0; t < TRI_CT; t++)
+                    if (cidx[t] == bestB) cok[t] = false;
+            } else {  // large node: stream the candidates from memory, claims in LDS
+                int best = INT_MAX;
+                for (int y = bs + lane; y < be; y += 64) {
+                    const int idxB = B.fv_feats[y];
+                    if (claimed[idxB] || B.mp[idxB] >= 0) continue;
+                    const int dd = hamming_r(a0, a1, B.desc + (size_t)idxB * 32);
+                    if (dd <= 50) best = min(best, dd);
+                }
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) best = min(best, __shfl_xor(best, o, 64));
+                if (best == INT_MAX) continue;
+                const int dth = min(2 * best, 50);
+                unsigned key = 0xffffffffu;
+                for (int y = bs + lane; y < be; y += 64) {
+                    const int idxB = B.fv_feats[y];
+                    if (claimed[idxB] || B.mp[idxB] >= 0) continue;
+                    const int dd = hamming_r(a0, a1, B.desc + (size_t)idxB * 32);
+                    if (dd > dth) continue;
+                    const unsigned k = ((unsigned)dd << 16) | (unsigned)idxB;
+                    if (k < key && epipolar_ok(la, lb, lc, B.kps[idxB], P)) key = k;
+                }
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) key = min(key, (unsigned)__shfl_xor((int)key, o, 64));
+                if (key == 0xffffffffu) continue;
+                bestB = (int)(key & 0xffffu);
+                if (lane == 0) claimed[bestB] = 1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (lane == 0) {
+                P.out[idxA] = bestB;
+                const int r = atomicAdd(&s_nm, 1);
+                rec[r] = idxA;
+                float rot = kp1.z - B.kps[bestB].angle;  // kp1.angle - kp2.angle
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == HISTO_LENGTH) bin = 0;
+                rbin[r] = (uint8_t)bin;
+            }
         }
-        atomicSub(&s_nm, drop);
-        __syncthreads();
+        }
     }
+    __syncthreads();
+    const int nm = s_nm;
+    if (check_ori) rotation_filter(nm, rbin, rec, P.out, s_hist, s_keep, &s_nm);
     if (tid == 0) nmatches[blockIdx.x] = s_nm;
 }
 
@@ -549,13 +763,12 @@ int gf_match_bow_dev(gf_ctx* ctx, int mode, float nnratio, int check_ori, int np
     return GF_OK;
 }
 
-int gf_match_bow(gf_ctx* ctx, int mode, float nnratio, int check_ori, const gf_bow_side* a, const gf_bow_side* b,
-                 int32_t* out, int* nmatches) {
-    GF_CHECK(ctx && a && b && out && nmatches, GF_ERR_ARG, "null arg");
-    GF_CHECK(a->n <= BOW_MAX && b->n <= BOW_MAX, GF_ERR_UNSUPPORTED, "at most 4096 features per side");
-    GF_HIP(hipSetDevice(ctx->device));
-    // stage both sides in one scratch block
-    gf_bow_side sd[2] = {*a, *b};
+// Copies both sides of a host pair into one scratch block (slot 53); sd
+// receives the device views, dout / dnm the output vector and count.
+static int stage_bow_pair(gf_ctx* ctx, const gf_bow_side* a, const gf_bow_side* b, int nout, gf_bow_side sd[2],
+                          int32_t** dout, int32_t** dnm) {
+    sd[0] = *a;
+    sd[1] = *b;
     size_t off = 0;
     std::vector<std::pair<const void*, size_t>> parts;
     auto add = [&](const void* h, size_t bytes) {
@@ -570,7 +783,6 @@ int gf_match_bow(gf_ctx* ctx, int mode, float nnratio, int check_ori, const gf_b
     size_t o_bn = add(b->fv_nodes, 4 * (size_t)b->nfv), o_bs = add(b->fv_start, 4 * (size_t)(b->nfv + 1)),
            o_bf = add(b->fv_feats, 4 * (size_t)b->n), o_bd = add(b->desc, 32 * (size_t)b->n),
            o_bk = add(b->kps, sizeof(gf_keypoint) * (size_t)b->n), o_bm = add(b->mp, 4 * (size_t)b->n);
-    const int nout = mode == 0 ? b->n : a->n;
     const size_t o_out = add(nullptr, 4 * (size_t)std::max(nout, 1)), o_nm = add(nullptr, 4);
     void* dbuf;
     int rc = gf::ws_get(ctx, 53, off, &dbuf);
@@ -593,16 +805,81 @@ int gf_match_bow(gf_ctx* ctx, int mode, float nnratio, int check_ori, const gf_b
     sd[1].desc = base + o_bd;
     sd[1].kps = (const gf_keypoint*)(base + o_bk);
     sd[1].mp = (const int32_t*)(base + o_bm);
-    int32_t* dout = (int32_t*)(base + o_out);
-    rc = gf_match_bow_dev(ctx, mode, nnratio, check_ori, 1, &sd[0], &sd[1], &dout, (int32_t*)(base + o_nm),
-                          ctx->stream);
-    if (rc) return rc;
+    *dout = (int32_t*)(base + o_out);
+    *dnm = (int32_t*)(base + o_nm);
+    return GF_OK;
+}
+
+static int fetch_bow_result(gf_ctx* ctx, int nout, const int32_t* dout, const int32_t* dnm, int32_t* out,
+                            int* nmatches) {
     int32_t nm = 0;
     if (nout) GF_HIP(hipMemcpyAsync(out, dout, 4 * (size_t)nout, hipMemcpyDeviceToHost, ctx->stream));
-    GF_HIP(hipMemcpyAsync(&nm, base + o_nm, 4, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP(hipMemcpyAsync(&nm, dnm, 4, hipMemcpyDeviceToHost, ctx->stream));
     GF_HIP(hipStreamSynchronize(ctx->stream));
     *nmatches = nm;
     return GF_OK;
+}
+
+int gf_match_bow(gf_ctx* ctx, int mode, float nnratio, int check_ori, const gf_bow_side* a, const gf_bow_side* b,
+                 int32_t* out, int* nmatches) {
+    GF_CHECK(ctx && a && b && out && nmatches, GF_ERR_ARG, "null arg");
+    GF_CHECK(a->n <= BOW_MAX && b->n <= BOW_MAX, GF_ERR_UNSUPPORTED, "at most 4096 features per side");
+    GF_HIP(hipSetDevice(ctx->device));
+    const int nout = mode == 0 ? b->n : a->n;
+    gf_bow_side sd[2];
+    int32_t *dout, *dnm;
+    int rc = stage_bow_pair(ctx, a, b, nout, sd, &dout, &dnm);
+    if (rc) return rc;
+    rc = gf_match_bow_dev(ctx, mode, nnratio, check_ori, 1, &sd[0], &sd[1], &dout, dnm, ctx->stream);
+    if (rc) return rc;
+    return fetch_bow_result(ctx, nout, dout, dnm, out, nmatches);
+}
+
+int gf_search_for_triangulation_dev(gf_ctx* ctx, int check_ori, int npairs, const gf_bow_side* a,
+                                    const gf_bow_side* b, const float* F12, const float* sigma2_b, int nlevels,
+                                    int32_t* const* outs, int32_t* d_nmatches, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    if (npairs <= 0) return GF_OK;
+    GF_CHECK(a && b && F12 && sigma2_b && outs && d_nmatches, GF_ERR_ARG, "null arg");
+    GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels must be in 1..16");
+    std::vector<TriPair> T(npairs);
+    for (int p = 0; p < npairs; p++) {
+        GF_CHECK(a[p].n >= 0 && b[p].n >= 0 && a[p].n <= BOW_MAX && b[p].n <= BOW_MAX && a[p].nfv <= a[p].n &&
+                     b[p].nfv <= b[p].n,
+                 GF_ERR_UNSUPPORTED, "at most 4096 features per side");
+        T[p] = TriPair{};
+        T[p].a = a[p];
+        T[p].b = b[p];
+        for (int i = 0; i < 9; i++) T[p].F[i] = F12[9 * p + i];
+        for (int i = 0; i < nlevels; i++) T[p].sigma2[i] = sigma2_b[i];
+        T[p].nlevels = nlevels;
+        T[p].out = outs[p];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    void* dp;
+    int rc = gf::ws_get(ctx, 60, sizeof(TriPair) * npairs, &dp);
+    if (rc) return rc;
+    GF_HIP(hipMemcpyAsync(dp, T.data(), sizeof(TriPair) * npairs, hipMemcpyHostToDevice, s));
+    GF_PROF(ctx, s, "k_search_tri");
+    k_search_tri<<<npairs, TRI_THREADS, 0, s>>>((const TriPair*)dp, check_ori, d_nmatches);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_search_for_triangulation(gf_ctx* ctx, int check_ori, const gf_bow_side* a, const gf_bow_side* b,
+                                const float* F12, const float* sigma2_b, int nlevels, int32_t* out, int* nmatches) {
+    GF_CHECK(ctx && a && b && F12 && sigma2_b && nmatches && (a->n == 0 || out), GF_ERR_ARG, "null arg");
+    GF_CHECK(a->n >= 0 && b->n >= 0 && a->n <= BOW_MAX && b->n <= BOW_MAX, GF_ERR_UNSUPPORTED,
+             "at most 4096 features per side");
+    GF_HIP(hipSetDevice(ctx->device));
+    gf_bow_side sd[2];
+    int32_t *dout, *dnm;
+    int rc = stage_bow_pair(ctx, a, b, a->n, sd, &dout, &dnm);
+    if (rc) return rc;
+    rc = gf_search_for_triangulation_dev(ctx, check_ori, 1, &sd[0], &sd[1], F12, sigma2_b, nlevels, &dout, dnm,
+                                         ctx->stream);
+    if (rc) return rc;
+    return fetch_bow_result(ctx, a->n, dout, dnm, out, nmatches);
 }
 
 }  // extern "C"

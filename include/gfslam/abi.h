@@ -505,6 +505,85 @@ int gf_undistort_keypoints(gf_ctx* ctx, const float K[4], const float dist[5], c
 int gf_undistort_keypoints_dev(gf_ctx* ctx, int nframes, const float K[4], const float dist[5],
                                const gf_keypoint* d_in, const int32_t* d_n, int cap, gf_keypoint* d_out, void* stream);
 
+/* ------------------------------------------ local-mapping matchers (§8f rank 3)
+ * MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:197-262) for nmp
+ * map points at once: point p's observation descriptors (non-bad keyframes,
+ * observation-map order) are rows offsets[p] .. offsets[p+1]-1 of desc
+ * (offsets has nmp + 1 entries, offsets[0] = 0). best[p] = the row (relative
+ * to offsets[p]) with the least median Hamming distance to the others, -1 for
+ * a point without observations; out_desc (optional, nmp x 32, in/out)
+ * receives that row (mDescriptor), untouched for an empty point. */
+int gf_distinctive_descriptors(gf_ctx* ctx, int nmp, const uint8_t* desc, const int32_t* offsets, int32_t* best,
+                               uint8_t* out_desc);
+/* Device family: total = offsets[nmp] (host value: sizes the row grid). */
+int gf_distinctive_descriptors_dev(gf_ctx* ctx, int nmp, const uint8_t* d_desc, const int32_t* d_offsets,
+                                   int32_t* d_best, uint8_t* d_out_desc, int total, void* stream);
+
+/* ORBmatcher::Fuse(KeyFrame* pKF, vector<MapPoint*>& vpMapPoints, th)
+ * (src/ORBmatcher.cc:1590-1707). The keyframe: bounds/intrinsics/pyramid in
+ * fi, pose Tcw (row-major 4x4), camera centre Ow (KeyFrame::GetCameraCenter),
+ * undistorted keypoints, descriptors, kf_mp[k] = id of the map point at slot k
+ * (-1 none) and kf_mp_bad[k] its isBad() (optional). The candidates:
+ * gf_map_point (mfMin/MaxDistance are the invariance distances), descriptors,
+ * mp_skip[i] (optional) = NULL / isBad() / IsInKeyFrame(pKF), mp_ids[i]
+ * (optional, default i) the id reported as a Replace() target. Result per
+ * candidate in list order:
+ *   kp      keypoint fused with (bestDist <= TH_LOW) or -1;
+ *   action  GF_FUSE_ADD      pMP->AddObservation(pKF, kp), pKF->AddMapPoint;
+ *           GF_FUSE_REPLACE  pMP->Replace(target): target is the slot's
+ *                            occupant, or the earlier candidate that took the
+ *                            empty slot in this call;
+ *           GF_FUSE_KEEP     the occupant isBad(): nothing changes;
+ *   nfused = number of candidates with kp >= 0 (the reference's nFused). */
+enum { GF_FUSE_NONE = 0, GF_FUSE_ADD = 1, GF_FUSE_REPLACE = 2, GF_FUSE_KEEP = 3 };
+typedef struct gf_fuse_result {
+    int32_t kp, action, target;
+} gf_fuse_result;
+int gf_fuse(gf_ctx* ctx, const gf_frame_info* fi, const float* Tcw, const float* Ow, const gf_keypoint* kps,
+            const uint8_t* desc, int n, const int32_t* kf_mp, const uint8_t* kf_mp_bad, const gf_map_point* mps,
+            const uint8_t* mp_desc, const uint8_t* mp_skip, const int32_t* mp_ids, int m, float th,
+            gf_fuse_result* res, int* nfused);
+/* Device family: nprob independent (keyframe, candidate list) problems that
+ * share fi; every pointer in a problem is a device pointer (the array itself
+ * is host memory, copied at the call). At most 4096 keypoints per keyframe. */
+typedef struct gf_fuse_problem {
+    float Tcw[16];
+    float Ow[3];
+    const gf_keypoint* kps;
+    const uint8_t* desc;
+    int32_t n;
+    const int32_t* kf_mp;
+    const uint8_t* kf_mp_bad;
+    const gf_map_point* mps;
+    const uint8_t* mp_desc;
+    const uint8_t* mp_skip;
+    const int32_t* mp_ids;
+    int32_t m;
+    float th;
+    gf_fuse_result* res;
+    int32_t* nfused;
+} gf_fuse_problem;
+int gf_fuse_dev(gf_ctx* ctx, const gf_frame_info* fi, int nprob, const gf_fuse_problem* probs, void* stream);
+
+/* ORBmatcher::SearchForTriangulation(pKF1, pKF2, F12, ...) (src/ORBmatcher.cc:
+ * 1426-1588): keypoints of a (pKF1) and b (pKF2) without a map point
+ * (mp < 0) that share a FeatureVector node; best distance <= TH_LOW, the
+ * candidates within 2x the best walked in (distance, index) order, the first
+ * passing CheckDistEpipolarLine (:705-722: squared distance to the epipolar
+ * line x1' F12 < 3.84 sigma2_b[octave]) matches; rotation consistency when
+ * check_ori. F12 row-major 3x3; sigma2_b = pKF2's mvLevelSigma2 (nlevels <= 16).
+ * out[i] (a.n entries) = the b keypoint matched to a keypoint i or -1
+ * (vMatches12; vMatchedPairs are its non-negative entries in order). */
+int gf_search_for_triangulation(gf_ctx* ctx, int check_ori, const gf_bow_side* a, const gf_bow_side* b,
+                                const float* F12, const float* sigma2_b, int nlevels, int32_t* out, int* nmatches);
+/* Device family: npairs independent (a[p], b[p]) keyframe pairs (device
+ * pointers; LocalMapping::CreateNewMapPoints pairs the new keyframe with each
+ * covisible neighbour), F12 host array of npairs x 9, one sigma2 table,
+ * outs[p] device output of pair p, d_nmatches[p]. One workgroup per pair. */
+int gf_search_for_triangulation_dev(gf_ctx* ctx, int check_ori, int npairs, const gf_bow_side* a,
+                                    const gf_bow_side* b, const float* F12, const float* sigma2_b, int nlevels,
+                                    int32_t* const* outs, int32_t* d_nmatches, void* stream);
+
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end
  * step stays on the device. One workgroup per frame.

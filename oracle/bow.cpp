@@ -8,7 +8,8 @@
 //     (ScoringObject.h:74-89);
 //   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (src/ORBmatcher.cc:724-853)
 //   and SearchByBoW(KeyFrame*, KeyFrame*, ...) (:1289-1424) with
-//   ComputeThreeMaxima (:2338-2379).
+//   ComputeThreeMaxima (:2338-2379);
+//   SearchForTriangulation (:1426-1588) with CheckDistEpipolarLine (:705-722).
 // The vocabulary tree arrives as the loaders build it (node 0 = root, nodes
 // in record order, children in record order, word ids in record order of the
 // leaves). DBoW2 is vendored, so these rows restate vendored text; parity is
@@ -78,6 +79,8 @@ struct Vocab {
 };
 
 }  // namespace
+
+void three_maxima(const int* histo, int L, int& ind1, int& ind2, int& ind3);  // match.cpp
 }  // namespace orc
 
 extern "C" {
@@ -235,6 +238,88 @@ int orc_match_bow(int mode, float nnratio, int check_ori, const int32_t* a_nodes
         for (int i = 0; i < HISTO_LENGTH; i++) {
             if (i == ind1 || i == ind2 || i == ind3) continue;
             for (int j : rotHist[i]) {
+                out[j] = -1;
+                nm--;
+            }
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchForTriangulation(pKF1 = a, pKF2 = b, F12, ...)
+// (ORBmatcher.cc:1426-1588). out[a index] = matched b index (vMatches12).
+int orc_search_triangulation(int check_ori, const int32_t* a_nodes, const int32_t* a_start, const int32_t* a_feats,
+                             int a_nn, const uint8_t* a_desc, const gf_keypoint* a_kps, const int32_t* a_mp, int a_n,
+                             const int32_t* b_nodes, const int32_t* b_start, const int32_t* b_feats, int b_nn,
+                             const uint8_t* b_desc, const gf_keypoint* b_kps, const int32_t* b_mp, int b_n,
+                             const float* F12, const float* sigma2_b, int32_t* out, int* nmatches) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    auto epipolar = [&](const gf_keypoint& kp1, const gf_keypoint& kp2) {  // CheckDistEpipolarLine
+        const float a = kp1.x * F12[0] + kp1.y * F12[3] + F12[6];
+        const float b = kp1.x * F12[1] + kp1.y * F12[4] + F12[7];
+        const float c = kp1.x * F12[2] + kp1.y * F12[5] + F12[8];
+        const float num = a * kp2.x + b * kp2.y + c;
+        const float den = a * a + b * b;
+        if (den == 0) return false;
+        const float dsqr = num * num / den;
+        return dsqr < 3.84 * sigma2_b[kp2.octave];
+    };
+    std::vector<char> vbMatched2(b_n, 0);
+    for (int i = 0; i < a_n; i++) out[i] = -1;
+    std::vector<int> rotHist[30];
+    const float factor = 1.0f / HISTO_LENGTH;
+    int nm = 0, ia = 0, ib = 0;
+    while (ia < a_nn && ib < b_nn) {
+        if (a_nodes[ia] == b_nodes[ib]) {
+            for (int x = a_start[ia]; x < a_start[ia + 1]; x++) {
+                const int idx1 = a_feats[x];
+                if (a_mp[idx1] >= 0) continue;
+                std::vector<std::pair<int, int>> vDistIndex;
+                for (int y = b_start[ib]; y < b_start[ib + 1]; y++) {
+                    const int idx2 = b_feats[y];
+                    if (vbMatched2[idx2] || b_mp[idx2] >= 0) continue;
+                    const int dist = orc::hamming(a_desc + 32 * (size_t)idx1, b_desc + 32 * (size_t)idx2);
+                    if (dist > TH_LOW) continue;
+                    vDistIndex.push_back({dist, idx2});
+                }
+                if (vDistIndex.empty()) continue;
+                std::sort(vDistIndex.begin(), vDistIndex.end());
+                const int BestDist = vDistIndex.front().first;
+                const int DistTh = (int)std::round(2 * BestDist);
+                for (const auto& di : vDistIndex) {
+                    if (di.first > DistTh) break;
+                    const int idx2 = di.second;
+                    if (epipolar(a_kps[idx1], b_kps[idx2])) {
+                        vbMatched2[idx2] = 1;
+                        out[idx1] = idx2;
+                        nm++;
+                        if (check_ori) {
+                            float rot = a_kps[idx1].angle - b_kps[idx2].angle;
+                            if (rot < 0.0) rot += 360.0f;
+                            int bin = (int)std::round(rot * factor);
+                            if (bin == HISTO_LENGTH) bin = 0;
+                            rotHist[bin].push_back(idx1);
+                        }
+                        break;
+                    }
+                }
+            }
+            ia++;
+            ib++;
+        } else if (a_nodes[ia] < b_nodes[ib]) {
+            ia = (int)(std::lower_bound(a_nodes + ia, a_nodes + a_nn, b_nodes[ib]) - a_nodes);
+        } else {
+            ib = (int)(std::lower_bound(b_nodes + ib, b_nodes + b_nn, a_nodes[ia]) - b_nodes);
+        }
+    }
+    if (check_ori) {
+        int sizes[30], i1, i2, i3;
+        for (int b = 0; b < HISTO_LENGTH; b++) sizes[b] = (int)rotHist[b].size();
+        orc::three_maxima(sizes, HISTO_LENGTH, i1, i2, i3);
+        for (int b = 0; b < HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int j : rotHist[b]) {
                 out[j] = -1;
                 nm--;
             }

@@ -1,5 +1,8 @@
 // CPU ORACLE (test infrastructure) — matching rows E8, M1-M3, M7 of
-// SURVEY.md §8a, restated sequentially from src/ORBmatcher.cc and src/Frame.cc.
+// SURVEY.md §8a, restated sequentially from src/ORBmatcher.cc and src/Frame.cc,
+// and the local-mapping rows of §8(f) rank 3: MapPoint::ComputeDistinctive-
+// Descriptors (src/MapPoint.cc:197-262) and ORBmatcher::Fuse (:1590-1707).
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstring>
@@ -284,6 +287,111 @@ int orc_match_lastframe(const gf_frame_info* fi, const gf_keypoint* kps, const u
         }
     }
     *nmatches = nm;
+    return GF_OK;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:227-261) for nmp
+// points: the float N x N distance table, each row copied to vector<int> and
+// sorted, median = row[0.5 * (N - 1)], strict < keeps the first minimum.
+int orc_distinctive_descriptors(int nmp, const uint8_t* desc, const int32_t* offsets, int32_t* best,
+                                uint8_t* out_desc) {
+    for (int p = 0; p < nmp; p++) {
+        const int o = offsets[p], N = offsets[p + 1] - o;
+        best[p] = -1;
+        if (N <= 0) continue;
+        std::vector<float> D((size_t)N * N);
+        for (int i = 0; i < N; i++) {
+            D[(size_t)i * N + i] = 0;
+            for (int j = i + 1; j < N; j++) {
+                const int d = orc::descriptor_distance(desc + 32 * (size_t)(o + i), desc + 32 * (size_t)(o + j));
+                D[(size_t)i * N + j] = (float)d;
+                D[(size_t)j * N + i] = (float)d;
+            }
+        }
+        int BestMedian = INT_MAX, BestIdx = 0;
+        for (int i = 0; i < N; i++) {
+            std::vector<int> v(D.begin() + (size_t)i * N, D.begin() + (size_t)(i + 1) * N);
+            std::sort(v.begin(), v.end());
+            const int median = v[(size_t)(0.5 * (N - 1))];
+            if (median < BestMedian) {
+                BestMedian = median;
+                BestIdx = i;
+            }
+        }
+        best[p] = BestIdx;
+        if (out_desc) std::memcpy(out_desc + 32 * (size_t)p, desc + 32 * (size_t)(o + BestIdx), 32);
+    }
+    return GF_OK;
+}
+
+// ORBmatcher::Fuse(KeyFrame*, vector<MapPoint*>&, th) (ORBmatcher.cc:1590-1707),
+// walked in list order with the keyframe's slots updated as the reference
+// does (AddMapPoint fills a slot; Replace() leaves the slot's occupant).
+int orc_fuse(const gf_frame_info* fi, const float* Tcw, const float* Ow, const gf_keypoint* kps,
+             const uint8_t* desc, int n, const int32_t* kf_mp, const uint8_t* kf_mp_bad, const gf_map_point* mps,
+             const uint8_t* mp_desc, const uint8_t* mp_skip, const int32_t* mp_ids, int m, float th,
+             gf_fuse_result* res, int* nfused) {
+    orc::FrameGrid G(fi, kps, n);
+    const int nMaxLevel = fi->nlevels - 1;
+    // slot -> (occupant id, occupant bad); list-point occupants are not bad
+    std::vector<int> occ(kf_mp, kf_mp + n);
+    std::vector<char> bad(n, 0);
+    if (kf_mp_bad)
+        for (int k = 0; k < n; k++) bad[k] = (char)kf_mp_bad[k];
+    int nFused = 0;
+    for (int i = 0; i < m; i++) {
+        res[i] = gf_fuse_result{-1, GF_FUSE_NONE, -1};
+        if (mp_skip && mp_skip[i]) continue;
+        const gf_map_point& mp = mps[i];
+        float Pc[3];
+        orc::transform(Tcw, mp.pos, Pc);
+        if (Pc[2] < 0.0f) continue;
+        const float invz = 1 / Pc[2];
+        const float x = Pc[0] * invz;
+        const float y = Pc[1] * invz;
+        const float u = fi->fx * x + fi->cx;
+        const float v = fi->fy * y + fi->cy;
+        if (!(u >= fi->min_x && u < fi->max_x && v >= fi->min_y && v < fi->max_y)) continue;  // KeyFrame::IsInImage
+        const float maxDistance = mp.max_dist, minDistance = mp.min_dist;
+        const float PO[3] = {mp.pos[0] - Ow[0], mp.pos[1] - Ow[1], mp.pos[2] - Ow[2]};
+        const float dist3D = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const double dot = (double)PO[0] * mp.normal[0] + (double)PO[1] * mp.normal[1] + (double)PO[2] * mp.normal[2];
+        if (dot < 0.5 * dist3D) continue;
+        const float ratio = dist3D / minDistance;
+        const int lb = (int)(std::lower_bound(G.scales.begin(), G.scales.end(), ratio) - G.scales.begin());
+        const int nPredictedLevel = std::min(lb, nMaxLevel);
+        const float radius = th * G.scales[nPredictedLevel];
+        const std::vector<int> idxs = G.area(u, v, radius, -1, -1);  // KeyFrame::GetFeaturesInArea
+        if (idxs.empty()) continue;
+        int bestDist = INT_MAX, bestIdx = -1;
+        for (int idx : idxs) {
+            const int kpLevel = kps[idx].octave;
+            if (kpLevel < nPredictedLevel - 1 || kpLevel > nPredictedLevel) continue;
+            const int dist = orc::descriptor_distance(mp_desc + 32 * (size_t)i, desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx = idx;
+            }
+        }
+        if (bestDist <= orc::TH_LOW) {
+            gf_fuse_result& r = res[i];
+            r.kp = bestIdx;
+            if (occ[bestIdx] >= 0) {
+                if (!bad[bestIdx]) {
+                    r.action = GF_FUSE_REPLACE;  // pMP->Replace(pMPinKF)
+                    r.target = occ[bestIdx];
+                } else {
+                    r.action = GF_FUSE_KEEP;
+                }
+            } else {
+                r.action = GF_FUSE_ADD;
+                occ[bestIdx] = mp_ids ? mp_ids[i] : i;
+            }
+            nFused++;
+        }
+    }
+    *nfused = nFused;
     return GF_OK;
 }
 

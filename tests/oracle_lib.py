@@ -255,3 +255,50 @@ def undistort_keypoints(kps, K, dist):
     d[:len(dist)] = np.asarray(dist, np.float32)
     assert orc().orc_undistort_keypoints(_p(Kf), _p(d), _p(k), len(k), _p(out)) == 0
     return out
+
+
+def distinctive_descriptors(desc, offsets):
+    """MapPoint::ComputeDistinctiveDescriptors on the CPU oracle: best row per point."""
+    d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    off = np.ascontiguousarray(offsets, np.int32)
+    nmp = len(off) - 1
+    best = np.zeros(max(nmp, 1), np.int32)
+    out = np.zeros((max(nmp, 1), 32), np.uint8)
+    assert orc().orc_distinctive_descriptors(nmp, _p(d), _p(off), _p(best), _p(out)) == 0
+    return best[:nmp], out[:nmp]
+
+
+def fuse(info, Tcw, Ow, kps, desc, kf_mp, kf_mp_bad, mps, mp_desc, mp_skip, mp_ids, th):
+    """ORBmatcher::Fuse on the CPU oracle: (nFused, results)."""
+    from gf_orb_slam_amd.matcher import FUSE_RESULT_DTYPE, MAP_POINT_DTYPE
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    res = np.zeros(len(mps), FUSE_RESULT_DTYPE)
+    opt = lambda a, dt: None if a is None else np.ascontiguousarray(a, dt)
+    n = ctypes.c_int()
+    T, O = np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(Ow, np.float32)
+    args = [ctypes.byref(info), _p(T), _p(O), _p(kps), _p(np.ascontiguousarray(desc, np.uint8)), len(kps),
+            _p(np.ascontiguousarray(kf_mp, np.int32)), _p(opt(kf_mp_bad, np.uint8)), _p(mps),
+            _p(np.ascontiguousarray(mp_desc, np.uint8)), _p(opt(mp_skip, np.uint8)), _p(opt(mp_ids, np.int32)),
+            len(mps), ctypes.c_float(th), _p(res), ctypes.byref(n)]
+    assert orc().orc_fuse(*args) == 0
+    return n.value, res
+
+
+def search_triangulation(check_ori, a, b, F12, sigma2):
+    """ORBmatcher::SearchForTriangulation on the CPU oracle: (n, vMatches12)."""
+    def side(s):
+        (nodes, start, feats), desc, kps, mp = s
+        return [np.ascontiguousarray(nodes, np.int32), np.ascontiguousarray(start, np.int32),
+                np.ascontiguousarray(feats, np.int32), np.ascontiguousarray(desc, np.uint8),
+                np.ascontiguousarray(kps, KEYPOINT_DTYPE), np.ascontiguousarray(mp, np.int32)]
+    A, B = side(a), side(b)
+    out = np.zeros(max(len(A[3]), 1), np.int32)
+    nm = ctypes.c_int()
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    s2 = np.ascontiguousarray(sigma2, np.float32)
+    assert orc().orc_search_triangulation(int(check_ori), _p(A[0]), _p(A[1]), _p(A[2]), len(A[0]), _p(A[3]),
+                                          _p(A[4]), _p(A[5]), len(A[3]), _p(B[0]), _p(B[1]), _p(B[2]), len(B[0]),
+                                          _p(B[3]), _p(B[4]), _p(B[5]), len(B[3]), _p(F), _p(s2), _p(out),
+                                          ctypes.byref(nm)) == 0
+    return nm.value, out[:len(A[3])].copy()
