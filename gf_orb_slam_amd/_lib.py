@@ -125,6 +125,9 @@ _PROTOS = {
     "gf_bow_transform_dev": [_P, _I, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P],
     "gf_match_bow": [_P, _I, _F, _I, _P, _P, _P, _P],
     "gf_match_bow_dev": [_P, _I, _F, _I, _I, _P, _P, _P, _P, _P],
+    "gf_pnp_init": [_I, _P, _P],
+    "gf_pnp_iterate": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P],
+    "gf_pnp_iterate_dev": [_P, _I, _P, _P, _P, _I, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P],
     "gf_local_ba": [_P, _P, _P],
     "gf_ba_plan_create": [_P, _I, _P, _P],
     "gf_ba_plan_solve": [_P, _P, _P],

@@ -584,6 +584,59 @@ int gf_search_for_triangulation_dev(gf_ctx* ctx, int check_ori, int npairs, cons
                                     const gf_bow_side* b, const float* F12, const float* sigma2_b, int nlevels,
                                     int32_t* const* outs, int32_t* d_nmatches, void* stream);
 
+/* ------------------------------------------------ relocalisation PnP
+ * ORB_SLAM::PnPsolver (src/PnPsolver.cc, include/PnPsolver.h): EPnP
+ * (Lepetit et al.) on random minimal sets inside RANSAC, then a refinement
+ * over the best inlier set; Tracking::Relocalization drives it
+ * (Tracking.cc:3916-3942: SetRansacParameters(0.99,10,300,4,0.5,5.991), then
+ * iterate(5) per candidate keyframe). A problem is the solver's correspondence
+ * list in PnPsolver order (ctor :50-72): p3d (n x 3 world points), p2d (n x 2
+ * undistorted keypoints), sigma2 (level sigma^2 of each keypoint octave). The
+ * keypoint-index mapping (mvKeyPointIndices) stays with the caller. */
+typedef struct gf_pnp_params { /* SetRansacParameters arguments (:93) */
+    double probability;
+    int32_t min_inliers;
+    int32_t max_iterations;
+    int32_t min_set; /* 4..8 */
+    float epsilon;
+    float th2;
+} gf_pnp_params;
+typedef struct gf_pnp_state { /* one solver across iterate() calls */
+    int32_t n;              /* N correspondences */
+    int32_t min_inliers;    /* mRansacMinInliers after the adjustment (:106-111) */
+    int32_t max_iterations; /* mRansacMaxIts after the adjustment (:116-124) */
+    int32_t min_set;        /* mRansacMinSet */
+    float epsilon;          /* mRansacEpsilon after the adjustment (:113-114) */
+    float th2;              /* mvMaxError[i] = sigma2[i] * th2 (:126-128) */
+    int32_t iterations;     /* mnIterations */
+    int32_t best_inliers;   /* mnBestInliers */
+    float best_Tcw[16];     /* mBestTcw, row-major */
+} gf_pnp_state;
+#define GF_PNP_FOUND 1   /* iterate returned a pose (refined or best)      */
+#define GF_PNP_NOMORE 2  /* bNoMore                                        */
+#define GF_PNP_REFINED 4 /* the pose came from Refine() (:198-208)         */
+/* PnPsolver::SetRansacParameters (host scalar set-up; resets the iteration
+ * count and the best hypothesis as a fresh solver has them). */
+int gf_pnp_init(int n, const gf_pnp_params* params, gf_pnp_state* state);
+/* PnPsolver::iterate(nIterations, bNoMore, vbInliers, nInliers) (:137-230)
+ * for one solver; rng is the process-wide std::rand() state the minimal sets
+ * are drawn from (DUtils::Random::RandomInt, :165), advanced by 4 draws per
+ * iteration run. best_mask (n bytes, mvbBestInliers) persists across calls
+ * with the state. Outputs: Tcw (row-major, valid when flags & FOUND), inliers
+ * (n bytes), ninliers, flags. */
+int gf_pnp_iterate(gf_ctx* ctx, const float* p3d, const float* p2d, const float* sigma2, const float K[4],
+                   gf_pnp_state* state, uint8_t* best_mask, int n_iterations, gf_rng* rng, float Tcw[16],
+                   uint8_t* inliers, int32_t* ninliers, int32_t* flags);
+/* Device batch: nprob independent solvers, problem b's correspondences at
+ * [b][cap] of d_p3d/d_p2d/d_sigma2/d_best_mask/d_inliers, its size in
+ * d_state[b].n; each problem draws from its own d_rng[b]. d_Tcw is [nprob][16].
+ * max_iterations bounds every problem's loop count (the params value it was
+ * initialised with). */
+int gf_pnp_iterate_dev(gf_ctx* ctx, int nprob, const float* d_p3d, const float* d_p2d, const float* d_sigma2,
+                       int cap, const float K[4], gf_pnp_state* d_state, uint8_t* d_best_mask, int n_iterations,
+                       int max_iterations, gf_rng* d_rng, float* d_Tcw, uint8_t* d_inliers, int32_t* d_ninliers,
+                       int32_t* d_flags, void* stream);
+
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end
  * step stays on the device. One workgroup per frame.

@@ -302,3 +302,26 @@ def search_triangulation(check_ori, a, b, F12, sigma2):
                                           _p(B[3]), _p(B[4]), _p(B[5]), len(B[3]), _p(F), _p(s2), _p(out),
                                           ctypes.byref(nm)) == 0
     return nm.value, out[:len(A[3])].copy()
+
+
+def pnp_run(p3d, p2d, sigma2, K, params, seed, n_iter):
+    """PnPsolver on the CPU oracle: std::srand(seed), then iterate(n_iter[c])
+    for each c. Returns (Tcw [c,4,4], inliers [c,n], ninliers, flags, rand_calls)."""
+    from gf_orb_slam_amd.pnp import PNP_PARAMS_DTYPE
+
+    p3d = np.ascontiguousarray(p3d, np.float32).reshape(-1, 3)
+    p2d = np.ascontiguousarray(p2d, np.float32).reshape(-1, 2)
+    s2 = np.ascontiguousarray(sigma2, np.float32).reshape(-1)
+    n = len(p3d)
+    c = len(n_iter)
+    it = np.ascontiguousarray(n_iter, np.int32)
+    prm = np.ascontiguousarray(params, PNP_PARAMS_DTYPE).reshape(1)
+    Kf = np.asarray(K, np.float32).reshape(4)
+    T = np.zeros((c, 4, 4), np.float32)
+    inl = np.zeros((c, max(n, 1)), np.uint8)
+    ninl = np.zeros(c, np.int32)
+    fl = np.zeros(c, np.int32)
+    rc = np.zeros(c, np.int32)
+    assert orc().orc_pnp_run(_p(p3d), _p(p2d), _p(s2), n, _p(Kf), _p(prm), ctypes.c_uint(seed), c, _p(it), _p(T),
+                             _p(inl), _p(ninl), _p(fl), _p(rc)) == 0
+    return T, inl[:, :n], ninl, fl, rc
