@@ -133,6 +133,24 @@ _PROTOS = {
     "gf_ba_plan_solve": [_P, _P, _P],
     "gf_ba_plan_results": [_P, _P],
     "gf_ba_plan_destroy": [_P],
+    "gf_orb_extract_ptrs_dev": [_P, _I, _P, _I, _P, _P, _P, _I, _P],
+    "gf_frustum_list_dev": [_P, _P, _I, _P, _P, _I, _P, _P, _F, _P, _P, _P],
+    "gf_match_project_list_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _F, _F, _P, _P, _P, _P],
+    "gf_frontend_create": [_P, _P, _P],
+    "gf_frontend_destroy": [_P],
+    "gf_frontend_capacity": [_P, _P],
+    "gf_frontend_set_source": [_P, _P, _P, _I, _S],
+    "gf_frontend_set_map": [_P, _I, _P, _P, _I],
+    "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
+    "gf_frontend_bootstrap": [_P, _P, _P, _D],
+    "gf_frontend_step": [_P],
+    "gf_frontend_step_host": [_P, _P],
+    "gf_frontend_capture": [_P],
+    "gf_frontend_sync": [_P],
+    "gf_frontend_read": [_P, _I, _P, _S],
+    "gf_frontend_write": [_P, _I, _P, _S],
+    "gf_frontend_field": [_P, _I, _P, _P],
+    "gf_set_budgets": [_P, _D, _D],
 }
 
 

@@ -40,6 +40,8 @@ struct gf_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool prof = false;
+    // gf_set_budgets: reference time budgets in seconds (+inf = parity mode)
+    double match_budget_s = __builtin_inf(), select_budget_s = __builtin_inf();
     std::vector<gf::ProfEntry> prof_entries;
     std::vector<hipEvent_t> event_pool;
     // grow-only device scratch for the host-family wrappers (one slot per use)

@@ -70,6 +70,7 @@ struct Planes {
     const uint8_t* img0;
     long long fstride0;
     int stride0;
+    const uint8_t* const* ptrs;  // optional: level 0 of frame f at ptrs[f] (device pointer table)
     uint8_t* pyr;
     uint8_t* blur;
 };
@@ -78,7 +79,7 @@ __device__ __forceinline__ const uint8_t* level_plane(const Planes& P, const Lev
                                                       int& stride) {
     if (l == 0) {
         stride = P.stride0;
-        return P.img0 + (long long)f * P.fstride0;
+        return P.ptrs ? P.ptrs[f] : P.img0 + (long long)f * P.fstride0;
     }
     stride = g.w[l];
     return P.pyr + (long long)f * g.slab + g.off[l];
@@ -1059,6 +1060,9 @@ static int upload_constants(int device) {
     return GF_OK;
 }
 
+static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* d_kps, uint8_t* d_desc,
+                          int32_t* d_counts, int cap, void* stream);
+
 extern "C" {
 
 int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlevels, int score_type, int fast_th,
@@ -1185,6 +1189,22 @@ int gf_extractor_capacity(gf_extractor* ex, int* cap) {
 int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_imgs, size_t frame_stride, int stride,
                              gf_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, void* stream) {
     GF_CHECK(ex && d_imgs && d_kps && d_desc && d_counts, GF_ERR_ARG, "null arg");
+    Planes P{d_imgs, (long long)frame_stride, stride, nullptr, ex->d_pyr, ex->d_blur};
+    return extract_planes(ex, nframes, P, d_kps, d_desc, d_counts, cap, stream);
+}
+
+int gf_orb_extract_ptrs_dev(gf_extractor* ex, int nframes, const uint8_t* const* d_img_ptrs, int stride,
+                            gf_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, void* stream) {
+    GF_CHECK(ex && d_img_ptrs && d_kps && d_desc && d_counts, GF_ERR_ARG, "null arg");
+    Planes P{nullptr, 0, stride, d_img_ptrs, ex->d_pyr, ex->d_blur};
+    return extract_planes(ex, nframes, P, d_kps, d_desc, d_counts, cap, stream);
+}
+
+}  // extern "C"
+
+static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* d_kps, uint8_t* d_desc,
+                          int32_t* d_counts, int cap, void* stream) {
+    const int stride = P.stride0;
     GF_CHECK(nframes >= 0 && nframes <= ex->max_batch, GF_ERR_ARG, "nframes exceeds max_batch");
     GF_CHECK(cap >= ex->capacity, GF_ERR_CAP, "cap below extractor capacity");
     GF_CHECK(stride >= ex->width, GF_ERR_ARG,
@@ -1192,7 +1212,6 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     if (nframes == 0) return GF_OK;
     hipStream_t s = (hipStream_t)stream;
     const LevelGeom& g = ex->g;
-    Planes P{d_imgs, (long long)frame_stride, stride, ex->d_pyr, ex->d_blur};
     ex->last = P;
     gf_ctx* ctx = ex->ctx;
     {
@@ -1228,6 +1247,8 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
+
+extern "C" {
 
 int gf_orb_extract(gf_extractor* ex, const uint8_t* img, int stride, gf_keypoint* kps, uint8_t* desc, int cap,
                    int* n_out) {
@@ -1267,7 +1288,13 @@ int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, 
         GF_HIP(hipMemcpy(out, ex->d_blur + (long long)frame * g.bslab + g.boff[level], (size_t)g.w[level] * g.h[level],
                          hipMemcpyDeviceToHost));
     } else if (level == 0) {
-        GF_CHECK(ex->last.img0, GF_ERR_ARG, "no batch run yet");
+        GF_CHECK(ex->last.img0 || ex->last.ptrs, GF_ERR_ARG, "no batch run yet");
+        if (ex->last.ptrs) {
+            const uint8_t* src = nullptr;
+            GF_HIP(hipMemcpy(&src, ex->last.ptrs + frame, sizeof(src), hipMemcpyDeviceToHost));
+            GF_HIP(hipMemcpy2D(out, g.w[0], src, ex->last.stride0, g.w[0], g.h[0], hipMemcpyDeviceToHost));
+            return GF_OK;
+        }
         GF_HIP(hipMemcpy2D(out, g.w[0], ex->last.img0 + (long long)frame * ex->last.fstride0, ex->last.stride0, g.w[0],
                            g.h[0], hipMemcpyDeviceToHost));
     } else {

@@ -1,0 +1,841 @@
+// Batched tracking front end: Tracking::GrabImage (Tracking.cc:461-917) in the
+// WORKING state for B independent sequences, chained on one HIP stream with
+// no host round trip (see gf_frontend_* in include/gfslam/abi.h for the
+// reference call sequence). The stages are the library's device-family entry
+// points; this file owns the per-stream state buffers and the small
+// bookkeeping kernels between the stages:
+//   k_fe_begin   frame source pointer, timestamps, motion model
+//                mTcw = mVelocity * mLastFrame.mTcw (Tracking.cc:1519), the
+//                fresh Frame's mvpMapPoints / mvpMatchScore / mvbOutlier
+//   k_fe_branch  SearchReferencePointsInFrustum's num_to_match <= 0 exit
+//                (Tracking.cc:3231-3249): mLeftMapPoints from the stale
+//                mbTrackInView flags, mbNeedVizCheck
+//   k_fe_decide  nToMatch after isInFrustum and the choice between
+//                SearchByProjection (nToMatch < 400) and runActiveMapMatching
+//                (Tracking.cc:3316-3343)
+//   k_fe_post    motion-model update mVelocity = mTcw * LastTwc (:729-738)
+//                and the post-publish list of SearchAdditionalMatchesInFrame
+//   k_fe_end     outliers set NULL (:899-905), mLastFrame = Frame(mCurrentFrame)
+//                (:907), updateAtFrameId stamps shifted to the next frame
+// Branch choices are per stream, so each gated stage gets a per-stream count
+// that is 0 for the streams that skip it (the kernels then do nothing for
+// that stream and leave its state untouched).
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+struct FeDev {
+    int B, cap, M, budget, gf, src_mode, period;
+    double dt;
+    long long frame_stride;
+    // frame source
+    const uint8_t** ptrs;
+    const uint8_t* const* bases;
+    const int32_t* phase;
+    int32_t* step;
+    // current frame
+    int32_t* nkp;
+    float* Tcw;
+    int32_t* kp2mp;
+    int32_t* score;
+    uint8_t* outl;
+    gf_keypoint* kps;
+    uint8_t* desc;
+    // last frame
+    gf_keypoint* last_kps;
+    uint8_t* last_desc;
+    int32_t* last_nkp;
+    int32_t* last_kp2mp;
+    uint8_t* last_outl;
+    float* last_pos;
+    float* Tcw_last;
+    float* V;
+    double* t_prev;
+    double* t_cur;
+    // map
+    const gf_map_point* map;
+    const int32_t* nmp;
+    gf_mp_view* views;
+    int32_t* upd;
+    // lists and gates
+    int32_t* left;
+    int32_t* left1;
+    int32_t* nleft;
+    int32_t* nlist;
+    int32_t* nlist_viz;
+    int32_t* m_frustum;
+    int32_t* m_active;
+    int32_t* m_m2;
+    int32_t* nm2;    // matches of SearchByProjection(F, local, 1)
+    int32_t* stats;  // [GF_FE_NSTAT][B]
+    // budgets (device clock ticks of 100 MHz; < 0: no budget)
+    long long match_ticks, select_ticks;
+    unsigned long long* t0;
+};
+
+__device__ __forceinline__ int32_t* stat(const FeDev& D, int which) { return D.stats + (long long)which * D.B; }
+
+__device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
+// 4x4 row-major float product, summation order of the reference's cv::Mat
+// gemm restatement (oracle/chain.cpp uses the same order).
+__device__ __forceinline__ void mat44(const float* a, const float* b, float* o) {
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            float s = a[4 * i] * b[j];
+            for (int k = 1; k < 4; k++) s = s + a[4 * i + k] * b[4 * k + j];
+            o[4 * i + j] = s;
+        }
+}
+
+__global__ __launch_bounds__(256) void k_fe_begin(FeDev D) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (t == 0) {
+        if (D.src_mode == 1) {
+            const int k = *D.step;
+            const int idx = (int)(((long long)D.phase[b] + k) % D.period);
+            D.ptrs[b] = D.bases[b] + (long long)idx * D.frame_stride;
+        }
+        D.t_cur[b] = D.t_prev[b] + D.dt;
+        float o[16];
+        mat44(D.V + 16 * b, D.Tcw_last + 16 * b, o);
+        for (int i = 0; i < 16; i++) D.Tcw[16 * b + i] = o[i];
+        D.t0[b] = now_ticks();
+        for (int s = 0; s < GF_FE_NSTAT; s++)
+            if (s != GF_ST_FRAMES) stat(D, s)[b] = 0;
+    }
+    const long long o = (long long)b * D.cap;
+    for (int i = t; i < D.cap; i += 256) {
+        D.kp2mp[o + i] = -1;
+        D.score[o + i] = 999;
+        D.outl[o + i] = 0;
+    }
+}
+
+// Ordered compaction of views[i].in_view over the stream's map (one wave).
+__device__ int compact_in_view(const FeDev& D, int b, int32_t* out) {
+    const int lane = threadIdx.x;
+    const int m = D.nmp[b];
+    int cnt = 0;
+    for (int base = 0; base < m; base += 64) {
+        const int i = base + lane;
+        const bool on = i < m && D.views[(long long)b * D.M + i].in_view;
+        const unsigned long long msk = __ballot(on);
+        if (on) out[(long long)b * D.M + cnt + __popcll(msk & ((1ull << lane) - 1ull))] = i;
+        cnt += __popcll(msk);
+    }
+    return cnt;
+}
+
+__global__ __launch_bounds__(64) void k_fe_branch(FeDev D) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const int ntm = stat(D, GF_ST_TO_MATCH)[b];
+    // isInFrustum time cap (Tracking.cc:3262-3270): past half of the matching
+    // budget every remaining local point goes to mLeftMapPoints
+    const bool late = D.match_ticks >= 0 && (long long)(now_ticks() - D.t0[b]) > D.match_ticks / 2;
+    if (D.gf && ntm <= 0) {
+        // mbTrackInView as left by earlier frames (matched points already false)
+        const int n = compact_in_view(D, b, D.left1);
+        if (lane == 0) {
+            stat(D, GF_ST_BRANCH)[b] = 1;
+            D.nlist[b] = n;
+            D.nlist_viz[b] = n;
+            D.m_frustum[b] = 0;
+        }
+    } else if (D.gf && late) {
+        // the cut falls on the first point of the list: every point goes to
+        // mLeftMapPoints (vector(vit, vend)); nToMatch stays 0
+        const int m = D.nmp[b];
+        for (int i = lane; i < m; i += 64) D.left1[(long long)b * D.M + i] = i;
+        if (lane == 0) {
+            stat(D, GF_ST_BRANCH)[b] = 5;
+            stat(D, GF_ST_FLAGS)[b] |= 8;
+            D.nlist[b] = m;
+            D.nlist_viz[b] = m;
+            D.m_frustum[b] = 0;
+        }
+    } else if (lane == 0) {
+        stat(D, GF_ST_BRANCH)[b] = 0;
+        D.nlist[b] = 0;
+        D.nlist_viz[b] = 0;
+        D.m_frustum[b] = D.nmp[b];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
+    __shared__ int s_cnt;
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
+    const int br = stat(D, GF_ST_BRANCH)[b];
+    if (br == 0) {
+        const int m = D.nmp[b];
+        int c = 0;
+        for (int i = t; i < m; i += 256) c += D.views[(long long)b * D.M + i].in_view ? 1 : 0;
+        c = gfd::warp_sum(c);
+        if ((t & 63) == 0) atomicAdd(&s_cnt, c);
+    }
+    __syncthreads();
+    if (t != 0) return;
+    D.m_active[b] = 0;
+    D.m_m2[b] = 0;
+    if (br != 0) return;
+    const int n = s_cnt;
+    stat(D, GF_ST_IN_VIEW)[b] = n;
+    int nb;
+    if (n == 0) {
+        nb = 4;
+    } else if (!D.gf || n < 400) {  // Tracking.cc:3322
+        nb = 2;
+        D.m_m2[b] = D.nmp[b];
+    } else {
+        nb = 3;
+        D.m_active[b] = D.nmp[b];
+    }
+    stat(D, GF_ST_BRANCH)[b] = nb;
+}
+
+__global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int br = stat(D, GF_ST_BRANCH)[b];
+    int n = 0;
+    if (br == 1 || br == 5) {
+        n = D.nlist[b];
+        for (int i = t; i < n; i += 256) D.left[(long long)b * D.M + i] = D.left1[(long long)b * D.M + i];
+    } else if (br == 3) {
+        n = D.nleft[b];
+    }
+    if (t != 0) return;
+    if (br == 2) stat(D, GF_ST_LOCAL)[b] = D.nm2[b];
+    // motion model (Tracking.cc:729-738): LastTwc from mLastFrame.mTcw, mVelocity = mTcw * LastTwc
+    const float* L = D.Tcw_last + 16 * b;
+    float Twc[16] = {0};
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) Twc[4 * i + j] = L[4 * j + i];
+    for (int i = 0; i < 3; i++) {
+        float s = Twc[4 * i] * L[3];
+        s = s + Twc[4 * i + 1] * L[7];
+        s = s + Twc[4 * i + 2] * L[11];
+        Twc[4 * i + 3] = -s;
+    }
+    Twc[15] = 1.f;
+    float o[16];
+    mat44(D.Tcw + 16 * b, Twc, o);
+    for (int i = 0; i < 16; i++) D.V[16 * b + i] = o[i];
+    D.nlist[b] = n;
+    stat(D, GF_ST_NLEFT)[b] = n;
+    const bool viz = (br == 1 || br == 5);
+    // SearchByProjection_Budget returns at once without budget (ORBmatcher.cc:281-282)
+    const bool no_time = D.select_ticks >= 0 && (long long)(now_ticks() - D.t0[b]) >= D.select_ticks;
+    D.nlist_viz[b] = (viz && !no_time) ? n : 0;
+    if (no_time) {
+        D.nlist[b] = 0;
+        if (n) stat(D, GF_ST_FLAGS)[b] |= 8;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int n = D.nkp[b];
+    const long long o = (long long)b * D.cap;
+    for (int i = t; i < n; i += 256) {
+        int mp = D.kp2mp[o + i];
+        const uint8_t ou = D.outl[o + i];
+        if (mp >= 0 && ou) mp = -1;  // Tracking.cc:899-905 (mvbOutlier stays set)
+        D.kp2mp[o + i] = mp;
+        D.last_kp2mp[o + i] = mp;
+        D.last_outl[o + i] = ou;
+        D.last_kps[o + i] = D.kps[o + i];
+        float* p = D.last_pos + 3 * (o + i);
+        if (mp >= 0) {
+            const gf_map_point& P = D.map[(long long)b * D.M + mp];
+            p[0] = P.pos[0];
+            p[1] = P.pos[1];
+            p[2] = P.pos[2];
+        } else {
+            p[0] = p[1] = p[2] = 0.f;
+        }
+    }
+    const uint4* ds = (const uint4*)(D.desc + o * 32);
+    uint4* dd = (uint4*)(D.last_desc + o * 32);
+    for (int i = t; i < 2 * n; i += 256) dd[i] = ds[i];
+    const int m = D.nmp[b];
+    for (int i = t; i < m; i += 256) D.upd[(long long)b * D.M + i] -= 1;
+    if (t == 0) {
+        D.last_nkp[b] = n;
+        for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
+        D.t_prev[b] = D.t_cur[b];
+        int fl = stat(D, GF_ST_FLAGS)[b];
+        if (stat(D, GF_ST_M3)[b] < 20) fl |= 1;
+        if (stat(D, GF_ST_FOUND)[b] < 10) fl |= 2;
+        if (stat(D, GF_ST_INL2)[b] < 15) fl |= 4;
+        stat(D, GF_ST_FLAGS)[b] = fl;
+        stat(D, GF_ST_FRAMES)[b] += 1;
+        if (b == 0) *D.step += 1;
+    }
+}
+
+// Bootstrap: the matched frame becomes the last frame (kp2mp as matched).
+__global__ __launch_bounds__(256) void k_fe_boot_end(FeDev D) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int n = D.nkp[b];
+    const long long o = (long long)b * D.cap;
+    for (int i = t; i < n; i += 256) {
+        const int mp = D.kp2mp[o + i];
+        D.last_kp2mp[o + i] = mp;
+        D.last_outl[o + i] = 0;
+        D.last_kps[o + i] = D.kps[o + i];
+        float* p = D.last_pos + 3 * (o + i);
+        if (mp >= 0) {
+            const gf_map_point& P = D.map[(long long)b * D.M + mp];
+            p[0] = P.pos[0];
+            p[1] = P.pos[1];
+            p[2] = P.pos[2];
+        } else {
+            p[0] = p[1] = p[2] = 0.f;
+        }
+    }
+    const uint4* ds = (const uint4*)(D.desc + o * 32);
+    uint4* dd = (uint4*)(D.last_desc + o * 32);
+    for (int i = t; i < 2 * n; i += 256) dd[i] = ds[i];
+    if (t == 0) {
+        D.last_nkp[b] = n;
+        for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
+        D.t_prev[b] = D.t_cur[b];
+        if (b == 0) *D.step += 1;
+    }
+}
+
+__global__ void k_fe_boot_begin(FeDev D) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= D.B) return;
+    if (D.src_mode == 1) {
+        const int idx = (int)(((long long)D.phase[b] + *D.step) % D.period);
+        D.ptrs[b] = D.bases[b] + (long long)idx * D.frame_stride;
+    }
+}
+
+}  // namespace
+
+struct gf_frontend {
+    gf_ctx* ctx = nullptr;
+    gf_frontend_params p{};
+    gf_extractor* ex = nullptr;
+    int cap = 0;
+    gf_frame_info fi{};
+    gf_obs_camera ocam{};
+    float inv_sigma2[16] = {}, level_sigma2[16] = {};
+    FeDev D{};
+    // fields
+    void* field_ptr[GF_FE_NFIELDS] = {};
+    size_t field_bytes[GF_FE_NFIELDS] = {};
+    // device buffers not exported as fields
+    int32_t* scratch = nullptr;
+    int32_t* num_to_match = nullptr;  // = stats column
+    double* Xv = nullptr;
+    double* Xv_next = nullptr;
+    double* base = nullptr;
+    double* mp_H = nullptr;
+    double* mp_info = nullptr;
+    float* mp_uv = nullptr;
+    float* mp_pos = nullptr;
+    uint8_t* mp_updated = nullptr;
+    int32_t* nview = nullptr;
+    uint8_t* staging = nullptr;
+    const uint8_t** staging_ptrs = nullptr;
+    std::vector<void*> allocs;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    bool sourced = false;
+};
+
+namespace {
+
+int fe_alloc(gf_frontend* fe, size_t bytes, void** out) {
+    GF_HIP(hipMalloc(out, std::max<size_t>(bytes, 16)));
+    fe->allocs.push_back(*out);
+    GF_HIP(hipMemset(*out, 0, std::max<size_t>(bytes, 16)));
+    return GF_OK;
+}
+
+template <typename T>
+int fe_field(gf_frontend* fe, int field, size_t count, T** out) {
+    void* p = nullptr;
+    int rc = fe_alloc(fe, sizeof(T) * count, &p);
+    if (rc) return rc;
+    *out = (T*)p;
+    if (field >= 0) {
+        fe->field_ptr[field] = p;
+        fe->field_bytes[field] = sizeof(T) * count;
+    }
+    return GF_OK;
+}
+
+void fe_free(gf_frontend* fe) {
+    if (fe->exec) (void)hipGraphExecDestroy(fe->exec);
+    if (fe->graph) (void)hipGraphDestroy(fe->graph);
+    for (void* p : fe->allocs) (void)hipFree(p);
+    fe->allocs.clear();
+    if (fe->ex) (void)gf_extractor_destroy(fe->ex);
+    fe->ex = nullptr;
+}
+
+#define FE_RC(expr)                \
+    do {                           \
+        int _rc = (expr);          \
+        if (_rc) return _rc;       \
+    } while (0)
+
+// The tracking step after the frame source pointers are set.
+int fe_track(gf_frontend* fe, hipStream_t s) {
+    gf_ctx* ctx = fe->ctx;
+    FeDev& D = fe->D;
+    const int B = D.B, cap = D.cap, M = D.M;
+    const gf_frame_info* fi = &fe->fi;
+    int32_t* st = D.stats;
+    auto col = [&](int c) { return st + (size_t)c * B; };
+    {
+        GF_PROF(ctx, s, "k_fe_begin");
+        k_fe_begin<<<B, 256, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    }
+    FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
+                                  s));
+    // TrackWithMotionModel
+    FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
+                                 D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp, D.score,
+                                 col(GF_ST_M3), fe->scratch, s));
+    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
+                                 fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
+                                 col(GF_ST_ITER1), col(GF_ST_EDGES1), s));
+    FE_RC(gf_discard_outliers_dev(ctx, B, D.kp2mp, D.outl, D.nkp, cap, D.budget, col(GF_ST_FOUND),
+                                  col(GF_ST_TO_MATCH), s));
+    // TrackLocalMap -> SearchReferencePointsInFrustum
+    if (D.gf) {
+        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, s));
+        FE_RC(gf_obs_frame_info_dev(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp, cap, D.kp2mp, D.outl, fe->mp_pos, D.nmp,
+                                    M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, s));
+        FE_RC(gf_obs_accumulate_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
+                                            fe->base, s));
+    }
+    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+    {
+        GF_PROF(ctx, s, "k_fe_branch");
+        k_fe_branch<<<B, 64, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    }
+    FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
+    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+    {
+        GF_PROF(ctx, s, "k_fe_decide");
+        k_fe_decide<<<B, 256, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    }
+    if (D.gf) {
+        FE_RC(gf_obs_map_info_dev(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
+                                  fe->mp_info, fe->mp_uv, fe->mp_updated, s));
+        FE_RC(gf_obs_active_match_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
+                                      (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], fe->mp_updated, fe->mp_info,
+                                      fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2, col(GF_ST_TO_MATCH), 1.f,
+                                      0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score, D.left, D.nleft,
+                                      col(GF_ST_LOCAL), s));
+    }
+    FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
+                               (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], D.m_m2, M, 1.f, 0.8f, D.kp2mp, D.score,
+                               D.nm2, s));
+    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
+                                 fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL2),
+                                 col(GF_ST_ITER2), col(GF_ST_EDGES2), s));
+    {
+        GF_PROF(ctx, s, "k_fe_post");
+        k_fe_post<<<B, 256, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    }
+    if (D.gf) {
+        // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz)
+        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, s));
+        FE_RC(gf_obs_map_info_dev(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
+                                  fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, s));
+        // SearchAdditionalMatchesInFrame
+        FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview, s));
+        FE_RC(gf_match_project_list_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
+                                        (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], M, D.left, D.nlist, 0.8f,
+                                        0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA), s));
+    }
+    {
+        GF_PROF(ctx, s, "k_fe_end");
+        k_fe_end<<<B, 256, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    }
+    return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** out) {
+    GF_CHECK(ctx && p && out, GF_ERR_ARG, "null arg");
+    GF_CHECK(p->batch > 0 && p->map_cap > 0 && p->map_cap <= 4096, GF_ERR_ARG, "batch / map_cap out of range");
+    GF_CHECK(p->nlevels >= 1 && p->nlevels <= 16 && p->dt > 0, GF_ERR_ARG, "bad front-end parameters");
+    GF_HIP(hipSetDevice(ctx->device));
+    gf_frontend* fe = new gf_frontend();
+    fe->ctx = ctx;
+    fe->p = *p;
+    int rc = gf_extractor_create(ctx, p->nfeatures, p->scale_factor, p->nlevels, 1, p->fast_th, p->width, p->height,
+                                 p->batch, &fe->ex);
+    if (rc) {
+        delete fe;
+        return rc;
+    }
+    gf_extractor_capacity(fe->ex, &fe->cap);
+    const int B = p->batch, cap = fe->cap, M = p->map_cap;
+    // Frame tables: bounds of the undistorted image (k1 = 0: the image,
+    // Frame.cc:470-476), mvScaleFactors as float products, mvLevelSigma2 and
+    // mvInvLevelSigma2 (ORBextractor.cc:474-478, Frame.cc:93-98).
+    fe->fi = gf_frame_info{0, p->width, 0, p->height, p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
+    float sf = 1.f;
+    for (int l = 0; l < p->nlevels; l++) {
+        if (l) sf = sf * p->scale_factor;
+        fe->level_sigma2[l] = sf * sf;
+        fe->inv_sigma2[l] = 1.0f / (sf * sf);
+    }
+    // Observability camera + the margins Tracking sets (Tracking.cc:875-877)
+    gf_obs_camera& oc = fe->ocam;
+    oc.fu = p->fx;
+    oc.fv = p->fy;
+    oc.cx = p->cx;
+    oc.cy = p->cy;
+    oc.nrows = p->height;
+    oc.ncols = p->width;
+    oc.min_x = 0;
+    oc.max_x = p->width;
+    oc.min_y = 0;
+    oc.max_y = p->height;
+    oc.bound_x = (int)((p->width - 0) * 0.1);
+    oc.bound_y = (int)((p->height - 0) * 0.1);
+    oc.bound_depth = 0.f;
+    FeDev& D = fe->D;
+    D.B = B;
+    D.cap = cap;
+    D.M = M;
+    D.budget = p->gf_budget;
+    D.gf = p->gf ? 1 : 0;
+    D.dt = p->dt;
+    D.match_ticks = -1;
+    D.select_ticks = -1;
+    auto bail = [&](int e) {
+        fe_free(fe);
+        delete fe;
+        return e;
+    };
+#define F(field, type, count, dst)                          \
+    if ((rc = fe_field<type>(fe, field, (count), &(dst)))) \
+        return bail(rc);
+    F(GF_FE_KPS, gf_keypoint, (size_t)B * cap, D.kps);
+    F(GF_FE_DESC, uint8_t, (size_t)B * cap * 32, D.desc);
+    F(GF_FE_NKP, int32_t, B, D.nkp);
+    F(GF_FE_TCW, float, (size_t)B * 16, D.Tcw);
+    F(GF_FE_KP2MP, int32_t, (size_t)B * cap, D.kp2mp);
+    F(GF_FE_SCORE, int32_t, (size_t)B * cap, D.score);
+    F(GF_FE_OUTLIER, uint8_t, (size_t)B * cap, D.outl);
+    F(GF_FE_LAST_KPS, gf_keypoint, (size_t)B * cap, D.last_kps);
+    F(GF_FE_LAST_DESC, uint8_t, (size_t)B * cap * 32, D.last_desc);
+    F(GF_FE_LAST_NKP, int32_t, B, D.last_nkp);
+    F(GF_FE_LAST_KP2MP, int32_t, (size_t)B * cap, D.last_kp2mp);
+    F(GF_FE_LAST_OUTLIER, uint8_t, (size_t)B * cap, D.last_outl);
+    F(GF_FE_LAST_POS, float, (size_t)B * cap * 3, D.last_pos);
+    F(GF_FE_TCW_LAST, float, (size_t)B * 16, D.Tcw_last);
+    F(GF_FE_VELOCITY, float, (size_t)B * 16, D.V);
+    F(GF_FE_T_PREV, double, B, D.t_prev);
+    F(GF_FE_T_CUR, double, B, D.t_cur);
+    gf_map_point* map = nullptr;
+    F(GF_FE_MAP, gf_map_point, (size_t)B * M, map);
+    D.map = map;
+    uint8_t* mdesc = nullptr;
+    F(GF_FE_MAP_DESC, uint8_t, (size_t)B * M * 32, mdesc);
+    int32_t* nmp = nullptr;
+    F(GF_FE_NMP, int32_t, B, nmp);
+    D.nmp = nmp;
+    F(GF_FE_VIEWS, gf_mp_view, (size_t)B * M, D.views);
+    F(GF_FE_XV, double, (size_t)B * 13, fe->Xv);
+    F(GF_FE_XV_NEXT, double, (size_t)B * 13, fe->Xv_next);
+    F(GF_FE_BASE, double, (size_t)B * 49, fe->base);
+    F(GF_FE_MP_H, double, (size_t)B * M * 14, fe->mp_H);
+    F(GF_FE_MP_INFO, double, (size_t)B * M * 49, fe->mp_info);
+    F(GF_FE_MP_UV, float, (size_t)B * M * 2, fe->mp_uv);
+    F(GF_FE_MP_UPD, int32_t, (size_t)B * M, D.upd);
+    gf_rng* rng = nullptr;
+    F(GF_FE_RNG, gf_rng, B, rng);
+    F(GF_FE_LEFT, int32_t, (size_t)B * M, D.left);
+    F(GF_FE_STATS, int32_t, (size_t)GF_FE_NSTAT * B, D.stats);
+    F(-1, int32_t, (size_t)B * M, D.left1);
+    F(-1, int32_t, B, D.nleft);
+    F(-1, int32_t, B, D.nlist);
+    F(-1, int32_t, B, D.nlist_viz);
+    F(-1, int32_t, B, D.m_frustum);
+    F(-1, int32_t, B, D.m_active);
+    F(-1, int32_t, B, D.m_m2);
+    F(-1, int32_t, B, D.nm2);
+    F(-1, int32_t, (size_t)2 * B * cap, fe->scratch);
+    F(-1, float, (size_t)B * M * 3, fe->mp_pos);
+    F(-1, uint8_t, (size_t)B * M, fe->mp_updated);
+    F(-1, int32_t, B, fe->nview);
+    F(-1, int32_t, 1, D.step);
+    F(-1, unsigned long long, B, D.t0);
+    const uint8_t** ptrs = nullptr;
+    F(-1, const uint8_t*, B, ptrs);
+    D.ptrs = ptrs;
+    const uint8_t** bases = nullptr;
+    F(-1, const uint8_t*, B, bases);
+    D.bases = bases;
+    int32_t* phase = nullptr;
+    F(-1, int32_t, B, phase);
+    D.phase = phase;
+#undef F
+    // updateAtFrameId = -1 (never): no stamp equals the current (1) or next (2) frame
+    std::vector<int32_t> neg((size_t)B * M, -1000);
+    if (hipMemcpy(D.upd, neg.data(), neg.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(gf::fail(GF_ERR_HIP, "upload stamps"));
+    // std::srand(1) for every stream until set_rng
+    std::vector<gf_rng> r(B);
+    for (int b = 0; b < B; b++) gf_rng_seed(&r[b], 1);
+    if (hipMemcpy(rng, r.data(), sizeof(gf_rng) * B, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(gf::fail(GF_ERR_HIP, "upload rng"));
+    std::vector<float> I((size_t)B * 16, 0.f);
+    for (int b = 0; b < B; b++)
+        for (int i = 0; i < 4; i++) I[16 * b + 5 * i] = 1.f;
+    if (hipMemcpy(D.Tcw_last, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(D.V, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(gf::fail(GF_ERR_HIP, "upload poses"));
+    *out = fe;
+    return GF_OK;
+}
+
+int gf_frontend_destroy(gf_frontend* fe) {
+    if (!fe) return GF_OK;
+    (void)hipSetDevice(fe->ctx->device);
+    (void)hipStreamSynchronize(fe->ctx->stream);
+    if (fe->staging) (void)hipHostUnregister(fe->staging);
+    fe_free(fe);
+    delete fe;
+    return GF_OK;
+}
+
+int gf_frontend_capacity(gf_frontend* fe, int* cap) {
+    GF_CHECK(fe && cap, GF_ERR_ARG, "null arg");
+    *cap = fe->cap;
+    return GF_OK;
+}
+
+int gf_frontend_set_source(gf_frontend* fe, const uint8_t* const* d_bases, const int32_t* phase, int period,
+                           size_t frame_stride) {
+    GF_CHECK(fe && d_bases && phase && period > 0, GF_ERR_ARG, "bad source");
+    GF_CHECK(frame_stride >= (size_t)fe->p.width * fe->p.height, GF_ERR_ARG, "frame stride below the image size");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    const int B = fe->D.B;
+    for (int b = 0; b < B; b++) GF_CHECK(d_bases[b] && phase[b] >= 0, GF_ERR_ARG, "bad source entry");
+    GF_HIP(hipMemcpy((void*)fe->D.bases, d_bases, sizeof(void*) * B, hipMemcpyHostToDevice));
+    GF_HIP(hipMemcpy((void*)fe->D.phase, phase, sizeof(int32_t) * B, hipMemcpyHostToDevice));
+    fe->D.period = period;
+    fe->D.frame_stride = (long long)frame_stride;
+    fe->D.src_mode = 1;
+    fe->sourced = true;
+    return GF_OK;
+}
+
+int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, const uint8_t* desc, int m) {
+    GF_CHECK(fe && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad stream");
+    GF_CHECK(m >= 0 && m <= fe->D.M && (m == 0 || (mps && desc)), GF_ERR_ARG, "bad map");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    const size_t M = fe->D.M, o = (size_t)stream * M;
+    std::vector<float> pos(3 * (size_t)m);
+    for (int i = 0; i < m; i++)
+        for (int c = 0; c < 3; c++) pos[3 * i + c] = mps[i].pos[c];
+    if (m) {
+        GF_HIP(hipMemcpy((gf_map_point*)fe->D.map + o, mps, sizeof(gf_map_point) * m, hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy((uint8_t*)fe->field_ptr[GF_FE_MAP_DESC] + o * 32, desc, 32 * (size_t)m,
+                         hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy(fe->mp_pos + 3 * o, pos.data(), 12 * (size_t)m, hipMemcpyHostToDevice));
+    }
+    GF_HIP(hipMemcpy((int32_t*)fe->D.nmp + stream, &m, 4, hipMemcpyHostToDevice));
+    std::vector<int32_t> neg(M, -1000);
+    GF_HIP(hipMemcpy(fe->D.upd + o, neg.data(), 4 * M, hipMemcpyHostToDevice));
+    GF_HIP(hipMemset(fe->D.views + o, 0, sizeof(gf_mp_view) * M));
+    return GF_OK;
+}
+
+int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed) {
+    GF_CHECK(fe && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad stream");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    gf_rng r;
+    gf_rng_seed(&r, seed);
+    GF_HIP(hipMemcpy((gf_rng*)fe->field_ptr[GF_FE_RNG] + stream, &r, sizeof(r), hipMemcpyHostToDevice));
+    return GF_OK;
+}
+
+int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0) {
+    GF_CHECK(fe && Tcw && V, GF_ERR_ARG, "null arg");
+    GF_CHECK(fe->sourced, GF_ERR_ARG, "no frame source set");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    FeDev& D = fe->D;
+    const int B = D.B, cap = D.cap, M = D.M;
+    hipStream_t s = fe->ctx->stream;
+    gf_ctx* ctx = fe->ctx;
+    std::vector<double> t(B, t0);
+    GF_HIP(hipMemcpyAsync(D.Tcw, Tcw, sizeof(float) * 16 * B, hipMemcpyHostToDevice, s));
+    GF_HIP(hipMemcpyAsync(D.V, V, sizeof(float) * 16 * B, hipMemcpyHostToDevice, s));
+    GF_HIP(hipMemcpyAsync(D.t_cur, t.data(), sizeof(double) * B, hipMemcpyHostToDevice, s));
+    k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(D);
+    GF_HIP(hipGetLastError());
+    GF_HIP(hipMemsetAsync(D.kp2mp, 0xff, sizeof(int32_t) * B * cap, s));
+    std::vector<int32_t> s999((size_t)B * cap, 999);
+    GF_HIP(hipMemcpyAsync(D.score, s999.data(), 4 * s999.size(), hipMemcpyHostToDevice, s));
+    FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
+                                  s));
+    FE_RC(gf_frustum_dev(ctx, &fe->fi, B, D.Tcw, D.map, D.nmp, M, 0.5f, D.views, fe->nview, s));
+    FE_RC(gf_match_project_dev(ctx, &fe->fi, B, D.kps, D.desc, D.nkp, cap, D.views,
+                               (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], D.nmp, M, 1.f, 0.8f, D.kp2mp, D.score,
+                               fe->scratch, s));
+    k_fe_boot_end<<<B, 256, 0, s>>>(D);
+    GF_HIP(hipGetLastError());
+    GF_HIP(hipStreamSynchronize(s));
+    return GF_OK;
+}
+
+int gf_frontend_step(gf_frontend* fe) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(fe->sourced || fe->D.src_mode == 2, GF_ERR_ARG, "no frame source set");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    // budgets of the context, as device clock ticks (100 MHz)
+    auto ticks = [](double s) -> long long { return std::isfinite(s) && s >= 0 ? (long long)(s * 1e8) : -1; };
+    const long long mt = ticks(fe->ctx->match_budget_s), stt = ticks(fe->ctx->select_budget_s);
+    if (fe->exec && mt == fe->D.match_ticks && stt == fe->D.select_ticks) {
+        GF_HIP(hipGraphLaunch(fe->exec, fe->ctx->stream));
+        return GF_OK;
+    }
+    if (fe->exec && (mt != fe->D.match_ticks || stt != fe->D.select_ticks)) {  // budgets changed: re-capture
+        (void)hipGraphExecDestroy(fe->exec);
+        (void)hipGraphDestroy(fe->graph);
+        fe->exec = nullptr;
+        fe->graph = nullptr;
+    }
+    fe->D.match_ticks = mt;
+    fe->D.select_ticks = stt;
+    return fe_track(fe, fe->ctx->stream);
+}
+
+int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
+    GF_CHECK(fe && imgs, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    FeDev& D = fe->D;
+    const size_t fb = (size_t)fe->p.width * fe->p.height;
+    hipStream_t s = fe->ctx->stream;
+    if (!fe->staging) {
+        void* p = nullptr;
+        FE_RC(fe_alloc(fe, fb * D.B, &p));
+        fe->staging = (uint8_t*)p;
+        std::vector<const uint8_t*> ptr(D.B);
+        for (int b = 0; b < D.B; b++) ptr[b] = fe->staging + fb * b;
+        GF_HIP(hipMemcpy((void*)D.ptrs, ptr.data(), sizeof(void*) * D.B, hipMemcpyHostToDevice));
+    }
+    GF_HIP(hipMemcpyAsync(fe->staging, imgs, fb * D.B, hipMemcpyHostToDevice, s));
+    const int mode = D.src_mode;
+    D.src_mode = 2;  // pointers stay on the staging buffer
+    auto ticks = [](double v) -> long long { return std::isfinite(v) && v >= 0 ? (long long)(v * 1e8) : -1; };
+    D.match_ticks = ticks(fe->ctx->match_budget_s);
+    D.select_ticks = ticks(fe->ctx->select_budget_s);
+    int rc = fe_track(fe, s);
+    D.src_mode = mode;
+    if (mode == 1) {  // the next sourced step recomputes its pointers
+    }
+    return rc;
+}
+
+int gf_frontend_capture(gf_frontend* fe) {
+    GF_CHECK(fe && fe->sourced, GF_ERR_ARG, "capture needs a frame source");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    hipStream_t s = fe->ctx->stream;
+    GF_HIP(hipStreamSynchronize(s));
+    if (fe->exec) (void)hipGraphExecDestroy(fe->exec);
+    if (fe->graph) (void)hipGraphDestroy(fe->graph);
+    fe->exec = nullptr;
+    fe->graph = nullptr;
+    auto ticks = [](double v) -> long long { return std::isfinite(v) && v >= 0 ? (long long)(v * 1e8) : -1; };
+    fe->D.match_ticks = ticks(fe->ctx->match_budget_s);
+    fe->D.select_ticks = ticks(fe->ctx->select_budget_s);
+    const bool prof = fe->ctx->prof;
+    fe->ctx->prof = false;  // no event records inside the graph
+    GF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = fe_track(fe, s);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(s, &g);
+    fe->ctx->prof = prof;
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess) return gf::fail(GF_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
+    fe->graph = g;
+    GF_HIP(hipGraphInstantiate(&fe->exec, g, nullptr, nullptr, 0));
+    return GF_OK;
+}
+
+int gf_frontend_sync(gf_frontend* fe) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    return GF_OK;
+}
+
+int gf_frontend_field(gf_frontend* fe, int field, size_t* bytes, void** d_ptr) {
+    GF_CHECK(fe && field >= 0 && field < GF_FE_NFIELDS, GF_ERR_ARG, "bad field");
+    if (bytes) *bytes = fe->field_bytes[field];
+    if (d_ptr) *d_ptr = fe->field_ptr[field];
+    return GF_OK;
+}
+
+int gf_frontend_read(gf_frontend* fe, int field, void* host, size_t bytes) {
+    GF_CHECK(fe && host && field >= 0 && field < GF_FE_NFIELDS, GF_ERR_ARG, "bad field");
+    GF_CHECK(bytes == fe->field_bytes[field], GF_ERR_ARG,
+             "field size is " + std::to_string(fe->field_bytes[field]) + " bytes");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    GF_HIP(hipMemcpy(host, fe->field_ptr[field], bytes, hipMemcpyDeviceToHost));
+    return GF_OK;
+}
+
+int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes) {
+    GF_CHECK(fe && host && field >= 0 && field < GF_FE_NFIELDS, GF_ERR_ARG, "bad field");
+    GF_CHECK(bytes == fe->field_bytes[field], GF_ERR_ARG,
+             "field size is " + std::to_string(fe->field_bytes[field]) + " bytes");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    GF_HIP(hipMemcpy(fe->field_ptr[field], host, bytes, hipMemcpyHostToDevice));
+    if (field == GF_FE_MAP) {  // keep the float3 position copy the Jacobian kernels read
+        const size_t n = bytes / sizeof(gf_map_point);
+        const gf_map_point* m = (const gf_map_point*)host;
+        std::vector<float> pos(3 * n);
+        for (size_t i = 0; i < n; i++)
+            for (int c = 0; c < 3; c++) pos[3 * i + c] = m[i].pos[c];
+        GF_HIP(hipMemcpy(fe->mp_pos, pos.data(), 12 * n, hipMemcpyHostToDevice));
+    }
+    return GF_OK;
+}
+
+int gf_set_budgets(gf_ctx* ctx, double match_s, double select_s) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    GF_CHECK(!(match_s < 0) && !(select_s < 0), GF_ERR_ARG, "negative budget");
+    ctx->match_budget_s = match_s;
+    ctx->select_budget_s = select_s;
+    return GF_OK;
+}
+
+}  // extern "C"

@@ -42,6 +42,8 @@ struct MatchArgs {
     const uint8_t* qdesc;
     const int32_t* m;
     int q_cap;
+    const int32_t* list;   // MODE_PROJECT: optional query list [F][q_cap] (map indices, in order)
+    const int32_t* nlist;  // its length per frame
     // MODE_LAST queries
     const gf_keypoint* last_kps;
     const int32_t* last_kp2mp;
@@ -78,6 +80,7 @@ __device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int
     q.cx0 = 1;
     q.cx1 = 0;
     if (A.mode == MODE_PROJECT) {
+        if (A.list) k = A.list[(long long)f * A.q_cap + k];
         const gf_mp_view v = A.views[(long long)f * A.q_cap + k];
         if (!v.in_view) return q;
         const int pl = min(max(v.level, 0), fc.nlevels - 1);
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
 
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], KP_MAX);
-    const int nq = min(A.m[f], Q_MAX);
+    const int nq = min(A.list ? A.nlist[f] : A.m[f], Q_MAX);
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
@@ -530,12 +533,15 @@ size_t seq_lds_bytes(int kp_cap, int q_cap) { return sizeof(int) * ((size_t)kp_c
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
                           const int32_t* __restrict__ m, int cap, float viewCosLimit, gf_mp_view* __restrict__ views,
-                          int32_t* __restrict__ nview) {
+                          int32_t* __restrict__ nview, const int32_t* __restrict__ list,
+                          const int32_t* __restrict__ nlist) {
     const int f = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
     const float* T = Tcw + 16 * f;
     int in = 0;
-    if (i < m[f]) {
+    const bool run = list ? i < nlist[f] : i < m[f];
+    if (run && list) i = list[(long long)f * cap + i];  // the list's map point
+    if (run) {
         gf_mp_view v;
         v.in_view = 0;
         v.u = v.v = v.view_cos = 0.f;
@@ -658,7 +664,25 @@ int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const floa
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, "k_frustum");
     k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
-                                                                   d_views, d_nview);
+                                                                   d_views, d_nview, nullptr, nullptr);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf_frustum_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw,
+                        const gf_map_point* d_mps, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                        float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    if (nframes <= 0 || mp_cap <= 0) return GF_OK;
+    GF_CHECK(d_Tcw && d_mps && d_list && d_nlist && d_views && d_nview, GF_ERR_ARG, "null arg");
+    hipStream_t s = (hipStream_t)stream;
+    FrameConst fc = gf::make_frame_const(fi);
+    GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
+    GF_PROF(ctx, s, "k_frustum_list");
+    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, nullptr, mp_cap, view_cos_limit,
+                                                                   d_views, d_nview, d_list, d_nlist);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -689,6 +713,41 @@ int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.nmatches = d_nmatches;
     void* err;
     rc = gf::ws_get(ctx, 31, sizeof(int32_t) * nframes, &err);
+    if (rc) return rc;
+    A.err = (int32_t*)err;
+    return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
+}
+
+int gf_match_project_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                              const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                              const uint8_t* d_mp_desc, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                              float th, float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches,
+                              void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    GF_CHECK(kp_cap <= KP_MAX && mp_cap <= Q_MAX, GF_ERR_UNSUPPORTED, "frame exceeds matcher limits (4096 kps, 8192 mps)");
+    GF_CHECK(d_list && d_nlist, GF_ERR_ARG, "null list");
+    if (nframes <= 0) return GF_OK;
+    MatchArgs A{};
+    A.mode = MODE_PROJECT;
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.kp_cap = kp_cap;
+    A.views = d_views;
+    A.qdesc = d_mp_desc;
+    A.m = d_nlist;
+    A.q_cap = mp_cap;
+    A.list = d_list;
+    A.nlist = d_nlist;
+    A.th = th;
+    A.nnratio = nnratio;
+    A.kp2mp = d_kp2mp;
+    A.score = d_score;
+    A.nmatches = d_nmatches;
+    void* err;
+    rc = gf::ws_get(ctx, 38, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
     A.err = (int32_t*)err;
     return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);

@@ -169,6 +169,47 @@ def synth_scene(camera: str, n_mp: int, n_kp: int, seed: int, nlevels: int = 8, 
             "descriptors": np.ascontiguousarray(desc), "kp_mp": kp_mp, "camera": cam}
 
 
+def build_local_map(kps: np.ndarray, desc: np.ndarray, cam, rng, n_map: int, scale: float = 1.2,
+                    nlevels: int = 8, keep: float = 0.9, max_flip: int = 20, return_assoc: bool = False,
+                    noise_px: float = 0.5):
+    """Synthetic local map for one frame: most keypoints back-projected at a
+    random depth (camera at the origin), descriptor = keypoint descriptor with
+    a few flipped bits, plus distractor points with random descriptors. The
+    back-projection is perturbed by N(0, noise_px) pixels so poses have a
+    non-zero residual. With return_assoc, also the keypoint -> map index association (-1: none)."""
+    w, h, fx, fy, cx, cy = cam
+    n = len(kps)
+    sel = np.nonzero(rng.uniform(size=n) < keep)[0][:n_map]
+    z = rng.uniform(2, 8, len(sel))
+    du = rng.normal(0, noise_px, (len(sel), 2)) if noise_px else np.zeros((len(sel), 2))
+    X = np.stack([(kps["x"][sel] + du[:, 0] - cx) / fx * z, (kps["y"][sel] + du[:, 1] - cy) / fy * z, z], 1)
+    nd = n_map - len(sel)
+    zd = rng.uniform(2, 8, nd)
+    Xd = np.stack([(rng.uniform(0, w, nd) - cx) / fx * zd, (rng.uniform(0, h, nd) - cy) / fy * zd, zd], 1)
+    X = np.concatenate([X, Xd])
+    sf = np.array([np.float32(scale) ** i for i in range(nlevels)], np.float64)
+    lvl = np.concatenate([kps["octave"][sel], rng.integers(0, nlevels, nd)])
+    dist = np.linalg.norm(X, axis=1)
+    from .matcher import MAP_POINT_DTYPE
+
+    mp = np.zeros(n_map, MAP_POINT_DTYPE)
+    mp["pos"] = X
+    nrm = X / dist[:, None] + rng.normal(scale=0.01, size=X.shape)
+    mp["normal"] = nrm / np.linalg.norm(nrm, axis=1, keepdims=True)
+    mp["min_dist"] = dist / (sf[lvl] * 0.98)
+    mp["max_dist"] = mp["min_dist"] * sf[-1] * 1.2
+    mdesc = np.concatenate([flip_bits(rng, desc[sel], max_flip),
+                            rng.integers(0, 256, (nd, 32), dtype=np.uint8)])
+    perm = rng.permutation(n_map)  # local-map order is arbitrary (Tracking.cc:3780-3821)
+    if not return_assoc:
+        return mp[perm], np.ascontiguousarray(mdesc[perm])
+    inv = np.empty(n_map, np.int64)
+    inv[perm] = np.arange(n_map)
+    assoc = np.full(n, -1, np.int32)
+    assoc[sel] = inv[np.arange(len(sel))]
+    return mp[perm], np.ascontiguousarray(mdesc[perm]), assoc
+
+
 POSE_EDGE_DTYPE = np.dtype([("X", "<f4", 3), ("z", "<f4", 2), ("inv_sigma2", "<f4")])
 
 

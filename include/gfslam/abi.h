@@ -92,6 +92,13 @@ int gf_orb_extract_batch_dev(gf_extractor* ex, int nframes, const uint8_t* d_img
                              size_t frame_stride, int stride, gf_keypoint* d_kps,
                              uint8_t* d_desc, int32_t* d_counts, int cap, void* stream);
 
+/* Pointer-table form of gf_orb_extract_batch_dev: level 0 of frame f is the
+ * width x height image at d_img_ptrs[f] (a device array of device pointers,
+ * row stride `stride`), so frames can come from anywhere in HBM (a sequence
+ * ring, a staging buffer) without a gather copy. */
+int gf_orb_extract_ptrs_dev(gf_extractor* ex, int nframes, const uint8_t* const* d_img_ptrs, int stride,
+                            gf_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap, void* stream);
+
 /* Debug/parity hook: copies one intermediate plane of frame f of the last
  * batch to host. which: 0 = pyramid level (unblurred, ComputePyramid
  * ORBextractor.cc:922-998), 1 = blurred level interior (GaussianBlur :842).
@@ -175,6 +182,23 @@ int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, co
                            const uint8_t* d_last_outlier, const float* d_last_pos, const int32_t* d_n_last,
                            int last_cap, float th, int check_ori, int32_t* d_kp2mp, int32_t* d_score,
                            int32_t* d_nmatches, int32_t* d_scratch, void* stream);
+
+/* List forms (device family). Frame::isInFrustum for the map points
+ * d_list[f][0 .. d_nlist[f]) only (the visibility pass of
+ * SearchAdditionalMatchesInFrame over mLeftMapPoints, Tracking.cc:3105-3126);
+ * views of other points are left as they are. And
+ * ORBmatcher::SearchByProjection_Budget(F, vpMapPoints, th, time)
+ * (ORBmatcher.cc:276-379) = SearchByProjection over the map points of the
+ * list in list order (th != 1 scales the window; claims and the ratio test as
+ * M2). Lists are strided by mp_cap. */
+int gf_frustum_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw,
+                        const gf_map_point* d_mps, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                        float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview, void* stream);
+int gf_match_project_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                              const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                              const uint8_t* d_mp_desc, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                              float th, float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches,
+                              void* stream);
 
 /* ORBmatcher::DescriptorDistance (ORBmatcher.cc:2384-2400) over n pairs of
  * 32-byte rows: dist[i] = popcount(a[i] ^ b[i]). */
@@ -660,6 +684,142 @@ int gf_matched_gather_dev(gf_ctx* ctx, int nframes, const gf_keypoint* d_kps, co
 int gf_views_exclude_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
                                  int kp_stride, gf_mp_view* d_views, const int32_t* d_nmp, int mp_stride,
                                  void* stream);
+
+/* ------------------------------------------------ batched tracking front end
+ * Tracking::GrabImage in the WORKING state (Tracking.cc:461-917) for B
+ * independent sequences ("streams"), every frame of every stream on the
+ * device, no host round trip inside a step:
+ *   Frame (ORB extraction, E1-E8)
+ *   TrackWithMotionModel (Tracking.cc:1506-1642): Tcw = V * Tlast, M3
+ *     SearchByProjection(Cur, Last, 15), PoseOptimization, discard outliers
+ *   TrackLocalMap (:2732-2844) with SearchReferencePointsInFrustum
+ *     (:3149-3410): updatePWLSVec, FRAME_INFO_MATRIX, mCurrentInfoMat; then
+ *     num_to_match <= 0: mLeftMapPoints = in-view (stale mbTrackInView)
+ *       local points, mbNeedVizCheck;
+ *     else isInFrustum; nToMatch < 400: SearchByProjection(F, local, 1);
+ *       else MAP_INFO_MATRIX + runActiveMapMatching (leftovers = unmatched
+ *       pool); PoseOptimization (outliers kept, :2776)
+ *   motion model update V = Tcw * LastTwc (:729-738), updatePWLSVec +
+ *     predictPWLSVec(dt, 2), RunMapPointsSelection's MAP_INFO_MATRIX at
+ *     kinematic[1] (:1717-1779), SearchAdditionalMatchesInFrame
+ *     (:3097-3145: isInFrustum when mbNeedVizCheck, SearchByProjection_Budget
+ *     th 0.8), outliers set NULL, mLastFrame = Frame(mCurrentFrame) (:901-910).
+ * The local map (UpdateReference, :3689-3852) is the map set with
+ * gf_frontend_set_map, in that order; keyframe insertion and local mapping
+ * are outside the path. Track-loss fall-backs (TrackPreviousFrame,
+ * relocalisation) are not modelled: the step flags them in GF_FE_STATS and
+ * continues. updateAtFrameId stamps are stored relative to the current frame
+ * (the frame being tracked is 1, the next 2; every step shifts them by -1),
+ * so a step has no per-frame host argument and can be replayed as a HIP
+ * graph. Time budgets follow gf_set_budgets of the context (+inf = parity). */
+typedef struct gf_frontend_params {
+    int32_t width, height;
+    float fx, fy, cx, cy;       /* Camera.fx/fy/cx/cy; k1 = 0 (undistortion is a copy) */
+    int32_t nfeatures;          /* ORBextractor.nFeatures */
+    float scale_factor;         /* ORBextractor.scaleFactor */
+    int32_t nlevels;            /* ORBextractor.nLevels */
+    int32_t fast_th;            /* ORBextractor.fastTh */
+    int32_t batch;              /* streams B */
+    int32_t map_cap;            /* local-map capacity per stream (<= 4096) */
+    int32_t gf_budget;          /* num_good_inlier_predef (main.cc GF budget) */
+    int32_t gf;                 /* 1 GOOD_FEATURE_MAP_MATCHING, 0 ORB-SLAM baseline matching */
+    double dt;                  /* frame period 1 / Camera.fps (timestamps t_k = t_0 + k dt) */
+} gf_frontend_params;
+typedef struct gf_frontend gf_frontend;
+
+/* Per-stream state and outputs, readable / writable as whole-batch arrays. */
+enum {
+    GF_FE_KPS = 0,      /* [B][cap] gf_keypoint  mCurrentFrame.mvKeysUn      */
+    GF_FE_DESC,         /* [B][cap][32] u8       mDescriptors               */
+    GF_FE_NKP,          /* [B] i32               N                          */
+    GF_FE_TCW,          /* [B][16] f32           mTcw                       */
+    GF_FE_KP2MP,        /* [B][cap] i32          mvpMapPoints (map index)   */
+    GF_FE_SCORE,        /* [B][cap] i32          mvpMatchScore              */
+    GF_FE_OUTLIER,      /* [B][cap] u8           mvbOutlier                 */
+    GF_FE_LAST_KPS,     /* mLastFrame: as the four above                    */
+    GF_FE_LAST_DESC,
+    GF_FE_LAST_NKP,
+    GF_FE_LAST_KP2MP,
+    GF_FE_LAST_OUTLIER, /* [B][cap] u8                                      */
+    GF_FE_LAST_POS,     /* [B][cap][3] f32 world position of each last MP  */
+    GF_FE_TCW_LAST,     /* [B][16] f32 mLastFrame.mTcw                      */
+    GF_FE_VELOCITY,     /* [B][16] f32 mVelocity                            */
+    GF_FE_T_PREV,       /* [B] f64 mLastFrame.mTimeStamp                    */
+    GF_FE_T_CUR,        /* [B] f64 mCurrentFrame.mTimeStamp                 */
+    GF_FE_MAP,          /* [B][M] gf_map_point                              */
+    GF_FE_MAP_DESC,     /* [B][M][32] u8                                    */
+    GF_FE_NMP,          /* [B] i32                                          */
+    GF_FE_VIEWS,        /* [B][M] gf_mp_view (mbTrackInView & projection)   */
+    GF_FE_XV,           /* [B][13] f64 kinematic[0].Xv                      */
+    GF_FE_XV_NEXT,      /* [B][13] f64 kinematic[1].Xv                      */
+    GF_FE_BASE,         /* [B][49] f64 mCurrentInfoMat                      */
+    GF_FE_MP_H,         /* [B][M][14] f64 MapPoint::H_meas                  */
+    GF_FE_MP_INFO,      /* [B][M][49] f64 MapPoint::ObsMat                  */
+    GF_FE_MP_UV,        /* [B][M][2] f32 u_proj, v_proj                     */
+    GF_FE_MP_UPD,       /* [B][M] i32 updateAtFrameId (relative stamps)     */
+    GF_FE_RNG,          /* [B] gf_rng std::rand() state per stream          */
+    GF_FE_LEFT,         /* [B][M] i32 mLeftMapPoints of the last step       */
+    GF_FE_STATS,        /* [GF_FE_NSTAT][B] i32, see GF_ST_*                */
+    GF_FE_NFIELDS
+};
+enum {
+    GF_ST_M3 = 0,       /* SearchByProjection(Cur, Last) matches            */
+    GF_ST_FOUND,        /* nMatchesFound after the outlier discard          */
+    GF_ST_TO_MATCH,     /* num_to_match = budget - nMatchesFound            */
+    GF_ST_BRANCH,       /* 1 leftovers only, 2 SearchByProjection, 3 active matching, 4 nothing in view */
+    GF_ST_IN_VIEW,      /* nToMatch                                         */
+    GF_ST_LOCAL,        /* matches of the local-map search (M2 or active)   */
+    GF_ST_INL1,         /* inliers of the first PoseOptimization            */
+    GF_ST_INL2,         /* mnMatchesInliers                                 */
+    GF_ST_EXTRA,        /* SearchAdditionalMatchesInFrame matches           */
+    GF_ST_NLEFT,        /* mLeftMapPoints size                              */
+    GF_ST_ITER1, GF_ST_ITER2, GF_ST_EDGES1, GF_ST_EDGES2,
+    GF_ST_FLAGS,        /* 1: M3 < 20 (TrackPreviousFrame fall-back), 2: < 10 after PoseOptimization,
+                           4: mnMatchesInliers < 15 (LOST), 8: a time budget cut a loop */
+    GF_ST_FRAMES,       /* frames tracked                                   */
+    GF_FE_NSTAT
+};
+int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);
+int gf_frontend_destroy(gf_frontend* fe);
+/* Keypoint capacity per frame (sum of the extractor's level quotas). */
+int gf_frontend_capacity(gf_frontend* fe, int* cap);
+/* Frame source: stream b's frame at step k is the image at d_bases[b] +
+ * ((phase[b] + k) mod period) * frame_stride (device memory, row stride =
+ * width). d_bases / phase are host arrays of B entries (copied). */
+int gf_frontend_set_source(gf_frontend* fe, const uint8_t* const* d_bases, const int32_t* phase, int period,
+                           size_t frame_stride);
+/* The local map of one stream (host arrays; m <= map_cap), in
+ * mvpLocalMapPoints order. Resets that stream's observability state. */
+int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, const uint8_t* desc, int m);
+int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed);
+/* Start of tracking: the current source frame of every stream is taken at the
+ * given pose (Tcw [B][16]) and matched to its local map
+ * (isInFrustum + SearchByProjection(F, local, 1) with nnratio 0.8); it becomes
+ * mLastFrame with timestamp t0, V [B][16] the motion model, and the step
+ * counter advances by one. */
+int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0);
+/* One frame per stream from the source (asynchronous on the context stream). */
+int gf_frontend_step(gf_frontend* fe);
+/* Same with the B frames taken from host memory ([B][height][width] u8):
+ * the PCIe copy is part of the step. */
+int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs);
+/* Capture gf_frontend_step as one HIP graph; later steps replay it. */
+int gf_frontend_capture(gf_frontend* fe);
+int gf_frontend_sync(gf_frontend* fe);
+/* Copy a whole-batch field (synchronises; bytes must equal the field size). */
+int gf_frontend_read(gf_frontend* fe, int field, void* host, size_t bytes);
+int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes);
+/* Size and device pointer of a field. */
+int gf_frontend_field(gf_frontend* fe, int field, size_t* bytes, void** d_ptr);
+
+/* Wall-clock budgets of the reference's time-capped loops, in seconds:
+ * match_s = time_total_match (Tracking.cc:3230; the isInFrustum cap at half of
+ * it :3262-3270, runActiveMapMatching's cap :1366-1370), select_s = the
+ * post-publish budget of SearchAdditionalMatchesInFrame /
+ * SearchByProjection_Budget (Tracking.cc:3113-3137, ORBmatcher.cc:366-371).
+ * +inf (the default) is parity mode: no loop is cut. Measured on the device
+ * clock from the start of the frame's step. */
+int gf_set_budgets(gf_ctx* ctx, double match_s, double select_s);
 
 #ifdef __cplusplus
 }

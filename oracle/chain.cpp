@@ -1,0 +1,506 @@
+// CPU oracle of the batched tracking front end (test infrastructure: only
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline load it).
+//
+// One stream of gf_frontend_step restated sequentially on the oracle
+// operators, in the call order of Tracking::GrabImage in the WORKING state
+// (Tracking.cc:461-917; see include/gfslam/abi.h "batched tracking front
+// end"): Frame -> TrackWithMotionModel (:1506-1642) -> TrackLocalMap
+// (:2732-2844) with SearchReferencePointsInFrustum (:3149-3410) -> motion
+// model (:729-738) -> predictPWLSVec + RunMapPointsSelection (:795-800,
+// :1717-1779) -> SearchAdditionalMatchesInFrame (:3097-3145) -> outliers NULL
+// and mLastFrame = mCurrentFrame (:899-907). State lives in the same field
+// layouts as the device front end (B = 1), so a test can copy a device
+// stream's state in, run one frame here and compare every field.
+// Parity mode only: the time budgets are infinite.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "oracle_common.h"
+
+extern "C" {
+int orc_extract(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
+                int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+int orc_extractor_plan(int w, int h, int nfeatures, float scale_factor, int nlevels, int* level_w, int* level_h,
+                       int* feat_per_level, float* scales, int* umax16);
+int orc_frustum(const gf_frame_info* fi, const float* Tcw, const gf_map_point* mps, int m, float viewCosLimit,
+                gf_mp_view* views, int* n_in_view);
+int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                      const gf_mp_view* views, const uint8_t* mp_desc, int m, float th, float nnratio,
+                      int32_t* kp2mp, int32_t* score, int* nmatches);
+int orc_match_lastframe(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n, const float* Tcw,
+                        const gf_keypoint* last_kps, const uint8_t* last_desc, const int32_t* last_kp2mp,
+                        const uint8_t* last_outlier, const float* last_pos, int n_last, float th, int check_ori,
+                        int32_t* kp2mp, int32_t* score, int* nmatches);
+int orc_pose_opt(const float* Tcw_in, const float* X, const float* z, const int32_t* octave,
+                 const float* inv_sigma2_levels, int n, float fx, float fy, float cx, float cy, float* Tcw_out,
+                 uint8_t* outlier, int* ninliers, int* iterations);
+int orc_obs_update(double t0, const float* Tcw0, double t1, const float* Twc1, double* Xv);
+int orc_obs_predict(const double* Xv, double dt, int nseg, gf_kine* out);
+int orc_obs_build_info(const gf_obs_camera* cam, const double* Xv, const float* pos, const float* sigma2, int n,
+                       int check_viz, double* H, double* info, float* uv, uint8_t* valid);
+int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                             const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
+                             const double* info, const double* H, int m, const double* base,
+                             const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
+                             int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
+}
+
+namespace {
+
+// glibc srand(): the oracle's own restatement for seeding (TYPE_3, 310 discards)
+void rng_seed(gf_rng* r, uint32_t s) {
+    if (s == 0) s = 1;
+    r->state[0] = (int32_t)s;
+    int32_t word = (int32_t)s;
+    for (int i = 1; i < 31; ++i) {
+        long long hi = word / 127773, lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        r->state[i] = word;
+    }
+    r->f = 3;
+    r->r = 0;
+    for (int k = 0; k < 310; k++) {
+        uint32_t val = (uint32_t)r->state[r->f] + (uint32_t)r->state[r->r];
+        r->state[r->f] = (int32_t)val;
+        if (++r->f >= 31) {
+            r->f = 0;
+            ++r->r;
+        } else if (++r->r >= 31) {
+            r->r = 0;
+        }
+    }
+}
+
+void mat44(const float* a, const float* b, float* o) {
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            float s = a[4 * i] * b[j];
+            for (int k = 1; k < 4; k++) s = s + a[4 * i + k] * b[4 * k + j];
+            o[4 * i + j] = s;
+        }
+}
+
+// Frame::getTwc (Frame.cc:152-163) and LastTwc (Tracking.cc:731-735):
+// Rwc = R^T, twc = -Rwc * t.
+void twc_of(const float* T, float* W) {
+    for (int i = 0; i < 16; i++) W[i] = (i % 5 == 0) ? 1.f : 0.f;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) W[4 * i + j] = T[4 * j + i];
+        const float a = -T[i] * T[3], b = -T[4 + i] * T[7], c = -T[8 + i] * T[11];
+        W[4 * i + 3] = (a + b) + c;
+    }
+}
+
+}  // namespace
+
+struct orc_chain {
+    gf_frontend_params p{};
+    int cap = 0, M = 0;
+    gf_frame_info fi{};
+    gf_obs_camera oc{};
+    float inv_sigma2[16] = {}, level_sigma2[16] = {};
+    // fields (B = 1), layouts as gf_frontend
+    std::vector<gf_keypoint> kps, last_kps;
+    std::vector<uint8_t> desc, last_desc, outl, last_outl, map_desc;
+    int32_t nkp = 0, last_nkp = 0, nmp = 0;
+    float Tcw[16] = {}, Tcw_last[16] = {}, V[16] = {};
+    std::vector<int32_t> kp2mp, score, last_kp2mp, upd, left;
+    std::vector<float> last_pos, mp_uv;
+    double t_prev = 0, t_cur = 0;
+    std::vector<gf_map_point> map;
+    std::vector<gf_mp_view> views;
+    double Xv[13] = {}, Xv_next[13] = {}, base[49] = {};
+    std::vector<double> mp_H, mp_info;
+    gf_rng rng{};
+    int32_t stats[GF_FE_NSTAT] = {};
+};
+
+namespace {
+
+void field(orc_chain* c, int f, void** ptr, size_t* bytes) {
+    *ptr = nullptr;
+    *bytes = 0;
+#define FV(v) (*ptr = (void*)c->v.data(), *bytes = sizeof(c->v[0]) * c->v.size())
+#define FS(v) (*ptr = (void*)&c->v, *bytes = sizeof(c->v))
+    switch (f) {
+        case GF_FE_KPS: FV(kps); break;
+        case GF_FE_DESC: FV(desc); break;
+        case GF_FE_NKP: FS(nkp); break;
+        case GF_FE_TCW: FS(Tcw); break;
+        case GF_FE_KP2MP: FV(kp2mp); break;
+        case GF_FE_SCORE: FV(score); break;
+        case GF_FE_OUTLIER: FV(outl); break;
+        case GF_FE_LAST_KPS: FV(last_kps); break;
+        case GF_FE_LAST_DESC: FV(last_desc); break;
+        case GF_FE_LAST_NKP: FS(last_nkp); break;
+        case GF_FE_LAST_KP2MP: FV(last_kp2mp); break;
+        case GF_FE_LAST_OUTLIER: FV(last_outl); break;
+        case GF_FE_LAST_POS: FV(last_pos); break;
+        case GF_FE_TCW_LAST: FS(Tcw_last); break;
+        case GF_FE_VELOCITY: FS(V); break;
+        case GF_FE_T_PREV: FS(t_prev); break;
+        case GF_FE_T_CUR: FS(t_cur); break;
+        case GF_FE_MAP: FV(map); break;
+        case GF_FE_MAP_DESC: FV(map_desc); break;
+        case GF_FE_NMP: FS(nmp); break;
+        case GF_FE_VIEWS: FV(views); break;
+        case GF_FE_XV: FS(Xv); break;
+        case GF_FE_XV_NEXT: FS(Xv_next); break;
+        case GF_FE_BASE: FS(base); break;
+        case GF_FE_MP_H: FV(mp_H); break;
+        case GF_FE_MP_INFO: FV(mp_info); break;
+        case GF_FE_MP_UV: FV(mp_uv); break;
+        case GF_FE_MP_UPD: FV(upd); break;
+        case GF_FE_RNG: FS(rng); break;
+        case GF_FE_LEFT: FV(left); break;
+        case GF_FE_STATS: FS(stats); break;
+        default: break;
+    }
+#undef FV
+#undef FS
+}
+
+// batchInfoMat_Map (Observability.cc:556-644) over points i < m of the map:
+// skip those stamped fid and (check_viz == 0) those not in view; stamp the
+// valid ones. Returns updated flags (updateAtFrameId == fid).
+void map_info(orc_chain* c, const double* Xv, int m, int check_viz, int fid, std::vector<uint8_t>* updated) {
+    for (int i = 0; i < m; i++) {
+        if (c->upd[i] == fid) continue;
+        if (!check_viz && !c->views[i].in_view) continue;
+        double H[14], info[49];
+        float uv[2];
+        uint8_t valid = 0;
+        orc_obs_build_info(&c->oc, Xv, c->map[i].pos, nullptr, 1, check_viz, H, info, uv, &valid);
+        if (!valid) continue;
+        std::memcpy(&c->mp_H[14 * (size_t)i], H, sizeof(H));
+        std::memcpy(&c->mp_info[49 * (size_t)i], info, sizeof(info));
+        c->mp_uv[2 * i] = uv[0];
+        c->mp_uv[2 * i + 1] = uv[1];
+        c->upd[i] = fid;
+    }
+    if (updated) {
+        updated->assign(c->M, 0);
+        for (int i = 0; i < c->nmp; i++) (*updated)[i] = c->upd[i] == fid;
+    }
+}
+
+// Optimizer::PoseOptimization over the matched keypoints, in keypoint order.
+void pose(orc_chain* c, int* ninl, int* iters, int* nedges) {
+    std::vector<float> X, z;
+    std::vector<int32_t> oct, idx;
+    for (int i = 0; i < c->nkp; i++) {
+        const int mp = c->kp2mp[i];
+        if (mp < 0) continue;
+        for (int k = 0; k < 3; k++) X.push_back(c->map[mp].pos[k]);
+        z.push_back(c->kps[i].x);
+        z.push_back(c->kps[i].y);
+        oct.push_back(c->kps[i].octave);
+        idx.push_back(i);
+    }
+    const int n = (int)idx.size();
+    std::vector<uint8_t> o(n + 1);
+    float T[16];
+    int ni = 0, it = 0;
+    orc_pose_opt(c->Tcw, X.data(), z.data(), oct.data(), c->inv_sigma2, n, c->fi.fx, c->fi.fy, c->fi.cx, c->fi.cy, T,
+                 o.data(), &ni, &it);
+    std::memcpy(c->Tcw, T, sizeof(T));
+    for (int e = 0; e < n; e++) c->outl[idx[e]] = o[e];
+    *ninl = ni;
+    *iters = it;
+    *nedges = n;
+}
+
+// isInFrustum on the points of a list (others untouched).
+void frustum_list(orc_chain* c, const int32_t* list, int n) {
+    for (int k = 0; k < n; k++) {
+        const int i = list[k];
+        int cnt = 0;
+        orc_frustum(&c->fi, c->Tcw, &c->map[i], 1, 0.5f, &c->views[i], &cnt);
+    }
+}
+
+// SearchByProjection(F, vpMapPoints, th) over a list of map points in list
+// order (lists are ascending here, so the sequential loop over the whole map
+// with the non-members masked visits the members in list order).
+int project_list(orc_chain* c, const int32_t* list, int n, float th) {
+    std::vector<gf_mp_view> v(c->nmp);
+    for (int i = 0; i < c->nmp; i++) {
+        v[i] = c->views[i];
+        v[i].in_view = 0;
+    }
+    for (int k = 0; k < n; k++) v[list[k]].in_view = c->views[list[k]].in_view;
+    int nm = 0;
+    orc_match_project(&c->fi, c->kps.data(), c->desc.data(), c->nkp, v.data(), c->map_desc.data(), c->nmp, th, 0.8f,
+                      c->kp2mp.data(), c->score.data(), &nm);
+    return nm;
+}
+
+}  // namespace
+
+extern "C" {
+
+orc_chain* orc_chain_create(const gf_frontend_params* p) {
+    orc_chain* c = new orc_chain();
+    c->p = *p;
+    int lw[16], lh[16], fpl[16], um[16];
+    float sc[16];
+    orc_extractor_plan(p->width, p->height, p->nfeatures, p->scale_factor, p->nlevels, lw, lh, fpl, sc, um);
+    c->cap = 0;
+    for (int l = 0; l < p->nlevels; l++) c->cap += fpl[l];
+    c->M = p->map_cap;
+    c->fi = gf_frame_info{0, p->width, 0, p->height, p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
+    float sf = 1.f;
+    for (int l = 0; l < p->nlevels; l++) {
+        if (l) sf = sf * p->scale_factor;
+        c->level_sigma2[l] = sf * sf;
+        c->inv_sigma2[l] = 1.0f / (sf * sf);
+    }
+    gf_obs_camera& oc = c->oc;
+    oc.fu = p->fx;
+    oc.fv = p->fy;
+    oc.cx = p->cx;
+    oc.cy = p->cy;
+    oc.nrows = p->height;
+    oc.ncols = p->width;
+    oc.min_x = 0;
+    oc.max_x = p->width;
+    oc.min_y = 0;
+    oc.max_y = p->height;
+    oc.bound_x = (int)(p->width * 0.1);
+    oc.bound_y = (int)(p->height * 0.1);
+    oc.bound_depth = 0.f;
+    const size_t cap = c->cap, M = c->M;
+    c->kps.assign(cap, gf_keypoint{});
+    c->last_kps.assign(cap, gf_keypoint{});
+    c->desc.assign(cap * 32, 0);
+    c->last_desc.assign(cap * 32, 0);
+    c->outl.assign(cap, 0);
+    c->last_outl.assign(cap, 0);
+    c->kp2mp.assign(cap, 0);
+    c->score.assign(cap, 0);
+    c->last_kp2mp.assign(cap, 0);
+    c->last_pos.assign(cap * 3, 0.f);
+    c->map.assign(M, gf_map_point{});
+    c->map_desc.assign(M * 32, 0);
+    c->views.assign(M, gf_mp_view{});
+    c->upd.assign(M, -1000);
+    c->left.assign(M, 0);
+    c->mp_uv.assign(M * 2, 0.f);
+    c->mp_H.assign(M * 14, 0.0);
+    c->mp_info.assign(M * 49, 0.0);
+    for (int i = 0; i < 4; i++) c->Tcw_last[5 * i] = c->V[5 * i] = 1.f;
+    rng_seed(&c->rng, 1);
+    return c;
+}
+
+void orc_chain_destroy(orc_chain* c) { delete c; }
+
+int orc_chain_capacity(orc_chain* c) { return c->cap; }
+
+int orc_chain_read(orc_chain* c, int f, void* host, size_t bytes) {
+    void* p;
+    size_t b;
+    field(c, f, &p, &b);
+    if (!p || b != bytes) return GF_ERR_ARG;
+    std::memcpy(host, p, b);
+    return GF_OK;
+}
+
+int orc_chain_write(orc_chain* c, int f, const void* host, size_t bytes) {
+    void* p;
+    size_t b;
+    field(c, f, &p, &b);
+    if (!p || b != bytes) return GF_ERR_ARG;
+    std::memcpy(p, host, b);
+    return GF_OK;
+}
+
+int orc_chain_set_map(orc_chain* c, const gf_map_point* mps, const uint8_t* desc, int m) {
+    if (m < 0 || m > c->M) return GF_ERR_ARG;
+    std::memcpy(c->map.data(), mps, sizeof(gf_map_point) * m);
+    std::memcpy(c->map_desc.data(), desc, 32 * (size_t)m);
+    c->nmp = m;
+    std::fill(c->upd.begin(), c->upd.end(), -1000);
+    std::fill(c->views.begin(), c->views.end(), gf_mp_view{});
+    return GF_OK;
+}
+
+int orc_chain_set_rng(orc_chain* c, uint32_t seed) {
+    rng_seed(&c->rng, seed);
+    return GF_OK;
+}
+
+static int extract(orc_chain* c, const uint8_t* img) {
+    int n = 0;
+    int rc = orc_extract(img, c->p.width, c->p.height, c->p.width, c->p.nfeatures, c->p.scale_factor, c->p.nlevels,
+                         c->p.fast_th, c->kps.data(), c->desc.data(), c->cap, &n);
+    c->nkp = n;
+    return rc;
+}
+
+static void make_last(orc_chain* c) {
+    const int n = c->nkp;
+    for (int i = 0; i < n; i++) {
+        const int mp = c->kp2mp[i];
+        c->last_kp2mp[i] = mp;
+        c->last_outl[i] = c->outl[i];
+        c->last_kps[i] = c->kps[i];
+        for (int k = 0; k < 3; k++) c->last_pos[3 * i + k] = mp >= 0 ? c->map[mp].pos[k] : 0.f;
+    }
+    std::memcpy(c->last_desc.data(), c->desc.data(), 32 * (size_t)n);
+    c->last_nkp = n;
+    std::memcpy(c->Tcw_last, c->Tcw, sizeof(c->Tcw));
+    c->t_prev = c->t_cur;
+}
+
+int orc_chain_bootstrap(orc_chain* c, const uint8_t* img, const float* Tcw, const float* V, double t0) {
+    std::memcpy(c->Tcw, Tcw, sizeof(c->Tcw));
+    std::memcpy(c->V, V, sizeof(c->V));
+    c->t_cur = t0;
+    std::fill(c->kp2mp.begin(), c->kp2mp.end(), -1);
+    std::fill(c->score.begin(), c->score.end(), 999);
+    std::fill(c->outl.begin(), c->outl.end(), 0);
+    int rc = extract(c, img);
+    if (rc) return rc;
+    int nv = 0, nm = 0;
+    orc_frustum(&c->fi, c->Tcw, c->map.data(), c->nmp, 0.5f, c->views.data(), &nv);
+    orc_match_project(&c->fi, c->kps.data(), c->desc.data(), c->nkp, c->views.data(), c->map_desc.data(), c->nmp, 1.f,
+                      0.8f, c->kp2mp.data(), c->score.data(), &nm);
+    make_last(c);
+    return GF_OK;
+}
+
+int orc_chain_step(orc_chain* c, const uint8_t* img) {
+    int32_t* st = c->stats;
+    const int frames = st[GF_ST_FRAMES];
+    std::memset(st, 0, sizeof(c->stats));
+    st[GF_ST_FRAMES] = frames;
+    // Frame + TrackWithMotionModel (Tracking.cc:1506-1642)
+    c->t_cur = c->t_prev + c->p.dt;
+    mat44(c->V, c->Tcw_last, c->Tcw);
+    std::fill(c->kp2mp.begin(), c->kp2mp.end(), -1);
+    std::fill(c->score.begin(), c->score.end(), 999);
+    std::fill(c->outl.begin(), c->outl.end(), 0);
+    int rc = extract(c, img);
+    if (rc) return rc;
+    const int n = c->nkp;
+    int nm = 0;
+    orc_match_lastframe(&c->fi, c->kps.data(), c->desc.data(), n, c->Tcw, c->last_kps.data(), c->last_desc.data(),
+                        c->last_kp2mp.data(), c->last_outl.data(), c->last_pos.data(), c->last_nkp, 15.f, 1,
+                        c->kp2mp.data(), c->score.data(), &nm);
+    st[GF_ST_M3] = nm;
+    pose(c, &st[GF_ST_INL1], &st[GF_ST_ITER1], &st[GF_ST_EDGES1]);
+    int found = 0;
+    for (int i = 0; i < n; i++)
+        if (c->kp2mp[i] >= 0) {
+            if (c->outl[i]) {
+                c->kp2mp[i] = -1;
+                c->outl[i] = 0;
+            } else {
+                found++;
+            }
+        }
+    st[GF_ST_FOUND] = found;
+    const int ntm = c->p.gf_budget - found;
+    st[GF_ST_TO_MATCH] = ntm;
+    // TrackLocalMap -> SearchReferencePointsInFrustum (Tracking.cc:3149-3410)
+    const bool gf = c->p.gf != 0;
+    float Twc[16];
+    if (gf) {
+        twc_of(c->Tcw, Twc);
+        orc_obs_update(c->t_prev, c->Tcw_last, c->t_cur, Twc, c->Xv);
+        // FRAME_INFO_MATRIX over the matched keypoints (Observability.cc:386-554)
+        for (int i = 0; i < n; i++) {
+            const int mp = c->kp2mp[i];
+            if (mp < 0 || mp >= c->nmp || c->outl[i]) continue;
+            const float s2 = c->level_sigma2[c->kps[i].octave];
+            uint8_t valid;
+            orc_obs_build_info(&c->oc, c->Xv, c->map[mp].pos, &s2, 1, 0, &c->mp_H[14 * (size_t)mp],
+                               &c->mp_info[49 * (size_t)mp], &c->mp_uv[2 * mp], &valid);
+        }
+        // mCurrentInfoMat = 1e-5 I + matched ObsMat stamped for this frame (:3161, :3195-3219)
+        for (int e = 0; e < 49; e++) c->base[e] = (e % 8 == 0) ? 1e-5 : 0.0;
+        for (int i = 0; i < n; i++) {
+            const int mp = c->kp2mp[i];
+            if (mp < 0 || mp >= c->nmp || c->upd[mp] != 1) continue;
+            for (int e = 0; e < 49; e++) c->base[e] = c->base[e] + c->mp_info[49 * (size_t)mp + e];
+        }
+    }
+    for (int i = 0; i < n; i++)  // mbTrackInView = false for matched points (:3205)
+        if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
+    int branch = 0, nlist = 0;
+    bool viz = false;
+    std::vector<int32_t> list;
+    if (gf && ntm <= 0) {  // :3231-3249, stale mbTrackInView
+        for (int i = 0; i < c->nmp; i++)
+            if (c->views[i].in_view) list.push_back(i);
+        branch = 1;
+        viz = true;
+    } else {
+        int nv = 0;
+        orc_frustum(&c->fi, c->Tcw, c->map.data(), c->nmp, 0.5f, c->views.data(), &nv);
+        for (int i = 0; i < n; i++)
+            if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
+        int nin = 0;
+        for (int i = 0; i < c->nmp; i++) nin += c->views[i].in_view ? 1 : 0;
+        st[GF_ST_IN_VIEW] = nin;
+        if (nin == 0) {
+            branch = 4;
+        } else if (!gf || nin < 400) {  // :3322-3323
+            branch = 2;
+            int k = 0;
+            orc_match_project(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(), c->nmp,
+                              1.f, 0.8f, c->kp2mp.data(), c->score.data(), &k);
+            st[GF_ST_LOCAL] = k;
+        } else {  // :3329-3343
+            branch = 3;
+            std::vector<uint8_t> updated;
+            map_info(c, c->Xv, c->nmp, 0, 1, &updated);
+            std::vector<int32_t> left(c->M);
+            int nleft = 0, nmatched = 0;
+            orc_obs_active_match_rng(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(),
+                                     updated.data(), c->mp_info.data(), c->mp_H.data(), c->nmp, c->base,
+                                     c->level_sigma2, ntm, 1.f, 0.8f, &c->rng, c->kp2mp.data(), c->score.data(),
+                                     left.data(), &nleft, &nmatched);
+            st[GF_ST_LOCAL] = nmatched;
+            list.assign(left.begin(), left.begin() + nleft);
+        }
+    }
+    st[GF_ST_BRANCH] = branch;
+    pose(c, &st[GF_ST_INL2], &st[GF_ST_ITER2], &st[GF_ST_EDGES2]);  // outliers kept (:2776)
+    // motion model (:729-738)
+    float LastTwc[16];
+    twc_of(c->Tcw_last, LastTwc);
+    mat44(c->Tcw, LastTwc, c->V);
+    nlist = (int)list.size();
+    for (int k = 0; k < nlist; k++) c->left[k] = list[k];
+    st[GF_ST_NLEFT] = nlist;
+    if (gf) {
+        // predictPWLSVec(dt, 2) and RunMapPointsSelection at kinematic[1] (:795-800, :1717-1779)
+        twc_of(c->Tcw, Twc);
+        orc_obs_update(c->t_prev, c->Tcw_last, c->t_cur, Twc, c->Xv);
+        gf_kine kin[2];
+        orc_obs_predict(c->Xv, c->t_cur - c->t_prev, 2, kin);
+        std::memcpy(c->Xv_next, kin[1].Xv, sizeof(c->Xv_next));
+        map_info(c, c->Xv_next, c->nmp, 1, 2, nullptr);
+        // SearchAdditionalMatchesInFrame (:3097-3145)
+        if (viz) frustum_list(c, list.data(), nlist);
+        st[GF_ST_EXTRA] = project_list(c, list.data(), nlist, 0.8f);
+    }
+    // outliers NULL, mLastFrame = Frame(mCurrentFrame) (:899-907)
+    for (int i = 0; i < n; i++)
+        if (c->kp2mp[i] >= 0 && c->outl[i]) c->kp2mp[i] = -1;
+    make_last(c);
+    for (int i = 0; i < c->nmp; i++) c->upd[i] -= 1;
+    int fl = 0;
+    if (st[GF_ST_M3] < 20) fl |= 1;
+    if (st[GF_ST_FOUND] < 10) fl |= 2;
+    if (st[GF_ST_INL2] < 15) fl |= 4;
+    st[GF_ST_FLAGS] = fl;
+    st[GF_ST_FRAMES] = frames + 1;
+    return GF_OK;
+}
+
+}  // extern "C"

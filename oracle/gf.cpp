@@ -395,6 +395,19 @@ struct Rand {  // glibc random_r TYPE_3 (the generator behind std::rand)
         std::memset(&rd, 0, sizeof(rd));
         initstate_r(s, state, sizeof(state), &rd);
     }
+    // continue from a saved state (gf_rng: the 31 words and the front / rear
+    // indices of glibc's random_data)
+    void load(const gf_rng& g) {
+        seed(1);
+        for (int i = 0; i < 31; i++) rd.state[i] = g.state[i];
+        rd.fptr = rd.state + g.f;
+        rd.rptr = rd.state + g.r;
+    }
+    void save(gf_rng& g) const {
+        for (int i = 0; i < 31; i++) g.state[i] = rd.state[i];
+        g.f = (int32_t)(rd.fptr - rd.state);
+        g.r = (int32_t)(rd.rptr - rd.state);
+    }
     int next() {
         int32_t r;
         random_r(&rd, &r);
@@ -454,13 +467,43 @@ int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uin
                       int32_t* kp2mp, int32_t* score, int* nmatches);
 
 // runActiveMapMatching, Observability.cc:1249-1524 (FRAME_INFO_MATRIX).
+static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                        const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
+                        const double* H, int m, const double* base, const float* level_sigma2, int num_to_match,
+                        float th, float nnratio, int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft,
+                        int* nmatched);
+
 int orc_obs_active_match(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
                          const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
                          const double* H, const float* uv, int m, const double* base, const float* level_sigma2,
                          int num_to_match, float th, float nnratio, unsigned rng_seed, int32_t* kp2mp,
                          int32_t* score, int32_t* left, int* nleft, int* nmatched) {
+    (void)uv;
     orc::Rand R;
     R.seed(rng_seed);
+    return active_match(R, fi, kps, desc, n, views, mp_desc, updated, info, H, m, base, level_sigma2, num_to_match, th,
+                        nnratio, kp2mp, score, left, nleft, nmatched);
+}
+
+// Same, continuing the caller's std::rand() state (one sequence across frames).
+int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                             const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
+                             const double* info, const double* H, int m, const double* base,
+                             const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
+                             int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched) {
+    orc::Rand R;
+    R.load(*rng);
+    int rc = active_match(R, fi, kps, desc, n, views, mp_desc, updated, info, H, m, base, level_sigma2, num_to_match,
+                          th, nnratio, kp2mp, score, left, nleft, nmatched);
+    R.save(*rng);
+    return rc;
+}
+
+static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                        const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
+                        const double* H, int m, const double* base, const float* level_sigma2, int num_to_match,
+                        float th, float nnratio, int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft,
+                        int* nmatched) {
     *nleft = 0;
     *nmatched = 0;
     auto push_left_all = [&]() {

@@ -1,158 +1,103 @@
-"""One front-end step of the reference path on the CPU oracle (test
-infrastructure: bench.py's cpu_baseline and the pipeline tests only).
+"""The CPU oracle of the tracking front end (oracle/chain.cpp) for one stream
+— test infrastructure: bench.py's cpu_baseline and the pipeline tests only.
 
-Mirrors pipeline.FrontEnd.step stage by stage for a single stream:
-extract -> motion model -> SearchByProjection(last frame) -> PoseOptimization
--> discard outliers -> updatePWLSVec -> FRAME_INFO_MATRIX -> mCurrentInfoMat
--> isInFrustum -> MAP_INFO_MATRIX -> runActiveMapMatching -> PoseOptimization
--> discard outliers -> updatePWLSVec + 2-segment prediction -> next-frame
-MAP_INFO_MATRIX (check_viz) stamped frame_id + 1.
-
-The map-resident observability state (MapPoint::ObsMat, H_meas, u/v_proj,
-updateAtFrameId) lives in a MapState and carries over between steps.
+`Chain` mirrors gf_orb_slam_amd.pipeline.FrontEnd with B = 1 and the same
+field layouts, so a device stream's state can be copied in (`load_from`),
+one frame tracked on the CPU, and every field compared.
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 
 import oracle_lib as O
-from gf_orb_slam_amd import synth
-from gf_orb_slam_amd.matcher import FrameInfo
-from gf_orb_slam_amd.observability import ObsCamera
-from gf_orb_slam_amd.optimizer import inv_level_sigma2
-from gf_orb_slam_amd.pipeline import build_local_map
+from gf_orb_slam_amd.pipeline import FIELDS, NSTAT, STATS, FrontendParams, field_shape
+
+_P = ctypes.c_void_p
 
 
-class Prepared:
-    pass
+def _orc():
+    o = O.orc()
+    if not getattr(o, "_chain_declared", False):
+        o.orc_chain_create.restype = _P
+        o.orc_chain_create.argtypes = [_P]
+        o.orc_chain_destroy.argtypes = [_P]
+        o.orc_chain_capacity.argtypes = [_P]
+        o.orc_chain_read.argtypes = [_P, ctypes.c_int, _P, ctypes.c_size_t]
+        o.orc_chain_write.argtypes = [_P, ctypes.c_int, _P, ctypes.c_size_t]
+        o.orc_chain_set_map.argtypes = [_P, _P, _P, ctypes.c_int]
+        o.orc_chain_set_rng.argtypes = [_P, ctypes.c_uint32]
+        o.orc_chain_bootstrap.argtypes = [_P, _P, _P, _P, ctypes.c_double]
+        o.orc_chain_step.argtypes = [_P, _P]
+        o._chain_declared = True
+    return o
 
 
-class MapState:
-    """MapPoint::H_meas / ObsMat / u,v_proj / updateAtFrameId for M points."""
-
-    def __init__(self, m: int):
-        self.H = np.zeros((m, 14))
-        self.info = np.zeros((m, 49))
-        self.uv = np.zeros((m, 2), np.float32)
-        self.upd = np.full(m, -1, np.int64)
-
-    def copy(self):
-        c = MapState(len(self.upd))
-        c.H, c.info, c.uv, c.upd = self.H.copy(), self.info.copy(), self.uv.copy(), self.upd.copy()
-        return c
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
 
 
-def frame_info_stage(P, xv, kps, kp2mp, outl, st: MapState) -> None:
-    """batchInfoMat_Frame (Observability.cc:386-554) over the matched keypoints."""
-    idx = np.nonzero((kp2mp >= 0) & (outl == 0))[0]
-    if len(idx) == 0:
-        return
-    mp = kp2mp[idx]
-    H, info, uv, _ = O.obs_build_info(P.obs_cam, xv, P.mps["pos"][mp], P.level_sigma2[kps["octave"][idx]], 0)
-    st.H[mp], st.info[mp], st.uv[mp] = H, info, uv  # later keypoints win, as the sequential loop
+class Chain:
+    """One stream of the front end on the CPU oracle."""
+
+    def __init__(self, camera: str, nfeatures: int, map_size: int, gf_budget: int, gf: bool = True,
+                 fps: float = 20.0):
+        self.params = FrontendParams.make(camera, nfeatures, 1, map_size, gf_budget, gf, fps)
+        self.h = _orc().orc_chain_create(ctypes.byref(self.params))
+        self.cap = _orc().orc_chain_capacity(self.h)
+        self.M = map_size
+
+    def __del__(self):
+        try:
+            _orc().orc_chain_destroy(self.h)
+        except Exception:
+            pass
+
+    def set_map(self, mps, desc):
+        mps = np.ascontiguousarray(mps)
+        desc = np.ascontiguousarray(desc, np.uint8)
+        assert _orc().orc_chain_set_map(self.h, _p(mps), _p(desc), len(mps)) == 0
+
+    def set_rng(self, seed: int):
+        _orc().orc_chain_set_rng(self.h, ctypes.c_uint32(seed))
+
+    def bootstrap(self, img, Tcw, V, t0: float = 0.0):
+        img = np.ascontiguousarray(img, np.uint8)
+        T = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+        Vv = np.ascontiguousarray(V, np.float32).reshape(16)
+        assert _orc().orc_chain_bootstrap(self.h, _p(img), _p(T), _p(Vv), ctypes.c_double(t0)) == 0
+
+    def step(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        assert _orc().orc_chain_step(self.h, _p(img)) == 0
+
+    def read(self, name: str) -> np.ndarray:
+        fid, dt, shape = field_shape(name, 1, self.cap, self.M)
+        out = np.zeros(shape, dt)
+        assert _orc().orc_chain_read(self.h, fid, _p(out), out.nbytes) == 0, name
+        return out[:, 0] if name == "stats" else out[0]
+
+    def write(self, name: str, arr):
+        fid, dt, shape = field_shape(name, 1, self.cap, self.M)
+        a = np.ascontiguousarray(np.asarray(arr, dt).reshape(shape))
+        assert _orc().orc_chain_write(self.h, fid, _p(a), a.nbytes) == 0, name
+
+    def stats(self) -> dict:
+        s = self.read("stats")
+        return {k: int(s[i]) for i, k in enumerate(STATS)}
+
+    STATE = ["last_kps", "last_desc", "last_nkp", "last_kp2mp", "last_outlier", "last_pos", "Tcw_last", "velocity",
+             "t_prev", "map", "map_desc", "nmp", "views", "mp_H", "mp_info", "mp_uv", "mp_upd", "rng"]
+
+    def load_from(self, dev_state: dict, b: int):
+        """Copy stream b's carried-over state (FrontEnd.read outputs) in."""
+        for k in self.STATE:
+            self.write(k, dev_state[k][b])
+        st = np.zeros(NSTAT, np.int32)
+        st[STATS.index("frames")] = dev_state["stats"][STATS.index("frames"), b]
+        self.write("stats", st)
 
 
-def accumulate_stage(kp2mp, st: MapState, fid: int, diag: float = 1e-5) -> np.ndarray:
-    """mCurrentInfoMat (Tracking.cc:3184, 3195-3213)."""
-    acc = np.eye(7).reshape(-1) * diag
-    for mp in kp2mp:
-        if mp >= 0 and st.upd[mp] == fid:
-            acc = acc + st.info[mp]
-    return acc
-
-
-def map_info_stage(P, xv, views, check_viz: int, st: MapState, fid: int) -> np.ndarray:
-    """batchInfoMat_Map (Observability.cc:556-644); returns updateAtFrameId == fid."""
-    H, info, uv, valid = O.obs_build_info(P.obs_cam, xv, P.mps["pos"], None, check_viz)
-    sel = (st.upd != fid) & (valid != 0)
-    if not check_viz:
-        sel &= views["in_view"] != 0
-    st.H[sel], st.info[sel], st.uv[sel] = H[sel], info[sel], uv[sel]
-    st.upd[sel] = fid
-    return (st.upd == fid).astype(np.uint8)
-
-
-def twc_of(T: np.ndarray) -> np.ndarray:
-    """Frame::getTwc (Frame.cc:152-163) in float."""
-    Twc = np.eye(4, dtype=np.float32)
-    Twc[:3, :3] = T[:3, :3].T
-    Twc[:3, 3] = ((-T[0, :3] * T[0, 3]) + (-T[1, :3] * T[1, 3])) + (-T[2, :3] * T[2, 3])
-    return Twc
-
-
-def prepare(camera: str, nfeat: int, img: np.ndarray, seed: int, map_size: int = 2000, last_matches: int = 60,
-            rot_deg: float = 0.3, trans: float = 0.01, fps: float = 20.0) -> Prepared:
-    """Same set-up as FrontEnd.build_maps for one stream (camera at identity)."""
-    P = Prepared()
-    P.cam = synth.CAMERAS[camera]
-    w, h, fx, fy, cx, cy = P.cam
-    P.nfeat, P.img, P.fps = nfeat, img, fps
-    P.info = FrameInfo.make(*P.cam)
-    P.obs_cam = ObsCamera.for_tracking(fx, fy, cx, cy, w, h)
-    P.inv_sigma2 = inv_level_sigma2()
-    sf = P.info.scale_factors()
-    P.level_sigma2 = (sf * sf).astype(np.float32)
-    rng = np.random.default_rng(seed)
-    k, d = O.extract(img, nfeatures=nfeat)
-    P.mps, P.mdesc, assoc = build_local_map(k, d, P.cam, rng, map_size, return_assoc=True)
-    cand = np.nonzero(assoc >= 0)[0]
-    keep = np.sort(rng.choice(cand, min(last_matches, len(cand)), replace=False))
-    P.last_kps, P.last_desc = k, d
-    P.last_kp2mp = np.full(len(k), -1, np.int32)
-    P.last_kp2mp[keep] = assoc[keep]
-    P.last_pos = np.zeros((len(k), 3), np.float32)
-    P.last_pos[keep] = P.mps["pos"][assoc[keep]]
-    P.V = synth.look_pose(rng, trans, rot_deg)
-    P.Tlast = np.eye(4, dtype=np.float32)
-    P.seed = seed
-    P.state = MapState(map_size)
-    P.fid = 1
-    return P
-
-
-def _pose(P, T0, kps, kp2mp):
-    idx = np.nonzero(kp2mp >= 0)[0]
-    X = P.mps["pos"][kp2mp[idx]]
-    z = np.c_[kps["x"][idx], kps["y"][idx]]
-    T, outl, ninl, iters = O.pose_opt(T0, X, z, kps["octave"][idx].astype(np.int32), P.inv_sigma2, *P.cam[2:])
-    kp2mp[idx[outl == 1]] = -1  # Tracking.cc:1550-1563
-    return T, ninl, iters
-
-
-def _matmul_f32(A, B):
-    out = np.zeros((4, 4), np.float32)
-    for i in range(4):
-        for j in range(4):
-            s = np.float32(A[i, 0] * B[0, j])
-            for k in range(1, 4):
-                s = np.float32(s + np.float32(A[i, k] * B[k, j]))
-            out[i, j] = s
-    return out
-
-
-def step(P: Prepared, budget: int = 100) -> dict:
-    kps, desc = O.extract(P.img, nfeatures=P.nfeat)
-    n = len(kps)
-    T = _matmul_f32(P.V, P.Tlast)
-    kp2mp = np.full(n, -1, np.int32)
-    score = np.full(n, 999, np.int32)
-    O.match_lastframe(P.info, kps, desc, T, P.last_kps, P.last_desc, P.last_kp2mp.copy(),
-                      np.zeros(len(P.last_kps), np.uint8), P.last_pos, 15.0, 1, kp2mp, score)
-    T, _, it1 = _pose(P, T, kps, kp2mp)
-    nmatch = int((kp2mp >= 0).sum())
-    st, fid, dt = P.state, P.fid, 1.0 / P.fps
-    xv = O.obs_update(0.0, P.Tlast, dt, twc_of(T))
-    outl = np.zeros(n, np.uint8)
-    frame_info_stage(P, xv, kps, kp2mp, outl, st)
-    base = accumulate_stage(kp2mp, st, fid)
-    views, _ = O.frustum(P.info, T, P.mps)
-    views["in_view"][kp2mp[kp2mp >= 0]] = 0
-    updated = map_info_stage(P, xv, views, 0, st, fid)
-    nact, _ = O.active_match(P.info, kps, desc, views, P.mdesc, updated, st.info, st.H, st.uv, base,
-                             P.level_sigma2, budget - nmatch, 1.0, 0.8, P.seed, kp2mp, score)
-    T, ninl, it2 = _pose(P, T, kps, kp2mp)
-    xv = O.obs_update(0.0, P.Tlast, dt, twc_of(T))
-    xv1 = np.array(O.obs_predict(xv, dt, 2)[1].Xv)
-    map_info_stage(P, xv1, None, 1, st, fid + 1)
-    P.fid += 1
-    return {"Tcw": T, "kp2mp": kp2mp, "ninliers": ninl, "iterations": (it1, it2), "n_active": nact}
+def read_state(fe, names=None) -> dict:
+    return {k: fe.read(k) for k in (names or FIELDS)}

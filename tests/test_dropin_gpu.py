@@ -14,7 +14,6 @@ from gf_orb_slam_amd.matcher import FrameInfo
 from gf_orb_slam_amd.observability import ObsCamera
 from gf_orb_slam_amd.optimizer import inv_level_sigma2
 from gf_orb_slam_amd.orb import KEYPOINT_DTYPE
-from gf_orb_slam_amd.pipeline import build_local_map
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "tests", "cpp", "dropin_frontend")
@@ -31,7 +30,7 @@ def test_dropin_frontend_matches_oracle(tmp_path):
     img = synth.synth_frame(w, h, synth.frame_seed(3, 7))
     k, d = O.extract(img)
     rng = np.random.default_rng(12)
-    mps, mdesc = build_local_map(k, d, cam, rng, 1500)
+    mps, mdesc = synth.build_local_map(k, d, cam, rng, 1500)
     T0 = synth.look_pose(rng, 0.005, 0.2)
     with open(tmp_path / "params.txt", "w") as f:
         f.write(f"{w} {h} {fx} {fy} {cx} {cy} {len(mps)}\n" + " ".join(repr(float(x)) for x in T0.reshape(-1)))

@@ -1,214 +1,212 @@
-"""The composed device front end (pipeline.FrontEnd) against the oracle chain.
+"""The batched tracking front end (gf_frontend_*, pipeline.FrontEnd) against
+the CPU oracle chain (oracle/chain.cpp) on rendered sequences.
 
-After one warm-up step (so the map carries observability state stamped by the
-previous frame's prediction pass), every stage of the next step runs on the
-device for B streams; its inputs and outputs are snapshotted and the oracle
-runs the same stage on the same inputs (tests/oracle_chain.py): keypoint and
-match indices, information blocks and frame stamps bit-exact, poses within
-1e-5 relative (north_star), active-matching claims identical. This is what
-makes the bench step a measurement of the reference path and not of a
-look-alike.
+Every step, each checked stream's carried-over state is copied from the
+device into the oracle, the oracle tracks the same frame, and every field is
+compared: keypoints, descriptors, match indices, scores, outlier flags,
+views, updateAtFrameId stamps, leftovers, std::rand() state and the stage
+counters bit-exact; poses and the motion model within 1e-5 relative
+(north_star); observability blocks within 1e-9 relative (f64 transcendental
+ulps in the motion prediction). A second oracle runs the same streams free
+(no copy-in) and must stay in agreement with the device frame after frame.
 """
 import numpy as np
 import pytest
 
 import oracle_chain as C
 import oracle_lib as O
-from gf_orb_slam_amd import synth
-from gf_orb_slam_amd.matcher import MAP_POINT_DTYPE, MP_VIEW_DTYPE
-from gf_orb_slam_amd.orb import KEYPOINT_DTYPE
+from gf_orb_slam_amd import scene
 
-B = 3
-
-
-def _np(t):
-    return t.cpu().numpy().copy()
+EXACT = ["kps", "desc", "nkp", "kp2mp", "score", "outlier", "last_kps", "last_desc", "last_nkp", "last_kp2mp",
+         "last_outlier", "last_pos", "views", "mp_upd", "rng", "t_prev", "t_cur"]
+POSE = ["Tcw", "velocity", "Tcw_last"]
+F64 = ["Xv", "Xv_next", "base", "mp_H", "mp_info", "mp_uv"]
+STATE = C.Chain.STATE + ["stats"]
 
 
-def _kp(t, b, n):
-    return t[b].cpu().numpy().view(KEYPOINT_DTYPE).reshape(-1)[:n].copy()
-
-
-class _P:  # the oracle_chain.Prepared fields the stage helpers read
-    pass
-
-
-def _prep(fe, mps_b):
-    P = _P()
-    P.obs_cam, P.level_sigma2, P.mps, P.info = fe.obs_cam, fe.level_sigma2, mps_b, fe.info
-    return P
-
-
-def _state(fe, b):
-    st = C.MapState(fe.M)
-    st.H = _np(fe.mp_H[b]).reshape(-1, 14)
-    st.info = _np(fe.mp_info[b]).reshape(-1, 49)
-    st.uv = _np(fe.mp_uv[b]).reshape(-1, 2)
-    st.upd = _np(fe.mp_upd[b]).astype(np.int64)
-    return st
-
-
-def _same_state(fe, b, st):
-    assert np.array_equal(_np(fe.mp_upd[b]), st.upd)
-    assert np.array_equal(_np(fe.mp_info[b]).reshape(-1, 49), st.info)
-    assert np.array_equal(_np(fe.mp_H[b]).reshape(-1, 14), st.H)
-    assert np.array_equal(_np(fe.mp_uv[b]).reshape(-1, 2), st.uv)
-
-
-def _check_pose(fe, T0, kps, kp2mp_before, mps, Tg, outl_g, ninl_g):
-    idx = np.nonzero(kp2mp_before >= 0)[0]
-    To, oo, no, _ = O.pose_opt(T0, mps["pos"][kp2mp_before[idx]], np.c_[kps["x"][idx], kps["y"][idx]],
-                               kps["octave"][idx].astype(np.int32), fe.inv_sigma2, *fe.cam[2:])
-    assert ninl_g == no
-    assert np.array_equal(outl_g[idx], oo)
-    assert np.all(np.abs(Tg.reshape(4, 4).astype(np.float64) - To) <= 1e-5 * np.maximum(1, np.abs(To)))
-
-
-# config 2 (EuRoC 752x480, 1000 feats, GF budget 100, 2000-point map) and
-# config 3 (TUM 640x480, 2000 feats, GF budget 160, 3000-point map)
-@pytest.fixture(scope="module", params=[("euroc", 1000, 2000, 100), ("tum", 2000, 3000, 160)],
-                ids=["config2", "config3"])
-def fe(request):
-    from gf_orb_slam_amd.pipeline import FrontEnd
-
-    cam, nfeat, nmap, budget = request.param
-    fe = FrontEnd(cam, nfeat, B, nmap, gf_budget=budget, seed=3)
-    w, h = fe.cam[:2]
-    fe.load_frames(np.stack([synth.synth_frame(w, h, synth.frame_seed(40 + b, 0)) for b in range(B)]))
-    fe.build_maps()
-    return fe
-
-
-@pytest.mark.gpu
-def test_pipeline_stages_match_oracle(fe):
+def _setup(camera, nfeat, B, nmap, budget, gf=True, seed=3, n_scenes=2):
     import torch
 
-    fe.reset_state()
-    fe.step()  # warm: leaves next-frame stamps in the map
-    fe.sync()
-    fid = fe.frame_id
-    states = [_state(fe, b) for b in range(B)]
-    assert all((s.upd == fid).sum() > 100 for s in states)  # predicted-visible points carry the stamp
+    from gf_orb_slam_amd.pipeline import FrontEnd
 
-    s = fe.stream
-    with torch.cuda.stream(s):
-        fe.extract()
-        fe.predict_pose()
-        fe.reset_matches()
-        fe.match_last_frame()
-    fe.sync()
-    nk = _np(fe.nkp)
-    T_pred = _np(fe.Tcw)
-    mps = fe.mps.cpu().numpy().view(MAP_POINT_DTYPE).reshape(B, -1)
-    mdesc = _np(fe.mp_desc)
-    last_kp2mp, last_pos = _np(fe.last_kp2mp), _np(fe.last_pos)
-    kp2mp_m3, score_m3 = _np(fe.kp2mp), _np(fe.score)
-    kps = [_kp(fe.kps, b, nk[b]) for b in range(B)]
-    desc = [fe.desc[b, :nk[b]].cpu().numpy() for b in range(B)]
+    W = scene.Workload(camera, B, n_scenes=n_scenes, period=32, seed=seed)
+    frames = W.render_all("cuda").contiguous()
+    maps = W.build_maps(lambda im: O.extract(im, nfeatures=nfeat), nmap)
+    fe = FrontEnd(camera, nfeat, B, nmap, budget, gf=gf)
     for b in range(B):
-        # M3: SearchByProjection(CurrentFrame, LastFrame, 15), checkOri
-        k2 = np.full(nk[b], -1, np.int32)
-        sc = np.full(nk[b], 999, np.int32)
-        O.match_lastframe(fe.info, kps[b], desc[b], T_pred[b].reshape(4, 4), kps[b], desc[b],
-                          last_kp2mp[b, :nk[b]].copy(), np.zeros(nk[b], np.uint8), last_pos[b, :nk[b]], 15.0, 1,
-                          k2, sc)
-        assert np.array_equal(k2, kp2mp_m3[b, :nk[b]]) and np.array_equal(sc, score_m3[b, :nk[b]])
-        assert (k2 >= 0).sum() >= 20  # TrackWithMotionModel needs >= 20 (Tracking.cc:1541)
+        fe.set_map(b, *maps[W.scene_of[b]])
+        fe.set_rng(b, 1 + seed * 1000 + b)
+    fe.set_source(frames, W.scene_of, W.phase)
+    T, V = W.boot_state()
+    fe.bootstrap(T, V, 0.0)
+    torch.cuda.synchronize()
+    return W, frames.cpu().numpy(), maps, fe, T, V
 
-    with torch.cuda.stream(s):
-        fe.pose_optimization(0)
-    fe.sync()
-    T1, outl, ninl = _np(fe.Tcw), _np(fe.outl), _np(fe.ninl)
-    for b in range(B):
-        _check_pose(fe, T_pred[b], kps[b], kp2mp_m3[b, :nk[b]], mps[b], T1[b], outl[b, :nk[b]], ninl[b])
 
-    with torch.cuda.stream(s):
-        fe.discard_outliers()
-        fe.frame_info()
-        fe.frustum()
-        fe.map_info()
-    fe.sync()
-    kp2mp_d, score_d = _np(fe.kp2mp), _np(fe.score)
-    nmatch, ntm = _np(fe.nmatch), _np(fe.num_to_match)
-    Xv, base = _np(fe.Xv), _np(fe.base)
-    views = fe.views.cpu().numpy().view(MP_VIEW_DTYPE).reshape(B, -1)
-    updated = _np(fe.mp_updated)
-    for b in range(B):
-        k = kp2mp_m3[b, :nk[b]].copy()
-        k[outl[b, :nk[b]] == 1] = -1
-        assert np.array_equal(k, kp2mp_d[b, :nk[b]])
-        assert nmatch[b] == (k >= 0).sum() and ntm[b] == fe.budget - nmatch[b]
-        T = T1[b].reshape(4, 4)
-        xv = O.obs_update(0.0, np.eye(4, dtype=np.float32), 1.0 / fe.fps, C.twc_of(T))
-        np.testing.assert_allclose(Xv[b], xv, rtol=1e-12, atol=1e-12)
-        P, st = _prep(fe, mps[b]), states[b]
-        C.frame_info_stage(P, Xv[b], kps[b], k, np.zeros(nk[b], np.uint8), st)
-        acc = C.accumulate_stage(k, st, fid)
-        np.testing.assert_allclose(base[b], acc, rtol=1e-13, atol=1e-18)
-        assert np.abs(acc - np.eye(7).reshape(-1) * 1e-5).max() > 0  # stamped matches contribute
-        v, _ = O.frustum(fe.info, T, mps[b])
-        v["in_view"][k[k >= 0]] = 0
-        assert np.array_equal(v, views[b])
-        upd = C.map_info_stage(P, Xv[b], v, 0, st, fid)
-        assert np.array_equal(upd, updated[b])
-        _same_state(fe, b, st)
+def _img(W, frames, b, k):
+    return frames[W.scene_of[b], (W.phase[b] + k) % W.period]
 
-    fe.rng.copy_(fe.rng0)
-    with torch.cuda.stream(s):
-        fe.active_match()
-    fe.sync()
-    kp2mp_a, score_a, n_act = _np(fe.kp2mp), _np(fe.score), _np(fe.n_active)
-    for b in range(B):
-        k2 = kp2mp_d[b, :nk[b]].copy()
-        sc = score_d[b, :nk[b]].copy()
-        st = states[b]
-        nm, _ = O.active_match(fe.info, kps[b], desc[b], views[b], mdesc[b], updated[b], st.info, st.H, st.uv,
-                               base[b], fe.level_sigma2, int(ntm[b]), 1.0, 0.8, 1 + fe.seed * 1000 + b, k2, sc)
-        assert nm == n_act[b] and nm > 0
-        assert np.array_equal(k2, kp2mp_a[b, :nk[b]])
-        assert np.array_equal(sc, score_a[b, :nk[b]])
 
-    with torch.cuda.stream(s):
-        fe.pose_optimization(1)
-        fe.discard_outliers()
-        fe.predict_next()
-    fe.sync()
-    T2, outl2, ninl2 = _np(fe.Tcw), _np(fe.outl), _np(fe.ninl)
-    Xv2, Xn = _np(fe.Xv), _np(fe.Xv_next)
-    for b in range(B):
-        _check_pose(fe, T1[b], kps[b], kp2mp_a[b, :nk[b]], mps[b], T2[b], outl2[b, :nk[b]], ninl2[b])
-        assert np.abs(T2[b].reshape(4, 4) - np.eye(4)).max() < 2e-2  # map built from the identity camera
-        xv = O.obs_update(0.0, np.eye(4, dtype=np.float32), 1.0 / fe.fps, C.twc_of(T2[b].reshape(4, 4)))
-        np.testing.assert_allclose(Xv2[b], xv, rtol=1e-12, atol=1e-12)
-        xn = np.array(O.obs_predict(Xv2[b], 1.0 / fe.fps, 2)[1].Xv)
-        np.testing.assert_allclose(Xn[b], xn, rtol=1e-12, atol=1e-13)
-        st = states[b]
-        C.map_info_stage(_prep(fe, mps[b]), Xn[b], None, 1, st, fid + 1)
-        _same_state(fe, b, st)
+def _compare(dev, ch, b, name_prefix=""):
+    for k in EXACT:
+        a, o = dev[k][b], ch.read(k)
+        if k == "left":
+            continue
+        assert np.array_equal(a, o), f"{name_prefix}{k} differs (stream {b})"
+    nl = int(ch.stats()["nleft"])
+    assert np.array_equal(dev["left"][b][:nl], ch.read("left")[:nl]), f"{name_prefix}leftovers differ (stream {b})"
+    for k in POSE:
+        a, o = dev[k][b].astype(np.float64), ch.read(k).astype(np.float64)
+        assert np.all(np.abs(a - o) <= 1e-5 * np.maximum(1, np.abs(o))), f"{name_prefix}{k} differs (stream {b})"
+    for k in F64:
+        np.testing.assert_allclose(dev[k][b], ch.read(k), rtol=1e-9, atol=1e-12,
+                                   err_msg=f"{name_prefix}{k} (stream {b})")
+    sd = dev["stats"][:, b]
+    so = ch.read("stats")
+    assert np.array_equal(sd, so), f"{name_prefix}stage counters differ (stream {b}): {sd} vs {so}"
+
+
+CASES = {
+    # config 2: EuRoC 752x480, 1000 feats, GF budget 100, 2000-point local map
+    "config2": ("euroc", 1000, 4, 2000, 100, True),
+    # the same with a GF budget above the tracked count: runActiveMapMatching every frame
+    "config2_active": ("euroc", 1000, 4, 2000, 400, True),
+    # config 3: TUM 640x480, 2000 feats, GF budget 160, 3000-point local map
+    "config3": ("tum", 2000, 3, 3000, 160, True),
+    # ORB-SLAM baseline matching (GF off)
+    "baseline": ("euroc", 1000, 3, 2000, 100, False),
+}
 
 
 @pytest.mark.gpu
-def test_pipeline_step_repeatable(fe):
-    """A full step is deterministic given the RNG state and the map stamps."""
-    fe.reset_state()
-    fe.step()
-    fe.step()
-    fe.sync()
-    a = (_np(fe.Tcw), _np(fe.kp2mp), _np(fe.mp_info))
-    fe.reset_state()
-    fe.step()
-    fe.step()
-    fe.sync()
-    assert np.array_equal(a[0], _np(fe.Tcw)) and np.array_equal(a[1], _np(fe.kp2mp))
-    assert np.array_equal(a[2], _np(fe.mp_info))
+@pytest.mark.parametrize("case", list(CASES))
+def test_sequence_matches_oracle(case):
+    camera, nfeat, B, nmap, budget, gf = CASES[case]
+    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf)
+    free = []
+    for b in range(B):
+        ch = C.Chain(camera, nfeat, nmap, budget, gf)
+        ch.set_map(*maps[W.scene_of[b]])
+        ch.set_rng(1 + 3 * 1000 + b)
+        ch.bootstrap(_img(W, frames, b, 0), T[b], V[b])
+        free.append(ch)
+    dev = C.read_state(fe)
+    for b in range(B):
+        for k in ("last_kps", "last_kp2mp", "views", "Tcw_last", "last_pos"):
+            assert np.array_equal(dev[k][b], free[b].read(k)), f"bootstrap {k} (stream {b})"
+    branches = []
+    nsteps = 12
+    for k in range(1, nsteps + 1):
+        before = dev
+        fe.step()
+        dev = C.read_state(fe)
+        for b in range(B):
+            ch = C.Chain(camera, nfeat, nmap, budget, gf)
+            ch.load_from(before, b)
+            ch.step(_img(W, frames, b, k))
+            _compare(dev, ch, b, f"step {k}: ")
+            free[b].step(_img(W, frames, b, k))
+            _compare(dev, free[b], b, f"free-running step {k}: ")
+            branches.append(int(dev["stats"][3, b]))
+            assert dev["stats"][14, b] & 4 == 0, "track lost"
+    if case == "config2_active":
+        assert branches.count(3) >= len(branches) // 2
+    if case == "config2":
+        assert branches.count(1) >= len(branches) // 2  # the steady state: matches carried from the last frame
+    fe.close()
 
 
-def test_oracle_chain_tracks_pose():
-    """CPU chain sanity (also what bench.py times as cpu_baseline)."""
-    P = C.prepare("euroc", 1000, synth.synth_frame(752, 480, synth.frame_seed(77, 0)), 7)
-    r1 = C.step(P)
-    r2 = C.step(P)
-    for r in (r1, r2):
-        assert r["ninliers"] >= 80 and r["n_active"] > 0
-        assert np.abs(r["Tcw"] - np.eye(4)).max() < 2e-2
-    assert (P.state.upd == P.fid).sum() > 100
+@pytest.mark.gpu
+def test_bench_shape_parity():
+    """The timed configuration itself: 768 streams in 3 groups of 256 (as
+    bench.py runs them, each group on its own context / HIP stream, launches
+    interleaved), streams {0, 127, 255} of each group checked for 2 steps."""
+    import torch
+
+    from gf_orb_slam_amd.pipeline import FrontEnd
+
+    G, Bg = 3, 256
+    W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5)
+    frames = W.render_all("cuda").contiguous()
+    maps = W.build_maps(lambda im: O.extract(im), 2000)
+    T, V = W.boot_state()
+    fes = []
+    for g in range(G):
+        sl = slice(g * Bg, (g + 1) * Bg)
+        fe = FrontEnd("euroc", 1000, Bg, 2000, 100)
+        for b in range(Bg):
+            fe.set_map(b, *maps[W.scene_of[g * Bg + b]])
+            fe.set_rng(b, 1 + g * Bg + b)
+        fe.set_source(frames, W.scene_of[sl], W.phase[sl])
+        fe.bootstrap(T[sl], V[sl], 0.0)
+        fes.append(fe)
+    torch.cuda.synchronize()
+    fr = frames.cpu().numpy()
+    check = [0, 127, 255]
+    states = [C.read_state(fe, STATE) for fe in fes]
+    for k in (1, 2):
+        for fe in fes:
+            fe.step()
+        for g, fe in enumerate(fes):
+            dev = C.read_state(fe)
+            for b in check:
+                ch = C.Chain("euroc", 1000, 2000, 100)
+                ch.load_from(states[g], b)
+                ch.step(_img(W, fr, g * Bg + b, k))
+                _compare(dev, ch, b, f"group {g} step {k}: ")
+            states[g] = dev
+    for fe in fes:
+        fe.close()
+
+
+@pytest.mark.gpu
+def test_graph_replay_equals_eager():
+    """gf_frontend_capture: a replayed step equals an eager one."""
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, 2000, 100)
+    W2, _, _, fe2, _, _ = _setup("euroc", 1000, 4, 2000, 100)
+    fe2.step()
+    fe2.capture_graph()  # records the step without running it
+    fe.step()
+    for _ in range(4):
+        fe.step()
+        fe2.step()
+    a, b = C.read_state(fe), C.read_state(fe2)
+    for k in ("kp2mp", "Tcw", "mp_info", "rng", "views", "stats"):
+        assert np.array_equal(a[k], b[k]), k
+    fe.close()
+    fe2.close()
+
+
+@pytest.mark.gpu
+def test_step_host_equals_source():
+    """Frames handed over from host memory (PCIe copy in the step) track the same."""
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, 2, 2000, 100)
+    W2, _, _, fe2, _, _ = _setup("euroc", 1000, 2, 2000, 100)
+    for k in range(1, 4):
+        fe.step()
+        fe2.step_host(np.stack([_img(W, frames, b, k) for b in range(2)]))
+    a, b = C.read_state(fe), C.read_state(fe2)
+    for k in ("kp2mp", "Tcw", "mp_info", "rng"):
+        assert np.array_equal(a[k], b[k]), k
+    fe.close()
+    fe2.close()
+
+
+def test_oracle_chain_tracks_sequence():
+    """CPU chain on a CPU-rendered loop: tracking holds against ground truth
+    (also what bench.py times as cpu_baseline)."""
+    W = scene.Workload("euroc", 1, n_scenes=1, period=32, seed=2, tex_size=512)
+    fr = W.render_all("cpu").numpy()
+    maps = W.build_maps(lambda im: O.extract(im), 2000)
+    T, V = W.boot_state()
+    ch = C.Chain("euroc", 1000, 2000, 100)
+    ch.set_map(*maps[0])
+    ch.set_rng(1)
+    ch.bootstrap(_img(W, fr, 0, 0), T[0], V[0])
+    assert (ch.read("last_kp2mp") >= 0).sum() > 200
+    for k in range(1, 6):
+        ch.step(_img(W, fr, 0, k))
+        st = ch.stats()
+        assert st["inl2"] >= 50 and st["flags"] == 0
+        err = np.abs(ch.read("Tcw").reshape(4, 4) - W.gt_pose(0, k)).max()
+        assert err < 0.02, err
