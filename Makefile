@@ -28,13 +28,20 @@ build/%.cpp.o: $(CSRC)/%.cpp $(HDRS)
 	$(CXX) -O3 -fno-tree-vectorize -std=c++17 -fPIC -ffp-contract=off -Wall -c $< -o $@
 
 $(LIB): $(HIPOBJS) $(CPPOBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -L/opt/rocm/lib -lrccl -o $@
 
 $(ORCLIB): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h $(CSRC)/libm_sincosf.h include/gfslam/abi.h
-	$(CXX) $(ORCFLAGS) -shared $(ORCSRCS) -o $@
+	$(CXX) $(ORCFLAGS) -shared $(ORCSRCS) -o $@ -lpthread
+
+# timing copy of the oracle for bench.py's cpu_baseline: vectorisation on,
+# AVX2-class target (portable to the GPU node's host), same arithmetic order
+ORCFAST = oracle/liboracle_fast.so
+all: $(ORCFAST)
+$(ORCFAST): $(ORCSRCS) $(wildcard oracle/*.h) $(CSRC)/orb_pattern.h $(CSRC)/select.h $(CSRC)/libm_sincosf.h include/gfslam/abi.h
+	$(CXX) -O3 -march=x86-64-v3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -shared $(ORCSRCS) -o $@ -lpthread
 
 clean:
-	rm -rf build $(LIB) $(ORCLIB)
+	rm -rf build $(LIB) $(ORCLIB) $(ORCFAST)
 
 .PHONY: all clean
 

@@ -2,13 +2,21 @@
 """GF-ORB-SLAM front-end benchmark (BASELINE.json metric).
 
 Metric: front-end fps (extract + match + GF-select) @ 752x480 / 1000 feats,
-plus pose-opt ms/iter (config 2: EuRoC-geometry synthetic frames, GF budget
-100, one MI355X per rank). One step = one frame of each of B independent
-streams through the device-resident hot path (gf_orb_slam_amd.pipeline.
-FrontEnd: extract, motion-model matching, pose LM, GF active matching, pose
-LM); value = frames of all ranks / wall time. Multi-GPU: one process per GPU (torchrun), streams shard across ranks
-with no data-path collective ("weak" scaling); rank 0 broadcasts the shared
-vocabulary/map blob over RCCL once before timing.
+plus pose-opt ms/iter. Config 2 (EuRoC camera, 1000 feats, GF budget 100,
+2000-point local maps) on rendered sequences: one step = one frame of each
+of B independent tracked sequences through libgfslam's batched front end
+(gf_frontend_step: Tracking::GrabImage in the WORKING state — extraction,
+TrackWithMotionModel, TrackLocalMap with the GF branch, motion model,
+next-frame prediction, SearchAdditionalMatchesInFrame, hand-over to the last
+frame). Every stream carries its pose, velocity, matches, map stamps and
+std::rand() state from frame to frame. value = frames of all ranks / wall
+time, frames resident in HBM.
+
+Multi-GPU (config 5): one process per GPU. `--gpus N` launches N ranks itself
+(torch.distributed.run) when it is not already running under a launcher.
+Rank 0 builds the world (scenes, vocabulary, local maps) and broadcasts it
+over RCCL (gf_dist_*, xGMI); each rank then tracks its own sequences (its own
+phases of the loops), weak scaling, no per-frame communication.
 
 Prints ONE JSON line on rank 0.
 """
@@ -18,6 +26,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,7 +37,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # Algorithmic bytes per frame for the extraction kernels,
-# computed from the level sizes: P = sum of pyramid pixels.
+# from the level sizes: P = sum of pyramid pixels.
 LEVELS = {"euroc": [(752, 480), (627, 400), (522, 333), (435, 278), (363, 231), (302, 193), (252, 161), (210, 134)],
           "tum": [(640, 480), (533, 400), (444, 333), (370, 278), (309, 231), (257, 193), (214, 161), (179, 134)]}
 
@@ -37,49 +47,78 @@ def kernel_bytes(camera: str, nfeat: int) -> dict:
     P, P0, P7 = sum(px), px[0], px[-1]
     return {
         "k_resize": (P - P7) + (P - P0),  # read level l-1, write level l
-        "k_blur_fast": 3 * P,             # blur read + write every level, FAST reads every pixel once
+        "k_blur_fast": 3 * P,             # read every level, write blurred level + FAST score map
         "k_describe": 60 * nfeat,         # 32 B descriptor + 28 B keypoint out
         "extract_total": (P - P7) + (P - P0) + P + 2 * P + 60 * nfeat,
     }
 
 
-def _cpu_worker(args) -> tuple:
-    """One host core running the oracle chain on its own stream (no GPU)."""
-    camera, nfeat, stream, budget_s = args
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+# ------------------------------------------------------------- CPU baseline
+def _chain_worker(args) -> tuple:
+    """One host core tracking one sequence on the CPU oracle chain
+    (oracle/chain.cpp, timing build); no GPU."""
+    camera, nfeat, nmap, budget, fps, mp, desc, frames, T, V, seed, budget_s, lib = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_chain
+    os.environ["GF_ORACLE_LIB"] = lib
+    import oracle_chain as C
 
-    from gf_orb_slam_amd import synth
-
-    cam = synth.CAMERAS[camera]
-    preps = [oracle_chain.prepare(camera, nfeat, synth.synth_frame(cam[0], cam[1], synth.frame_seed(stream, i)),
-                                  1000 + 7 * stream + i) for i in range(2)]
-    n, times, t0 = 0, [], time.perf_counter()
+    ch = C.Chain(camera, nfeat, nmap, budget, fps=fps)
+    ch.set_map(mp, desc)
+    ch.set_rng(seed)
+    ch.bootstrap(frames[0], T, V)
+    times, stages = [], []
+    t0 = time.perf_counter()
+    k = 0
     while time.perf_counter() - t0 < budget_s:
+        k += 1
         t1 = time.perf_counter()
-        oracle_chain.step(preps[n % len(preps)])
+        ch.step(frames[k % len(frames)])
         times.append(time.perf_counter() - t1)
-        n += 1
-    return n, time.perf_counter() - t0, times
+        stages.append(ch.timings())
+    return k, time.perf_counter() - t0, times, np.array(stages)
 
 
-def cpu_baseline(camera: str, nfeat: int, budget_s: float = 12.0, workers: int = 16) -> dict:
-    """The oracle chain (CPU restatement) on a bounded sample of the same
-    workload, one full front-end step per frame (tests/oracle_chain.py):
-    (i) one core, one stream — the baseline value — with per-frame median and
-    p90; (ii) `workers` host cores, one independent stream per process
-    (throughput), as SURVEY.md §8(d) asks."""
-    import multiprocessing as mp
+def cpu_baseline(camera, nfeat, nmap, budget, fps, maps, W, frames_host, budget_s=12.0, workers=16) -> dict:
+    """The oracle chain (CPU restatement of the same step) on a bounded sample
+    of the same workload: (i) one core, one sequence — the baseline value —
+    with median / p90 per frame and per stage; (ii) `workers` host cores,
+    one independent sequence per process (throughput). Timing build of the
+    oracle: -O3 -march=x86-64-v3 with vectorisation (oracle/liboracle_fast.so;
+    the parity build is -fno-tree-vectorize), std::thread matrix building."""
+    import multiprocessing as mp_
     import platform
 
-    n, dt, times = _cpu_worker((camera, nfeat, 99, budget_s))
-    t = np.sort(np.asarray(times))
+    lib = os.path.join(ROOT, "oracle", "liboracle_fast.so")
+    if not os.path.exists(lib):
+        lib = os.path.join(ROOT, "oracle", "liboracle.so")
+
+    def job(b, secs):
+        s = W.scene_of[b]
+        seq = np.stack([frames_host[s][(W.phase[b] + k) % W.period] for k in range(W.period)])
+        T, V = W.boot_state()
+        return (camera, nfeat, nmap, budget, fps, maps[s][0], maps[s][1], seq, T[b], V[b], 1 + b, secs, lib)
+
+    n, dt, times, stages = _chain_worker(job(0, budget_s))
+    t = np.sort(np.asarray(times)) * 1e3
+    names = ["extract", "track_motion_model", "frame_info", "local_map_search", "pose_opt_2",
+             "predict_next", "additional_matches"]
+    st = np.asarray(stages) * 1e3
     out = {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-           "sample": f"{n} frames ({camera} {nfeat} feats, 2000-point local map, GF budget 100): extract + "
-                     f"motion model + SearchByProjection(last) + PoseOptimization + G1-G7 active matching + "
-                     f"PoseOptimization, 1 thread, {dt:.1f} s",
-           "ms_per_frame_median": round(float(np.median(t)) * 1e3, 2),
-           "ms_per_frame_p90": round(float(t[int(0.9 * (len(t) - 1))]) * 1e3, 2)}
+           "sample": f"{n} consecutive frames of one rendered {camera} sequence ({nfeat} feats, {nmap}-point local "
+                     f"map, GF budget {budget}), full tracking step per frame on the C++ oracle chain, "
+                     f"1 thread, {dt:.1f} s",
+           "build": os.path.basename(lib),
+           "ms_per_frame_median": round(float(np.median(t)), 2),
+           "ms_per_frame_p90": round(float(t[int(0.9 * (len(t) - 1))]), 2),
+           "stages_ms_median": {k: round(float(np.median(st[:, i])), 3) for i, k in enumerate(names)}}
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as fh:
@@ -87,40 +126,18 @@ def cpu_baseline(camera: str, nfeat: int, budget_s: float = 12.0, workers: int =
     except OSError:
         pass
     w = max(1, min(workers, os.cpu_count() or 1))
-    ctx = mp.get_context("spawn")  # fresh interpreters: the workers never touch the GPU
+    ctx = mp_.get_context("spawn")  # fresh interpreters: the workers never touch the GPU
     with ctx.Pool(w) as pool:
-        res = pool.map(_cpu_worker, [(camera, nfeat, 200 + i, budget_s * 0.75) for i in range(w)])
+        res = pool.map(_chain_worker, [job(1 + i, budget_s * 0.6) for i in range(w)])
     frames = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     out["all_cores"] = {"value": round(frames / wall, 2), "unit": "frames/s", "cores": w,
-                        "sample": f"{frames} frames, one stream per process, {wall:.1f} s"}
+                        "sample": f"{frames} frames, one sequence per process, {wall:.1f} s"}
     out["host"] = {"nproc": os.cpu_count(), "cpu_model": cpu_model or platform.processor()}
     return out
 
 
-def single_stream(camera: str, nfeat: int, budget: int, steps: int) -> dict:
-    """Per-frame latency of ONE sequence (B = 1) through the same device path."""
-    import torch
-
-    from gf_orb_slam_amd import synth
-    from gf_orb_slam_amd.pipeline import FrontEnd
-
-    w, h = synth.CAMERAS[camera][:2]
-    fe = FrontEnd(camera, nfeat, 1, 2000, gf_budget=budget, seed=99)
-    fe.load_frames(synth.synth_frame(w, h, synth.frame_seed(99, 0))[None])
-    fe.build_maps()
-    for _ in range(3):
-        fe.step()
-    fe.sync()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fe.step()
-    fe.sync()
-    dt = (time.perf_counter() - t0) / steps
-    return {"ms_per_frame": round(dt * 1e3, 3), "fps": round(1.0 / dt, 2), "steps": steps}
-
-
+# ------------------------------------------------------------- local BA leg
 def schur_flops(prob: dict) -> float:
     """Algorithmic flops of one Schur contraction (k_ba_gemm) for one LBA
     window: per map point with k edges to local (free) keyframes, the k(k+1)/2
@@ -197,41 +214,16 @@ def lba_leg(batch: int, repeats: int = 3, cpu: bool = True) -> dict:
     return out
 
 
-def share_startup_state(dist, device, world: int, rank: int, vocab_levels: int = 6):
-    """The one exchange step: rank 0 builds the ORB
-    vocabulary (ORBvoc-sized synthetic tree: k = 10, L = 6, 1.1 M nodes, 50 MB
-    packed) and broadcasts it to every rank — RCCL over xGMI on the GPU node,
-    gloo in the CPU tests. Returns (vocabulary dict, checksum); every rank must
-    hold the same checksum."""
-    import torch
+# ------------------------------------------------------------- main
+def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, device: int):
+    """Rank 0: the scenes of the loops and each scene's keyframe-built local
+    map (keyframes extracted with the product extractor on this GPU)."""
+    from gf_orb_slam_amd import ORBextractor, scene
 
-    from gf_orb_slam_amd import synth
-
-    size = torch.zeros(1, dtype=torch.int64, device=device)
-    if rank == 0:
-        blob_np = synth.pack_vocabulary(synth.synth_vocabulary_fast(seed=7, k=10, L=vocab_levels))
-        size[0] = blob_np.size
-    if world > 1:
-        dist.broadcast(size, src=0)
-    n = int(size.item())
-    blob = torch.empty(n, dtype=torch.uint8, device=device)
-    if rank == 0:
-        blob.copy_(torch.from_numpy(blob_np))
-    if world > 1:
-        dist.broadcast(blob, src=0)
-    host = blob.cpu().numpy()
-    ck = int(host[:: max(1, n // 65536)].astype(np.int64).sum() + n)
-    return synth.unpack_vocabulary(host), ck
-
-
-def max_over_ranks(dist, device, world: int, seconds: float) -> float:
-    """The timed region's wall time: max over ranks (bench contract)."""
-    import torch
-
-    t = torch.tensor([seconds], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    W0 = scene.Workload(cam, B, n_scenes=S, period=period, seed=0)
+    ex = ORBextractor(nfeat, 1.2, 8, 1, 20)
+    maps = W0.build_maps(lambda im: ex(im), nmap, device=f"cuda:{device}")
+    return W0.scenes, maps
 
 
 def main():
@@ -239,67 +231,106 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=768, help="independent streams per GPU")
+    ap.add_argument("--batch", type=int, default=768, help="independent sequences per GPU")
     ap.add_argument("--groups", type=int, default=3,
-                    help="stream groups per GPU, each on its own HIP stream (their kernels overlap)")
+                    help="stream groups per GPU, each a front end on its own HIP stream (their kernels overlap)")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
+    ap.add_argument("--map", type=int, default=2000, help="local-map points per sequence")
+    ap.add_argument("--scenes", type=int, default=8)
+    ap.add_argument("--period", type=int, default=32, help="frames per loop of the rendered trajectory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--lba-batch", type=int, default=64, help="local-BA windows solved together (0: skip)")
-    ap.add_argument("--single-stream-steps", type=int, default=20,
-                    help="also time one stream alone (per-frame latency of a single sequence)")
+    ap.add_argument("--single-stream-steps", type=int, default=40,
+                    help="also time one sequence alone (per-frame latency, HIP graph replay)")
+    ap.add_argument("--pcie-steps", type=int, default=5,
+                    help="also time one group with the frames handed over from host memory")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launch one process per GPU before anything touches the GPU
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from gf_orb_slam_amd import synth
-    from gf_orb_slam_amd.pipeline import FrontEnd
+    from gf_orb_slam_amd import scene, synth
+    from gf_orb_slam_amd.bow import ORBVocabulary
+    from gf_orb_slam_amd.dist import GfDist, checksum, share_world
+    from gf_orb_slam_amd.orb import Context
+    from gf_orb_slam_amd.pipeline import STATS, FrontEnd
 
     cam = args.camera
-    w, h = synth.CAMERAS[cam][:2]
-    B = args.batch
-    G = max(1, args.groups)
+    B, G = args.batch, max(1, args.groups)
     if B % G:
         raise SystemExit(f"--batch {B} must be a multiple of --groups {G}")
     Bg = B // G
-    # G groups of B/G streams, each a FrontEnd with its own context and HIP
-    # stream: their kernels overlap, so one group's latency-bound stages (pose
-    # LM, active matching) run beside another group's extraction
+    S = min(args.scenes, B)
+
+    # ---- start-up exchange (config 5): world, vocabulary, maps from rank 0 over RCCL
+    t_su = time.perf_counter()
+    ctx0 = Context(local)
+    gd = GfDist(ctx0, rank, world)
+    scenes, maps, world_ck, world_span, world_bytes = share_world(
+        gd, rank, lambda: build_world(cam, B, S, args.period, args.nfeatures, args.map, local))
+    voc = ORBVocabulary(synth.synth_vocabulary_fast(seed=7, k=10, L=6), ctx=ctx0) if rank == 0 else None
+    voc = gd.bcast_vocab(voc, 0)
+    voc_ck = voc.checksum()
+    voc_span = gd.gather_ints([voc_ck])
+    W = scene.Workload(cam, B, n_scenes=S, period=args.period, seed=0, scenes=scenes, phase_offset=3 * rank)
+    frames = W.render_all(f"cuda:{local}").contiguous()
+    T, V = W.boot_state()
     fes = []
+    map_cks = []
     for g in range(G):
-        fe = FrontEnd(cam, args.nfeatures, Bg, 2000, gf_budget=args.gf_budget, seed=rank * G + g)
-        base = rank * B + g * Bg
-        frames = np.stack([synth.synth_frame(w, h, synth.frame_seed(base + b, 0)) for b in range(min(Bg, 8))])
-        fe.load_frames(frames[np.arange(Bg) % len(frames)])
-        fe.build_maps()
+        sl = slice(g * Bg, (g + 1) * Bg)
+        fe = FrontEnd(cam, args.nfeatures, Bg, args.map, args.gf_budget, ctx=Context(local))
+        if rank == 0:
+            for b in range(Bg):
+                fe.set_map(b, *maps[W.scene_of[g * Bg + b]])
+        gd.bcast_map(fe, 0)  # every rank's streams get rank 0's local maps, device to device
+        map_cks.append(checksum(fe.read("map")) ^ checksum(fe.read("map_desc")))
+        for b in range(Bg):
+            fe.set_rng(b, 1 + rank * B + g * Bg + b)
+        fe.set_source(frames, W.scene_of[sl], W.phase[sl])
+        fe.bootstrap(T[sl], V[sl], 0.0)
         fes.append(fe)
-
-    # one-off exchange before timing: rank 0 broadcasts the ORB vocabulary (RCCL over xGMI)
-    t_bc = time.perf_counter()
-    voc_tree, voc_ck = share_startup_state(dist, "cuda", world, rank)
+    map_span = gd.gather_ints(map_cks)
     torch.cuda.synchronize()
-    t_bc = time.perf_counter() - t_bc
-    from gf_orb_slam_amd.bow import ORBVocabulary
-    vocab = ORBVocabulary(voc_tree)  # every rank holds it on its own device (D1 path)
-    startup = {"vocabulary_nodes": vocab.info()["nnodes"], "broadcast_MB": round(voc_tree["desc"].nbytes * 45 / 32 / 1e6, 1),
-               "broadcast_s": round(t_bc, 3), "checksum": voc_ck}
+    t_su = time.perf_counter() - t_su
+    startup = {"world_bytes": world_bytes, "vocabulary_nodes": voc.info()["nnodes"],
+               "checksums_equal_across_ranks": bool(np.all(world_span[0] == world_span[1]) and
+                                                    np.all(voc_span[0] == voc_span[1]) and
+                                                    np.all(map_span[0] == map_span[1])),
+               "world_checksum": world_ck, "vocabulary_checksum": voc_ck, "seconds": round(t_su, 2),
+               "transport": "RCCL (gf_dist_bcast / gf_dist_bcast_vocab / gf_dist_bcast_map)"}
 
+    # ---- warm-up (also the branch mix of the steady state)
+    hist = np.zeros(6, np.int64)
+    lost = 0
     for _ in range(args.warmup):
         for fe in fes:
             fe.step()
+        for fe in fes:
+            st = fe.read("stats")
+            hist += np.bincount(st[STATS.index("branch")], minlength=6)[:6]
+            lost += int((st[STATS.index("flags")] & 4 != 0).sum())
     for fe in fes:
         fe.sync()
-        # HIP events around every launch on its group's stream, over the timed region
-        fe.prof_enable(True)
+        fe.prof_enable(True)  # HIP events around every launch on its group's stream
         fe.prof_reset()
     torch.cuda.synchronize()
     if world > 1:
@@ -315,7 +346,10 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt = max_over_ranks(dist, "cuda", world, dt)
+    tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dt = float(tt.item())
     prof = {}
     for fe in fes:
         for k, (ms, cnt) in fe.prof_report().items():
@@ -323,59 +357,40 @@ def main():
             a[0] += ms
             a[1] += cnt
         fe.prof_enable(False)
-    prof_steps = args.steps
-    fe = fes[0]
+    stats = [fe.stats() for fe in fes]
+    final = {k: np.concatenate([s[k] for s in stats]) for k in STATS}
 
     frames_total = world * B * args.steps
     fps = frames_total / dt
-    nk = float(np.mean([f.nkp.float().mean().item() for f in fes]))
-    iters = np.concatenate([f.iters.cpu().numpy() for f in fes], axis=1).astype(np.float64)   # [2][B] LM iterations
-    nedges = np.concatenate([f.nedges.cpu().numpy() for f in fes], axis=1).astype(np.float64)  # [2][B] edges
-    n_active = float(np.mean([f.n_active.float().mean().item() for f in fes]))
-    ninl = float(np.mean([f.ninl.float().mean().item() for f in fes]))
-
-    # algorithmic bytes per launch for the kernels with a §8(d) formula
     kb = kernel_bytes(cam, args.nfeatures)
     per_launch_bytes = {k: kb[k] * Bg for k in ("k_resize", "k_blur_fast", "k_describe")}
-    # pose LM: N_e * 40 B per LM iteration per problem, summed over the launch
-    per_launch_bytes["k_pose_opt"] = float((nedges * iters).sum(axis=1).mean() * 40.0) / G
-    per_kernel = {k: {"avg_ms": v[0] / max(v[1], 1), "launches": v[1], "ms_per_step": v[0] / prof_steps}
-                  for k, v in prof.items()}
-    # the roofline is priced on the kernel with the largest total time that has
-    # an algorithmic byte count; a latency-bound stage that ranks above it
-    # (one wave per frame walking a sequential loop: active matching) is named
-    # beside it, since an HBM roofline says nothing about it
+    iters = np.stack([final["iter1"], final["iter2"]]).astype(np.float64)
+    nedges = np.stack([final["edges1"], final["edges2"]]).astype(np.float64)
+    per_launch_bytes["k_pose_opt"] = float((nedges * iters).sum() * 40.0) / (2 * G)
     top = max(prof, key=lambda k: prof[k][0])
     priced = [k for k in prof if k in per_launch_bytes]
     dom = max(priced, key=lambda k: prof[k][0]) if priced else top
     avg_s = prof[dom][0] / prof[dom][1] / 1e3
-    # HBM bytes per launch from the committed rocprofv3 PMC passes of this code
-    # (profiles/r01/pmc_traffic.json, scripts/pmc_extract.sh), when taken at this batch
     traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     try:
-        pmc = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01",
-                                          "pmc_traffic.json")))
+        pmc = json.load(open(pmc_path))
         if pmc.get("batch") == Bg and dom in pmc.get("kernels", {}):
             traffic = round(pmc["kernels"][dom]["traffic_bytes"])
     except (OSError, ValueError, KeyError):
         traffic = None
-    if dom in per_launch_bytes:
-        achieved = per_launch_bytes[dom] / avg_s / 1e9
-        roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
-                "frac": round(achieved / 8000.0, 5), "traffic": traffic,
-                "traffic_source": "profiles/r01/pmc_traffic.json (FETCH_SIZE+WRITE_SIZE per launch)" if traffic else None,
-                "algorithmic_bytes_per_launch": per_launch_bytes[dom], "frames_per_launch": Bg,
-                "avg_launch_ms": round(avg_s * 1e3, 4)}
-    else:
-        roof = {"kernel": dom, "bound": "hbm", "achieved": None, "peak": 8000.0, "unit": "GB/s", "frac": None,
-                "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4)}
+    achieved = per_launch_bytes[dom] / avg_s / 1e9
+    roof = {"kernel": dom, "bound": "hbm", "achieved": round(achieved, 2), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 5), "traffic": traffic,
+            "traffic_source": "profiles/r02/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE per launch)"
+            if traffic else None,
+            "algorithmic_bytes_per_launch": per_launch_bytes[dom], "frames_per_launch": Bg,
+            "avg_launch_ms": round(avg_s * 1e3, 4)}
     if top != dom:
-        roof["largest_kernel"] = {"kernel": top, "avg_launch_ms": round(prof[top][0] / prof[top][1], 4),
-                                  "bound": "latency: one wave per frame runs the reference's sequential "
-                                           "selection loop; its time stretches while it waits for CUs "
-                                           "beside the other groups' extraction"}
-    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe") if k in prof)
-    ext_bw = kb["extract_total"] * B * prof_steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
+        roof["largest_kernel"] = {"kernel": top, "avg_launch_ms": round(prof[top][0] / prof[top][1], 4)}
+    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
+                 if k in prof)
+    ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
     pose_ms = prof.get("k_pose_opt", (0.0, 1))
     pose_avg_ms = pose_ms[0] / max(pose_ms[1], 1)
     mean_iters = float(iters.mean())
@@ -392,36 +407,93 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/int32 (extract, match), f64 (GF, pose LM)",
-        "data": "synthetic (seeded 752x480 frames + synthetic 2000-point local maps; no dataset reachable)",
-        "config": {"workload": f"config 2: {cam} {w}x{h}, {args.nfeatures} feats, GF budget {args.gf_budget}, "
-                               f"{B} streams/GPU in {G} groups; step = extract + motion model + SearchByProjection(last frame) + "
-                               f"PoseOptimization + G1-G7 active map matching + PoseOptimization",
-                   "streams_per_gpu": B, "stream_groups": G, "parallelism": f"{B} streams x {world} ranks"},
+        "data": "synthetic: rendered sequences (textured-plane rooms, closed EuRoC-speed loops), keyframe-built "
+                "local maps; no dataset reachable",
+        "config": {"workload": f"config 2: {cam} {W.cam[0]}x{W.cam[1]}, {args.nfeatures} feats, GF budget "
+                               f"{args.gf_budget}, {args.map}-point local maps, {B} tracked sequences per GPU in {G} "
+                               f"groups; step = one frame of every sequence through Tracking::GrabImage (WORKING): "
+                               f"extract, motion model + SearchByProjection(last) + PoseOptimization, GF "
+                               f"SearchReferencePointsInFrustum branch, PoseOptimization, motion update, next-frame "
+                               f"MAP_INFO prediction, SearchAdditionalMatchesInFrame",
+                   "sequences_per_gpu": B, "stream_groups": G,
+                   "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
         "startup": startup,
         "roofline": roof,
         "pose_opt": {"ms_per_iter": round(pose_avg_ms / max(mean_iters, 1e-9), 5),
-                     "ms_per_iter_per_problem": round(pose_avg_ms / max(mean_iters * Bg, 1e-9), 6),
                      "avg_launch_ms": round(pose_avg_ms, 4), "mean_iterations": round(mean_iters, 2),
                      "mean_edges": [round(float(x), 1) for x in nedges.mean(axis=1)],
-                     "note": "ms_per_iter = launch time / mean LM iterations (all B problems run concurrently)"},
-        "extraction_stage": {"ms_per_frame": round(ext_ms / (B * prof_steps), 5),
+                     "note": f"ms_per_iter = launch time / mean LM iterations ({Bg} problems per launch run "
+                             f"concurrently)"},
+        "tracking": {"branch_mix_warmup": {"leftovers_only": int(hist[1]), "search_by_projection": int(hist[2]),
+                                           "active_matching": int(hist[3]), "nothing_in_view": int(hist[4])},
+                     "mean_inliers": round(float(final["inl2"].mean()), 1),
+                     "mean_last_frame_matches": round(float(final["m3"].mean()), 1),
+                     "mean_additional_matches": round(float(final["extra"].mean()), 1),
+                     "lost_frames_warmup": lost},
+        "extraction_stage": {"ms_per_frame": round(ext_ms / (B * args.steps), 5),
                              "algorithmic_GBps": round(ext_bw, 2) if ext_bw else None},
-        "kernels_note": f"HIP events per launch over the timed region; each launch covers one group ({Bg} streams) "
-                        f"and the {G} groups' launches overlap, so ms_per_step sums exceed the wall time per step",
-        "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
-                        "ms_per_step": round(v["ms_per_step"], 4)} for k, v in per_kernel.items()},
-        "avg_keypoints": nk,
-        "avg_active_matches": n_active,
-        "avg_inliers": ninl,
+        "kernels_note": f"HIP events per launch over the timed region; each launch covers one group ({Bg} sequences)"
+                        f" and the {G} groups' launches overlap, so ms_per_step sums exceed the wall time per step",
+        "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1],
+                        "ms_per_step": round(v[0] / args.steps, 4)} for k, v in prof.items()},
     }
+    for fe in fes:
+        fe.close()
     if rank == 0 and args.single_stream_steps > 0:
-        out["single_stream"] = single_stream(cam, args.nfeatures, args.gf_budget, args.single_stream_steps)
+        # one sequence alone: per-frame latency, the step replayed as one HIP graph
+        fe = FrontEnd(cam, args.nfeatures, 1, args.map, args.gf_budget, ctx=Context(local))
+        fe.set_map(0, *maps[W.scene_of[0]])
+        fe.set_rng(0, 1)
+        fe.set_source(frames, W.scene_of[:1], W.phase[:1])
+        fe.bootstrap(T[:1], V[:1], 0.0)
+        res = {}
+        for mode in ("eager", "graph"):
+            for _ in range(3):
+                fe.step()
+            if mode == "graph":
+                fe.capture_graph()
+            fe.sync()
+            t1 = time.perf_counter()
+            for _ in range(args.single_stream_steps):
+                fe.step()
+            fe.sync()
+            d = (time.perf_counter() - t1) / args.single_stream_steps
+            res[mode] = {"ms_per_frame": round(d * 1e3, 3), "fps": round(1.0 / d, 1)}
+        out["single_stream"] = {**res["graph"], "eager": res["eager"], "steps": args.single_stream_steps}
+        fe.close()
+    if rank == 0 and args.pcie_steps > 0:
+        # frames handed over from host memory: the PCIe copy inside the step (not `value`)
+        fe = FrontEnd(cam, args.nfeatures, Bg, args.map, args.gf_budget, ctx=Context(local))
+        for b in range(Bg):
+            fe.set_map(b, *maps[W.scene_of[b]])
+        fe.set_source(frames, W.scene_of[:Bg], W.phase[:Bg])
+        fe.bootstrap(T[:Bg], V[:Bg], 0.0)
+        fh = frames.cpu().numpy()
+        host = [np.stack([fh[W.scene_of[b], (W.phase[b] + k) % W.period] for b in range(Bg)])
+                for k in range(1, args.pcie_steps + 2)]
+        fe.step_host(host[0])
+        fe.sync()
+        t1 = time.perf_counter()
+        for k in range(args.pcie_steps):
+            fe.step_host(host[k + 1])
+        fe.sync()
+        d = (time.perf_counter() - t1) / args.pcie_steps
+        out["pcie_inclusive"] = {"frames_per_s": round(Bg / d, 1), "ms_per_step": round(d * 1e3, 3),
+                                 "sequences": Bg, "note": "one group, frames copied from pageable host memory "
+                                                          "in each step (hipMemcpyAsync), not the headline value"}
+        fe.close()
     if rank == 0 and args.lba_batch > 0:
         out["local_ba"] = lba_leg(args.lba_batch, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures)
+        out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures, args.map, args.gf_budget, 20.0, maps, W,
+                                           frames.cpu().numpy(), budget_s=args.cpu_seconds)
+        out["cpu_baseline"]["vs_gpu"] = {
+            "single_sequence_speedup": round(out.get("single_stream", {}).get("fps", 0) / out["cpu_baseline"]["value"],
+                                             1) if "single_stream" in out else None,
+            "aggregate_vs_all_cores": round(fps / world / out["cpu_baseline"]["all_cores"]["value"], 1)}
     if rank == 0:
         print(json.dumps(out), flush=True)
+    gd.close()
     if world > 1:
         dist.destroy_process_group()
 

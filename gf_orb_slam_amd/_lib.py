@@ -151,6 +151,15 @@ _PROTOS = {
     "gf_frontend_write": [_P, _I, _P, _S],
     "gf_frontend_field": [_P, _I, _P, _P],
     "gf_set_budgets": [_P, _D, _D],
+    "gf_dist_unique_id": [_P],
+    "gf_dist_init": [_P, _I, _I, _P, _P],
+    "gf_dist_destroy": [_P],
+    "gf_dist_info": [_P, _P, _P],
+    "gf_dist_bcast": [_P, _P, _S, _I],
+    "gf_dist_allreduce": [_P, _P, _S, _I],
+    "gf_dist_bcast_vocab": [_P, _P, _I],
+    "gf_dist_bcast_map": [_P, _P, _I],
+    "gf_vocab_download": [_P, _P, _P, _P, _P],
 }
 
 

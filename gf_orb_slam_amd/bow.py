@@ -75,6 +75,25 @@ class ORBVocabulary:
                               *[self._tree[k].ctypes.data for k in ("parent", "desc", "weight", "is_leaf")])
             check(lib().gf_vocab_create(self.ctx.handle, ctypes.byref(arr), ctypes.byref(self.handle)))
 
+    @classmethod
+    def from_handle(cls, handle, ctx):
+        """Wrap a device vocabulary created by the library (gf_dist_bcast_vocab)."""
+        v = cls.__new__(cls)
+        v.ctx, v.handle = ctx, handle
+        return v
+
+    def checksum(self) -> int:
+        """Sum over the device node arrays (descriptors, weights, word ids, CSR),
+        for comparing copies across ranks."""
+        n = self.info()["nnodes"]
+        d = np.zeros((n, 32), np.uint8)
+        w = np.zeros(n)
+        word = np.zeros(n, np.int32)
+        cs = np.zeros(n + 1, np.int32)
+        check(lib().gf_vocab_download(self.handle, ptr(d), ptr(w), ptr(word), ptr(cs)))
+        return int(d.astype(np.int64).sum() * 31 + word.astype(np.int64).sum() * 7 + cs.astype(np.int64).sum()
+                   + int(np.round(w.sum() * 1e6)))
+
     def info(self) -> dict:
         k, L, n, w = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib().gf_vocab_info(self.handle, ctypes.byref(k), ctypes.byref(L), ctypes.byref(n), ctypes.byref(w)))

@@ -22,6 +22,7 @@
 // for the context; ORBvoc-size trees (k = 10, L = 6: ~1.1 M nodes, ~45 MB)
 // stay in HBM, their top levels in L2.
 #include <climits>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -883,3 +884,74 @@ int gf_search_for_triangulation(gf_ctx* ctx, int check_ori, const gf_bow_side* a
 }
 
 }  // extern "C"
+
+// Vocabulary broadcast: rank `root` holds *voc; every other
+// rank receives the tree into a vocabulary of its own on the communicator's
+// device (*voc created here; pass *voc == NULL). Device to device: the
+// header first, then the node arrays in place.
+extern "C" int gf_dist_bcast_vocab(gf_dist* d, gf_vocab** voc, int root) {
+    GF_CHECK(d && voc, GF_ERR_ARG, "null arg");
+    gf_ctx* ctx = gf::dist_ctx(d);
+    const bool is_root = gf::dist_rank(d) == root;
+    GF_CHECK(!is_root || *voc, GF_ERR_ARG, "root has no vocabulary");
+    GF_HIP(hipSetDevice(ctx->device));
+    int32_t hdr[8] = {0};
+    if (is_root) {
+        gf_vocab* v = *voc;
+        int32_t h[8] = {v->k, v->L, v->scoring, v->weighting, v->nnodes, v->nwords, 0, 0};
+        memcpy(hdr, h, sizeof(h));
+    }
+    int32_t* dh = nullptr;
+    GF_HIP(hipMalloc(&dh, sizeof(hdr)));
+    hipError_t e = hipMemcpy(dh, hdr, sizeof(hdr), hipMemcpyHostToDevice);
+    int rc = e == hipSuccess ? gf::dist_bcast(d, dh, sizeof(hdr), root) : GF_ERR_HIP;
+    if (!rc) e = hipMemcpyAsync(hdr, dh, sizeof(hdr), hipMemcpyDeviceToHost, ctx->stream);
+    if (!rc && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(dh);
+    if (rc) return rc;
+    GF_HIP(e);
+    const int n = hdr[4];
+    GF_CHECK(n >= 1, GF_ERR_ARG, "empty vocabulary");
+    gf_vocab* v = *voc;
+    if (!is_root) {
+        v = new gf_vocab();
+        v->ctx = ctx;
+        v->k = hdr[0];
+        v->L = hdr[1];
+        v->scoring = hdr[2];
+        v->weighting = hdr[3];
+        v->nnodes = n;
+        v->nwords = hdr[5];
+        if ((e = hipMalloc((void**)&v->d_desc, 32 * (size_t)n)) ||
+            (e = hipMalloc((void**)&v->d_cstart, 4 * (size_t)(n + 1))) ||
+            (e = hipMalloc((void**)&v->d_child, 4 * (size_t)std::max(n - 1, 1))) ||
+            (e = hipMalloc((void**)&v->d_word, 4 * (size_t)n)) || (e = hipMalloc((void**)&v->d_weight, 8 * (size_t)n))) {
+            gf_vocab_destroy(v);
+            return gf::fail(GF_ERR_HIP, hipGetErrorString(e));
+        }
+    }
+    if ((rc = gf::dist_bcast(d, v->d_desc, 32 * (size_t)n, root)) ||
+        (rc = gf::dist_bcast(d, v->d_cstart, 4 * (size_t)(n + 1), root)) ||
+        (rc = gf::dist_bcast(d, v->d_child, 4 * (size_t)std::max(n - 1, 1), root)) ||
+        (rc = gf::dist_bcast(d, v->d_word, 4 * (size_t)n, root)) ||
+        (rc = gf::dist_bcast(d, v->d_weight, 8 * (size_t)n, root))) {
+        if (!is_root) gf_vocab_destroy(v);
+        return rc;
+    }
+    GF_HIP(hipStreamSynchronize(ctx->stream));
+    *voc = v;
+    return GF_OK;
+}
+
+// Host copy of a device vocabulary's node arrays (for checksums across ranks):
+// desc (nnodes x 32), weight (nnodes), word (nnodes), cstart (nnodes + 1).
+extern "C" int gf_vocab_download(gf_vocab* v, uint8_t* desc, double* weight, int32_t* word, int32_t* cstart) {
+    GF_CHECK(v, GF_ERR_ARG, "null vocabulary");
+    GF_HIP(hipSetDevice(v->ctx->device));
+    const size_t n = v->nnodes;
+    if (desc) GF_HIP(hipMemcpy(desc, v->d_desc, 32 * n, hipMemcpyDeviceToHost));
+    if (weight) GF_HIP(hipMemcpy(weight, v->d_weight, 8 * n, hipMemcpyDeviceToHost));
+    if (word) GF_HIP(hipMemcpy(word, v->d_word, 4 * n, hipMemcpyDeviceToHost));
+    if (cstart) GF_HIP(hipMemcpy(cstart, v->d_cstart, 4 * (n + 1), hipMemcpyDeviceToHost));
+    return GF_OK;
+}

@@ -56,6 +56,11 @@ int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out);
 // Host-family helper: copy host -> scratch slot (returns device pointer).
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out);
 
+// RCCL broadcast on the communicator's stream (dist.hip), asynchronous.
+int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);
+int dist_rank(gf_dist* d);
+gf_ctx* dist_ctx(gf_dist* d);
+
 // RAII bracket for one kernel launch when profiling is on.
 struct ProfScope {
     gf_ctx* ctx;

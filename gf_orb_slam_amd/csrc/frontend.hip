@@ -839,3 +839,29 @@ int gf_set_budgets(gf_ctx* ctx, double match_s, double select_s) {
 }
 
 }  // extern "C"
+
+// Map-state broadcast: every stream's local map (points,
+// descriptors, sizes) of rank `root`'s front end into the front ends of all
+// ranks (same batch and map capacity), device to device; the observability
+// state of the received streams starts fresh as after gf_frontend_set_map.
+extern "C" int gf_dist_bcast_map(gf_dist* d, gf_frontend* fe, int root) {
+    GF_CHECK(d && fe, GF_ERR_ARG, "null arg");
+    GF_CHECK(gf::dist_ctx(d)->device == fe->ctx->device, GF_ERR_ARG, "communicator and front end on different devices");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    int rc;
+    if ((rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_MAP], fe->field_bytes[GF_FE_MAP], root)) ||
+        (rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_MAP_DESC], fe->field_bytes[GF_FE_MAP_DESC], root)) ||
+        (rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_NMP], fe->field_bytes[GF_FE_NMP], root)) ||
+        (rc = gf::dist_bcast(d, fe->mp_pos, sizeof(float) * 3 * (size_t)fe->D.B * fe->D.M, root)))
+        return rc;
+    GF_HIP(hipStreamSynchronize(gf::dist_ctx(d)->stream));
+    if (gf::dist_rank(d) != root) {
+        const size_t n = (size_t)fe->D.B * fe->D.M;
+        std::vector<int32_t> neg(n, -1000);
+        GF_HIP(hipMemcpy(fe->D.upd, neg.data(), 4 * n, hipMemcpyHostToDevice));
+        GF_HIP(hipMemset(fe->D.views, 0, sizeof(gf_mp_view) * n));
+    }
+    return GF_OK;
+}
+

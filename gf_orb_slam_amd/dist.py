@@ -1,0 +1,166 @@
+"""The config-5 start-up exchange over gf_dist_* (RCCL
+over xGMI inside libgfslam), and the same protocol over a torch.distributed
+process group (gloo) for CPU tests of the packing and the checksums.
+
+Rank 0 builds the shared state — the rendered world (plane geometry and
+textures of every scene), the ORB vocabulary and each stream's local map —
+and broadcasts it; every rank then tracks its own sequences (its own phases
+of the loops) with no further communication until the final timing
+reduction. One process per GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import zlib
+
+import numpy as np
+
+from ._lib import check, lib
+
+
+def checksum(a: np.ndarray) -> int:
+    return zlib.crc32(np.ascontiguousarray(a).view(np.uint8).reshape(-1).tobytes()) & 0xFFFFFFFF
+
+
+class GfDist:
+    """An RCCL communicator of libgfslam (gf_dist_*) on one context's device.
+    The 128-byte unique id travels over the torch.distributed group `pg`."""
+
+    def __init__(self, ctx, rank: int, world: int, pg=None):
+        import torch
+        import torch.distributed as dist
+
+        self.ctx, self.rank, self.world = ctx, rank, world
+        uid = np.zeros(128, np.uint8)
+        if rank == 0:
+            check(lib().gf_dist_unique_id(uid.ctypes.data_as(ctypes.c_void_p)))
+        if world > 1:
+            t = torch.from_numpy(uid).to(f"cuda:{ctx.device}")
+            dist.broadcast(t, src=0, group=pg)
+            uid = t.cpu().numpy()
+        self.handle = ctypes.c_void_p()
+        check(lib().gf_dist_init(ctx.handle, rank, world, uid.ctypes.data_as(ctypes.c_void_p),
+                                 ctypes.byref(self.handle)))
+
+    def bcast_array(self, a: np.ndarray | None, root: int = 0) -> np.ndarray:
+        """Broadcast a host byte array through a device buffer (size first)."""
+        import torch
+
+        dev = f"cuda:{self.ctx.device}"
+        n = torch.zeros(1, dtype=torch.float64, device=dev)
+        if self.rank == root:
+            n[0] = float(a.nbytes)
+        check(lib().gf_dist_bcast(self.handle, ctypes.c_void_p(n.data_ptr()), 8, root))
+        nb = int(n.item())
+        buf = torch.empty(nb, dtype=torch.uint8, device=dev)
+        if self.rank == root:
+            buf.copy_(torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)))
+        check(lib().gf_dist_bcast(self.handle, ctypes.c_void_p(buf.data_ptr()), nb, root))
+        return buf.cpu().numpy()
+
+    def bcast_vocab(self, voc, root: int = 0):
+        from .bow import ORBVocabulary
+
+        h = voc.handle if self.rank == root else ctypes.c_void_p()
+        check(lib().gf_dist_bcast_vocab(self.handle, ctypes.byref(h), root))
+        return voc if self.rank == root else ORBVocabulary.from_handle(h, self.ctx)
+
+    def bcast_map(self, fe, root: int = 0) -> None:
+        check(lib().gf_dist_bcast_map(self.handle, fe.handle, root))
+
+    def gather_ints(self, vals) -> np.ndarray:
+        """Every rank's values (max / min all-reduce pair): rows [min, max]."""
+        import torch
+
+        v = np.asarray(vals, np.float64)
+        out = []
+        for op in (2, 1):
+            t = torch.from_numpy(v.copy()).to(f"cuda:{self.ctx.device}")
+            check(lib().gf_dist_allreduce(self.handle, ctypes.c_void_p(t.data_ptr()), len(v), op))
+            out.append(t.cpu().numpy())
+        return np.stack(out)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().gf_dist_destroy(self.handle)
+            self.handle = None
+
+
+class TorchComm:
+    """The same byte broadcast over a torch.distributed group (gloo on CPU)."""
+
+    def __init__(self, rank: int, world: int, pg=None):
+        self.rank, self.world, self.pg = rank, world, pg
+
+    def bcast_array(self, a: np.ndarray | None, root: int = 0) -> np.ndarray:
+        import torch
+        import torch.distributed as dist
+
+        n = torch.zeros(1, dtype=torch.int64)
+        if self.rank == root:
+            n[0] = a.nbytes
+        if self.world > 1:
+            dist.broadcast(n, src=root, group=self.pg)
+        buf = torch.zeros(int(n.item()), dtype=torch.uint8)
+        if self.rank == root:
+            buf.copy_(torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)))
+        if self.world > 1:
+            dist.broadcast(buf, src=root, group=self.pg)
+        return buf.numpy()
+
+    def gather_ints(self, vals) -> np.ndarray:
+        import torch
+        import torch.distributed as dist
+
+        v = torch.tensor(np.asarray(vals, np.float64))
+        lo, hi = v.clone(), v.clone()
+        if self.world > 1:
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.pg)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.pg)
+        return np.stack([lo.numpy(), hi.numpy()])
+
+
+# ------------------------------------------------------------- packing
+def pack_world(scenes, maps) -> np.ndarray:
+    """Scenes (Scene.pack) and per-scene local maps in one blob."""
+    from .matcher import MAP_POINT_DTYPE
+
+    parts = []
+    for sc, (mp, d) in zip(scenes, maps):
+        sb = sc.pack()
+        mb = np.ascontiguousarray(mp, MAP_POINT_DTYPE).view(np.uint8).reshape(-1)
+        db = np.ascontiguousarray(d, np.uint8).reshape(-1)
+        hdr = np.array([sb.nbytes, len(mp)], np.int64).view(np.uint8)
+        parts += [hdr, sb, mb, db]
+    return np.concatenate([np.array([len(scenes)], np.int64).view(np.uint8)] + parts)
+
+
+def unpack_world(blob: np.ndarray):
+    from .matcher import MAP_POINT_DTYPE
+    from .scene import Scene
+
+    S = int(blob[:8].view(np.int64)[0])
+    o = 8
+    scenes, maps = [], []
+    for _ in range(S):
+        sb, m = (int(x) for x in blob[o:o + 16].view(np.int64))
+        o += 16
+        scenes.append(Scene.unpack(blob[o:o + sb]))
+        o += sb
+        mp = blob[o:o + m * MAP_POINT_DTYPE.itemsize].copy().view(MAP_POINT_DTYPE)
+        o += m * MAP_POINT_DTYPE.itemsize
+        d = blob[o:o + 32 * m].copy().reshape(m, 32)
+        o += 32 * m
+        maps.append((mp, d))
+    return scenes, maps
+
+
+def share_world(comm, rank: int, build) -> tuple:
+    """Rank 0 calls build() -> (scenes, maps) and broadcasts them; returns
+    (scenes, maps, blob checksum, [min, max] of every rank's checksum)."""
+    blob = pack_world(*build()) if rank == 0 else None
+    got = comm.bcast_array(blob, 0)
+    ck = checksum(got)
+    span = comm.gather_ints([ck])
+    scenes, maps = unpack_world(got)
+    return scenes, maps, ck, span, got.nbytes

@@ -60,6 +60,25 @@ class Scene:
         self.textures = np.stack([synth.synth_frame(tex_size, tex_size, seed * 100 + k, n_shapes=nshape)
                                   for k in range(len(planes))])
 
+    # --------------------------------------------------------- transport
+    def pack(self) -> np.ndarray:
+        """One byte blob (plane geometry f64 + textures u8), for the start-up broadcast."""
+        geo = np.concatenate([self.o.ravel(), self.u.ravel(), self.v.ravel(), self.su, self.sv])
+        hdr = np.array([len(self.o), self.tex_size], np.int64)
+        return np.concatenate([hdr.view(np.uint8), geo.view(np.uint8), self.textures.reshape(-1)])
+
+    @classmethod
+    def unpack(cls, blob: np.ndarray) -> "Scene":
+        P, T = (int(x) for x in blob[:16].view(np.int64))
+        geo = blob[16:16 + 8 * 11 * P].view(np.float64)
+        sc = cls.__new__(cls)
+        sc.o, sc.u, sc.v = geo[:3 * P].reshape(P, 3), geo[3 * P:6 * P].reshape(P, 3), geo[6 * P:9 * P].reshape(P, 3)
+        sc.su, sc.sv = geo[9 * P:10 * P].copy(), geo[10 * P:11 * P].copy()
+        sc.n = np.cross(sc.u, sc.v)
+        sc.tex_size = T
+        sc.textures = blob[16 + 8 * 11 * P:].reshape(P, T, T).copy()
+        return sc
+
     # --------------------------------------------------------- geometry
     def intersect(self, C: np.ndarray, d: np.ndarray):
         """Nearest plane hit of rays C + lam d (d: [N, 3]), float64: returns
@@ -204,12 +223,12 @@ class Workload:
     """B streams over n_scenes rendered loops (see module docstring)."""
 
     def __init__(self, camera: str, batch: int, n_scenes: int = 8, period: int = 32, seed: int = 0,
-                 phase_stride: int = 5, tex_size: int = 1024):
+                 phase_stride: int = 5, tex_size: int = 1024, scenes: list | None = None, phase_offset: int = 0):
         self.cam = synth.CAMERAS[camera]
         self.B, self.S, self.period, self.seed = batch, min(n_scenes, batch), period, seed
-        self.scenes = [Scene(seed * 1000 + s, tex_size) for s in range(self.S)]
+        self.scenes = scenes if scenes is not None else [Scene(seed * 1000 + s, tex_size) for s in range(self.S)]
         self.scene_of = np.arange(batch) % self.S
-        self.phase = ((np.arange(batch) // self.S) * phase_stride + seed) % period
+        self.phase = ((np.arange(batch) // self.S) * phase_stride + seed + phase_offset) % period
         self.traj_seed = [seed * 1000 + s for s in range(self.S)]
 
     def render_all(self, device="cpu"):

@@ -821,6 +821,33 @@ int gf_frontend_field(gf_frontend* fe, int field, size_t* bytes, void** d_ptr);
  * clock from the start of the frame's step. */
 int gf_set_budgets(gf_ctx* ctx, double match_s, double select_s);
 
+/* ------------------------------------------------ multi-GPU start-up exchange
+ * Config 5: one process per GPU, sequences independent,
+ * and one exchange step before tracking: an RCCL communicator over xGMI and
+ * broadcasts from rank 0 of the shared state. The reference has no
+ * distributed layer (one process, main.cc:92-157); the vocabulary it loads
+ * once (main.cc:92-106, TemplatedVocabulary.h:1469-1536) and the map it
+ * tracks against are what every rank receives. The communicator uses the
+ * context's device and stream; calls are synchronous. */
+typedef struct gf_dist gf_dist;
+/* ncclGetUniqueId on one rank (128 bytes); the caller hands it to the others. */
+int gf_dist_unique_id(uint8_t* id);
+int gf_dist_init(gf_ctx* ctx, int rank, int world, const uint8_t* id, gf_dist** out);
+int gf_dist_destroy(gf_dist* d);
+int gf_dist_info(gf_dist* d, int* rank, int* world);
+/* Device buffer broadcast from root. */
+int gf_dist_bcast(gf_dist* d, void* d_buf, size_t bytes, int root);
+/* In-place all-reduce of n doubles: op 0 sum, 1 max, 2 min. */
+int gf_dist_allreduce(gf_dist* d, double* d_buf, size_t n, int op);
+/* The vocabulary of root into every rank (*voc == NULL on the others: a
+ * vocabulary is created on the communicator's device). */
+int gf_dist_bcast_vocab(gf_dist* d, gf_vocab** voc, int root);
+/* Every stream's local map (gf_frontend_set_map state) of root's front end
+ * into the same-shaped front ends of the other ranks. */
+int gf_dist_bcast_map(gf_dist* d, gf_frontend* fe, int root);
+/* Host copy of a device vocabulary's node arrays (any may be NULL). */
+int gf_vocab_download(gf_vocab* voc, uint8_t* desc, double* weight, int32_t* word, int32_t* cstart);
+
 #ifdef __cplusplus
 }
 #endif

@@ -12,8 +12,11 @@
 // layouts as the device front end (B = 1), so a test can copy a device
 // stream's state in, run one frame here and compare every field.
 // Parity mode only: the time budgets are infinite.
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "oracle_common.h"
@@ -115,6 +118,7 @@ struct orc_chain {
     std::vector<double> mp_H, mp_info;
     gf_rng rng{};
     int32_t stats[GF_FE_NSTAT] = {};
+    double tm[8] = {};  // stage seconds of the last step
 };
 
 namespace {
@@ -166,19 +170,34 @@ void field(orc_chain* c, int f, void** ptr, size_t* bytes) {
 // skip those stamped fid and (check_viz == 0) those not in view; stamp the
 // valid ones. Returns updated flags (updateAtFrameId == fid).
 void map_info(orc_chain* c, const double* Xv, int m, int check_viz, int fid, std::vector<uint8_t>* updated) {
-    for (int i = 0; i < m; i++) {
-        if (c->upd[i] == fid) continue;
-        if (!check_viz && !c->views[i].in_view) continue;
-        double H[14], info[49];
-        float uv[2];
-        uint8_t valid = 0;
-        orc_obs_build_info(&c->oc, Xv, c->map[i].pos, nullptr, 1, check_viz, H, info, uv, &valid);
-        if (!valid) continue;
-        std::memcpy(&c->mp_H[14 * (size_t)i], H, sizeof(H));
-        std::memcpy(&c->mp_info[49 * (size_t)i], info, sizeof(info));
-        c->mp_uv[2 * i] = uv[0];
-        c->mp_uv[2 * i + 1] = uv[1];
-        c->upd[i] = fid;
+    // runMatrixBuilding (Observability.cc:646-713): hardware_concurrency equal
+    // grains of the point list, one std::thread each (ORC_THREADS overrides)
+    auto grain = [&](int lo, int hi) {
+        for (int i = lo; i < hi; i++) {
+            if (c->upd[i] == fid) continue;
+            if (!check_viz && !c->views[i].in_view) continue;
+            double H[14], info[49];
+            float uv[2];
+            uint8_t valid = 0;
+            orc_obs_build_info(&c->oc, Xv, c->map[i].pos, nullptr, 1, check_viz, H, info, uv, &valid);
+            if (!valid) continue;
+            std::memcpy(&c->mp_H[14 * (size_t)i], H, sizeof(H));
+            std::memcpy(&c->mp_info[49 * (size_t)i], info, sizeof(info));
+            c->mp_uv[2 * i] = uv[0];
+            c->mp_uv[2 * i + 1] = uv[1];
+            c->upd[i] = fid;
+        }
+    };
+    int nt = (int)std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("ORC_THREADS")) nt = std::atoi(e);
+    nt = std::max(1, std::min(nt, m / 64));
+    if (nt <= 1) {
+        grain(0, m);
+    } else {
+        std::vector<std::thread> th;
+        const int step = (m + nt - 1) / nt;
+        for (int t = 0; t < nt; t++) th.emplace_back(grain, t * step, std::min(m, (t + 1) * step));
+        for (auto& x : th) x.join();
     }
     if (updated) {
         updated->assign(c->M, 0);
@@ -372,7 +391,19 @@ int orc_chain_bootstrap(orc_chain* c, const uint8_t* img, const float* Tcw, cons
     return GF_OK;
 }
 
+int orc_chain_timings(orc_chain* c, double* out) {
+    std::memcpy(out, c->tm, sizeof(c->tm));
+    return GF_OK;
+}
+
 int orc_chain_step(orc_chain* c, const uint8_t* img) {
+    using clk = std::chrono::steady_clock;
+    auto tprev = clk::now();
+    auto lap = [&](int k) {
+        auto t = clk::now();
+        c->tm[k] = std::chrono::duration<double>(t - tprev).count();
+        tprev = t;
+    };
     int32_t* st = c->stats;
     const int frames = st[GF_ST_FRAMES];
     std::memset(st, 0, sizeof(c->stats));
@@ -385,6 +416,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     std::fill(c->outl.begin(), c->outl.end(), 0);
     int rc = extract(c, img);
     if (rc) return rc;
+    lap(0);
     const int n = c->nkp;
     int nm = 0;
     orc_match_lastframe(&c->fi, c->kps.data(), c->desc.data(), n, c->Tcw, c->last_kps.data(), c->last_desc.data(),
@@ -405,6 +437,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     st[GF_ST_FOUND] = found;
     const int ntm = c->p.gf_budget - found;
     st[GF_ST_TO_MATCH] = ntm;
+    lap(1);
     // TrackLocalMap -> SearchReferencePointsInFrustum (Tracking.cc:3149-3410)
     const bool gf = c->p.gf != 0;
     float Twc[16];
@@ -428,6 +461,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
             for (int e = 0; e < 49; e++) c->base[e] = c->base[e] + c->mp_info[49 * (size_t)mp + e];
         }
     }
+    lap(2);
     for (int i = 0; i < n; i++)  // mbTrackInView = false for matched points (:3205)
         if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
     int branch = 0, nlist = 0;
@@ -469,7 +503,9 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
         }
     }
     st[GF_ST_BRANCH] = branch;
+    lap(3);
     pose(c, &st[GF_ST_INL2], &st[GF_ST_ITER2], &st[GF_ST_EDGES2]);  // outliers kept (:2776)
+    lap(4);
     // motion model (:729-738)
     float LastTwc[16];
     twc_of(c->Tcw_last, LastTwc);
@@ -485,6 +521,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
         orc_obs_predict(c->Xv, c->t_cur - c->t_prev, 2, kin);
         std::memcpy(c->Xv_next, kin[1].Xv, sizeof(c->Xv_next));
         map_info(c, c->Xv_next, c->nmp, 1, 2, nullptr);
+        lap(5);
         // SearchAdditionalMatchesInFrame (:3097-3145)
         if (viz) frustum_list(c, list.data(), nlist);
         st[GF_ST_EXTRA] = project_list(c, list.data(), nlist, 0.8f);
@@ -500,6 +537,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     if (st[GF_ST_INL2] < 15) fl |= 4;
     st[GF_ST_FLAGS] = fl;
     st[GF_ST_FRAMES] = frames + 1;
+    lap(6);
     return GF_OK;
 }
 

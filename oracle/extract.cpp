@@ -3,6 +3,7 @@
 // OpenCV 3.4 internals it calls (FAST, KeyPointsFilter::retainBest, resize,
 // GaussianBlur, fastAtan2) as documented in DESIGN.md "Oracle assumptions".
 #include <algorithm>
+#include <climits>
 #include <cfloat>
 #include <cstring>
 #include <vector>
@@ -104,9 +105,15 @@ static Image resize_linear(const Image& src, int dw, int dh) {
                 out[dx] = S[sx] * ONE;
         }
     };
+    int c0 = INT_MIN, c1 = INT_MIN;  // source rows held in r0 / r1
     for (int dy = 0; dy < dh; dy++) {
-        hrow(yofs[dy], r0);
-        hrow(yofs[dy] + 1, r1);
+        const int s0 = std::min(std::max(yofs[dy], 0), src.h - 1), s1 = std::min(std::max(yofs[dy] + 1, 0), src.h - 1);
+        if (s0 == c1) {
+            std::swap(r0, r1);
+            std::swap(c0, c1);
+        }
+        if (s0 != c0) hrow(s0, r0), c0 = s0;
+        if (s1 != c1) hrow(s1, r1), c1 = s1;
         int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
         uint8_t* D = &dst.px[(size_t)dy * dw];
         for (int dx = 0; dx < dw; dx++) {
@@ -140,20 +147,35 @@ static Image gaussian_blur(const Image& src) {
     int k[7];
     gauss_kernel7(k);
     Image dst = src;
-    std::vector<int> rows((size_t)src.w * src.h);
-    for (int y = 0; y < src.h; y++)
-        for (int x = 0; x < src.w; x++) {
+    const int w = src.w, h = src.h;
+    std::vector<int> rows((size_t)w * h);
+    for (int y = 0; y < h; y++) {
+        const uint8_t* S = &src.px[(size_t)y * w];
+        int* R = &rows[(size_t)y * w];
+        for (int x = 0; x < w; x++) {
+            if (x == 3 && w > 6) {  // interior: no border arithmetic
+                const int k0 = k[0], k1 = k[1], k2 = k[2], k3 = k[3], k4 = k[4], k5 = k[5], k6 = k[6];
+                for (; x + 3 < w; x++)
+                    R[x] = k0 * S[x - 3] + k1 * S[x - 2] + k2 * S[x - 1] + k3 * S[x] + k4 * S[x + 1] + k5 * S[x + 2] +
+                           k6 * S[x + 3];
+                if (x >= w) break;
+            }
             int s = 0;
-            for (int i = 0; i < 7; i++) s += k[i] * src.at(reflect101(x + i - 3, src.w), y);
-            rows[(size_t)y * src.w + x] = s;
+            for (int i = 0; i < 7; i++) s += k[i] * S[reflect101(x + i - 3, w)];
+            R[x] = s;
         }
-    for (int y = 0; y < src.h; y++)
-        for (int x = 0; x < src.w; x++) {
+    }
+    for (int y = 0; y < h; y++) {
+        const int* r[7];
+        for (int i = 0; i < 7; i++) r[i] = &rows[(size_t)reflect101(y + i - 3, h) * w];
+        uint8_t* D = &dst.px[(size_t)y * w];
+        for (int x = 0; x < w; x++) {
             int s = 0;
-            for (int i = 0; i < 7; i++) s += k[i] * rows[(size_t)reflect101(y + i - 3, src.h) * src.w + x];
+            for (int i = 0; i < 7; i++) s += k[i] * r[i][x];
             int v = (s + (1 << 15)) >> 16;
-            dst.px[(size_t)y * src.w + x] = (uint8_t)std::min(std::max(v, 0), 255);
+            D[x] = (uint8_t)std::min(std::max(v, 0), 255);
         }
+    }
     return dst;
 }
 
@@ -219,14 +241,52 @@ bool fast_is_corner(const Image& im, int x, int y, int th) {
 static void fast_roi(const Image& im, int x0, int y0, int w, int h, int th, std::vector<KP>& out) {
     out.clear();
     if (w < 7 || h < 7) return;
-    std::vector<int> score((size_t)w * h, 0);
-    std::vector<char> corner((size_t)w * h, 0);
-    for (int i = 3; i < h - 3; i++)
-        for (int j = 3; j < w - 3; j++)
-            if (fast_is_corner(im, x0 + j, y0 + i, th)) {
+    thread_local std::vector<int> score;
+    thread_local std::vector<char> corner;
+    score.assign((size_t)w * h, 0);
+    corner.assign((size_t)w * h, 0);
+    // OpenCV FAST_t's exact pre-test (threshold_tab, opposite pairs of the
+    // circle): a pixel whose pairs cannot hold a 9-arc is not a corner; the
+    // others get the full segment test.
+    int off[16];
+    for (int k = 0; k < 16; k++) off[k] = kCircle[k][1] * im.w + kCircle[k][0];
+    uint8_t tab[512];
+    for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -th ? 1 : i > th ? 2 : 0);
+    for (int i = 3; i < h - 3; i++) {
+        const uint8_t* row = &im.px[(size_t)(y0 + i) * im.w + x0];
+        for (int j = 3; j < w - 3; j++) {
+            const uint8_t* p = row + j;
+            const uint8_t* tb = tab + 255 - p[0];
+            int d = tb[p[off[0]]] | tb[p[off[8]]];
+            if (!d) continue;
+            d &= tb[p[off[2]]] | tb[p[off[10]]];
+            d &= tb[p[off[4]]] | tb[p[off[12]]];
+            d &= tb[p[off[6]]] | tb[p[off[14]]];
+            if (!d) continue;
+            d &= tb[p[off[1]]] | tb[p[off[9]]];
+            d &= tb[p[off[3]]] | tb[p[off[11]]];
+            d &= tb[p[off[5]]] | tb[p[off[13]]];
+            d &= tb[p[off[7]]] | tb[p[off[15]]];
+            if (!d) continue;
+            // the segment test (fast_is_corner) on the circle through offsets
+            const int v = p[0], lo = v - th, hi = v + th;
+            int cnt_d = 0, cnt_b = 0;
+            bool is_corner = false;
+            for (int k = 0; k < 25; k++) {
+                const int q = p[off[k & 15]];
+                cnt_d = q < lo ? cnt_d + 1 : 0;
+                cnt_b = q > hi ? cnt_b + 1 : 0;
+                if (cnt_d > 8 || cnt_b > 8) {
+                    is_corner = true;
+                    break;
+                }
+            }
+            if (is_corner) {
                 corner[(size_t)i * w + j] = 1;
                 score[(size_t)i * w + j] = (uint8_t)fast_corner_score(im, x0 + j, y0 + i, th);
             }
+        }
+    }
     // Row-major scan = the order FAST_t pushes keypoints (row i-1 emitted while
     // row i is scanned); neighbours outside the detection window score 0.
     for (int i = 3; i < h - 3; i++)

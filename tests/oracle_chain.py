@@ -30,6 +30,7 @@ def _orc():
         o.orc_chain_set_rng.argtypes = [_P, ctypes.c_uint32]
         o.orc_chain_bootstrap.argtypes = [_P, _P, _P, _P, ctypes.c_double]
         o.orc_chain_step.argtypes = [_P, _P]
+        o.orc_chain_timings.argtypes = [_P, _P]
         o._chain_declared = True
     return o
 
@@ -82,6 +83,14 @@ class Chain:
         fid, dt, shape = field_shape(name, 1, self.cap, self.M)
         a = np.ascontiguousarray(np.asarray(arr, dt).reshape(shape))
         assert _orc().orc_chain_write(self.h, fid, _p(a), a.nbytes) == 0, name
+
+    def timings(self) -> np.ndarray:
+        """Seconds of the last step's stages: extract, motion-model tracking,
+        frame info, local-map search, second PoseOptimization, next-frame
+        prediction, additional matches."""
+        t = np.zeros(8)
+        _orc().orc_chain_timings(self.h, _p(t))
+        return t[:7]
 
     def stats(self) -> dict:
         s = self.read("stats")

@@ -19,7 +19,7 @@ _orc = None
 def orc() -> ctypes.CDLL:
     global _orc
     if _orc is None:
-        _orc = ctypes.CDLL(ORACLE_PATH)
+        _orc = ctypes.CDLL(os.environ.get("GF_ORACLE_LIB", ORACLE_PATH))
         _orc.orc_fast_atan2.restype = ctypes.c_float
         _orc.orc_fast_atan2.argtypes = [ctypes.c_float, ctypes.c_float]
     return _orc
