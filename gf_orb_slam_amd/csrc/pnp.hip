@@ -535,6 +535,15 @@ __device__ __forceinline__ bool is_inlier(const float* p3d, const float* p2d, fl
     return error2 < max_err;
 }
 
+// A state from device memory is clamped to what the kernels can hold: the
+// minimal set to [1, kMaxSet] (private arrays), n to the problem capacity.
+__device__ __forceinline__ gf_pnp_state load_state(const gf_pnp_state* states, int b, int cap) {
+    gf_pnp_state st = states[b];
+    st.min_set = min(max(st.min_set, 1), kMaxSet);
+    st.n = min(max(st.n, 0), cap);
+    return st;
+}
+
 __device__ __forceinline__ int loop_count(const gf_pnp_state& st, int n_iterations) {
     if (st.n < st.min_inliers) return 0;
     const int a = st.max_iterations - st.iterations;
@@ -548,10 +557,10 @@ __device__ __forceinline__ int random_int(int32_t* s, int32_t* f, int32_t* r, in
 }
 
 __global__ void k_pnp_draw(int nprob, const gf_pnp_state* __restrict__ states, const gf_rng* __restrict__ rngs,
-                           int n_iterations, int lcap, int32_t* __restrict__ draws) {
+                           int n_iterations, int lcap, int32_t* __restrict__ draws, int cap) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nprob) return;
-    const gf_pnp_state st = states[b];
+    const gf_pnp_state st = load_state(states, b, cap);
     const int L = min(loop_count(st, n_iterations), lcap);
     int32_t s[31];
     for (int i = 0; i < 31; i++) s[i] = rngs[b].state[i];
@@ -592,7 +601,7 @@ __global__ void __launch_bounds__(64) k_pnp_hyp(const float* __restrict__ p3d, c
                                                 const int32_t* __restrict__ draws, double* __restrict__ hyp_rt,
                                                 int32_t* __restrict__ hyp_cnt) {
     const int b = blockIdx.y, h = blockIdx.x * blockDim.x + threadIdx.x;
-    const gf_pnp_state st = states[b];
+    const gf_pnp_state st = load_state(states, b, cap);
     if (h >= min(loop_count(st, n_iterations), lcap)) return;
     const float* P3 = p3d + (size_t)b * cap * 3;
     const float* P2 = p2d + (size_t)b * cap * 2;
@@ -664,7 +673,7 @@ __global__ void __launch_bounds__(256) k_pnp_scan(const float* __restrict__ p3d,
     __shared__ double sRt[12];
     __shared__ gf_pnp_state sst;
     const int b = blockIdx.x;
-    if (threadIdx.x == 0) sst = states[b];
+    if (threadIdx.x == 0) sst = load_state(states, b, cap);
     __syncthreads();
     gf_pnp_state st = sst;  // every wave works from the call's starting state
     const int n = st.n;
@@ -674,6 +683,7 @@ __global__ void __launch_bounds__(256) k_pnp_scan(const float* __restrict__ p3d,
     uint8_t* bm = best_mask + (size_t)b * cap;
     uint8_t* out_mask = inliers + (size_t)b * cap;
     const int L = min(loop_count(st, n_iterations), lcap);
+    const bool truncated = loop_count(st, n_iterations) > lcap;  // max_iterations below the state's loop
     int ran = 0, fl = 0, ninl = 0;
     bool refine_pending = true;  // Refine() of the current best set not yet evaluated in this call
     float T[16];
@@ -749,7 +759,7 @@ __global__ void __launch_bounds__(256) k_pnp_scan(const float* __restrict__ p3d,
     if (threadIdx.x == 0) {
         for (int i = 0; i < 16; i++) Tcw_out[(size_t)b * 16 + i] = (fl & GF_PNP_FOUND) ? T[i] : 0.f;
         ninliers[b] = ninl;
-        flags[b] = fl;
+        flags[b] = truncated ? (fl | GF_PNP_TRUNCATED) : fl;
         states[b] = st;
         gf_rng g = rngs[b];
         for (int i = 0; i < ran * st.min_set; i++) (void)gfrng::next(g.state, &g.f, &g.r);
@@ -800,15 +810,16 @@ int gf_pnp_iterate_dev(gf_ctx* ctx, int nprob, const float* d_p3d, const float* 
     hipStream_t s = (hipStream_t)stream;
     void *draws, *rt, *cnt, *work;
     int rc;
-    if ((rc = gf::ws_get(ctx, 10, sizeof(int32_t) * kMaxSet * (size_t)lcap * nprob, &draws)) ||
-        (rc = gf::ws_get(ctx, 11, sizeof(double) * 12 * (size_t)lcap * nprob, &rt)) ||
-        (rc = gf::ws_get(ctx, 12, sizeof(int32_t) * (size_t)lcap * nprob, &cnt)) ||
-        (rc = gf::ws_get(ctx, 13, sizeof(double) * kWork * (size_t)cap * nprob, &work)))
+    // device-family scratch slots of their own (45-48): the host wrappers own 0-16
+    if ((rc = gf::ws_get(ctx, 45, sizeof(int32_t) * kMaxSet * (size_t)lcap * nprob, &draws)) ||
+        (rc = gf::ws_get(ctx, 46, sizeof(double) * 12 * (size_t)lcap * nprob, &rt)) ||
+        (rc = gf::ws_get(ctx, 47, sizeof(int32_t) * (size_t)lcap * nprob, &cnt)) ||
+        (rc = gf::ws_get(ctx, 48, sizeof(double) * kWork * (size_t)cap * nprob, &work)))
         return rc;
     const Cam cam{(double)K[0], (double)K[1], (double)K[2], (double)K[3]};
     {
         GF_PROF(ctx, s, "k_pnp_draw");
-        k_pnp_draw<<<(nprob + 63) / 64, 64, 0, s>>>(nprob, d_state, d_rng, n_iterations, lcap, (int32_t*)draws);
+        k_pnp_draw<<<(nprob + 63) / 64, 64, 0, s>>>(nprob, d_state, d_rng, n_iterations, lcap, (int32_t*)draws, cap);
         GF_HIP(hipGetLastError());
     }
     {

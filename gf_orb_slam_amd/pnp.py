@@ -72,9 +72,15 @@ class PnPsolver:
 
     def set_ransac_parameters(self, probability=0.99, min_inliers=8, max_iterations=300, min_set=4, epsilon=0.4,
                               th2=5.991):
+        # SetRansacParameters (PnPsolver.cc:93-129) leaves mnIterations,
+        # mnBestInliers and the best pose as they are: keep them across a re-call
+        old = getattr(self, "state", None)
         self.state = np.zeros(1, PNP_STATE_DTYPE)
         prm = pnp_params(probability, min_inliers, max_iterations, min_set, epsilon, th2)
         check(lib().gf_pnp_init(self.N, ptr(prm), ptr(self.state)))
+        if old is not None:
+            for k in ("iterations", "best_inliers", "best_Tcw"):
+                self.state[k] = old[k]
 
     def iterate(self, n_iterations: int, rng: Rand):
         T = np.zeros(16, np.float32)

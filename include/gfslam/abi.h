@@ -621,7 +621,7 @@ typedef struct gf_pnp_params { /* SetRansacParameters arguments (:93) */
     double probability;
     int32_t min_inliers;
     int32_t max_iterations;
-    int32_t min_set; /* 4..8 */
+    int32_t min_set; /* 1..8 (the reference uses 4) */
     float epsilon;
     float th2;
 } gf_pnp_params;
@@ -639,13 +639,14 @@ typedef struct gf_pnp_state { /* one solver across iterate() calls */
 #define GF_PNP_FOUND 1   /* iterate returned a pose (refined or best)      */
 #define GF_PNP_NOMORE 2  /* bNoMore                                        */
 #define GF_PNP_REFINED 4 /* the pose came from Refine() (:198-208)         */
+#define GF_PNP_TRUNCATED 8 /* device path: max_iterations cut the state's loop short */
 /* PnPsolver::SetRansacParameters (host scalar set-up; resets the iteration
  * count and the best hypothesis as a fresh solver has them). */
 int gf_pnp_init(int n, const gf_pnp_params* params, gf_pnp_state* state);
 /* PnPsolver::iterate(nIterations, bNoMore, vbInliers, nInliers) (:137-230)
  * for one solver; rng is the process-wide std::rand() state the minimal sets
- * are drawn from (DUtils::Random::RandomInt, :165), advanced by 4 draws per
- * iteration run. best_mask (n bytes, mvbBestInliers) persists across calls
+ * are drawn from (DUtils::Random::RandomInt, :165), advanced by min_set draws
+ * per iteration run. best_mask (n bytes, mvbBestInliers) persists across calls
  * with the state. Outputs: Tcw (row-major, valid when flags & FOUND), inliers
  * (n bytes), ninliers, flags. */
 int gf_pnp_iterate(gf_ctx* ctx, const float* p3d, const float* p2d, const float* sigma2, const float K[4],
@@ -655,7 +656,8 @@ int gf_pnp_iterate(gf_ctx* ctx, const float* p3d, const float* p2d, const float*
  * [b][cap] of d_p3d/d_p2d/d_sigma2/d_best_mask/d_inliers, its size in
  * d_state[b].n; each problem draws from its own d_rng[b]. d_Tcw is [nprob][16].
  * max_iterations bounds every problem's loop count (the params value it was
- * initialised with). */
+ * initialised with); a problem whose loop it cuts short gets GF_PNP_TRUNCATED.
+ * States are clamped on the device (min_set to 1..8, n to cap). */
 int gf_pnp_iterate_dev(gf_ctx* ctx, int nprob, const float* d_p3d, const float* d_p2d, const float* d_sigma2,
                        int cap, const float K[4], gf_pnp_state* d_state, uint8_t* d_best_mask, int n_iterations,
                        int max_iterations, gf_rng* d_rng, float* d_Tcw, uint8_t* d_inliers, int32_t* d_ninliers,
