@@ -623,7 +623,6 @@ int gf_frontend_destroy(gf_frontend* fe) {
     if (!fe) return GF_OK;
     (void)hipSetDevice(fe->ctx->device);
     (void)hipStreamSynchronize(fe->ctx->stream);
-    if (fe->staging) (void)hipHostUnregister(fe->staging);
     fe_free(fe);
     delete fe;
     return GF_OK;
