@@ -160,6 +160,7 @@ _PROTOS = {
     "gf_dist_bcast_vocab": [_P, _P, _I],
     "gf_dist_bcast_map": [_P, _P, _I],
     "gf_vocab_download": [_P, _P, _P, _P, _P],
+    "gf_select_map_points": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
 }
 
 

@@ -18,6 +18,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstring>
 
 #include "common.h"
 #include "match_common.h"
@@ -1304,6 +1305,65 @@ int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n
     return GF_OK;
 }
 
+// Observability::setSelction_Number over map points (Observability.cc:
+// 1021-1247): MAP_INFO_MATRIX with the visibility check on the device, the
+// visible pool in list order, then the greedy of greedy_mtd on the device
+// (k_maxvol); mode 3 splits a large pool into threadNeeded chunks as the
+// reference does (:1086-1160), run in chunk order on the caller's rand()
+// stream, and finishes with an automatic pass over the merged selections.
+int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv, const float* pos, int n, int k,
+                         int greedy_mtd, int max_threads, gf_rng* rng, int32_t* out_idx, int* nout) {
+    GF_CHECK(ctx && cam && Xv && rng && nout, GF_ERR_ARG, "null arg");
+    GF_CHECK(greedy_mtd >= 1 && greedy_mtd <= 3, GF_ERR_ARG, "greedy_mtd must be 1, 2 or 3");
+    *nout = 0;
+    if (n <= 0) return GF_OK;
+    GF_CHECK(pos && out_idx, GF_ERR_ARG, "null arg");
+    std::vector<double> H(14 * (size_t)n), info(49 * (size_t)n);
+    std::vector<float> uv(2 * (size_t)n);
+    std::vector<uint8_t> valid(n);
+    int rc = gf_obs_build_info(ctx, cam, Xv, pos, nullptr, n, 1, H.data(), info.data(), uv.data(), valid.data());
+    if (rc) return rc;
+    std::vector<int> pool;
+    for (int i = 0; i < n; i++)
+        if (valid[i]) pool.push_back(i);
+    const int P = (int)pool.size();
+    std::vector<double> pinfo(49 * (size_t)std::max(P, 1)), pscore(std::max(P, 1), 1.0);
+    for (int j = 0; j < P; j++) memcpy(&pinfo[49 * (size_t)j], &info[49 * (size_t)pool[j]], 49 * sizeof(double));
+    const double scale = 6.0;  // random_sample_scale of the map overload (:1035)
+    std::vector<int32_t> sel(std::max(P, 1));
+    int ns = 0;
+    int T = 1;
+    if (greedy_mtd == 3 && !((float)P - 1.2f * (float)k <= 10 || P < 2 * 1000))
+        T = std::max(1, std::min((int)std::lround((float)P / 1000.f), max_threads));
+    if (T == 1) {
+        rc = gf_maxvol_select(ctx, pinfo.data(), pscore.data(), P, k, scale, greedy_mtd, rng, sel.data(), &ns);
+        if (rc) return rc;
+    } else {
+        const int kpar = (int)std::ceil((float)k / (float)T * 1.2f);
+        const int npar = (int)std::ceil((float)P / (float)T);
+        std::vector<int> merged;
+        for (int t = 0; t < T; t++) {
+            const int lo = t * npar, hi = std::min(P, (t + 1) * npar);
+            if (hi <= lo) continue;
+            std::vector<int32_t> o(hi - lo);
+            int no = 0;
+            rc = gf_maxvol_select(ctx, &pinfo[49 * (size_t)lo], &pscore[lo], hi - lo, kpar, scale, 3, rng, o.data(), &no);
+            if (rc) return rc;
+            for (int q = 0; q < no; q++) merged.push_back(lo + o[q]);
+        }
+        const int Mg = (int)merged.size();
+        std::vector<double> minfo(49 * (size_t)std::max(Mg, 1)), mscore(std::max(Mg, 1), 1.0);
+        for (int j = 0; j < Mg; j++) memcpy(&minfo[49 * (size_t)j], &pinfo[49 * (size_t)merged[j]], 49 * sizeof(double));
+        std::vector<int32_t> o(std::max(Mg, 1));
+        int no = 0;
+        rc = gf_maxvol_select(ctx, minfo.data(), mscore.data(), Mg, k, scale, 3, rng, o.data(), &no);
+        if (rc) return rc;
+        for (int q = 0; q < no; q++) sel[ns++] = merged[o[q]];
+    }
+    for (int q = 0; q < ns; q++) out_idx[(*nout)++] = pool[sel[q]];
+    return GF_OK;
+}
+
 }  // extern "C"
 
 // G1 on the device: Observability::updatePWLSVec(mLastFrame.mTimeStamp,
@@ -1419,22 +1479,42 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
 
 // mCurrentInfoMat = diag*I + sum over matched points (keypoint order) with
 // updateAtFrameId == frame_id of their ObsMat (Tracking.cc:3184, 3195-3213).
-__global__ void k_obs_accumulate_matched(const int32_t* __restrict__ kp2mp, const int32_t* __restrict__ nkps,
-                                         int kp_stride, const double* __restrict__ info,
-                                         const int32_t* __restrict__ upd_id, const int32_t* __restrict__ nmp,
-                                         int map_stride, int frame_id, double diag, double* __restrict__ out) {
-    const int f = blockIdx.x;
-    const int e = threadIdx.x;
-    if (e >= 49) return;
-    double s = (e % 8 == 0) ? diag : 0.0;
-    const int n = nkps[f], m = nmp[f];
-    for (int i = 0; i < n; i++) {
-        const int mp = kp2mp[(long long)f * kp_stride + i];
-        if (mp < 0 || mp >= m) continue;
-        const long long g = (long long)f * map_stride + mp;
-        if (upd_id[g] == frame_id) s = s + info[49 * g + e];
+__global__ __launch_bounds__(64) void k_obs_accumulate_matched(const int32_t* __restrict__ kp2mp,
+                                                               const int32_t* __restrict__ nkps, int kp_stride,
+                                                               const double* __restrict__ info,
+                                                               const int32_t* __restrict__ upd_id,
+                                                               const int32_t* __restrict__ nmp, int map_stride,
+                                                               int frame_id, double diag, double* __restrict__ out) {
+    __shared__ int list[KP_MAX];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int n = min(nkps[f], KP_MAX), m = nmp[f];
+    // the contributing map points in keypoint order (ballot compaction)
+    int cnt = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int i = base + lane;
+        int mp = i < n ? kp2mp[(long long)f * kp_stride + i] : -1;
+        const bool on = mp >= 0 && mp < m && upd_id[(long long)f * map_stride + mp] == frame_id;
+        const unsigned long long msk = __ballot(on);
+        if (on) list[cnt + __popcll(msk & ((1ull << lane) - 1ull))] = mp;
+        cnt += __popcll(msk);
     }
-    out[49LL * f + e] = s;
+    __syncthreads();
+    if (lane >= 49) return;
+    // lane = matrix entry; the additions stay in keypoint order (bit-exact with
+    // the sequential loop), the loads run ahead of them
+    double s = (lane % 8 == 0) ? diag : 0.0;
+    const double* I = info + (long long)f * map_stride * 49 + lane;
+    int i = 0;
+    for (; i + 4 <= cnt; i += 4) {
+        const double a = I[49LL * list[i]], b = I[49LL * list[i + 1]], c = I[49LL * list[i + 2]],
+                     d = I[49LL * list[i + 3]];
+        s = s + a;
+        s = s + b;
+        s = s + c;
+        s = s + d;
+    }
+    for (; i < cnt; i++) s = s + I[49LL * list[i]];
+    out[49LL * f + lane] = s;
 }
 
 }  // namespace

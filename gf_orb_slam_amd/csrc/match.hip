@@ -415,8 +415,8 @@ __device__ __forceinline__ void top2_insert(unsigned long long key, unsigned lon
 
 __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
-    int* claim = lds;                // kp_cap
-    int* qlist = claim + A.kp_cap;   // q_cap
+    int* claim = lds;                          // kp_cap
+    SeqPre* spre = (SeqPre*)(claim + A.kp_cap);  // q_cap: the precomputed outcomes, staged once
     __shared__ int s_nm, s_hist[HISTO_LENGTH], s_keep[3];
 
     const int f = blockIdx.x, lane = threadIdx.x;
@@ -434,27 +434,17 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
     for (int i = lane; i < n; i += SEQ_THREADS) claim[i] = kp2mp[i];
-    __syncthreads();
-
-    // ordered list of the queries that project into the image
-    int nvalid = 0;
-    for (int base = 0; base < nq; base += SEQ_THREADS) {
-        const int k = base + lane;
-        bool ok = false;
-        if (k < nq) {
-            if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = -1;
-            ok = make_query(A, fc, f, k).valid;
-        }
-        const unsigned long long m = __ballot(ok);
-        if (ok) qlist[nvalid + __popcll(m & ((1ull << lane) - 1ull))] = k;
-        nvalid += __popcll(m);
+    for (int k = lane; k < nq; k += SEQ_THREADS) {
+        spre[k] = A.pre[(long long)f * A.q_cap + k];
+        if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = -1;
     }
     __syncthreads();
 
+    // queries in the reference order; a query that does not project into the
+    // image has no holders and no result, so it passes as a no-op
     const unsigned long long NONE = ~0ull;
-    for (int qi = 0; qi < nvalid; qi++) {
-        const int k = qlist[qi];
-        const SeqPre pr = A.pre[(long long)f * A.q_cap + k];
+    for (int k = 0; k < nq; k++) {
+        const SeqPre pr = spre[k];
         if ((pr.holder1 < 0 || claim[pr.holder1] < 0) && (pr.holder2 < 0 || claim[pr.holder2] < 0)) {
             if (lane == 0 && pr.res >= 0) {  // the precomputed outcome still holds
                 claim[pr.res] = pr.id;
@@ -528,7 +518,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
     if (lane == 0) A.nmatches[f] = s_nm;
 }
 
-size_t seq_lds_bytes(int kp_cap, int q_cap) { return sizeof(int) * ((size_t)kp_cap + q_cap); }
+size_t seq_lds_bytes(int kp_cap, int q_cap) { return sizeof(int) * (size_t)kp_cap + sizeof(SeqPre) * (size_t)q_cap; }
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,

@@ -122,6 +122,19 @@ class Observability:
         self.mLeftMapPoints = left[:nleft.value].copy()
         return nmatched.value
 
+    def setSelction_Number(self, num_good_inlier: int, greedy_mtd: int, map_pos, max_threads: int = 8):
+        """Observability::setSelction_Number over map points
+        (Observability.cc:1021-1247) at kinematic[1] (mKineIdx = 1): the
+        selected map indices (mpVec idx) in selection order."""
+        pos = np.ascontiguousarray(map_pos, np.float32).reshape(-1, 3)
+        xv = np.ascontiguousarray(self.kinematic[1].Xv[:] if len(self.kinematic) > 1 else self.Xv, np.float64)
+        out = np.zeros(max(len(pos), 1), np.int32)
+        nout = ctypes.c_int()
+        check(lib().gf_select_map_points(self.ctx.handle, ctypes.byref(self.camera), ptr(xv), ptr(pos), len(pos),
+                                         int(num_good_inlier), int(greedy_mtd), int(max_threads),
+                                         ctypes.byref(self.rng), ptr(out), ctypes.byref(nout)))
+        return out[:nout.value].copy()
+
     def maxvol_select(self, info, score, k, sample_scale, mode):
         info = np.ascontiguousarray(info, np.float64).reshape(-1, 49)
         n = len(info)

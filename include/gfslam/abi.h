@@ -289,6 +289,21 @@ int gf_obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint*
 int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n, int k, double sample_scale,
                      int mode, gf_rng* rng, int32_t* out_idx, int* nout);
 
+/* Observability::setSelction_Number(num_good_inlier, greedy_mtd, time,
+ * mapPoints, mpVec) (Observability.cc:1021-1247; test/test_GoodMap.cpp drives
+ * it): MAP_INFO_MATRIX with the visibility check (mKineIdx = 1: Xv is the
+ * predicted kinematic[1] state) over the n map points at pos, the visible ones
+ * form the pool in list order, then greedy_mtd 1 = BaselineGreedy, 2 =
+ * LazierGreedy, 3 = maxVolAutomatic_LazierGreedy with the multi-thread split
+ * (threadNeeded = min(round(pool / 1000), max_threads) when pool >= 2000 and
+ * pool - 1.2 k > 10; chunks of ceil(pool / T) selecting ceil(k / T * 1.2)
+ * each, then one pass over the merged selections). sample_scale 6. The chunks
+ * draw from `rng` in chunk order (the reference's threads share std::rand()
+ * in race order). out_idx = map indices in selection order (deletion
+ * variant: pool order); at most 4096 visible points per greedy call. */
+int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv, const float* pos, int n, int k,
+                         int greedy_mtd, int max_threads, gf_rng* rng, int32_t* out_idx, int* nout);
+
 /* Device family of the GF rows, batched over frames (per-frame arrays strided
  * by cap / mp_cap; d_Xv is [F][13], d_base [F][49], d_rng [F]). Pool limit
  * for active matching and max-volume selection: 4096 landmarks.
