@@ -55,3 +55,9 @@ DROPIN = tests/cpp/dropin_frontend
 all: $(DROPIN)
 $(DROPIN): tests/cpp/dropin_frontend.cpp include/gfslam/orbslam.h include/gfslam/abi.h $(LIB)
 	$(CXX) -O2 -std=c++17 -Iinclude $< -Lgf_orb_slam_amd -lgfslam -Wl,-rpath,'$$ORIGIN/../../gf_orb_slam_amd' -o $@
+
+# C-ABI-only caller: batched front-end sequence + local BA (tests/test_dropin_gpu.py)
+SEQDRV = tests/cpp/sequence_driver
+all: $(SEQDRV)
+$(SEQDRV): tests/cpp/sequence_driver.cpp include/gfslam/orbslam.h include/gfslam/abi.h $(LIB)
+	$(CXX) -O2 -std=c++17 -Iinclude $< -Lgf_orb_slam_amd -lgfslam -Wl,-rpath,'$$ORIGIN/../../gf_orb_slam_amd' -o $@

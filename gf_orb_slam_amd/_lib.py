@@ -133,6 +133,8 @@ _PROTOS = {
     "gf_ba_plan_solve": [_P, _P, _P],
     "gf_ba_plan_results": [_P, _P],
     "gf_ba_plan_destroy": [_P],
+    "gf_ba_plan_solve_stop": [_P, _P, _P, _P],
+    "gf_local_ba_stop": [_P, _P, _P, _P],
     "gf_orb_extract_ptrs_dev": [_P, _I, _P, _I, _P, _P, _P, _I, _P],
     "gf_frustum_list_dev": [_P, _P, _I, _P, _P, _I, _P, _P, _F, _P, _P, _P],
     "gf_match_project_list_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _P, _F, _F, _P, _P, _P, _P],
@@ -144,6 +146,7 @@ _PROTOS = {
     "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
+    "gf_frontend_bootstrap_host": [_P, _P, _P, _P, _D],
     "gf_frontend_step_host": [_P, _P],
     "gf_frontend_capture": [_P],
     "gf_frontend_sync": [_P],

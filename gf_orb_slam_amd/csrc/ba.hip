@@ -115,6 +115,10 @@ struct BAArena {
     float* out_X;
     // diagnostics: phase stamps of k_ba_solve (s_memrealtime, 100 MHz) when non-null
     unsigned long long* tstamp;
+    // setForceStopFlag (Optimizer.cc:1579-1580): != 0 ends every optimize()
+    // call at its next iteration boundary (SparseOptimizer::optimize checks
+    // terminate() before each iteration, sparse_optimizer.cpp:376)
+    const int* stop;
 };
 
 __device__ __forceinline__ gfse3::SE3 load_T(const BAArena& A, int buf, int gk) {
@@ -930,7 +934,7 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
             st.need_lin = 0;  // another trial on the same system
         } else {
             st.iters[st.round]++;
-            bool term = (st.q == 10 || rho == 0);
+            bool term = (st.q == 10 || rho == 0) || (A.stop && *A.stop);
             if (!term) {
                 if ((st.iniChi - st.currentChi) * 1e3 < st.iniChi)
                     st.nbad++;
@@ -994,6 +998,11 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         if (s2.round == 1 && s_cnt == 0) {  // no edge left: optimize(10) does not run
             s2.round = 2;
             s2.iters[1] = -1;
+        } else if (s2.round == 1 && A.stop && *A.stop) {
+            // stopped: optimize(10) returns before its first iteration; its
+            // outlier check sees the estimate the first pass just checked
+            s2.round = 2;
+            s2.iters[1] = 0;
         }
         s2.iter = 0;
         s2.q = 0;
@@ -1053,6 +1062,7 @@ struct gf_ba_plan {
     std::vector<void*> owned;
     BAState* h_state = nullptr;  // pinned
     BADesc* d_desc = nullptr;
+    int* d_stop = nullptr;       // device copy of the caller's stop flag
     std::vector<uint8_t> h_out;  // scratch for results
 };
 
@@ -1358,12 +1368,21 @@ extern "C" int gf_ba_plan_debug_stamps(gf_ba_plan* P, unsigned long long* d_stam
 
 extern "C" {
 
-int gf_ba_plan_solve(gf_ba_plan* P, void* stream, int* steps) {
+int gf_ba_plan_solve(gf_ba_plan* P, void* stream, int* steps) { return gf_ba_plan_solve_stop(P, stream, nullptr, steps); }
+
+int gf_ba_plan_solve_stop(gf_ba_plan* P, void* stream, const volatile uint8_t* stop_flag, int* steps) {
     GF_CHECK(P, GF_ERR_ARG, "null plan");
     if (steps) *steps = 0;
     if (P->nprob == 0) return GF_OK;
     GF_HIP(hipSetDevice(P->ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : P->ctx->stream;
+    if (!P->d_stop) {
+        GF_HIP(hipMalloc(&P->d_stop, sizeof(int)));
+        P->owned.push_back(P->d_stop);
+        P->A.stop = P->d_stop;
+    }
+    GF_HIP(hipMemsetAsync(P->d_stop, 0, sizeof(int), s));
+    bool stop_sent = false;
     GF_HIP(hipMemsetAsync(P->A.panel, 0, P->panel_doubles * sizeof(double), s));
     {
         GF_PROF(P->ctx, s, "k_ba_init");
@@ -1375,6 +1394,11 @@ int gf_ba_plan_solve(gf_ba_plan* P, void* stream, int* steps) {
     bool done = false;
     while (!done) {
         GF_CHECK(n < BA_MAXSTEPS, GF_ERR_HIP, "local BA did not terminate");
+        if (stop_flag && *stop_flag && !stop_sent) {  // the caller raised mbAbortBA
+            static const int one = 1;
+            GF_HIP(hipMemcpyAsync(P->d_stop, &one, sizeof(int), hipMemcpyHostToDevice, s));
+            stop_sent = true;
+        }
         for (int c = 0; c < chunk; c++, n++) {
             int rc = ba_launch_step(P, s);
             if (rc) return rc;
@@ -1417,11 +1441,15 @@ int gf_ba_plan_results(gf_ba_plan* P, gf_ba_result* res) {
 }
 
 int gf_local_ba(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res) {
+    return gf_local_ba_stop(ctx, prob, res, nullptr);
+}
+
+int gf_local_ba_stop(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res, const volatile uint8_t* stop_flag) {
     GF_CHECK(ctx && prob && res, GF_ERR_ARG, "null arg");
     gf_ba_plan* P = nullptr;
     int rc = gf_ba_plan_create(ctx, 1, prob, &P);
     if (rc) return rc;
-    rc = gf_ba_plan_solve(P, nullptr, nullptr);
+    rc = gf_ba_plan_solve_stop(P, nullptr, stop_flag, nullptr);
     if (!rc) rc = gf_ba_plan_results(P, res);
     gf_ba_plan_destroy(P);
     return rc;

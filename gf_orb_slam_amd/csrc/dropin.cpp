@@ -417,4 +417,36 @@ int Optimizer::PoseOptimization(Frame* pFrame) {
     return ninl;
 }
 
+void Optimizer::LocalBundleAdjustment(LocalBAWindow* w, bool* pbStopFlag) {
+    if (!w) throw GpuError(GF_ERR_ARG, "null window");
+    gf_ba_problem P{};
+    P.nkf = (int32_t)w->kf_kind.size();
+    P.npts = (int32_t)(w->pt_pos.size() / 3);
+    P.nedges = (int32_t)w->edge_pt.size();
+    if (w->kf_Tcw.size() != 16 * (size_t)P.nkf || w->kf_cam.size() != 4 * (size_t)P.nkf ||
+        w->edge_kf.size() != (size_t)P.nedges || w->edge_z.size() != 2 * (size_t)P.nedges ||
+        w->edge_inv_sigma2.size() != (size_t)P.nedges)
+        throw GpuError(GF_ERR_ARG, "inconsistent local BA window");
+    P.kf_Tcw = w->kf_Tcw.data();
+    P.kf_kind = w->kf_kind.data();
+    P.kf_cam = w->kf_cam.data();
+    P.pt_pos = w->pt_pos.data();
+    P.edge_pt = w->edge_pt.data();
+    P.edge_kf = w->edge_kf.data();
+    P.edge_z = w->edge_z.data();
+    P.edge_inv_sigma2 = w->edge_inv_sigma2.data();
+    std::vector<float> T(w->kf_Tcw.size()), X(w->pt_pos.size());
+    w->edge_outlier.assign(P.nedges, 0);
+    gf_ba_result R{};
+    R.kf_Tcw = T.data();
+    R.pt_pos = X.data();
+    R.edge_outlier = w->edge_outlier.data();
+    static_assert(sizeof(bool) == 1, "bool flag read as a byte");
+    check(gf_local_ba_stop(Context(), &P, &R, reinterpret_cast<const volatile uint8_t*>(pbStopFlag)));
+    w->kf_Tcw = T;
+    w->pt_pos = X;
+    w->iterations[0] = R.iterations[0];
+    w->iterations[1] = R.iterations[1];
+}
+
 }  // namespace ORB_SLAM

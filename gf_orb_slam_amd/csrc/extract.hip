@@ -570,7 +570,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
 // -------------------------------------------------------------- k_select
 // One workgroup per (level, frame).
 #define SEL_MAX_CELLS 1024
-#define SEL_LDS 12288  // staged entries (cell lists + level list), 48 KB
 __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
                                                 uint32_t* __restrict__ lists, long long list_stride,
                                                 const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
@@ -621,34 +620,9 @@ __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __r
         }
     }
     __syncthreads();
-    // Stage the level's cell lists in LDS when they fit (the selection walks
-    // them with data-dependent accesses: nth_element in LDS instead of HBM).
-    extern __shared__ uint32_t sel_lds[];
-    __shared__ int s_total;
-    __shared__ int soff[SEL_MAX_CELLS + 1];
-    if (threadIdx.x == 0) {
-        int t = 0;
-        for (int c = 0; c < nc; c++) {
-            soff[c] = t;
-            t += valid[c] ? cnt[c] : 0;
-        }
-        soff[nc] = t;
-        s_total = t;
-    }
-    __syncthreads();
-    const bool staged = 2 * s_total <= SEL_LDS;
-    const uint32_t* glist = lists + (long long)f * list_stride;
-    if (staged) {
-        for (int c = 0; c < nc; c++) {
-            if (!valid[c]) continue;
-            const uint32_t* a = glist + cells[cb + c].cap_off;
-            for (int i = threadIdx.x; i < cnt[c]; i += blockDim.x) sel_lds[soff[c] + i] = a[i];
-        }
-        __syncthreads();
-    }
     for (int c = threadIdx.x; c < nc; c += blockDim.x) {
         if (!valid[c]) continue;
-        uint32_t* a = staged ? sel_lds + soff[c] : lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
         keep[c] = gfsel::retain_best_truncate(a, cnt[c], keep[c], gfsel::RespGreater());
     }
     __syncthreads();
@@ -662,22 +636,17 @@ __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __r
     }
     __syncthreads();
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
-    uint32_t* Ls = staged ? sel_lds + s_total : L;  // the level list, in LDS when staged
     for (int c = threadIdx.x; c < nc; c += blockDim.x) {
         if (!valid[c]) continue;
-        const uint32_t* a = staged ? sel_lds + soff[c] : lists + (long long)f * list_stride + cells[cb + c].cap_off;
-        for (int i = 0; i < keep[c]; i++) Ls[off[c] + i] = a[i];
+        const uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        for (int i = 0; i < keep[c]; i++) L[off[c] + i] = a[i];
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         int total = off[nc];
-        total = gfsel::retain_best_truncate(Ls, total, g.ndesired[l], gfsel::RespGreater());
+        total = gfsel::retain_best_truncate(L, total, g.ndesired[l], gfsel::RespGreater());
         lvl_counts[(long long)f * g.nlevels + l] = total;
-        s_total = total;
     }
-    __syncthreads();
-    if (staged)
-        for (int i = threadIdx.x; i < s_total; i += blockDim.x) L[i] = Ls[i];
 }
 
 // -------------------------------------------------------------- k_describe
@@ -1265,7 +1234,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     }
     {
         GF_PROF(ctx, s, "k_select");
-        k_select<<<dim3(ex->nlevels, nframes), 256, SEL_LDS * sizeof(uint32_t), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+        k_select<<<dim3(ex->nlevels, nframes), 256, 0, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }

@@ -680,9 +680,37 @@ int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed) {
     return GF_OK;
 }
 
+static int fe_staging(gf_frontend* fe, const uint8_t* imgs) {
+    FeDev& D = fe->D;
+    const size_t fb = (size_t)fe->p.width * fe->p.height;
+    if (!fe->staging) {
+        void* p = nullptr;
+        FE_RC(fe_alloc(fe, fb * D.B, &p));
+        fe->staging = (uint8_t*)p;
+        std::vector<const uint8_t*> ptr(D.B);
+        for (int b = 0; b < D.B; b++) ptr[b] = fe->staging + fb * b;
+        GF_HIP(hipMemcpy((void*)D.ptrs, ptr.data(), sizeof(void*) * D.B, hipMemcpyHostToDevice));
+    }
+    GF_HIP(hipMemcpyAsync(fe->staging, imgs, fb * D.B, hipMemcpyHostToDevice, fe->ctx->stream));
+    return GF_OK;
+}
+
+static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0, bool host);
+
 int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0) {
     GF_CHECK(fe && Tcw && V, GF_ERR_ARG, "null arg");
     GF_CHECK(fe->sourced, GF_ERR_ARG, "no frame source set");
+    return fe_bootstrap(fe, Tcw, V, t0, false);
+}
+
+int gf_frontend_bootstrap_host(gf_frontend* fe, const uint8_t* imgs, const float* Tcw, const float* V, double t0) {
+    GF_CHECK(fe && imgs && Tcw && V, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    FE_RC(fe_staging(fe, imgs));
+    return fe_bootstrap(fe, Tcw, V, t0, true);
+}
+
+static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0, bool host) {
     GF_HIP(hipSetDevice(fe->ctx->device));
     FeDev& D = fe->D;
     const int B = D.B, cap = D.cap, M = D.M;
@@ -692,8 +720,15 @@ int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, dou
     GF_HIP(hipMemcpyAsync(D.Tcw, Tcw, sizeof(float) * 16 * B, hipMemcpyHostToDevice, s));
     GF_HIP(hipMemcpyAsync(D.V, V, sizeof(float) * 16 * B, hipMemcpyHostToDevice, s));
     GF_HIP(hipMemcpyAsync(D.t_cur, t.data(), sizeof(double) * B, hipMemcpyHostToDevice, s));
-    k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(D);
-    GF_HIP(hipGetLastError());
+    if (!host) {
+        k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(D);
+        GF_HIP(hipGetLastError());
+    } else {  // the step counter still advances: a sourced step after a host bootstrap continues the loop
+        FeDev Dh = D;
+        Dh.src_mode = 0;
+        k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(Dh);
+        GF_HIP(hipGetLastError());
+    }
     GF_HIP(hipMemsetAsync(D.kp2mp, 0xff, sizeof(int32_t) * B * cap, s));
     std::vector<int32_t> s999((size_t)B * cap, 999);
     GF_HIP(hipMemcpyAsync(D.score, s999.data(), 4 * s999.size(), hipMemcpyHostToDevice, s));
@@ -735,17 +770,8 @@ int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
     GF_CHECK(fe && imgs, GF_ERR_ARG, "null arg");
     GF_HIP(hipSetDevice(fe->ctx->device));
     FeDev& D = fe->D;
-    const size_t fb = (size_t)fe->p.width * fe->p.height;
     hipStream_t s = fe->ctx->stream;
-    if (!fe->staging) {
-        void* p = nullptr;
-        FE_RC(fe_alloc(fe, fb * D.B, &p));
-        fe->staging = (uint8_t*)p;
-        std::vector<const uint8_t*> ptr(D.B);
-        for (int b = 0; b < D.B; b++) ptr[b] = fe->staging + fb * b;
-        GF_HIP(hipMemcpy((void*)D.ptrs, ptr.data(), sizeof(void*) * D.B, hipMemcpyHostToDevice));
-    }
-    GF_HIP(hipMemcpyAsync(fe->staging, imgs, fb * D.B, hipMemcpyHostToDevice, s));
+    FE_RC(fe_staging(fe, imgs));
     const int mode = D.src_mode;
     D.src_mode = 2;  // pointers stay on the staging buffer
     auto ticks = [](double v) -> long long { return std::isfinite(v) && v >= 0 ? (long long)(v * 1e8) : -1; };

@@ -306,17 +306,20 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     if (tid == 0) A.nmatches[f] = s_nm;
 }
 
-// ---- Per-query precompute for the wave-sequential matcher. Every valid query
-// runs its window scan at once (one thread each) against the frame's starting
-// claims, keeping the keypoints that end in first and second place of the
-// best / second-best loop. Claims only remove keypoints and the loop's outcome
-// depends on those two holders alone (the first keypoint at the minimum
-// distance, the first other one at the second smallest), so in the ordered
-// pass a query whose holders are both still unclaimed takes its precomputed
-// result as is; only the others scan again.
+// ---- Per-query precompute for the wave-sequential matcher (SearchByProjection
+// (Cur, Last), best candidate only). Every valid query runs its window scan at
+// once (one thread each) against the frame's starting claims and keeps its
+// four smallest (distance, candidate order) candidates. Claims only remove
+// keypoints, so in the ordered pass a query's outcome is the first of its four
+// still unclaimed (ties already resolved by candidate order, as the
+// sequential `dist < bestDist` loop does); only a query that lost all four
+// while its window holds more candidates scans again.
 struct SeqPre {
     int32_t id;
-    int16_t res, dist, holder1, holder2;
+    int16_t h[4];   // the four smallest (distance, candidate order) candidates, ascending; -1 = none
+    int16_t d[4];   // their distances
+    int16_t ncand;  // candidates in the window, capped at 5
+    int16_t pad;
 };
 
 #define SEQ_PRE_THREADS 1024
@@ -351,9 +354,13 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
     const uint8_t* DD = dl ? (const uint8_t*)Ds : D;
     for (int k = tid; k < nq; k += SEQ_PRE_THREADS) {
         const Query q = make_query(A, fc, f, k);
-        SeqPre r{q.id, -1, 0, -1, -1};
+        SeqPre r;
+        r.id = q.id;
+        r.ncand = 0;
+        r.pad = 0;
+        for (int j = 0; j < 4; j++) r.h[j] = -1, r.d[j] = 0;
         if (q.valid) {
-            int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, h1 = -1, h2 = -1;
+            int hd[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX}, hi[4] = {-1, -1, -1, -1}, nc = 0;
             for (int ix = q.cx0; ix <= q.cx1; ix++) {
                 const int s0 = cell_start[ix * GRID_ROWS + q.cy0], s1 = cell_start[ix * GRID_ROWS + q.cy1 + 1];
                 for (int t = s0; t < s1; t++) {
@@ -364,27 +371,22 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
                         claim[idx] >= 0)
                         continue;
                     const int dist = hamming32(q.d, DD + (long long)idx * 32);
-                    if (dist < bestDist) {
-                        bestDist2 = bestDist;
-                        bestDist = dist;
-                        bestLevel2 = bestLevel;
-                        bestLevel = oct;
-                        h2 = h1;
-                        h1 = idx;
-                    } else if (dist < bestDist2) {
-                        bestLevel2 = oct;
-                        bestDist2 = dist;
-                        h2 = idx;
+                    nc++;
+                    // insert (dist, order): strict <, so ties keep the earlier candidate
+                    int j = 4;
+                    while (j > 0 && dist < hd[j - 1]) j--;
+                    if (j < 4) {
+                        for (int m = 3; m > j; m--) hd[m] = hd[m - 1], hi[m] = hi[m - 1];
+                        hd[j] = dist;
+                        hi[j] = idx;
                     }
                 }
             }
-            r.holder1 = (int16_t)h1;
-            r.holder2 = (int16_t)h2;
-            if (h1 >= 0 && bestDist <= TH_HIGH &&
-                !(A.mode == MODE_PROJECT && bestLevel == bestLevel2 && (float)bestDist > A.nnratio * (float)bestDist2)) {
-                r.res = (int16_t)h1;
-                r.dist = (int16_t)bestDist;
+            for (int j = 0; j < 4; j++) {
+                r.h[j] = (int16_t)hi[j];
+                r.d[j] = (int16_t)(hi[j] >= 0 ? hd[j] : 0);
             }
+            r.ncand = (int16_t)min(nc, 5);
         }
         out[(long long)f * A.q_cap + k] = r;
     }
@@ -415,8 +417,13 @@ __device__ __forceinline__ void top2_insert(unsigned long long key, unsigned lon
 
 __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
-    int* claim = lds;                          // kp_cap
+    // everything the ordered loop touches lives in LDS, so its per-query
+    // barrier waits on LDS only (global stores would be drained every query)
+    int* claim = lds;                            // kp_cap
     SeqPre* spre = (SeqPre*)(claim + A.kp_cap);  // q_cap: the precomputed outcomes, staged once
+    int16_t* sdist = (int16_t*)(spre + A.q_cap); // kp_cap: score of each claim made here
+    int16_t* sres = sdist + A.kp_cap;            // q_cap: matched keypoint per query (-1 none)
+    int16_t* qidx = sres + A.q_cap;              // q_cap: query index of each staged outcome
     __shared__ int s_nm, s_hist[HISTO_LENGTH], s_keep[3];
 
     const int f = blockIdx.x, lane = threadIdx.x;
@@ -433,24 +440,50 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
         s_nm = 0;
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
-    for (int i = lane; i < n; i += SEQ_THREADS) claim[i] = kp2mp[i];
-    for (int k = lane; k < nq; k += SEQ_THREADS) {
-        spre[k] = A.pre[(long long)f * A.q_cap + k];
-        if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = -1;
+    for (int i = lane; i < n; i += SEQ_THREADS) {
+        claim[i] = kp2mp[i];
+        sdist[i] = -1;
+    }
+    // the queries with candidates, in the reference order (the others match
+    // nothing); their precomputed outcomes staged in LDS
+    int nvalid = 0;
+    for (int base = 0; base < nq; base += SEQ_THREADS) {
+        const int k = base + lane;
+        SeqPre pr;
+        bool on = false;
+        if (k < nq) {
+            pr = A.pre[(long long)f * A.q_cap + k];
+            on = pr.ncand > 0;
+            sres[k] = -1;
+        }
+        const unsigned long long m = __ballot(on);
+        if (on) {
+            pr.pad = 0;
+            spre[nvalid + __popcll(m & ((1ull << lane) - 1ull))] = pr;
+            qidx[nvalid + __popcll(m & ((1ull << lane) - 1ull))] = (int16_t)k;
+        }
+        nvalid += __popcll(m);
     }
     __syncthreads();
 
-    // queries in the reference order; a query that does not project into the
-    // image has no holders and no result, so it passes as a no-op
     const unsigned long long NONE = ~0ull;
-    for (int k = 0; k < nq; k++) {
-        const SeqPre pr = spre[k];
-        if ((pr.holder1 < 0 || claim[pr.holder1] < 0) && (pr.holder2 < 0 || claim[pr.holder2] < 0)) {
-            if (lane == 0 && pr.res >= 0) {  // the precomputed outcome still holds
-                claim[pr.res] = pr.id;
-                score[pr.res] = pr.dist;
+    for (int qi = 0; qi < nvalid; qi++) {
+        const SeqPre pr = spre[qi];
+        const int k = qidx[qi];
+        // SearchByProjection(Cur, Last) keeps the best candidate only (no
+        // ratio test): the outcome is the first of the four precomputed best
+        // candidates still unclaimed; a query whose four are all taken while
+        // the window holds more candidates scans again
+        int j = 0;
+        while (j < 4 && pr.h[j] >= 0 && claim[pr.h[j]] >= 0) j++;
+        const bool known = (j < 4 && pr.h[j] >= 0) || j >= pr.ncand;
+        if (known) {
+            if (lane == 0 && j < pr.ncand && j < 4 && pr.d[j] <= TH_HIGH) {
+                const int res = pr.h[j];
+                claim[res] = pr.id;
+                sdist[res] = pr.d[j];
                 s_nm++;
-                if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = pr.res;
+                sres[k] = (int16_t)res;
             }
             __syncthreads();
             continue;
@@ -505,20 +538,26 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
                     }
                     const int bestIdx = items[cell_start[c * GRID_ROWS + q.cy0] + tt];
                     claim[bestIdx] = q.id;
-                    score[bestIdx] = bestDist;
+                    sdist[bestIdx] = (int16_t)bestDist;
                     s_nm++;
-                    if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = bestIdx;
+                    sres[k] = (int16_t)bestIdx;
                 }
             }
         }
         __syncthreads();
     }
+    for (int i = lane; i < n; i += SEQ_THREADS)
+        if (sdist[i] >= 0) score[i] = sdist[i];
+    for (int k = lane; k < nq; k += SEQ_THREADS) A.qres[(long long)f * A.q_cap + k] = sres[k];
+    __syncthreads();
     if (A.mode == MODE_LAST && A.check_ori) rotation_filter(A, f, nq, K, claim, score, &s_nm, s_hist, s_keep, SEQ_THREADS);
     for (int i = lane; i < n; i += SEQ_THREADS) kp2mp[i] = claim[i];
     if (lane == 0) A.nmatches[f] = s_nm;
 }
 
-size_t seq_lds_bytes(int kp_cap, int q_cap) { return sizeof(int) * (size_t)kp_cap + sizeof(SeqPre) * (size_t)q_cap; }
+size_t seq_lds_bytes(int kp_cap, int q_cap) {
+    return sizeof(int) * (size_t)kp_cap + sizeof(SeqPre) * (size_t)q_cap + 2 * ((size_t)kp_cap + 2 * q_cap) + 4;
+}
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
@@ -619,7 +658,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
         GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)match_lds_bytes()));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)seq_lds_bytes(KP_MAX, Q_MAX)));
+                                   152 * 1024));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq_pre, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)seq_pre_lds_bytes(KP_MAX)));
         attr_mask |= 1ull << ctx->device;
@@ -788,7 +827,8 @@ int gf_match_lastframe_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, co
         return rc;
     A.grid_cs = (int*)gcs;
     A.grid_items = (int*)gitems;
-    GF_CHECK(seq_pre_lds_bytes(kp_cap) <= 160 * 1024, GF_ERR_UNSUPPORTED, "keypoint capacity too large");
+    GF_CHECK(seq_pre_lds_bytes(kp_cap) <= 160 * 1024 && seq_lds_bytes(kp_cap, last_cap) <= 152 * 1024,
+             GF_ERR_UNSUPPORTED, "keypoint / last-frame capacity too large for LDS");
     return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
 }
 

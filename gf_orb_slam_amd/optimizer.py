@@ -129,13 +129,15 @@ class BAArrays:
                 tuple(int(i) for i in self.result.iterations))
 
 
-def local_bundle_adjustment(prob: dict, ctx=None):
-    """Optimizer::LocalBundleAdjustment (Optimizer.cc:1515-1764) on one local
-    window (dict with the gf_ba_problem arrays, e.g. synth.synth_lba_problem).
-    Returns (kf_Tcw, pt_pos, edge_outlier, iterations)."""
+def local_bundle_adjustment(prob: dict, ctx=None, stop_flag=None):
+    """Optimizer::LocalBundleAdjustment(pKF, pbStopFlag) (Optimizer.cc:1515-1764)
+    on one local window (dict with the gf_ba_problem arrays, e.g.
+    synth.synth_lba_problem). stop_flag: optional ctypes.c_uint8 polled as
+    mbAbortBA. Returns (kf_Tcw, pt_pos, edge_outlier, iterations)."""
     ctx = ctx or default_context()
     arr = BAArrays(prob)
-    check(lib().gf_local_ba(ctx.handle, ctypes.byref(arr.problem), ctypes.byref(arr.result)))
+    check(lib().gf_local_ba_stop(ctx.handle, ctypes.byref(arr.problem), ctypes.byref(arr.result),
+                                 ctypes.byref(stop_flag) if stop_flag is not None else None))
     return arr.out()
 
 

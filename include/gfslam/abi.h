@@ -532,6 +532,16 @@ int gf_local_ba(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res);
 int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_plan** out);
 int gf_ba_plan_solve(gf_ba_plan* plan, void* stream, int* steps);
 int gf_ba_plan_results(gf_ba_plan* plan, gf_ba_result* res);
+/* The abortable forms: LocalBundleAdjustment(pKF, &mbAbortBA) with
+ * optimizer.setForceStopFlag(pbStopFlag) (Optimizer.cc:1515, 1579-1580;
+ * LocalMapping.cc:108). The host polls *stop_flag (written by another thread,
+ * as LocalMapping's mbAbortBA is) between LM iterations; once it is set every
+ * problem's running optimize() call ends at its next iteration boundary (the
+ * iteration in flight completes, as SparseOptimizer::optimize checks
+ * terminate() before each iteration), optimize(10) then runs 0 iterations and
+ * both outlier checks still run. NULL = never stop. */
+int gf_ba_plan_solve_stop(gf_ba_plan* plan, void* stream, const volatile uint8_t* stop_flag, int* steps);
+int gf_local_ba_stop(gf_ctx* ctx, const gf_ba_problem* prob, gf_ba_result* res, const volatile uint8_t* stop_flag);
 int gf_ba_plan_destroy(gf_ba_plan* plan);
 
 /* ------------------------------------------------ keypoint undistortion
@@ -815,6 +825,10 @@ int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed);
  * mLastFrame with timestamp t0, V [B][16] the motion model, and the step
  * counter advances by one. */
 int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0);
+/* Same with the B bootstrap frames from host memory ([B][height][width] u8),
+ * for callers without a device frame source (then step with
+ * gf_frontend_step_host). */
+int gf_frontend_bootstrap_host(gf_frontend* fe, const uint8_t* imgs, const float* Tcw, const float* V, double t0);
 /* One frame per stream from the source (asynchronous on the context stream). */
 int gf_frontend_step(gf_frontend* fe);
 /* Same with the B frames taken from host memory ([B][height][width] u8):

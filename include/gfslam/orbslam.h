@@ -226,6 +226,25 @@ public:
      * pFrame->mTcw and mvbOutlier of the matched keypoints, returns the
      * number of inliers. */
     static int PoseOptimization(Frame* pFrame);
+
+    /* Optimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag)
+     * (Optimizer.cc:1515-1764). The local window the reference collects from
+     * pKF's covisibility graph (:1518-1566) is passed as a LocalBAWindow in
+     * the reference's vertex and edge orders (gf_ba_problem); the optimised
+     * poses and points and the outlier flags come back in the same window.
+     * *pbStopFlag (LocalMapping::mbAbortBA) is polled between iterations. */
+    struct LocalBAWindow {
+        std::vector<float> kf_Tcw;        /* nkf x 16 (in / out) */
+        std::vector<uint8_t> kf_kind;     /* 0 local, 1 local fixed (mnId 0), 2 fixed camera */
+        std::vector<float> kf_cam;        /* nkf x 4: fx fy cx cy */
+        std::vector<float> pt_pos;        /* npts x 3 (in / out) */
+        std::vector<int32_t> edge_pt, edge_kf;
+        std::vector<float> edge_z;        /* nedges x 2 */
+        std::vector<float> edge_inv_sigma2;
+        std::vector<uint8_t> edge_outlier; /* out: 1 removed after optimize(5), 2 after optimize(10) */
+        int iterations[2] = {0, 0};
+    };
+    static void LocalBundleAdjustment(LocalBAWindow* pWindow, bool* pbStopFlag);
 };
 
 }  // namespace ORB_SLAM

@@ -367,8 +367,14 @@ struct LBA {
 
 extern "C" {
 
+int orc_local_ba_iters(const gf_ba_problem* P, gf_ba_result* R, int its0, int its1);
+
 // Optimizer::LocalBundleAdjustment on an explicit local window (gf_ba_problem).
-int orc_local_ba(const gf_ba_problem* P, gf_ba_result* R) {
+int orc_local_ba(const gf_ba_problem* P, gf_ba_result* R) { return orc_local_ba_iters(P, R, 5, 10); }
+
+// The same with other iteration caps for the two optimize() calls (a force
+// stop after its0 iterations is optimize(its0) then optimize(0)).
+int orc_local_ba_iters(const gf_ba_problem* P, gf_ba_result* R, int its0, int its1) {
     if (!P || !R) return GF_ERR_ARG;
     orc::LBA L;
     L.delta = (double)(float)std::sqrt(5.991);  // const float thHuber = sqrt(5.991)
@@ -394,13 +400,13 @@ int orc_local_ba(const gf_ba_problem* P, gf_ba_result* R) {
         L.E.push_back(g);
         R->edge_outlier[e] = 0;
     }
-    R->iterations[0] = L.optimize(5);
+    R->iterations[0] = L.optimize(its0);
     for (int e = 0; e < P->nedges; e++)
         if (L.is_outlier(L.E[e])) {
             L.E[e].active = false;  // EraseMapPointMatch / EraseObservation / removeEdge
             R->edge_outlier[e] = 1;
         }
-    R->iterations[1] = L.optimize(10);
+    R->iterations[1] = L.optimize(its1);
     for (int e = 0; e < P->nedges; e++)
         if (L.E[e].active && L.is_outlier(L.E[e])) R->edge_outlier[e] = 2;
     for (int k = 0; k < P->nkf; k++) {

@@ -196,12 +196,13 @@ def ldlt_solve(H, b):
     return bool(ok), x
 
 
-def local_ba(prob: dict):
+def local_ba(prob: dict, its=(5, 10)):
     """Optimizer::LocalBundleAdjustment on the CPU oracle; returns
-    (kf_Tcw [nkf,4,4], pt_pos [npts,3], edge_outlier, iterations)."""
+    (kf_Tcw [nkf,4,4], pt_pos [npts,3], edge_outlier, iterations). `its` caps
+    the two optimize() calls (a force stop = fewer iterations)."""
     from gf_orb_slam_amd.optimizer import BAArrays
     arr = BAArrays(prob)
-    rc = orc().orc_local_ba(ctypes.byref(arr.problem), ctypes.byref(arr.result))
+    rc = orc().orc_local_ba_iters(ctypes.byref(arr.problem), ctypes.byref(arr.result), int(its[0]), int(its[1]))
     assert rc == 0, rc
     return arr.out()
 

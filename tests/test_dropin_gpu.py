@@ -94,3 +94,82 @@ def test_dropin_frontend_matches_oracle(tmp_path):
                             0.8, 5, ka, s3.copy())
     assert nao == nact and nact > 0
     assert np.array_equal(ka, rd("kp2mp_act.i32", np.int32))
+
+
+SEQ_BIN = os.path.join(ROOT, "tests", "cpp", "sequence_driver")
+
+
+def test_sequence_driver_built():
+    assert os.path.exists(SEQ_BIN), "run make (or __graft_entry__.build())"
+
+
+@pytest.mark.gpu
+def test_cpp_sequence_and_local_ba_through_the_abi(tmp_path):
+    """tests/cpp/sequence_driver: a C++ program that only links libgfslam
+    tracks two rendered sequences for 7 frames (bootstrap + steps from host
+    frames) and runs LocalBundleAdjustment(pKF, &mbAbortBA) free and stopped;
+    every step equals the CPU oracle chain running free, the local BA results
+    equal the oracle (iterations capped at (1, 0) for the stopped call)."""
+    import oracle_chain as C
+    from gf_orb_slam_amd import scene
+
+    B, F, M, nfeat, budget = 2, 8, 1500, 1000, 100
+    W = scene.Workload("euroc", B, n_scenes=2, period=32, seed=6, tex_size=256)
+    fr = W.render_all("cpu").numpy()
+    maps = W.build_maps(lambda im: O.extract(im), M)
+    T, V = W.boot_state()
+    w, h, fx, fy, cx, cy = W.cam
+    frames = np.stack([np.stack([fr[W.scene_of[b], (W.phase[b] + k) % W.period] for b in range(B)])
+                       for k in range(F)])
+    frames.tofile(tmp_path / "frames.u8")
+    mp = np.zeros((B, M), maps[0][0].dtype)
+    md = np.zeros((B, M, 32), np.uint8)
+    nmp = np.zeros(B, np.int32)
+    for b in range(B):
+        m, d = maps[W.scene_of[b]]
+        mp[b, :len(m)], md[b, :len(m)], nmp[b] = m, d, len(m)
+    mp.tofile(tmp_path / "maps.bin")
+    md.tofile(tmp_path / "maps_desc.bin")
+    nmp.tofile(tmp_path / "nmp.i32")
+    np.concatenate([T.reshape(-1), V.reshape(-1)]).astype(np.float32).tofile(tmp_path / "boot.f32")
+    with open(tmp_path / "params.txt", "w") as f:
+        f.write(f"{w} {h} {fx} {fy} {cx} {cy} {nfeat} {B} {M} {budget} {F}\n")
+    p = synth.synth_lba_problem(21, 12, 1500)
+    np.array([len(p["kf_kind"]), len(p["pt_pos"]), len(p["edge_pt"])], np.int32).tofile(tmp_path / "ba_sizes.i32")
+    for k, name in (("kf_Tcw", "kf_Tcw"), ("kf_kind", "kf_kind"), ("kf_cam", "kf_cam"), ("pt_pos", "pt_pos"),
+                    ("edge_pt", "edge_pt"), ("edge_kf", "edge_kf"), ("edge_z", "edge_z"),
+                    ("edge_inv_sigma2", "edge_is2")):
+        np.ascontiguousarray(p[k]).tofile(tmp_path / f"ba_{name}.bin")
+    r = subprocess.run([SEQ_BIN, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+
+    chains = []
+    for b in range(B):
+        ch = C.Chain("euroc", nfeat, M, budget)
+        ch.set_map(*maps[W.scene_of[b]])
+        ch.set_rng(1 + b)
+        ch.bootstrap(frames[0, b], T[b], V[b])
+        chains.append(ch)
+    cap = chains[0].cap
+    kp2mp = np.fromfile(tmp_path / "seq_kp2mp.i32", np.int32).reshape(F - 1, B, cap)
+    tcw = np.fromfile(tmp_path / "seq_tcw.f32", np.float32).reshape(F - 1, B, 16)
+    for k in range(1, F):
+        for b in range(B):
+            chains[b].step(frames[k, b])
+            assert np.array_equal(kp2mp[k - 1, b], chains[b].read("kp2mp")), (k, b)
+            To = chains[b].read("Tcw").astype(np.float64)
+            assert np.all(np.abs(tcw[k - 1, b] - To) <= 1e-5 * np.maximum(1, np.abs(To))), (k, b)
+
+    def _lba(tag):
+        nkf, npts = len(p["kf_kind"]), len(p["pt_pos"])
+        return (np.fromfile(tmp_path / f"lba_{tag}_T.f32", np.float32).reshape(nkf, 4, 4),
+                np.fromfile(tmp_path / f"lba_{tag}_X.f32", np.float32).reshape(npts, 3),
+                np.fromfile(tmp_path / f"lba_{tag}_out.u8", np.uint8),
+                np.fromfile(tmp_path / f"lba_{tag}_it.i32", np.int32))
+
+    for tag, its in (("free", (5, 10)), ("stop", (1, 0))):
+        Tg, Xg, og, ig = _lba(tag)
+        To, Xo, oo, io = O.local_ba(p, its=its)
+        assert list(ig) == list(io) and np.array_equal(og, oo), tag
+        assert np.all(np.abs(Tg - To) <= 1e-5 * np.maximum(1, np.abs(To))), tag
+        assert np.all(np.abs(Xg - Xo) <= 1e-5 * np.maximum(1, np.abs(Xo))), tag
