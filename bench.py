@@ -234,6 +234,8 @@ def main():
     ap.add_argument("--batch", type=int, default=768, help="independent sequences per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="stream groups per GPU, each a front end on its own HIP stream (their kernels overlap)")
+    ap.add_argument("--no-gate", action="store_true",
+                    help="let the groups' extraction stages overlap (default: chained, one at a time)")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
@@ -271,7 +273,7 @@ def main():
     from gf_orb_slam_amd.bow import ORBVocabulary
     from gf_orb_slam_amd.dist import GfDist, checksum, share_world
     from gf_orb_slam_amd.orb import Context
-    from gf_orb_slam_amd.pipeline import STATS, FrontEnd
+    from gf_orb_slam_amd.pipeline import STATS, FrontEnd, chain_extraction
 
     cam = args.camera
     B, G = args.batch, max(1, args.groups)
@@ -308,6 +310,7 @@ def main():
         fe.set_source(frames, W.scene_of[sl], W.phase[sl])
         fe.bootstrap(T[sl], V[sl], 0.0)
         fes.append(fe)
+    gates = [] if args.no_gate else chain_extraction(fes)
     map_span = gd.gather_ints(map_cks)
     torch.cuda.synchronize()
     t_su = time.perf_counter() - t_su
@@ -416,6 +419,7 @@ def main():
                                f"SearchReferencePointsInFrustum branch, PoseOptimization, motion update, next-frame "
                                f"MAP_INFO prediction, SearchAdditionalMatchesInFrame",
                    "sequences_per_gpu": B, "stream_groups": G,
+                   "extraction_gate": bool(gates),
                    "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
         "startup": startup,
         "roofline": roof,
@@ -433,7 +437,8 @@ def main():
         "extraction_stage": {"ms_per_frame": round(ext_ms / (B * args.steps), 5),
                              "algorithmic_GBps": round(ext_bw, 2) if ext_bw else None},
         "kernels_note": f"HIP events per launch over the timed region; each launch covers one group ({Bg} sequences)"
-                        f" and the {G} groups' launches overlap, so ms_per_step sums exceed the wall time per step",
+                        f" and the {G} groups' launches overlap (extraction stages chained one group at a time"
+                        f" when extraction_gate), so ms_per_step sums exceed the wall time per step",
         "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1],
                         "ms_per_step": round(v[0] / args.steps, 4)} for k, v in prof.items()},
     }

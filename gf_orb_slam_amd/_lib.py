@@ -146,6 +146,9 @@ _PROTOS = {
     "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
+    "gf_frontend_set_gate": [_P, _P, _P],
+    "gf_event_create": [_P, _P],
+    "gf_event_destroy": [_P],
     "gf_frontend_bootstrap_host": [_P, _P, _P, _P, _D],
     "gf_frontend_step_host": [_P, _P],
     "gf_frontend_capture": [_P],

@@ -46,6 +46,7 @@ __constant__ int c_umax[16];
 struct LevelGeom {
     int nlevels;
     int w[GF_MAX_LEVELS], h[GF_MAX_LEVELS];
+    int pw[GF_MAX_LEVELS];          // row pitch of the blurred / score planes (64-B multiple)
     long long off[GF_MAX_LEVELS];   // pyramid slab offset (levels >= 1)
     long long boff[GF_MAX_LEVELS];  // blurred slab offset (all levels)
     long long slab, bslab;          // bytes per frame
@@ -140,27 +141,25 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
     __syncthreads();
     // thread: column X0 + (tid & 63), rows Y0 + 4 (tid >> 6) .. +3 (a wave stores 64 consecutive bytes)
     if (x > xl) return;
-    const int sx = xt.x, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
-    const bool two = sx + 1 < sw;
+    // at sx = sw - 1 the table holds a0 = 2048, a1 = 0 (fx clamped to 0), so the
+    // second tap (an in-allocation LDS byte past the span) weighs nothing
+    const int sx = xt.x - cs, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
+    uint8_t* dp = D + (long long)yb * dw + x;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int y = yb + i;
-        if (y > yl) break;
+    for (int i = 0; i < 4; i++, dp += dw) {
+        if (yb + i > yl) break;
         const int2 yt = yts[i];
         const int r0 = min(max(yt.x, 0), sh - 1) - rs, r1 = min(max(yt.x + 1, 0), sh - 1) - rs;
         const int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
-        const uint8_t* s0 = src + r0 * pitch + rsh[r0] + (sx - cs);
-        const uint8_t* s1 = src + r1 * pitch + rsh[r1] + (sx - cs);
-        int t0, t1;
-        if (two) {
-            t0 = s0[0] * a0 + s0[1] * a1;
-            t1 = s1[0] * a0 + s1[1] * a1;
-        } else {
-            t0 = s0[0] * 2048;
-            t1 = s1[0] * 2048;
-        }
-        const int v = (((b0 * (t0 >> 4)) >> 16) + ((b1 * (t1 >> 4)) >> 16) + 2) >> 2;
-        D[(long long)y * dw + x] = (uint8_t)min(max(v, 0), 255);
+        // the two taps of a row from two aligned LDS dwords (a byte pair at an
+        // odd address would become one misaligned ds_read_u16, a slow path)
+        const int o0 = r0 * pitch + rsh[r0] + sx, o1 = r1 * pitch + rsh[r1] + sx;
+        const uint32_t p0 = __builtin_amdgcn_alignbyte(rs_lds[(o0 >> 2) + 1], rs_lds[o0 >> 2], o0 & 3);
+        const uint32_t p1 = __builtin_amdgcn_alignbyte(rs_lds[(o1 >> 2) + 1], rs_lds[o1 >> 2], o1 & 3);
+        const int t0 = __mul24((int)(p0 & 0xff), a0) + __mul24((int)((p0 >> 8) & 0xff), a1);
+        const int t1 = __mul24((int)(p1 & 0xff), a0) + __mul24((int)((p1 >> 8) & 0xff), a1);
+        const int v = ((__mul24(b0, t0 >> 4) >> 16) + (__mul24(b1, t1 >> 4) >> 16) + 2) >> 2;
+        *dp = (uint8_t)min(max(v, 0), 255);
     }
 }
 
@@ -185,81 +184,36 @@ __device__ __forceinline__ void circle_vals(const uint8_t* roi, int rw, int px, 
     c[15] = p[3 * rw - 1];
 }
 
-// Segment test (>= 9 contiguous darker/brighter by more than th) and, for a
-// corner, OpenCV cornerScore<16>. Returns 0x100 | score, or 0.
-__device__ int fast_score(int v, const int c[16], int th) {
-    unsigned dark = 0, bright = 0;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        dark |= (unsigned)(c[k] < v - th) << k;
-        bright |= (unsigned)(c[k] > v + th) << k;
-    }
-    // 9 contiguous set bits on the 16-ring: AND of 9 rotations.
-    unsigned d2 = dark | (dark << 16), b2 = bright | (bright << 16);
-    unsigned dm = d2, bm = b2;
-#pragma unroll
-    for (int s = 1; s < 9; s++) {
-        dm &= d2 >> s;
-        bm &= b2 >> s;
-    }
-    if (((dm | bm) & 0xffff) == 0) return 0;
-    int d[25];
-#pragma unroll
-    for (int k = 0; k < 25; k++) d[k] = v - c[k & 15];
-    int a0 = th;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int a = min(min(d[k + 1], d[k + 2]), d[k + 3]);
-        if (a <= a0) continue;
-        a = min(a, d[k + 4]);
-        a = min(a, d[k + 5]);
-        a = min(a, d[k + 6]);
-        a = min(a, d[k + 7]);
-        a = min(a, d[k + 8]);
-        a0 = max(a0, min(a, d[k]));
-        a0 = max(a0, min(a, d[k + 9]));
-    }
-    int b0 = -a0;
-#pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        int b = max(max(d[k + 1], d[k + 2]), d[k + 3]);
-        b = max(b, d[k + 4]);
-        b = max(b, d[k + 5]);
-        if (b >= b0) continue;
-        b = max(b, d[k + 6]);
-        b = max(b, d[k + 7]);
-        b = max(b, d[k + 8]);
-        b0 = min(b0, max(b, d[k]));
-        b0 = min(b0, max(b, d[k + 9]));
-    }
-    return 0x100 | ((-b0 - 1) & 0xff);
-}
-
-// The same test and score in closed form, branch-free on packed 16-bit pairs.
-// With d_k = v - c_k, OpenCV's cornerScore<16> returns
+// FAST-9 segment test and OpenCV cornerScore<16> in closed form, branch-free
+// on packed 16-bit pairs. With d_k = v - c_k, cornerScore returns
 // max(th, D, B) - 1 where D = max over the 16 arcs of 9 of min_arc d and
 // B = max over arcs of min_arc (-d) (its early-outs only skip arcs that cannot
 // raise the maximum), and the segment test at th passes exactly when
 // max(D, B) > th. So M = max(D, B) gives both: corner iff M > th, score
-// M - 1. (d, -d) share one register; the 9-wide circular minimum is
-// min(m8[k], d[k+8]) with m8 built by doubling (v_pk_min_i16 / v_pk_max_i16).
+// M - 1. (d, -d) share one register. The arcs starting at 2i and 2i + 1 share
+// the 8 values 2i + 1 .. 2i + 8, built by doubling over odd starts only
+// (8 + 8 + 8 v_pk_min_i16), then each pair of arcs costs 2 mins and 2 maxes.
 typedef short gf_s2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int fast_max_arc(int v, const int c[16]) {
-    gf_s2 p[16], m2[16], m4[16], m8[16];
+    const gf_s2 vn = {(short)v, (short)-v}, sgn = {-1, 1};
+    gf_s2 p[16], m2[8], m4[8], m8[8];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        p[k].x = (short)(v - c[k]);
-        p[k].y = (short)(c[k] - v);
+        const gf_s2 cc = {(short)c[k], (short)c[k]};
+        p[k] = cc * sgn + vn;  // (v - c, c - v): one v_pk_mad_i16
     }
 #pragma unroll
-    for (int k = 0; k < 16; k++) m2[k] = __builtin_elementwise_min(p[k], p[(k + 1) & 15]);
+    for (int i = 0; i < 8; i++) m2[i] = __builtin_elementwise_min(p[2 * i + 1], p[(2 * i + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 2) & 15]);
+    for (int i = 0; i < 8; i++) m4[i] = __builtin_elementwise_min(m2[i], m2[(i + 1) & 7]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) m8[k] = __builtin_elementwise_min(m4[k], m4[(k + 4) & 15]);
-    gf_s2 mx = __builtin_elementwise_min(m8[0], p[8]);
+    for (int i = 0; i < 8; i++) m8[i] = __builtin_elementwise_min(m4[i], m4[(i + 2) & 7]);
+    gf_s2 mx = __builtin_elementwise_min(p[0], m8[0]);
 #pragma unroll
-    for (int k = 1; k < 16; k++) mx = __builtin_elementwise_max(mx, __builtin_elementwise_min(m8[k], p[(k + 8) & 15]));
+    for (int i = 0; i < 8; i++) {
+        if (i) mx = __builtin_elementwise_max(mx, __builtin_elementwise_min(p[2 * i], m8[i]));
+        mx = __builtin_elementwise_max(mx, __builtin_elementwise_min(m8[i], p[(2 * i + 9) & 15]));
+    }
     return max((int)mx.x, (int)mx.y);
 }
 
@@ -286,101 +240,106 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 // in LDS once and used twice:
 //   * GaussianBlur 7x7 sigma 2 (reflect-101 border; ORBextractor.cc:842):
 //     integer row pass, column pass with the (s + 2^15) >> 16 cast;
-//   * the FAST-9 score map of the unblurred level at the lower of the two
-//     thresholds (:621, :626): S + 1 (S = cornerScore<16> <= 254) for a
-//     pixel that passes the segment test, else 0 (and 0 within 3 px of the
-//     level border).
-//     cornerScore does not depend on the threshold once the test passes, and
-//     a pixel is a corner at th >= the map's threshold iff S >= th, so the
-//     cells run both the fast_th pass and the min_th retry, NMS included,
-//     from this one map (k_fast_cells). Every pixel gets the 4-point
-//     compass test only; the few that pass are compacted into an LDS list and
-//     the full segment test + cornerScore runs on that list, so whole waves do
-//     it (a divergent ~250-op branch per lane otherwise).
+//   * the FAST-9 score map of the unblurred level at iniThFAST (:621):
+//     S + 1 (S = cornerScore<16> <= 254) for a pixel that passes the segment
+//     test, else 0 (and 0 within 3 px of the level border). The cells run
+//     their fast_th pass, NMS included, from this map; the rare cell that
+//     retries at minThFAST (:623-628) recomputes its window from the level
+//     (k_fast_cells).
 // LDS column j of the source tile holds x = X0 - 4 + j, so the tile's rows are
-// whole dwords: x-interior tiles load them as aligned global dwords realigned
-// with v_alignbyte (two loads per dword, all in flight together); border
-// tiles load bytes through reflect-101. The row pass makes four outputs from
+// whole dwords, loaded as aligned global dwords realigned with v_alignbyte
+// (two loads per dword, all in flight together); only the dwords at the
+// level's left and right edges load bytes through reflect-101. The row pass makes four outputs from
 // three LDS dwords with v_dot4_u32_u8 (two per output: the 7 taps are bytes).
-// Thread t then owns column t & 63 and rows BT_RPT (t >> 6) .. +BT_RPT-1 for
-// the column pass, the compass test and the stores.
+// Thread t then owns the pixel quad x = X0 + 4 (t & 15) .. +3 in rows
+// 2 (t >> 4) and +1: one ds_read_b128 per row sum row for the column pass
+// (the taps sum to 257, so the rounded value saturates at 255 as
+// saturate_cast does), one dword store per quad and row for the blurred plane, and the
+// 4-point compass pre-test on the quad at once in packed 16-bit lanes (bytes
+// 0/2 and 1/3 of the dword; the sign of c + th - v is "darker", of
+// v + th - c "brighter"). The few pixels that pass are compacted into an LDS
+// list (one workgroup scan), the full segment test + cornerScore runs on
+// that list so whole waves do it, the scores land in an LDS score tile and go
+// out as one dword per quad and row. The planes are pitched to 64 B, so a
+// quad past the level's right edge writes the row padding.
 #define BT_W 64
 #define BT_H 32
-#define BT_RPT (BT_H / 4)  // rows per thread in the column pass
 #define BT_R (BT_H + 6)   // source rows
 #define BT_SW (BT_W + 8)  // source row: 72 bytes = 18 dwords, x = X0 - 4 .. X0 + 67
 
-// Necessary condition for a 9-arc: it covers two neighbouring compass points
-// of the ring (positions 0, 4, 8, 12), both darker or both brighter.
-__device__ __forceinline__ bool fast_compass(const uint8_t* p, int rw, int th) {
-    const int v = p[0], c0 = p[3 * rw], c4 = p[3], c8 = p[-3 * rw], c12 = p[-3];
-    const bool d0 = c0 < v - th, d4 = c4 < v - th, d8 = c8 < v - th, d12 = c12 < v - th;
-    const bool b0 = c0 > v + th, b4 = c4 > v + th, b8 = c8 > v + th, b12 = c12 > v + th;
-    return (d0 && d4) || (d4 && d8) || (d8 && d12) || (d12 && d0) || (b0 && b4) || (b4 && b8) || (b8 && b12) ||
-           (b12 && b0);
+typedef short gf_i16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ gf_i16x2 as_i16x2(uint32_t v) { return __builtin_bit_cast(gf_i16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(gf_i16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// Compass pre-test of FAST-9 on two pixels packed as 16-bit lanes (values
+// 0..255): a 9-arc of the 16-ring covers two neighbouring compass points
+// (ring positions 0, 4, 8, 12), both darker or both brighter than v by more
+// than th. Returns the lanes' sign bits (bit 15: lane 0, bit 31: lane 1).
+__device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t c0, uint32_t c4, uint32_t c8, uint32_t c12,
+                                             uint32_t th2) {
+    const gf_i16x2 V = as_i16x2(v), T = as_i16x2(th2), VT = V + T;
+    const uint32_t d0 = as_u32(as_i16x2(c0) + T - V), d4 = as_u32(as_i16x2(c4) + T - V);
+    const uint32_t d8 = as_u32(as_i16x2(c8) + T - V), d12 = as_u32(as_i16x2(c12) + T - V);
+    const uint32_t b0 = as_u32(VT - as_i16x2(c0)), b4 = as_u32(VT - as_i16x2(c4));
+    const uint32_t b8 = as_u32(VT - as_i16x2(c8)), b12 = as_u32(VT - as_i16x2(c12));
+    return (((d0 | d8) & (d4 | d12)) | ((b0 | b8) & (b4 | b12))) & 0x80008000u;
 }
+
+__device__ __forceinline__ uint32_t bytes02(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c020c00u); }
+__device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
     __shared__ __align__(16) uint8_t src[BT_R][BT_SW];
-    __shared__ int rows[BT_R][BT_W];
+    __shared__ __align__(16) int rows[BT_R][BT_W];
+    __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
     __shared__ uint16_t cand[BT_W * BT_H];
-    __shared__ int s_nc;
+    __shared__ int scan_tmp[4];
     const int f = blockIdx.y, tid = threadIdx.x;
     int t = blockIdx.x, l = 0;
 #pragma unroll
     for (int i = 1; i < GF_MAX_LEVELS; i++) l += (i < g.nlevels && t >= g.tile_begin[i]) ? 1 : 0;
     t -= g.tile_begin[l];
     const int tx = t % g.tiles_x[l], ty = t / g.tiles_x[l];
-    const int w = g.w[l], h = g.h[l];
+    const int w = g.w[l], h = g.h[l], pw = g.pw[l];
     const int X0 = tx * BT_W, Y0 = ty * BT_H;
     int stride;
     const uint8_t* S = level_plane(P, g, f, l, stride);
-    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l];
-    uint8_t* SC = score + (long long)f * g.bslab + g.boff[l];
-    if (tid == 0) s_nc = 0;
-    if (X0 >= 4 && X0 + BT_SW <= w) {
-        // 22 rows x 18 dwords; rows reflect-101 at the top and bottom
+    {
+        // 38 rows x 18 dwords; rows reflect-101 at the top and bottom. A dword
+        // inside the level row (with the next 4 bytes: the realignment's second
+        // load) comes as aligned loads; the x-border ones byte by byte through
+        // reflect-101.
         constexpr int NT = BT_R * (BT_SW / 4), NI = (NT + 255) / 256;
         uint32_t lo[NI], hi[NI];
         int sh[NI];
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int i = tid + 256 * k;
+            lo[k] = hi[k] = 0u;
+            sh[k] = 0;
             if (i < NT) {
                 const int ry = i / (BT_SW / 4), q = i - ry * (BT_SW / 4);
                 const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                const uintptr_t a = (uintptr_t)(S + (long long)yy * stride + X0 - 4 + 4 * q);
-                const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-                sh[k] = (int)(a & 3);
-                lo[k] = al[0];
-                hi[k] = sh[k] ? al[1] : 0u;  // al[1] holds needed bytes whenever sh != 0
+                const int x0 = X0 - 4 + 4 * q;
+                const uint8_t* row = S + (long long)yy * stride;
+                if (x0 >= 0 && x0 + 8 <= w) {
+                    const uintptr_t a = (uintptr_t)(row + x0);
+                    const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+                    sh[k] = (int)(a & 3);
+                    lo[k] = al[0];
+                    hi[k] = sh[k] ? al[1] : 0u;  // al[1] holds needed bytes whenever sh != 0
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        lo[k] |= (uint32_t)row[gfd::reflect101(min(x0 + j, w + 2), w)] << (8 * j);
+                }
             }
         }
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int i = tid + 256 * k;
             if (i < NT) reinterpret_cast<uint32_t*>(&src[0][0])[i] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
-        }
-    } else {
-        constexpr int NSRC = BT_R * (BT_W + 6), NLD = (NSRC + 255) / 256;
-        uint8_t v[NLD];
-#pragma unroll
-        for (int k = 0; k < NLD; k++) {
-            const int i = tid + 256 * k;
-            if (i < NSRC) {
-                const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
-                const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                const int xx = gfd::reflect101(min(X0 + rx - 3, w + 2), w);
-                v[k] = S[(long long)yy * stride + xx];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NLD; k++) {
-            const int i = tid + 256 * k;
-            if (i < NSRC) {
-                const int ry = i / (BT_W + 6), rx = i - ry * (BT_W + 6);
-                src[ry][rx + 1] = v[k];
-            }
         }
     }
     __syncthreads();
@@ -401,37 +360,67 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         *reinterpret_cast<int4*>(&rows[ry][4 * q]) = o;
     }
     __syncthreads();
-    const int cx = tid & 63, ry0 = (tid >> 6) * BT_RPT, x = X0 + cx;
-    int rv[BT_RPT + 6];
+    const int qx = tid & 15, r0 = 2 * (tid >> 4), x = X0 + 4 * qx;
+    // column pass: rows r0 .. r0 + 7 of the row sums give output rows r0, r0 + 1
+    int4 rs[8];
 #pragma unroll
-    for (int k = 0; k < BT_RPT + 6; k++) rv[k] = rows[ry0 + k][cx];
-    // row pointers advanced by w per row (no 64-bit multiply per store); the
-    // taps fit 24-bit multiplies (row sums < 2^17), which issue at full rate
-    const long long o0 = (long long)(Y0 + ry0) * w + x;
-    uint8_t* dp = D + o0;
-    uint8_t* sp = SC + o0;
+    for (int k = 0; k < 8; k++) rs[k] = *reinterpret_cast<const int4*>(&rows[r0 + k][4 * qx]);
+    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
 #pragma unroll
-    for (int r = 0; r < BT_RPT; r++, dp += w, sp += w) {
-        const int y = Y0 + ry0 + r;
-        if (y >= h || x >= w) continue;
-        const unsigned sum = __umul24(18u, (unsigned)(rv[r] + rv[r + 6])) + __umul24(34u, (unsigned)(rv[r + 1] + rv[r + 5])) +
-                             __umul24(49u, (unsigned)(rv[r + 2] + rv[r + 4])) + __umul24(55u, (unsigned)rv[r + 3]);
-        *dp = (uint8_t)min((sum + (1u << 15)) >> 16, 255u);
-        const bool cand_px = x >= 3 && x < w - 3 && y >= 3 && y < h - 3 &&
-                             fast_compass(&src[ry0 + r + 3][cx + 4], BT_SW, map_th);
-        if (cand_px)
-            cand[atomicAdd(&s_nc, 1)] = (uint16_t)((ry0 + r) * BT_W + cx);
-        else
-            *sp = 0;
+    for (int r = 0; r < 2; r++) {
+        auto col = [&](int a0, int a1, int a2, int a3, int a4, int a5, int a6) -> uint32_t {
+            return min((__umul24(18u, (unsigned)(a0 + a6)) + __umul24(34u, (unsigned)(a1 + a5)) +
+                        __umul24(49u, (unsigned)(a2 + a4)) + __umul24(55u, (unsigned)a3) + (1u << 15)) >> 16,
+                       255u);
+        };
+        const uint32_t o0 = col(rs[r].x, rs[r + 1].x, rs[r + 2].x, rs[r + 3].x, rs[r + 4].x, rs[r + 5].x, rs[r + 6].x);
+        const uint32_t o1 = col(rs[r].y, rs[r + 1].y, rs[r + 2].y, rs[r + 3].y, rs[r + 4].y, rs[r + 5].y, rs[r + 6].y);
+        const uint32_t o2 = col(rs[r].z, rs[r + 1].z, rs[r + 2].z, rs[r + 3].z, rs[r + 4].z, rs[r + 5].z, rs[r + 6].z);
+        const uint32_t o3 = col(rs[r].w, rs[r + 1].w, rs[r + 2].w, rs[r + 3].w, rs[r + 4].w, rs[r + 5].w, rs[r + 6].w);
+        if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(D + (long long)r * pw) = o0 | o1 << 8 | o2 << 16 | o3 << 24;
+    }
+    // compass pre-test of the quad in rows r0, r0 + 1 (LDS rows r0 + 3, r0 + 4)
+    const uint32_t th2 = (uint32_t)map_th * 0x00010001u;
+    uint32_t xm = 0;  // pixels of the quad at least 3 px inside the level, in x
+#pragma unroll
+    for (int i = 0; i < 4; i++) xm |= (uint32_t)(x + i >= 3 && x + i < w - 3) << i;
+    int mask = 0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(&src[r0 + r + 3][0]) + qx;
+        const uint32_t L = c32[0], V = c32[1], R = c32[2];
+        const uint32_t U = reinterpret_cast<const uint32_t*>(&src[r0 + r][0])[qx + 1];      // dy = -3 (ring 8)
+        const uint32_t Dn = reinterpret_cast<const uint32_t*>(&src[r0 + r + 6][0])[qx + 1];  // dy = +3 (ring 0)
+        const uint32_t Rt = __builtin_amdgcn_alignbyte(R, V, 3), Lt = __builtin_amdgcn_alignbyte(V, L, 1);
+        const uint32_t e = compass2(bytes02(V), bytes02(Dn), bytes02(Rt), bytes02(U), bytes02(Lt), th2);
+        const uint32_t o = compass2(bytes13(V), bytes13(Dn), bytes13(Rt), bytes13(U), bytes13(Lt), th2);
+        uint32_t m = ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
+        const int y = Y0 + r0 + r;
+        m &= (y >= 3 && y < h - 3) ? xm : 0u;
+        mask |= (int)m << (4 * r);
+        sco[r0 + r][qx] = 0u;
+    }
+    int nc;
+    int pos = block_scan_256(__popc(mask), scan_tmp, nc);  // its barriers also order the sco zeroing
+    while (mask) {
+        const int b = __ffs(mask) - 1;
+        mask &= mask - 1;
+        cand[pos++] = (uint16_t)((r0 + (b >> 2)) * BT_W + 4 * qx + (b & 3));
     }
     __syncthreads();
-    for (int i = tid; i < s_nc; i += 256) {
+    uint8_t* sc8 = reinterpret_cast<uint8_t*>(&sco[0][0]);
+    for (int i = tid; i < nc; i += 256) {
         const int q = cand[i], py = q >> 6, px = q & 63;
         int c[16];
         circle_vals(&src[0][0], BT_SW, px + 4, py + 3, c);
         const int M = fast_max_arc(src[py + 3][px + 4], c);  // corner iff M > th; map entry S + 1 = M
-        SC[(long long)(Y0 + py) * w + X0 + px] = M > map_th ? (uint8_t)M : 0;
+        sc8[q] = M > map_th ? (uint8_t)M : 0;
     }
+    __syncthreads();
+    uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+        if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(SC + (long long)r * pw) = sco[r0 + r][qx];
 }
 
 // -------------------------------------------------------------- k_fast_cells
@@ -440,7 +429,8 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 // fast_th survive strict 3x3 non-maximum suppression inside the window
 // (neighbours outside it or not corners count 0, as in FAST's row buffers)
 // and are listed in row-major order. When at most 3 survive (:623-628) the
-// same map is suppressed again at min_th and the list rewritten.
+// window's map is recomputed at min_th from the unblurred level (the ROI's
+// pixels, staged in LDS), suppressed again and the list rewritten.
 // NMS: wave w walks rows [w dh/4, (w+1) dh/4) of each 64-column strip, lane =
 // column, keeping the three rows it compares in registers (three LDS reads a
 // pixel); survivors set their bit in an LDS bit array (bit = row-major pixel
@@ -491,7 +481,7 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
     return cnt;  // this wave's survivors
 }
 
-__global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* __restrict__ score,
+__global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
                                                     const CellInfo* __restrict__ cells, uint32_t* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
@@ -510,7 +500,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
     uint8_t* sc = smem;                                                   // dh x pitch
     uint8_t* rsh = sc + dh * pitch;                                        // dh row shifts
     uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 15) & ~15));  // survivor bits
-    const int l = ci.level, lw = g.w[l];
+    const int l = ci.level, lw = g.pw[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
     // the window as aligned dwords, 16 loads per thread in flight before the LDS writes
     for (int i0 = 0; i0 < dh * ndw; i0 += 256 * 16) {
@@ -539,7 +529,22 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
     __syncthreads();
     int total = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
     if (total <= 3) {  // ORBextractor.cc:623-628: retry with the minimum threshold
+        // the ROI (window + 3-px ring margin) of the unblurred level to LDS
+        uint8_t* roi = reinterpret_cast<uint8_t*>(bits + ((nwords + 3) & ~3));
+        int sstride;
+        const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
+        for (int i = tid; i < ci.w * ci.h; i += 256) {
+            const int r = i / ci.w;
+            roi[i] = Sl[(long long)r * sstride + (i - r * ci.w)];
+        }
         __syncthreads();
+        for (int i = tid; i < n; i += 256) {
+            const int y = i / dw, x = i - y * dw;
+            int c[16];
+            circle_vals(roi, ci.w, x + 3, y + 3, c);
+            const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
+            sc[y * pitch + rsh[y] + x] = M > min_th ? (uint8_t)M : 0;
+        }
         for (int i = tid; i < nwords; i += 256) bits[i] = 0;
         __syncthreads();
         c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, min_th);
@@ -568,15 +573,136 @@ __global__ __launch_bounds__(256) void k_fast_cells(LevelGeom g, const uint8_t* 
 }
 
 // -------------------------------------------------------------- k_select
-// One workgroup per (level, frame).
+// One workgroup per (level, frame). KeyPointsFilter::retainBest is
+// std::nth_element (libstdc++ __introselect: median-of-three pivot, unguarded
+// Hoare partition, heap_select past the depth limit, insertion sort below 4),
+// and the keypoint order it leaves is what every later stage sees, so each
+// selection replays it exactly — one wave per list, the list in LDS:
+//   * the pivot choice, the depth bookkeeping and the small-range insertion
+//     sort run on lane 0 (O(1) per round);
+//   * the partition runs on all 64 lanes. __unguarded_partition swaps the k-th
+//     element from the left that is not better than the pivot with the k-th
+//     element from the right that is not worse, for every k while the left
+//     one lies before the right one (the swapped elements act as sentinels, so
+//     the scans never see a swapped position before that condition fails);
+//     it returns min(L_k*, R_{k*-1}) for the first failing k*. The two
+//     stopper position lists come from ballots over 64-element windows, k*
+//     from one more ballot pass (L_k < R_k is monotone in k), the swaps are
+//     disjoint.
+// Lists longer than the LDS buffer fall back to the sequential replay on
+// global memory (gfsel::retain_best_truncate, same result).
 #define SEL_MAX_CELLS 1024
+#define SEL_BUF 1024  // entries per wave
+struct SelWave {
+    uint32_t a[SEL_BUF];
+    uint16_t lp[SEL_BUF], rp[SEL_BUF];
+};
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int sel_resp(uint32_t e) { return (int)(e >> 24); }
+
+// __unguarded_partition(a + lo, a + hi, a + pivot) with KeypointResponseGreater.
+__device__ int wave_partition(SelWave& W, int lo, int hi, int P) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int nL = 0, nR = 0;
+    for (int i0 = 0; i0 < hi - lo; i0 += 64) {
+        const int i = lo + i0 + lane, j = hi - 1 - i0 - lane;
+        const bool sl = i < hi && !(sel_resp(W.a[i]) > P);  // left scan stops: not better than the pivot
+        const bool sr = j >= lo && !(P > sel_resp(W.a[j]));  // right scan stops: not worse
+        const unsigned long long bl = __ballot(sl), br = __ballot(sr);
+        if (sl) W.lp[nL + __popcll(bl & lt)] = (uint16_t)i;
+        if (sr) W.rp[nR + __popcll(br & lt)] = (uint16_t)j;
+        nL += __popcll(bl);
+        nR += __popcll(br);
+    }
+    wave_sync();
+    const int m = min(nL, nR);
+    int ks = 0;
+    for (int k0 = 0; k0 < m; k0 += 64) {
+        const int k = k0 + lane;
+        const unsigned long long ok = __ballot(k < m && W.lp[k] < W.rp[k]);
+        ks += __popcll(ok);
+        if (~ok & ((k0 + 64 <= m) ? ~0ull : ((1ull << (m - k0)) - 1ull))) break;  // monotone: done
+    }
+    for (int k = lane; k < ks; k += 64) {
+        const int x = W.lp[k], y = W.rp[k];
+        const uint32_t ax = W.a[x], ay = W.a[y];
+        W.a[x] = ay;
+        W.a[y] = ax;
+    }
+    const int Lk = ks < nL ? (int)W.lp[ks] : hi;
+    const int Rk = ks > 0 ? (int)W.rp[ks - 1] : hi;
+    wave_sync();
+    return min(Lk, Rk);
+}
+
+// std::nth_element(a, a + nth, a + n) on the wave's LDS list, all lanes.
+__device__ void wave_nth_element(SelWave& W, int nth, int n) {
+    const int lane = threadIdx.x & 63;
+    const gfsel::RespGreater comp;
+    if (n == 0 || nth == n) return;
+    int first = 0, last = n;
+    int depth = 2 * gfsel::lg_(n);
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (lane == 0) {
+                gfsel::heap_select(W.a, first, nth + 1, last, comp);
+                gfsel::swap_(W.a[first], W.a[nth]);
+            }
+            wave_sync();
+            return;
+        }
+        --depth;
+        const int mid = first + (last - first) / 2;
+        if (lane == 0) gfsel::move_median_to_first(W.a, first, first + 1, mid, last - 1, comp);
+        wave_sync();
+        const int cut = wave_partition(W, first + 1, last, sel_resp(W.a[first]));
+        if (cut <= nth)
+            first = cut;
+        else
+            last = cut;
+    }
+    if (lane == 0) gfsel::insertion_sort(W.a, first, last, comp);
+    wave_sync();
+}
+
+// retainBest(list, keep) + truncation, written to dst[0 .. keep): one wave.
+__device__ void wave_retain_to(SelWave& W, uint32_t* list, int n, int keep, uint32_t* dst) {
+    const int lane = threadIdx.x & 63;
+    if (keep <= 0) return;
+    if (n <= keep) {
+        for (int i = lane; i < n; i += 64) dst[i] = list[i];
+        return;
+    }
+    if (n > SEL_BUF) {  // sequential replay on global memory
+        if (lane == 0) gfsel::retain_best_truncate(list, n, keep, gfsel::RespGreater());
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int i = lane; i < keep; i += 64) dst[i] = list[i];
+        return;
+    }
+    for (int i = lane; i < n; i += 64) W.a[i] = list[i];
+    wave_sync();
+    wave_nth_element(W, keep - 1, n);
+    for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
+}
+
 __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
                                                 uint32_t* __restrict__ lists, long long list_stride,
                                                 const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
                                                 long long lvl_stride, int* __restrict__ lvl_counts) {
     __shared__ int cnt[SEL_MAX_CELLS], keep[SEL_MAX_CELLS], off[SEL_MAX_CELLS + 1];
     __shared__ char valid[SEL_MAX_CELLS];
-    const int l = blockIdx.x, f = blockIdx.y;
+    extern __shared__ __align__(16) uint8_t sel_dyn[];
+    const int l = blockIdx.x, f = blockIdx.y, wv = threadIdx.x >> 6;
+    SelWave& W = reinterpret_cast<SelWave*>(sel_dyn)[wv];
     const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb;
     for (int c = threadIdx.x; c < nc; c += blockDim.x) {
         cnt[c] = counts[(long long)f * g.ncells + cb + c];
@@ -618,15 +744,7 @@ __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __r
                 }
             }
         }
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
-        if (!valid[c]) continue;
-        uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
-        keep[c] = gfsel::retain_best_truncate(a, cnt[c], keep[c], gfsel::RespGreater());
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
+        // keep[c] <= cnt[c], so retainBest leaves exactly keep[c] per cell (:734-736)
         int s = 0;
         for (int c = 0; c < nc; c++) {
             off[c] = s;
@@ -636,16 +754,24 @@ __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __r
     }
     __syncthreads();
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
-    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+    for (int c = wv; c < nc; c += 4) {
         if (!valid[c]) continue;
-        const uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
-        for (int i = 0; i < keep[c]; i++) L[off[c] + i] = a[i];
+        uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int total = off[nc];
-        total = gfsel::retain_best_truncate(L, total, g.ndesired[l], gfsel::RespGreater());
-        lvl_counts[(long long)f * g.nlevels + l] = total;
+    if (wv == 0) {  // the level's retainBest (:750-752)
+        const int total = off[nc], nd = g.ndesired[l];
+        if (nd >= 0 && total > nd && nd > 0 && total <= SEL_BUF) {
+            for (int i = threadIdx.x; i < total; i += 64) W.a[i] = L[i];
+            wave_sync();
+            wave_nth_element(W, nd - 1, total);
+            for (int i = threadIdx.x; i < nd; i += 64) L[i] = W.a[i];
+        } else if (threadIdx.x == 0) {
+            gfsel::retain_best_truncate(L, total, nd, gfsel::RespGreater());
+        }
+        if (threadIdx.x == 0)
+            lvl_counts[(long long)f * g.nlevels + l] = (nd < 0 || total <= nd) ? total : nd;
     }
 }
 
@@ -724,7 +850,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     const int lv = live ? l : 0;
     const uint32_t e = live ? lvl_lists[(long long)f * lvl_stride + g.lvl_off[lv] + idx] : 0u;
     const int x = e & 0xfff, y = (e >> 12) & 0xfff, score = e >> 24;
-    const int w = g.w[lv], h = g.h[lv];
+    const int w = g.w[lv], h = g.h[lv], pwl = g.pw[lv];
     int stride;
     const uint8_t* Pl = level_plane(P, g, f, lv, stride);
     const uint8_t* B = P.blur + (long long)f * g.bslab + g.boff[lv];
@@ -743,7 +869,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                 v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
             } else if (win && i >= DS_IC * DS_ICW && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
                 const int j = i - DS_IC * DS_ICW, r = j / DS_BLW, q = j - r * DS_BLW;
-                const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * w + x - 18);
+                const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * pwl + x - 18);
                 v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
             }
         }
@@ -754,9 +880,9 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             else if (i < DS_IC * DS_ICW + DS_BL * DS_BLW) W.bl[i - DS_IC * DS_ICW] = v[t];
         }
         if (hl < DS_IC) W.ic_sh[hl] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + hl) * stride + x - 15) & 3);
-        W.bl_sh[hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + hl) * w + x - 18) & 3);
+        W.bl_sh[hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + hl) * pwl + x - 18) & 3);
         if (hl < DS_BL - 32)
-            W.bl_sh[32 + hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + 32 + hl) * w + x - 18) & 3);
+            W.bl_sh[32 + hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + 32 + hl) * pwl + x - 18) & 3);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -805,7 +931,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                     const int xx = x + rx, yy = y + ry;
                     const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
                     t[q] = !live ? 0
-                           : inside ? B[(long long)yy * w + xx]
+                           : inside ? B[(long long)yy * pwl + xx]
                                     : Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
                 }
             }
@@ -892,6 +1018,7 @@ static int plan_extractor(gf_extractor* ex) {
     for (int l = 0; l < nl; l++) {
         g.w[l] = cv_round_f((float)ex->width * inv[l]);
         g.h[l] = cv_round_f((float)ex->height * inv[l]);
+        g.pw[l] = (g.w[l] + 63) & ~63;
         g.scale[l] = scale[l];
         GF_CHECK(g.w[l] >= 40 && g.h[l] >= 40 && g.w[l] < 4096 && g.h[l] < 4096, GF_ERR_ARG,
                  "level size out of supported range");
@@ -900,7 +1027,7 @@ static int plan_extractor(gf_extractor* ex) {
             off += ((long long)g.w[l] * g.h[l] + 255) & ~255LL;
         }
         g.boff[l] = boff;
-        boff += ((long long)g.w[l] * g.h[l] + 255) & ~255LL;
+        boff += ((long long)g.pw[l] * g.h[l] + 255) & ~255LL;
     }
     g.slab = off;
     g.bslab = boff;
@@ -974,7 +1101,7 @@ static int plan_extractor(gf_extractor* ex) {
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
                         size_t lds = (size_t)dh * (4 * (size_t)((dw + 6) / 4)) + (((size_t)dh + 15) & ~(size_t)15) +
-                                     4 * (((size_t)dw * dh + 31) / 32);
+                                     16 * (((size_t)dw * dh + 127) / 128) + (size_t)ci.w * ci.h;
                         max_lds = std::max(max_lds, lds);
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
                                  GF_ERR_ARG, "cell ROI outside level");
@@ -1137,7 +1264,7 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
             ex->rs_rows[l] = maxrows;
             ex->rs_tiles_x[l] = (dw + RS_W - 1) / RS_W;
             ex->rs_tiles[l] = ex->rs_tiles_x[l] * ((dh + RS_H - 1) / RS_H);
-            const size_t lds = (size_t)ex->rs_pitch[l] * maxrows + maxrows;
+            const size_t lds = (size_t)ex->rs_pitch[l] * maxrows + maxrows + 8;
             if (lds > 64 * 1024) {
                 free_extractor(ex);
                 delete ex;
@@ -1217,7 +1344,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     {
         GF_PROF(ctx, s, "k_resize");
         for (int l = 1; l < ex->nlevels; l++) {
-            const size_t lds = (size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l];
+            const size_t lds = (size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l] + 8;
             k_resize<<<dim3(ex->rs_tiles[l], nframes), 256, lds, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l],
                                                                       ex->d_ytab + ex->ytab_off[l], ex->rs_tiles_x[l],
                                                                       ex->rs_pitch[l], ex->rs_rows[l]);
@@ -1225,16 +1352,16 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     }
     {
         GF_PROF(ctx, s, "k_blur_fast");
-        k_blur_fast<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g, ex->d_score, std::min(ex->fast_th, ex->min_th));
+        k_blur_fast<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g, ex->d_score, ex->fast_th);
     }
     {
         GF_PROF(ctx, s, "k_fast_cells");
         k_fast_cells<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(
-            g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
+            P, g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
     }
     {
         GF_PROF(ctx, s, "k_select");
-        k_select<<<dim3(ex->nlevels, nframes), 256, 0, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+        k_select<<<dim3(ex->nlevels, nframes), 256, 4 * sizeof(SelWave), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }
@@ -1285,8 +1412,8 @@ int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, 
     GF_HIP(hipSetDevice(ex->ctx->device));
     GF_HIP(hipStreamSynchronize(ex->ctx->stream));
     if (which == 1) {
-        GF_HIP(hipMemcpy(out, ex->d_blur + (long long)frame * g.bslab + g.boff[level], (size_t)g.w[level] * g.h[level],
-                         hipMemcpyDeviceToHost));
+        GF_HIP(hipMemcpy2D(out, g.w[level], ex->d_blur + (long long)frame * g.bslab + g.boff[level], g.pw[level],
+                           g.w[level], g.h[level], hipMemcpyDeviceToHost));
     } else if (level == 0) {
         GF_CHECK(ex->last.img0 || ex->last.ptrs, GF_ERR_ARG, "no batch run yet");
         if (ex->last.ptrs) {

@@ -354,6 +354,8 @@ struct gf_frontend {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     bool sourced = false;
+    // extraction gate (gf_frontend_set_gate): caller-owned events
+    hipEvent_t gate_wait = nullptr, gate_done = nullptr;
 };
 
 namespace {
@@ -406,8 +408,10 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         k_fe_begin<<<B, 256, 0, s>>>(D);
         GF_HIP(hipGetLastError());
     }
+    if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
+    if (fe->gate_done) GF_HIP(hipEventRecord(fe->gate_done, s));
     // TrackWithMotionModel
     FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
                                  D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp, D.score,
@@ -741,6 +745,28 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
     k_fe_boot_end<<<B, 256, 0, s>>>(D);
     GF_HIP(hipGetLastError());
     GF_HIP(hipStreamSynchronize(s));
+    return GF_OK;
+}
+
+int gf_event_create(gf_ctx* ctx, void** out) {
+    GF_CHECK(ctx && out, GF_ERR_ARG, "null arg");
+    GF_HIP(hipSetDevice(ctx->device));
+    hipEvent_t e = nullptr;
+    GF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = (void*)e;
+    return GF_OK;
+}
+
+int gf_event_destroy(void* ev) {
+    if (ev) GF_HIP(hipEventDestroy((hipEvent_t)ev));
+    return GF_OK;
+}
+
+int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set the gate before capturing a graph");
+    fe->gate_wait = (hipEvent_t)wait_event;
+    fe->gate_done = (hipEvent_t)done_event;
     return GF_OK;
 }
 

@@ -92,6 +92,34 @@ def field_shape(name: str, B: int, cap: int, M: int):
     return fid, dt, (B,) + tuple(cap if s == "cap" else M if s == "M" else s for s in shp)
 
 
+class GateEvent:
+    """A hipEvent_t for gf_frontend_set_gate (gf_event_create)."""
+
+    def __init__(self, ctx: Context):
+        h = ctypes.c_void_p()
+        check(lib().gf_event_create(ctx.handle, ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        try:
+            lib().gf_event_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def chain_extraction(fes: list) -> list:
+    """Gate the front ends' extraction stages into a ring: front end g waits
+    for g - 1's extraction (g = 0 for the last one's, previous step), so the
+    bandwidth-bound stages run one at a time and each front end's tracking
+    overlaps the next one's extraction. Returns the events."""
+    if len(fes) < 2:
+        return []
+    evs = [GateEvent(fe.ctx) for fe in fes]
+    for g, fe in enumerate(fes):
+        fe.set_gate(evs[g - 1], evs[g])
+    return evs
+
+
 class FrontEnd:
     """B independent streams, one frame each per step."""
 
@@ -162,6 +190,13 @@ class FrontEnd:
 
     def capture_graph(self) -> None:
         check(lib().gf_frontend_capture(self.handle))
+
+    def set_gate(self, wait_event, done_event) -> None:
+        """gf_frontend_set_gate: wait for `wait_event` before extraction,
+        record `done_event` after it (GateEvent or None)."""
+        self._gate = (wait_event, done_event)  # keep the events alive
+        check(lib().gf_frontend_set_gate(self.handle, wait_event.handle if wait_event else None,
+                                         done_event.handle if done_event else None))
 
     def sync(self) -> None:
         check(lib().gf_frontend_sync(self.handle))

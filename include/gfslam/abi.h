@@ -754,6 +754,18 @@ typedef struct gf_frontend_params {
 } gf_frontend_params;
 typedef struct gf_frontend gf_frontend;
 
+// Extraction gate for several front ends sharing one GPU: before its
+// extraction kernels a step waits for `wait_event` (a hipEvent_t; NULL: no
+// wait), after them it records `done_event` (NULL: none). Chaining front end
+// g's done event into front end g+1's wait event serialises the
+// bandwidth-bound extraction stages while each front end's tracking kernels
+// overlap the next one's extraction. Events stay owned by the caller.
+// Not part of a captured graph (set before gf_frontend_capture).
+int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event);
+// A hipEvent_t (timing disabled) on the context's device, for the gate.
+int gf_event_create(gf_ctx* ctx, void** event_out);
+int gf_event_destroy(void* event);
+
 /* Per-stream state and outputs, readable / writable as whole-batch arrays. */
 enum {
     GF_FE_KPS = 0,      /* [B][cap] gf_keypoint  mCurrentFrame.mvKeysUn      */

@@ -1,7 +1,8 @@
 """Local BA on the device: wall time per solve for B copies of config 4 (diagnostic)."""
-import sys, time
-sys.path.insert(0, '.')
-sys.path.insert(0, 'tests')
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
 import numpy as np
 from gf_orb_slam_amd.optimizer import LocalBAPlan
 from gf_orb_slam_amd.synth import synth_lba_problem

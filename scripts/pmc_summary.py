@@ -11,7 +11,7 @@ import sys
 root = sys.argv[1]
 want = sys.argv[2:]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
     per = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
         name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"]).split("(")[0]
