@@ -1,14 +1,17 @@
 // Motion-only pose optimisation on gfx950.
 //
-// One 64-lane wave per problem (frame). Per-edge work — projection, error,
-// Huber weight, the 2x6 pose Jacobian and its 27 contributions to the lower
-// triangle of H and to b — runs one edge per lane; the reductions over edges
-// keep the reference's order: lane k of the wave owns accumulator k (21 lower
-// H entries, 6 b entries, robust chi2) and adds the per-edge terms staged in
-// LDS in edge order, exactly as g2o's sequential loop over _activeEdges
+// One 256-thread workgroup per problem (frame). Per-edge work — projection,
+// error, Huber weight, the 2x6 pose Jacobian and its 27 contributions to the
+// lower triangle of H and to b — runs one edge per thread, 256 edges at a time
+// (a frame's ~200 matches in one pass); the reductions over edges keep the
+// reference's order: thread k owns accumulator k (21 lower H entries, 6 b
+// entries, robust chi2) and adds the per-edge terms staged in LDS in edge
+// order, exactly as g2o's sequential loop over _activeEdges
 // (sparse_optimizer.cpp:100-114, block_solver.hpp:502-562). The scalar LM
 // logic (lambda schedule, LDLT, exp update, stop rules) runs redundantly on
-// every lane from the shared sums, so no broadcast is needed.
+// every thread from the shared sums, so no broadcast is needed. The problem
+// is latency-bound (one workgroup per frame, an ordered double-precision sum
+// chain per LM pass), so the edge work is spread over four waves.
 //
 // Reference: Optimizer::PoseOptimization src/Optimizer.cc:279-413,
 // OptimizationAlgorithmLevenberg::solve core/optimization_algorithm_levenberg.cpp:61-189,
@@ -21,10 +24,12 @@ namespace {
 
 constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
 constexpr int PO_CHI = 27;
-constexpr int PO_SPEC = 4;                     // LM trials evaluated together (see k_pose_opt)
-constexpr int PO_ROWS = PO_CHI + PO_SPEC;      // term rows: H, b, one chi2 row per speculative trial
+constexpr int PO_SPEC = 4;   // LM trials evaluated together (see k_pose_opt)
+constexpr int PO_ROWS = PO_CHI + PO_SPEC;  // term rows: H, b, one chi2 row per trial
+constexpr int PO_T = 256;    // threads per problem = edges per pass
+constexpr int PO_TP = PO_T + 1;  // term row pitch (doubles): accumulator threads read distinct banks
 constexpr int PO_STRIDE_MAX = 8192;
-constexpr int PO_LDS_EDGES = 512;  // problems up to this size keep edges and residuals in LDS (40 KB in all)
+constexpr int PO_LDS_EDGES = 384;  // problems up to this size keep edges and residuals in LDS (18 KB)
 
 struct PoseArgs {
     const gf_pose_edge* edges;
@@ -44,7 +49,7 @@ struct PoseArgs {
 
 struct Lane {
     const gf_pose_edge* E;
-    double *e0, *e1, *info;
+    double* info;
     int n, l;
     double fx, fy, cx, cy, delta, dsqr;
 };
@@ -72,16 +77,15 @@ __device__ __forceinline__ void edge_error(const Lane& L, const gfse3::SE3& T, i
 
 // computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
 // Returns the sums in sh_sum: [0,21) lower H row-major-packed, [21,27) b, 27 chi2.
-__device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[65], double* sh_sum) {
+__device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[PO_TP],
+                                     double* sh_sum) {
     // (build: the H/b rows too; the chi2 row is PO_CHI)
     double acc = 0.0;
-    for (int base = 0; base < L.n; base += 64) {
+    for (int base = 0; base < L.n; base += PO_T) {
         const int e = base + L.l;
         if (e < L.n) {
             double pc[3], r0, r1;
             edge_error(L, T, e, pc, r0, r1);
-            L.e0[e] = r0;
-            L.e1[e] = r1;
             const double info = L.info[e];
             const double chi2 = r0 * (info * r0) + r1 * (info * r1);
             double rho0, rho1;
@@ -114,7 +118,7 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
             }
         }
         __syncthreads();
-        const int m = min(64, L.n - base);
+        const int m = min(PO_T, L.n - base);
         if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
             // edge order, one dependent add per edge; loads batched ahead of the chain
             const double* row = term[L.l];
@@ -134,14 +138,16 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
     __syncthreads();
 }
 
-// computeActiveErrors + activeRobustChi2 at S trial estimates at once: lane
-// PO_CHI + s adds trial s's robust chi2 terms in edge order. The stored
-// residuals are not touched (the caller re-evaluates the estimate that was
-// evaluated last, as g2o's edges keep it, before the outlier pass).
-__device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[65],
+// computeActiveErrors + activeRobustChi2 at S trial estimates at once, and
+// buildSystem at trial 0's: lane PO_CHI + s adds trial s's robust chi2 terms
+// in edge order, lanes 0..26 trial 0's H and b terms. When trial 0 is
+// accepted (most LM iterations) the next iteration's linearisation is
+// already in sh_sum — the same arithmetic g2o's next computeActiveErrors +
+// buildSystem at that estimate performs.
+__device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[PO_TP],
                                             double* sh_sum) {
     double acc = 0.0;
-    for (int base = 0; base < L.n; base += 64) {
+    for (int base = 0; base < L.n; base += PO_T) {
         const int e = base + L.l;
         if (e < L.n) {
             const double info = L.info[e];
@@ -154,11 +160,36 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
                 double rho0, rho1;
                 robustify(chi2, L.delta, L.dsqr, rho0, rho1);
                 term[PO_CHI + s][L.l] = rho0;
+                if (s == 0) {
+                    const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
+                    double J0[6], J1[6];
+                    J0[0] = x * y / z2 * L.fx;
+                    J0[1] = -(1 + (x * x / z2)) * L.fx;
+                    J0[2] = y / z * L.fx;
+                    J0[3] = -1. / z * L.fx;
+                    J0[4] = 0;
+                    J0[5] = x / z2 * L.fx;
+                    J1[0] = (1 + y * y / z2) * L.fy;
+                    J1[1] = -x * y / z2 * L.fy;
+                    J1[2] = -x / z * L.fy;
+                    J1[3] = 0;
+                    J1[4] = -1. / z * L.fy;
+                    J1[5] = y / z2 * L.fy;
+                    const double w = rho1 * info;
+                    const double o0 = -(info * r0) * rho1, o1 = -(info * r1) * rho1;
+                    int k = 0;
+#pragma unroll
+                    for (int a = 0; a < 6; a++)
+#pragma unroll
+                        for (int b = 0; b <= a; b++) term[k++][L.l] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
+#pragma unroll
+                    for (int a = 0; a < 6; a++) term[21 + a][L.l] = J0[a] * o0 + J1[a] * o1;
+                }
             }
         }
         __syncthreads();
-        const int m = min(64, L.n - base);
-        if (L.l >= PO_CHI && L.l < PO_CHI + S) {
+        const int m = min(PO_T, L.n - base);
+        if (L.l < PO_CHI + S) {
             const double* row = term[L.l];
             int j = 0;
             for (; j + 8 <= m; j += 8) {
@@ -172,24 +203,12 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
         }
         __syncthreads();
     }
-    if (L.l >= PO_CHI && L.l < PO_CHI + S) sh_sum[L.l] = acc;
+    if (L.l < PO_CHI + S) sh_sum[L.l] = acc;
     __syncthreads();
 }
 
-// residuals of the non-flagged edges at T (the estimate g2o evaluated last)
-__device__ __forceinline__ void store_errors(const Lane& L, const gfse3::SE3& T, const uint8_t* ou) {
-    for (int e = L.l; e < L.n; e += 64) {
-        if (ou[e]) continue;
-        double pc[3], r0, r1;
-        edge_error(L, T, e, pc, r0, r1);
-        L.e0[e] = r0;
-        L.e1[e] = r1;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
-    __shared__ double term[PO_ROWS][65];
+__global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
+    __shared__ double term[PO_ROWS][PO_TP];
     __shared__ double sh_sum[PO_ROWS];
     __shared__ double sh_x[PO_SPEC][6];       // each speculative trial's solution
     __shared__ int sh_ok[PO_SPEC];
@@ -197,24 +216,20 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
     // every pass re-reads each edge and its residuals: for problems up to
     // PO_LDS_EDGES edges they live in LDS (generic pointers), else in HBM
     __shared__ gf_pose_edge sh_edges[PO_LDS_EDGES];
-    __shared__ double sh_res[3][PO_LDS_EDGES];
+    __shared__ double sh_info[PO_LDS_EDGES];
     const int p = blockIdx.x;
     Lane L;
     L.l = threadIdx.x;
     L.n = min(max(A.nedges[p], 0), A.stride);
     if (L.n <= PO_LDS_EDGES) {
         const gf_pose_edge* src = A.edges + (size_t)p * A.stride;
-        for (int e = L.l; e < L.n; e += 64) sh_edges[e] = src[e];
+        for (int e = L.l; e < L.n; e += PO_T) sh_edges[e] = src[e];
         L.E = sh_edges;
-        L.e0 = sh_res[0];
-        L.e1 = sh_res[1];
-        L.info = sh_res[2];
+        L.info = sh_info;
         __syncthreads();
     } else {
         L.E = A.edges + (size_t)p * A.stride;
-        L.e0 = A.work + (size_t)p * A.stride * 3;
-        L.e1 = L.e0 + A.stride;
-        L.info = L.e1 + A.stride;
+        L.info = A.work + (size_t)p * A.stride;
     }
     L.fx = A.fx;
     L.fy = A.fy;
@@ -235,9 +250,8 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
         for (int i = 0; i < 3; i++) T.t[i] = (double)Tp[4 * i + 3];
         gfse3::normalize(T.r);
     }
-    for (int e = L.l; e < L.n; e += 64) {
+    for (int e = L.l; e < L.n; e += PO_T) {
         L.info[e] = (double)L.E[e].inv_sigma2;
-        L.e0[e] = L.e1[e] = 0.0;
         ou[e] = 0;
     }
     __syncthreads();
@@ -252,9 +266,11 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
         // SparseOptimizer::optimize(its) with the Levenberg algorithm
         double lambda = 0, ni = 2;
         int nBad = 0;
+        bool have_build = false;  // sh_sum already holds H, b, chi2 at T (trial 0 accepted)
         for (int iter = 0; iter < its; iter++) {
             total_it++;
-            pass(L, T, true, term, sh_sum);
+            if (!have_build) pass(L, T, true, term, sh_sum);
+            have_build = false;
             double H[36], b[6];
             for (int a = 0, k = 0; a < 6; a++)
                 for (int c = 0; c <= a; c++, k++) H[6 * a + c] = H[6 * c + a] = sh_sum[k];
@@ -289,7 +305,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                     ni_s[s2] = ni_s[s2 - 1] * 2;
                 }
                 {
-                    const int g = L.l >> 4;  // this lane's trial
+                    const int g = (L.l & 63) >> 4;  // this lane's trial (every wave computes all four)
                     double lam_g = lam_s[0];
 #pragma unroll
                     for (int s2 = 1; s2 < PO_SPEC; s2++)
@@ -299,7 +315,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                     for (int j = 0; j < 6; j++) Hl[7 * j] += lam_g;
                     double xn[6];
                     const bool ok = gfse3::ldlt6(Hl, b, xn);
-                    if ((L.l & 15) == 0) {
+                    if (L.l < 64 && (L.l & 15) == 0) {
                         sh_ok[g] = ok;
                         for (int j = 0; j < 6; j++) sh_x[g][j] = xn[j];
                     }
@@ -309,7 +325,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                 // trial g solves with the last successful x among trials <= g
                 {
                     const int g = L.l >> 4;
-                    if ((L.l & 15) == 0 && g < S) {
+                    if (L.l < 64 && (L.l & 15) == 0 && g < S) {
                         double xg[6];
                         for (int j = 0; j < 6; j++) xg[j] = xs[j];
                         for (int s2 = 0; s2 <= g; s2++)
@@ -341,6 +357,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                         ni = 2;
                         currentChi = tempChi;
                         T = sh_T[s2];
+                        have_build = s2 == 0;
                     } else {
                         lambda = lam_s[s2] * ni_s[s2];
                         ni = ni_s[s2] * 2;
@@ -361,20 +378,19 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
         // outlier classification (Optimizer.cc:373-395); errors are those of
         // the last evaluated estimate, recomputed at the current one for
         // flagged edges.
-        store_errors(L, last_eval, ou);
         int nb = 0;
-        for (int base = 0; base < L.n; base += 64) {
+        for (int base = 0; base < L.n; base += PO_T) {
             const int e = base + L.l;
             bool bad = false;
             if (e < L.n) {
+                double pc[3], r0, r1;
                 if (ou[e]) {
                     L.info[e] = (double)L.E[e].inv_sigma2;
-                    double pc[3], r0, r1;
                     edge_error(L, T, e, pc, r0, r1);
-                    L.e0[e] = r0;
-                    L.e1[e] = r1;
+                } else {
+                    edge_error(L, last_eval, e, pc, r0, r1);
                 }
-                const double r0 = L.e0[e], r1 = L.e1[e], info = L.info[e];
+                const double info = L.info[e];
                 const double c2 = r0 * (info * r0) + r1 * (info * r1);
                 if (c2 > chi2th) {
                     ou[e] = 1;
@@ -384,7 +400,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
                     ou[e] = 0;
                 }
             }
-            nb += __popcll(__ballot(bad));
+            nb += __syncthreads_count(bad);
         }
         nBadEdges = nb;
         __syncthreads();
@@ -406,7 +422,7 @@ __global__ __launch_bounds__(64) void k_pose_opt(PoseArgs A) {
         if (A.iters) A.iters[p] = total_it;
     }
     if (A.kp_outl)
-        for (int e = L.l; e < L.n; e += 64)
+        for (int e = L.l; e < L.n; e += PO_T)
             A.kp_outl[(size_t)p * A.kp_stride + A.edge_kp[(size_t)p * A.stride + e]] = ou[e];
 }
 
@@ -458,7 +474,7 @@ __global__ __launch_bounds__(64) void k_pose_gather(GatherArgs G) {
 
 int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
     GF_PROF(ctx, s, "k_pose_opt");
-    k_pose_opt<<<nprob, 64, 0, s>>>(A);
+    k_pose_opt<<<nprob, PO_T, 0, s>>>(A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -78,11 +78,7 @@ void rng_seed(gf_rng* r, uint32_t s) {
 
 void mat44(const float* a, const float* b, float* o) {
     for (int i = 0; i < 4; i++)
-        for (int j = 0; j < 4; j++) {
-            float s = a[4 * i] * b[j];
-            for (int k = 1; k < 4; k++) s = s + a[4 * i + k] * b[4 * k + j];
-            o[4 * i + j] = s;
-        }
+        for (int j = 0; j < 4; j++) o[4 * i + j] = orc::dot4(a + 4 * i, 1, b + j, 4);
 }
 
 // Frame::getTwc (Frame.cc:152-163) and LastTwc (Tracking.cc:731-735):
@@ -91,8 +87,7 @@ void twc_of(const float* T, float* W) {
     for (int i = 0; i < 16; i++) W[i] = (i % 5 == 0) ? 1.f : 0.f;
     for (int i = 0; i < 3; i++) {
         for (int j = 0; j < 3; j++) W[4 * i + j] = T[4 * j + i];
-        const float a = -T[i] * T[3], b = -T[4 + i] * T[7], c = -T[8 + i] * T[11];
-        W[4 * i + 3] = (a + b) + c;
+        W[4 * i + 3] = orc::dot3(-T[i], T[3], -T[4 + i], T[7], -T[8 + i], T[11]);
     }
 }
 

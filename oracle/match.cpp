@@ -123,19 +123,20 @@ void three_maxima(const int* histo, int L, int& ind1, int& ind2, int& ind3) {
 // Pc = R * P + t, float, left-to-right, no contraction (cv::Mat
 // float gemm restated).
 static inline void transform(const float* T, const float* P, float* Pc) {
-    for (int r = 0; r < 3; r++) {
-        float a = T[4 * r + 0] * P[0];
-        float b = T[4 * r + 1] * P[1];
-        float c = T[4 * r + 2] * P[2];
-        Pc[r] = ((a + b) + c) + T[4 * r + 3];
-    }
+    for (int r = 0; r < 3; r++)
+        Pc[r] = dot3p(T[4 * r + 0], P[0], T[4 * r + 1], P[1], T[4 * r + 2], P[2], T[4 * r + 3]);
 }
+
+int g_gemm_mode = 0;
 
 }  // namespace orc
 
 extern "C" {
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return orc::descriptor_distance(a, b); }
+
+// docs/ORACLE_ASSUMPTIONS.md A1 (sensitivity runs only; 0 = parity)
+void orc_set_gemm_mode(int mode) { orc::g_gemm_mode = mode; }
 
 // Frame::isInFrustum, Frame.cc:166-227
 int orc_frustum(const gf_frame_info* fi, const float* Tcw, const gf_map_point* mps, int m, float viewCosLimit,
@@ -145,10 +146,7 @@ int orc_frustum(const gf_frame_info* fi, const float* Tcw, const gf_map_point* m
     for (int i = 1; i < fi->nlevels; i++) scales[i] = scales[i - 1] * fi->scale_factor;
     // Ow = -Rcw^T * tcw (Frame::UpdatePoseMatrices :143-148)
     float Ow[3];
-    for (int c = 0; c < 3; c++) {
-        float a = Tcw[0 * 4 + c] * Tcw[3], b = Tcw[1 * 4 + c] * Tcw[7], d = Tcw[2 * 4 + c] * Tcw[11];
-        Ow[c] = -((a + b) + d);
-    }
+    for (int c = 0; c < 3; c++) Ow[c] = -orc::dot3(Tcw[0 * 4 + c], Tcw[3], Tcw[1 * 4 + c], Tcw[7], Tcw[2 * 4 + c], Tcw[11]);
     int cnt = 0;
     for (int i = 0; i < m; i++) {
         gf_mp_view& v = views[i];

@@ -35,6 +35,37 @@
 
 namespace orc {
 
+// Accumulation order of the reference's small cv::Mat float products
+// (Rcw*x3Dw+tcw, V*LastTcw, Tcw*LastTwc, -Rcw^T*tcw). docs/ORACLE_ASSUMPTIONS.md
+// A1: 0 = float products, float left-to-right sums (the parity setting, what
+// the device does); 1 = products and sums in double, one rounding to float
+// (cv::gemm's generic GEMMSingleMul<float,double> path); 2 = fused
+// multiply-adds left to right. Modes 1 and 2 exist only for
+// scripts/oracle_sensitivity.py (orc_set_gemm_mode).
+extern int g_gemm_mode;
+inline float dot3(float a0, float b0, float a1, float b1, float a2, float b2) {
+    if (g_gemm_mode == 1) return (float)((double)a0 * b0 + (double)a1 * b1 + (double)a2 * b2);
+    if (g_gemm_mode == 2) return std::fma(a2, b2, std::fma(a1, b1, a0 * b0));
+    const float x = a0 * b0, y = a1 * b1, z = a2 * b2;
+    return (x + y) + z;
+}
+inline float dot3p(float a0, float b0, float a1, float b1, float a2, float b2, float t) {
+    if (g_gemm_mode == 1) return (float)((double)a0 * b0 + (double)a1 * b1 + (double)a2 * b2 + (double)t);
+    if (g_gemm_mode == 2) return std::fma(a2, b2, std::fma(a1, b1, a0 * b0)) + t;
+    const float x = a0 * b0, y = a1 * b1, z = a2 * b2;
+    return ((x + y) + z) + t;
+}
+inline float dot4(const float* a, int sa, const float* b, int sb) {
+    if (g_gemm_mode == 1) {
+        double s = 0;
+        for (int k = 0; k < 4; k++) s += (double)a[k * sa] * b[k * sb];
+        return (float)s;
+    }
+    float s = a[0] * b[0];
+    for (int k = 1; k < 4; k++) s = g_gemm_mode == 2 ? std::fma(a[k * sa], b[k * sb], s) : s + a[k * sa] * b[k * sb];
+    return s;
+}
+
 // cvRound for float/double: round half to even (lrint under the default mode).
 static inline int cv_round(float v) { return (int)std::lrint(v); }
 static inline int cv_round(double v) { return (int)std::lrint(v); }
