@@ -76,6 +76,20 @@ struct ProfScope {
 // Device-side helpers ------------------------------------------------------
 namespace gfd {
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1, bijective form):
+// the dispatcher hands consecutive workgroups to the 8 XCDs in turn, so
+// neighbouring tiles — which share halo rows and cache lines — would land in
+// 8 different L2s. This maps the 2-D grid's linear id so that each group of
+// workgroups sharing an XCD gets one contiguous run of the logical
+// (x fastest, then y) order. Speed only: any placement is correct.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+    const int nwg = (int)(gridDim.x * gridDim.y), id = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int q = nwg >> 3, r = nwg & 7, x = id & 7, slot = id >> 3;
+    const int lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + slot;
+    by = lid / (int)gridDim.x;
+    bx = lid - by * (int)gridDim.x;
+}
+
 __device__ __forceinline__ int reflect101(int p, int len) {
     // BORDER_REFLECT_101 for the <= 18 px excursions the kernels make.
     if (p < 0) p = -p;

@@ -100,8 +100,10 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
     extern __shared__ __align__(16) uint32_t rs_lds[];
     uint8_t* src = reinterpret_cast<uint8_t*>(rs_lds);
     uint8_t* rsh = src + (size_t)pitch * max_rows;  // byte offset of each row's first needed column
-    const int f = blockIdx.y, tid = threadIdx.x;
-    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    int bx, f;
+    gfd::xcd_block(bx, f);
+    const int tid = threadIdx.x;
+    const int tx = bx % tiles_x, ty = bx / tiles_x;
     const int dw = g.w[l], dh = g.h[l], sw = g.w[l - 1], sh = g.h[l - 1];
     const int X0 = tx * RS_W, Y0 = ty * RS_H;
     const int xl = min(X0 + RS_W - 1, dw - 1), yl = min(Y0 + RS_H - 1, dh - 1);
@@ -295,8 +297,10 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
     __shared__ uint16_t cand[BT_W * BT_H];
     __shared__ int scan_tmp[4];
-    const int f = blockIdx.y, tid = threadIdx.x;
-    int t = blockIdx.x, l = 0;
+    int t, f;
+    gfd::xcd_block(t, f);
+    const int tid = threadIdx.x;
+    int l = 0;
 #pragma unroll
     for (int i = 1; i < GF_MAX_LEVELS; i++) l += (i < g.nlevels && t >= g.tile_begin[i]) ? 1 : 0;
     t -= g.tile_begin[l];
@@ -488,7 +492,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ int s_cnt[2][4];
     __shared__ int scan_tmp[4];
-    const int f = blockIdx.y, cid = blockIdx.x, tid = threadIdx.x;
+    int cid, f;
+    gfd::xcd_block(cid, f);
+    const int tid = threadIdx.x;
     const CellInfo ci = cells[cid];
     const int dw = ci.w - 6, dh = ci.h - 6;
     if (!ci.valid || dw <= 0 || dh <= 0) {  // degenerate ROI: FAST finds nothing
@@ -828,10 +834,11 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
     __shared__ DescLds sh_all[8];
-    const int f = blockIdx.y;
+    int bx, f;
+    gfd::xcd_block(bx, f);
     const int lane = threadIdx.x & 63, hl = lane & 31, half = (threadIdx.x >> 5);  // half = slot 0..7
     DescLds& W = sh_all[half];
-    const int k = blockIdx.x * 8 + half;
+    const int k = bx * 8 + half;
     int cnt[GF_MAX_LEVELS];  // all level counts in one batch of loads
 #pragma unroll
     for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = i < g.nlevels ? lvl_counts[(long long)f * g.nlevels + i] : 0;
