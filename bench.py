@@ -197,6 +197,13 @@ def lba_leg(batch: int, repeats: int = 3, cpu: bool = True) -> dict:
             entry["schur_gemm"] = {"bound": "mfma", "achieved": round(tf, 4), "peak": 78.6, "unit": "TFLOP/s",
                                    "frac": round(tf / 78.6, 6), "algorithmic_flops_per_launch": flops,
                                    "note": "f64 MFMA 16x16x4; peak = AMD spec FP64 matrix (not measured here)"}
+            try:
+                pm = json.load(open(os.path.join(ROOT, "profiles", "r02", "pmc_lba_mfma.json")))
+                if pm.get("batch") == B:
+                    entry["schur_gemm"]["mfma_busy_pmc"] = round(pm["mfma_busy_fraction"], 5)
+                    entry["schur_gemm"]["mfma_busy_source"] = "profiles/r02/pmc_lba_mfma.json"
+            except (OSError, ValueError, KeyError):
+                pass
         out["batch_%d" % B] = entry
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -146,6 +146,8 @@ _PROTOS = {
     "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
+    "gf_update_reference": [_P, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P],
+    "gf_update_reference_dev": [_P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P],
     "gf_frontend_set_gate": [_P, _P, _P],
     "gf_event_create": [_P, _P],
     "gf_event_destroy": [_P],

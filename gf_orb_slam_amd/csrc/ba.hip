@@ -574,11 +574,16 @@ __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
 
 // ------------------------------------------------------------------ reduced camera system
 // S = Hpp + lambda I - C (lower, packed in LDS), b_s = b_p - C[:, n]; inactive
-// poses decouple with x = 0. LL^T right-looking with one barrier per column,
-// the trailing matrix in registers (6x6 pose blocks per thread, see below).
-// Forward / back substitution on one wave with the values in registers,
-// broadcast by readlane, in the oracle's order.
+// poses decouple with x = 0. Blocked LL^T with one 6x6 block per pose (two
+// barriers per pose), substitutions one pose block at a time on one wave —
+// all in the oracle's operation order (see below).
 constexpr int BA_ST = 1024;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     const long long u = __double_as_longlong(v);
@@ -590,8 +595,8 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     __shared__ double sL[BA_MAXN * (BA_MAXN + 1) / 2];
     __shared__ double sb[BA_MAXN], sbp[BA_MAXN], srinv[BA_MAXN];
-    __shared__ double scol[2][BA_MAXN];  // column k of the trailing matrix (unscaled), double-buffered
     __shared__ uint8_t sact[BA_MAXFREE];
+    __shared__ double scol6[6];
     __shared__ int s_fail;
     const int p = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const BADesc d = A.desc[p];
@@ -627,162 +632,154 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     }
     __syncthreads();
     BA_STAMP(1);
-    // Right-looking LL^T with the trailing matrix in registers: thread t owns
-    // the BS x BS block (bi, bj), bi >= bj, of the packed lower triangle
-    // (<= 2080 blocks of 3 for 32 free poses: at most two per thread). At step k every owner of a
-    // trailing element subtracts (S_ik r_k)(S_jk r_k) — bit for bit the
-    // oracle's L_ik L_jk in its left-looking order — with column k read from
-    // an LDS buffer its owners filled at step k - 1 (double-buffered), and
-    // r_k = 1 / sqrt(S_kk) published by the owner of S_kk. One barrier per
-    // column; no read-modify-write of the matrix in LDS.
-    constexpr int BS = 3;  // block edge (n is a multiple of 6)
-    constexpr int NBT = 2;  // blocks per thread: 2080 blocks of 3 at n = 192
-    const int nb = n / BS, nblk = nb * (nb + 1) / 2;
-    int I0[NBT], J0[NBT];
-    bool own[NBT];
-    double R[NBT][BS][BS];
-#pragma unroll
-    for (int q = 0; q < NBT; q++) {
-        const int t = tid + q * BA_ST;
-        own[q] = t < nblk;
-        int bi = 0, bj = 0;
-        if (own[q]) {  // t -> (bi, bj): row-major over the lower block triangle
-            bi = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-            while (tri(bi + 1) <= t) bi++;
-            while (tri(bi) > t) bi--;
-            bj = t - tri(bi);
-        }
-        I0[q] = BS * bi;
-        J0[q] = BS * bj;
-#pragma unroll
-        for (int a = 0; a < BS; a++)
-#pragma unroll
-            for (int c = 0; c < BS; c++)
-                R[q][a][c] = (own[q] && J0[q] + c <= I0[q] + a) ? sL[tri(I0[q] + a) + J0[q] + c] : 0.0;
-    }
-    if (tid < n) scol[0][tid] = sL[tri(tid)];  // column 0
-    if (tid == 0) {
-        const double d0 = n > 0 ? sL[0] : 1.0;
-        s_fail = !(d0 > 0.0);
-        srinv[0] = 1.0 / sqrt(d0);
-    }
+    // Blocked LL^T, one 6x6 block per pose, in place on the packed lower
+    // triangle: per block column, (1) the diagonal block factored in registers
+    // by the waves that own panel rows (every lane the same values), (2) the
+    // panel rows below by one thread each, (3) the trailing update by the
+    // whole workgroup. Every element still sees its subtractions
+    // L_ik L_jk one at a time in ascending k and a product rounded before
+    // it is subtracted, so the factor is bit for bit the oracle's left-looking
+    // LL^T (oracle/lba.cpp) — with 2 barriers per pose instead of one per
+    // column. On exit sL holds L (scaled, j < i) and d_j on the diagonal,
+    // srinv[j] = 1 / d_j.
+    if (tid == 0) s_fail = 0;
     __syncthreads();
-    for (int k = 0; k < n; k++) {
-        if (s_fail) break;
-        const double rk = srinv[k];
-        const double* colk = scol[k & 1];
-        double* coln = scol[(k + 1) & 1];
+    for (int k0 = 0; k0 < n; k0 += 6) {
+        const int nrow = n - k0 - 6;  // panel rows below the block
+        double Db[6][6], rb[6];
+        bool ok = true;
+        if (tid < ((nrow + 63) & ~63) || (nrow == 0 && tid < 64)) {
 #pragma unroll
-        for (int q = 0; q < NBT; q++) {
-            const int i0 = I0[q], j0 = J0[q];
-            if (!own[q] || i0 + BS - 1 <= k || j0 + BS - 1 <= k) continue;  // no trailing elements
-            double li[BS], lj[BS];
+            for (int c = 0; c < 6; c++) {
+                double sv = sL[tri(k0 + c) + k0 + c];
 #pragma unroll
-            for (int a = 0; a < BS; a++) li[a] = (i0 + a > k) ? colk[i0 + a] * rk : 0.0;
+                for (int m = 0; m < c; m++) sv = sv - Db[c][m] * Db[c][m];
+                ok = ok && sv > 0.0;
+                const double dj = sqrt(sv);
+                Db[c][c] = dj;
+                rb[c] = 1.0 / dj;
 #pragma unroll
-            for (int c = 0; c < BS; c++) lj[c] = (j0 + c > k) ? colk[j0 + c] * rk : 0.0;
+                for (int a2 = c + 1; a2 < 6; a2++) {
+                    double t = sL[tri(k0 + a2) + k0 + c];
 #pragma unroll
-            for (int a = 0; a < BS; a++)
-#pragma unroll
-                for (int c = 0; c < BS; c++) {
-                    const int i = i0 + a, j = j0 + c;
-                    if (j > k && j <= i) R[q][a][c] = R[q][a][c] - li[a] * lj[c];
+                    for (int m = 0; m < c; m++) t = t - Db[a2][m] * Db[c][m];
+                    Db[a2][c] = t * rb[c];
                 }
-            // column k + 1 is final now: publish it (and its pivot)
-            const int cc = k + 1 - j0;
-            if (cc >= 0 && cc < BS) {
+            }
+            if (tid < nrow) {  // panel row i = k0 + 6 + tid
+                const int i = k0 + 6 + tid;
+                double P[6];
 #pragma unroll
-                for (int a = 0; a < BS; a++)
+                for (int c = 0; c < 6; c++) {
+                    double t = sL[tri(i) + k0 + c];
 #pragma unroll
-                    for (int c = 0; c < BS; c++)
-                        if (c == cc && i0 + a >= k + 1) {
-                            coln[i0 + a] = R[q][a][c];
-                            if (i0 + a == k + 1) {
-                                if (!(R[q][a][c] > 0.0)) s_fail = 1;
-                                srinv[k + 1] = 1.0 / sqrt(R[q][a][c]);
-                            }
-                        }
+                    for (int m = 0; m < c; m++) t = t - P[m] * Db[c][m];
+                    P[c] = t * rb[c];
+                }
+#pragma unroll
+                for (int c = 0; c < 6; c++) sL[tri(i) + k0 + c] = P[c];
             }
         }
         __syncthreads();
+        if (tid == 0) {  // the block's factor (no one reads these rows before the substitutions)
+            if (!ok) s_fail = 1;
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                srinv[k0 + c] = rb[c];
+#pragma unroll
+                for (int a2 = c; a2 < 6; a2++) sL[tri(k0 + a2) + k0 + c] = Db[a2][c];
+            }
+        }
+        // trailing update: R_ij -= L_i,k0+m L_j,k0+m, m = 0..5, for k0+6 <= j <= i
+        const int ntr = tri(nrow);
+        for (int e = tid; e < ntr; e += BA_ST) {
+            int ii = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+            while (tri(ii + 1) <= e) ii++;
+            while (tri(ii) > e) ii--;
+            const int jj = e - tri(ii), i = k0 + 6 + ii, j = k0 + 6 + jj;
+            double Rv = sL[tri(i) + j];
+#pragma unroll
+            for (int m = 0; m < 6; m++) Rv = Rv - sL[tri(i) + k0 + m] * sL[tri(j) + k0 + m];
+            sL[tri(i) + j] = Rv;
+        }
+        __syncthreads();
+        if (s_fail) break;
     }
-    // the factor back into sL, scaled: L_ij = S_ij r_j (the substitutions read it)
-    if (!s_fail) {
-#pragma unroll
-        for (int q = 0; q < NBT; q++)
-#pragma unroll
-            for (int a = 0; a < BS; a++)
-#pragma unroll
-                for (int c = 0; c < BS; c++) {
-                    const int i = I0[q] + a, j = J0[q] + c;
-                    if (own[q] && j < i) sL[tri(i) + j] = R[q][a][c] * srinv[j];
-                }
-    }
-    __syncthreads();
     const bool fail = s_fail;
     __syncthreads();
     BA_STAMP(2);
     if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 5] = __builtin_amdgcn_s_memtime();
-    if (!fail && w == 0) {  // the scaled last column needs no write-back (no entries below its diagonal)
+    if (!fail && w == 0) {
+        // Substitutions on one wave, one pose block at a time: lane l holds
+        // rows l, l + 64, l + 128 in registers; a block's 6 values go through
+        // LDS (srow) and are solved redundantly on
+        // every lane, then every row outside the block subtracts the block's
+        // 6 terms in the oracle's order (forward: ascending k; backward:
+        // descending k).
+        double* srow = scol6;
         double r[3];
         for (int u = 0; u < 3; u++) r[u] = (lane + 64 * u < n) ? sb[lane + 64 * u] : 0.0;
-        // forward: y_k = r_k / L_kk, r_i -= L_ik y_k; next step's L column and 1 / L_kk loaded ahead
-        double Ln[3], rn = n > 0 ? srinv[0] : 0.0;
+        for (int k0 = 0; k0 < n; k0 += 6) {
 #pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = lane + 64 * u;
-            Ln[u] = (i > 0 && i < n) ? sL[tri(i)] : 0.0;
-        }
-        for (int k = 0; k < n; k++) {
-            double Lc[3];
+            for (int u = 0; u < 3; u++) {
+                const int i = lane + 64 * u;
+                if (i >= k0 && i < k0 + 6) srow[i - k0] = r[u];
+            }
+            wave_lds_sync();
+            double y[6];
 #pragma unroll
-            for (int u = 0; u < 3; u++) Lc[u] = Ln[u];
-            const double rc = rn;
-            if (k + 1 < n) {
+            for (int c = 0; c < 6; c++) {
+                double sv = srow[c];
 #pragma unroll
-                for (int u = 0; u < 3; u++) {
-                    const int i = lane + 64 * u;
-                    Ln[u] = (i > k + 1 && i < n) ? sL[tri(i) + k + 1] : 0.0;
+                for (int m = 0; m < c; m++) sv = sv - sL[tri(k0 + c) + k0 + m] * y[m];
+                y[c] = sv * srinv[k0 + c];
+            }
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int i = lane + 64 * u;
+                if (i >= k0 && i < k0 + 6) {
+#pragma unroll
+                    for (int c = 0; c < 6; c++)
+                        if (i == k0 + c) r[u] = y[c];
+                } else if (i >= k0 + 6 && i < n) {
+                    double t = r[u];
+#pragma unroll
+                    for (int m = 0; m < 6; m++) t = t - sL[tri(i) + k0 + m] * y[m];
+                    r[u] = t;
                 }
-                rn = srinv[k + 1];
             }
-            const int reg = k >> 6;
-            const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
-            const double yk = readlane_d(mine, k & 63) * rc;
+            wave_lds_sync();
+        }
+        for (int k0 = n - 6; k0 >= 0; k0 -= 6) {
 #pragma unroll
-            for (int u = 0; u < 3; u++) {  // Lc = 0 off the rows below k: r - 0 * y = r
-                const double upd = r[u] - Lc[u] * yk;
-                r[u] = (lane + 64 * u == k) ? yk : upd;
+            for (int u = 0; u < 3; u++) {
+                const int i = lane + 64 * u;
+                if (i >= k0 && i < k0 + 6) srow[i - k0] = r[u];
             }
-        }
-        // backward: x_k = r_k / L_kk, r_i -= L_ki x_k (descending k); row k of L loaded ahead
-        rn = n > 0 ? srinv[n - 1] : 0.0;
+            wave_lds_sync();
+            double x[6];
 #pragma unroll
-        for (int u = 0; u < 3; u++) {
-            const int i = lane + 64 * u;
-            Ln[u] = (n > 0 && i < n - 1) ? sL[tri(n - 1) + i] : 0.0;
-        }
-        for (int k = n - 1; k >= 0; k--) {
-            double Lc[3];
+            for (int c = 5; c >= 0; c--) {
+                double sv = srow[c];
 #pragma unroll
-            for (int u = 0; u < 3; u++) Lc[u] = Ln[u];
-            const double rc = rn;
-            if (k > 0) {
+                for (int m = 5; m > c; m--) sv = sv - sL[tri(k0 + m) + k0 + c] * x[m];
+                x[c] = sv * srinv[k0 + c];
+            }
 #pragma unroll
-                for (int u = 0; u < 3; u++) {
-                    const int i = lane + 64 * u;
-                    Ln[u] = (i < k - 1) ? sL[tri(k - 1) + i] : 0.0;
+            for (int u = 0; u < 3; u++) {
+                const int i = lane + 64 * u;
+                if (i >= k0 && i < k0 + 6) {
+#pragma unroll
+                    for (int c = 0; c < 6; c++)
+                        if (i == k0 + c) r[u] = x[c];
+                } else if (i < k0) {
+                    double t = r[u];
+#pragma unroll
+                    for (int m = 5; m >= 0; m--) t = t - sL[tri(k0 + m) + i] * x[m];
+                    r[u] = t;
                 }
-                rn = srinv[k - 1];
             }
-            const int reg = k >> 6;
-            const double mine = reg == 0 ? r[0] : (reg == 1 ? r[1] : r[2]);
-            const double xk = readlane_d(mine, k & 63) * rc;
-#pragma unroll
-            for (int u = 0; u < 3; u++) {  // Lc = 0 off the rows above k
-                const double upd = r[u] - Lc[u] * xk;
-                r[u] = (lane + 64 * u == k) ? xk : upd;
-            }
+            wave_lds_sync();
         }
 #pragma unroll
         for (int u = 0; u < 3; u++)

@@ -445,3 +445,71 @@ def write_vocab_text(voc: dict, path: str) -> None:
         for i in range(1, len(voc["parent"])):
             d = " ".join(str(int(x)) for x in voc["desc"][i])
             f.write(f"{voc['parent'][i]} {int(voc['is_leaf'][i])} {d}  {float(voc['weight'][i])!r}\n")
+
+
+def synth_covis_graph(seed: int, nkf: int = 300, nmp: int = 20000, slots: int = 1000, bad_kf: float = 0.05,
+                      bad_mp: float = 0.05, span: int = 6, max_obs: int = 8) -> dict:
+    """A map for local-map assembly (localmap.CovisGraph):
+    nkf keyframes along a trajectory, each map point observed by 2..max_obs
+    keyframes within `span` of its home keyframe (one slot each, slots
+    shuffled, the rest NULL), covisibility = keyframes sharing points ordered
+    by shared count (descending, then index) as UpdateBestCovisibles does;
+    a fraction of keyframes and points is bad."""
+    rng = np.random.default_rng(seed)
+    home = np.sort(rng.integers(0, nkf, nmp))
+    obs = []
+    for m in range(nmp):
+        k = int(rng.integers(2, max_obs + 1))
+        lo, hi = max(0, home[m] - span), min(nkf, home[m] + span + 1)
+        obs.append(np.sort(rng.choice(np.arange(lo, hi), size=min(k, hi - lo), replace=False)))
+    kf_slots = [[] for _ in range(nkf)]
+    for m, o in enumerate(obs):
+        for k in o:
+            kf_slots[k].append(m)
+    kf_mp_off = [0]
+    kf_mp = []
+    for k in range(nkf):
+        s = np.full(max(slots, len(kf_slots[k])), -1, np.int32)
+        pos = rng.choice(len(s), size=len(kf_slots[k]), replace=False)
+        s[pos] = kf_slots[k]
+        kf_mp.append(s)
+        kf_mp_off.append(kf_mp_off[-1] + len(s))
+    shared = np.zeros((nkf, nkf), np.int32)
+    for o in obs:
+        for a in o:
+            for b in o:
+                if a != b:
+                    shared[a, b] += 1
+    kf_cov_off = [0]
+    kf_cov = []
+    for k in range(nkf):
+        nb = np.nonzero(shared[k] >= 15)[0]
+        nb = nb[np.lexsort((nb, -shared[k, nb]))]
+        kf_cov.append(nb.astype(np.int32))
+        kf_cov_off.append(kf_cov_off[-1] + len(nb))
+    mp_obs_off = np.concatenate([[0], np.cumsum([len(o) for o in obs])]).astype(np.int32)
+    return dict(kf_bad=(rng.random(nkf) < bad_kf).astype(np.uint8), kf_mp_off=np.array(kf_mp_off, np.int32),
+                kf_mp=np.concatenate(kf_mp) if kf_mp else np.zeros(0, np.int32),
+                kf_cov_off=np.array(kf_cov_off, np.int32),
+                kf_cov=np.concatenate(kf_cov) if kf_cov else np.zeros(0, np.int32),
+                mp_bad=(rng.random(nmp) < bad_mp).astype(np.uint8), mp_obs_off=mp_obs_off,
+                mp_obs=np.concatenate(obs).astype(np.int32) if obs else np.zeros(0, np.int32))
+
+
+def synth_frame_mps(seed: int, graph: dict, nkp: int = 1000, center: int | None = None, matched: float = 0.4,
+                    window: int = 4) -> np.ndarray:
+    """mvpMapPoints of a frame near keyframe `center`: a fraction of the
+    keypoints matched to points observed by keyframes within `window`
+    (duplicates possible, bad points included as the reference's frame may
+    hold them), the rest NULL."""
+    rng = np.random.default_rng(seed)
+    nkf = len(graph["kf_bad"])
+    c = int(rng.integers(0, nkf)) if center is None else center
+    lo, hi = max(0, c - window), min(nkf, c + window + 1)
+    cand = graph["kf_mp"][graph["kf_mp_off"][lo]:graph["kf_mp_off"][hi]]
+    cand = cand[cand >= 0]
+    fm = np.full(nkp, -1, np.int32)
+    if len(cand):
+        on = rng.random(nkp) < matched
+        fm[on] = rng.choice(cand, size=int(on.sum()))
+    return fm

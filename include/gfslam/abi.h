@@ -633,6 +633,51 @@ int gf_search_for_triangulation_dev(gf_ctx* ctx, int check_ori, int npairs, cons
                                     const gf_bow_side* b, const float* F12, const float* sigma2_b, int nlevels,
                                     int32_t* const* outs, int32_t* d_nmatches, void* stream);
 
+/* ----------------------------------------- local-map assembly
+ * Tracking::UpdateReference (Tracking.cc:3689-3706) =
+ * UpdateReferenceKeyFrames (:3768-3852) + UpdateReferencePoints (:3708-3766),
+ * for a batch of frames tracking against one map:
+ *   - every map point of the frame (mvpMapPoints, keypoint order) that is
+ *     not bad votes once for each keyframe observing it; bad ones are set to
+ *     -1 in the frame (:3778-3793);
+ *   - local keyframes = the voted keyframes that are not bad, in
+ *     std::map<KeyFrame*,int> order, i.e. ascending KeyFrame* — which is the
+ *     order keyframes are passed in here (Map::GetAllKeyFrames iterates its
+ *     std::set<KeyFrame*> that way); the reference keyframe is the first one
+ *     with the most votes (:3798-3817);
+ *   - while the list holds <= 80, each of the keyframes found so far adds the
+ *     first of its best 10 covisible keyframes (GetBestCovisibilityKeyFrames(10))
+ *     that is neither bad nor in the list (:3820-3848);
+ *   - local map points = the map points of the local keyframes
+ *     (GetMapPointMatches, slot order), first occurrence only, not bad
+ *     (:3737-3763; GOOD_FEATURE_MAP_BOUND is off in the reference build).
+ * The keyframe / map-point "mnTrackReferenceForFrame" marks are the
+ * call's own: every call starts from unmarked keyframes and points. */
+typedef struct gf_covis_map {
+    int32_t nkf, nmp;           /* keyframes (<= 8192), map points            */
+    const uint8_t* kf_bad;      /* [nkf] KeyFrame::isBad, ascending KeyFrame* */
+    const int32_t* kf_mp_off;   /* [nkf+1] CSR of KeyFrame::mvpMapPoints      */
+    const int32_t* kf_mp;       /*   map point index per slot, -1 = NULL      */
+    const int32_t* kf_cov_off;  /* [nkf+1] CSR of mvpOrderedConnectedKeyFrames */
+    const int32_t* kf_cov;      /*   keyframe indices (the first 10 are used) */
+    const uint8_t* mp_bad;      /* [nmp] MapPoint::isBad                      */
+    const int32_t* mp_obs_off;  /* [nmp+1] CSR of MapPoint::mObservations     */
+    const int32_t* mp_obs;      /*   observing keyframe indices               */
+} gf_covis_map;
+/* One frame, host arrays (the map is uploaded per call). frame_mps[nkp] is
+ * updated in place. Outputs up to the caps; the counts are the full sizes
+ * (GF_ERR_CAP when a cap is exceeded). ref_kf = pKFmax index or -1. */
+int gf_update_reference(gf_ctx* ctx, const gf_covis_map* map, int32_t* frame_mps, int nkp, int32_t* local_kfs,
+                        int* n_local_kfs, int kf_cap, int32_t* local_mps, int* n_local_mps, int mp_cap,
+                        int32_t* ref_kf);
+/* B frames against one map whose arrays are device pointers (the struct is
+ * host memory). d_frame_mps [B][stride] with d_nkps[B]; outputs
+ * [B][kf_cap] / [B][mp_cap], counts [B], d_ref_kf [B]. */
+int gf_update_reference_dev(gf_ctx* ctx, const gf_covis_map* d_map, int nframes, int32_t* d_frame_mps,
+                            const int32_t* d_nkps, int stride, int32_t* d_local_kfs, int32_t* d_n_local_kfs,
+                            int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap,
+                            int32_t* d_ref_kf, void* stream);
+
 /* ------------------------------------------------ relocalisation PnP
  * ORB_SLAM::PnPsolver (src/PnPsolver.cc, include/PnPsolver.h): EPnP
  * (Lepetit et al.) on random minimal sets inside RANSAC, then a refinement
