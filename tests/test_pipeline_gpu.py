@@ -120,10 +120,11 @@ def test_sequence_matches_oracle(case):
 def test_bench_shape_parity():
     """The timed configuration itself: 768 streams in 3 groups of 256 (as
     bench.py runs them, each group on its own context / HIP stream, launches
-    interleaved), streams {0, 127, 255} of each group checked for 2 steps."""
+    interleaved, extraction stages chained by gf_frontend_set_gate), streams
+    {0, 127, 255} of each group checked for 2 steps."""
     import torch
 
-    from gf_orb_slam_amd.pipeline import FrontEnd
+    from gf_orb_slam_amd.pipeline import FrontEnd, chain_extraction
 
     G, Bg = 3, 256
     W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5)
@@ -140,6 +141,8 @@ def test_bench_shape_parity():
         fe.set_source(frames, W.scene_of[sl], W.phase[sl])
         fe.bootstrap(T[sl], V[sl], 0.0)
         fes.append(fe)
+    gates = chain_extraction(fes)
+    assert len(gates) == G
     torch.cuda.synchronize()
     fr = frames.cpu().numpy()
     check = [0, 127, 255]
