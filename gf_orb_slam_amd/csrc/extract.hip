@@ -700,7 +700,8 @@ __device__ void wave_retain_to(SelWave& W, uint32_t* list, int n, int keep, uint
     for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
 }
 
-__global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
+#define SEL_THREADS 512
+__global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
                                                 uint32_t* __restrict__ lists, long long list_stride,
                                                 const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
                                                 long long lvl_stride, int* __restrict__ lvl_counts) {
@@ -760,7 +761,7 @@ __global__ __launch_bounds__(256) void k_select(LevelGeom g, const CellInfo* __r
     }
     __syncthreads();
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
-    for (int c = wv; c < nc; c += 4) {
+    for (int c = wv; c < nc; c += SEL_THREADS / 64) {
         if (!valid[c]) continue;
         uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
         wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
@@ -1291,6 +1292,8 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
         GF_HIP(hipMemcpy(ex->d_ytab, yall.data(), sizeof(int2) * yall.size(), hipMemcpyHostToDevice));
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
+    GF_HIP(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)((SEL_THREADS / 64) * sizeof(SelWave))));
     GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ex->fast_lds));
     *out = ex;
@@ -1368,7 +1371,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     }
     {
         GF_PROF(ctx, s, "k_select");
-        k_select<<<dim3(ex->nlevels, nframes), 256, 4 * sizeof(SelWave), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+        k_select<<<dim3(ex->nlevels, nframes), SEL_THREADS, (SEL_THREADS / 64) * sizeof(SelWave), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }

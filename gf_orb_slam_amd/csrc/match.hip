@@ -324,6 +324,7 @@ struct SeqPre {
 
 #define SEQ_PRE_THREADS 1024
 #define SEQ_PRE_DESC_MAX 2048
+#define SEQ_PRE_G 4  // lanes per query
 __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,
                                                                    SeqPre* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -352,18 +353,25 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
     for (int c = tid; c < NCELLS + 1; c += SEQ_PRE_THREADS) A.grid_cs[(long long)f * (NCELLS + 1) + c] = cell_start[c];
     for (int i = tid; i < n; i += SEQ_PRE_THREADS) A.grid_items[(long long)f * A.kp_cap + i] = items[i];
     const uint8_t* DD = dl ? (const uint8_t*)Ds : D;
-    for (int k = tid; k < nq; k += SEQ_PRE_THREADS) {
-        const Query q = make_query(A, fc, f, k);
-        SeqPre r;
-        r.id = q.id;
-        r.ncand = 0;
-        r.pad = 0;
-        for (int j = 0; j < 4; j++) r.h[j] = -1, r.d[j] = 0;
-        if (q.valid) {
-            int hd[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX}, hi[4] = {-1, -1, -1, -1}, nc = 0;
+    // SEQ_PRE_G lanes per query: lane g of the group takes candidates
+    // g, g + G, ... of the window (ix-major, then the CSR: the reference's
+    // order t) and keeps its four smallest (distance, t); a butterfly over the
+    // group merges them, so the four smallest over the window come out with
+    // the sequential loop's tie order.
+    const int g = tid & (SEQ_PRE_G - 1);
+    constexpr unsigned long long NONE = ~0ull;
+    for (int k0 = 0; k0 < nq; k0 += SEQ_PRE_THREADS / SEQ_PRE_G) {
+        const int k = k0 + tid / SEQ_PRE_G;
+        const bool live = k < nq;
+        Query q;
+        if (live) q = make_query(A, fc, f, k);
+        unsigned long long key[4] = {NONE, NONE, NONE, NONE};
+        int nc = 0;
+        if (live && q.valid) {
+            int t0 = 0;  // candidate order of the column's first item
             for (int ix = q.cx0; ix <= q.cx1; ix++) {
                 const int s0 = cell_start[ix * GRID_ROWS + q.cy0], s1 = cell_start[ix * GRID_ROWS + q.cy1 + 1];
-                for (int t = s0; t < s1; t++) {
+                for (int t = s0 + g; t < s1; t += SEQ_PRE_G) {
                     const int idx = items[t];
                     const float4 kp = X[idx];
                     const int oct = __float_as_int(kp.z);
@@ -372,23 +380,46 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
                         continue;
                     const int dist = hamming32(q.d, DD + (long long)idx * 32);
                     nc++;
-                    // insert (dist, order): strict <, so ties keep the earlier candidate
-                    int j = 4;
-                    while (j > 0 && dist < hd[j - 1]) j--;
-                    if (j < 4) {
-                        for (int m = 3; m > j; m--) hd[m] = hd[m - 1], hi[m] = hi[m - 1];
-                        hd[j] = dist;
-                        hi[j] = idx;
+                    const unsigned long long kk = ((unsigned long long)dist << 48) |
+                                                  ((unsigned long long)(t0 + t - s0) << 16) | (unsigned)idx;
+                    if (kk < key[3]) {
+                        key[3] = kk;
+                        if (key[3] < key[2]) { const unsigned long long x = key[2]; key[2] = key[3]; key[3] = x; }
+                        if (key[2] < key[1]) { const unsigned long long x = key[1]; key[1] = key[2]; key[2] = x; }
+                        if (key[1] < key[0]) { const unsigned long long x = key[0]; key[0] = key[1]; key[1] = x; }
                     }
                 }
+                t0 += s1 - s0;
             }
-            for (int j = 0; j < 4; j++) {
-                r.h[j] = (int16_t)hi[j];
-                r.d[j] = (int16_t)(hi[j] >= 0 ? hd[j] : 0);
-            }
-            r.ncand = (int16_t)min(nc, 5);
         }
-        out[(long long)f * A.q_cap + k] = r;
+#pragma unroll
+        for (int o = 1; o < SEQ_PRE_G; o <<= 1) {
+            unsigned long long p[4], m[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) p[j] = __shfl_xor(key[j], o, 64);
+            nc += __shfl_xor(nc, o, 64);
+            // merge two ascending lists, keep the four smallest
+            int a = 0, b = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const unsigned long long ka = a < 4 ? key[a] : NONE, kb = b < 4 ? p[b] : NONE;
+                if (ka <= kb) { m[j] = ka; a++; } else { m[j] = kb; b++; }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) key[j] = m[j];
+        }
+        if (live && g == 0) {
+            SeqPre r;
+            r.id = q.id;
+            r.pad = 0;
+            for (int j = 0; j < 4; j++) {
+                const bool on = q.valid && key[j] != NONE;
+                r.h[j] = on ? (int16_t)(key[j] & 0xffff) : (int16_t)-1;
+                r.d[j] = on ? (int16_t)(key[j] >> 48) : (int16_t)0;
+            }
+            r.ncand = q.valid ? (int16_t)min(nc, 5) : (int16_t)0;
+            out[(long long)f * A.q_cap + k] = r;
+        }
     }
 }
 
@@ -424,6 +455,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
     int16_t* sdist = (int16_t*)(spre + A.q_cap); // kp_cap: score of each claim made here
     int16_t* sres = sdist + A.kp_cap;            // q_cap: matched keypoint per query (-1 none)
     int16_t* qidx = sres + A.q_cap;              // q_cap: query index of each staged outcome
+    int* mk = (int*)(((uintptr_t)(qidx + A.q_cap) + 15) & ~(uintptr_t)15);  // kp_cap: first claiming lane of a batch
     __shared__ int s_nm, s_hist[HISTO_LENGTH], s_keep[3];
 
     const int f = blockIdx.x, lane = threadIdx.x;
@@ -467,27 +499,67 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
     __syncthreads();
 
     const unsigned long long NONE = ~0ull;
-    for (int qi = 0; qi < nvalid; qi++) {
-        const SeqPre pr = spre[qi];
-        const int k = qidx[qi];
-        // SearchByProjection(Cur, Last) keeps the best candidate only (no
-        // ratio test): the outcome is the first of the four precomputed best
-        // candidates still unclaimed; a query whose four are all taken while
-        // the window holds more candidates scans again
-        int j = 0;
-        while (j < 4 && pr.h[j] >= 0 && claim[pr.h[j]] >= 0) j++;
-        const bool known = (j < 4 && pr.h[j] >= 0) || j >= pr.ncand;
-        if (known) {
-            if (lane == 0 && j < pr.ncand && j < 4 && pr.d[j] <= TH_HIGH) {
-                const int res = pr.h[j];
-                claim[res] = pr.id;
-                sdist[res] = pr.d[j];
-                s_nm++;
-                sres[k] = (int16_t)res;
+    // Queries in batches of 64, one per lane, against the claims at the
+    // batch start. A query's outcome can only change when an earlier query
+    // of its batch claims the keypoint it picked (claims only remove
+    // candidates, and its earlier candidates were already claimed), so the
+    // outcomes up to the first such collision — or the first query that must
+    // rescan its window — are exactly the sequential ones and are committed
+    // together; that query then runs alone (rescan) or heads the next batch.
+    for (int i = lane; i < n; i += SEQ_THREADS) mk[i] = INT_MAX;
+    __syncthreads();
+    int qi0 = 0;
+    while (qi0 < nvalid) {
+        const int qi = qi0 + lane;
+        const bool in = qi < nvalid;
+        int k = 0, pick = -1, res = -1, id = 0;
+        int16_t dres = 0;
+        bool rescan = false;
+        if (in) {
+            const SeqPre pr = spre[qi];
+            k = qidx[qi];
+            id = pr.id;
+            int j = 0;
+            while (j < 4 && pr.h[j] >= 0 && claim[pr.h[j]] >= 0) j++;
+            const bool known = (j < 4 && pr.h[j] >= 0) || j >= pr.ncand;
+            rescan = !known;
+            if (known && j < 4 && pr.h[j] >= 0) {
+                pick = pr.h[j];
+                if (j < pr.ncand && pr.d[j] <= TH_HIGH) {
+                    res = pick;
+                    dres = pr.d[j];
+                }
             }
-            __syncthreads();
+            if (res >= 0) atomicMin(&mk[res], lane);
+        }
+        __syncthreads();
+        const bool unsafe = in && (rescan || (pick >= 0 && mk[pick] < lane));
+        const unsigned long long ub = __ballot(unsafe);
+        const int stop = ub ? __ffsll((long long)ub) - 1 : SEQ_THREADS;  // first lane not committed
+        const bool commit = in && lane < stop && res >= 0;
+        __syncthreads();  // every lane has read mk before it is reset
+        if (commit) {
+            claim[res] = id;
+            sdist[res] = dres;
+            sres[k] = (int16_t)res;
+        }
+        if (res >= 0) mk[res] = INT_MAX;
+        const unsigned long long cb = __ballot(commit);
+        if (lane == 0) s_nm += __popcll(cb);
+        __syncthreads();
+        if (stop >= SEQ_THREADS || qi0 + stop >= nvalid) {
+            qi0 += SEQ_THREADS;
             continue;
         }
+        const bool rs = (ub >> stop) & 1ull ? __shfl(rescan ? 1 : 0, stop, 64) != 0 : false;
+        if (!rs) {  // a collision: the query heads the next batch
+            qi0 += stop;
+            continue;
+        }
+        // the query at `stop` lost its four precomputed candidates: rescan its window
+        k = qidx[qi0 + stop];
+        qi0 += stop + 1;
+        {
         const Query q = make_query(A, fc, f, k);
         unsigned long long k1 = NONE, k2 = NONE;
         // walk the window's columns; candidate order t runs ix-major, then the CSR
@@ -544,6 +616,7 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
                 }
             }
         }
+        }
         __syncthreads();
     }
     for (int i = lane; i < n; i += SEQ_THREADS)
@@ -556,7 +629,8 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
 }
 
 size_t seq_lds_bytes(int kp_cap, int q_cap) {
-    return sizeof(int) * (size_t)kp_cap + sizeof(SeqPre) * (size_t)q_cap + 2 * ((size_t)kp_cap + 2 * q_cap) + 4;
+    return sizeof(int) * (size_t)kp_cap + sizeof(SeqPre) * (size_t)q_cap + 2 * ((size_t)kp_cap + 2 * q_cap) + 16 +
+           sizeof(int) * (size_t)kp_cap;
 }
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
