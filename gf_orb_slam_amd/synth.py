@@ -513,3 +513,79 @@ def synth_frame_mps(seed: int, graph: dict, nkp: int = 1000, center: int | None 
         on = rng.random(nkp) < matched
         fm[on] = rng.choice(cand, size=int(on.sum()))
     return fm
+
+
+def synth_two_view(seed: int, n_match: int = 300, n_extra: int = 200, planar: bool = False, baseline: float = 0.3,
+                   rot_deg: float = 5.0, noise_px: float = 0.5, outlier_frac: float = 0.1, width: int = 752,
+                   height: int = 480, f: float = 458.0) -> dict:
+    """Two views of one scene for the monocular initialiser (Initializer.cc):
+    reference keypoints kps1, current keypoints kps2 (KEYPOINT_DTYPE, both
+    with unmatched extras, shuffled), matches12 (n1 entries, -1 = unmatched),
+    K (3x3), and the ground truth R21, t21 (x2 = R21 x1 + t21) and X (points
+    in camera-1 coordinates, NaN for outlier matches). planar: the points lie
+    on one plane (the homography case); baseline 0 is a pure rotation (no
+    parallax: the initialisation has to fail)."""
+    from .orb import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    K = np.array([[f, 0, width / 2], [0, f, height / 2], [0, 0, 1]], np.float32)
+    ax = rng.normal(size=3)
+    ax /= np.linalg.norm(ax)
+    a = np.deg2rad(rot_deg)
+    S = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    R = np.eye(3) + np.sin(a) * S + (1 - np.cos(a)) * S @ S
+    tdir = rng.normal(size=3) * [1.0, 0.3, 0.2]
+    t = baseline * tdir / max(np.linalg.norm(tdir), 1e-12)
+
+    def project(P):
+        return (P[:, :2] / P[:, 2:3]) * [K[0, 0], K[1, 1]] + [K[0, 2], K[1, 2]]
+
+    X = np.zeros((0, 3))
+    while len(X) < n_match:
+        m = 4 * n_match
+        uv = rng.uniform([20, 20], [width - 20, height - 20], size=(m, 2))
+        if planar:
+            nrm = np.array([0.1, -0.2, 1.0]) + 0.1 * rng.normal(size=3)
+            d = 4.0
+            ray = np.c_[(uv - K[:2, 2]) / [K[0, 0], K[1, 1]], np.ones(m)]
+            z = d / (ray @ nrm)
+            P = ray * z[:, None]
+        else:
+            z = rng.uniform(2.0, 8.0, size=m)
+            P = np.c_[(uv - K[:2, 2]) / [K[0, 0], K[1, 1]] * z[:, None], z]
+        P2 = P @ R.T + t
+        u2 = project(P2) if len(P2) else P2[:, :2]
+        ok = (P[:, 2] > 0.5) & (P2[:, 2] > 0.5) & (u2[:, 0] > 5) & (u2[:, 0] < width - 5) & (u2[:, 1] > 5) & \
+             (u2[:, 1] < height - 5)
+        X = np.r_[X, P[ok]]
+    X = X[:n_match]
+    u1 = project(X) + rng.normal(scale=noise_px, size=(n_match, 2))
+    u2 = project(X @ R.T + t) + rng.normal(scale=noise_px, size=(n_match, 2))
+    nout = int(round(outlier_frac * n_match))
+    out_idx = rng.choice(n_match, nout, replace=False)
+    u2[out_idx] = rng.uniform([5, 5], [width - 5, height - 5], size=(nout, 2))
+    Xgt = X.copy()
+    Xgt[out_idx] = np.nan
+    n1, n2 = n_match + n_extra, n_match + n_extra
+
+    def kparr(uv):
+        k = np.zeros(len(uv), KEYPOINT_DTYPE)
+        k["x"], k["y"] = uv[:, 0], uv[:, 1]
+        k["size"] = 31.0
+        k["angle"] = rng.uniform(0, 360, size=len(uv))
+        k["response"] = rng.uniform(0, 100, size=len(uv))
+        k["octave"] = rng.integers(0, 4, size=len(uv))
+        k["class_id"] = -1
+        return k
+
+    e1 = rng.uniform([5, 5], [width - 5, height - 5], size=(n_extra, 2))
+    e2 = rng.uniform([5, 5], [width - 5, height - 5], size=(n_extra, 2))
+    p1, p2 = rng.permutation(n1), rng.permutation(n2)  # keypoint order in each frame
+    kps1 = kparr(np.r_[u1, e1])[np.argsort(p1)]
+    kps2 = kparr(np.r_[u2, e2])[np.argsort(p2)]
+    # row r of the stacked arrays sits at position p[r]
+    matches12 = np.full(n1, -1, np.int32)
+    matches12[p1[:n_match]] = p2[:n_match]
+    X1 = np.full((n1, 3), np.nan)
+    X1[p1[:n_match]] = Xgt
+    return dict(kps1=kps1, kps2=kps2, matches12=matches12, K=K, R21=R.astype(np.float32), t21=t.astype(np.float32),
+                X=X1)

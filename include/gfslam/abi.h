@@ -733,6 +733,46 @@ int gf_pnp_iterate_dev(gf_ctx* ctx, int nprob, const float* d_p3d, const float* 
                        int max_iterations, gf_rng* d_rng, float* d_Tcw, uint8_t* d_inliers, int32_t* d_ninliers,
                        int32_t* d_flags, void* stream);
 
+/* ------------------------------------------------ monocular initialisation
+ * ORB_SLAM::Initializer (src/Initializer.cc, include/Initializer.h):
+ * Initializer(ReferenceFrame, sigma, iterations) + Initialize(CurrentFrame,
+ * vMatches12, R21, t21, vP3D, vbTriangulated) (:44-132), called by
+ * Tracking::MonocularInitialization with sigma 1.0 and 200 iterations; the
+ * reference passes minTriangulated = THRES_INIT_MPT_NUM / 2 = 50. Frame 1 is
+ * the reference frame (mvKeys1 = its undistorted keypoints), frame 2 the
+ * current one; matches12[i] (n1 entries) is the frame-2 keypoint matched to
+ * keypoint i of frame 1 or -1. The 8-point sets are drawn from rng (the
+ * process-wide std::rand() state, DUtils::Random::RandomInt), which advances
+ * by 8 * iterations draws. Outputs p3d (n1 x 3) and triangulated (n1) are
+ * vP3D / vbTriangulated when ok, zeros otherwise. */
+typedef struct gf_init_result {
+    int32_t ok;         /* Initialize() returned true: R21, t21, p3d, triangulated valid      */
+    int32_t model;      /* 0 homography (RH > 0.40), 1 fundamental, -1 neither search scored  */
+    int32_t nmatches;   /* N = entries of matches12 >= 0                                       */
+    int32_t iter_H;     /* RANSAC iteration of the kept H (first strict best), -1 none         */
+    int32_t iter_F;     /* same for F                                                          */
+    int32_t ninliers_H; /* vbMatchesInliersH count                                             */
+    int32_t ninliers_F; /* vbMatchesInliersF count                                             */
+    int32_t best;       /* motion hypothesis with the most nGood (0..7 H, 0..3 F), -1 none     */
+    int32_t ngood[8];   /* CheckRT nGood of each motion hypothesis                             */
+    float SH, SF, RH;   /* scores and ratio (RH = 0 when both scores are 0)                    */
+    float parallax;     /* parallax (degrees) of hypothesis `best`                             */
+    float H21[9], F21[9]; /* kept models, row-major (zeros when none)                          */
+    float R21[9], t21[3]; /* accepted motion, row-major                                        */
+} gf_init_result;
+/* Host family: uploads, runs the device path, downloads. GF_ERR_ARG when a
+ * match index is >= n2 or fewer than 8 matches exist (nothing runs then). */
+int gf_initialize(gf_ctx* ctx, const float K[9], float sigma, int iterations, int min_triangulated,
+                  const gf_keypoint* kps1, int n1, const gf_keypoint* kps2, int n2, const int32_t* matches12,
+                  gf_rng* rng, gf_init_result* result, float* p3d, uint8_t* triangulated);
+/* Device family: all buffers in device memory; the caller guarantees the
+ * match indices are < n2. With fewer than 8 matches the result reports
+ * model -1 and nmatches, and rng is left as it was. */
+int gf_initialize_dev(gf_ctx* ctx, const float K[9], float sigma, int iterations, int min_triangulated,
+                      const gf_keypoint* d_kps1, int n1, const gf_keypoint* d_kps2, int n2,
+                      const int32_t* d_matches12, gf_rng* d_rng, gf_init_result* d_result, float* d_p3d,
+                      uint8_t* d_triangulated, void* stream);
+
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end
  * step stays on the device. One workgroup per frame.
