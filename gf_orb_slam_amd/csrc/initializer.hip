@@ -5,8 +5,11 @@
 //                   reference's sequential float sums, one lane, LDS-staged;
 //                   block 2: ordered compaction of vMatches12 (:51-63) and the
 //                   mMaxIterations 8-point sets (:80-95) from the caller's
-//                   std::rand() state (DUtils::Random::RandomInt; the
-//                   available-index list is an overwrite log, not a copy);
+//                   std::rand() state: lane 0 runs glibc's lagged-Fibonacci
+//                   recurrence with its 31-word window in registers, then one
+//                   lane per iteration turns 8 draws into RandomInt values and
+//                   replays the swap-remove of vAvailableIndices as an
+//                   overwrite log;
 //   k_init_hyp      one workgroup per RANSAC hypothesis, H and F side by side
 //                   (FindHomography :241-289 / FindFundamental :292-340):
 //                   lane 0 solves the 8-point system (ComputeH21 :343-383,
@@ -34,7 +37,6 @@
 #include <cmath>
 
 #include "common.h"
-#include "rng.h"
 
 namespace {
 
@@ -314,11 +316,6 @@ struct InitArgs {
 
 enum { C_N = 0, C_MODEL = 1, C_NHYP = 2, C_NIN = 3 };
 
-__device__ __forceinline__ int random_int(int32_t* s, int32_t* f, int32_t* r, int mn, int mx) {
-    const int d = mx - mn + 1;
-    return int(((double)gfrng::next(s, f, r) / ((double)2147483647 + 1.0)) * d) + mn;
-}
-
 __global__ __launch_bounds__(IN_BIG) void k_init_prepare(InitArgs A) {
     __shared__ float xs[IN_BIG], ys[IN_BIG];
     __shared__ int tmp[IN_BIG / 64];
@@ -400,40 +397,75 @@ __global__ __launch_bounds__(IN_BIG) void k_init_prepare(InitArgs A) {
         N += tot;
         __syncthreads();
     }
-    if (tid != 0) return;
-    A.ctl[C_N] = N;
+    if (tid == 0) A.ctl[C_N] = N;
     if (N < 8) return;
-    // the 8-point sets (:80-95): vAvailableIndices = 0..N-1 with an overwrite log
-    int32_t s[31];
-    for (int i = 0; i < 31; i++) s[i] = A.rng->state[i];
-    int32_t f = A.rng->f, r = A.rng->r;
-    for (int it = 0; it < A.iters; it++) {
-        int opos[8], oval[8], no = 0, size = N;
-        for (int j = 0; j < 8; j++) {
-            const int randi = random_int(s, &f, &r, 0, size - 1);
-            int idx = randi, back = size - 1;
-            for (int o = 0; o < no; o++) {
-                if (opos[o] == randi) idx = oval[o];
-                if (opos[o] == size - 1) back = oval[o];
+    // the 8-point sets (:80-95). glibc's TYPE_3 generator is x_k = x_{k-31} +
+    // x_{k-3}: lane 0 runs it 31 steps per unrolled block with the window in
+    // registers and stores every x_k (raw, full 32 bits) into the sets buffer
+    const int n = 8 * A.iters;
+    uint32_t* raw = reinterpret_cast<uint32_t*>(A.sets);
+    const int f0 = A.rng->f, r0 = A.rng->r;
+    if (tid == 0) {
+        uint32_t w[31];  // w[i] = x_{i-31}: the state word at (f0 + i) % 31
+#pragma unroll
+        for (int i = 0; i < 31; i++) w[i] = (uint32_t)A.rng->state[(f0 + i) % 31];
+        for (int b0 = 0; b0 < n; b0 += 31) {
+#pragma unroll
+            for (int j = 0; j < 31; j++) {
+                const uint32_t x = w[j] + w[(j + 28) % 31];
+                w[j] = x;
+                if (b0 + j < n) raw[b0 + j] = x;
             }
+        }
+    }
+    __syncthreads();
+    // the caller's state after n draws: x_k sits at position (f0 + k) % 31
+    if (tid < 31) {
+        const int k0 = (tid - f0 + 31) % 31;
+        if (k0 <= n - 1) A.rng->state[tid] = (int32_t)raw[k0 + 31 * ((n - 1 - k0) / 31)];
+    }
+    if (tid == 31) {
+        A.rng->f = (f0 + n) % 31;
+        A.rng->r = (r0 + n) % 31;
+    }
+    __syncthreads();
+    // one lane per iteration: RandomInt(0, size-1) and the swap-remove of
+    // vAvailableIndices = 0..N-1, kept as an overwrite log of <= 8 entries
+    for (int it = tid; it < A.iters; it += IN_BIG) {
+        uint32_t x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = raw[it * 8 + j];
+        int opos[8], oval[8], no = 0, size = N;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int randi = int(((double)(int32_t)(x[j] >> 1) / ((double)2147483647 + 1.0)) * size);
+            int idx = randi, back = size - 1;
+#pragma unroll
+            for (int o = 0; o < 8; o++)
+                if (o < no) {
+                    if (opos[o] == randi) idx = oval[o];
+                    if (opos[o] == size - 1) back = oval[o];
+                }
             A.sets[it * 8 + j] = idx;
             bool found = false;  // vAvailableIndices[randi] = back
-            for (int o = 0; o < no; o++)
-                if (opos[o] == randi) {
+#pragma unroll
+            for (int o = 0; o < 8; o++)
+                if (o < no && opos[o] == randi) {
                     oval[o] = back;
                     found = true;
                 }
             if (!found) {
-                opos[no] = randi;
-                oval[no] = back;
+#pragma unroll
+                for (int o = 0; o < 8; o++)
+                    if (o == no) {
+                        opos[o] = randi;
+                        oval[o] = back;
+                    }
                 no++;
             }
             size--;
         }
     }
-    for (int i = 0; i < 31; i++) A.rng->state[i] = s[i];
-    A.rng->f = f;
-    A.rng->r = r;
 }
 
 __device__ __forceinline__ void norm_T(const float* nm, float* T) {  // Normalize's T
