@@ -259,10 +259,11 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 // (two loads per dword, all in flight together); only the dwords at the
 // level's left and right edges load bytes through reflect-101. The row pass makes four outputs from
 // three LDS dwords with v_dot4_u32_u8 (two per output: the 7 taps are bytes).
-// Thread t then owns the pixel quad x = X0 + 4 (t & 15) .. +3 in rows
-// 2 (t >> 4) and +1: one ds_read_b128 per row sum row for the column pass
-// (the taps sum to 257, so the rounded value saturates at 255 as
-// saturate_cast does), one dword store per quad and row for the blurred plane, and the
+// Two rows' sums share a dword (each is at most 257 * 255 = 65535). Thread t
+// then owns the pixel quad x = X0 + 4 (t & 15) .. +3 in rows 2 (t >> 4) and
+// +1: four ds_read_b128 of row-pair sums, four v_dot2_u32_u16 per pixel for
+// the column pass (the taps sum to 257, so the rounded value saturates at 255
+// as saturate_cast does), one dword store per quad and row for the blurred plane, and the
 // 4-point compass pre-test on the quad at once in packed 16-bit lanes (bytes
 // 0/2 and 1/3 of the dword; the sign of c + th - v is "darker", of
 // v + th - c "brighter"). The few pixels that pass are compacted into an LDS
@@ -299,7 +300,7 @@ __device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgc
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
     __shared__ __align__(16) uint8_t src[BT_R][BT_SW];
-    __shared__ __align__(16) int rows[BT_R][BT_W];
+    __shared__ __align__(16) uint32_t rows2[BT_R / 2][BT_W];  // row sums of rows 2p | 2p+1 << 16
     __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
     __shared__ uint16_t cand[BT_W * BT_H];
     __shared__ int scan_tmp[4];
@@ -355,40 +356,55 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     __syncthreads();
     // taps round(256 * gaussian(7, sigma 2)) = 18 34 49 55 49 34 18
     constexpr uint32_t KLO = 18u | 34u << 8 | 49u << 16 | 55u << 24, KHI = 49u | 34u << 8 | 18u << 16;
-    for (int i = tid; i < BT_R * (BT_W / 4); i += 256) {
-        const int ry = i >> 4, q = i & 15;
-        const uint32_t* r32 = reinterpret_cast<const uint32_t*>(&src[ry][0]) + q;
-        const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2];
-        int4 o;  // output x = X0 + 4q + j reads LDS columns 4q + 1 + j .. 4q + 7 + j
-        o.x = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 1), KLO, 0u, false) +
-                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 1), KHI, 0u, false));
-        o.y = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 2), KLO, 0u, false) +
-                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 2), KHI, 0u, false));
-        o.z = (int)(__builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w1, w0, 3), KLO, 0u, false) +
-                    __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(w2, w1, 3), KHI, 0u, false));
-        o.w = (int)(__builtin_amdgcn_udot4(w1, KLO, 0u, false) + __builtin_amdgcn_udot4(w2, KHI, 0u, false));
-        *reinterpret_cast<int4*>(&rows[ry][4 * q]) = o;
+    // row pass, two source rows per item; a row sum is at most 257 * 255 =
+    // 65535, so the two rows share a dword (row 2p low, 2p + 1 high)
+    for (int i = tid; i < (BT_R / 2) * (BT_W / 4); i += 256) {
+        const int pr = i >> 4, q = i & 15;
+        uint4 o;
+        auto hsum = [&](int ry, int j) -> uint32_t {  // output x = X0 + 4q + j: LDS columns 4q + 1 + j ..
+            const uint32_t* r32 = reinterpret_cast<const uint32_t*>(&src[ry][0]) + q;
+            const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2];
+            const uint32_t lo = j == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, j + 1);
+            const uint32_t hi = j == 3 ? w2 : __builtin_amdgcn_alignbyte(w2, w1, j + 1);
+            return __builtin_amdgcn_udot4(lo, KLO, 0u, false) + __builtin_amdgcn_udot4(hi, KHI, 0u, false);
+        };
+        o.x = hsum(2 * pr, 0) | hsum(2 * pr + 1, 0) << 16;
+        o.y = hsum(2 * pr, 1) | hsum(2 * pr + 1, 1) << 16;
+        o.z = hsum(2 * pr, 2) | hsum(2 * pr + 1, 2) << 16;
+        o.w = hsum(2 * pr, 3) | hsum(2 * pr + 1, 3) << 16;
+        *reinterpret_cast<uint4*>(&rows2[pr][4 * q]) = o;
     }
     __syncthreads();
     const int qx = tid & 15, r0 = 2 * (tid >> 4), x = X0 + 4 * qx;
-    // column pass: rows r0 .. r0 + 7 of the row sums give output rows r0, r0 + 1
-    int4 rs[8];
+    // column pass: row pairs r0 / 2 .. + 3 (rows r0 .. r0 + 7) give output rows
+    // r0 and r0 + 1, four v_dot2_u32_u16 per pixel (the rounding bias as the
+    // accumulator's start)
+    uint4 rp[4];
 #pragma unroll
-    for (int k = 0; k < 8; k++) rs[k] = *reinterpret_cast<const int4*>(&rows[r0 + k][4 * qx]);
+    for (int k = 0; k < 4; k++) rp[k] = *reinterpret_cast<const uint4*>(&rows2[(r0 >> 1) + k][4 * qx]);
     uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        auto col = [&](int a0, int a1, int a2, int a3, int a4, int a5, int a6) -> uint32_t {
-            return min((__umul24(18u, (unsigned)(a0 + a6)) + __umul24(34u, (unsigned)(a1 + a5)) +
-                        __umul24(49u, (unsigned)(a2 + a4)) + __umul24(55u, (unsigned)a3) + (1u << 15)) >> 16,
-                       255u);
-        };
-        const uint32_t o0 = col(rs[r].x, rs[r + 1].x, rs[r + 2].x, rs[r + 3].x, rs[r + 4].x, rs[r + 5].x, rs[r + 6].x);
-        const uint32_t o1 = col(rs[r].y, rs[r + 1].y, rs[r + 2].y, rs[r + 3].y, rs[r + 4].y, rs[r + 5].y, rs[r + 6].y);
-        const uint32_t o2 = col(rs[r].z, rs[r + 1].z, rs[r + 2].z, rs[r + 3].z, rs[r + 4].z, rs[r + 5].z, rs[r + 6].z);
-        const uint32_t o3 = col(rs[r].w, rs[r + 1].w, rs[r + 2].w, rs[r + 3].w, rs[r + 4].w, rs[r + 5].w, rs[r + 6].w);
-        if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(D + (long long)r * pw) = o0 | o1 << 8 | o2 << 16 | o3 << 24;
-    }
+    typedef unsigned short gf_u16x2 __attribute__((ext_vector_type(2)));
+    auto u2 = [](uint32_t v) { return __builtin_bit_cast(gf_u16x2, v); };
+    const gf_u16x2 A0 = {18, 34}, A1 = {49, 55}, A2 = {49, 34}, A3 = {18, 0};  // output row r0
+    const gf_u16x2 B0 = {0, 18}, B1 = {34, 49}, B2 = {55, 49}, B3 = {34, 18};  // output row r0 + 1
+    auto colv = [&](uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3, gf_u16x2 c0, gf_u16x2 c1, gf_u16x2 c2,
+                    gf_u16x2 c3) -> uint32_t {
+        uint32_t a = __builtin_amdgcn_udot2(u2(p0), c0, 1u << 15, false);
+        a = __builtin_amdgcn_udot2(u2(p1), c1, a, false);
+        a = __builtin_amdgcn_udot2(u2(p2), c2, a, false);
+        a = __builtin_amdgcn_udot2(u2(p3), c3, a, false);
+        return min(a >> 16, 255u);
+    };
+    const uint32_t a0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, A0, A1, A2, A3);
+    const uint32_t a1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, A0, A1, A2, A3);
+    const uint32_t a2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, A0, A1, A2, A3);
+    const uint32_t a3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, A0, A1, A2, A3);
+    const uint32_t b0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, B0, B1, B2, B3);
+    const uint32_t b1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, B0, B1, B2, B3);
+    const uint32_t b2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, B0, B1, B2, B3);
+    const uint32_t b3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, B0, B1, B2, B3);
+    if (Y0 + r0 < h) *reinterpret_cast<uint32_t*>(D) = a0 | a1 << 8 | a2 << 16 | a3 << 24;
+    if (Y0 + r0 + 1 < h) *reinterpret_cast<uint32_t*>(D + pw) = b0 | b1 << 8 | b2 << 16 | b3 << 24;
     // compass pre-test of the quad in rows r0, r0 + 1 (LDS rows r0 + 3, r0 + 4)
     const uint32_t th2 = (uint32_t)map_th * 0x00010001u;
     uint32_t xm = 0;  // pixels of the quad at least 3 px inside the level, in x
