@@ -314,9 +314,51 @@ struct InitArgs {
     uint32_t* cosk;   // [8][n1] ordered keys of the good cosines
 };
 
+// A batch of independent problems (blockIdx.y = problem): problem p's view is
+// the base view with the caller's arrays and the scratch block offset by p.
+struct InitBatch {
+    InitArgs base;
+    const int32_t* n1s;  // per-problem sizes (null: base.n1 / base.n2)
+    const int32_t* n2s;
+    int cap1, cap2;      // rows per problem of the keypoint / match / output arrays
+    size_t ws_stride;    // scratch bytes per problem
+};
+
+__device__ __forceinline__ InitArgs at(const InitBatch& B, int p) {
+    InitArgs A = B.base;
+    const long long c1 = (long long)p * B.cap1, c2 = (long long)p * B.cap2;
+    A.k1 += c1;
+    A.k2 += c2;
+    A.matches += c1;
+    A.p3d += 3 * c1;
+    A.tri += c1;
+    A.rng += p;
+    A.res += p;
+    if (B.n1s) {
+        A.n1 = min(max(B.n1s[p], 0), B.cap1);
+        A.n2 = min(max(B.n2s[p], 0), B.cap2);
+    }
+    const size_t o = (size_t)p * B.ws_stride;
+    auto sh = [o](auto* q) { return reinterpret_cast<decltype(q)>(reinterpret_cast<char*>(q) + o); };
+    A.m1 = sh(A.m1);
+    A.m2 = sh(A.m2);
+    A.ctl = sh(A.ctl);
+    A.norm = sh(A.norm);
+    A.sets = sh(A.sets);
+    A.score = sh(A.score);
+    A.mats = sh(A.mats);
+    A.inl = sh(A.inl);
+    A.hyp = sh(A.hyp);
+    A.ngood = sh(A.ngood);
+    A.par = sh(A.par);
+    A.cosk = sh(A.cosk);
+    return A;
+}
+
 enum { C_N = 0, C_MODEL = 1, C_NHYP = 2, C_NIN = 3 };
 
-__global__ __launch_bounds__(IN_BIG) void k_init_prepare(InitArgs A) {
+__global__ __launch_bounds__(IN_BIG) void k_init_prepare(InitBatch Bt) {
+    const InitArgs A = at(Bt, blockIdx.y);
     __shared__ float xs[IN_BIG], ys[IN_BIG];
     __shared__ int tmp[IN_BIG / 64];
     const int tid = threadIdx.x;
@@ -524,7 +566,8 @@ __device__ __forceinline__ bool check_f(const float* F, float u1, float v1, floa
     return in;
 }
 
-__global__ __launch_bounds__(IN_T) void k_init_hyp(InitArgs A) {
+__global__ __launch_bounds__(IN_T) void k_init_hyp(InitBatch Bt) {
+    const InitArgs A = at(Bt, blockIdx.y);
     __shared__ float Ta[16 * 16];
     __shared__ float Hs[18];
     __shared__ float t1[IN_T], t2[IN_T];
@@ -689,7 +732,8 @@ __device__ int check_match(const RT& C, const float* K, float th2, const gf_keyp
     return (double)cosParallax < 0.99998 ? 2 : 1;
 }
 
-__global__ __launch_bounds__(IN_BIG) void k_init_decide(InitArgs A) {
+__global__ __launch_bounds__(IN_BIG) void k_init_decide(InitBatch Bt) {
+    const InitArgs A = at(Bt, blockIdx.y);
     __shared__ float sh[2 * 9 + 9];
     __shared__ int si[4];
     __shared__ int cntH, cntF;
@@ -848,7 +892,8 @@ __device__ __forceinline__ float key_val(uint32_t k) {
     return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-__global__ __launch_bounds__(IN_T) void k_init_checkrt(InitArgs A) {
+__global__ __launch_bounds__(IN_T) void k_init_checkrt(InitBatch Bt) {
+    const InitArgs A = at(Bt, blockIdx.y);
     __shared__ int s_cnt;
     __shared__ int hist[256];
     __shared__ uint32_t s_prefix;
@@ -906,7 +951,8 @@ __global__ __launch_bounds__(IN_T) void k_init_checkrt(InitArgs A) {
     }
 }
 
-__global__ __launch_bounds__(IN_BIG) void k_init_finish(InitArgs A) {
+__global__ __launch_bounds__(IN_BIG) void k_init_finish(InitBatch Bt) {
+    const InitArgs A = at(Bt, blockIdx.y);
     __shared__ int s_best;
     const int tid = threadIdx.x;
     const int nh = A.ctl[C_NHYP];
@@ -973,31 +1019,24 @@ __global__ __launch_bounds__(IN_BIG) void k_init_finish(InitArgs A) {
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int gf_initialize_dev(gf_ctx* ctx, const float K[9], float sigma, int iterations, int min_triangulated,
-                      const gf_keypoint* d_kps1, int n1, const gf_keypoint* d_kps2, int n2,
-                      const int32_t* d_matches12, gf_rng* d_rng, gf_init_result* d_result, float* d_p3d,
-                      uint8_t* d_triangulated, void* stream) {
-    GF_CHECK(ctx && K, GF_ERR_ARG, "gf_initialize_dev: null arg");
-    GF_CHECK(d_kps1 && d_kps2 && d_matches12 && d_rng && d_result && d_p3d && d_triangulated, GF_ERR_ARG,
-             "gf_initialize_dev: null buffer");
-    GF_CHECK(n1 > 0 && n2 > 0, GF_ERR_ARG, "gf_initialize_dev: empty frame");
-    GF_CHECK(iterations > 0 && iterations <= 65536, GF_ERR_ARG, "gf_initialize_dev: iterations out of range");
-    GF_CHECK(sigma > 0.f, GF_ERR_ARG, "gf_initialize_dev: sigma <= 0");
-    const size_t nn = (size_t)n1, it = (size_t)iterations;
-    // one scratch block (slot 62): m1, m2, inl, sets, ctl, norm, score, mats, hyp, ngood, par, cosk
+static int init_launch(gf_ctx* ctx, int nprob, const float K[9], float sigma, int iterations, int min_triangulated,
+                       const gf_keypoint* d_kps1, int n1, int cap1, const int32_t* d_n1, const gf_keypoint* d_kps2,
+                       int n2, int cap2, const int32_t* d_n2, const int32_t* d_matches12, gf_rng* d_rng,
+                       gf_init_result* d_result, float* d_p3d, uint8_t* d_triangulated, void* stream) {
+    GF_CHECK(iterations > 0 && iterations <= 65536, GF_ERR_ARG, "gf_initialize: iterations out of range");
+    GF_CHECK(sigma > 0.f, GF_ERR_ARG, "gf_initialize: sigma <= 0");
+    const size_t nn = (size_t)std::max(cap1, 1), it = (size_t)iterations;
+    // one scratch block per problem (slot 62): m1, m2, sets, ctl, norm, score, mats, hyp, ngood, par, cosk, inl
     const size_t off_m1 = 0, off_m2 = off_m1 + 4 * nn, off_sets = off_m2 + 4 * nn, off_ctl = off_sets + 32 * it,
                  off_norm = off_ctl + 64, off_score = off_norm + 32, off_mats = off_score + 8 * it,
                  off_hyp = off_mats + 72 * it, off_ngood = off_hyp + 4 * 96, off_par = off_ngood + 32,
-                 off_cosk = off_par + 32, off_inl = off_cosk + 32 * nn, total = off_inl + nn + 16;
+                 off_cosk = off_par + 32, off_inl = off_cosk + 32 * nn, per = (off_inl + nn + 255) & ~(size_t)255;
     void* ws = nullptr;
-    int rc = gf::ws_get(ctx, 62, total, &ws);
+    int rc = gf::ws_get(ctx, 62, per * (size_t)nprob, &ws);
     if (rc) return rc;
     char* b = (char*)ws;
-    InitArgs A{};
+    InitBatch Bt{};
+    InitArgs& A = Bt.base;
     for (int i = 0; i < 9; i++) A.K[i] = K[i];
     A.sigma = sigma;
     A.iters = iterations;
@@ -1023,33 +1062,68 @@ int gf_initialize_dev(gf_ctx* ctx, const float K[9], float sigma, int iterations
     A.par = (float*)(b + off_par);
     A.cosk = (uint32_t*)(b + off_cosk);
     A.inl = (uint8_t*)(b + off_inl);
+    Bt.n1s = d_n1;
+    Bt.n2s = d_n2;
+    Bt.cap1 = cap1;
+    Bt.cap2 = cap2;
+    Bt.ws_stride = per;
     hipStream_t s = (hipStream_t)stream;
     {
         GF_PROF(ctx, s, "k_init_prepare");
-        k_init_prepare<<<3, IN_BIG, 0, s>>>(A);
+        k_init_prepare<<<dim3(3, nprob), IN_BIG, 0, s>>>(Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_hyp");
-        k_init_hyp<<<2 * iterations, IN_T, 0, s>>>(A);
+        k_init_hyp<<<dim3(2 * iterations, nprob), IN_T, 0, s>>>(Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_decide");
-        k_init_decide<<<1, IN_BIG, 0, s>>>(A);
+        k_init_decide<<<dim3(1, nprob), IN_BIG, 0, s>>>(Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_checkrt");
-        k_init_checkrt<<<8, IN_T, 0, s>>>(A);
+        k_init_checkrt<<<dim3(8, nprob), IN_T, 0, s>>>(Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_finish");
-        k_init_finish<<<1, IN_BIG, 0, s>>>(A);
+        k_init_finish<<<dim3(1, nprob), IN_BIG, 0, s>>>(Bt);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gf_initialize_dev(gf_ctx* ctx, const float K[9], float sigma, int iterations, int min_triangulated,
+                      const gf_keypoint* d_kps1, int n1, const gf_keypoint* d_kps2, int n2,
+                      const int32_t* d_matches12, gf_rng* d_rng, gf_init_result* d_result, float* d_p3d,
+                      uint8_t* d_triangulated, void* stream) {
+    GF_CHECK(ctx && K, GF_ERR_ARG, "gf_initialize_dev: null arg");
+    GF_CHECK(d_kps1 && d_kps2 && d_matches12 && d_rng && d_result && d_p3d && d_triangulated, GF_ERR_ARG,
+             "gf_initialize_dev: null buffer");
+    GF_CHECK(n1 > 0 && n2 > 0, GF_ERR_ARG, "gf_initialize_dev: empty frame");
+    return init_launch(ctx, 1, K, sigma, iterations, min_triangulated, d_kps1, n1, n1, nullptr, d_kps2, n2, n2,
+                       nullptr, d_matches12, d_rng, d_result, d_p3d, d_triangulated, stream);
+}
+
+int gf_initialize_batch_dev(gf_ctx* ctx, int nprob, const float K[9], float sigma, int iterations,
+                            int min_triangulated, const gf_keypoint* d_kps1, int cap1, const int32_t* d_n1,
+                            const gf_keypoint* d_kps2, int cap2, const int32_t* d_n2, const int32_t* d_matches12,
+                            gf_rng* d_rng, gf_init_result* d_result, float* d_p3d, uint8_t* d_triangulated,
+                            void* stream) {
+    GF_CHECK(ctx && K, GF_ERR_ARG, "gf_initialize_batch_dev: null arg");
+    if (nprob <= 0) return GF_OK;
+    GF_CHECK(d_kps1 && d_kps2 && d_n1 && d_n2 && d_matches12 && d_rng && d_result && d_p3d && d_triangulated,
+             GF_ERR_ARG, "gf_initialize_batch_dev: null buffer");
+    GF_CHECK(cap1 > 0 && cap2 > 0 && nprob <= 65535, GF_ERR_ARG, "gf_initialize_batch_dev: bad caps or batch");
+    return init_launch(ctx, nprob, K, sigma, iterations, min_triangulated, d_kps1, cap1, cap1, d_n1, d_kps2, cap2,
+                       cap2, d_n2, d_matches12, d_rng, d_result, d_p3d, d_triangulated, stream);
 }
 
 int gf_initialize(gf_ctx* ctx, const float K[9], float sigma, int iterations, int min_triangulated,

@@ -83,3 +83,26 @@ def initialize_device(ctx, K, kps1, kps2, matches12, rng_state, sigma: float = 1
                                   kps1.data_ptr(), n1, kps2.data_ptr(), n2, matches12.data_ptr(),
                                   rng_state.data_ptr(), res.data_ptr(), p3d.data_ptr(), tri.data_ptr(), s))
     return res, p3d, tri
+
+
+def initialize_batch_device(ctx, K, kps1, n1, kps2, n2, matches12, rng_states, sigma: float = 1.0,
+                            iterations: int = 200, min_triangulated: int = MIN_TRIANGULATED, stream=None):
+    """Device batch (gf_initialize_batch_dev): kps1 [P, cap1, 28] / kps2
+    [P, cap2, 28] uint8 (KEYPOINT_DTYPE rows), n1 / n2 [P] int32, matches12
+    [P, cap1] int32, rng_states [P, 132] uint8 (advanced in place). Returns
+    (results [P, 200] uint8, p3d [P, cap1, 3] f32, triangulated [P, cap1] u8)."""
+    import torch
+
+    P, cap1 = kps1.shape[0], kps1.shape[1]
+    cap2 = kps2.shape[1]
+    dev = kps1.device
+    res = torch.zeros((P, INIT_RESULT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    p3d = torch.zeros((P, cap1, 3), dtype=torch.float32, device=dev)
+    tri = torch.zeros((P, cap1), dtype=torch.uint8, device=dev)
+    Kf = np.ascontiguousarray(np.asarray(K, np.float32).reshape(9))
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    check(lib().gf_initialize_batch_dev(ctx.handle, P, ptr(Kf), float(sigma), int(iterations), int(min_triangulated),
+                                        kps1.data_ptr(), cap1, n1.data_ptr(), kps2.data_ptr(), cap2, n2.data_ptr(),
+                                        matches12.data_ptr(), rng_states.data_ptr(), res.data_ptr(), p3d.data_ptr(),
+                                        tri.data_ptr(), s))
+    return res, p3d, tri

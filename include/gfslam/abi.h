@@ -772,6 +772,17 @@ int gf_initialize_dev(gf_ctx* ctx, const float K[9], float sigma, int iterations
                       const gf_keypoint* d_kps1, int n1, const gf_keypoint* d_kps2, int n2,
                       const int32_t* d_matches12, gf_rng* d_rng, gf_init_result* d_result, float* d_p3d,
                       uint8_t* d_triangulated, void* stream);
+/* Device batch: nprob independent initialisations in one launch set (e.g. every
+ * sequence of a multi-sequence tracker at start-up). Problem p's reference /
+ * current keypoints at [p][cap1] / [p][cap2] with d_n1[p] / d_n2[p] valid
+ * (clamped to the caps), matches12 [p][cap1], rng [p], result [p], p3d
+ * [p][cap1][3], triangulated [p][cap1]. Same per-problem results as
+ * gf_initialize_dev. */
+int gf_initialize_batch_dev(gf_ctx* ctx, int nprob, const float K[9], float sigma, int iterations,
+                            int min_triangulated, const gf_keypoint* d_kps1, int cap1, const int32_t* d_n1,
+                            const gf_keypoint* d_kps2, int cap2, const int32_t* d_n2, const int32_t* d_matches12,
+                            gf_rng* d_rng, gf_init_result* d_result, float* d_p3d, uint8_t* d_triangulated,
+                            void* stream);
 
 /* ------------------------------------------------ tracking glue (device)
  * Per-frame bookkeeping of Tracking between the stages above, so a front-end

@@ -222,3 +222,50 @@ def test_initializer_class_recovers_motion():
     ok, R21, t21, p3d, tri = ini.initialize(d["kps2"], d["matches12"], Rand(42))
     assert ok and _rot_err_deg(R21, d["R21"]) < 1.0 and tri.sum() >= 200
     assert float(t21[:, 0] @ (d["t21"] / np.linalg.norm(d["t21"]))) > 0.99
+
+
+@pytest.mark.gpu
+def test_initialize_batch_dev_matches_oracle():
+    """gf_initialize_batch_dev: 20 ragged problems (general, planar, pure
+    rotation, outliers, fewer than 8 matches) with their own rand() streams in
+    one launch set, each equal to the oracle run alone."""
+    import torch
+
+    from gf_orb_slam_amd.initializer import INIT_RESULT_DTYPE, initialize_batch_device
+    from gf_orb_slam_amd.matcher import default_context
+
+    cases = [dict(seed=s) for s in range(6)] + [dict(seed=s, planar=True) for s in range(4)] + \
+        [dict(seed=3, baseline=0.0), dict(seed=4, outlier_frac=0.4), dict(seed=5, n_match=5, n_extra=9),
+         dict(seed=6, n_match=30, n_extra=2), dict(seed=7, n_match=900, n_extra=100)] + \
+        [dict(seed=20 + s, n_match=150 + 50 * s, n_extra=20 * s) for s in range(5)]
+    ds = [synth_two_view(**c) for c in cases]
+    P = len(ds)
+    cap1 = max(len(d["kps1"]) for d in ds)
+    cap2 = max(len(d["kps2"]) for d in ds)
+    k1 = np.zeros((P, cap1, 28), np.uint8)
+    k2 = np.zeros((P, cap2, 28), np.uint8)
+    m = np.full((P, cap1), -1, np.int32)
+    n1 = np.array([len(d["kps1"]) for d in ds], np.int32)
+    n2 = np.array([len(d["kps2"]) for d in ds], np.int32)
+    rs = np.stack([_rng(100 + i).view(np.uint8) for i in range(P)]).reshape(P, -1)
+    for i, d in enumerate(ds):
+        k1[i, :n1[i]] = d["kps1"].view(np.uint8).reshape(-1, 28)
+        k2[i, :n2[i]] = d["kps2"].view(np.uint8).reshape(-1, 28)
+        m[i, :n1[i]] = d["matches12"]
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    rs_d = t(rs)
+    res, p3d, tri = initialize_batch_device(default_context(), ds[0]["K"], t(k1), t(n1), t(k2), t(n2), t(m), rs_d)
+    torch.cuda.synchronize()
+    res = res.cpu().numpy().view(INIT_RESULT_DTYPE).reshape(P)
+    p3d, tri, rs_d = p3d.cpu().numpy(), tri.cpu().numpy(), rs_d.cpu().numpy()
+    for i, d in enumerate(ds):
+        ro = _rng(100 + i)
+        rc, reso, p3do, trio = O.initialize(d["K"], d["kps1"], d["kps2"], d["matches12"], ro)
+        if rc != 0:  # fewer than 8 matches: reported, rng untouched
+            assert res[i]["model"] == -1 and res[i]["nmatches"] == reso[0]["nmatches"], i
+            assert rs_d[i].tobytes() == _rng(100 + i).tobytes(), i
+            continue
+        assert res[i].tobytes() == reso[0].tobytes(), (i, cases[i])
+        assert p3d[i, :n1[i]].tobytes() == p3do.tobytes() and tri[i, :n1[i]].tobytes() == trio.tobytes(), i
+        assert rs_d[i].tobytes() == ro.tobytes(), i
