@@ -20,7 +20,9 @@
 //                   W = Hpl Dinv into the panel Wt, db as Wt's column n
 //   k_ba_gemm       C = Ht^T Wt on v_mfma_f64_16x16x4 (split-K, fixed order):
 //                   the Schur product Hpl Dinv Hpl^T and the coefficient
-//                   vector Hpl db in one pass — the J^T J-shaped contraction
+//                   vector Hpl db in one pass — the J^T J-shaped contraction;
+//                   k_ba_spgemm, the same product as a host-built task list of
+//                   only the nonzero tile products (batches of <= 8 windows)
 //   k_ba_solve      S = Hpp + lambda I - C, b_s = b_p - C[:, n]; dense LL^T
 //                   and the triangular solves in LDS; trial poses exp(x) * T
 //   k_ba_update     landmark back-substitution, trial points, trial errors
@@ -60,6 +62,7 @@ struct BADesc {
     int ntiles, nwg;      // Schur GEMM tiles; point workgroups
     int nsplit, newg;     // GEMM k-splits; edge workgroups
     int kf0, pt0, e0, f0, fe0, pl0, tile0, wg0, mask0, ss0;
+    int item0, nitems, kl0, tip0;  // Schur GEMM task list: items, k-step list, per-tile item ranges
     long long panel0;  // Ht at panel0, Wt at panel0 + K * npad (doubles)
 };
 
@@ -107,6 +110,9 @@ struct BAArena {
     // split sums (S lower packed + the coefficient column), per-workgroup partials
     double* panel;
     const uint16_t* kmask;
+    const int4* items;        // (ti, tj, kb, ke): tile and its k-step range in klist
+    const int32_t* klist;     // k-steps (4 panel rows) where both operand tiles are nonzero
+    const int32_t* tile_iptr; // per problem ntiles + 1: the items of tile t, in order
     double* tiles;
     double* Ssum;
     double *wg_chi, *wg_chi_t, *wg_maxd, *wg_scale;
@@ -543,9 +549,51 @@ __global__ __launch_bounds__(64 * BA_GW) void k_ba_gemm(BAArena A) {
 
 size_t ba_gemm_lds(int npad) { return sizeof(double) * 2 * BA_GCH * 4 * (npad + 2); }
 
+// The same product as a task list: one wave per item = one output tile over
+// a run of the k-steps where both its operand tiles are nonzero (listed on the
+// host from the graph structure), operands read straight from the panels
+// (16 consecutive doubles per row, 4 rows per MFMA), the tile's partial sum
+// written per item and reduced in item order (k_ba_gemm_reduce). No k-step
+// that contributes nothing is visited, and no mask test runs per tile.
+constexpr int BA_SW = 4;   // waves (items) per workgroup
+constexpr int BA_KCH = 16; // k-steps per item at most
+__global__ __launch_bounds__(64 * BA_SW) void k_ba_spgemm(BAArena A) {
+    const int p = blockIdx.y;
+    const BADesc d = A.desc[p];
+    const int it = blockIdx.x * BA_SW + (threadIdx.x >> 6);
+    if (it >= d.nitems) return;
+    if (A.st[p].round >= 2) return;
+    const int4 item = A.items[d.item0 + it];
+    const int l = threadIdx.x & 63, kr = l >> 4, cl = l & 15;
+    const double* Ht = A.panel + d.panel0;
+    const double* Wt = Ht + (size_t)d.K * d.npad;
+    const int32_t* kl = A.klist + d.kl0;
+    const int ca = 16 * item.x + cl, cw = 16 * item.y + cl;
+    // every k-step's operands in flight at once (an item holds at most
+    // BA_KCH k-steps), then the MFMA chain
+    double a[BA_KCH], w[BA_KCH];
+#pragma unroll
+    for (int u = 0; u < BA_KCH; u++) {
+        a[u] = 0.0;
+        w[u] = 0.0;
+        if (item.z + u < item.w) {
+            const size_t r = (size_t)(4 * kl[item.z + u] + kr) * d.npad;
+            a[u] = Ht[r + ca];
+            w[u] = Wt[r + cw];
+        }
+    }
+    d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < BA_KCH; u++)
+        if (item.z + u < item.w) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], w[u], acc, 0, 0, 0);
+    double* out = A.tiles + ((size_t)d.item0 + it) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; r++) out[(kr + 4 * r) * 16 + cl] = acc[r];
+}
+
 __device__ __forceinline__ int tri(int i) { return i * (i + 1) / 2; }
 
-// Split sums in split order: Ssum = [S lower packed (n(n+1)/2) | column n (n)].
+// Item sums in item order: Ssum = [S lower packed (n(n+1)/2) | column n (n)].
 __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
     const int p = blockIdx.y;
     const BADesc d = A.desc[p];
@@ -566,9 +614,26 @@ __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
         t = ti >= tdb ? tri(ti) + tdb : nt * (nt + 1) / 2 + ti;
         e = (i & 15) * 16 + (n & 15);
     }
-    const double* tiles = A.tiles + (size_t)d.tile0 * 256;
     double g = 0.0;
-    for (int s = 0; s < d.nsplit; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
+    if (d.nitems < 0) {  // dense split-K GEMM (large batches): split sums in split order
+        const double* tiles = A.tiles + (size_t)d.tile0 * 256;
+        for (int s = 0; s < d.nsplit; s++) g += tiles[((size_t)s * d.ntiles + t) * 256 + e];
+        A.Ssum[(size_t)d.ss0 + u] = g;
+        return;
+    }
+    const double* part = A.tiles + (size_t)d.item0 * 256;
+    const int32_t* tp = A.tile_iptr + d.tip0;
+    // item order, loads eight at a time (independent), adds in sequence
+    const int i0 = tp[t], i1 = tp[t + 1];
+    int it = i0;
+    for (; it + 8 <= i1; it += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = part[(size_t)(it + q) * 256 + e];
+#pragma unroll
+        for (int q = 0; q < 8; q++) g += v[q];
+    }
+    for (; it < i1; it++) g += part[(size_t)it * 256 + e];
     A.Ssum[(size_t)d.ss0 + u] = g;
 }
 
@@ -1054,6 +1119,8 @@ struct gf_ba_plan {
     int nprob = 0;
     std::vector<BADesc> desc;
     int max_nwg = 1, max_free = 1, max_tiles = 1, max_newg = 1, max_split = 1, max_ss = 1, max_npad = 16;
+    int max_items = 1;
+    bool sparse_gemm = true;  // task-list Schur GEMM (small batches); dense split-K otherwise
     size_t panel_doubles = 0;
     BAArena A{};
     std::vector<void*> owned;
@@ -1068,8 +1135,8 @@ namespace {
 int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
     const BAArena& A = P->A;
     const int B = P->nprob;
-    const dim3 gpt(P->max_nwg, B), gpose(P->max_free, B), gedge(P->max_newg, B), ggemm(P->max_split, B),
-        gred((P->max_ss + 255) / 256, B);
+    const dim3 gpt(P->max_nwg, B), gpose(P->max_free, B), gedge(P->max_newg, B),
+        ggemm((P->max_items + BA_SW - 1) / BA_SW, B), gred((P->max_ss + 255) / 256, B);
     {
         GF_PROF(P->ctx, s, "k_ba_linearize");
         k_ba_linearize<<<gpt, BA_T, 0, s>>>(A);
@@ -1084,7 +1151,10 @@ int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
     }
     {
         GF_PROF(P->ctx, s, "k_ba_gemm");
-        k_ba_gemm<<<ggemm, 64 * BA_GW, ba_gemm_lds(P->max_npad), s>>>(A);
+        if (P->sparse_gemm)
+            k_ba_spgemm<<<ggemm, 64 * BA_SW, 0, s>>>(A);
+        else
+            k_ba_gemm<<<dim3(P->max_split, B), 64 * BA_GW, ba_gemm_lds(P->max_npad), s>>>(A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_gemm_reduce");
@@ -1129,6 +1199,14 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     std::vector<double> e_meas;
     std::vector<float> kf_T, pt_pos;
     std::vector<uint16_t> kmask;
+    std::vector<int4> items;
+    std::vector<int32_t> klist, tile_iptr;
+    // k-steps per item: short runs keep a single window's GEMM spread over the chip
+    const int kch = BA_KCH;
+    // few windows: the task list (only the nonzero tile products; 3.97 -> 3.64 ms
+    // per window alone); many windows: the dense split-K product streams the
+    // panels, which beats scattered 128-byte reads once they leave the caches
+    const bool sparse = nprob <= 8;
     const int nsplit = std::max(1, std::min(BA_MAXSPLIT, (256 + std::max(nprob, 1) - 1) / std::max(nprob, 1)));
     int ss_tot = 0;
     std::vector<uint8_t> kf_kind;
@@ -1231,6 +1309,42 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
                 const uint16_t bits = (uint16_t)((1u << ((6 * c) >> 4)) | (1u << ((6 * c + 5) >> 4)));
                 for (int r = 3 * i; r < 3 * i + 3; r++) kmask[d.mask0 + r / 4] |= bits;
             }
+        d.nitems = -1;
+        if (sparse) {  // the GEMM task list: per output tile, the k-steps where both operand tiles are nonzero
+            const int tdb = d.n >> 4, lower = nt * (nt + 1) / 2;
+            d.item0 = (int)items.size();
+            d.kl0 = (int)klist.size();
+            d.tip0 = (int)tile_iptr.size();
+            int nloc = 0;
+            std::vector<int> ks;
+            for (int t = 0; t < d.ntiles; t++) {
+                int ti, tj;
+                if (t < lower) {
+                    int a = 0;
+                    while ((a + 1) * (a + 2) / 2 <= t) a++;
+                    ti = a;
+                    tj = t - a * (a + 1) / 2;
+                } else {
+                    ti = t - lower;
+                    tj = tdb;
+                }
+                tile_iptr.push_back(nloc);
+                ks.clear();
+                for (int k = 0; k < steps; k++) {
+                    const unsigned m = kmask[d.mask0 + k], mb = m | (1u << tdb);
+                    if (m && ((m >> ti) & (mb >> tj) & 1u)) ks.push_back(k);
+                }
+                for (size_t c = 0; c < ks.size(); c += kch) {
+                    const int kb = (int)klist.size() - d.kl0;
+                    const int ke = kb + (int)std::min<size_t>(kch, ks.size() - c);
+                    for (size_t q = c; q < c + (size_t)(ke - kb); q++) klist.push_back(ks[q]);
+                    items.push_back(make_int4(ti, tj, kb, ke));
+                    nloc++;
+                }
+            }
+            tile_iptr.push_back(nloc);
+            d.nitems = nloc;
+        }
         nkf_tot += Q.nkf;
         npt_tot += Q.npts;
         ne_tot += Q.nedges;
@@ -1253,7 +1367,9 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         P->max_split = std::max(P->max_split, d.nsplit);
         P->max_ss = std::max(P->max_ss, d.n * (d.n + 1) / 2 + d.n);
         P->max_npad = std::max(P->max_npad, d.npad);
+        P->max_items = std::max(P->max_items, d.nitems);
     }
+    P->sparse_gemm = sparse;
     P->panel_doubles = (size_t)panel;
     BAArena& A = P->A;
     A.nkf_tot = nkf_tot;
@@ -1263,6 +1379,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     BAState* ds;
     double *kfT, *ptX, *Hll, *bl, *Dinv, *xl, *e_err, *Hpl, *Hpp, *bp, *xp, *pnl, *tiles, *w0, *w1, *w2, *w3, *ssum;
     uint16_t* kmk;
+    int4* itm;
+    int32_t *kls, *tip;
     float *kT0, *pX0, *oT, *oX;
     uint8_t *kk, *pa, *ea, *eo, *fa;
     int32_t *kc, *peb, *pee, *ept, *ekf, *fkf, *fep, *fel;
@@ -1281,11 +1399,12 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         (rc = dalloc(&fep, f_eptr.size(), o)) || (rc = dalloc(&fel, f_elist.size(), o)) ||
         (rc = dalloc(&Hpp, 36 * (size_t)nf_tot, o)) || (rc = dalloc(&bp, 6 * (size_t)nf_tot, o)) ||
         (rc = dalloc(&xp, 6 * (size_t)nf_tot, o)) || (rc = dalloc(&fa, nf_tot, o)) ||
-        (rc = dalloc(&pnl, P->panel_doubles, o)) || (rc = dalloc(&tiles, 256 * (size_t)ntile_tot, o)) ||
+        (rc = dalloc(&pnl, P->panel_doubles, o)) || (rc = dalloc(&tiles, 256 * std::max<size_t>(sparse ? items.size() : (size_t)ntile_tot, 1), o)) ||
         (rc = dalloc(&w0, nwg_tot, o)) || (rc = dalloc(&w1, nwg_tot, o)) || (rc = dalloc(&w2, nwg_tot, o)) ||
         (rc = dalloc(&w3, nwg_tot, o)) || (rc = dalloc(&oT, 16 * (size_t)nkf_tot, o)) ||
         (rc = dalloc(&oX, 3 * (size_t)npt_tot, o)) || (rc = dalloc(&kmk, kmask.size(), o)) ||
-        (rc = dalloc(&ssum, ss_tot, o))) {
+        (rc = dalloc(&ssum, ss_tot, o)) || (rc = dalloc(&itm, items.size(), o)) ||
+        (rc = dalloc(&kls, klist.size(), o)) || (rc = dalloc(&tip, tile_iptr.size(), o))) {
         gf_ba_plan_destroy(P);
         return rc;
     }
@@ -1305,6 +1424,8 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
         (he = up(ekf, e_kf.data(), 4 * e_kf.size())) || (he = up(em, e_meas.data(), 8 * e_meas.size())) ||
         (he = up(fkf, f_kf.data(), 4 * f_kf.size())) || (he = up(fep, f_eptr.data(), 4 * f_eptr.size())) ||
         (he = up(fel, f_elist.data(), 4 * f_elist.size())) || (he = up(kmk, kmask.data(), 2 * kmask.size())) ||
+        (he = up(itm, items.data(), sizeof(int4) * items.size())) || (he = up(kls, klist.data(), 4 * klist.size())) ||
+        (he = up(tip, tile_iptr.data(), 4 * tile_iptr.size())) ||
         (he = hipStreamSynchronize(s))) {
         gf_ba_plan_destroy(P);
         return gf::fail(GF_ERR_HIP, hipGetErrorString(he));
@@ -1342,6 +1463,9 @@ int gf_ba_plan_create(gf_ctx* ctx, int nprob, const gf_ba_problem* probs, gf_ba_
     A.panel = pnl;
     A.tiles = tiles;
     A.kmask = kmk;
+    A.items = itm;
+    A.klist = kls;
+    A.tile_iptr = tip;
     A.Ssum = ssum;
     A.wg_chi = w0;
     A.wg_chi_t = w1;
