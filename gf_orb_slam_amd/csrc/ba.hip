@@ -47,7 +47,7 @@
 
 namespace {
 
-constexpr int BA_T = 256;     // threads of the point kernels
+constexpr int BA_T = 64;      // threads of the point / edge kernels (one wave: more CUs for one window)
 constexpr int BA_MAXSPLIT = 64;  // split-K of the Schur GEMM (per plan: more splits for small batches)
 constexpr int BA_MAXFREE = 32;
 constexpr int BA_MAXN = 6 * BA_MAXFREE;  // LDS of k_ba_solve
@@ -346,8 +346,10 @@ __global__ __launch_bounds__(BA_T) void k_ba_linearize(BAArena A) {
 }
 
 // ------------------------------------------------------------------ buildSystem, pose half
-__global__ __launch_bounds__(64) void k_ba_poses(BAArena A) {
-    const int p = blockIdx.y, a = blockIdx.x, lane = threadIdx.x;
+constexpr int BA_PT = 256;  // threads per free pose (k_ba_poses)
+__global__ __launch_bounds__(BA_PT) void k_ba_poses(BAArena A) {
+    __shared__ double sacc[BA_PT / 64][28];
+    const int p = blockIdx.y, a = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const BADesc d = A.desc[p];
     if (a >= d.nfree) return;
     const BAState st = A.st[p];
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(64) void k_ba_poses(BAArena A) {
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
     int cnt = 0;
     const int j0 = A.f_eptr[d.fe0 + a], j1 = A.f_eptr[d.fe0 + a + 1];
-    for (int j = j0 + lane; j < j1; j += 64) {
+    for (int j = j0 + (int)threadIdx.x; j < j1; j += BA_PT) {
         const int ge = d.e0 + A.f_elist[d.pl0 + j];
         if (!A.e_act[ge]) continue;
         cnt++;
@@ -391,6 +393,20 @@ __global__ __launch_bounds__(64) void k_ba_poses(BAArena A) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 27; k++) sacc[wv][k] = acc[k];
+        sacc[wv][27] = (double)cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 27; k++) {
+            double v = sacc[0][k];
+            for (int q = 1; q < BA_PT / 64; q++) v += sacc[q][k];
+            acc[k] = v;
+        }
+        cnt = 0;
+        for (int q = 0; q < BA_PT / 64; q++) cnt += (int)sacc[q][27];
         double* H = A.Hpp + (size_t)(d.f0 + a) * 36;
         int k = 0;
         for (int r = 0; r < 6; r++)
@@ -1143,7 +1159,7 @@ int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
     }
     {
         GF_PROF(P->ctx, s, "k_ba_poses");
-        k_ba_poses<<<gpose, 64, 0, s>>>(A);
+        k_ba_poses<<<gpose, BA_PT, 0, s>>>(A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_schur_pts");
