@@ -53,6 +53,23 @@ def kernel_bytes(camera: str, nfeat: int) -> dict:
     }
 
 
+class _StdoutToStderr:
+    """Send fd 1 to fd 2 for a block: RCCL prints its version banner on
+    stdout at communicator init, and the bench's stdout is one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -326,7 +343,8 @@ def main():
     # ---- start-up exchange (config 5): world, vocabulary, maps from rank 0 over RCCL
     t_su = time.perf_counter()
     ctx0 = Context(local)
-    gd = GfDist(ctx0, rank, world)
+    with _StdoutToStderr():
+        gd = GfDist(ctx0, rank, world)
     scenes, maps, world_ck, world_span, world_bytes = share_world(
         gd, rank, lambda: build_world(cam, B, S, args.period, args.nfeatures, args.map, local))
     voc = ORBVocabulary(synth.synth_vocabulary_fast(seed=7, k=10, L=6), ctx=ctx0) if rank == 0 else None
