@@ -6,7 +6,7 @@
 //
 //   k_resize  x (nlevels-1)  level l from level l-1 (cv::resize INTER_LINEAR,
 //                            11-bit fixed point; ComputePyramid :922-998)
-//   k_blur_fast              one 64x32 tile per workgroup: 7x7 sigma-2
+//   k_blur_fast              one 64x64 tile per workgroup: 7x7 sigma-2
 //                            Gaussian of every level (:842) and, from the same
 //                            LDS tile, the FAST-9 score map of the level
 //   k_fast_cells             one workgroup per (frame, grid cell): corners of
@@ -244,7 +244,7 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 }
 
 // -------------------------------------------------------------- k_blur_fast
-// One 64x32 tile of one level per 256-thread workgroup, its 3-px halo staged
+// One 64 x BT_H (64) tile of one level per 256-thread workgroup, its 3-px halo staged
 // in LDS once and used twice:
 //   * GaussianBlur 7x7 sigma 2 (reflect-101 border; ORBextractor.cc:842):
 //     integer row pass, column pass with the (s + 2^15) >> 16 cast;
@@ -272,9 +272,13 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 // out as one dword per quad and row. The planes are pitched to 64 B, so a
 // quad past the level's right edge writes the row padding.
 #define BT_W 64
-#define BT_H 32
+#ifndef BT_H
+#define BT_H 64
+#endif
 #define BT_R (BT_H + 6)   // source rows
 #define BT_SW (BT_W + 8)  // source row: 72 bytes = 18 dwords, x = X0 - 4 .. X0 + 67
+#define BT_NQ (BT_H / 32) // row blocks of 32 per thread (quad x 2 rows each)
+#define BT_U32 ((BT_R / 2) * BT_W > BT_W * BT_H / 2 ? (BT_R / 2) * BT_W : BT_W * BT_H / 2)
 
 typedef short gf_i16x2 __attribute__((ext_vector_type(2)));
 
@@ -300,10 +304,13 @@ __device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgc
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
     __shared__ __align__(16) uint8_t src[BT_R][BT_SW];
-    __shared__ __align__(16) uint32_t rows2[BT_R / 2][BT_W];  // row sums of rows 2p | 2p+1 << 16
+    // the row sums (rows 2p | 2p+1 << 16) are dead once the column pass has
+    // read them; the candidate list, written after the scan's barriers, reuses them
+    __shared__ __align__(16) uint32_t u32buf[BT_U32];
     __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
-    __shared__ uint16_t cand[BT_W * BT_H];
     __shared__ int scan_tmp[4];
+    uint32_t(*rows2)[BT_W] = reinterpret_cast<uint32_t(*)[BT_W]>(u32buf);
+    uint16_t* cand = reinterpret_cast<uint16_t*>(u32buf);
     int t, f;
     gfd::xcd_block(t, f);
     const int tid = threadIdx.x;
@@ -317,29 +324,34 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     int stride;
     const uint8_t* S = level_plane(P, g, f, l, stride);
     {
-        // 38 rows x 18 dwords; rows reflect-101 at the top and bottom. A dword
-        // inside the level row (with the next 4 bytes: the realignment's second
-        // load) comes as aligned loads; the x-border ones byte by byte through
-        // reflect-101.
-        constexpr int NT = BT_R * (BT_SW / 4), NI = (NT + 255) / 256;
+        // BT_R rows x 18 dwords. Thread (lr, lq) = (tid / 18, tid % 18) owns
+        // dword column lq of rows lr, lr + 14, ... (252 threads, 14 rows a
+        // sweep), so its x range, border test and LDS column are fixed. Rows
+        // reflect-101 at the top and bottom (a uniform test per tile). A dword
+        // inside the level row comes as two aligned loads realigned with
+        // v_alignbyte (the level rows are unpadded, so the byte shift varies
+        // by row); the x-border ones byte by byte through reflect-101.
+        constexpr int NQD = BT_SW / 4, LR = 256 / NQD, NI = (BT_R + LR - 1) / LR;
+        const int lr = tid / NQD, lq = tid - lr * NQD;
+        const int x0 = X0 - 4 + 4 * lq;
+        const bool xin = x0 >= 0 && x0 + 8 <= w;
+        const bool yin = Y0 >= 3 && Y0 + BT_R - 3 <= h;
         uint32_t lo[NI], hi[NI];
         int sh[NI];
 #pragma unroll
         for (int k = 0; k < NI; k++) {
-            const int i = tid + 256 * k;
+            const int ry = lr + LR * k;
             lo[k] = hi[k] = 0u;
             sh[k] = 0;
-            if (i < NT) {
-                const int ry = i / (BT_SW / 4), q = i - ry * (BT_SW / 4);
-                const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                const int x0 = X0 - 4 + 4 * q;
+            if (lr < LR && ry < BT_R) {
+                const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
                 const uint8_t* row = S + (long long)yy * stride;
-                if (x0 >= 0 && x0 + 8 <= w) {
+                if (xin) {
                     const uintptr_t a = (uintptr_t)(row + x0);
                     const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
                     sh[k] = (int)(a & 3);
                     lo[k] = al[0];
-                    hi[k] = sh[k] ? al[1] : 0u;  // al[1] holds needed bytes whenever sh != 0
+                    hi[k] = al[1];  // bytes x0 + 4 .. x0 + 7 lie inside the row
                 } else {
 #pragma unroll
                     for (int j = 0; j < 4; j++)
@@ -347,42 +359,48 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
                 }
             }
         }
+        uint32_t* s32 = reinterpret_cast<uint32_t*>(&src[0][0]) + lr * NQD + lq;
 #pragma unroll
-        for (int k = 0; k < NI; k++) {
-            const int i = tid + 256 * k;
-            if (i < NT) reinterpret_cast<uint32_t*>(&src[0][0])[i] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
-        }
+        for (int k = 0; k < NI; k++)
+            if (lr < LR && lr + LR * k < BT_R) s32[LR * NQD * k] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
     }
     __syncthreads();
     // taps round(256 * gaussian(7, sigma 2)) = 18 34 49 55 49 34 18
-    constexpr uint32_t KLO = 18u | 34u << 8 | 49u << 16 | 55u << 24, KHI = 49u | 34u << 8 | 18u << 16;
+    // output x = X0 + 4q + j takes LDS columns 4q + 1 + j .. 4q + 7 + j, i.e.
+    // bytes of the row's dwords q, q + 1, q + 2 (w0, w1, w2): per j a chain of
+    // v_dot4_u32_u8 with the taps placed at those byte lanes (no realignment)
+    constexpr uint32_t T0_0 = 18u << 8 | 34u << 16 | 49u << 24, T0_1 = 55u | 49u << 8 | 34u << 16 | 18u << 24;
+    constexpr uint32_t T1_0 = 18u << 16 | 34u << 24, T1_1 = 49u | 55u << 8 | 49u << 16 | 34u << 24, T1_2 = 18u;
+    constexpr uint32_t T2_0 = 18u << 24, T2_1 = 34u | 49u << 8 | 55u << 16 | 49u << 24, T2_2 = 34u | 18u << 8;
+    constexpr uint32_t T3_1 = 18u | 34u << 8 | 49u << 16 | 55u << 24, T3_2 = 49u | 34u << 8 | 18u << 16;
     // row pass, two source rows per item; a row sum is at most 257 * 255 =
     // 65535, so the two rows share a dword (row 2p low, 2p + 1 high)
     for (int i = tid; i < (BT_R / 2) * (BT_W / 4); i += 256) {
         const int pr = i >> 4, q = i & 15;
         uint4 o;
-        auto hsum = [&](int ry, int j) -> uint32_t {  // output x = X0 + 4q + j: LDS columns 4q + 1 + j ..
+        auto hsum = [&](int ry, int j) -> uint32_t {
             const uint32_t* r32 = reinterpret_cast<const uint32_t*>(&src[ry][0]) + q;
             const uint32_t w0 = r32[0], w1 = r32[1], w2 = r32[2];
-            const uint32_t lo = j == 3 ? w1 : __builtin_amdgcn_alignbyte(w1, w0, j + 1);
-            const uint32_t hi = j == 3 ? w2 : __builtin_amdgcn_alignbyte(w2, w1, j + 1);
-            return __builtin_amdgcn_udot4(lo, KLO, 0u, false) + __builtin_amdgcn_udot4(hi, KHI, 0u, false);
+            if (j == 0) return __builtin_amdgcn_udot4(w1, T0_1, __builtin_amdgcn_udot4(w0, T0_0, 0u, false), false);
+            if (j == 1)
+                return __builtin_amdgcn_udot4(
+                    w2, T1_2, __builtin_amdgcn_udot4(w1, T1_1, __builtin_amdgcn_udot4(w0, T1_0, 0u, false), false),
+                    false);
+            if (j == 2)
+                return __builtin_amdgcn_udot4(
+                    w2, T2_2, __builtin_amdgcn_udot4(w1, T2_1, __builtin_amdgcn_udot4(w0, T2_0, 0u, false), false),
+                    false);
+            return __builtin_amdgcn_udot4(w2, T3_2, __builtin_amdgcn_udot4(w1, T3_1, 0u, false), false);
         };
-        o.x = hsum(2 * pr, 0) | hsum(2 * pr + 1, 0) << 16;
-        o.y = hsum(2 * pr, 1) | hsum(2 * pr + 1, 1) << 16;
-        o.z = hsum(2 * pr, 2) | hsum(2 * pr + 1, 2) << 16;
-        o.w = hsum(2 * pr, 3) | hsum(2 * pr + 1, 3) << 16;
+        // low halves of the two rows' sums into one dword (one v_perm_b32)
+        o.x = __builtin_amdgcn_perm(hsum(2 * pr + 1, 0), hsum(2 * pr, 0), 0x05040100u);
+        o.y = __builtin_amdgcn_perm(hsum(2 * pr + 1, 1), hsum(2 * pr, 1), 0x05040100u);
+        o.z = __builtin_amdgcn_perm(hsum(2 * pr + 1, 2), hsum(2 * pr, 2), 0x05040100u);
+        o.w = __builtin_amdgcn_perm(hsum(2 * pr + 1, 3), hsum(2 * pr, 3), 0x05040100u);
         *reinterpret_cast<uint4*>(&rows2[pr][4 * q]) = o;
     }
     __syncthreads();
-    const int qx = tid & 15, r0 = 2 * (tid >> 4), x = X0 + 4 * qx;
-    // column pass: row pairs r0 / 2 .. + 3 (rows r0 .. r0 + 7) give output rows
-    // r0 and r0 + 1, four v_dot2_u32_u16 per pixel (the rounding bias as the
-    // accumulator's start)
-    uint4 rp[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) rp[k] = *reinterpret_cast<const uint4*>(&rows2[(r0 >> 1) + k][4 * qx]);
-    uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
+    const int qx = tid & 15, x = X0 + 4 * qx;
     typedef unsigned short gf_u16x2 __attribute__((ext_vector_type(2)));
     auto u2 = [](uint32_t v) { return __builtin_bit_cast(gf_u16x2, v); };
     const gf_u16x2 A0 = {18, 34}, A1 = {49, 55}, A2 = {49, 34}, A3 = {18, 0};  // output row r0
@@ -395,43 +413,54 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         a = __builtin_amdgcn_udot2(u2(p3), c3, a, false);
         return min(a >> 16, 255u);
     };
-    const uint32_t a0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, A0, A1, A2, A3);
-    const uint32_t a1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, A0, A1, A2, A3);
-    const uint32_t a2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, A0, A1, A2, A3);
-    const uint32_t a3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, A0, A1, A2, A3);
-    const uint32_t b0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, B0, B1, B2, B3);
-    const uint32_t b1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, B0, B1, B2, B3);
-    const uint32_t b2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, B0, B1, B2, B3);
-    const uint32_t b3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, B0, B1, B2, B3);
-    if (Y0 + r0 < h) *reinterpret_cast<uint32_t*>(D) = a0 | a1 << 8 | a2 << 16 | a3 << 24;
-    if (Y0 + r0 + 1 < h) *reinterpret_cast<uint32_t*>(D + pw) = b0 | b1 << 8 | b2 << 16 | b3 << 24;
-    // compass pre-test of the quad in rows r0, r0 + 1 (LDS rows r0 + 3, r0 + 4)
     const uint32_t th2 = (uint32_t)map_th * 0x00010001u;
     uint32_t xm = 0;  // pixels of the quad at least 3 px inside the level, in x
 #pragma unroll
     for (int i = 0; i < 4; i++) xm |= (uint32_t)(x + i >= 3 && x + i < w - 3) << i;
-    int mask = 0;
+    int mask = 0;  // bit 8k + 4r + i: pixel i of the quad in row 32k + r0 + r
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-        const uint32_t* c32 = reinterpret_cast<const uint32_t*>(&src[r0 + r + 3][0]) + qx;
-        const uint32_t L = c32[0], V = c32[1], R = c32[2];
-        const uint32_t U = reinterpret_cast<const uint32_t*>(&src[r0 + r][0])[qx + 1];      // dy = -3 (ring 8)
-        const uint32_t Dn = reinterpret_cast<const uint32_t*>(&src[r0 + r + 6][0])[qx + 1];  // dy = +3 (ring 0)
-        const uint32_t Rt = __builtin_amdgcn_alignbyte(R, V, 3), Lt = __builtin_amdgcn_alignbyte(V, L, 1);
-        const uint32_t e = compass2(bytes02(V), bytes02(Dn), bytes02(Rt), bytes02(U), bytes02(Lt), th2);
-        const uint32_t o = compass2(bytes13(V), bytes13(Dn), bytes13(Rt), bytes13(U), bytes13(Lt), th2);
-        uint32_t m = ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
-        const int y = Y0 + r0 + r;
-        m &= (y >= 3 && y < h - 3) ? xm : 0u;
-        mask |= (int)m << (4 * r);
-        sco[r0 + r][qx] = 0u;
+    for (int k = 0; k < BT_NQ; k++) {
+        const int r0 = 2 * (tid >> 4) + 32 * k;
+        // column pass: row pairs r0 / 2 .. + 3 (rows r0 .. r0 + 7) give output
+        // rows r0 and r0 + 1, four v_dot2_u32_u16 per pixel (the rounding bias
+        // as the accumulator's start)
+        uint4 rp[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) rp[j] = *reinterpret_cast<const uint4*>(&rows2[(r0 >> 1) + j][4 * qx]);
+        uint8_t* D = P.blur + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
+        const uint32_t a0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, A0, A1, A2, A3);
+        const uint32_t a1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, A0, A1, A2, A3);
+        const uint32_t a2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, A0, A1, A2, A3);
+        const uint32_t a3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, A0, A1, A2, A3);
+        const uint32_t b0 = colv(rp[0].x, rp[1].x, rp[2].x, rp[3].x, B0, B1, B2, B3);
+        const uint32_t b1 = colv(rp[0].y, rp[1].y, rp[2].y, rp[3].y, B0, B1, B2, B3);
+        const uint32_t b2 = colv(rp[0].z, rp[1].z, rp[2].z, rp[3].z, B0, B1, B2, B3);
+        const uint32_t b3 = colv(rp[0].w, rp[1].w, rp[2].w, rp[3].w, B0, B1, B2, B3);
+        if (Y0 + r0 < h) *reinterpret_cast<uint32_t*>(D) = a0 | a1 << 8 | a2 << 16 | a3 << 24;
+        if (Y0 + r0 + 1 < h) *reinterpret_cast<uint32_t*>(D + pw) = b0 | b1 << 8 | b2 << 16 | b3 << 24;
+        // compass pre-test of the quad in rows r0, r0 + 1 (LDS rows r0 + 3, r0 + 4)
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t* c32 = reinterpret_cast<const uint32_t*>(&src[r0 + r + 3][0]) + qx;
+            const uint32_t L = c32[0], V = c32[1], R = c32[2];
+            const uint32_t U = reinterpret_cast<const uint32_t*>(&src[r0 + r][0])[qx + 1];      // dy = -3 (ring 8)
+            const uint32_t Dn = reinterpret_cast<const uint32_t*>(&src[r0 + r + 6][0])[qx + 1];  // dy = +3 (ring 0)
+            const uint32_t Rt = __builtin_amdgcn_alignbyte(R, V, 3), Lt = __builtin_amdgcn_alignbyte(V, L, 1);
+            const uint32_t e = compass2(bytes02(V), bytes02(Dn), bytes02(Rt), bytes02(U), bytes02(Lt), th2);
+            const uint32_t o = compass2(bytes13(V), bytes13(Dn), bytes13(Rt), bytes13(U), bytes13(Lt), th2);
+            uint32_t m = ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
+            const int y = Y0 + r0 + r;
+            m &= (y >= 3 && y < h - 3) ? xm : 0u;
+            mask |= (int)m << (8 * k + 4 * r);
+            sco[r0 + r][qx] = 0u;
+        }
     }
     int nc;
     int pos = block_scan_256(__popc(mask), scan_tmp, nc);  // its barriers also order the sco zeroing
     while (mask) {
         const int b = __ffs(mask) - 1;
         mask &= mask - 1;
-        cand[pos++] = (uint16_t)((r0 + (b >> 2)) * BT_W + 4 * qx + (b & 3));
+        cand[pos++] = (uint16_t)((2 * (tid >> 4) + 32 * (b >> 3) + ((b >> 2) & 1)) * BT_W + 4 * qx + (b & 3));
     }
     __syncthreads();
     uint8_t* sc8 = reinterpret_cast<uint8_t*>(&sco[0][0]);
@@ -443,10 +472,14 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         sc8[q] = M > map_th ? (uint8_t)M : 0;
     }
     __syncthreads();
-    uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
 #pragma unroll
-    for (int r = 0; r < 2; r++)
-        if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(SC + (long long)r * pw) = sco[r0 + r][qx];
+    for (int k = 0; k < BT_NQ; k++) {
+        const int r0 = 2 * (tid >> 4) + 32 * k;
+        uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(Y0 + r0) * pw + x;
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+            if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(SC + (long long)r * pw) = sco[r0 + r][qx];
+    }
 }
 
 // -------------------------------------------------------------- k_fast_cells

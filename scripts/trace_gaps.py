@@ -6,6 +6,8 @@ import sys
 from collections import defaultdict
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+for r in rows:
+    r["Kernel_Name"] = r["Kernel_Name"].replace("(anonymous namespace)::", "")
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 50
 starts = [i for i, r in enumerate(rows) if r["Kernel_Name"].split("(")[0].endswith("k_fe_begin")]
 sel = rows[starts[-N - 1]:starts[-1]]
