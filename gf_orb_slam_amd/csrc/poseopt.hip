@@ -31,6 +31,23 @@ constexpr int PO_TP = PO_T + 1;  // term row pitch (doubles): accumulator thread
 constexpr int PO_STRIDE_MAX = 8192;
 constexpr int PO_LDS_EDGES = 384;  // problems up to this size keep edges and residuals in LDS (18 KB)
 
+// Phase timing (diagnostic build only: -DGF_POSE_STAMPS): problem 0, lane 0
+// accumulates s_memrealtime ticks (100 MHz) per phase and prints them.
+#ifdef GF_POSE_STAMPS
+#define PO_ST_DECL unsigned long long _st_prev = wall_clock64(), _st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PO_ST(i)                                           \
+    do {                                                   \
+        const unsigned long long _n = wall_clock64();      \
+        _st[i] += _n - _st_prev;                           \
+        _st_prev = _n;                                     \
+    } while (0)
+#else
+#define PO_ST_DECL
+#define PO_ST(i) \
+    do {         \
+    } while (0)
+#endif
+
 struct PoseArgs {
     const gf_pose_edge* edges;
     const int32_t* nedges;
@@ -73,6 +90,42 @@ __device__ __forceinline__ void edge_error(const Lane& L, const gfse3::SE3& T, i
     const double px = pc[0] / pc[2], py = pc[1] / pc[2];
     r0 = (double)g.z[0] - (px * L.fx + L.cx);
     r1 = (double)g.z[1] - (py * L.fy + L.cy);
+}
+
+// acc += row[0] + ... + row[m - 1], one dependent add per term in order
+// (the reference's sequential sum); the next 8 terms' LDS loads are issued
+// before the current 8 are added, so the chain waits on the adds only. Loads
+// are unconditional (a tail past m reads neighbouring LDS, not added) so the
+// compiler can count them.
+__device__ __forceinline__ double chain_sum(const double* row, int m, double acc) {
+    // two named buffers alternate (no register rotation, so no wait for the
+    // batch in flight before the adds)
+    double a[8], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) a[u] = row[u];
+    for (int j = 8;; j += 16) {
+        if (j >= m) {  // a holds terms j - 8 .. m - 1
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (j - 8 + u < m) acc += a[u];
+            break;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) b[u] = row[j + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += a[u];
+        if (j + 8 >= m) {  // b holds terms j .. m - 1
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (j + u < m) acc += b[u];
+            break;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) a[u] = row[j + 8 + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc += b[u];
+    }
+    return acc;
 }
 
 // computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
@@ -120,17 +173,7 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
         __syncthreads();
         const int m = min(PO_T, L.n - base);
         if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
-            // edge order, one dependent add per edge; loads batched ahead of the chain
-            const double* row = term[L.l];
-            int j = 0;
-            for (; j + 8 <= m; j += 8) {
-                double v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = row[j + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) acc += v[u];
-            }
-            for (; j < m; j++) acc += row[j];
+            acc = chain_sum(term[L.l], m, acc);
         }
         __syncthreads();
     }
@@ -190,16 +233,7 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
         __syncthreads();
         const int m = min(PO_T, L.n - base);
         if (L.l < PO_CHI + S) {
-            const double* row = term[L.l];
-            int j = 0;
-            for (; j + 8 <= m; j += 8) {
-                double v[8];
-#pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = row[j + u];
-#pragma unroll
-                for (int u = 0; u < 8; u++) acc += v[u];
-            }
-            for (; j < m; j++) acc += row[j];
+            acc = chain_sum(term[L.l], m, acc);
         }
         __syncthreads();
     }
@@ -218,6 +252,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
     __shared__ gf_pose_edge sh_edges[PO_LDS_EDGES];
     __shared__ double sh_info[PO_LDS_EDGES];
     const int p = blockIdx.x;
+    PO_ST_DECL
     Lane L;
     L.l = threadIdx.x;
     L.n = min(max(A.nedges[p], 0), A.stride);
@@ -269,7 +304,9 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
         bool have_build = false;  // sh_sum already holds H, b, chi2 at T (trial 0 accepted)
         for (int iter = 0; iter < its; iter++) {
             total_it++;
+            PO_ST(0);
             if (!have_build) pass(L, T, true, term, sh_sum);
+            PO_ST(1);
             have_build = false;
             double H[36], b[6];
             for (int a = 0, k = 0; a < 6; a++)
@@ -321,6 +358,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
                     }
                 }
                 __syncthreads();
+                PO_ST(2);
                 // a failed factorisation keeps the previous solution (Solver::_x):
                 // trial g solves with the last successful x among trials <= g
                 {
@@ -335,7 +373,9 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
                     }
                 }
                 __syncthreads();
+                PO_ST(3);
                 pass_trials(L, sh_T, S, term, sh_sum);
+                PO_ST(4);
                 for (int s2 = 0; s2 < S; s2++) {
                     const bool ok = sh_ok[s2];
                     if (ok)
@@ -368,6 +408,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
                     }
                 }
             }
+            PO_ST(5);
             if (q == 10 || rho == 0) break;
             if ((iniChi - currentChi) * 1e3 < iniChi)
                 nBad++;
@@ -404,6 +445,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
         }
         nBadEdges = nb;
         __syncthreads();
+        PO_ST(6);
         if (L.n < 10) break;
     }
 
@@ -420,6 +462,11 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
         Tp[15] = 1.f;
         A.ninl[p] = L.n - nBadEdges;
         if (A.iters) A.iters[p] = total_it;
+#ifdef GF_POSE_STAMPS
+        if (p == 0)
+            printf("POSE_STAMPS n=%d it=%d pre=%llu build=%llu ldlt=%llu exp=%llu trials=%llu dec=%llu class=%llu\n",
+                   L.n, total_it, _st[0], _st[1], _st[2], _st[3], _st[4], _st[5], _st[6]);
+#endif
     }
     if (A.kp_outl)
         for (int e = L.l; e < L.n; e += PO_T)

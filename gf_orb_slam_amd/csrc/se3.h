@@ -42,7 +42,27 @@ SE3_HD void normalize(Quat& q) {
     q.w /= n;
 }
 
-// Eigen quaternionbase_assign_impl<Matrix3>; R row-major.
+// Eigen quaternionbase_assign_impl<Matrix3>; R row-major. The branch on the
+// largest diagonal entry i is expanded into three compile-time cases (the
+// same arithmetic), so m is never indexed by a run-time value: on the device
+// that would put the matrix in scratch memory.
+template <int I>
+SE3_HD Quat from_R_diag(const double* m) {
+    constexpr int J = (I + 1) % 3, K = (J + 1) % 3;
+    double t = sqrt(m[4 * I] - m[4 * J] - m[4 * K] + 1.0);
+    double c[3];
+    c[I] = 0.5 * t;
+    t = 0.5 / t;
+    Quat q;
+    q.w = (m[3 * K + J] - m[3 * J + K]) * t;
+    c[J] = (m[3 * J + I] + m[3 * I + J]) * t;
+    c[K] = (m[3 * K + I] + m[3 * I + K]) * t;
+    q.x = c[0];
+    q.y = c[1];
+    q.z = c[2];
+    return q;
+}
+
 SE3_HD Quat from_R(const double* m) {
     Quat q;
     double t = m[0] + (m[4] + m[8]);
@@ -56,18 +76,8 @@ SE3_HD Quat from_R(const double* m) {
     } else {
         int i = 0;
         if (m[4] > m[0]) i = 1;
-        if (m[8] > m[4 * i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[4 * i] - m[4 * j] - m[4 * k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (m[3 * k + j] - m[3 * j + k]) * t;
-        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-        q.x = c[0];
-        q.y = c[1];
-        q.z = c[2];
+        if (m[8] > (i ? m[4] : m[0])) i = 2;
+        q = i == 0 ? from_R_diag<0>(m) : i == 1 ? from_R_diag<1>(m) : from_R_diag<2>(m);
     }
     return q;
 }
