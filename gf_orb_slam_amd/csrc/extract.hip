@@ -563,11 +563,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
     uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 15) & ~15));  // survivor bits
     const int l = ci.level, lw = g.pw[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
-    // the window as aligned dwords, 16 loads per thread in flight before the LDS writes
-    for (int i0 = 0; i0 < dh * ndw; i0 += 256 * 16) {
-        uint32_t v[16];
+    // the window as aligned dwords (a cell window is a few hundred dwords: two
+    // loads per thread in flight before the LDS writes)
+    constexpr int FC_LB = 2;
+    for (int i0 = 0; i0 < dh * ndw; i0 += 256 * FC_LB) {
+        uint32_t v[FC_LB];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
+        for (int k = 0; k < FC_LB; k++) {
             const int i = i0 + 256 * k + tid;
             const int r = i / ndw, q = i - r * ndw;
             v[k] = 0;
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
             }
         }
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
+        for (int k = 0; k < FC_LB; k++) {
             const int i = i0 + 256 * k + tid;
             if (i < dh * ndw) reinterpret_cast<uint32_t*>(sc)[i] = v[k];
         }
