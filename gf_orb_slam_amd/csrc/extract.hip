@@ -494,47 +494,59 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 // column, keeping the three rows it compares in registers (three LDS reads a
 // pixel); survivors set their bit in an LDS bit array (bit = row-major pixel
 // index). Listing: a workgroup scan over the popcounts of the bit words.
+// (Cell windows are at most ~40 px wide, so one strip.)
 __device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buffer value at th
     const int S = m - 1;  // entries are S + 1 for corners at the map threshold, 0 otherwise
     return S >= th ? S : 0;
 }
 
-// sc: the window rows as loaded (row y at byte y * pitch + rsh[y]).
+// sc: the window rows as loaded (row y at byte y * pitch + rsh[y]). Every LDS
+// read is unconditional (addresses clamped into the window, out-of-window
+// values replaced by 0 afterwards) and each row's base offset is read one
+// step before the row itself, so a row step issues its reads together and
+// waits once, not once per read.
 __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* rsh, int pitch, uint32_t* bits, int dw,
                                              int dh, int th) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int ya = wv * dh / 4, yb = (wv + 1) * dh / 4;
     int cnt = 0;
-    // two 64-column strips per pass, walked together: their LDS reads are
-    // independent, so each row step waits for one latency, not two
-    for (int x0 = 0; x0 < dw; x0 += 128) {
-        const int xa = x0 + lane, xb = x0 + 64 + lane;
-        auto rd = [&](int y, int xx) -> int {
-            return (y >= 0 && y < dh && xx >= 0 && xx < dw) ? nms_at(sc[y * pitch + rsh[y] + xx], th) : 0;
+    // rows outside the window read row dh, a row of zeros with rsh[dh] = 0
+    auto rowi = [&](int y) -> int { return (y >= 0 && y < dh) ? y : dh; };
+    for (int x0 = 0; x0 < dw; x0 += 64) {
+        const int x = x0 + lane;
+        const bool okc = x < dw;
+        // lane masks (all ones inside the window) instead of conditions, so
+        // no read is predicated away behind a branch
+        const int ml = -(int)(x >= 1 && x - 1 < dw), mc = -(int)okc, mr = -(int)(x + 1 < dw);
+        const int cl = min(max(x - 1, 0), dw - 1), cc = min(x, dw - 1), cr = min(x + 1, dw - 1);
+        auto row3 = [&](int b, int& v0, int& v1, int& v2) {
+            const uint8_t* r = sc + b;
+            const int r0 = r[cl], r1 = r[cc], r2 = r[cr];
+            v0 = nms_at(r0, th) & ml;
+            v1 = nms_at(r1, th) & mc;
+            v2 = nms_at(r2, th) & mr;
         };
-        int ua0 = rd(ya - 1, xa - 1), ua1 = rd(ya - 1, xa), ua2 = rd(ya - 1, xa + 1);
-        int ca0 = rd(ya, xa - 1), ca1 = rd(ya, xa), ca2 = rd(ya, xa + 1);
-        int da0 = rd(ya + 1, xa - 1), da1 = rd(ya + 1, xa), da2 = rd(ya + 1, xa + 1);
-        int ub0 = rd(ya - 1, xb - 1), ub1 = rd(ya - 1, xb), ub2 = rd(ya - 1, xb + 1);
-        int cb0 = rd(ya, xb - 1), cb1 = rd(ya, xb), cb2 = rd(ya, xb + 1);
-        int db0 = rd(ya + 1, xb - 1), db1 = rd(ya + 1, xb), db2 = rd(ya + 1, xb + 1);
+        int u0, u1, u2, c0, c1, c2, d0, d1, d2;
+        {
+            const int i0 = rowi(ya - 1), i1 = rowi(ya), i2 = rowi(ya + 1);
+            row3(i0 * pitch + rsh[i0], u0, u1, u2);
+            row3(i1 * pitch + rsh[i1], c0, c1, c2);
+            row3(i2 * pitch + rsh[i2], d0, d1, d2);
+        }
+        int ie = rowi(ya + 2), se = rsh[ie];
         for (int y = ya; y < yb; y++) {
-            // row y + 2 is read one step ahead, so its LDS latency overlaps this step
-            const int ea0 = rd(y + 2, xa - 1), ea1 = rd(y + 2, xa), ea2 = rd(y + 2, xa + 1);
-            const int eb0 = rd(y + 2, xb - 1), eb1 = rd(y + 2, xb), eb2 = rd(y + 2, xb + 1);
-            const int mxa = max(max(max(ua0, ua1), max(ua2, ca0)), max(max(ca2, da0), max(da1, da2)));
-            const int mxb = max(max(max(ub0, ub1), max(ub2, cb0)), max(max(cb2, db0), max(db1, db2)));
-            const bool ka = xa < dw && ca1 != 0 && ca1 > mxa;
-            const bool kb = xb < dw && cb1 != 0 && cb1 > mxb;
-            if (ka) atomicOr(&bits[(y * dw + xa) >> 5], 1u << ((y * dw + xa) & 31));
-            if (kb) atomicOr(&bits[(y * dw + xb) >> 5], 1u << ((y * dw + xb) & 31));
-            cnt += __popcll(__ballot(ka)) + __popcll(__ballot(kb));
-            ua0 = ca0, ua1 = ca1, ua2 = ca2;
-            ca0 = da0, ca1 = da1, ca2 = da2;
-            da0 = ea0, da1 = ea1, da2 = ea2;
-            ub0 = cb0, ub1 = cb1, ub2 = cb2;
-            cb0 = db0, cb1 = db1, cb2 = db2;
-            db0 = eb0, db1 = eb1, db2 = eb2;
+            int e0, e1, e2;
+            row3(ie * pitch + se, e0, e1, e2);  // row y + 2, read one step ahead
+            const int in = rowi(y + 3), sn = rsh[in];  // its shift is used next step
+            const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
+            const bool keep = okc && c1 != 0 && c1 > mx;
+            if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
+            cnt += __popcll(__ballot(keep));
+            u0 = c0, u1 = c1, u2 = c2;
+            c0 = d0, c1 = d1, c2 = d2;
+            d0 = e0, d1 = e1, d2 = e2;
+            ie = in;
+            se = sn;
         }
     }
     return cnt;  // this wave's survivors
@@ -558,9 +570,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
     }
     const int n = dw * dh, nwords = (n + 31) >> 5;
     const int ndw = (dw + 6) >> 2, pitch = 4 * ndw;  // dwords per row: dw bytes at any alignment
-    uint8_t* sc = smem;                                                   // dh x pitch
-    uint8_t* rsh = sc + dh * pitch;                                        // dh row shifts
-    uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 15) & ~15));  // survivor bits
+    uint8_t* sc = smem;                                                   // (dh + 1) x pitch, row dh zeros
+    uint8_t* rsh = sc + (dh + 1) * pitch;                                  // dh + 1 row shifts
+    uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 16) & ~15));  // survivor bits
     const int l = ci.level, lw = g.pw[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
     // the window as aligned dwords (a cell window is a few hundred dwords: two
@@ -585,6 +597,8 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
         }
     }
     for (int r = tid; r < dh; r += 256) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)r * lw) & 3);
+    if (tid == 0) rsh[dh] = 0;
+    for (int i = tid; i < ndw; i += 256) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
     for (int i = tid; i < nwords; i += 256) bits[i] = 0;
     __syncthreads();
     int c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, fast_th);
@@ -1165,7 +1179,7 @@ static int plan_extractor(gf_extractor* ex) {
                         ci.cap_off = cap_off;
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
-                        size_t lds = (size_t)dh * (4 * (size_t)((dw + 6) / 4)) + (((size_t)dh + 15) & ~(size_t)15) +
+                        size_t lds = ((size_t)dh + 1) * (4 * (size_t)((dw + 6) / 4)) + (((size_t)dh + 16) & ~(size_t)15) +
                                      16 * (((size_t)dw * dh + 127) / 128) + (size_t)ci.w * ci.h;
                         max_lds = std::max(max_lds, lds);
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
