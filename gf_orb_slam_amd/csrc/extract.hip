@@ -40,7 +40,7 @@
 
 namespace {
 
-__constant__ int c_pattern[256 * 4];
+__constant__ uint32_t c_pattern8[256];  // test i: (x0, y0, x1, y1) of its two points as int8
 __constant__ int c_umax[16];
 
 struct LevelGeom {
@@ -890,7 +890,7 @@ __device__ float fast_atan2f(float y, float x) {
 struct DescLds {
     uint32_t ic[DS_IC * DS_ICW];
     uint32_t bl[DS_BL * DS_BLW];
-    uint8_t ic_sh[DS_IC], bl_sh[DS_BL];
+    uint8_t ic_sh[DS_IC];
 };
 
 // Two keypoints per wave, one per 32-lane half: the halves' loads go out in
@@ -906,6 +906,9 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
     __shared__ DescLds sh_all[8];
+    __shared__ uint32_t sh_pat[256];  // the rBRIEF pattern, one dword per test
+    sh_pat[threadIdx.x] = c_pattern8[threadIdx.x];
+    __syncthreads();
     int bx, f;
     gfd::xcd_block(bx, f);
     const int lane = threadIdx.x & 63, hl = lane & 31, half = (threadIdx.x >> 5);  // half = slot 0..7
@@ -959,9 +962,6 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             else if (i < DS_IC * DS_ICW + DS_BL * DS_BLW) W.bl[i - DS_IC * DS_ICW] = v[t];
         }
         if (hl < DS_IC) W.ic_sh[hl] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + hl) * stride + x - 15) & 3);
-        W.bl_sh[hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + hl) * pwl + x - 18) & 3);
-        if (hl < DS_BL - 32)
-            W.bl_sh[32 + hl] = (uint8_t)((uintptr_t)(B + (long long)(y - 18 + 32 + hl) * pwl + x - 18) & 3);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -988,7 +988,10 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     m01 = half_sum(m01);
     const float angle = fast_atan2f((float)m01, (float)m10);
 
-    // rBRIEF: lane hl of the half computes descriptor byte hl (16 tests).
+    // rBRIEF: lane hl of the half computes descriptor byte hl (16 tests). The
+    // blurred rows are pitched to 64 B, so every window row has the same byte
+    // shift in its first dword.
+    const int bsh = (int)((uintptr_t)(B + (long long)(y - 18) * pwl + x - 18) & 3);
     {
         const float factorPI = (float)(M_PI / 180.f);
         const float ang = angle * factorPI;
@@ -999,13 +1002,13 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             int t[2];
 #pragma unroll
             for (int q = 0; q < 2; q++) {
-                const int pi = hl * 16 + bit * 2 + q;
-                const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
+                const uint32_t pt = sh_pat[hl * 8 + bit] >> (16 * q);
+                const float px = (float)(int8_t)(pt & 0xff), py = (float)(int8_t)((pt >> 8) & 0xff);
                 const int ry = __float2int_rn(px * b + py * a);
                 const int rx = __float2int_rn(px * a - py * b);
                 if (win) {
                     const int r = ry + 18;
-                    t[q] = bl8[r * (4 * DS_BLW) + W.bl_sh[r] + rx + 18];
+                    t[q] = bl8[r * (4 * DS_BLW) + bsh + rx + 18];
                 } else {
                     const int xx = x + rx, yy = y + ry;
                     const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
@@ -1247,7 +1250,19 @@ static void free_extractor(gf_extractor* ex) {
 static int upload_constants(int device) {
     static unsigned long long done_mask = 0;
     if (done_mask & (1ull << device)) return GF_OK;
-    GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, sizeof(kOrbPattern31)));
+    {
+        uint32_t p8[256];
+        for (int i = 0; i < 256; i++) {
+            uint32_t v = 0;
+            for (int j = 0; j < 4; j++) {
+                const int c = kOrbPattern31[4 * i + j];
+                GF_CHECK(c >= -128 && c <= 127, GF_ERR_ARG, "pattern coordinate out of int8 range");
+                v |= (uint32_t)(uint8_t)(int8_t)c << (8 * j);
+            }
+            p8[i] = v;
+        }
+        GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern8), p8, sizeof(p8)));
+    }
     // umax of the circular patch (ORBextractor.cc:500-517)
     int umax[16];
     const int hp = 15;
