@@ -305,6 +305,8 @@ def main():
     ap.add_argument("--lba-batch", type=int, default=64, help="local-BA windows solved together (0: skip)")
     ap.add_argument("--single-stream-steps", type=int, default=40,
                     help="also time one sequence alone (per-frame latency, HIP graph replay)")
+    ap.add_argument("--isolated-steps", type=int, default=5,
+                    help="also time the priced kernel with one group running alone")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="also time one group with the frames handed over from host memory")
     args = ap.parse_args()
@@ -504,6 +506,25 @@ def main():
         "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1],
                         "ms_per_step": round(v[0] / args.steps, 4)} for k, v in prof.items()},
     }
+    if args.isolated_steps > 0:
+        # the priced kernel with one group running alone (after the timed
+        # region): in the timed region the other groups' tracking kernels share
+        # its CUs, so its HIP-event duration there includes that contention
+        fe = fes[0]
+        fe.prof_enable(True)
+        fe.prof_reset()
+        for _ in range(args.isolated_steps):
+            fe.step()
+        fe.sync()
+        iso = fe.prof_report().get(dom)
+        fe.prof_enable(False)
+        if iso:
+            iso_s = iso[0] / iso[1] / 1e3
+            iso_ach = per_launch_bytes[dom] / iso_s / 1e9
+            out["roofline"]["isolated"] = {"avg_launch_ms": round(iso_s * 1e3, 4), "achieved": round(iso_ach, 2),
+                                           "frac": round(iso_ach / 8000.0, 5), "steps": args.isolated_steps,
+                                           "note": "one group alone, HIP events; `frac` above is the timed region "
+                                                   "with the groups overlapping"}
     for fe in fes:
         fe.close()
     if rank == 0 and args.single_stream_steps > 0:
