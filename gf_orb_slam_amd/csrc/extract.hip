@@ -778,6 +778,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
                                                 long long lvl_stride, int* __restrict__ lvl_counts) {
     __shared__ int cnt[SEL_MAX_CELLS], keep[SEL_MAX_CELLS], off[SEL_MAX_CELLS + 1];
     __shared__ char valid[SEL_MAX_CELLS];
+    __shared__ int s_red[2];
     extern __shared__ __align__(16) uint8_t sel_dyn[];
     const int l = blockIdx.x, f = blockIdx.y, wv = threadIdx.x >> 6;
     SelWave& W = reinterpret_cast<SelWave*>(sel_dyn)[wv];
@@ -787,48 +788,80 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
         valid[c] = (char)cells[cb + c].valid;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        // Quota redistribution, ORBextractor.cc:673-721. Cells skipped by the
-        // ROI loop (valid == 0) keep nTotal = 0, nToRetain = 0, bNoMore = false.
+    // Quota redistribution, ORBextractor.cc:673-721, by the whole workgroup:
+    // each round is a per-cell map with integer sums (order-free), so the
+    // rounds give the sequential loop's keep[] exactly. Cells skipped by the
+    // ROI loop (valid == 0) keep nTotal = 0, nToRetain = 0, bNoMore = false.
+    // off[c] is the noMore flag until the final prefix sum.
+    {
         const int nf = g.nfcell[l];
-        int nNoMore = 0, nToDistribute = 0;
-        for (int c = 0; c < nc; c++) {
-            off[c] = 0;  // used as the noMore flag during redistribution
+        if (threadIdx.x == 0) {
+            s_red[0] = 0;  // nToDistribute
+            s_red[1] = 0;  // nNoMore
+        }
+        __syncthreads();
+        int dist = 0, nomore = 0;
+        for (int c = threadIdx.x; c < nc; c += SEL_THREADS) {
+            off[c] = 0;
             if (!valid[c]) {
                 keep[c] = 0;
-                continue;
-            }
-            if (cnt[c] > nf) {
+            } else if (cnt[c] > nf) {
                 keep[c] = nf;
             } else {
                 keep[c] = cnt[c];
-                nToDistribute += nf - cnt[c];
+                dist += nf - cnt[c];
                 off[c] = 1;
-                nNoMore++;
+                nomore++;
             }
         }
-        while (nToDistribute > 0 && nNoMore < nc) {
-            int nNew = nf + (int)ceilf((float)nToDistribute / (float)(nc - nNoMore));
-            nToDistribute = 0;
-            for (int c = 0; c < nc; c++) {
-                if (off[c]) continue;
+        if (dist) atomicAdd(&s_red[0], dist);
+        if (nomore) atomicAdd(&s_red[1], nomore);
+        __syncthreads();
+        int nToDistribute = s_red[0], nNoMore = s_red[1];
+        while (nToDistribute > 0 && nNoMore < nc) {  // uniform: every thread read the same sums
+            const int nNew = nf + (int)ceilf((float)nToDistribute / (float)(nc - nNoMore));
+            __syncthreads();  // all have read s_red
+            if (threadIdx.x == 0) s_red[0] = 0;
+            __syncthreads();
+            dist = 0;
+            nomore = 0;
+            for (int c = threadIdx.x; c < nc; c += SEL_THREADS) {
+                if (off[c]) continue;  // (skipped cells take part: nTotal 0, bNoMore false)
                 if (cnt[c] > nNew) {
                     keep[c] = nNew;
                 } else {
                     keep[c] = cnt[c];
-                    nToDistribute += nNew - cnt[c];
+                    dist += nNew - cnt[c];
                     off[c] = 1;
-                    nNoMore++;
+                    nomore++;
                 }
             }
+            if (dist) atomicAdd(&s_red[0], dist);
+            if (nomore) atomicAdd(&s_red[1], nomore);
+            __syncthreads();
+            nToDistribute = s_red[0];
+            nNoMore = s_red[1];
         }
-        // keep[c] <= cnt[c], so retainBest leaves exactly keep[c] per cell (:734-736)
-        int s = 0;
-        for (int c = 0; c < nc; c++) {
-            off[c] = s;
-            s += valid[c] ? keep[c] : 0;
+        // keep[c] <= cnt[c], so retainBest leaves exactly keep[c] per cell
+        // (:734-736); off = exclusive prefix of the kept counts
+        __syncthreads();
+        if (wv == 0) {
+            const int lane = threadIdx.x & 63;
+            int base = 0;
+            for (int c0 = 0; c0 < nc; c0 += 64) {
+                const int c = c0 + lane;
+                const int v = c < nc && valid[c] ? keep[c] : 0;
+                int x = v;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int y = __shfl_up(x, o, 64);
+                    if (lane >= o) x += y;
+                }
+                if (c < nc) off[c] = base + x - v;
+                base += __shfl(x, 63, 64);
+            }
+            if (lane == 0) off[nc] = base;
         }
-        off[nc] = s;
     }
     __syncthreads();
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
@@ -907,7 +940,9 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                                                   int* __restrict__ out_counts, int cap) {
     __shared__ DescLds sh_all[8];
     __shared__ uint32_t sh_pat[256];  // the rBRIEF pattern, one dword per test
+    __shared__ int sh_umax[16];       // IC_Angle's umax (a lane-indexed read)
     sh_pat[threadIdx.x] = c_pattern8[threadIdx.x];
+    if (threadIdx.x < 16) sh_umax[threadIdx.x] = c_umax[threadIdx.x];
     __syncthreads();
     int bx, f;
     gfd::xcd_block(bx, f);
@@ -973,7 +1008,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     // the circular patch (|u| > umax[|v|]) weigh 0. Integer moments: order-free.
     int m10 = 0, m01 = 0;
     if (hl < 31) {
-        const int v = hl - 15, d = c_umax[v < 0 ? -v : v];
+        const int v = hl - 15, d = sh_umax[v < 0 ? -v : v];
         const uint8_t* row = ic8 + hl * (4 * DS_ICW) + W.ic_sh[hl] + 15;
         int sum = 0;
 #pragma unroll
