@@ -352,7 +352,7 @@ __global__ __launch_bounds__(PO_T) void k_pose_opt(PoseArgs A) {
                     for (int j = 0; j < 6; j++) Hl[7 * j] += lam_g;
                     double xn[6];
                     const bool ok = gfse3::ldlt6(Hl, b, xn);
-                    if (L.l < 64 && (L.l & 15) == 0) {
+                    if (L.l < 64 && (L.l & 15) == 0 && g < PO_SPEC) {
                         sh_ok[g] = ok;
                         for (int j = 0; j < 6; j++) sh_x[g][j] = xn[j];
                     }
