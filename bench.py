@@ -289,8 +289,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=768, help="independent sequences per GPU")
-    ap.add_argument("--groups", type=int, default=3,
+    ap.add_argument("--batch", type=int, default=1024, help="independent sequences per GPU")
+    ap.add_argument("--groups", type=int, default=2,
                     help="stream groups per GPU, each a front end on its own HIP stream (their kernels overlap)")
     ap.add_argument("--no-gate", action="store_true",
                     help="let the groups' extraction stages overlap (default: chained, one at a time)")
