@@ -105,6 +105,8 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
     extern __shared__ __align__(16) uint32_t rs_lds[];
     uint8_t* src = reinterpret_cast<uint8_t*>(rs_lds);
     uint8_t* rsh = src + (size_t)pitch * max_rows;  // byte offset of each row's first needed column
+    // the tile's RS_H y-table entries (a row's entry is the same for a whole wave)
+    int2* yt_s = reinterpret_cast<int2*>(src + (((size_t)pitch * max_rows + max_rows + 15) & ~(size_t)15));
     int bx, f;
     gfd::xcd_block(bx, f);
     const int tid = threadIdx.x;
@@ -122,9 +124,7 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
     // this thread's table entries, fetched alongside the source rows
     const int x = X0 + (tid & 63), yb = Y0 + RS_RPT * (tid >> 6);
     const int2 xt = xtab[min(x, xl)];
-    int2 yts[RS_RPT];
-#pragma unroll
-    for (int i = 0; i < RS_RPT; i++) yts[i] = ytab[min(yb + i, yl)];
+    if (tid < RS_H) yt_s[tid] = ytab[min(Y0 + tid, yl)];
     constexpr int RS_LB = 8;  // dwords per thread per load batch
     for (int i0 = 0; i0 < nrows * ndw; i0 += 256 * RS_LB) {
         uint32_t v[RS_LB];
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
 #pragma unroll
     for (int i = 0; i < RS_RPT; i++, dp += dw) {
         if (yb + i > yl) continue;  // (no break: the loop stays unrolled, yts in registers)
-        const int2 yt = yts[i];
+        const int2 yt = yt_s[yb - Y0 + i];
         const int r0 = min(max(yt.x, 0), sh - 1) - rs, r1 = min(max(yt.x + 1, 0), sh - 1) - rs;
         const int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
         // the two taps of a row from two aligned LDS dwords (a byte pair at an
@@ -1475,7 +1475,8 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     {
         GF_PROF(ctx, s, "k_resize");
         for (int l = 1; l < ex->nlevels; l++) {
-            const size_t lds = (size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l] + 8;
+            const size_t lds = (((size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l] + 15) & ~(size_t)15) +
+                               RS_H * sizeof(int2) + 8;
             k_resize<<<dim3(ex->rs_tiles[l], nframes), 256, lds, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l],
                                                                       ex->d_ytab + ex->ytab_off[l], ex->rs_tiles_x[l],
                                                                       ex->rs_pitch[l], ex->rs_rows[l]);
