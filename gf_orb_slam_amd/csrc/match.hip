@@ -191,6 +191,12 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
         __syncthreads();
 }
 
+// k_match stages the frame's keypoint positions / octaves (float4) and
+// descriptors in LDS after its fixed arrays when kp_cap <= MATCH_STAGE_MAX
+// (48 B a keypoint; the candidate loops then read no global memory).
+#define MATCH_BASE_LDS ((sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX + 15) & ~(size_t)15)
+#define MATCH_STAGE_MAX ((150 * 1024 - (int)MATCH_BASE_LDS) / 48)
+
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
     int* cell_start = lds;                  // NCELLS + 1
@@ -208,6 +214,31 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* score = A.score + (long long)f * A.kp_cap;
+    const bool stg = A.kp_cap <= MATCH_STAGE_MAX;
+    float4* X = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(lds) + MATCH_BASE_LDS);
+    uint8_t* Ds = reinterpret_cast<uint8_t*>(X + A.kp_cap);
+    if (stg) {
+        for (int i = tid; i < n; i += MATCH_THREADS) {
+            const gf_keypoint kp = K[i];
+            X[i] = make_float4(kp.x, kp.y, __int_as_float(kp.octave), 0.f);
+        }
+        for (int i = tid; i < 2 * n; i += MATCH_THREADS)
+            reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
+    }
+    const uint8_t* DD = stg ? (const uint8_t*)Ds : D;
+    auto cand = [&](int idx, float& x, float& y, int& oct) {
+        if (stg) {
+            const float4 v = X[idx];
+            x = v.x;
+            y = v.y;
+            oct = __float_as_int(v.z);
+        } else {
+            const gf_keypoint kp = K[idx];
+            x = kp.x;
+            y = kp.y;
+            oct = kp.octave;
+        }
+    };
 
     if (tid == 0) {
         s_nm = 0;
@@ -232,9 +263,11 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
                 for (int t = s; t < e; t++) {
                     const int idx = items[t];
                     if (claim[idx] >= 0) continue;
-                    const gf_keypoint kp = K[idx];
-                    if (!level_ok(kp.octave, q.minL, q.maxL)) continue;
-                    if (fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
+                    float kx, ky;
+                    int ko;
+                    cand(idx, kx, ky, ko);
+                    if (!level_ok(ko, q.minL, q.maxL)) continue;
+                    if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
                     atomicMin(&minU[idx], k);
                 }
             }
@@ -250,24 +283,26 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
                     const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
                     for (int t = s; t < e; t++) {
                         const int idx = items[t];
-                        const gf_keypoint kp = K[idx];
-                        if (!level_ok(kp.octave, q.minL, q.maxL)) continue;
-                        if (fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
+                        float kx, ky;
+                        int ko;
+                        cand(idx, kx, ky, ko);
+                        if (!level_ok(ko, q.minL, q.maxL)) continue;
+                        if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
                         if (__hip_atomic_load(&claim[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
                             continue;
                         if (minU[idx] != k) {
                             ok = false;
                             break;
                         }
-                        const int dist = hamming32(q.d, D + (long long)idx * 32);
+                        const int dist = hamming32(q.d, DD + (long long)idx * 32);
                         if (dist < bestDist) {
                             bestDist2 = bestDist;
                             bestDist = dist;
                             bestLevel2 = bestLevel;
-                            bestLevel = kp.octave;
+                            bestLevel = ko;
                             bestIdx = idx;
                         } else if (dist < bestDist2) {
-                            bestLevel2 = kp.octave;
+                            bestLevel2 = ko;
                             bestDist2 = dist;
                         }
                     }
@@ -695,7 +730,10 @@ __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* di
     if (i < n) dist[i] = hamming32(a + 32LL * i, b + 32LL * i);
 }
 
-size_t match_lds_bytes() { return sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX; }
+size_t match_lds_bytes(int kp_cap) {
+    return kp_cap <= MATCH_STAGE_MAX ? MATCH_BASE_LDS + 48 * (size_t)kp_cap
+                                     : sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX;
+}
 
 }  // namespace
 
@@ -729,8 +767,7 @@ static int check_fi(const gf_frame_info* fi) {
 static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, int nframes, hipStream_t s) {
     static unsigned long long attr_mask = 0;
     if (!(attr_mask & (1ull << ctx->device))) {
-        GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)match_lds_bytes()));
+        GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    152 * 1024));
         GF_HIP(hipFuncSetAttribute((const void*)k_match_seq_pre, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -747,7 +784,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
         k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
     } else {  // many queries, narrow windows: claim-resolution rounds
         GF_PROF(ctx, s, "k_match_project");
-        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(), s>>>(A, fc);
+        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(A.kp_cap), s>>>(A, fc);
     }
     GF_HIP(hipGetLastError());
     return GF_OK;
