@@ -38,6 +38,7 @@ struct ProfEntry {
 
 struct gf_ctx {
     int device = 0;
+    int num_cus = 256;  // compute units of the device (launch-shape choices)
     hipStream_t stream = nullptr;
     bool prof = false;
     // gf_set_budgets: reference time budgets in seconds (+inf = parity mode)

@@ -95,6 +95,11 @@ int gf_ctx_create(int hip_device, gf_ctx** out) {
     GF_HIP(hipSetDevice(hip_device));
     gf_ctx* c = new gf_ctx();
     c->device = hip_device;
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && ncu > 0)
+            c->num_cus = ncu;
+    }
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
