@@ -195,7 +195,9 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
 // descriptors in LDS after its fixed arrays when kp_cap <= MATCH_STAGE_MAX
 // (48 B a keypoint; the candidate loops then read no global memory).
 #define MATCH_BASE_LDS ((sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX + 15) & ~(size_t)15)
+#ifndef MATCH_STAGE_MAX
 #define MATCH_STAGE_MAX ((150 * 1024 - (int)MATCH_BASE_LDS) / 48)
+#endif
 
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
