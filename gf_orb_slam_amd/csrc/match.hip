@@ -191,33 +191,44 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
         __syncthreads();
 }
 
-// k_match stages the frame's keypoint positions / octaves (float4) and
-// descriptors in LDS after its fixed arrays when kp_cap <= MATCH_STAGE_MAX
-// (48 B a keypoint; the candidate loops then read no global memory).
-#define MATCH_BASE_LDS ((sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX + 15) & ~(size_t)15)
-#ifndef MATCH_STAGE_MAX
-#define MATCH_STAGE_MAX ((150 * 1024 - (int)MATCH_BASE_LDS) / 48)
+// k_match's LDS is sized by the front end's capacities (kp_cap keypoints,
+// q_cap queries), not by the KP_MAX / Q_MAX maxima, so a workgroup fits
+// beside other kernels' workgroups on a CU. With MATCH_STAGE it also stages
+// the frame's keypoint positions / octaves (float4) and descriptors (48 B a
+// keypoint; the candidate loops then read no global memory) when that stays
+// within MATCH_STAGE_LDS.
+#ifndef MATCH_STAGE
+#define MATCH_STAGE 1
 #endif
+#define MATCH_STAGE_LDS (96 * 1024)
+__host__ __device__ __forceinline__ size_t match_base_lds(int kp_cap, int q_cap) {
+    const int kc = kp_cap < KP_MAX ? kp_cap : KP_MAX, qc = q_cap < Q_MAX ? q_cap : Q_MAX;
+    return (sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kc) + (size_t)qc + 15) & ~(size_t)15;
+}
+__host__ __device__ __forceinline__ bool match_stage(int kp_cap, int q_cap) {
+    return MATCH_STAGE && match_base_lds(kp_cap, q_cap) + 48 * (size_t)kp_cap <= MATCH_STAGE_LDS;
+}
 
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
     extern __shared__ __align__(16) int lds[];
+    const int kc = min(A.kp_cap, KP_MAX);
     int* cell_start = lds;                  // NCELLS + 1
     int* cursor = cell_start + NCELLS + 1;  // NCELLS
-    int* items = cursor + NCELLS;           // KP_MAX
-    int* claim = items + KP_MAX;            // KP_MAX
-    int* minU = claim + KP_MAX;             // KP_MAX
-    uint8_t* done = (uint8_t*)(minU + KP_MAX);  // Q_MAX
+    int* items = cursor + NCELLS;           // kc
+    int* claim = items + kc;                // kc
+    int* minU = claim + kc;                 // kc
+    uint8_t* done = (uint8_t*)(minU + kc);  // min(q_cap, Q_MAX)
     __shared__ int s_any, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
 
     const int f = blockIdx.x, tid = threadIdx.x;
-    const int n = min(A.n[f], KP_MAX);
-    const int nq = min(A.list ? A.nlist[f] : A.m[f], Q_MAX);
+    const int n = min(A.n[f], kc);
+    const int nq = min(A.list ? A.nlist[f] : A.m[f], min(A.q_cap, Q_MAX));
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* score = A.score + (long long)f * A.kp_cap;
-    const bool stg = A.kp_cap <= MATCH_STAGE_MAX;
-    float4* X = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(lds) + MATCH_BASE_LDS);
+    const bool stg = match_stage(A.kp_cap, A.q_cap);
+    float4* X = reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(lds) + match_base_lds(A.kp_cap, A.q_cap));
     uint8_t* Ds = reinterpret_cast<uint8_t*>(X + A.kp_cap);
     if (stg) {
         for (int i = tid; i < n; i += MATCH_THREADS) {
@@ -732,9 +743,8 @@ __global__ void k_hamming(const uint8_t* a, const uint8_t* b, int n, int32_t* di
     if (i < n) dist[i] = hamming32(a + 32LL * i, b + 32LL * i);
 }
 
-size_t match_lds_bytes(int kp_cap) {
-    return kp_cap <= MATCH_STAGE_MAX ? MATCH_BASE_LDS + 48 * (size_t)kp_cap
-                                     : sizeof(int) * (2 * NCELLS + 1 + 3 * KP_MAX) + Q_MAX;
+size_t match_lds_bytes(int kp_cap, int q_cap) {
+    return match_base_lds(kp_cap, q_cap) + (match_stage(kp_cap, q_cap) ? 48 * (size_t)kp_cap : 0);
 }
 
 }  // namespace
@@ -786,7 +796,7 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, i
         k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
     } else {  // many queries, narrow windows: claim-resolution rounds
         GF_PROF(ctx, s, "k_match_project");
-        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(A.kp_cap), s>>>(A, fc);
+        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
     }
     GF_HIP(hipGetLastError());
     return GF_OK;
