@@ -26,8 +26,11 @@ constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
 constexpr int PO_CHI = 27;
 constexpr int PO_SPEC = 4;   // LM trials evaluated together (see k_pose_opt)
 constexpr int PO_ROWS = PO_CHI + PO_SPEC;  // term rows: H, b, one chi2 row per trial
-constexpr int PO_T = 256;    // threads per problem = edges per pass
-constexpr int PO_TP = PO_T + 1;  // term row pitch (doubles): accumulator threads read distinct banks
+constexpr int PO_T = 256;    // threads per problem
+#ifndef PO_E
+#define PO_E 256             // edges per pass (a term row's length)
+#endif
+constexpr int PO_TP = PO_E + 1;  // term row pitch (doubles): accumulator threads read distinct banks
 constexpr int PO_STRIDE_MAX = 8192;
 constexpr int PO_LDS_EDGES = 384;  // problems up to this size keep edges and residuals in LDS (18 KB)
 
@@ -134,9 +137,9 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
                                      double* sh_sum) {
     // (build: the H/b rows too; the chi2 row is PO_CHI)
     double acc = 0.0;
-    for (int base = 0; base < L.n; base += PO_T) {
+    for (int base = 0; base < L.n; base += PO_E) {
         const int e = base + L.l;
-        if (e < L.n) {
+        if (L.l < PO_E && e < L.n) {
             double pc[3], r0, r1;
             edge_error(L, T, e, pc, r0, r1);
             const double info = L.info[e];
@@ -171,7 +174,7 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
             }
         }
         __syncthreads();
-        const int m = min(PO_T, L.n - base);
+        const int m = min(PO_E, L.n - base);
         if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
             acc = chain_sum(term[L.l], m, acc);
         }
@@ -190,9 +193,9 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
 __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[PO_TP],
                                             double* sh_sum) {
     double acc = 0.0;
-    for (int base = 0; base < L.n; base += PO_T) {
+    for (int base = 0; base < L.n; base += PO_E) {
         const int e = base + L.l;
-        if (e < L.n) {
+        if (L.l < PO_E && e < L.n) {
             const double info = L.info[e];
 #pragma unroll
             for (int s = 0; s < PO_SPEC; s++) {
@@ -231,7 +234,7 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
             }
         }
         __syncthreads();
-        const int m = min(PO_T, L.n - base);
+        const int m = min(PO_E, L.n - base);
         if (L.l < PO_CHI + S) {
             acc = chain_sum(term[L.l], m, acc);
         }
