@@ -454,7 +454,9 @@ struct OnePre {  // one-point result against the frame's starting claims
 // (x, y, octave) and (up to 2048 keypoints) their descriptors in LDS, then
 // one thread per in-view map point runs the one-point scan. The active
 // matcher takes these results until a claim hits one of their holders.
+#ifndef PRE_THREADS
 #define PRE_THREADS 1024
+#endif
 #define PRE_DESC_LDS_MAX 2048
 __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OnePre* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem[];

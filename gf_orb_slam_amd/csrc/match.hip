@@ -370,7 +370,9 @@ struct SeqPre {
     int16_t pad;
 };
 
+#ifndef SEQ_PRE_THREADS
 #define SEQ_PRE_THREADS 1024
+#endif
 #define SEQ_PRE_DESC_MAX 2048
 #define SEQ_PRE_G 4  // lanes per query
 __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,

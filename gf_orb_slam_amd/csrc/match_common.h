@@ -9,7 +9,9 @@
 #define NCELLS (GRID_COLS * GRID_ROWS)
 #define KP_MAX 4096
 #define Q_MAX 8192
+#ifndef MATCH_THREADS
 #define MATCH_THREADS 1024
+#endif
 #define TH_HIGH 100
 #define HISTO_LENGTH 30
 
