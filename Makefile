@@ -61,3 +61,15 @@ SEQDRV = tests/cpp/sequence_driver
 all: $(SEQDRV)
 $(SEQDRV): tests/cpp/sequence_driver.cpp include/gfslam/orbslam.h include/gfslam/abi.h $(LIB)
 	$(CXX) -O2 -std=c++17 -Iinclude $< -Lgf_orb_slam_amd -lgfslam -Wl,-rpath,'$$ORIGIN/../../gf_orb_slam_amd' -o $@
+
+# diagnostic build: k_active_match phase stamps (scripts/am_stamps.py), never the product
+STAMPLIB = gf_orb_slam_amd/diag/libgfslam_am.so
+stamp: $(STAMPLIB)
+build/stamp/gf.o: $(CSRC)/gf.hip $(HDRS)
+	@mkdir -p build/stamp
+	$(HIPCC) $(HIPFLAGS) -DGF_AM_STAMP -c $< -o $@
+$(STAMPLIB): build/stamp/gf.o $(filter-out build/gf.o,$(HIPOBJS)) $(CPPOBJS) | gf_orb_slam_amd/diag
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -L/opt/rocm/lib -lrccl -o $@
+gf_orb_slam_amd/diag:
+	mkdir -p $@
+.PHONY: stamp

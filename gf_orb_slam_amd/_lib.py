@@ -11,7 +11,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgfslam.so")
+# GF_LIB: a diagnostic build of the same sources (e.g. the phase-stamp build
+# `make stamp`); the product build otherwise
+LIB_PATH = os.environ.get("GF_LIB") or os.path.join(_HERE, "libgfslam.so")
 ABI_HEADER = os.path.join(os.path.dirname(_HERE), "include", "gfslam", "abi.h")
 
 GF_OK = 0
@@ -92,7 +94,7 @@ _PROTOS = {
     "gf_obs_build_info_dev": [_P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P],
     "gf_obs_accumulate_dev": [_P, _I, _P, _P, _P, _I, _D, _P, _P],
     "gf_obs_active_match_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _F, _F, _P,
-                                _P, _P, _P, _P, _P, _P],
+                                _P, _P, _P, _P, _P, _P, _P],
     "gf_maxvol_select_dev": [_P, _I, _P, _P, _P, _I, _I, _D, _I, _P, _P, _P, _P],
     "gf_match_lastframe_dev": [_P, _P, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P,
                                _P, _P],

@@ -169,6 +169,15 @@ __device__ __forceinline__ void huber(double e, double& rho0, double& rho1) {
 }
 
 // EdgeSE3ProjectXYZ::computeError; pc = T.map(X)
+// SparseOptimizer::optimize checks terminate() before every iteration
+// (sparse_optimizer.cpp:376): an iteration that would start while the
+// caller's stop flag is raised does not run. The step's kernels then do
+// nothing and k_ba_decide ends the round. (Within a step the flag is
+// constant: the host writes it on the same stream between steps.)
+__device__ __forceinline__ bool ba_halted(const BAArena& A, const BAState& st) {
+    return st.need_lin && A.stop && *A.stop;
+}
+
 __device__ __forceinline__ void edge_error(const double* m, const gfse3::SE3& T, const double* X, double* pc,
                                            double& e0, double& e1) {
     gfse3::map(T, X, pc);
@@ -264,6 +273,10 @@ __global__ __launch_bounds__(256) void k_ba_init(BAArena A) {
     for (int e = tid; e < d.nedges; e += 256) {
         A.e_act[d.e0 + e] = 1;
         A.e_out[d.e0 + e] = 0;
+        // an edge's _error before any computeError: taken as 0 (g2o leaves the
+        // Eigen member uninitialised; read by a stop before the first iteration)
+        A.e_err[(size_t)(d.e0 + e) * 2] = 0.0;
+        A.e_err[(size_t)(d.e0 + e) * 2 + 1] = 0.0;
     }
     for (int i = tid; i < 6 * d.nfree; i += 256) A.xp[(size_t)d.f0 * 6 + i] = 0.0;
     if (tid == 0) {
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(BA_T) void k_ba_linearize(BAArena A) {
     const BADesc d = A.desc[p];
     if (blockIdx.x >= d.nwg) return;
     const BAState st = A.st[p];
-    if (st.round >= 2 || !st.need_lin) return;
+    if (st.round >= 2 || !st.need_lin || ba_halted(A, st)) return;
     const int i = blockIdx.x * BA_T + threadIdx.x;
     double chi = 0.0, maxd = 0.0;
     if (i < d.npts) {
@@ -353,7 +366,7 @@ __global__ __launch_bounds__(BA_PT) void k_ba_poses(BAArena A) {
     const BADesc d = A.desc[p];
     if (a >= d.nfree) return;
     const BAState st = A.st[p];
-    if (st.round >= 2 || !st.need_lin) return;
+    if (st.round >= 2 || !st.need_lin || ba_halted(A, st)) return;
     const int cur = st.cur;
     const int kf = A.f_kf[d.f0 + a];
     const gfse3::SE3 T = load_T(A, cur, d.kf0 + kf);
@@ -439,7 +452,7 @@ __global__ __launch_bounds__(BA_T) void k_ba_schur_pts(BAArena A) {
     const BADesc d = A.desc[p];
     if (blockIdx.x >= d.newg) return;
     const BAState st = A.st[p];
-    if (st.round >= 2) return;
+    if (st.round >= 2 || ba_halted(A, st)) return;
     const double lam = trial_lambda(A, d, st, sh);
     if (blockIdx.x == 0 && threadIdx.x == 0 && st.iter == 0 && st.q == 0) A.st[p].lambda = lam;
     const int e = blockIdx.x * BA_T + threadIdx.x;
@@ -497,7 +510,7 @@ __global__ __launch_bounds__(64 * BA_GW) void k_ba_gemm(BAArena A) {
     const int p = blockIdx.y, s = blockIdx.x;
     const BADesc d = A.desc[p];
     if (s >= d.nsplit) return;
-    if (A.st[p].round >= 2) return;
+    if (A.st[p].round >= 2 || ba_halted(A, A.st[p])) return;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const int nt = d.npad >> 4, lower = nt * (nt + 1) / 2, tdb = d.n >> 4;
     const int ld = d.npad + 2;  // padded LDS row: the 4 k-rows of an operand fall in different banks
@@ -578,7 +591,7 @@ __global__ __launch_bounds__(64 * BA_SW) void k_ba_spgemm(BAArena A) {
     const BADesc d = A.desc[p];
     const int it = blockIdx.x * BA_SW + (threadIdx.x >> 6);
     if (it >= d.nitems) return;
-    if (A.st[p].round >= 2) return;
+    if (A.st[p].round >= 2 || ba_halted(A, A.st[p])) return;
     const int4 item = A.items[d.item0 + it];
     const int l = threadIdx.x & 63, kr = l >> 4, cl = l & 15;
     const double* Ht = A.panel + d.panel0;
@@ -616,7 +629,7 @@ __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
     const int n = d.n, npk = tri(n);
     const int u = blockIdx.x * 256 + threadIdx.x;
     if (u >= npk + n) return;
-    if (A.st[p].round >= 2) return;
+    if (A.st[p].round >= 2 || ba_halted(A, A.st[p])) return;
     int t, e;
     if (u < npk) {
         int i = (int)((sqrt(8.0 * u + 1.0) - 1.0) * 0.5);
@@ -682,7 +695,7 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     const int p = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const BADesc d = A.desc[p];
     const BAState st = A.st[p];
-    if (st.round >= 2) return;
+    if (st.round >= 2 || ba_halted(A, st)) return;
 #define BA_STAMP(k)                                                                      \
     if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
     BA_STAMP(0);
@@ -904,7 +917,7 @@ __global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
     const BADesc d = A.desc[p];
     if (blockIdx.x >= d.nwg) return;
     const BAState st = A.st[p];
-    if (st.round >= 2) return;
+    if (st.round >= 2 || ba_halted(A, st)) return;
     const int i = blockIdx.x * BA_T + threadIdx.x;
     double chi = 0.0, sc = 0.0;
     if (i < d.npts) {
@@ -979,7 +992,10 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         s_part[2][w] = A.wg_scale[d.wg0 + w];
     }
     __syncthreads();
-    if (tid == 0) {
+    if (tid == 0 && ba_halted(A, A.st[p])) {  // terminate() before this iteration: optimize() returns
+        s_end = 1;
+        s_cnt = 0;
+    } else if (tid == 0) {
         BAState st = A.st[p];
         if (st.q == 0) {  // activeRobustChi2 at the iteration start
             double c = 0.0;
@@ -1008,7 +1024,7 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         }
         st.q++;
         int end = 0;
-        if (rho < 0 && st.q < 10) {
+        if (rho < 0 && st.q < 10 && !(A.stop && *A.stop)) {  // the trial loop also ends on terminate()
             st.need_lin = 0;  // another trial on the same system
         } else {
             st.iters[st.round]++;

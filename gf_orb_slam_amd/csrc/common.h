@@ -49,6 +49,9 @@ struct gf_ctx {
     static const int kSlots = 64;
     void* ws[kSlots] = {};
     size_t ws_size[kSlots] = {};
+    // captured graphs (gf_frontend_capture) alive on this context: their
+    // kernels hold scratch pointers, so no slot may be reallocated meanwhile
+    int ws_pinned = 0;
 };
 
 namespace gf {

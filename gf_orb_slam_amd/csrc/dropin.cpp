@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <thread>
 #include <unordered_map>
 
 namespace ORB_SLAM {
@@ -67,6 +68,48 @@ void SetDevice(int device) {
     t_device = device;
 }
 
+/* ---------------------------------------------------------------- ORBVocabulary */
+ORBVocabulary::~ORBVocabulary() {
+    if (voc_) gf_vocab_destroy(voc_);
+}
+
+bool ORBVocabulary::loadFromTextFile(const std::string& filename) {
+    if (filename.size() < 4 || filename.compare(filename.size() - 4, 4, ".txt") != 0) return false;
+    gf_vocab* v = nullptr;
+    if (gf_vocab_load(Context(), filename.c_str(), &v) != GF_OK) return false;
+    if (voc_) gf_vocab_destroy(voc_);
+    voc_ = v;
+    return true;
+}
+
+bool ORBVocabulary::loadFromBinaryFile(const std::string& filename) {
+    if (filename.size() >= 4 && filename.compare(filename.size() - 4, 4, ".txt") == 0) return false;
+    gf_vocab* v = nullptr;
+    if (gf_vocab_load(Context(), filename.c_str(), &v) != GF_OK) return false;
+    if (voc_) gf_vocab_destroy(voc_);
+    voc_ = v;
+    return true;
+}
+
+void ORBVocabulary::transform(const Descriptors& features, BowVector& v, FeatureVector& fv, int levelsup) const {
+    if (!voc_) throw GpuError(GF_ERR_ARG, "vocabulary not loaded");
+    const int n = features.rows;
+    const int cap = std::max(n, 1);
+    v.words.assign(cap, 0);
+    v.values.assign(cap, 0.0);
+    fv.nodes.assign(cap, 0);
+    fv.start.assign(n + 1, 0);
+    fv.feats.assign(cap, 0);
+    int nw = 0, nfv = 0;
+    check(gf_bow_transform(voc_, features.data.data(), n, levelsup, v.words.data(), v.values.data(), &nw,
+                           fv.nodes.data(), fv.start.data(), fv.feats.data(), &nfv));
+    v.words.resize(nw);
+    v.values.resize(nw);
+    fv.nodes.resize(nfv);
+    fv.start.resize(nfv + 1);
+    fv.feats.resize(fv.start[nfv]);
+}
+
 /* ---------------------------------------------------------------- ORBextractor */
 ORBextractor::ORBextractor(int nfeatures_, float scaleFactor_, int nlevels_, int scoreType_, int fastTh_)
     : nfeatures(nfeatures_), scaleFactor(scaleFactor_), nlevels(nlevels_), scoreType(scoreType_), fastTh(fastTh_) {}
@@ -124,6 +167,18 @@ Frame::Frame(const ImageView& im, double timeStamp, ORBextractor* extractor, con
         mvLevelSigma2[i] = mvScaleFactors[i] * mvScaleFactors[i];
         mvInvLevelSigma2[i] = 1.0f / mvLevelSigma2[i];
     }
+}
+
+void Frame::ComputeBoW() {
+    if (!mpORBvocabulary) throw GpuError(GF_ERR_ARG, "Frame::ComputeBoW without a vocabulary");
+    if (mBowVec.words.empty()) mpORBvocabulary->transform(mDescriptors, mBowVec, mFeatVec, 4);
+}
+
+KeyFrame::KeyFrame(const Frame& F)
+    : mnFrameId(F.mnId), N(F.N), mvKeysUn(F.mvKeysUn), mDescriptors(F.mDescriptors), mBowVec(F.mBowVec),
+      mFeatVec(F.mFeatVec), mvpMapPoints(F.mvpMapPoints) {
+    static long unsigned int nNextId = 0;
+    mnId = nNextId++;
 }
 
 gf_frame_info Frame::info() const {
@@ -237,6 +292,100 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
     return n;
 }
 
+int ORBmatcher::SearchByProjection_OnePoint(Frame& F, MapPoint* pMP, const float th) {
+    if (!pMP || !pMP->mbTrackInView || pMP->isBad()) return -1;  // ORBmatcher.h:75-79
+    PointTable T;
+    T.id(pMP);
+    std::vector<int32_t> kp2mp(F.N), score(F.mvpMatchScore.begin(), F.mvpMatchScore.end());
+    for (int i = 0; i < F.N; i++) kp2mp[i] = T.id(F.mvpMapPoints[i]);
+    const int m = (int)T.ptrs.size();
+    std::vector<gf_mp_view> views(m);
+    std::vector<uint8_t> desc((size_t)m * 32);
+    for (int i = 0; i < m; i++) {
+        views[i] = view_of(T.ptrs[i]);
+        if (i > 0) views[i].in_view = 0;  // only pMP is searched
+        std::memcpy(&desc[32 * (size_t)i], T.ptrs[i]->mDescriptor, 32);
+    }
+    const gf_frame_info fi = F.info();
+    int n = 0;
+    check(gf_match_project(Context(), &fi, reinterpret_cast<const gf_keypoint*>(F.mvKeysUn.data()),
+                           F.mDescriptors.data.data(), F.N, views.data(), desc.data(), m, th, mfNNratio, kp2mp.data(),
+                           score.data(), &n));
+    if (n == 0) return -1;
+    for (int i = 0; i < F.N; i++)
+        if (kp2mp[i] == 0 && F.mvpMapPoints[i] != pMP) {
+            F.mvpMapPoints[i] = pMP;
+            F.mvpMatchScore[i] = score[i];
+            return i;
+        }
+    return -1;
+}
+
+int ORBmatcher::SearchByProjection_Budget(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th,
+                                          const double time_constr) {
+    if (time_constr <= 0) return 0;  // ORBmatcher.cc:281-282
+    std::vector<MapPoint*> before(F.mvpMapPoints);
+    const int n = SearchByProjection(F, vpMapPoints, th);
+    for (int i = 0; i < F.N; i++)
+        if (F.mvpMapPoints[i] && F.mvpMapPoints[i] != before[i]) F.mvpMapPoints[i]->IncreaseFound();  // :357
+    return n;
+}
+
+namespace {
+// One side of SearchByBoW: FeatureVector, descriptors, keypoints and the map
+// point of each feature as an index into T (-1 = none or bad).
+struct BowSide {
+    std::vector<int32_t> mp;
+    gf_bow_side side{};
+    BowSide(const FeatureVector& fv, const Descriptors& d, const std::vector<KeyPoint>& kps,
+            const std::vector<MapPoint*>* pts, PointTable& T) {
+        const int n = (int)kps.size();
+        mp.assign(std::max(n, 1), -1);
+        if (pts)
+            for (int i = 0; i < n; i++) {
+                MapPoint* p = (*pts)[i];
+                if (p && !p->isBad()) mp[i] = T.id(p);
+            }
+        side.fv_nodes = fv.nodes.data();
+        side.fv_start = fv.start.data();
+        side.fv_feats = fv.feats.data();
+        side.nfv = (int32_t)fv.nodes.size();
+        side.desc = d.data.data();
+        side.kps = reinterpret_cast<const gf_keypoint*>(kps.data());
+        side.mp = mp.data();
+        side.n = n;
+    }
+};
+}  // namespace
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+    if (!pKF) throw GpuError(GF_ERR_ARG, "null keyframe");
+    PointTable T;
+    BowSide a(pKF->mFeatVec, pKF->mDescriptors, pKF->mvKeysUn, &pKF->mvpMapPoints, T);
+    BowSide b(F.mFeatVec, F.mDescriptors, F.mvKeysUn, nullptr, T);
+    std::vector<int32_t> out(std::max(F.N, 1));
+    int n = 0;
+    check(gf_match_bow(Context(), 0, mfNNratio, mbCheckOrientation ? 1 : 0, &a.side, &b.side, out.data(), &n));
+    vpMapPointMatches.assign(F.N, nullptr);  // ORBmatcher.cc:728
+    for (int j = 0; j < F.N; j++)
+        if (out[j] >= 0) vpMapPointMatches[j] = T.ptrs[out[j]];
+    return n;
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12) {
+    if (!pKF1 || !pKF2) throw GpuError(GF_ERR_ARG, "null keyframe");
+    PointTable T;
+    BowSide a(pKF1->mFeatVec, pKF1->mDescriptors, pKF1->mvKeysUn, &pKF1->mvpMapPoints, T);
+    BowSide b(pKF2->mFeatVec, pKF2->mDescriptors, pKF2->mvKeysUn, &pKF2->mvpMapPoints, T);
+    std::vector<int32_t> out(std::max(pKF1->N, 1));
+    int n = 0;
+    check(gf_match_bow(Context(), 1, mfNNratio, mbCheckOrientation ? 1 : 0, &a.side, &b.side, out.data(), &n));
+    vpMatches12.assign(pKF1->N, nullptr);  // :1303
+    for (int i = 0; i < pKF1->N; i++)
+        if (out[i] >= 0) vpMatches12[i] = T.ptrs[out[i]];
+    return n;
+}
+
 /* ---------------------------------------------------------------- Observability */
 Observability::Observability(double fu, double fv, int nRows, int nCols, double cx, double cy, double, double) {
     camera.fu = fu;
@@ -250,6 +399,7 @@ Observability::Observability(double fu, double fv, int nRows, int nCols, double 
     camera.min_y = 0;
     camera.max_y = nRows;
     gf_rng_seed(&rng_, 1);  // glibc: rand() without srand() behaves as srand(1)
+    mNumThreads = std::max(1u, std::thread::hardware_concurrency());  // Observability.h:186
 }
 
 gf_obs_camera Observability::cam_now() const {
@@ -376,6 +526,56 @@ int Observability::runActiveMapMatching(Frame* F, size_t, const double base[49],
     }
     for (int i = 0; i < nleft; i++) mLeftMapPoints.push_back(T.ptrs[left[i]]);
     return nmatched;
+}
+
+bool Observability::setSelction_Number(size_t num_good_inlier, int greedy_mtd, double time_for_select,
+                                       std::vector<MapPoint*>* mapPoints, std::vector<GoodPoint>* mpVec) {
+    if (!mapPoints || !mpVec || time_for_select <= 0) return false;  // Observability.cc:1026-1027
+    if (kinematic.size() < 2) return false;
+    mKineIdx = 1;
+    mMapPoints = mapPoints;
+    std::vector<int> idx;
+    std::vector<float> pos;
+    for (size_t i = 0; i < mapPoints->size(); i++) {
+        MapPoint* p = (*mapPoints)[i];
+        if (!p || p->isBad()) continue;
+        idx.push_back((int)i);
+        float x[3];
+        p->GetWorldPos(x);
+        pos.insert(pos.end(), x, x + 3);
+    }
+    mpVec->clear();
+    const int n = (int)idx.size();
+    if (n == 0) return true;
+    const gf_obs_camera cam = cam_now();
+    std::vector<int32_t> out(n);
+    int nout = 0;
+    check(gf_select_map_points(Context(), &cam, kinematic[1].Xv, pos.data(), n, (int)num_good_inlier, greedy_mtd,
+                               (int)mNumThreads, &rng_, out.data(), &nout));
+    // the MAP_INFO_MATRIX blocks of the selection (ObsMat at kinematic[1])
+    std::vector<float> spos(3 * (size_t)std::max(nout, 1));
+    for (int j = 0; j < nout; j++) std::memcpy(&spos[3 * (size_t)j], &pos[3 * (size_t)out[j]], 12);
+    std::vector<double> H(14 * (size_t)std::max(nout, 1)), info(49 * (size_t)std::max(nout, 1));
+    std::vector<float> uv(2 * (size_t)std::max(nout, 1));
+    std::vector<uint8_t> valid(std::max(nout, 1));
+    if (nout)
+        check(gf_obs_build_info(Context(), &cam, kinematic[1].Xv, spos.data(), nullptr, nout, 1, H.data(), info.data(),
+                                uv.data(), valid.data()));
+    for (int j = 0; j < nout; j++) {
+        GoodPoint g;
+        g.idx = (size_t)idx[out[j]];
+        g.obs_score = 1.0;  // batchInfoMat_Map: ObsScore = 1 for a visible point
+        std::memcpy(g.obs_block.data(), &info[49 * (size_t)j], sizeof(double) * 49);
+        MapPoint* p = (*mapPoints)[g.idx];
+        std::memcpy(p->ObsMat, g.obs_block.data(), sizeof(p->ObsMat));
+        std::memcpy(p->H_meas, &H[14 * (size_t)j], sizeof(p->H_meas));
+        p->u_proj = uv[2 * j];
+        p->v_proj = uv[2 * j + 1];
+        p->ObsScore = 1.0;
+        p->updateAtFrameId = (long)mnFrameId;
+        mpVec->push_back(g);
+    }
+    return true;
 }
 
 std::vector<int> Observability::maxVolSelection(const std::vector<std::array<double, 49>>& pool,

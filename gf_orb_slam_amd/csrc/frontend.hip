@@ -75,6 +75,7 @@ struct FeDev {
     int32_t* m_m2;
     int32_t* nm2;    // matches of SearchByProjection(F, local, 1)
     int32_t* stats;  // [GF_FE_NSTAT][B]
+    int32_t* hist;   // [B][8] running counters (GF_FE_HIST)
     // budgets (device clock ticks of 100 MHz; < 0: no budget)
     long long match_ticks, select_ticks;
     unsigned long long* t0;
@@ -278,6 +279,11 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
         if (stat(D, GF_ST_INL2)[b] < 15) fl |= 4;
         stat(D, GF_ST_FLAGS)[b] = fl;
         stat(D, GF_ST_FRAMES)[b] += 1;
+        int32_t* h = D.hist + 8LL * b;
+        const int br = stat(D, GF_ST_BRANCH)[b];
+        if (br >= 0 && br < 6) h[br] += 1;
+        h[6] += stat(D, GF_ST_LDETS)[b];
+        h[7] += stat(D, GF_ST_LOCAL)[b];
         if (b == 0) *D.step += 1;
     }
 }
@@ -380,9 +386,17 @@ int fe_field(gf_frontend* fe, int field, size_t count, T** out) {
     return GF_OK;
 }
 
-void fe_free(gf_frontend* fe) {
+// Drop the captured graph (if any) and release the context's scratch pin.
+void fe_drop_graph(gf_frontend* fe) {
     if (fe->exec) (void)hipGraphExecDestroy(fe->exec);
     if (fe->graph) (void)hipGraphDestroy(fe->graph);
+    if (fe->exec || fe->graph) fe->ctx->ws_pinned--;
+    fe->exec = nullptr;
+    fe->graph = nullptr;
+}
+
+void fe_free(gf_frontend* fe) {
+    fe_drop_graph(fe);
     for (void* p : fe->allocs) (void)hipFree(p);
     fe->allocs.clear();
     if (fe->ex) (void)gf_extractor_destroy(fe->ex);
@@ -449,7 +463,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                       (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], fe->mp_updated, fe->mp_info,
                                       fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2, col(GF_ST_TO_MATCH), 1.f,
                                       0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score, D.left, D.nleft,
-                                      col(GF_ST_LOCAL), s));
+                                      col(GF_ST_LOCAL), col(GF_ST_LDETS), s));
     }
     FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
                                (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], D.m_m2, M, 1.f, 0.8f, D.kp2mp, D.score,
@@ -580,6 +594,7 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     F(GF_FE_RNG, gf_rng, B, rng);
     F(GF_FE_LEFT, int32_t, (size_t)B * M, D.left);
     F(GF_FE_STATS, int32_t, (size_t)GF_FE_NSTAT * B, D.stats);
+    F(GF_FE_HIST, int32_t, (size_t)8 * B, D.hist);
     F(-1, int32_t, (size_t)B * M, D.left1);
     F(-1, int32_t, B, D.nleft);
     F(-1, int32_t, B, D.nlist);
@@ -643,6 +658,7 @@ int gf_frontend_set_source(gf_frontend* fe, const uint8_t* const* d_bases, const
     GF_CHECK(fe && d_bases && phase && period > 0, GF_ERR_ARG, "bad source");
     GF_CHECK(frame_stride >= (size_t)fe->p.width * fe->p.height, GF_ERR_ARG, "frame stride below the image size");
     GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));  // a step in flight reads these buffers
     const int B = fe->D.B;
     for (int b = 0; b < B; b++) GF_CHECK(d_bases[b] && phase[b] >= 0, GF_ERR_ARG, "bad source entry");
     GF_HIP(hipMemcpy((void*)fe->D.bases, d_bases, sizeof(void*) * B, hipMemcpyHostToDevice));
@@ -658,6 +674,7 @@ int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, co
     GF_CHECK(fe && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad stream");
     GF_CHECK(m >= 0 && m <= fe->D.M && (m == 0 || (mps && desc)), GF_ERR_ARG, "bad map");
     GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));  // a step in flight reads these buffers
     const size_t M = fe->D.M, o = (size_t)stream * M;
     std::vector<float> pos(3 * (size_t)m);
     for (int i = 0; i < m; i++)
@@ -678,6 +695,7 @@ int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, co
 int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed) {
     GF_CHECK(fe && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad stream");
     GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));  // a step in flight reads these buffers
     gf_rng r;
     gf_rng_seed(&r, seed);
     GF_HIP(hipMemcpy((gf_rng*)fe->field_ptr[GF_FE_RNG] + stream, &r, sizeof(r), hipMemcpyHostToDevice));
@@ -764,7 +782,7 @@ int gf_event_destroy(void* ev) {
 
 int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
     GF_CHECK(fe, GF_ERR_ARG, "null front end");
-    GF_CHECK(!fe->exec, GF_ERR_ARG, "set the gate before capturing a graph");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot be gated");
     fe->gate_wait = (hipEvent_t)wait_event;
     fe->gate_done = (hipEvent_t)done_event;
     return GF_OK;
@@ -781,11 +799,10 @@ int gf_frontend_step(gf_frontend* fe) {
         GF_HIP(hipGraphLaunch(fe->exec, fe->ctx->stream));
         return GF_OK;
     }
-    if (fe->exec && (mt != fe->D.match_ticks || stt != fe->D.select_ticks)) {  // budgets changed: re-capture
-        (void)hipGraphExecDestroy(fe->exec);
-        (void)hipGraphDestroy(fe->graph);
-        fe->exec = nullptr;
-        fe->graph = nullptr;
+    if (fe->exec) {  // budgets changed: the tick limits are kernel arguments, so capture again
+        FE_RC(gf_frontend_capture(fe));
+        GF_HIP(hipGraphLaunch(fe->exec, fe->ctx->stream));
+        return GF_OK;
     }
     fe->D.match_ticks = mt;
     fe->D.select_ticks = stt;
@@ -812,13 +829,13 @@ int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
 
 int gf_frontend_capture(gf_frontend* fe) {
     GF_CHECK(fe && fe->sourced, GF_ERR_ARG, "capture needs a frame source");
+    // a recorded event in a graph is not the caller's event at replay: the
+    // extraction gate would silently stop gating
+    GF_CHECK(!fe->gate_wait && !fe->gate_done, GF_ERR_ARG, "a gated front end cannot be captured as a graph");
     GF_HIP(hipSetDevice(fe->ctx->device));
     hipStream_t s = fe->ctx->stream;
     GF_HIP(hipStreamSynchronize(s));
-    if (fe->exec) (void)hipGraphExecDestroy(fe->exec);
-    if (fe->graph) (void)hipGraphDestroy(fe->graph);
-    fe->exec = nullptr;
-    fe->graph = nullptr;
+    fe_drop_graph(fe);
     auto ticks = [](double v) -> long long { return std::isfinite(v) && v >= 0 ? (long long)(v * 1e8) : -1; };
     fe->D.match_ticks = ticks(fe->ctx->match_budget_s);
     fe->D.select_ticks = ticks(fe->ctx->select_budget_s);
@@ -835,6 +852,7 @@ int gf_frontend_capture(gf_frontend* fe) {
     }
     if (e != hipSuccess) return gf::fail(GF_ERR_HIP, std::string("capture: ") + hipGetErrorString(e));
     fe->graph = g;
+    fe->ctx->ws_pinned++;  // the graph's kernels hold the context's scratch pointers
     GF_HIP(hipGraphInstantiate(&fe->exec, g, nullptr, nullptr, 0));
     return GF_OK;
 }

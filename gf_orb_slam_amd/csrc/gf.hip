@@ -272,6 +272,7 @@ struct ActiveArgs {
     int32_t* left;
     int32_t* nleft;
     int32_t* nmatched;
+    int32_t* nldet;  // [F] logDet evaluations (optional)
     int32_t* err;
     const struct OnePre* pre;  // [F][mp_cap] one-point results against the starting claims
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
@@ -463,6 +464,7 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], KP_MAX);
     const int m = min(A.m[f], 32767);
+    if (m == 0 || A.num_to_match[f] <= 0) return;  // k_active_match takes its early exit
     float4* X = (float4*)smem;                  // kp_cap
     int* cell_start = (int*)(X + A.kp_cap);     // NCELLS + 1
     int* cursor = cell_start + NCELLS + 1;      // NCELLS
@@ -668,6 +670,14 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     const FrameConst& fc = A.fc;
     const int n = min(A.n[f], A.kp_cap);
     const int m = min(A.m[f], 32767);
+    if (m == 0) {  // not this frame's branch: nothing to do, no LDS touched
+        if (lane == 0) {
+            A.nleft[f] = 0;
+            A.nmatched[f] = 0;
+            if (A.nldet) A.nldet[f] = 0;
+        }
+        return;
+    }
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
@@ -712,6 +722,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         if (lane == 0) {
             A.nleft[f] = N;
             A.nmatched[f] = 0;
+            if (A.nldet) A.nldet[f] = 0;
         }
         return;
     }
@@ -732,7 +743,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         const int f0 = A.rng[f].f;
         rs = lane < 31 ? (uint32_t)A.rng[f].state[(f0 + lane) % 31] : 0u;
     }
-    int used = 0, nm = 0;
+    int used = 0, nm = 0, nld = 0;  // nld: logDet calls of the reference (one per draw)
     __syncthreads();
     AM_T(1);
 
@@ -755,6 +766,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         }
         AM_T(2);
         if (nc < sz) {  // the initial subset could not be completed
+            nld += nc;
             for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
             used += exh_at;
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
@@ -810,6 +822,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
+        nld += nused;
         const int T = exh ? exh_at : C.tries[nused - 1];
         for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
         used += T;
@@ -860,6 +873,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             A.rng[f].r = (f1 + 28) % 31;
             A.nleft[f] = N;
             A.nmatched[f] = nm;
+            if (A.nldet) A.nldet[f] = nld;
         }
     }
 }
@@ -1085,7 +1099,7 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
                             const double* d_H, const int32_t* d_m, int mp_cap, const double* d_base,
                             const float* level_sigma2, const int32_t* d_num_to_match, float th, float nnratio,
                             gf_rng* d_rng, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_left, int32_t* d_nleft,
-                            int32_t* d_nmatched, void* stream) {
+                            int32_t* d_nmatched, int32_t* d_nldet, void* stream) {
     GF_CHECK(ctx && fi && level_sigma2, GF_ERR_ARG, "null arg");
     GF_CHECK(kp_cap <= KP_MAX && mp_cap <= 32767, GF_ERR_UNSUPPORTED, "frame exceeds active-matching limits");
     GF_CHECK(fi->nlevels >= 1 && fi->nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
@@ -1115,6 +1129,7 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
     A.left = d_left;
     A.nleft = d_nleft;
     A.nmatched = d_nmatched;
+    A.nldet = d_nldet;
     void* err;
     int rc = gf::ws_get(ctx, 30, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
@@ -1262,7 +1277,7 @@ int gf_obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint*
                                  (const gf_mp_view*)dV, (const uint8_t*)dQ, (const uint8_t*)dU, (const double*)dI,
                                  (const double*)dH, (const int32_t*)dm, mm, (const double*)dB, level_sigma2,
                                  (const int32_t*)dT, th, nnratio, (gf_rng*)dR, (int32_t*)dC, (int32_t*)dS,
-                                 (int32_t*)dL, (int32_t*)dNL, (int32_t*)dNM, ctx->stream);
+                                 (int32_t*)dL, (int32_t*)dNL, (int32_t*)dNM, nullptr, ctx->stream);
     if (rc) return rc;
     int e = 0;
     GF_HIP(hipMemcpyAsync(&e, err, 4, hipMemcpyDeviceToHost, ctx->stream));

@@ -18,6 +18,9 @@ int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out) {
     GF_CHECK(slot >= 0 && slot < gf_ctx::kSlots, GF_ERR_ARG, "bad scratch slot");
     if (bytes == 0) bytes = 16;
     if (ctx->ws_size[slot] < bytes) {
+        GF_CHECK(ctx->ws_pinned == 0, GF_ERR_ARG,
+                 "scratch slot " + std::to_string(slot) +
+                     " would grow while a captured front-end graph holds it: use another context for this call");
         if (ctx->ws[slot]) GF_HIP(hipFree(ctx->ws[slot]));
         ctx->ws[slot] = nullptr;
         ctx->ws_size[slot] = 0;

@@ -47,14 +47,16 @@ class GfDist:
         import torch
 
         dev = f"cuda:{self.ctx.device}"
-        n = torch.zeros(1, dtype=torch.float64, device=dev)
-        if self.rank == root:
-            n[0] = float(a.nbytes)
+        n = torch.tensor([float(a.nbytes) if self.rank == root else 0.0], dtype=torch.float64).to(dev)
+        # the library broadcasts on its own (non-blocking) stream: torch's
+        # stream must have finished writing the buffers before the call
+        torch.cuda.current_stream(dev).synchronize()
         check(lib().gf_dist_bcast(self.handle, ctypes.c_void_p(n.data_ptr()), 8, root))
         nb = int(n.item())
         buf = torch.empty(nb, dtype=torch.uint8, device=dev)
         if self.rank == root:
             buf.copy_(torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)))
+        torch.cuda.current_stream(dev).synchronize()
         check(lib().gf_dist_bcast(self.handle, ctypes.c_void_p(buf.data_ptr()), nb, root))
         return buf.cpu().numpy()
 
@@ -76,6 +78,7 @@ class GfDist:
         out = []
         for op in (2, 1):
             t = torch.from_numpy(v.copy()).to(f"cuda:{self.ctx.device}")
+            torch.cuda.current_stream(t.device).synchronize()
             check(lib().gf_dist_allreduce(self.handle, ctypes.c_void_p(t.data_ptr()), len(v), op))
             out.append(t.cpu().numpy())
         return np.stack(out)

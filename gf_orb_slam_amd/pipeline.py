@@ -62,9 +62,10 @@ FIELDS = {
     "rng": (28, np.uint8, (ctypes.sizeof(Rng),)),
     "left": (29, np.int32, ("M",)),
     "stats": (30, np.int32, None),  # [NSTAT][B]
+    "hist": (31, np.int32, (8,)),  # running counters: steps per branch [0..5], log-dets [6], local matches [7]
 }
 STATS = ["m3", "found", "to_match", "branch", "in_view", "local", "inl1", "inl2", "extra", "nleft", "iter1",
-         "iter2", "edges1", "edges2", "flags", "frames"]
+         "iter2", "edges1", "edges2", "flags", "frames", "ldets"]
 NSTAT = len(STATS)
 
 

@@ -174,14 +174,26 @@ def velocity(T_prev: np.ndarray, T_cur: np.ndarray) -> np.ndarray:
 
 # ------------------------------------------------------------- local map
 def build_map(scene: Scene, cam, extract, period: int, traj_seed: int, n_map: int, seed: int,
-              n_kf: int = 8, nlevels: int = 8, scale: float = 1.2, device="cpu"):
+              n_kf: int = 8, nlevels: int = 8, scale: float = 1.2, device="cpu", stale_desc: float = 0.0):
     """Map points from n_kf keyframes along the loop: every keypoint of a
     keyframe back-projected onto the scene (duplicates within 2 cm merged,
     first keyframe wins), the keyframe descriptor, normal and the
     scale-invariance distances of UpdateNormalAndDepth. Returns
     (MAP_POINT_DTYPE array, descriptors), at most n_map points in a seeded
     arbitrary order (the reference's std::map<KeyFrame*> pointer order).
-    `extract(img) -> (keypoints, descriptors)`."""
+    `extract(img) -> (keypoints, descriptors)`.
+
+    stale_desc: fraction of the points whose descriptor no longer describes
+    them: a seeded random 256-bit descriptor (Bernoulli 0.5 bits, SURVEY.md
+    §8d's map-descriptor model). These points project into view and enter
+    every visibility and information computation but can practically never
+    be matched (Hamming distance to any keypoint ~128 +- 8 > TH_HIGH = 100),
+    as local-map points triangulated from distant keyframes are in a real
+    sequence. It sets how many matches a frame
+    carries to the next one, hence the SearchReferencePointsInFrustum branch:
+    config 2's recipe (about 60 last-frame matches against GF
+    budget 100, so runActiveMapMatching runs every frame) is stale_desc = 0.94
+    (bench.py --stale-desc)."""
     from .matcher import MAP_POINT_DTYPE
 
     sf = [np.float32(1.0)]
@@ -216,15 +228,22 @@ def build_map(scene: Scene, cam, extract, period: int, traj_seed: int, n_map: in
     mp["normal"] = np.concatenate(Ns)[keep]
     mp["min_dist"] = np.concatenate(dmin)[keep]
     mp["max_dist"] = np.concatenate(dmax)[keep]
-    return mp, np.ascontiguousarray(D[keep])
+    D = np.ascontiguousarray(D[keep])
+    if stale_desc > 0:
+        srng = np.random.default_rng(seed + 0x5747)
+        sel = srng.permutation(len(keep))[:int(round(stale_desc * len(keep)))]
+        D[sel] = srng.integers(0, 256, (len(sel), 32), dtype=np.uint8)
+    return mp, D
 
 
 class Workload:
     """B streams over n_scenes rendered loops (see module docstring)."""
 
     def __init__(self, camera: str, batch: int, n_scenes: int = 8, period: int = 32, seed: int = 0,
-                 phase_stride: int = 5, tex_size: int = 1024, scenes: list | None = None, phase_offset: int = 0):
+                 phase_stride: int = 5, tex_size: int = 1024, scenes: list | None = None, phase_offset: int = 0,
+                 stale_desc: float = 0.0):
         self.cam = synth.CAMERAS[camera]
+        self.stale_desc = stale_desc
         self.B, self.S, self.period, self.seed = batch, min(n_scenes, batch), period, seed
         self.scenes = scenes if scenes is not None else [Scene(seed * 1000 + s, tex_size) for s in range(self.S)]
         self.scene_of = np.arange(batch) % self.S
@@ -254,4 +273,4 @@ class Workload:
 
     def build_maps(self, extract, n_map: int, device="cpu"):
         return [build_map(sc, self.cam, extract, self.period, self.traj_seed[s], n_map, self.seed * 7919 + s,
-                          device=device) for s, sc in enumerate(self.scenes)]
+                          device=device, stale_desc=self.stale_desc) for s, sc in enumerate(self.scenes)]

@@ -308,7 +308,10 @@ int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv
  * by cap / mp_cap; d_Xv is [F][13], d_base [F][49], d_rng [F]). Pool limit
  * for active matching and max-volume selection: 4096 landmarks.
  * gf_obs_accumulate_dev: d_out[f] = diag*I + sum of d_info rows with d_flag
- * set (mCurrentInfoMat accumulation, Tracking.cc:3161 and :3195-3219). */
+ * set (mCurrentInfoMat accumulation, Tracking.cc:3161 and :3195-3219).
+ * gf_obs_active_match_dev: d_nldet (optional, [F]) = logDet evaluations the
+ * reference makes (one per heap push, Observability.cc:1373); frames whose
+ * d_m or d_num_to_match is 0 exit before any LDS use. */
 int gf_obs_build_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_pos,
                           const float* d_sigma2, const int32_t* d_n, int cap, int check_viz, double* d_H,
                           double* d_info, float* d_uv, uint8_t* d_valid, void* stream);
@@ -320,7 +323,7 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
                             const double* d_H, const int32_t* d_m, int mp_cap, const double* d_base,
                             const float* level_sigma2, const int32_t* d_num_to_match, float th, float nnratio,
                             gf_rng* d_rng, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_left, int32_t* d_nleft,
-                            int32_t* d_nmatched, void* stream);
+                            int32_t* d_nmatched, int32_t* d_nldet, void* stream);
 int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const double* d_score, const int32_t* d_n,
                          int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
                          int32_t* d_nout, void* stream);
@@ -856,7 +859,8 @@ typedef struct gf_frontend gf_frontend;
 // g's done event into front end g+1's wait event serialises the
 // bandwidth-bound extraction stages while each front end's tracking kernels
 // overlap the next one's extraction. Events stay owned by the caller.
-// Not part of a captured graph (set before gf_frontend_capture).
+// A gated front end cannot be captured as a graph (gf_frontend_capture
+// refuses), nor can a captured one be gated.
 int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event);
 // A hipEvent_t (timing disabled) on the context's device, for the gate.
 int gf_event_create(gf_ctx* ctx, void** event_out);
@@ -895,6 +899,9 @@ enum {
     GF_FE_RNG,          /* [B] gf_rng std::rand() state per stream          */
     GF_FE_LEFT,         /* [B][M] i32 mLeftMapPoints of the last step       */
     GF_FE_STATS,        /* [GF_FE_NSTAT][B] i32, see GF_ST_*                */
+    GF_FE_HIST,         /* [B][8] i32 running counters since the last write:
+                           [0..5] steps per GF_ST_BRANCH value, [6] logDet
+                           evaluations, [7] local-map search matches         */
     GF_FE_NFIELDS
 };
 enum {
@@ -912,6 +919,8 @@ enum {
     GF_ST_FLAGS,        /* 1: M3 < 20 (TrackPreviousFrame fall-back), 2: < 10 after PoseOptimization,
                            4: mnMatchesInliers < 15 (LOST), 8: a time budget cut a loop */
     GF_ST_FRAMES,       /* frames tracked                                   */
+    GF_ST_LDETS,        /* logDet evaluations of runActiveMapMatching (heap
+                           pushes, Observability.cc:1373): SURVEY §8d E_ld  */
     GF_FE_NSTAT
 };
 int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);
@@ -942,7 +951,11 @@ int gf_frontend_step(gf_frontend* fe);
 /* Same with the B frames taken from host memory ([B][height][width] u8):
  * the PCIe copy is part of the step. */
 int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs);
-/* Capture gf_frontend_step as one HIP graph; later steps replay it. */
+/* Capture gf_frontend_step as one HIP graph; later steps replay it (and
+ * capture again when gf_set_budgets changed the budgets). While the graph
+ * exists the context's scratch buffers are pinned: a call on the same context
+ * that would need a larger one fails with GF_ERR_ARG instead of freeing
+ * memory the graph uses. */
 int gf_frontend_capture(gf_frontend* fe);
 int gf_frontend_sync(gf_frontend* fe);
 /* Copy a whole-batch field (synchronises; bytes must equal the field size). */

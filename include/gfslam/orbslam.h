@@ -3,11 +3,14 @@
  * Re-declares the reference classes on the hot path with the same names,
  * method names and argument meaning (namespace ORB_SLAM):
  *   ORBextractor            include/ORBextractor.h:47-70
- *   ORBmatcher              include/ORBmatcher.h:40-290 (M2, M3, OnePoint, distance)
- *   Frame / MapPoint        include/Frame.h, include/MapPoint.h (the fields the path reads/writes)
+ *   ORBmatcher              include/ORBmatcher.h:40-290 (M2, M3, OnePoint, Budget, SearchByBoW x2,
+ *                           distance)
+ *   Frame / KeyFrame /      include/Frame.h, include/KeyFrame.h, include/MapPoint.h (the fields
+ *   MapPoint                the path reads/writes)
+ *   ORBVocabulary           Thirdparty/DBoW2 TemplatedVocabulary (loaders, transform)
  *   Observability           include/Observability.h:165-741 (PWLS kinematics, matrix building,
- *                           active map matching, max-volume selection)
- *   Optimizer               include/Optimizer.h:53 (PoseOptimization)
+ *                           active map matching, max-volume selection, setSelction_Number)
+ *   Optimizer               include/Optimizer.h:53-54 (PoseOptimization, LocalBundleAdjustment)
  * OpenCV/Armadillo types are replaced by plain value types with the same
  * memory layout where one exists (KeyPoint == cv::KeyPoint, 28 B; Tcw is a
  * row-major float 4x4 like the CV_32F cv::Mat; matrices are row-major f64).
@@ -86,9 +89,42 @@ struct MapPoint {
     float u_proj = 0, v_proj = 0;
     double ObsScore = 0;
     long updateAtFrameId = -1;
+    /* tracking counters (MapPoint.cc:298-312) */
+    int mnVisible = 1, mnFound = 1;
 
     bool isBad() const { return mbBad; }
     void GetWorldPos(float out[3]) const { std::memcpy(out, mWorldPos, sizeof(mWorldPos)); }
+    void IncreaseVisible(int n = 1) { mnVisible += n; }
+    void IncreaseFound(int n = 1) { mnFound += n; }
+};
+
+/* DBoW2 BowVector (word id -> weight) and FeatureVector (node id -> feature
+ * indices) as sorted arrays: node i holds feats[start[i] .. start[i+1]). */
+struct BowVector {
+    std::vector<int32_t> words;
+    std::vector<double> values;
+};
+struct FeatureVector {
+    std::vector<int32_t> nodes, start{0}, feats;
+};
+
+/* ORBVocabulary = TemplatedVocabulary<FORB::TDescriptor, FORB>
+ * (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h), resident on the GPU. */
+class ORBVocabulary {
+public:
+    ORBVocabulary() = default;
+    ~ORBVocabulary();
+    ORBVocabulary(const ORBVocabulary&) = delete;
+    ORBVocabulary& operator=(const ORBVocabulary&) = delete;
+    /* loadFromTextFile (:1352-1432) / loadFromBinaryFile (:1469-1510); false on failure */
+    bool loadFromTextFile(const std::string& filename);
+    bool loadFromBinaryFile(const std::string& filename);
+    /* transform(features, BowVector, FeatureVector, levelsup) (:1141-1270) */
+    void transform(const struct Descriptors& features, BowVector& v, FeatureVector& fv, int levelsup) const;
+    gf_vocab* handle() const { return voc_; }
+
+private:
+    gf_vocab* voc_ = nullptr;
 };
 
 class ORBextractor;
@@ -116,6 +152,12 @@ public:
     float mfScaleFactor = 1.2f;
     std::vector<float> mvScaleFactors, mvLevelSigma2, mvInvLevelSigma2;
 
+    /* Frame::ComputeBoW (Frame.cc:380-387): transform with levelsup 4 */
+    ORBVocabulary* mpORBvocabulary = nullptr;
+    BowVector mBowVec;
+    FeatureVector mFeatVec;
+    void ComputeBoW();
+
     void SetPose(const float Tcw[16]) { std::memcpy(mTcw, Tcw, sizeof(mTcw)); }
     /* Frame::getTwc (Frame.cc:152-163) */
     void getTwc(float Twc[16]) const;
@@ -125,6 +167,24 @@ public:
     int isInFrustum(const std::vector<MapPoint*>& vpMapPoints, float viewingCosLimit);
 
     gf_frame_info info() const;
+};
+
+/* ---------------------------------------------------------------- KeyFrame
+ * The fields of ORB_SLAM::KeyFrame that SearchByBoW reads: built from a
+ * Frame as KeyFrame::KeyFrame(Frame&, Map*, KeyFrameDatabase*) copies them
+ * (KeyFrame.cc:31-58). */
+class KeyFrame {
+public:
+    explicit KeyFrame(const Frame& F);
+    long unsigned int mnId = 0, mnFrameId = 0;
+    int N = 0;
+    std::vector<KeyPoint> mvKeysUn;
+    Descriptors mDescriptors;
+    BowVector mBowVec;
+    FeatureVector mFeatVec;
+    std::vector<MapPoint*> mvpMapPoints;
+    std::vector<MapPoint*> GetMapPointMatches() const { return mvpMapPoints; }
+    MapPoint* GetMapPoint(size_t idx) const { return mvpMapPoints[idx]; }
 };
 
 /* ---------------------------------------------------------------- ORBextractor */
@@ -167,6 +227,23 @@ public:
     int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, float th = 3);
     /* SearchByProjection(Frame& Cur, const Frame& Last, th) (ORBmatcher.cc:2081-2202) */
     int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, float th);
+    /* SearchByProjection_OnePoint(F, pMP, th) (ORBmatcher.h:71-145): the keypoint
+     * index pMP claims in F (F.mvpMapPoints / mvpMatchScore written) or -1. */
+    int SearchByProjection_OnePoint(Frame& F, MapPoint* pMP, const float th);
+    /* SearchByProjection_Budget(F, vpMapPoints, th, time_constr)
+     * (ORBmatcher.cc:276-379): M2 over the list in order with IncreaseFound on
+     * every match. time_constr <= 0 returns 0 at once (:281-282); otherwise the
+     * list is matched in one GPU call (microseconds), so the per-point wall-clock
+     * cut of :366-371 is not reached. */
+    int SearchByProjection_Budget(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th,
+                                  const double time_constr);
+    /* SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) (ORBmatcher.cc:724-853):
+     * vpMapPointMatches[j] = the keyframe's map point matched to F's feature j.
+     * Needs both FeatureVectors (ComputeBoW). Returns the match count. */
+    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
+    /* SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12) (:1289-1424):
+     * vpMatches12[i] = pKF2's map point matched to pKF1's feature i. */
+    int SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoint*>& vpMatches12);
 
     float mfNNratio;
     bool mbCheckOrientation;
@@ -174,6 +251,15 @@ public:
 
 /* ---------------------------------------------------------------- Observability */
 enum { FRAME_INFO_MATRIX = 0, MAP_INFO_MATRIX = 1 };
+
+/* GoodPoint (Util.hpp:65-129): a selected map point, idx into the list given
+ * to setSelction_Number; obs_block is the 7x7 ObsMat row-major. */
+struct GoodPoint {
+    size_t idx = 0;
+    double obs_score = 0;
+    bool selected = false;
+    std::array<double, 49> obs_block{};
+};
 
 class Observability {
 public:
@@ -199,6 +285,17 @@ public:
     std::vector<int> maxVolSelection(const std::vector<std::array<double, 49>>& pool,
                                      const std::vector<double>& score, int k, double sample_scale, int mode);
 
+    /* setSelction_Number(num_good_inlier, greedy_mtd, time_for_select,
+     * mapPoints, mpVec) (Observability.cc:1021-1247): MAP_INFO_MATRIX with the
+     * visibility check at kinematic[1] (mKineIdx = 1) over *mapPoints, then
+     * greedy_mtd 1 BaselineGreedy / 2 LazierGreedy / 3 automatic lazier greedy
+     * with the reference's multi-thread split (sample scale 6). mpVec = the
+     * selection in order. Null / bad points take no part. false when
+     * time_for_select <= 0, mapPoints or mpVec is null, or predictPWLSVec has
+     * not produced kinematic[1]. The time budget is otherwise not applied. */
+    bool setSelction_Number(size_t num_good_inlier, int greedy_mtd, double time_for_select,
+                            std::vector<MapPoint*>* mapPoints, std::vector<GoodPoint>* mpVec);
+
     /* std::srand for the lazier-greedy draws (the reference seeds once). */
     void srand(unsigned seed);
 
@@ -213,6 +310,9 @@ public:
     std::vector<MapPoint*> mLeftMapPoints;
     Frame* pFrame = nullptr;
     bool mbNeedVizCheck = false;
+    /* std::thread::hardware_concurrency() (Observability.h:186): the thread
+     * count of setSelction_Number's greedy split */
+    size_t mNumThreads = 1;
 
 private:
     gf_rng rng_{};

@@ -47,6 +47,7 @@ int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, co
                              const double* info, const double* H, int m, const double* base,
                              const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
                              int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
+long long orc_last_ldets(void);
 }
 
 namespace {
@@ -494,6 +495,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
                                      c->level_sigma2, ntm, 1.f, 0.8f, &c->rng, c->kp2mp.data(), c->score.data(),
                                      left.data(), &nleft, &nmatched);
             st[GF_ST_LOCAL] = nmatched;
+            st[GF_ST_LDETS] = (int32_t)orc_last_ldets();
             list.assign(left.begin(), left.begin() + nleft);
         }
     }

@@ -12,6 +12,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <memory>
 #include <queue>
 #include <vector>
 
@@ -384,6 +385,7 @@ double logdet7(const double* M) {
 }
 
 // ------------------------------------------------------------ RNG
+long long g_ldets = 0;
 static int g_rand_calls = 0;  // rand() calls of the last active-match / max-vol call
 
 struct Rand {  // glibc random_r TYPE_3 (the generator behind std::rand)
@@ -506,6 +508,7 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
                         int* nmatched) {
     *nleft = 0;
     *nmatched = 0;
+    orc::g_ldets = 0;
     auto push_left_all = [&]() {
         for (int i = 0; i < m; i++)
             if (views[i].in_view) left[(*nleft)++] = i;
@@ -523,6 +526,8 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
         }
     const size_t N = lmkIdx.size();
     const size_t szLazier = (size_t)((float)N / (float)num_to_match * 1.0);
+    std::unique_ptr<orc::OnePointGrid, void (*)(orc::OnePointGrid*)> grid(orc::one_point_grid(fi, kps, n),
+                                                                          orc::one_point_grid_free);
     double cur[49];
     std::memcpy(cur, base, sizeof(cur));
     struct SP {
@@ -552,25 +557,16 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
             double M[49];
             for (int k = 0; k < 49; k++) M[k] = cur[k] + info[49 * (size_t)q + k];
             heap.push(SP{q, orc::logdet7(M)});
+            ++orc::g_ldets;
             if (numHit >= szActual) {
                 SP top = heap.top();
-                // one-point match of map point top.idx
-                gf_mp_view one = views[top.idx];
-                int32_t before = -1;
-                (void)before;
-                int cnt = 0;
-                // run the single-query matcher restricted to this map point
-                std::vector<gf_mp_view> vv(m);
-                for (int k = 0; k < m; k++) vv[k] = views[k], vv[k].in_view = 0;
-                vv[top.idx] = one;
-                std::vector<int32_t> kp_before(kp2mp, kp2mp + n);
-                orc_match_project(fi, kps, desc, n, vv.data(), mp_desc, m, th, nnratio, kp2mp, score, &cnt);
-                int bestIdx = -1;
-                if (cnt) {
-                    for (int k = 0; k < n; k++)
-                        if (kp2mp[k] != kp_before[k]) bestIdx = k;
-                }
+                // SearchByProjection_OnePoint of map point top.idx (claims the keypoint)
+                int bd = 0;
+                const int bestIdx = orc::one_point(grid.get(), views[top.idx], mp_desc + 32 * (size_t)top.idx, desc,
+                                                   th, nnratio, kp2mp, &bd);
                 if (bestIdx >= 0) {
+                    kp2mp[bestIdx] = top.idx;
+                    score[bestIdx] = bd;
                     double s2 = (double)level_sigma2[kps[bestIdx].octave];
                     double blk[49];
                     orc::info_block(H + 14 * (size_t)top.idx, s2, blk);
@@ -844,5 +840,8 @@ static int maxvol_select(orc::Rand& R, const double* info, const double* score, 
 
 // rand() calls made by the last orc_obs_active_match / orc_maxvol_select
 int orc_last_rand_calls(void) { return orc::g_rand_calls; }
+
+// logDet evaluations (heap pushes) of the last orc_obs_active_match(_rng)
+long long orc_last_ldets(void) { return orc::g_ldets; }
 
 }  // extern "C"

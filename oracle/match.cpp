@@ -129,6 +129,47 @@ static inline void transform(const float* T, const float* P, float* Pc) {
 
 int g_gemm_mode = 0;
 
+// ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) over a grid
+// built once per frame (runActiveMapMatching's one-point matches).
+struct OnePointGrid {
+    FrameGrid G;
+    OnePointGrid(const gf_frame_info* f, const gf_keypoint* k, int n) : G(f, k, n) {}
+};
+OnePointGrid* one_point_grid(const gf_frame_info* fi, const gf_keypoint* kps, int n) {
+    return new OnePointGrid(fi, kps, n);
+}
+void one_point_grid_free(OnePointGrid* g) { delete g; }
+
+int one_point(const OnePointGrid* g, const gf_mp_view& v, const uint8_t* mp_desc, const uint8_t* desc, float th,
+              float nnratio, const int32_t* kp2mp, int* dist_out) {
+    const FrameGrid& G = g->G;
+    if (!v.in_view) return -1;
+    const int pl = v.level;
+    float r = radius_by_viewing_cos(v.view_cos);
+    if (th != 1.0) r *= th;
+    std::vector<int> near = G.area(v.u, v.v, r * G.scales[pl], pl - 1, pl);
+    if (near.empty()) return -1;
+    int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+    for (int idx : near) {
+        if (kp2mp[idx] >= 0) continue;
+        const int dist = descriptor_distance(mp_desc, desc + 32 * (size_t)idx);
+        if (dist < bestDist) {
+            bestDist2 = bestDist;
+            bestDist = dist;
+            bestLevel2 = bestLevel;
+            bestLevel = G.kps[idx].octave;
+            bestIdx = idx;
+        } else if (dist < bestDist2) {
+            bestLevel2 = G.kps[idx].octave;
+            bestDist2 = dist;
+        }
+    }
+    if (bestDist > TH_HIGH) return -1;
+    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) return -1;
+    *dist_out = bestDist;
+    return bestIdx;
+}
+
 }  // namespace orc
 
 extern "C" {

@@ -82,6 +82,17 @@ static inline int reflect101(int p, int len) {
     return p;
 }
 
+// SearchByProjection_OnePoint over a frame grid built once (oracle/match.cpp):
+// returns the keypoint the map point would claim (not claimed here) or -1.
+struct OnePointGrid;
+OnePointGrid* one_point_grid(const gf_frame_info* fi, const gf_keypoint* kps, int n);
+void one_point_grid_free(OnePointGrid* g);
+int one_point(const OnePointGrid* g, const gf_mp_view& v, const uint8_t* mp_desc, const uint8_t* desc, float th,
+              float nnratio, const int32_t* kp2mp, int* dist_out);
+
+// log-det evaluations of the last runActiveMapMatching (oracle/gf.cpp)
+extern long long g_ldets;
+
 struct Image {
     int w = 0, h = 0;
     std::vector<uint8_t> px;

@@ -5,6 +5,7 @@
 // <dir>/params.txt : w h fx fy cx cy M  then 16 floats Tcw
 // <dir>/img.u8     : h*w bytes
 // <dir>/map.bin    : M x (gf_map_point 32 B + descriptor 32 B)
+// <dir>/voc.bin    : a DBoW2 binary vocabulary
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -123,6 +124,75 @@ int main(int argc, char** argv) {
         std::fprintf(s, "%d %d %d %d %d %d %d %d\n", F.N, nview, nm, ninl, F2.N, n3, nact,
                      ORBmatcher::DescriptorDistance(F.mDescriptors.ptr(0), F.mDescriptors.ptr(1)));
         std::fclose(s);
+
+        auto idx_of = [&](const std::vector<MapPoint*>& v) {
+            std::vector<int32_t> o(v.size());
+            for (size_t i = 0; i < v.size(); i++) o[i] = v[i] ? (int32_t)(v[i] - mps.data()) : -1;
+            return o;
+        };
+
+        // Frame::ComputeBoW (D1) and SearchByBoW KeyFrame-Frame / KeyFrame-KeyFrame (M6)
+        ORBVocabulary voc;
+        if (!voc.loadFromBinaryFile(dir + "/voc.bin") || voc.loadFromTextFile(dir + "/voc.bin")) return 3;
+        F.mpORBvocabulary = &voc;
+        F.ComputeBoW();
+        F2.mpORBvocabulary = &voc;
+        F2.ComputeBoW();
+        dump(dir + "/bow_words.i32", F.mBowVec.words.data(), F.mBowVec.words.size());
+        dump(dir + "/bow_values.f64", F.mBowVec.values.data(), F.mBowVec.values.size());
+        dump(dir + "/fv_nodes.i32", F.mFeatVec.nodes.data(), F.mFeatVec.nodes.size());
+        dump(dir + "/fv_start.i32", F.mFeatVec.start.data(), F.mFeatVec.start.size());
+        dump(dir + "/fv_feats.i32", F.mFeatVec.feats.data(), F.mFeatVec.feats.size());
+        KeyFrame KF(F);    // map points of F: the M2 claims
+        KeyFrame KF2(F2);  // map points of F2: M3 + active matching
+        ORBmatcher mbow(0.75f, true);
+        std::vector<MapPoint*> vm, v12;
+        const int nb0 = mbow.SearchByBoW(&KF, F2, vm);
+        const int nb1 = mbow.SearchByBoW(&KF, &KF2, v12);
+        dump(dir + "/bow_kf_f.i32", idx_of(vm).data(), vm.size());
+        dump(dir + "/bow_kf_kf.i32", idx_of(v12).data(), v12.size());
+
+        // SearchByProjection_OnePoint (M4) then SearchByProjection_Budget (M5) on a fresh frame
+        Frame F3(im, 0.1, &extractor, K);
+        F3.SetPose(F.mTcw);
+        F3.isInFrustum(local, 0.5f);
+        MapPoint* p0 = nullptr;
+        for (MapPoint* q : F.mvpMapPoints)
+            if (q) {
+                p0 = q;
+                break;
+            }
+        ORBmatcher m8(0.8f);
+        const int one = m8.SearchByProjection_OnePoint(F3, p0, 1.0f);
+        const int nbud0 = m8.SearchByProjection_Budget(F3, local, 0.8f, 0.0);  // no time: nothing
+        const int nbud = m8.SearchByProjection_Budget(F3, local, 0.8f, 1.0);
+        dump(dir + "/budget_kp2mp.i32", idx_of(F3.mvpMapPoints).data(), F3.N);
+        dump(dir + "/budget_score.i32", F3.mvpMatchScore.data(), F3.N);
+        long found = 0;
+        for (const MapPoint& q : mps) found += q.mnFound - 1;
+
+        // Observability::setSelction_Number over the local map (G7, map scale)
+        Observability sel(K[0], K[1], h, w, K[2], K[3], 0, 0);
+        sel.mBoundXInFrame = (int)(0.1 * w);
+        sel.mBoundYInFrame = (int)(0.1 * h);
+        sel.updatePWLSVec(0.0, F.mTcw, 0.05, Twc);
+        sel.predictPWLSVec(0.05, 2);
+        sel.mNumThreads = 8;
+        sel.srand(9);
+        std::vector<GoodPoint> good;
+        const bool no_time = sel.setSelction_Number(300, 3, 0.0, &local, &good);
+        const bool ok = sel.setSelction_Number(300, 3, 1.0, &local, &good);
+        std::vector<int32_t> gidx;
+        for (const GoodPoint& g : good) gidx.push_back((int32_t)g.idx);
+        dump(dir + "/select.i32", gidx.data(), gidx.size());
+        std::vector<double> gblk;
+        for (const GoodPoint& g : good) gblk.insert(gblk.end(), g.obs_block.begin(), g.obs_block.end());
+        dump(dir + "/select_blocks.f64", gblk.data(), gblk.size());
+
+        FILE* s2 = std::fopen((dir + "/summary2.txt").c_str(), "w");
+        std::fprintf(s2, "%d %d %d %d %d %ld %d %d %d\n", nb0, nb1, (int)(p0 ? p0 - mps.data() : -1), one, nbud0,
+                     found, nbud, (int)no_time, (int)ok);
+        std::fclose(s2);
     } catch (const GpuError& e) {
         std::fprintf(stderr, "GpuError %d: %s\n", e.code, e.what());
         return 1;

@@ -1,7 +1,9 @@
 """The C++ drop-in layer (include/gfslam/orbslam.h) driven the way Tracking
 drives the reference classes (tests/cpp/dropin_frontend.cpp), compared with
 the CPU oracle: keypoints/descriptors and match indices bit-exact, pose within
-1e-5 relative, outlier flags and active-matching claims identical."""
+1e-5 relative, outlier flags and active-matching claims identical; then
+ComputeBoW, both SearchByBoW overloads, SearchByProjection_OnePoint,
+SearchByProjection_Budget and setSelction_Number through the same layer."""
 import os
 import subprocess
 
@@ -39,6 +41,8 @@ def test_dropin_frontend_matches_oracle(tmp_path):
     rec[:, :32] = mps.view(np.uint8).reshape(-1, 32)
     rec[:, 32:] = mdesc
     rec.tofile(tmp_path / "map.bin")
+    voc = synth.synth_vocabulary(7, k=10, L=3)
+    synth.write_vocab_binary(voc, str(tmp_path / "voc.bin"))
     r = subprocess.run([BIN, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     N, nview, nm, ninl, N2, n3, nact, dd = map(int, open(tmp_path / "summary.txt").read().split())
@@ -95,6 +99,54 @@ def test_dropin_frontend_matches_oracle(tmp_path):
     assert nao == nact and nact > 0
     assert np.array_equal(ka, rd("kp2mp_act.i32", np.int32))
 
+    nb0, nb1, p0, one, nbud0, found, nbud, no_time, ok = map(int, open(tmp_path / "summary2.txt").read().split())
+    # Frame::ComputeBoW (D1): transform(levelsup 4)
+    from gf_orb_slam_amd.bow import read_vocabulary
+    vtree = read_vocabulary(str(tmp_path / "voc.bin"))  # the file's float weights, as the loader reads them
+    words, values, fv = O.bow_transform(vtree, d, 4)
+    assert np.array_equal(rd("bow_words.i32", np.int32), words)
+    assert np.array_equal(rd("bow_values.f64", np.float64), values)
+    for name, o in zip(("fv_nodes", "fv_start", "fv_feats"), fv):
+        assert np.array_equal(rd(name + ".i32", np.int32), o), name
+    # SearchByBoW(KeyFrame, Frame) and SearchByBoW(KeyFrame, KeyFrame), nnratio 0.75 with the
+    # rotation check (M6): KF = F with its M2 claims, F2 = the same image, KF2 = F2 after active matching
+    n0, o0 = O.match_bow(0, 0.75, True, (fv, d, k, k2), (fv, d, k, np.full(N, -1, np.int32)))
+    assert n0 == nb0 and n0 > 0 and np.array_equal(o0, rd("bow_kf_f.i32", np.int32))
+    n1, o1 = O.match_bow(1, 0.75, True, (fv, d, k, k2), (fv, d, k, ka))
+    assert n1 == nb1 and n1 > 0 and np.array_equal(o1, rd("bow_kf_kf.i32", np.int32))
+    # SearchByProjection_OnePoint (M4) of F's first matched map point, then
+    # SearchByProjection_Budget (M5, th 0.8) over the whole local map on a fresh frame
+    assert p0 == k2[np.nonzero(k2 >= 0)[0][0]]
+    v3, _ = O.frustum(info, Tg, mps)
+    only = v3.copy()
+    only["in_view"][:] = 0
+    only["in_view"][p0] = v3["in_view"][p0]
+    kp3 = np.full(N, -1, np.int32)
+    sc3 = np.full(N, 999, np.int32)
+    O.match_project(info, k, d, only, mdesc, 1.0, 0.8, kp3, sc3)
+    hit = np.nonzero(kp3 == p0)[0]
+    assert one == (int(hit[0]) if len(hit) else -1) and one >= 0
+    assert nbud0 == 0  # time_constr <= 0 returns at once (ORBmatcher.cc:281-282)
+    nb = O.match_project(info, k, d, v3, mdesc, 0.8, 0.8, kp3, sc3)
+    assert nb == nbud and found == nbud
+    assert np.array_equal(kp3, rd("budget_kp2mp.i32", np.int32)) and np.array_equal(sc3, rd("budget_score.i32", np.int32))
+    # Observability::setSelction_Number(300, 3, ...) over the local map at kinematic[1] (G7)
+    import ctypes
+    from gf_orb_slam_amd.observability import Rng
+    ks = O.obs_predict(xv, 0.05, 2)
+    xv1 = np.array(ks[1].Xv[:])
+    sel = np.zeros(len(mps), np.int32)
+    nsel = ctypes.c_int()
+    pos = np.ascontiguousarray(mps["pos"], np.float32)
+    assert O.orc().orc_select_map_points(ctypes.byref(ocam), O._p(xv1), O._p(pos), len(pos), 300, 3, 8,
+                                         ctypes.byref(Rng.seeded(9)), O._p(sel), ctypes.byref(nsel)) == 0
+    assert no_time == 0 and ok == 1
+    gsel = rd("select.i32", np.int32)
+    assert len(gsel) == nsel.value == 300 and np.array_equal(gsel, sel[:nsel.value])
+    _, blk, _, _ = O.obs_build_info(ocam, xv1, pos[gsel], None, 1)
+    np.testing.assert_allclose(rd("select_blocks.f64", np.float64).reshape(-1, 49), blk.reshape(-1, 49), rtol=1e-9,
+                               atol=1e-12)
+
 
 SEQ_BIN = os.path.join(ROOT, "tests", "cpp", "sequence_driver")
 
@@ -109,7 +161,7 @@ def test_cpp_sequence_and_local_ba_through_the_abi(tmp_path):
     tracks two rendered sequences for 7 frames (bootstrap + steps from host
     frames) and runs LocalBundleAdjustment(pKF, &mbAbortBA) free and stopped;
     every step equals the CPU oracle chain running free, the local BA results
-    equal the oracle (iterations capped at (1, 0) for the stopped call)."""
+    equal the oracle (iterations capped at (0, 0) for the stopped call: the flag is raised before the solve)."""
     import oracle_chain as C
     from gf_orb_slam_amd import scene
 
@@ -167,7 +219,7 @@ def test_cpp_sequence_and_local_ba_through_the_abi(tmp_path):
                 np.fromfile(tmp_path / f"lba_{tag}_out.u8", np.uint8),
                 np.fromfile(tmp_path / f"lba_{tag}_it.i32", np.int32))
 
-    for tag, its in (("free", (5, 10)), ("stop", (1, 0))):
+    for tag, its in (("free", (5, 10)), ("stop", (0, 0))):
         Tg, Xg, og, ig = _lba(tag)
         To, Xo, oo, io = O.local_ba(p, its=its)
         assert list(ig) == list(io) and np.array_equal(og, oo), tag

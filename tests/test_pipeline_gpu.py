@@ -24,12 +24,12 @@ F64 = ["Xv", "Xv_next", "base", "mp_H", "mp_info", "mp_uv"]
 STATE = C.Chain.STATE + ["stats"]
 
 
-def _setup(camera, nfeat, B, nmap, budget, gf=True, seed=3, n_scenes=2):
+def _setup(camera, nfeat, B, nmap, budget, gf=True, seed=3, n_scenes=2, stale=0.0):
     import torch
 
     from gf_orb_slam_amd.pipeline import FrontEnd
 
-    W = scene.Workload(camera, B, n_scenes=n_scenes, period=32, seed=seed)
+    W = scene.Workload(camera, B, n_scenes=n_scenes, period=32, seed=seed, stale_desc=stale)
     frames = W.render_all("cuda").contiguous()
     maps = W.build_maps(lambda im: O.extract(im, nfeatures=nfeat), nmap)
     fe = FrontEnd(camera, nfeat, B, nmap, budget, gf=gf)
@@ -67,22 +67,28 @@ def _compare(dev, ch, b, name_prefix=""):
 
 
 CASES = {
-    # config 2: EuRoC 752x480, 1000 feats, GF budget 100, 2000-point local map
-    "config2": ("euroc", 1000, 4, 2000, 100, True),
+    # config 2 as the bench times it (SURVEY §8d recipe): 93% stale map
+    # descriptors, ~60 motion-model matches vs GF budget 100, so
+    # runActiveMapMatching runs every frame with ~40 points to match
+    "config2_gf": ("euroc", 1000, 4, 2000, 100, True, 0.93),
+    # config 2 with every map descriptor current: the matches carried from the
+    # last frame exceed the budget (leftovers-only steady state)
+    "config2": ("euroc", 1000, 4, 2000, 100, True, 0.0),
     # the same with a GF budget above the tracked count: runActiveMapMatching every frame
-    "config2_active": ("euroc", 1000, 4, 2000, 400, True),
+    "config2_active": ("euroc", 1000, 4, 2000, 400, True, 0.0),
     # config 3: TUM 640x480, 2000 feats, GF budget 160, 3000-point local map
-    "config3": ("tum", 2000, 3, 3000, 160, True),
+    "config3": ("tum", 2000, 3, 3000, 160, True, 0.0),
+    "config3_gf": ("tum", 2000, 3, 3000, 160, True, 0.93),
     # ORB-SLAM baseline matching (GF off)
-    "baseline": ("euroc", 1000, 3, 2000, 100, False),
+    "baseline": ("euroc", 1000, 3, 2000, 100, False, 0.0),
 }
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", list(CASES))
 def test_sequence_matches_oracle(case):
-    camera, nfeat, B, nmap, budget, gf = CASES[case]
-    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf)
+    camera, nfeat, B, nmap, budget, gf, stale = CASES[case]
+    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf, stale=stale)
     free = []
     for b in range(B):
         ch = C.Chain(camera, nfeat, nmap, budget, gf)
@@ -111,6 +117,8 @@ def test_sequence_matches_oracle(case):
             assert dev["stats"][14, b] & 4 == 0, "track lost"
     if case == "config2_active":
         assert branches.count(3) >= len(branches) // 4
+    if case.endswith("_gf"):
+        assert branches.count(3) >= 0.9 * len(branches)  # active matching on (nearly) every frame
     if case == "config2":
         assert branches.count(1) >= len(branches) // 2  # the steady state: matches carried from the last frame
     fe.close()
@@ -127,7 +135,7 @@ def test_bench_shape_parity():
     from gf_orb_slam_amd.pipeline import FrontEnd, chain_extraction
 
     G, Bg = 2, 512
-    W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5)
+    W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5, stale_desc=0.93)
     frames = W.render_all("cuda").contiguous()
     maps = W.build_maps(lambda im: O.extract(im), 2000)
     T, V = W.boot_state()
@@ -157,6 +165,8 @@ def test_bench_shape_parity():
                 ch.load_from(states[g], b)
                 ch.step(_img(W, fr, g * Bg + b, k))
                 _compare(dev, ch, b, f"group {g} step {k}: ")
+            if k == 2:  # the timed regime: active matching on most streams
+                assert (dev["stats"][3] == 3).mean() >= 0.8
             states[g] = dev
     for fe in fes:
         fe.close()
