@@ -368,6 +368,8 @@ def main():
                     help="also time one sequence alone (per-frame latency, HIP graph replay)")
     ap.add_argument("--isolated-steps", type=int, default=5,
                     help="also time the priced kernel with one group running alone")
+    ap.add_argument("--budget-steps", type=int, default=5,
+                    help="also time the step with the reference's time budgets on (gf_set_budgets)")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="also time one group with the frames handed over from host memory")
     args = ap.parse_args()
@@ -635,6 +637,41 @@ def main():
                                        "others": {k: v for k, v in iso.items() if k != dom},
                                        "note": "one group alone, HIP events; `frac` above is the timed region "
                                                "with the groups overlapping"}
+    if args.budget_steps > 0:
+        # the reference's own time budgets (SURVEY §7 budgets-on leg): time_total_match = 15 ms
+        # (Tracking.cc:3230) and the post-publish rest 1 / (0.5 fps) - 2 ms (Tracking.cc:866),
+        # measured on the device clock from each step's start
+        sel_s = 1.0 / (0.5 * 20.0) - 0.002
+        for fe in fes:
+            fe.set_budgets(0.015, sel_s)
+            fe.write("hist", np.zeros((fe.B, 8), np.int32))
+        for fe in fes:  # the first budgeted step runs eagerly
+            fe.step()
+        for fe in fes:
+            fe.sync()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        cut_f = cut_s = 0
+        for _ in range(args.budget_steps):
+            for fe in fes:
+                fe.step()
+        for fe in fes:
+            fe.sync()
+        db = time.perf_counter() - t1
+        for fe in fes:
+            st = fe.read("stats")
+            cut_f += int((st[STATS.index("branch")] == 5).sum())
+            cut_s += int((st[STATS.index("flags")] & 16 != 0).sum())
+            fe.set_budgets()
+        bh = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)
+        out["budgets_on"] = {"match_s": 0.015, "select_s": round(sel_s, 4), "steps": args.budget_steps,
+                             "frames_per_s": round(B * args.budget_steps / db, 1),
+                             "ms_per_step": round(db / args.budget_steps * 1e3, 3),
+                             "branch_mix": {"active_matching": int(bh[:, 3].sum()), "budget_cut": int(bh[:, 5].sum()),
+                                            "leftovers_only": int(bh[:, 1].sum())},
+                             "last_step_cuts": {"isInFrustum": cut_f, "additional_matches": cut_s},
+                             "note": "gf_set_budgets with the reference's budgets, device clock from the step "
+                                     "start of the whole batch; parity mode (+inf) is the headline"}
     for fe in fes:
         fe.close()
     if rank == 0 and args.single_stream_steps > 0:

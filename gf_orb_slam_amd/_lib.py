@@ -146,6 +146,7 @@ _PROTOS = {
     "gf_frontend_set_source": [_P, _P, _P, _I, _S],
     "gf_frontend_set_map": [_P, _I, _P, _P, _I],
     "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
+    "gf_frontend_set_covis": [_P, _I, _P],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
     "gf_update_reference": [_P, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P],

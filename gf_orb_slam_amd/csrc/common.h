@@ -60,6 +60,12 @@ int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out);
 // Host-family helper: copy host -> scratch slot (returns device pointer).
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out);
 
+// UpdateReference of B frames, each against its own keyframe graph (refmap.hip).
+int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap, int nframes, int32_t* d_frame_mps,
+                            const int32_t* d_nkps, int stride, int32_t* d_local_kfs, int32_t* d_n_local_kfs,
+                            int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap, int32_t* d_ref_kf,
+                            int32_t* d_first, hipStream_t s);
+
 // RCCL broadcast on the communicator's stream (dist.hip), asynchronous.
 int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);
 int dist_rank(gf_dist* d);

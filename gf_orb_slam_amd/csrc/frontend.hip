@@ -59,11 +59,21 @@ struct FeDev {
     float* V;
     double* t_prev;
     double* t_cur;
-    // map
+    // map the tracking stages work on: the stream's map, or with a keyframe
+    // graph (gf_frontend_set_covis) the local map UpdateReference assembled
+    // this step, gathered from the stream's map in mvpLocalMapPoints order
     const gf_map_point* map;
     const int32_t* nmp;
     gf_mp_view* views;
     int32_t* upd;
+    // the stream's map itself (GF_FE_MAP... fields) and the local-map lists
+    int refmap;
+    const gf_map_point* gmap;
+    const int32_t* gnmp;
+    int32_t* gupd;
+    int32_t* lmp;  // [B][M] local map points (map indices), mvpLocalMapPoints order
+    int32_t* nlm;  // [B]
+    int32_t* g2l;  // [B][M] map index -> local index, -1 outside the local map
     // lists and gates
     int32_t* left;
     int32_t* left1;
@@ -238,7 +248,23 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
     D.nlist_viz[b] = (viz && !no_time) ? n : 0;
     if (no_time) {
         D.nlist[b] = 0;
-        if (n) stat(D, GF_ST_FLAGS)[b] |= 8;
+        if (n) stat(D, GF_ST_FLAGS)[b] |= 8 | 16;
+    }
+}
+
+// The visibility pass of SearchAdditionalMatchesInFrame skips the points
+// matched before the local-map search (mnLastFrameSeen == mnId,
+// Tracking.cc:3110-3111), so they keep mbTrackInView = false: after the list
+// frustum of a stream that ran the pass, matched points are out of view again.
+// Only the isInFrustum-cut list (branch 5) holds such points.
+__global__ __launch_bounds__(256) void k_fe_viz_exclude(FeDev D) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    if (D.nlist_viz[b] <= 0) return;
+    const int n = D.nkp[b], m = D.nmp[b];
+    const long long o = (long long)b * D.cap;
+    for (int i = t; i < n; i += 256) {
+        const int mp = D.kp2mp[o + i];
+        if (mp >= 0 && mp < m) D.views[(long long)b * D.M + mp].in_view = 0;
     }
 }
 
@@ -256,7 +282,7 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
         D.last_kps[o + i] = D.kps[o + i];
         float* p = D.last_pos + 3 * (o + i);
         if (mp >= 0) {
-            const gf_map_point& P = D.map[(long long)b * D.M + mp];
+            const gf_map_point& P = D.gmap[(long long)b * D.M + mp];
             p[0] = P.pos[0];
             p[1] = P.pos[1];
             p[2] = P.pos[2];
@@ -267,8 +293,8 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
     const uint4* ds = (const uint4*)(D.desc + o * 32);
     uint4* dd = (uint4*)(D.last_desc + o * 32);
     for (int i = t; i < 2 * n; i += 256) dd[i] = ds[i];
-    const int m = D.nmp[b];
-    for (int i = t; i < m; i += 256) D.upd[(long long)b * D.M + i] -= 1;
+    const int m = D.gnmp[b];
+    for (int i = t; i < m; i += 256) D.gupd[(long long)b * D.M + i] -= 1;
     if (t == 0) {
         D.last_nkp[b] = n;
         for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
@@ -300,7 +326,7 @@ __global__ __launch_bounds__(256) void k_fe_boot_end(FeDev D) {
         D.last_kps[o + i] = D.kps[o + i];
         float* p = D.last_pos + 3 * (o + i);
         if (mp >= 0) {
-            const gf_map_point& P = D.map[(long long)b * D.M + mp];
+            const gf_map_point& P = D.gmap[(long long)b * D.M + mp];
             p[0] = P.pos[0];
             p[1] = P.pos[1];
             p[2] = P.pos[2];
@@ -317,6 +343,83 @@ __global__ __launch_bounds__(256) void k_fe_boot_end(FeDev D) {
         D.t_prev[b] = D.t_cur[b];
         if (b == 0) *D.step += 1;
     }
+}
+
+// Local-map arrays for the step (one workgroup per stream). Gather: entry k
+// of the local map is the stream's map point lmp[k] (UpdateReference order);
+// the frame's matches move to local indices (a match outside the local map is
+// dropped; UpdateReference puts every matched point's keyframes in it).
+struct MapArrays {
+    const gf_map_point* map;
+    const uint8_t* desc;
+    const float* pos;
+    gf_mp_view* views;
+    double* H;
+    double* info;
+    float* uv;
+    int32_t* upd;
+};
+
+__global__ __launch_bounds__(256) void k_fe_gather(FeDev D, MapArrays G, MapArrays L, int32_t* lnmp) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int n = D.nlm[b];
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    for (int k = t; k < n; k += 256) {
+        const long long g = o + lm[k], l = o + k;
+        ((gf_map_point*)L.map)[l] = G.map[g];
+        reinterpret_cast<uint4*>((uint8_t*)L.desc + 32 * l)[0] = reinterpret_cast<const uint4*>(G.desc + 32 * g)[0];
+        reinterpret_cast<uint4*>((uint8_t*)L.desc + 32 * l)[1] = reinterpret_cast<const uint4*>(G.desc + 32 * g)[1];
+        for (int c = 0; c < 3; c++) ((float*)L.pos)[3 * l + c] = G.pos[3 * g + c];
+        L.views[l] = G.views[g];
+        L.uv[2 * l] = G.uv[2 * g];
+        L.uv[2 * l + 1] = G.uv[2 * g + 1];
+        L.upd[l] = G.upd[g];
+        D.g2l[g] = k;
+    }
+    for (int e = t; e < 14 * n; e += 256) L.H[14 * o + e] = G.H[14 * (o + lm[e / 14]) + e % 14];
+    for (int e = t; e < 49 * n; e += 256) L.info[49 * o + e] = G.info[49 * (o + lm[e / 49]) + e % 49];
+    if (t == 0) {
+        lnmp[b] = n;
+        stat(D, GF_ST_NLOCAL)[b] = n;
+    }
+    __syncthreads();
+    const long long ko = (long long)b * D.cap;
+    const int nk = D.nkp[b];
+    for (int i = t; i < nk; i += 256) {
+        const int mp = D.kp2mp[ko + i];
+        if (mp < 0) continue;
+        const int l = D.g2l[o + mp];
+        D.kp2mp[ko + i] = l;
+        if (l < 0) D.score[ko + i] = 999;
+    }
+}
+
+// Scatter: the local map's observability state and visibility back to the
+// stream's map points, matches and mLeftMapPoints back to map indices.
+__global__ __launch_bounds__(256) void k_fe_scatter(FeDev D, MapArrays G, MapArrays L) {
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int n = D.nlm[b];
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    for (int k = t; k < n; k += 256) {
+        const long long g = o + lm[k], l = o + k;
+        G.views[g] = L.views[l];
+        G.uv[2 * g] = L.uv[2 * l];
+        G.uv[2 * g + 1] = L.uv[2 * l + 1];
+        G.upd[g] = L.upd[l];
+        D.g2l[g] = -1;
+    }
+    for (int e = t; e < 14 * n; e += 256) G.H[14 * (o + lm[e / 14]) + e % 14] = L.H[14 * o + e];
+    for (int e = t; e < 49 * n; e += 256) G.info[49 * (o + lm[e / 49]) + e % 49] = L.info[49 * o + e];
+    const long long ko = (long long)b * D.cap;
+    const int nk = D.nkp[b];
+    for (int i = t; i < nk; i += 256) {
+        const int l = D.kp2mp[ko + i];
+        if (l >= 0) D.kp2mp[ko + i] = lm[l];
+    }
+    const int nl = stat(D, GF_ST_NLEFT)[b];
+    for (int j = t; j < nl; j += 256) D.left[o + j] = lm[D.left[o + j]];
 }
 
 __global__ void k_fe_boot_begin(FeDev D) {
@@ -342,6 +445,25 @@ struct gf_frontend {
     // fields
     void* field_ptr[GF_FE_NFIELDS] = {};
     size_t field_bytes[GF_FE_NFIELDS] = {};
+    // the stream maps (the GF_FE_MAP... fields); the working arrays below
+    // (D.map, D.views, D.upd, D.nmp, mp_pos, mp_H, mp_info, mp_uv, wdesc) alias
+    // them, or with keyframe graphs hold the local map of the step
+    MapArrays gm{};
+    int32_t* g_nmp = nullptr;
+    const uint8_t* wdesc = nullptr;
+    int32_t* w_nmp = nullptr;
+    // keyframe graphs (gf_frontend_set_covis): per-stream slabs, device array of
+    // per-stream gf_covis_map, UpdateReference outputs and scratch
+    static const int KF_CAP = 64;
+    int covis_set = 0;
+    std::vector<int> h_nmp;
+    std::vector<uint8_t> has_covis;
+    gf_covis_map* d_covis = nullptr;
+    uint8_t *cv_kf_bad = nullptr, *cv_mp_bad = nullptr;
+    int32_t *cv_kf_mp_off = nullptr, *cv_kf_mp = nullptr, *cv_kf_cov_off = nullptr, *cv_kf_cov = nullptr;
+    int32_t *cv_mp_obs_off = nullptr, *cv_mp_obs = nullptr;
+    size_t slot_cap = 0;
+    int32_t *lkf = nullptr, *nlkf = nullptr, *ref_kf = nullptr, *rm_first = nullptr;
     // device buffers not exported as fields
     int32_t* scratch = nullptr;
     int32_t* num_to_match = nullptr;  // = stats column
@@ -430,11 +552,21 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
                                  D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp, D.score,
                                  col(GF_ST_M3), fe->scratch, s));
-    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
+    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
                                  fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
                                  col(GF_ST_ITER1), col(GF_ST_EDGES1), s));
     FE_RC(gf_discard_outliers_dev(ctx, B, D.kp2mp, D.outl, D.nkp, cap, D.budget, col(GF_ST_FOUND),
                                   col(GF_ST_TO_MATCH), s));
+    const MapArrays WM{D.map, fe->wdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
+    if (D.refmap) {
+        // TrackLocalMap -> UpdateReference (Tracking.cc:2745, 3689-3852): local
+        // keyframes and mvpLocalMapPoints from this frame's matches
+        FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp, cap, fe->lkf, fe->nlkf,
+                                          gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
+        GF_PROF(ctx, s, "k_fe_gather");
+        k_fe_gather<<<B, 256, 0, s>>>(D, fe->gm, WM, fe->w_nmp);
+        GF_HIP(hipGetLastError());
+    }
     // TrackLocalMap -> SearchReferencePointsInFrustum
     if (D.gf) {
         FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, s));
@@ -459,15 +591,14 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.gf) {
         FE_RC(gf_obs_map_info_dev(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
                                   fe->mp_info, fe->mp_uv, fe->mp_updated, s));
-        FE_RC(gf_obs_active_match_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
-                                      (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], fe->mp_updated, fe->mp_info,
+        FE_RC(gf_obs_active_match_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
+                                      fe->mp_info,
                                       fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2, col(GF_ST_TO_MATCH), 1.f,
                                       0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score, D.left, D.nleft,
                                       col(GF_ST_LOCAL), col(GF_ST_LDETS), s));
     }
-    FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
-                               (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], D.m_m2, M, 1.f, 0.8f, D.kp2mp, D.score,
-                               D.nm2, s));
+    FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, 1.f, 0.8f,
+                               D.kp2mp, D.score, D.nm2, s));
     FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
                                  fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL2),
                                  col(GF_ST_ITER2), col(GF_ST_EDGES2), s));
@@ -483,9 +614,18 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                   fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, s));
         // SearchAdditionalMatchesInFrame
         FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview, s));
-        FE_RC(gf_match_project_list_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views,
-                                        (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], M, D.left, D.nlist, 0.8f,
-                                        0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA), s));
+        {
+            GF_PROF(ctx, s, "k_fe_viz_exclude");
+            k_fe_viz_exclude<<<B, 256, 0, s>>>(D);
+            GF_HIP(hipGetLastError());
+        }
+        FE_RC(gf_match_project_list_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, M, D.left, D.nlist,
+                                        0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA), s));
+    }
+    if (D.refmap) {
+        GF_PROF(ctx, s, "k_fe_scatter");
+        k_fe_scatter<<<B, 256, 0, s>>>(D, fe->gm, WM);
+        GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_fe_end");
@@ -609,6 +749,16 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     F(-1, int32_t, B, fe->nview);
     F(-1, int32_t, 1, D.step);
     F(-1, unsigned long long, B, D.t0);
+    // the stream maps; the working arrays alias them until a keyframe graph is set
+    fe->gm = MapArrays{map, mdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
+    fe->g_nmp = nmp;
+    fe->wdesc = mdesc;
+    fe->w_nmp = nmp;
+    D.gmap = map;
+    D.gnmp = nmp;
+    D.gupd = D.upd;
+    D.refmap = 0;
+    fe->has_covis.assign(B, 0);
     const uint8_t** ptrs = nullptr;
     F(-1, const uint8_t*, B, ptrs);
     D.ptrs = ptrs;
@@ -680,15 +830,122 @@ int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, co
     for (int i = 0; i < m; i++)
         for (int c = 0; c < 3; c++) pos[3 * i + c] = mps[i].pos[c];
     if (m) {
-        GF_HIP(hipMemcpy((gf_map_point*)fe->D.map + o, mps, sizeof(gf_map_point) * m, hipMemcpyHostToDevice));
-        GF_HIP(hipMemcpy((uint8_t*)fe->field_ptr[GF_FE_MAP_DESC] + o * 32, desc, 32 * (size_t)m,
-                         hipMemcpyHostToDevice));
-        GF_HIP(hipMemcpy(fe->mp_pos + 3 * o, pos.data(), 12 * (size_t)m, hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy((gf_map_point*)fe->gm.map + o, mps, sizeof(gf_map_point) * m, hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy((uint8_t*)fe->gm.desc + o * 32, desc, 32 * (size_t)m, hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy((float*)fe->gm.pos + 3 * o, pos.data(), 12 * (size_t)m, hipMemcpyHostToDevice));
     }
-    GF_HIP(hipMemcpy((int32_t*)fe->D.nmp + stream, &m, 4, hipMemcpyHostToDevice));
+    GF_HIP(hipMemcpy(fe->g_nmp + stream, &m, 4, hipMemcpyHostToDevice));
     std::vector<int32_t> neg(M, -1000);
-    GF_HIP(hipMemcpy(fe->D.upd + o, neg.data(), 4 * M, hipMemcpyHostToDevice));
-    GF_HIP(hipMemset(fe->D.views + o, 0, sizeof(gf_mp_view) * M));
+    GF_HIP(hipMemcpy(fe->gm.upd + o, neg.data(), 4 * M, hipMemcpyHostToDevice));
+    GF_HIP(hipMemset(fe->gm.views + o, 0, sizeof(gf_mp_view) * M));
+    if (fe->covis_set) fe->has_covis[stream] = 0;  // the keyframe graph indexes the old points
+    return GF_OK;
+}
+
+static int fe_enable_covis(gf_frontend* fe) {
+    FeDev& D = fe->D;
+    const size_t B = D.B, M = D.M;
+    int rc;
+    void* p;
+#define A_(bytes, dst)                                 \
+    if ((rc = fe_alloc(fe, (bytes), &p))) return rc; \
+    dst = (decltype(dst))p;
+    gf_map_point* wmap;
+    uint8_t* wdesc;
+    A_(sizeof(gf_map_point) * B * M, wmap);
+    A_(32 * B * M, wdesc);
+    A_(12 * B * M, fe->mp_pos);
+    A_(sizeof(gf_mp_view) * B * M, D.views);
+    A_(8 * 14 * B * M, fe->mp_H);
+    A_(8 * 49 * B * M, fe->mp_info);
+    A_(8 * B * M, fe->mp_uv);
+    A_(4 * B * M, D.upd);
+    A_(4 * B, fe->w_nmp);
+    A_(4 * B * M, D.lmp);
+    A_(4 * B, D.nlm);
+    A_(4 * B * M, D.g2l);
+    A_(4 * B * gf_frontend::KF_CAP, fe->lkf);
+    A_(4 * B, fe->nlkf);
+    A_(4 * B, fe->ref_kf);
+    A_(4 * B * M, fe->rm_first);
+    fe->slot_cap = (size_t)gf_frontend::KF_CAP * (size_t)D.cap;
+    A_(sizeof(gf_covis_map) * B, fe->d_covis);
+    A_(B * gf_frontend::KF_CAP, fe->cv_kf_bad);
+    A_(4 * B * (gf_frontend::KF_CAP + 1), fe->cv_kf_mp_off);
+    A_(4 * B * fe->slot_cap, fe->cv_kf_mp);
+    A_(4 * B * (gf_frontend::KF_CAP + 1), fe->cv_kf_cov_off);
+    A_(4 * B * gf_frontend::KF_CAP * gf_frontend::KF_CAP, fe->cv_kf_cov);
+    A_(B * M, fe->cv_mp_bad);
+    A_(4 * B * (M + 1), fe->cv_mp_obs_off);
+    A_(4 * B * fe->slot_cap, fe->cv_mp_obs);
+#undef A_
+    GF_HIP(hipMemset(D.g2l, 0xff, 4 * B * M));
+    D.map = wmap;
+    D.nmp = fe->w_nmp;
+    fe->wdesc = wdesc;
+    D.refmap = 1;
+    fe->covis_set = 1;
+    return GF_OK;
+}
+
+int gf_frontend_set_covis(gf_frontend* fe, int stream, const gf_covis_map* g) {
+    GF_CHECK(fe && g && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad arguments");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set keyframe graphs before capturing a graph");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    int32_t nmp = 0;
+    GF_HIP(hipMemcpy(&nmp, fe->g_nmp + stream, 4, hipMemcpyDeviceToHost));
+    const int nkf = g->nkf;
+    GF_CHECK(g->nmp == nmp, GF_ERR_ARG, "the keyframe graph must index the stream's map points (gf_frontend_set_map)");
+    GF_CHECK(nkf >= 0 && nkf <= gf_frontend::KF_CAP, GF_ERR_UNSUPPORTED, "at most 64 keyframes per stream graph");
+    GF_CHECK(nkf == 0 || (g->kf_bad && g->kf_mp_off && g->kf_cov_off), GF_ERR_ARG, "null keyframe arrays");
+    GF_CHECK(nmp == 0 || (g->mp_bad && g->mp_obs_off), GF_ERR_ARG, "null map point arrays");
+    if (!fe->covis_set) FE_RC(fe_enable_covis(fe));
+    // host validation: the kernels index with these
+    const size_t ns = nkf ? (size_t)g->kf_mp_off[nkf] : 0, nc = nkf ? (size_t)g->kf_cov_off[nkf] : 0;
+    const size_t no = nmp ? (size_t)g->mp_obs_off[nmp] : 0;
+    GF_CHECK(ns <= fe->slot_cap && no <= fe->slot_cap && nc <= (size_t)nkf * nkf, GF_ERR_CAP,
+             "keyframe graph larger than the per-stream capacity");
+    for (int k = 0; k < nkf; k++)
+        GF_CHECK(g->kf_mp_off[k] >= 0 && g->kf_mp_off[k] <= g->kf_mp_off[k + 1] && g->kf_cov_off[k] >= 0 &&
+                     g->kf_cov_off[k] <= g->kf_cov_off[k + 1],
+                 GF_ERR_ARG, "keyframe offsets must be ascending");
+    for (size_t i = 0; i < ns; i++)
+        GF_CHECK(g->kf_mp[i] >= -1 && g->kf_mp[i] < nmp, GF_ERR_ARG, "keyframe slot out of range");
+    for (size_t i = 0; i < nc; i++) GF_CHECK(g->kf_cov[i] >= 0 && g->kf_cov[i] < nkf, GF_ERR_ARG, "bad covisible keyframe");
+    for (int m = 0; m < nmp; m++)
+        GF_CHECK(g->mp_obs_off[m] >= 0 && g->mp_obs_off[m] <= g->mp_obs_off[m + 1], GF_ERR_ARG,
+                 "observation offsets must be ascending");
+    for (size_t i = 0; i < no; i++) GF_CHECK(g->mp_obs[i] >= 0 && g->mp_obs[i] < nkf, GF_ERR_ARG, "bad observation");
+    const size_t b = stream, M = fe->D.M, KC = gf_frontend::KF_CAP;
+    gf_covis_map d{};
+    d.nkf = nkf;
+    d.nmp = nmp;
+    d.kf_bad = fe->cv_kf_bad + b * KC;
+    d.kf_mp_off = fe->cv_kf_mp_off + b * (KC + 1);
+    d.kf_mp = fe->cv_kf_mp + b * fe->slot_cap;
+    d.kf_cov_off = fe->cv_kf_cov_off + b * (KC + 1);
+    d.kf_cov = fe->cv_kf_cov + b * KC * KC;
+    d.mp_bad = fe->cv_mp_bad + b * M;
+    d.mp_obs_off = fe->cv_mp_obs_off + b * (M + 1);
+    d.mp_obs = fe->cv_mp_obs + b * fe->slot_cap;
+    auto up = [](const void* dst, const void* src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpy((void*)dst, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+    };
+    if (nkf) {
+        GF_HIP(up(d.kf_bad, g->kf_bad, nkf));
+        GF_HIP(up(d.kf_mp_off, g->kf_mp_off, 4 * ((size_t)nkf + 1)));
+        GF_HIP(up(d.kf_cov_off, g->kf_cov_off, 4 * ((size_t)nkf + 1)));
+    }
+    GF_HIP(up(d.kf_mp, g->kf_mp, 4 * ns));
+    GF_HIP(up(d.kf_cov, g->kf_cov, 4 * nc));
+    if (nmp) {
+        GF_HIP(up(d.mp_bad, g->mp_bad, nmp));
+        GF_HIP(up(d.mp_obs_off, g->mp_obs_off, 4 * ((size_t)nmp + 1)));
+    }
+    GF_HIP(up(d.mp_obs, g->mp_obs, 4 * no));
+    GF_HIP(hipMemcpy(fe->d_covis + b, &d, sizeof(d), hipMemcpyHostToDevice));
+    fe->has_covis[b] = 1;
     return GF_OK;
 }
 
@@ -756,10 +1013,11 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
     GF_HIP(hipMemcpyAsync(D.score, s999.data(), 4 * s999.size(), hipMemcpyHostToDevice, s));
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
-    FE_RC(gf_frustum_dev(ctx, &fe->fi, B, D.Tcw, D.map, D.nmp, M, 0.5f, D.views, fe->nview, s));
-    FE_RC(gf_match_project_dev(ctx, &fe->fi, B, D.kps, D.desc, D.nkp, cap, D.views,
-                               (const uint8_t*)fe->field_ptr[GF_FE_MAP_DESC], D.nmp, M, 1.f, 0.8f, D.kp2mp, D.score,
-                               fe->scratch, s));
+    // the first frame is matched against the whole stream map (with keyframe
+    // graphs too: a local map needs the matches of a tracked frame)
+    FE_RC(gf_frustum_dev(ctx, &fe->fi, B, D.Tcw, fe->gm.map, fe->g_nmp, M, 0.5f, fe->gm.views, fe->nview, s));
+    FE_RC(gf_match_project_dev(ctx, &fe->fi, B, D.kps, D.desc, D.nkp, cap, fe->gm.views, fe->gm.desc, fe->g_nmp, M,
+                               1.f, 0.8f, D.kp2mp, D.score, fe->scratch, s));
     k_fe_boot_end<<<B, 256, 0, s>>>(D);
     GF_HIP(hipGetLastError());
     GF_HIP(hipStreamSynchronize(s));
@@ -788,9 +1046,17 @@ int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
     return GF_OK;
 }
 
+static int fe_check_covis(gf_frontend* fe) {
+    if (!fe->covis_set) return GF_OK;
+    for (int b = 0; b < fe->D.B; b++)
+        GF_CHECK(fe->has_covis[b], GF_ERR_ARG, "stream " + std::to_string(b) + " has no keyframe graph");
+    return GF_OK;
+}
+
 int gf_frontend_step(gf_frontend* fe) {
     GF_CHECK(fe, GF_ERR_ARG, "null front end");
     GF_CHECK(fe->sourced || fe->D.src_mode == 2, GF_ERR_ARG, "no frame source set");
+    FE_RC(fe_check_covis(fe));
     GF_HIP(hipSetDevice(fe->ctx->device));
     // budgets of the context, as device clock ticks (100 MHz)
     auto ticks = [](double s) -> long long { return std::isfinite(s) && s >= 0 ? (long long)(s * 1e8) : -1; };
@@ -811,6 +1077,7 @@ int gf_frontend_step(gf_frontend* fe) {
 
 int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
     GF_CHECK(fe && imgs, GF_ERR_ARG, "null arg");
+    FE_RC(fe_check_covis(fe));
     GF_HIP(hipSetDevice(fe->ctx->device));
     FeDev& D = fe->D;
     hipStream_t s = fe->ctx->stream;
@@ -829,6 +1096,7 @@ int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
 
 int gf_frontend_capture(gf_frontend* fe) {
     GF_CHECK(fe && fe->sourced, GF_ERR_ARG, "capture needs a frame source");
+    FE_RC(fe_check_covis(fe));
     // a recorded event in a graph is not the caller's event at replay: the
     // extraction gate would silently stop gating
     GF_CHECK(!fe->gate_wait && !fe->gate_done, GF_ERR_ARG, "a gated front end cannot be captured as a graph");
@@ -894,7 +1162,7 @@ int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes
         std::vector<float> pos(3 * n);
         for (size_t i = 0; i < n; i++)
             for (int c = 0; c < 3; c++) pos[3 * i + c] = m[i].pos[c];
-        GF_HIP(hipMemcpy(fe->mp_pos, pos.data(), 12 * n, hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy((float*)fe->gm.pos, pos.data(), 12 * n, hipMemcpyHostToDevice));
     }
     return GF_OK;
 }
@@ -922,14 +1190,14 @@ extern "C" int gf_dist_bcast_map(gf_dist* d, gf_frontend* fe, int root) {
     if ((rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_MAP], fe->field_bytes[GF_FE_MAP], root)) ||
         (rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_MAP_DESC], fe->field_bytes[GF_FE_MAP_DESC], root)) ||
         (rc = gf::dist_bcast(d, fe->field_ptr[GF_FE_NMP], fe->field_bytes[GF_FE_NMP], root)) ||
-        (rc = gf::dist_bcast(d, fe->mp_pos, sizeof(float) * 3 * (size_t)fe->D.B * fe->D.M, root)))
+        (rc = gf::dist_bcast(d, (void*)fe->gm.pos, sizeof(float) * 3 * (size_t)fe->D.B * fe->D.M, root)))
         return rc;
     GF_HIP(hipStreamSynchronize(gf::dist_ctx(d)->stream));
     if (gf::dist_rank(d) != root) {
         const size_t n = (size_t)fe->D.B * fe->D.M;
         std::vector<int32_t> neg(n, -1000);
-        GF_HIP(hipMemcpy(fe->D.upd, neg.data(), 4 * n, hipMemcpyHostToDevice));
-        GF_HIP(hipMemset(fe->D.views, 0, sizeof(gf_mp_view) * n));
+        GF_HIP(hipMemcpy(fe->gm.upd, neg.data(), 4 * n, hipMemcpyHostToDevice));
+        GF_HIP(hipMemset(fe->gm.views, 0, sizeof(gf_mp_view) * n));
     }
     return GF_OK;
 }

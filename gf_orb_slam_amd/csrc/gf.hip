@@ -515,27 +515,28 @@ struct Cands {
     uint8_t* alive;  // still in the heap
 };
 
+// True when a lower lane of the wave holds the same value (the earlier try of
+// a batch on the same column wins): 63 lane reads, no LDS.
+__device__ __forceinline__ bool dup_of_lower_lane(int v) {
+    const int lane = threadIdx.x;
+    bool dup = false;
+#pragma unroll
+    for (int k = 0; k < 63; k++) dup |= (k < lane) & (__builtin_amdgcn_readlane(v, k) == v);
+    return dup;
+}
+
 // One batch of 64 tries: tries are accepted in order when their column was not
 // visited this round and not drawn earlier in the batch; accepted columns are
 // marked visited at once (unused ones are unmarked at the round end). A draw
 // fails after MAX_RANDOM_QUERY_TIME rejected tries: *exh_at = tries count then.
 __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, const Pool& P, int16_t* vis,
-                          const Cands& C, int nc, int* exh_at, int* first, const uint32_t (&coef)[31]) {
+                          const Cands& C, int nc, int* exh_at, const uint32_t (&coef)[31]) {
     const int lane = threadIdx.x;
     const uint32_t o = rng_word(s, coef);
     const int j = (int)((o >> 1) % (uint32_t)N);
     const int sl = pool_select(P, j);
-    // an earlier try of this batch that drew the same column wins: the lowest
-    // lane per slot, through LDS marks reset right after
-    atomicMin(&first[sl], lane);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const bool acc = vis[sl] < round && first[sl] == lane;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    first[sl] = AW;
+    // an earlier try of this batch that drew the same column wins
+    const bool acc = vis[sl] < round && !dup_of_lower_lane(sl);
     const unsigned long long m = __ballot(acc);
     const int a0 = m ? __ffsll((long long)m) - 1 : 64;
     int got = 0;
@@ -561,19 +562,47 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
     return got;
 }
 
+// One-point state of every pool slot (the k_onepoint_pre result, refreshed
+// when a claim hits one of its holders): keypoint it would claim (-1: none),
+// distance, first- and second-place holders.
+struct SlotMatch {
+    int16_t* match;
+    int16_t* dist;
+    int16_t* h1;
+    int16_t* h2;
+};
+
+// The slot's one-point result under the current claims: rescanned (and
+// stored back) when a keypoint holding first or second place was claimed
+// since it was computed.
+__device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst& fc, int f, const SlotMatch& SM,
+                                          int sl, int q, const int* cell_start, const int* items, const int* claim,
+                                          const gf_keypoint* K, const uint8_t* D, int& md) {
+    int mi = SM.match[sl];
+    md = SM.dist[sl];
+    const int h1 = SM.h1[sl], h2 = SM.h2[sl];
+    if ((h1 >= 0 && claim[h1] >= 0) || (h2 >= 0 && claim[h2] >= 0)) {
+        int n1, n2;
+        one_point_scan(A, fc, f, q, cell_start, items, claim, KpGlobal{K, D}, mi, md, n1, n2);
+        if (mi < 0) md = 0;
+        SM.match[sl] = (int16_t)mi;
+        SM.dist[sl] = (int16_t)md;
+        SM.h1[sl] = (int16_t)n1;
+        SM.h2[sl] = (int16_t)n2;
+    }
+    return mi;
+}
+
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
-                           const int16_t* lmk, const double* cur, const double* info, const int* cell_start,
-                           const int* items, const int* claim, const gf_keypoint* K, const uint8_t* D) {
+                           const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
+                           const int* cell_start, const int* items, const int* claim, const gf_keypoint* K,
+                           const uint8_t* D) {
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
-        const int q = lmk[C.slot[c]];
-        const OnePre p = A.pre[(long long)f * A.mp_cap + q];  // in flight during the log-det
+        const int sl = C.slot[c];
+        const int q = lmk[sl];
         C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
-        int mi = p.idx, md = p.dist;
-        if ((p.holder1 >= 0 && claim[p.holder1] >= 0) || (p.holder2 >= 0 && claim[p.holder2] >= 0)) {
-            int h1, h2;  // a holder was claimed this frame: scan again
-            one_point_scan(A, fc, f, q, cell_start, items, claim, KpGlobal{K, D}, mi, md, h1, h2);
-            if (mi < 0) md = 0;
-        }
+        int md;
+        const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
         C.dist[c] = (int16_t)md;
         C.alive[c] = 0;
@@ -581,37 +610,102 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
     __syncthreads();
 }
 
+// A round in which no pool entry can be matched any more: every draw fails
+// its one-point match, so the heap order no longer matters and the round
+// (and runActiveMapMatching) ends when MAX_RANDOM_QUERY_TIME draws in a row
+// hit visited columns (Observability.cc:1347-1359, 1437-1440). Only the
+// accepted draws (one logDet each) and the rand() calls are observable; both
+// follow from the column sequence alone, so this replays the draws on a
+// column bitmask without evaluating anything. sd/tries/run continue the
+// round's draw state; on return sd is the rand() state after exactly
+// exh_at calls from the round start.
+__device__ void exhaust_draws(uint32_t& sd, int tries, int run, int N, unsigned long long* colvis, int& nacc,
+                              int& exh_at, const uint32_t (&coef)[31]) {
+    while (true) {
+        const uint32_t o = rng_word(sd, coef);
+        const int j = (int)((o >> 1) % (uint32_t)N);
+        const bool acc = !((colvis[j >> 6] >> (j & 63)) & 1ull) && !dup_of_lower_lane(j);
+        const unsigned long long m = __ballot(acc);
+        const int a0 = m ? __ffsll((long long)m) - 1 : 64;
+        if (run + a0 >= MAX_RANDOM_QUERY_TIME) {
+            const int k = MAX_RANDOM_QUERY_TIME - run;  // tries of this batch before the draw gives up
+            exh_at = tries + k;
+            sd = rng_advance(sd, o, k);
+            __syncthreads();
+            return;
+        }
+        if (acc) atomicOr(&colvis[j >> 6], 1ull << (j & 63));
+        nacc += __popcll(m);
+        run = m ? __clzll((long long)m) : run + 64;
+        sd = rng_advance(sd, o, 64);
+        tries += 64;
+        __syncthreads();
+    }
+}
+
+// Sort the wave's (score, candidate) pairs by score, descending; lanes with
+// candidate < 0 sort last. Bitonic over 64 lanes.
+__device__ __forceinline__ void wave_sort_desc(double& hs, int& hc) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const double os = __shfl_xor(hs, j, 64);
+            const int oc = __shfl_xor(hc, j, 64);
+            // "other before mine" in descending order
+            const bool ogt = oc >= 0 && (hc < 0 || os > hs);
+            const bool olt = hc >= 0 && (oc < 0 || os < hs);
+            const bool keep_first = ((lane & j) == 0) == ((lane & k) == 0);
+            if (keep_first ? ogt : olt) {
+                hs = os;
+                hc = oc;
+            }
+        }
+    }
+}
+
 // Heap top of the live candidates: the arg-max, unless the maximum is tied
 // or a score is NaN, when std::priority_queue's order is reproduced by
 // replaying its push/pop history (sz pushes, then pop/push pairs) exactly.
-__device__ int wave_top(const Cands& C, int ncand, int sz, int npop, int16_t* rheap, int* s_res) {
+// The live candidates are the al[0 .. na) list (na = sz: every pop is
+// followed by its replacement, which takes the popped entry's place), so a
+// top costs one pass over at most sz entries, not over every draw so far.
+// *pos = the top's place in al.
+__device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int npop, int16_t* rheap, int* s_res,
+                        int* pos) {
     const int lane = threadIdx.x;
     double best = -INFINITY;
     int bi = -1, nan = 0;
-    for (int c = lane; c < ncand; c += AW) {
-        if (!C.alive[c]) continue;
-        const double sc = C.score[c];
+    for (int i = lane; i < na; i += AW) {
+        const double sc = C.score[al[i]];
         if (sc != sc) {
             nan = 1;
         } else if (bi < 0 || sc > best) {
             best = sc;
-            bi = c;
+            bi = i;
         }
     }
     double gb = best;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) gb = fmax(gb, __shfl_xor(gb, o, 64));
-    int cnt = 0;
-    for (int c = lane; c < ncand; c += AW) cnt += C.alive[c] && C.score[c] == gb;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        cnt += __shfl_xor(cnt, o, 64);
-        nan |= __shfl_xor(nan, o, 64);
+    int cnt;
+    if (na <= AW) {
+        cnt = __popcll(__ballot(bi >= 0 && best == gb));
+    } else {
+        int c2 = 0;
+        for (int i = lane; i < na; i += AW) c2 += C.score[al[i]] == gb;
+        cnt = gfd::warp_sum(c2);
     }
-    if (!nan && cnt == 1) {
+    if (__ballot(nan) == 0ull && cnt == 1) {
         const unsigned long long m = __ballot(bi >= 0 && best == gb);
-        return __shfl(bi, __ffsll((long long)m) - 1, 64);
+        const int p = __shfl(bi, __ffsll((long long)m) - 1, 64);
+        *pos = p;
+        return al[p];
     }
+#ifdef GF_AM_STAMP
+    if (lane == 0) atomicAdd(&g_am_stamp[7], 1ull);  // heap replays (tied or NaN maximum)
+#endif
     if (lane == 0) {
         int hn = 0;
         const IdxLess cmp{C.score};
@@ -628,7 +722,14 @@ __device__ int wave_top(const Cands& C, int ncand, int sz, int npop, int16_t* rh
         *s_res = rheap[0];
     }
     __syncthreads();
-    return *s_res;
+    const int t = *s_res;
+    int p = -1;
+    for (int i0 = 0; i0 < na && p < 0; i0 += AW) {
+        const unsigned long long m = __ballot(i0 + lane < na && al[i0 + lane] == t);
+        if (m) p = i0 + __ffsll((long long)m) - 1;
+    }
+    *pos = p;
+    return t;
 }
 
 #ifdef GF_AM_STAMP  // diagnostic build only: shader cycles per phase, summed over frames
@@ -652,8 +753,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     const int PC = A.pool_cap;
     double* c_score = (double*)smem;                                       // PC
     unsigned long long* pbits = (unsigned long long*)(c_score + PC);       // 64
-    int* first = (int*)(pbits + 64);                                       // PC: draw-batch duplicate marks
-    int* claim = first + PC;                                               // kp_cap
+    int* claim = (int*)(pbits + 64);                                       // kp_cap
     int* ppre = claim + A.kp_cap;                                          // 65 (+3 pad)
     int32_t* c_tries = ppre + 68;                                          // PC
     int16_t* lmk = (int16_t*)(c_tries + PC);                               // PC: map point of each slot
@@ -662,9 +762,15 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     int16_t* c_match = c_slot + PC;                                        // PC
     int16_t* c_dist = c_match + PC;                                        // PC
     int16_t* rheap = c_dist + PC;                                          // PC: replay heap
-    uint8_t* c_alive = (uint8_t*)(rheap + PC);                             // PC
+    int16_t* sm_match = rheap + PC;                                        // PC: one-point state per slot
+    int16_t* sm_dist = sm_match + PC;                                      // PC
+    int16_t* sm_h1 = sm_dist + PC;                                         // PC
+    int16_t* sm_h2 = sm_h1 + PC;                                           // PC
+    int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
+    uint8_t* c_alive = (uint8_t*)(alv + PC);                               // PC
     __shared__ double cur[49];
-    __shared__ int s_res, s_exh;
+    __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
+    __shared__ int s_res, s_exh, s_nsucc;
 
     const int f = blockIdx.x, lane = threadIdx.x;
     const FrameConst& fc = A.fc;
@@ -687,7 +793,6 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
     for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
-    for (int i = lane; i < PC; i += AW) first[i] = AW;
     uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
 #pragma unroll
     for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
@@ -737,6 +842,20 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         __syncthreads();
         pool_prefix(P);
     }
+    const SlotMatch SM{sm_match, sm_dist, sm_h1, sm_h2};
+    {  // one-point state of every slot from the precompute; matchable slots counted
+        int ns = 0;
+        for (int sl = lane; sl < N; sl += AW) {
+            const OnePre p = A.pre[(long long)f * A.mp_cap + lmk[sl]];
+            sm_match[sl] = p.idx;
+            sm_dist[sl] = p.dist;
+            sm_h1[sl] = p.holder1;
+            sm_h2[sl] = p.holder2;
+            ns += p.idx >= 0;
+        }
+        ns = gfd::warp_sum(ns);
+        if (lane == 0) s_nsucc = ns;
+    }
     if (lane < 49) cur[lane] = A.base[49LL * f + lane];
     uint32_t rs;  // RNG history (oldest first) at the last committed rand() call
     {
@@ -749,6 +868,9 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
 
     const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
     const int S = (int)((float)N / (float)num_to_match * 1.0);
+    const int nw0 = (N + 63) >> 6;  // pool words (slots never move; only bits clear)
+    bool nsucc_valid = true;        // s_nsucc counts the matchable pool slots
+    int last_npop = 0;
     const double* info = A.info + (long long)f * A.mp_cap * 49;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
 
@@ -758,10 +880,39 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         // -- draws, ahead of need
         uint32_t sd = rs;
         int tries = 0, run = 0, nc = 0, evald = 0, exh_at = -1;
+        if (!nsucc_valid && last_npop > sz) {
+            // the last round had to pop: count the pool entries that can still be
+            // matched (slots whose holders were claimed are scanned again)
+            int ns = 0;
+            for (int w = 0; w < nw0; w++) {
+                const int sl = w * 64 + lane;
+                int mi = -1;
+                if ((pbits[w] >> lane) & 1ull) {
+                    int md;
+                    mi = slot_match(A, fc, f, SM, sl, lmk[sl], cell_start, items, claim, K, D, md);
+                }
+                ns += mi >= 0;
+            }
+            ns = gfd::warp_sum(ns);
+            if (lane == 0) s_nsucc = ns;
+            nsucc_valid = true;
+            __syncthreads();
+        }
+        if (nsucc_valid && s_nsucc == 0) {  // nothing left to match: the round draws until the draws give out
+            colvis[lane] = 0ull;
+            __syncthreads();
+            int nacc = 0, ex = 0;
+            exhaust_draws(sd, 0, 0, N, colvis, nacc, ex, rcoef);
+            nld += nacc;
+            used += ex;
+            rs = sd;
+            AM_T(2);
+            break;
+        }
         while (nc < sz && exh_at < 0) {
             if (lane == 0) s_exh = -1;
             __syncthreads();
-            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, first, rcoef);
+            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
             exh_at = s_exh;
         }
         AM_T(2);
@@ -772,16 +923,42 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, cur, info, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
         evald = nc;
-        for (int c = lane; c < sz; c += AW) C.alive[c] = 1;
+        for (int c = lane; c < sz; c += AW) {
+            C.alive[c] = 1;
+            alv[c] = (int16_t)c;
+        }
         __syncthreads();
         AM_T(3);
-        // -- the sequential heap loop, now over known scores and match results
-        int npop = 0, top = -1;
+        // -- the sequential heap loop, now over known scores and match results.
+        // While the live set fits the wave and no two live scores tie (NaN
+        // counts as a tie), it is kept sorted in registers, lane 0 = heap top:
+        // a pop is a one-lane shift and a rank by ballot. Otherwise (or from
+        // the first tie on) wave_top, with the exact heap replay for ties.
+        int npop = 0, top = -1, tpos = -1;
         bool exh = false, success = false;
+        bool sorted = sz <= AW;
+        double hs = -INFINITY;
+        int hc = -1;
+        if (sorted) {
+            if (lane < sz) {
+                hc = lane;
+                hs = C.score[lane];
+            }
+            if (__ballot(lane < sz && hs != hs)) {
+                sorted = false;
+            } else {
+                wave_sort_desc(hs, hc);
+                const double nx = __shfl(hs, min(lane + 1, AW - 1), 64);
+                if (__ballot(lane + 1 < sz && nx == hs)) sorted = false;
+            }
+        }
         while (true) {
-            top = wave_top(C, sz + npop, sz, npop, rheap, &s_res);
+            if (sorted)
+                top = __shfl(hc, 0, 64);
+            else
+                top = wave_top(C, alv, sz, sz, npop, rheap, &s_res, &tpos);
             if (C.match[top] >= 0) {
                 success = true;
                 break;
@@ -791,7 +968,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             while (rep >= nc && exh_at < 0) {
                 if (lane == 0) s_exh = -1;
                 __syncthreads();
-                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, first, rcoef);
+                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
                 exh_at = s_exh;
             }
             if (rep >= nc) {
@@ -799,8 +976,31 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                 break;
             }
             if (rep >= evald) {
-                eval_cands(A, fc, f, C, evald, nc, lmk, cur, info, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
                 evald = nc;
+            }
+            if (sorted) {
+                const double x = C.score[rep];
+                const bool live = lane >= 1 && lane < sz;  // lane 0 was the popped top
+                if (x != x || __ballot(live && hs == x)) {
+                    // a tie: hand the live set (lanes 1.., then the replacement) to wave_top
+                    if (live) alv[lane - 1] = (int16_t)hc;
+                    if (lane == 0) alv[sz - 1] = (int16_t)rep;
+                    sorted = false;
+                } else {
+                    const int r = __popcll(__ballot(live && hs > x));  // the replacement's place
+                    const double hs1 = __shfl(hs, min(lane + 1, AW - 1), 64);
+                    const int hc1 = __shfl(hc, min(lane + 1, AW - 1), 64);
+                    if (lane < r) {
+                        hs = hs1;
+                        hc = hc1;
+                    } else if (lane == r) {
+                        hs = x;
+                        hc = rep;
+                    }
+                }
+            } else if (lane == 0) {
+                alv[tpos] = (int16_t)rep;  // the replacement takes the popped entry's place
             }
             if (lane == 0) C.alive[rep] = 1;
             npop++;
@@ -853,6 +1053,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         __syncthreads();
         pool_prefix(P);
         N -= nrem;
+        nsucc_valid = false;  // a claim and removed columns: recounted when it may pay off
+        last_npop = npop;
         __syncthreads();
         AM_T(6);
     }
@@ -882,8 +1084,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
 #undef AM_T
 
 size_t active_lds_bytes(int pool_cap, int kp_cap) {
-    return sizeof(double) * pool_cap + 8 * 64 + sizeof(int) * ((size_t)pool_cap + kp_cap + 68) +
-           sizeof(int32_t) * pool_cap + sizeof(int16_t) * 6 * (size_t)pool_cap + pool_cap;
+    return sizeof(double) * pool_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) +
+           sizeof(int32_t) * pool_cap + sizeof(int16_t) * 11 * (size_t)pool_cap + pool_cap;
 }
 
 // ------------------------------------------------------------- max-volume selection

@@ -30,6 +30,8 @@ constexpr int RM_MAXKF = 8192;
 
 struct RefArgs {
     gf_covis_map m;
+    const gf_covis_map* maps;  // per-frame maps (device array), else m for every frame
+    int first_stride;          // map points per frame in `first`
     int32_t* frame_mps;
     const int32_t* nkps;
     int stride;
@@ -74,7 +76,7 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     __shared__ unsigned long long s_best;
     __shared__ int s_nl;
     const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const gf_covis_map& M = A.m;
+    const gf_covis_map M = A.maps ? A.maps[f] : A.m;
     const int nkf = M.nkf;
     int32_t* fm = A.frame_mps + (size_t)f * A.stride;
     const int nkp = min(max(A.nkps[f], 0), A.stride);
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     }
     if (tid == 0) cnt[nl] = total;
     __syncthreads();
-    int32_t* first = A.first + (size_t)f * M.nmp;
+    int32_t* first = A.first + (size_t)f * A.first_stride;
     auto slot_mp = [&](int q) -> int {  // map point of sequence position q
         int lo = 0, hi = nl - 1;        // last p with cnt[p] <= q
         while (lo < hi) {
@@ -236,12 +238,48 @@ int gf_update_reference_dev(gf_ctx* ctx, const gf_covis_map* d_map, int nframes,
     A.mp_cap = mp_cap;
     A.ref_kf = d_ref_kf;
     A.first = (int32_t*)first;
+    A.first_stride = m.nmp;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_update_reference");
     k_update_reference<<<nframes, RM_T, 0, s>>>(A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
+
+}  // extern "C"
+
+namespace gf {
+// UpdateReference for B frames each against its own map: d_maps is a device
+// array of B gf_covis_map whose arrays are device pointers, every map with at
+// most nmp_cap points and RM_MAXKF keyframes (the front end's per-stream
+// keyframe graphs); d_first is scratch of B * nmp_cap ints.
+int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap, int nframes, int32_t* d_frame_mps,
+                            const int32_t* d_nkps, int stride, int32_t* d_local_kfs, int32_t* d_n_local_kfs,
+                            int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap, int32_t* d_ref_kf,
+                            int32_t* d_first, hipStream_t s) {
+    if (nframes <= 0) return GF_OK;
+    RefArgs A{};
+    A.maps = d_maps;
+    A.first_stride = nmp_cap;
+    A.frame_mps = d_frame_mps;
+    A.nkps = d_nkps;
+    A.stride = stride;
+    A.local_kfs = d_local_kfs;
+    A.n_local_kfs = d_n_local_kfs;
+    A.kf_cap = kf_cap;
+    A.local_mps = d_local_mps;
+    A.n_local_mps = d_n_local_mps;
+    A.mp_cap = mp_cap;
+    A.ref_kf = d_ref_kf;
+    A.first = d_first;
+    GF_PROF(ctx, s, "k_update_reference");
+    k_update_reference<<<nframes, RM_T, 0, s>>>(A);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+}  // namespace gf
+
+extern "C" {
 
 int gf_update_reference(gf_ctx* ctx, const gf_covis_map* map, int32_t* frame_mps, int nkp, int32_t* local_kfs,
                         int* n_local_kfs, int kf_cap, int32_t* local_mps, int* n_local_mps, int mp_cap,

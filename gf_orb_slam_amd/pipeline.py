@@ -65,7 +65,7 @@ FIELDS = {
     "hist": (31, np.int32, (8,)),  # running counters: steps per branch [0..5], log-dets [6], local matches [7]
 }
 STATS = ["m3", "found", "to_match", "branch", "in_view", "local", "inl1", "inl2", "extra", "nleft", "iter1",
-         "iter2", "edges1", "edges2", "flags", "frames", "ldets"]
+         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal"]
 NSTAT = len(STATS)
 
 
@@ -170,6 +170,16 @@ class FrontEnd:
         mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
         desc = np.ascontiguousarray(desc, np.uint8)
         check(lib().gf_frontend_set_map(self.handle, stream, ptr(mps), ptr(desc), len(mps)))
+
+    def set_covis(self, stream: int, graph) -> None:
+        """gf_frontend_set_covis: the keyframe graph of the stream's map
+        (localmap.CovisGraph or the dict scene.build_global_map returns)."""
+        from .localmap import CovisGraph
+
+        g = graph if isinstance(graph, CovisGraph) else CovisGraph(**graph)
+        self._graphs = getattr(self, "_graphs", {})
+        self._graphs[stream] = g
+        check(lib().gf_frontend_set_covis(self.handle, stream, ctypes.byref(g.struct())))
 
     def set_rng(self, stream: int, seed: int) -> None:
         check(lib().gf_frontend_set_rng(self.handle, stream, ctypes.c_uint32(seed)))

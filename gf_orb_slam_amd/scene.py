@@ -236,6 +236,117 @@ def build_map(scene: Scene, cam, extract, period: int, traj_seed: int, n_map: in
     return mp, D
 
 
+def keyframe_pose(k: int, n_kf: int, period: int, traj_seed: int, sweep: float) -> np.ndarray:
+    """Keyframe k of a mapping sweep: the loop's position at phase k period /
+    n_kf, turned about the vertical axis by a yaw spread evenly over
+    [-sweep, +sweep] rad (the mapping pass looked around the room; the
+    tracked loop looks ahead)."""
+    T = trajectory_pose(k * period / n_kf, period, traj_seed).astype(np.float64)
+    yaw = -sweep + 2 * sweep * k / max(n_kf - 1, 1)
+    Rwc = T[:3, :3].T @ _rot("y", yaw)
+    C = -T[:3, :3].T @ T[:3, 3]
+    out = np.eye(4)
+    out[:3, :3] = Rwc.T
+    out[:3, 3] = -Rwc.T @ C
+    return out.astype(np.float32)
+
+
+def build_global_map(scene: Scene, cam, extract, period: int, traj_seed: int, g_cap: int, seed: int, n_kf: int = 24,
+                     nlevels: int = 8, scale: float = 1.2, device="cpu", stale_desc: float = 0.0,
+                     min_shared: int = 15, sweep: float = 2.4) -> dict:
+    """A keyframe map for Tracking::UpdateReference: n_kf keyframes of a
+    mapping sweep (keyframe_pose), every keypoint back-projected onto the
+    scene; a
+    keypoint whose 3-D point falls within 2 cm of an existing map point becomes
+    an observation of it (one slot per keyframe and point), else a new point
+    (its keyframe's descriptor, normal and UpdateNormalAndDepth distances, as
+    build_map). At most g_cap points are kept (a seeded subset, in a seeded
+    order: the map's point indices); slots of dropped points are NULL.
+    Keyframes are in creation order (= ascending KeyFrame*); each keyframe's
+    covisible keyframes sharing >= min_shared points, by weight descending
+    (ties: later keyframe first), are mvpOrderedConnectedKeyFrames
+    (KeyFrame::UpdateConnections, KeyFrame.cc). stale_desc as build_map.
+    Returns dict(mp, desc, graph=localmap.CovisGraph arrays, kf_Tcw)."""
+    from .matcher import MAP_POINT_DTYPE
+
+    sf = [np.float32(1.0)]
+    for _ in range(1, nlevels):
+        sf.append(np.float32(sf[-1] * np.float32(scale)))
+    sf = np.array(sf, np.float32)
+    poses = [keyframe_pose(k, n_kf, period, traj_seed, sweep) for k in range(n_kf)]
+    imgs = scene.render(poses, cam, device).cpu().numpy()
+    key_to_pt = {}
+    X_l, D_l, N_l, dmin_l, dmax_l = [], [], [], [], []
+    slots = []  # per keyframe: point id per keypoint slot (-1 = NULL)
+    for T, img in zip(poses, imgs):
+        k, d = extract(img)
+        X, ok = scene.backproject(T, k["x"].astype(np.float64), k["y"].astype(np.float64), cam)
+        C = -T[:3, :3].astype(np.float64).T @ T[:3, 3].astype(np.float64)
+        sl = np.full(len(k), -1, np.int64)
+        seen = set()
+        for i in np.nonzero(ok)[0]:
+            key = tuple(np.floor(X[i] / 0.02).astype(np.int64))
+            pid = key_to_pt.get(key)
+            if pid is None:
+                pid = len(X_l)
+                key_to_pt[key] = pid
+                PC = (X[i] - C).astype(np.float32)
+                dist = np.float32(np.sqrt((PC.astype(np.float64) ** 2).sum()))
+                X_l.append(X[i])
+                D_l.append(d[i])
+                N_l.append(PC / dist)
+                oc = int(k["octave"][i])
+                dmin_l.append((np.float32(1.0) / np.float32(scale)) * dist / sf[oc])
+                dmax_l.append(np.float32(scale) * dist * sf[nlevels - 1 - oc])
+            if pid in seen:
+                continue  # one slot per keyframe and point
+            seen.add(pid)
+            sl[i] = pid
+        slots.append(sl)
+    npt = len(X_l)
+    rng = np.random.default_rng(seed)
+    keep = rng.permutation(npt)[:g_cap]  # kept points, in their new index order
+    newid = np.full(npt, -1, np.int64)
+    newid[keep] = np.arange(len(keep))
+    G = len(keep)
+    mp = np.zeros(G, MAP_POINT_DTYPE)
+    mp["pos"] = np.array(X_l)[keep]
+    mp["normal"] = np.array(N_l)[keep]
+    mp["min_dist"] = np.array(dmin_l, np.float32)[keep]
+    mp["max_dist"] = np.array(dmax_l, np.float32)[keep]
+    desc = np.ascontiguousarray(np.array(D_l, np.uint8)[keep])
+    if stale_desc > 0:
+        srng = np.random.default_rng(seed + 0x5747)
+        sel = srng.permutation(G)[:int(round(stale_desc * G))]
+        desc[sel] = srng.integers(0, 256, (len(sel), 32), dtype=np.uint8)
+    kf_mp = [np.where(sl >= 0, newid[np.maximum(sl, 0)], -1).astype(np.int32) for sl in slots]
+    kf_mp_off = np.zeros(n_kf + 1, np.int32)
+    kf_mp_off[1:] = np.cumsum([len(x) for x in kf_mp])
+    obs = [[] for _ in range(G)]
+    for kf, x in enumerate(kf_mp):
+        for m in x[x >= 0]:
+            obs[m].append(kf)
+    mp_obs_off = np.zeros(G + 1, np.int32)
+    mp_obs_off[1:] = np.cumsum([len(o) for o in obs])
+    shared = np.zeros((n_kf, n_kf), np.int64)
+    for o in obs:
+        for a in o:
+            for b in o:
+                if a != b:
+                    shared[a, b] += 1
+    cov = []
+    for a in range(n_kf):
+        nb = [b for b in range(n_kf) if b != a and shared[a, b] >= min_shared]
+        cov.append(sorted(nb, key=lambda b: (-shared[a, b], -b)))
+    kf_cov_off = np.zeros(n_kf + 1, np.int32)
+    kf_cov_off[1:] = np.cumsum([len(c) for c in cov])
+    graph = dict(kf_bad=np.zeros(n_kf, np.uint8), kf_mp_off=kf_mp_off, kf_mp=np.concatenate(kf_mp),
+                 kf_cov_off=kf_cov_off, kf_cov=np.array([b for c in cov for b in c], np.int32),
+                 mp_bad=np.zeros(G, np.uint8), mp_obs_off=mp_obs_off,
+                 mp_obs=np.array([k for o in obs for k in o], np.int32))
+    return dict(mp=mp, desc=desc, graph=graph, kf_Tcw=np.stack(poses))
+
+
 class Workload:
     """B streams over n_scenes rendered loops (see module docstring)."""
 
@@ -270,6 +381,13 @@ class Workload:
         T = np.stack([self.gt_pose(b, 0).reshape(16) for b in range(self.B)])
         V = np.stack([velocity(self.gt_pose(b, -1), self.gt_pose(b, 0)).reshape(16) for b in range(self.B)])
         return np.ascontiguousarray(T, np.float32), np.ascontiguousarray(V, np.float32)
+
+    def build_global_maps(self, extract, g_cap: int, n_kf: int = 24, device="cpu", sweep: float = 2.4):
+        """Per scene: build_global_map (keyframes, covisibility, points) for
+        local maps assembled per frame by UpdateReference."""
+        return [build_global_map(sc, self.cam, extract, self.period, self.traj_seed[s], g_cap, self.seed * 7919 + s,
+                                 n_kf=n_kf, device=device, stale_desc=self.stale_desc, sweep=sweep)
+                for s, sc in enumerate(self.scenes)]
 
     def build_maps(self, extract, n_map: int, device="cpu"):
         return [build_map(sc, self.cam, extract, self.period, self.traj_seed[s], n_map, self.seed * 7919 + s,

@@ -917,10 +917,12 @@ enum {
     GF_ST_NLEFT,        /* mLeftMapPoints size                              */
     GF_ST_ITER1, GF_ST_ITER2, GF_ST_EDGES1, GF_ST_EDGES2,
     GF_ST_FLAGS,        /* 1: M3 < 20 (TrackPreviousFrame fall-back), 2: < 10 after PoseOptimization,
-                           4: mnMatchesInliers < 15 (LOST), 8: a time budget cut a loop */
+                           4: mnMatchesInliers < 15 (LOST), 8: a time budget cut a loop,
+                           16: the cut fell on SearchAdditionalMatchesInFrame (no time left) */
     GF_ST_FRAMES,       /* frames tracked                                   */
     GF_ST_LDETS,        /* logDet evaluations of runActiveMapMatching (heap
                            pushes, Observability.cc:1373): SURVEY §8d E_ld  */
+    GF_ST_NLOCAL,       /* mvpLocalMapPoints size (keyframe graphs only)    */
     GF_FE_NSTAT
 };
 int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);
@@ -936,6 +938,17 @@ int gf_frontend_set_source(gf_frontend* fe, const uint8_t* const* d_bases, const
  * mvpLocalMapPoints order. Resets that stream's observability state. */
 int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, const uint8_t* desc, int m);
 int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed);
+/* The keyframe graph of one stream's map (host arrays, gf_covis_map over the
+ * map set with gf_frontend_set_map: g->nmp must equal its size; at most 64
+ * keyframes, 64 x keypoint-capacity slots and observations). Once any stream
+ * has a graph, every step first runs Tracking::UpdateReference
+ * (Tracking.cc:2745, 3689-3852) on the frame's matches after
+ * TrackWithMotionModel and tracks the rest of the frame against the local map
+ * it returns (local keyframes' points, mvpLocalMapPoints order), so the local
+ * map follows the camera; every stream then needs a graph. The map fields
+ * (GF_FE_MAP, VIEWS, MP_*) keep indexing the stream's map, and GF_FE_LEFT /
+ * GF_FE_KP2MP map indices. The bootstrap matches the whole map. */
+int gf_frontend_set_covis(gf_frontend* fe, int stream, const gf_covis_map* graph);
 /* Start of tracking: the current source frame of every stream is taken at the
  * given pose (Tcw [B][16]) and matched to its local map
  * (isInFrustum + SearchByProjection(F, local, 1) with nnratio 0.8); it becomes

@@ -48,6 +48,8 @@ int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, co
                              const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
                              int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
 long long orc_last_ldets(void);
+int orc_update_reference(const gf_covis_map* M, int32_t* frame_mps, int nkp, int32_t* local_kfs, int* n_local_kfs,
+                         int kf_cap, int32_t* local_mps, int* n_local_mps, int mp_cap, int32_t* ref_kf);
 }
 
 namespace {
@@ -115,7 +117,39 @@ struct orc_chain {
     gf_rng rng{};
     int32_t stats[GF_FE_NSTAT] = {};
     double tm[8] = {};  // stage seconds of the last step
+    // time-budget cuts the next steps take (orc_chain_set_cuts): the device
+    // decides them on its clock and reports them in GF_ST_BRANCH / GF_ST_FLAGS
+    int cut_frustum = 0, cut_select = 0;
+    // keyframe graph (orc_chain_set_covis): UpdateReference every step, the
+    // frame tracked against the local map gathered from the stream map
+    int refmap = 0, g_nkf = 0;
+    std::vector<uint8_t> g_kf_bad, g_mp_bad;
+    std::vector<int32_t> g_kf_mp_off, g_kf_mp, g_kf_cov_off, g_kf_cov, g_mp_obs_off, g_mp_obs;
 };
+
+namespace {
+// The map-point arrays of a chain: the stream map, or a step's local map.
+struct MapState {
+    std::vector<gf_map_point> map;
+    std::vector<uint8_t> desc;
+    std::vector<gf_mp_view> views;
+    std::vector<double> H, info;
+    std::vector<float> uv;
+    std::vector<int32_t> upd;
+    int32_t nmp = 0;
+};
+
+void take_map(orc_chain* c, MapState& s) {
+    s.map.swap(c->map);
+    s.desc.swap(c->map_desc);
+    s.views.swap(c->views);
+    s.H.swap(c->mp_H);
+    s.info.swap(c->mp_info);
+    s.uv.swap(c->mp_uv);
+    s.upd.swap(c->upd);
+    std::swap(s.nmp, c->nmp);
+}
+}  // namespace
 
 namespace {
 
@@ -387,6 +421,34 @@ int orc_chain_bootstrap(orc_chain* c, const uint8_t* img, const float* Tcw, cons
     return GF_OK;
 }
 
+// The budget cuts of the following steps: cut_frustum = the isInFrustum cap
+// fired on the first local point (Tracking.cc:3262-3270, GF_ST_BRANCH 5),
+// cut_select = no time left for SearchAdditionalMatchesInFrame
+// (ORBmatcher.cc:281-282, GF_ST_FLAGS bit 16).
+int orc_chain_set_cuts(orc_chain* c, int cut_frustum, int cut_select) {
+    c->cut_frustum = cut_frustum;
+    c->cut_select = cut_select;
+    return GF_OK;
+}
+
+// The keyframe graph over the chain's map (gf_frontend_set_covis).
+int orc_chain_set_covis(orc_chain* c, const gf_covis_map* g) {
+    if (!g || g->nmp != c->nmp || g->nkf < 0) return GF_ERR_ARG;
+    const int nkf = g->nkf, nmp = g->nmp;
+    const size_t ns = nkf ? g->kf_mp_off[nkf] : 0, nc = nkf ? g->kf_cov_off[nkf] : 0, no = nmp ? g->mp_obs_off[nmp] : 0;
+    c->g_nkf = nkf;
+    c->g_kf_bad.assign(g->kf_bad, g->kf_bad + nkf);
+    c->g_kf_mp_off.assign(g->kf_mp_off, g->kf_mp_off + (nkf ? nkf + 1 : 0));
+    c->g_kf_mp.assign(g->kf_mp, g->kf_mp + ns);
+    c->g_kf_cov_off.assign(g->kf_cov_off, g->kf_cov_off + (nkf ? nkf + 1 : 0));
+    c->g_kf_cov.assign(g->kf_cov, g->kf_cov + nc);
+    c->g_mp_bad.assign(g->mp_bad, g->mp_bad + nmp);
+    c->g_mp_obs_off.assign(g->mp_obs_off, g->mp_obs_off + (nmp ? nmp + 1 : 0));
+    c->g_mp_obs.assign(g->mp_obs, g->mp_obs + no);
+    c->refmap = 1;
+    return GF_OK;
+}
+
 int orc_chain_timings(orc_chain* c, double* out) {
     std::memcpy(out, c->tm, sizeof(c->tm));
     return GF_OK;
@@ -433,6 +495,51 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     st[GF_ST_FOUND] = found;
     const int ntm = c->p.gf_budget - found;
     st[GF_ST_TO_MATCH] = ntm;
+    // TrackLocalMap -> UpdateReference (Tracking.cc:2745, 3689-3852), then the
+    // local map in mvpLocalMapPoints order replaces the map for the rest of
+    // the frame (matches as local indices)
+    MapState G;
+    std::vector<int32_t> lmp;
+    if (c->refmap) {
+        gf_covis_map g{c->g_nkf, c->nmp, c->g_kf_bad.data(), c->g_kf_mp_off.data(), c->g_kf_mp.data(),
+                       c->g_kf_cov_off.data(), c->g_kf_cov.data(), c->g_mp_bad.data(), c->g_mp_obs_off.data(),
+                       c->g_mp_obs.data()};
+        std::vector<int32_t> lk(64);
+        lmp.assign(c->M, 0);
+        int nk = 0, nl = 0, ref = -1;
+        orc_update_reference(&g, c->kp2mp.data(), n, lk.data(), &nk, 64, lmp.data(), &nl, c->M, &ref);
+        nl = std::min(nl, c->M);
+        lmp.resize(nl);
+        take_map(c, G);  // c's arrays are now empty; rebuild them as the local map
+        const size_t M = c->M;
+        c->map.assign(M, gf_map_point{});
+        c->map_desc.assign(M * 32, 0);
+        c->views.assign(M, gf_mp_view{});
+        c->mp_H.assign(M * 14, 0.0);
+        c->mp_info.assign(M * 49, 0.0);
+        c->mp_uv.assign(M * 2, 0.f);
+        c->upd.assign(M, 0);
+        std::vector<int32_t> g2l(M, -1);
+        for (int k = 0; k < nl; k++) {
+            const int q = lmp[k];
+            c->map[k] = G.map[q];
+            std::memcpy(&c->map_desc[32 * (size_t)k], &G.desc[32 * (size_t)q], 32);
+            c->views[k] = G.views[q];
+            std::memcpy(&c->mp_H[14 * (size_t)k], &G.H[14 * (size_t)q], 14 * sizeof(double));
+            std::memcpy(&c->mp_info[49 * (size_t)k], &G.info[49 * (size_t)q], 49 * sizeof(double));
+            c->mp_uv[2 * k] = G.uv[2 * q];
+            c->mp_uv[2 * k + 1] = G.uv[2 * q + 1];
+            c->upd[k] = G.upd[q];
+            g2l[q] = k;
+        }
+        c->nmp = nl;
+        st[GF_ST_NLOCAL] = nl;
+        for (int i = 0; i < n; i++)
+            if (c->kp2mp[i] >= 0) {
+                c->kp2mp[i] = g2l[c->kp2mp[i]];
+                if (c->kp2mp[i] < 0) c->score[i] = 999;
+            }
+    }
     lap(1);
     // TrackLocalMap -> SearchReferencePointsInFrustum (Tracking.cc:3149-3410)
     const bool gf = c->p.gf != 0;
@@ -468,6 +575,13 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
             if (c->views[i].in_view) list.push_back(i);
         branch = 1;
         viz = true;
+    } else if (gf && c->cut_frustum) {
+        // isInFrustum time cap (:3262-3270) on the first point: mLeftMapPoints =
+        // the whole local map in order, mbNeedVizCheck, nToMatch = 0 (no search)
+        for (int i = 0; i < c->nmp; i++) list.push_back(i);
+        branch = 5;
+        viz = true;
+        st[GF_ST_FLAGS] |= 8;
     } else {
         int nv = 0;
         orc_frustum(&c->fi, c->Tcw, c->map.data(), c->nmp, 0.5f, c->views.data(), &nv);
@@ -519,16 +633,42 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
         std::memcpy(c->Xv_next, kin[1].Xv, sizeof(c->Xv_next));
         map_info(c, c->Xv_next, c->nmp, 1, 2, nullptr);
         lap(5);
-        // SearchAdditionalMatchesInFrame (:3097-3145)
-        if (viz) frustum_list(c, list.data(), nlist);
-        st[GF_ST_EXTRA] = project_list(c, list.data(), nlist, 0.8f);
+        // SearchAdditionalMatchesInFrame (:3097-3145); without time left
+        // SearchByProjection_Budget returns at once (ORBmatcher.cc:281-282)
+        if (c->cut_select) {
+            if (nlist) st[GF_ST_FLAGS] |= 8 | 16;
+        } else {
+            if (viz) {
+                frustum_list(c, list.data(), nlist);
+                // matched points are skipped by the visibility pass (mnLastFrameSeen, :3110-3111)
+                for (int i = 0; i < n; i++)
+                    if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
+            }
+            st[GF_ST_EXTRA] = project_list(c, list.data(), nlist, 0.8f);
+        }
+    }
+    if (c->refmap) {  // the local map's state back to the stream map, indices back to map indices
+        const int nl = (int)lmp.size();
+        for (int k = 0; k < nl; k++) {
+            const int q = lmp[k];
+            G.views[q] = c->views[k];
+            std::memcpy(&G.H[14 * (size_t)q], &c->mp_H[14 * (size_t)k], 14 * sizeof(double));
+            std::memcpy(&G.info[49 * (size_t)q], &c->mp_info[49 * (size_t)k], 49 * sizeof(double));
+            G.uv[2 * q] = c->mp_uv[2 * k];
+            G.uv[2 * q + 1] = c->mp_uv[2 * k + 1];
+            G.upd[q] = c->upd[k];
+        }
+        for (int i = 0; i < n; i++)
+            if (c->kp2mp[i] >= 0) c->kp2mp[i] = lmp[c->kp2mp[i]];
+        for (int j = 0; j < st[GF_ST_NLEFT]; j++) c->left[j] = lmp[c->left[j]];
+        take_map(c, G);  // the stream map back in place
     }
     // outliers NULL, mLastFrame = Frame(mCurrentFrame) (:899-907)
     for (int i = 0; i < n; i++)
         if (c->kp2mp[i] >= 0 && c->outl[i]) c->kp2mp[i] = -1;
     make_last(c);
     for (int i = 0; i < c->nmp; i++) c->upd[i] -= 1;
-    int fl = 0;
+    int fl = st[GF_ST_FLAGS];
     if (st[GF_ST_M3] < 20) fl |= 1;
     if (st[GF_ST_FOUND] < 10) fl |= 2;
     if (st[GF_ST_INL2] < 15) fl |= 4;

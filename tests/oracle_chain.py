@@ -31,6 +31,8 @@ def _orc():
         o.orc_chain_bootstrap.argtypes = [_P, _P, _P, _P, ctypes.c_double]
         o.orc_chain_step.argtypes = [_P, _P]
         o.orc_chain_timings.argtypes = [_P, _P]
+        o.orc_chain_set_cuts.argtypes = [_P, ctypes.c_int, ctypes.c_int]
+        o.orc_chain_set_covis.argtypes = [_P, _P]
         o._chain_declared = True
     return o
 
@@ -60,6 +62,12 @@ class Chain:
         desc = np.ascontiguousarray(desc, np.uint8)
         assert _orc().orc_chain_set_map(self.h, _p(mps), _p(desc), len(mps)) == 0
 
+    def set_covis(self, graph):
+        from gf_orb_slam_amd.localmap import CovisGraph
+
+        self._g = graph if isinstance(graph, CovisGraph) else CovisGraph(**graph)
+        assert _orc().orc_chain_set_covis(self.h, ctypes.byref(self._g.struct())) == 0
+
     def set_rng(self, seed: int):
         _orc().orc_chain_set_rng(self.h, ctypes.c_uint32(seed))
 
@@ -83,6 +91,10 @@ class Chain:
         fid, dt, shape = field_shape(name, 1, self.cap, self.M)
         a = np.ascontiguousarray(np.asarray(arr, dt).reshape(shape))
         assert _orc().orc_chain_write(self.h, fid, _p(a), a.nbytes) == 0, name
+
+    def set_cuts(self, frustum: bool, select: bool):
+        """Take the time-budget cuts the device took (GF_ST_BRANCH 5 / GF_ST_FLAGS bit 16)."""
+        assert _orc().orc_chain_set_cuts(self.h, int(frustum), int(select)) == 0
 
     def timings(self) -> np.ndarray:
         """Seconds of the last step's stages: extract, motion-model tracking,

@@ -133,6 +133,8 @@ def test_dropin_frontend_matches_oracle(tmp_path):
     # Observability::setSelction_Number(300, 3, ...) over the local map at kinematic[1] (G7)
     import ctypes
     from gf_orb_slam_amd.observability import Rng
+    # the driver's Observability gets the camera as the float K[] it read (Observability(fu, fv, ...) takes doubles)
+    ocam = ObsCamera.for_tracking(*(float(np.float32(v)) for v in (fx, fy, cx, cy)), w, h)
     ks = O.obs_predict(xv, 0.05, 2)
     xv1 = np.array(ks[1].Xv[:])
     sel = np.zeros(len(mps), np.int32)

@@ -125,6 +125,108 @@ def test_sequence_matches_oracle(case):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stale,budget", [(0.93, 100), (0.0, 100)])
+def test_update_reference_in_step(stale, budget):
+    """Keyframe graphs (gf_frontend_set_covis): every step runs
+    Tracking::UpdateReference on the frame's matches and tracks the rest of
+    the frame against that local map (Tracking.cc:2745, 3689-3852). 24
+    keyframes of a mapping sweep around the room; the device and the oracle chain (the same
+    UpdateReference, gather and scatter) agree on every field for 10 frames,
+    free-running and with state copy-in, and the local map changes with the
+    frame."""
+    import torch
+
+    from gf_orb_slam_amd.pipeline import FrontEnd
+
+    B, G = 3, 2600
+    W = scene.Workload("euroc", B, n_scenes=3, period=32, seed=4, stale_desc=stale)
+    frames = W.render_all("cuda").contiguous()
+    gmaps = W.build_global_maps(lambda im: O.extract(im), G)
+    fe = FrontEnd("euroc", 1000, B, G, budget)
+    free = []
+    T, V = W.boot_state()
+    for b in range(B):
+        gm = gmaps[W.scene_of[b]]
+        fe.set_map(b, gm["mp"], gm["desc"])
+        fe.set_covis(b, gm["graph"])
+        fe.set_rng(b, 7 + b)
+    fe.set_source(frames, W.scene_of, W.phase)
+    fe.bootstrap(T, V, 0.0)
+    torch.cuda.synchronize()
+    fr = frames.cpu().numpy()
+    for b in range(B):
+        gm = gmaps[W.scene_of[b]]
+        ch = C.Chain("euroc", 1000, G, budget)
+        ch.set_map(gm["mp"], gm["desc"])
+        ch.set_covis(gm["graph"])
+        ch.set_rng(7 + b)
+        ch.bootstrap(_img(W, fr, b, 0), T[b], V[b])
+        free.append(ch)
+    dev = C.read_state(fe)
+    nlocal = []
+    for k in range(1, 11):
+        before = dev
+        fe.step()
+        dev = C.read_state(fe)
+        for b in range(B):
+            gm = gmaps[W.scene_of[b]]
+            ch = C.Chain("euroc", 1000, G, budget)
+            ch.load_from(before, b)
+            ch.set_covis(gm["graph"])
+            ch.step(_img(W, fr, b, k))
+            _compare(dev, ch, b, f"refmap step {k}: ")
+            free[b].step(_img(W, fr, b, k))
+            _compare(dev, free[b], b, f"refmap free-running step {k}: ")
+            assert dev["stats"][14, b] & 4 == 0, "track lost"
+        nlocal.append(dev["stats"][C.STATS.index("nlocal")].copy())
+    nl = np.array(nlocal)
+    assert (nl > 0).all() and (nl < G).any() and len(np.unique(nl)) > 1, nl
+    fe.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("match_s,select_s", [(0.0, 0.0), (0.0, 1e9), (1e9, 0.0), (1e9, 1e9), (4e-4, 6e-4)])
+def test_budgets_match_oracle(match_s, select_s):
+    """gf_set_budgets (Tracking.cc:3230, 3262-3270; ORBmatcher.cc:276-282,
+    366-371). Budget 0 reproduces the reference's early exits: the isInFrustum
+    cap fires on the first local point (every point to mLeftMapPoints,
+    nToMatch = 0: branch 5) and SearchByProjection_Budget returns at once
+    (no additional matches, flag 16). A finite budget cuts at the pass
+    boundary the device clock decides; the oracle chain takes the cut the
+    device reports and the whole state must stay identical. A budget far
+    above the step time is parity mode."""
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, 2000, 100, stale=0.93)
+    fe.set_budgets(match_s, select_s)
+    dev = C.read_state(fe)
+    cuts = []
+    for k in range(1, 7):
+        before = dev
+        fe.step()
+        dev = C.read_state(fe)
+        for b in range(4):
+            br, fl = int(dev["stats"][3, b]), int(dev["stats"][14, b])
+            ch = C.Chain("euroc", 1000, 2000, 100)
+            ch.load_from(before, b)
+            ch.set_cuts(br == 5, fl & 16 != 0)
+            ch.step(_img(W, frames, b, k))
+            _compare(dev, ch, b, f"budgets ({match_s}, {select_s}) step {k}: ")
+            cuts.append((br == 5, fl & 16 != 0, int(dev["stats"][8, b]), int(dev["stats"][2, b])))
+    cf = np.array([c[0] for c in cuts])
+    cs = np.array([c[1] for c in cuts])
+    extra = np.array([c[2] for c in cuts])
+    ntm = np.array([c[3] for c in cuts])
+    if match_s == 0.0:
+        assert cf[ntm > 0].all() and not cf[ntm <= 0].any()
+    if select_s == 0.0:
+        assert (extra == 0).all() and cs.any()
+    if match_s == 1e9:
+        assert not cf.any()
+    if select_s == 1e9:
+        assert not cs.any()
+    fe.close()
+
+
+@pytest.mark.gpu
 def test_bench_shape_parity():
     """The timed configuration itself: 1024 streams in 2 groups of 512 (as
     bench.py runs them, each group on its own context / HIP stream, launches
