@@ -20,6 +20,8 @@
 #include <cmath>
 #include <cstring>
 
+#include <type_traits>
+
 #include "common.h"
 #include "match_common.h"
 #include "rng.h"
@@ -665,6 +667,87 @@ __device__ __forceinline__ void wave_sort_desc(double& hs, int& hc) {
     }
 }
 
+// The live set as K registers per lane, position p = 64 r + lane, sorted by
+// score descending (positions past the set hold candidate -1 and sort last).
+template <int K>
+struct LiveSet {
+    double s[K];
+    int c[K];
+    int m[K];  // the candidate's one-point match was found
+};
+
+__device__ __forceinline__ bool before_desc(double as, int ac, double bs, int bc) {  // a sorts before b
+    return ac >= 0 && (bc < 0 || as > bs);
+}
+
+template <int K>
+__device__ __forceinline__ void live_cmpx(LiveSet<K>& L, int r0, int r1, bool desc_first) {
+    // registers r0 < r1 of one lane: position r0 gets the earlier one when desc_first
+    const bool sw = desc_first ? before_desc(L.s[r1], L.c[r1], L.s[r0], L.c[r0])
+                               : before_desc(L.s[r0], L.c[r0], L.s[r1], L.c[r1]);
+    if (sw) {
+        const double ts = L.s[r0];
+        const int tc = L.c[r0];
+        L.s[r0] = L.s[r1];
+        L.c[r0] = L.c[r1];
+        L.s[r1] = ts;
+        L.c[r1] = tc;
+    }
+}
+
+// Bitonic sort of the 64 K positions (payload: candidate; match flags are
+// loaded after the sort).
+template <int K>
+__device__ __forceinline__ void live_sort(LiveSet<K>& L) {
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int k = 2; k <= 64 * K; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const int rj = j >> 6;
+#pragma unroll
+                for (int r = 0; r < K; r++) {
+                    if (r & rj) continue;
+                    const bool asc_block = ((64 * r + lane) & k) != 0;  // this block sorts ascending
+                    live_cmpx<K>(L, r, r | rj, !asc_block);
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < K; r++) {
+                    const double os = __shfl_xor(L.s[r], j, 64);
+                    const int oc = __shfl_xor(L.c[r], j, 64);
+                    const int p = 64 * r + lane;
+                    const bool ogt = before_desc(os, oc, L.s[r], L.c[r]);
+                    const bool olt = before_desc(L.s[r], L.c[r], os, oc);
+                    const bool keep_first = ((p & j) == 0) == ((p & k) == 0);
+                    if (keep_first ? ogt : olt) {
+                        L.s[r] = os;
+                        L.c[r] = oc;
+                    }
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ double rl0(double v) {  // lane 0's value
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 0);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
+__device__ __forceinline__ int dpp_next(int v) {  // lane i <- lane i + 1 (wave_shl:1)
+    return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ double dpp_next(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)dpp_next((int)(uint32_t)b), hi = (uint32_t)dpp_next((int)(uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
 // Heap top of the live candidates: the arg-max, unless the maximum is tied
 // or a score is NaN, when std::priority_queue's order is reproduced by
 // replaying its push/pop history (sz pushes, then pop/push pairs) exactly.
@@ -703,9 +786,6 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
         *pos = p;
         return al[p];
     }
-#ifdef GF_AM_STAMP
-    if (lane == 0) atomicAdd(&g_am_stamp[7], 1ull);  // heap replays (tied or NaN maximum)
-#endif
     if (lane == 0) {
         int hn = 0;
         const IdxLess cmp{C.score};
@@ -770,7 +850,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     uint8_t* c_alive = (uint8_t*)(alv + PC);                               // PC
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
-    __shared__ int s_res, s_exh, s_nsucc;
+    __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
 
     const int f = blockIdx.x, lane = threadIdx.x;
     const FrameConst& fc = A.fc;
@@ -880,24 +960,38 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         // -- draws, ahead of need
         uint32_t sd = rs;
         int tries = 0, run = 0, nc = 0, evald = 0, exh_at = -1;
+        AM_T(6);
         if (!nsucc_valid && last_npop > sz) {
             // the last round had to pop: count the pool entries that can still be
             // matched (slots whose holders were claimed are scanned again)
-            int ns = 0;
+            // pass 1, loads only: a slot whose holders are unclaimed keeps its result
+            bool known = false;
+            unsigned long long stale = 0ull;  // bit w: this lane's slot in word w needs a rescan
             for (int w = 0; w < nw0; w++) {
                 const int sl = w * 64 + lane;
-                int mi = -1;
-                if ((pbits[w] >> lane) & 1ull) {
-                    int md;
-                    mi = slot_match(A, fc, f, SM, sl, lmk[sl], cell_start, items, claim, K, D, md);
-                }
-                ns += mi >= 0;
+                if (!((pbits[w] >> lane) & 1ull)) continue;
+                const int h1 = sm_h1[sl], h2 = sm_h2[sl];
+                if ((h1 >= 0 && claim[h1] >= 0) || (h2 >= 0 && claim[h2] >= 0))
+                    stale |= 1ull << w;
+                else
+                    known |= sm_match[sl] >= 0;
             }
-            ns = gfd::warp_sum(ns);
+            int ns = __ballot(known) ? 1 : 0;  // only "none left" matters
+            // pass 2: rescans, until a matchable slot turns up
+            for (int w = 0; w < nw0 && !ns; w++) {
+                int mi = -1;
+                if ((stale >> w) & 1ull) {
+                    int md;
+                    mi = slot_match(A, fc, f, SM, w * 64 + lane, lmk[w * 64 + lane], cell_start, items, claim, K, D,
+                                    md);
+                }
+                ns = __ballot(mi >= 0) ? 1 : 0;
+            }
             if (lane == 0) s_nsucc = ns;
             nsucc_valid = true;
             __syncthreads();
         }
+        AM_T(7);
         if (nsucc_valid && s_nsucc == 0) {  // nothing left to match: the round draws until the draws give out
             colvis[lane] = 0ull;
             __syncthreads();
@@ -925,11 +1019,6 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         }
         eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
         evald = nc;
-        for (int c = lane; c < sz; c += AW) {
-            C.alive[c] = 1;
-            alv[c] = (int16_t)c;
-        }
-        __syncthreads();
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
         // While the live set fits the wave and no two live scores tie (NaN
@@ -938,73 +1027,173 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         // the first tie on) wave_top, with the exact heap replay for ties.
         int npop = 0, top = -1, tpos = -1;
         bool exh = false, success = false;
-        bool sorted = sz <= AW;
-        double hs = -INFINITY;
-        int hc = -1;
-        if (sorted) {
-            if (lane < sz) {
-                hc = lane;
-                hs = C.score[lane];
+        // (a) the live set sorted in registers (K per lane, position p = 64 r +
+        // lane, descending): the top is position 0; a failed top is popped by
+        // shifting positions 1.. down one (DPP wave_shl, plus the neighbouring
+        // register's lane 0 for lane 63) and the replacement goes to the
+        // place its rank (ballots) gives. Ties (and NaN) leave for (b), where
+        // the heap replay fixes their order. Alive flags are written at the end.
+        auto draw_eval = [&](int rep) {
+            if (rep >= nc && exh_at < 0) {
+                AM_T(4);
+                while (rep >= nc && exh_at < 0) {
+                    if (lane == 0) s_exh = -1;
+                    __syncthreads();
+                    nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
+                    exh_at = s_exh;
+                }
+                AM_T(2);
             }
-            if (__ballot(lane < sz && hs != hs)) {
-                sorted = false;
-            } else {
-                wave_sort_desc(hs, hc);
-                const double nx = __shfl(hs, min(lane + 1, AW - 1), 64);
-                if (__ballot(lane + 1 < sz && nx == hs)) sorted = false;
-            }
-        }
-        while (true) {
-            if (sorted)
-                top = __shfl(hc, 0, 64);
-            else
-                top = wave_top(C, alv, sz, sz, npop, rheap, &s_res, &tpos);
-            if (C.match[top] >= 0) {
-                success = true;
-                break;
-            }
-            if (lane == 0) C.alive[top] = 0;  // heapSubset.pop()
-            const int rep = sz + npop;       // the replacement draw
-            while (rep >= nc && exh_at < 0) {
-                if (lane == 0) s_exh = -1;
-                __syncthreads();
-                nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
-                exh_at = s_exh;
-            }
-            if (rep >= nc) {
-                exh = true;
-                break;
-            }
-            if (rep >= evald) {
+            if (rep < nc && rep >= evald) {
+                AM_T(4);
                 eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
                 evald = nc;
+                AM_T(3);
             }
-            if (sorted) {
+        };
+        auto sorted_loop = [&](auto kk) -> int {  // 1: round decided, 0: leave for (b)
+            constexpr int KR = decltype(kk)::value;
+            LiveSet<KR> L;
+            bool bad = false;
+#pragma unroll
+            for (int r = 0; r < KR; r++) {
+                const int p = 64 * r + lane;
+                L.c[r] = p < sz ? p : -1;
+                L.s[r] = p < sz ? C.score[p] : -INFINITY;
+                bad |= p < sz && L.s[r] != L.s[r];
+            }
+            if (__ballot(bad)) return 0;
+            live_sort<KR>(L);
+            bool tie = false;
+#pragma unroll
+            for (int r = 0; r < KR; r++) {
+                const double nx0 = dpp_next(L.s[r]);
+                const double nx = lane < 63 ? nx0 : (r + 1 < KR ? rl0(L.s[r + 1 < KR ? r + 1 : r]) : -INFINITY);
+                const int p = 64 * r + lane;
+                tie |= p + 1 < sz && nx == L.s[r];
+                L.m[r] = L.c[r] >= 0 && C.match[max(L.c[r], 0)] >= 0;
+            }
+            if (__ballot(tie)) return 0;
+            while (true) {
+                top = __builtin_amdgcn_readlane(L.c[0], 0);
+                if (__builtin_amdgcn_readlane(L.m[0], 0)) {
+                    success = true;
+                    break;
+                }
+                const int rep = sz + npop;  // the replacement draw
+                draw_eval(rep);
+                if (rep >= nc) {
+                    exh = true;
+                    break;
+                }
                 const double x = C.score[rep];
-                const bool live = lane >= 1 && lane < sz;  // lane 0 was the popped top
-                if (x != x || __ballot(live && hs == x)) {
-                    // a tie: hand the live set (lanes 1.., then the replacement) to wave_top
-                    if (live) alv[lane - 1] = (int16_t)hc;
-                    if (lane == 0) alv[sz - 1] = (int16_t)rep;
-                    sorted = false;
-                } else {
-                    const int r = __popcll(__ballot(live && hs > x));  // the replacement's place
-                    const double hs1 = __shfl(hs, min(lane + 1, AW - 1), 64);
-                    const int hc1 = __shfl(hc, min(lane + 1, AW - 1), 64);
-                    if (lane < r) {
-                        hs = hs1;
-                        hc = hc1;
-                    } else if (lane == r) {
-                        hs = x;
-                        hc = rep;
+                const int xm = C.match[rep] >= 0;
+                bool t2 = x != x;
+                int rank = 0;
+#pragma unroll
+                for (int r = 0; r < KR; r++) {
+                    const int p = 64 * r + lane;
+                    const bool live = p >= 1 && p < sz;  // position 0 is the popped top
+                    t2 |= __ballot(live && L.s[r] == x) != 0ull;
+                    rank += __popcll(__ballot(live && L.s[r] > x));
+                }
+                if (t2) {  // hand the live set (positions 1.., then the replacement) to (b)
+                    npop++;
+                    for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
+                    __syncthreads();
+#pragma unroll
+                    for (int r = 0; r < KR; r++) {
+                        const int p = 64 * r + lane;
+                        if (p >= 1 && p < sz) {
+                            alv[p - 1] = (int16_t)L.c[r];
+                            C.alive[L.c[r]] = 1;
+                        }
+                    }
+                    if (lane == 0) {
+                        alv[sz - 1] = (int16_t)rep;
+                        C.alive[rep] = 1;
+                    }
+                    __syncthreads();
+                    return 0;
+                }
+                // new[p] = old[p + 1] for p < rank, new[rank] = the replacement
+                double ns[KR];
+                int nc2[KR], nm[KR];
+#pragma unroll
+                for (int r = 0; r < KR; r++) {
+                    const double a = dpp_next(L.s[r]);
+                    const int b2 = dpp_next(L.c[r]), m2 = dpp_next(L.m[r]);
+                    const int rn = r + 1 < KR ? r + 1 : r;
+                    const double a63 = r + 1 < KR ? rl0(L.s[rn]) : -INFINITY;
+                    const int b63 = r + 1 < KR ? __builtin_amdgcn_readlane(L.c[rn], 0) : -1;
+                    const int m63 = r + 1 < KR ? __builtin_amdgcn_readlane(L.m[rn], 0) : 0;
+                    ns[r] = lane < 63 ? a : a63;
+                    nc2[r] = lane < 63 ? b2 : b63;
+                    nm[r] = lane < 63 ? m2 : m63;
+                }
+#pragma unroll
+                for (int r = 0; r < KR; r++) {
+                    const int p = 64 * r + lane;
+                    if (p < rank) {
+                        L.s[r] = ns[r];
+                        L.c[r] = nc2[r];
+                        L.m[r] = nm[r];
+                    } else if (p == rank) {
+                        L.s[r] = x;
+                        L.c[r] = rep;
+                        L.m[r] = xm;
                     }
                 }
-            } else if (lane == 0) {
-                alv[tpos] = (int16_t)rep;  // the replacement takes the popped entry's place
+                npop++;
             }
-            if (lane == 0) C.alive[rep] = 1;
-            npop++;
+            // alive flags of the candidates that entered: popped 0, live 1
+            for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
             __syncthreads();
+#pragma unroll
+            for (int r = 0; r < KR; r++) {
+                const int p = 64 * r + lane;
+                if (p < sz && !(exh && p == 0)) C.alive[L.c[r]] = 1;  // on exhaustion the top was popped
+            }
+            __syncthreads();
+            return 1;
+        };
+        const int kreg = (sz + 63) >> 6;
+        int decided = 0;
+        if (kreg == 1)
+            decided = sorted_loop(std::integral_constant<int, 1>{});
+        else if (kreg == 2)
+            decided = sorted_loop(std::integral_constant<int, 2>{});
+        else if (kreg <= 4)
+            decided = sorted_loop(std::integral_constant<int, 4>{});
+        if (!decided) {
+            if (npop == 0) {  // (b) from the start: the initial live set
+                for (int c = lane; c < sz; c += AW) {
+                    C.alive[c] = 1;
+                    alv[c] = (int16_t)c;
+                }
+                __syncthreads();
+            }
+            // (b) general: wave_top over the live list (ties replay the heap)
+            while (true) {
+                top = wave_top(C, alv, sz, sz, npop, rheap, &s_res, &tpos);
+                if (C.match[top] >= 0) {
+                    success = true;
+                    break;
+                }
+                if (lane == 0) C.alive[top] = 0;  // heapSubset.pop()
+                const int rep = sz + npop;       // the replacement draw
+                draw_eval(rep);
+                if (rep >= nc) {
+                    exh = true;
+                    break;
+                }
+                if (lane == 0) {
+                    C.alive[rep] = 1;
+                    alv[tpos] = (int16_t)rep;  // the replacement takes the popped entry's place
+                }
+                npop++;
+                __syncthreads();
+            }
         }
         AM_T(4);
         // the successful top's H row and its keypoint's octave, loaded now so

@@ -125,16 +125,24 @@ class TorchComm:
 
 # ------------------------------------------------------------- packing
 def pack_world(scenes, maps) -> np.ndarray:
-    """Scenes (Scene.pack) and per-scene local maps in one blob."""
+    """Scenes (Scene.pack) and per-scene maps in one blob: (points,
+    descriptors) or (points, descriptors, keyframe graph arrays)."""
+    from .localmap import _ARRAYS
     from .matcher import MAP_POINT_DTYPE
 
     parts = []
-    for sc, (mp, d) in zip(scenes, maps):
+    for sc, m in zip(scenes, maps):
+        mp, d = m[0], m[1]
+        g = m[2] if len(m) > 2 else None
         sb = sc.pack()
         mb = np.ascontiguousarray(mp, MAP_POINT_DTYPE).view(np.uint8).reshape(-1)
         db = np.ascontiguousarray(d, np.uint8).reshape(-1)
-        hdr = np.array([sb.nbytes, len(mp)], np.int64).view(np.uint8)
+        hdr = np.array([sb.nbytes, len(mp), 0 if g is None else 1], np.int64).view(np.uint8)
         parts += [hdr, sb, mb, db]
+        if g is not None:
+            for k, dt in _ARRAYS:
+                a = np.ascontiguousarray(g[k], dt).reshape(-1)
+                parts += [np.array([len(a)], np.int64).view(np.uint8), a.view(np.uint8)]
     return np.concatenate([np.array([len(scenes)], np.int64).view(np.uint8)] + parts)
 
 
@@ -142,19 +150,31 @@ def unpack_world(blob: np.ndarray):
     from .matcher import MAP_POINT_DTYPE
     from .scene import Scene
 
+    from .localmap import _ARRAYS
+
     S = int(blob[:8].view(np.int64)[0])
     o = 8
     scenes, maps = [], []
     for _ in range(S):
-        sb, m = (int(x) for x in blob[o:o + 16].view(np.int64))
-        o += 16
+        sb, m, hg = (int(x) for x in blob[o:o + 24].view(np.int64))
+        o += 24
         scenes.append(Scene.unpack(blob[o:o + sb]))
         o += sb
         mp = blob[o:o + m * MAP_POINT_DTYPE.itemsize].copy().view(MAP_POINT_DTYPE)
         o += m * MAP_POINT_DTYPE.itemsize
         d = blob[o:o + 32 * m].copy().reshape(m, 32)
         o += 32 * m
-        maps.append((mp, d))
+        if hg:
+            g = {}
+            for k, dt in _ARRAYS:
+                n = int(blob[o:o + 8].view(np.int64)[0])
+                o += 8
+                nb = n * np.dtype(dt).itemsize
+                g[k] = blob[o:o + nb].copy().view(dt)
+                o += nb
+            maps.append((mp, d, g))
+        else:
+            maps.append((mp, d))
     return scenes, maps
 
 

@@ -45,10 +45,10 @@ fe.sync()
 f(st.ctypes.data, 0)
 prof = fe.prof_report()
 h = fe.read("hist")
-names = ["setup", "pool", "draw_initial", "eval_initial", "heap_loop", "commit_rng", "pool_update"]
-per = st[:7].astype(np.float64) / (B * steps)
+names = ["setup", "pool", "draws", "evals", "heap_pops", "commit_rng", "pool_update", "recount"]
+per = st[:8].astype(np.float64) / (B * steps)
 out = {"B": B, "steps": steps, "cycles_per_frame": {k: round(float(v)) for k, v in zip(names, per)},
-       "heap_replays_per_frame": float(st[7]) / (B * steps), "logdets_per_frame": float(h[:, 6].sum()) / (B * steps), "matches_per_frame": float(h[:, 7].sum()) / (B * steps),
+       "logdets_per_frame": float(h[:, 6].sum()) / (B * steps), "matches_per_frame": float(h[:, 7].sum()) / (B * steps),
        "k_active_match_ms": prof["k_active_match"][0] / prof["k_active_match"][1],
        "k_onepoint_pre_ms": prof["k_onepoint_pre"][0] / prof["k_onepoint_pre"][1]}
 print(json.dumps(out))

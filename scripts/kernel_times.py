@@ -1,6 +1,7 @@
 """Per-kernel device time of one front-end group alone (no overlapping
 groups): B sequences of the bench workload, HIP events per launch.
-Usage: python scripts/kernel_times.py [B] [steps]"""
+Usage: python scripts/kernel_times.py [B] [steps] [stale]  (stale map-descriptor
+fraction, default 0.93: the bench's config-2 regime)"""
 import json
 import os
 import sys
@@ -14,7 +15,8 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0)
+stale = float(sys.argv[3]) if len(sys.argv) > 3 else 0.93
+W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=stale)
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
 maps = W.build_maps(lambda im: ex(im), 2000, device="cuda")
