@@ -82,13 +82,15 @@ def _free_port() -> int:
 def _chain_worker(args) -> tuple:
     """One host core tracking one sequence on the CPU oracle chain
     (oracle/chain.cpp, timing build); no GPU."""
-    camera, nfeat, nmap, budget, fps, mp, desc, frames, T, V, seed, budget_s, lib = args
+    camera, nfeat, nmap, budget, fps, m, frames, T, V, seed, budget_s, lib = args
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["GF_ORACLE_LIB"] = lib
     import oracle_chain as C
 
     ch = C.Chain(camera, nfeat, nmap, budget, fps=fps)
-    ch.set_map(mp, desc)
+    ch.set_map(m[0], m[1])
+    if len(m) > 2:
+        ch.set_covis(m[2])
     ch.set_rng(seed)
     ch.bootstrap(frames[0], T, V)
     times, stages = [], []
@@ -168,7 +170,7 @@ def cpu_baseline(camera, nfeat, nmap, budget, fps, maps, W, frames_host, budget_
         s = W.scene_of[b]
         seq = np.stack([frames_host[s][(W.phase[b] + k) % W.period] for k in range(W.period)])
         T, V = W.boot_state()
-        return (camera, nfeat, nmap, budget, fps, maps[s][0], maps[s][1], seq, T[b], V[b], 1 + b, secs, lib)
+        return (camera, nfeat, nmap, budget, fps, maps[s], seq, T[b], V[b], 1 + b, secs, lib)
 
     cpus = cpu_share()
     n, dt, times, stages = _pinned_chain_worker((cpus[0], job(0, budget_s)))
@@ -177,8 +179,9 @@ def cpu_baseline(camera, nfeat, nmap, budget, fps, maps, W, frames_host, budget_
              "predict_next", "additional_matches"]
     st = np.asarray(stages) * 1e3
     out = {"value": round(n / dt, 3), "unit": "frames/s", "cores": 1, "kind": "port",
-           "sample": f"{n} consecutive frames of one rendered {camera} sequence ({nfeat} feats, {nmap}-point local "
-                     f"map, GF budget {budget}), full tracking step per frame on the C++ oracle chain, "
+           "sample": f"{n} consecutive frames of one rendered {camera} sequence ({nfeat} feats, "
+                     f"{'keyframe map of %d points, UpdateReference every frame' % nmap if len(maps[0]) > 2 else '%d-point local map' % nmap}, "
+                     f"GF budget {budget}), full tracking step per frame on the C++ oracle chain, "
                      f"1 thread, {dt:.1f} s",
            "build": os.path.basename(lib),
            "ms_per_frame_median": round(float(np.median(t)), 2),
@@ -330,15 +333,30 @@ def lba_leg(batch: int, repeats: int = 3, cpu: bool = True) -> dict:
 
 
 # ------------------------------------------------------------- main
-def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, device: int, stale: float):
-    """Rank 0: the scenes of the loops and each scene's keyframe-built local
-    map (keyframes extracted with the product extractor on this GPU)."""
+def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, device: int, stale: float,
+                refmap: bool, n_kf: int):
+    """Rank 0: the scenes of the loops and each scene's map (keyframes
+    extracted with the product extractor on this GPU): with refmap a keyframe
+    map (points, descriptors, covisibility graph) whose local map
+    Tracking::UpdateReference assembles every frame, else one fixed
+    keyframe-built local map."""
     from gf_orb_slam_amd import ORBextractor, scene
 
     W0 = scene.Workload(cam, B, n_scenes=S, period=period, seed=0, stale_desc=stale)
     ex = ORBextractor(nfeat, 1.2, 8, 1, 20)
-    maps = W0.build_maps(lambda im: ex(im), nmap, device=f"cuda:{device}")
-    return W0.scenes, maps
+    if refmap:
+        gm = W0.build_global_maps(lambda im: ex(im), nmap, n_kf=n_kf, device=f"cuda:{device}")
+        return W0.scenes, [(g["mp"], g["desc"], g["graph"]) for g in gm]
+    return W0.scenes, W0.build_maps(lambda im: ex(im), nmap, device=f"cuda:{device}")
+
+
+def load_map(fe, b: int, m, with_points: bool = True):
+    """Stream b's map: points + descriptors (skipped when another rank's
+    broadcast supplies them), then its keyframe graph if the world has one."""
+    if with_points:
+        fe.set_map(b, m[0], m[1])
+    if len(m) > 2:
+        fe.set_covis(b, m[2])
 
 
 def main():
@@ -354,11 +372,16 @@ def main():
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
-    ap.add_argument("--map", type=int, default=2000, help="local-map points per sequence")
-    ap.add_argument("--stale-desc", type=float, default=0.93,
-                    help="fraction of local-map points with a stale (random) descriptor; 0.93 gives config 2's "
-                         "regime of SURVEY §8d: ~60 motion-model matches vs GF budget 100, runActiveMapMatching "
-                         "every frame (scene.build_map)")
+    ap.add_argument("--map", type=int, default=None,
+                    help="map points per sequence: the keyframe map (default 2100, local maps of ~2000 points "
+                         "assembled from it) or, with --fixed-map, the fixed local map (default 2000)")
+    ap.add_argument("--fixed-map", action="store_true",
+                    help="one fixed local map per sequence instead of UpdateReference over a keyframe map")
+    ap.add_argument("--keyframes", type=int, default=24, help="keyframes of each scene's map (UpdateReference mode)")
+    ap.add_argument("--stale-desc", type=float, default=None,
+                    help="fraction of map points with a stale (random) descriptor; the defaults (0.82 keyframe map, "
+                         "0.93 fixed map) give config 2's regime of SURVEY §8d: ~60 motion-model matches vs GF "
+                         "budget 100, runActiveMapMatching every frame (scene.build_map / build_global_map)")
     ap.add_argument("--scenes", type=int, default=8)
     ap.add_argument("--period", type=int, default=32, help="frames per loop of the rendered trajectory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -399,6 +422,11 @@ def main():
     from gf_orb_slam_amd.pipeline import STATS, FrontEnd, chain_extraction
 
     cam = args.camera
+    refmap = not args.fixed_map
+    if args.map is None:
+        args.map = 2000 if args.fixed_map else 2100
+    if args.stale_desc is None:
+        args.stale_desc = 0.93 if args.fixed_map else 0.82
     B, G = args.batch, max(1, args.groups)
     if B % G:
         raise SystemExit(f"--batch {B} must be a multiple of --groups {G}")
@@ -411,7 +439,8 @@ def main():
     with _StdoutToStderr():
         gd = GfDist(ctx0, rank, world)
     scenes, maps, world_ck, world_span, world_bytes = share_world(
-        gd, rank, lambda: build_world(cam, B, S, args.period, args.nfeatures, args.map, local, args.stale_desc))
+        gd, rank, lambda: build_world(cam, B, S, args.period, args.nfeatures, args.map, local, args.stale_desc,
+                                      refmap, args.keyframes))
     voc = ORBVocabulary(synth.synth_vocabulary_fast(seed=7, k=10, L=6), ctx=ctx0) if rank == 0 else None
     voc = gd.bcast_vocab(voc, 0)
     voc_ck = voc.checksum()
@@ -426,8 +455,10 @@ def main():
         fe = FrontEnd(cam, args.nfeatures, Bg, args.map, args.gf_budget, ctx=Context(local))
         if rank == 0:
             for b in range(Bg):
-                fe.set_map(b, *maps[W.scene_of[g * Bg + b]])
-        gd.bcast_map(fe, 0)  # every rank's streams get rank 0's local maps, device to device
+                fe.set_map(b, *maps[W.scene_of[g * Bg + b]][:2])
+        gd.bcast_map(fe, 0)  # every rank's streams get rank 0's maps, device to device
+        for b in range(Bg):  # keyframe graphs: host-side, from the world blob
+            load_map(fe, b, maps[W.scene_of[g * Bg + b]], with_points=False)
         map_cks.append(checksum(fe.read("map")) ^ checksum(fe.read("map_desc")))
         for b in range(Bg):
             fe.set_rng(b, 1 + rank * B + g * Bg + b)
@@ -557,6 +588,7 @@ def main():
     pose_avg_ms = pose_ms[0] / max(pose_ms[1], 1)
     mean_iters = float(iters.mean())
     nfr = max(B * args.steps, 1)
+    local_mean = float(final["nlocal"].mean()) if refmap else float(args.map)
 
     out = {
         "metric": "front-end fps (extract+match+GF-select) @ 752x480/1000 feats; pose-opt ms/iter",
@@ -570,17 +602,25 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/int32 (extract, match), f64 (GF, pose LM)",
-        "data": "synthetic: rendered sequences (textured-plane rooms, closed EuRoC-speed loops), keyframe-built "
-                "local maps with %.0f%% stale (random) map descriptors; no dataset reachable" % (100 * args.stale_desc),
+        "data": "synthetic: rendered sequences (textured-plane rooms, closed EuRoC-speed loops), %s with %.0f%% "
+                "stale (random) map descriptors; no dataset reachable"
+                % ("keyframe maps (%d keyframes of a mapping sweep, covisibility graph)" % args.keyframes if refmap
+                   else "keyframe-built fixed local maps", 100 * args.stale_desc),
         "config": {"workload": f"config 2: {cam} {W.cam[0]}x{W.cam[1]}, {args.nfeatures} feats, GF budget "
-                               f"{args.gf_budget}, {args.map}-point local maps ({args.stale_desc:.2f} stale "
-                               f"descriptors: ~60 motion-model matches, runActiveMapMatching every frame), {B} "
+                               f"{args.gf_budget}, "
+                               + (f"{args.keyframes}-keyframe maps of {args.map} points, the local map (~"
+                                  f"{local_mean:.0f} points) rebuilt every frame by Tracking::UpdateReference"
+                                  if refmap else f"{args.map}-point fixed local maps")
+                               + f" ({args.stale_desc:.2f} stale descriptors: ~60 motion-model matches, "
+                               f"runActiveMapMatching every frame), {B} "
                                f"tracked sequences per GPU in {G} groups; step = one frame of every sequence "
                                f"through Tracking::GrabImage (WORKING): extract, motion model + "
-                               f"SearchByProjection(last) + PoseOptimization, GF SearchReferencePointsInFrustum "
+                               f"SearchByProjection(last) + PoseOptimization, "
+                               + ("UpdateReference (local keyframes + local points), " if refmap else "")
+                               + f"GF SearchReferencePointsInFrustum "
                                f"(FRAME_INFO, isInFrustum, MAP_INFO, runActiveMapMatching), PoseOptimization, "
                                f"motion update, next-frame MAP_INFO prediction, SearchAdditionalMatchesInFrame",
-                   "sequences_per_gpu": B, "stream_groups": G,
+                   "sequences_per_gpu": B, "stream_groups": G, "update_reference": refmap,
                    "extraction_gate": bool(gates),
                    "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
         "startup": startup,
@@ -601,6 +641,7 @@ def main():
                                           "budget_cut": int(mix[5])},
                      "branch_mix_warmup": {"leftovers_only": int(hist[1]), "search_by_projection": int(hist[2]),
                                            "active_matching": int(hist[3]), "nothing_in_view": int(hist[4])},
+                     "mean_local_map_points": round(local_mean, 1),
                      "mean_inliers": round(float(final["inl2"].mean()), 1),
                      "mean_last_frame_matches": round(float(final["m3"].mean()), 1),
                      "mean_num_to_match": round(float(final["to_match"].mean()), 1),
@@ -677,7 +718,7 @@ def main():
     if rank == 0 and args.single_stream_steps > 0:
         # one sequence alone: per-frame latency, the step replayed as one HIP graph
         fe = FrontEnd(cam, args.nfeatures, 1, args.map, args.gf_budget, ctx=Context(local))
-        fe.set_map(0, *maps[W.scene_of[0]])
+        load_map(fe, 0, maps[W.scene_of[0]])
         fe.set_rng(0, 1)
         fe.set_source(frames, W.scene_of[:1], W.phase[:1])
         fe.bootstrap(T[:1], V[:1], 0.0)
@@ -700,7 +741,7 @@ def main():
         # frames handed over from host memory: the PCIe copy inside the step (not `value`)
         fe = FrontEnd(cam, args.nfeatures, Bg, args.map, args.gf_budget, ctx=Context(local))
         for b in range(Bg):
-            fe.set_map(b, *maps[W.scene_of[b]])
+            load_map(fe, b, maps[W.scene_of[b]])
         fe.set_source(frames, W.scene_of[:Bg], W.phase[:Bg])
         fe.bootstrap(T[:Bg], V[:Bg], 0.0)
         fh = frames.cpu().numpy()

@@ -66,6 +66,29 @@ int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap
                             int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap, int32_t* d_ref_kf,
                             int32_t* d_first, hipStream_t s);
 
+// The observability passes with the map-point state (H / ObsMat / u_proj) kept
+// in map order while the step runs over a local map: local point q of frame f
+// reads and writes entry remap[f * map_stride + q] (null: q itself). The
+// extern "C" gf_obs_*_dev entry points are these with remap = null (gf.hip).
+int obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const gf_keypoint* d_kps,
+                   const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp, const uint8_t* d_outlier,
+                   const float* d_map_pos, const int32_t* d_nmp, int map_stride, const float* level_sigma2,
+                   int nlevels, double* d_H, double* d_info, float* d_uv, const int32_t* d_remap, void* stream);
+int obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
+                 const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views, int32_t* d_upd_id,
+                 int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated, const int32_t* d_remap,
+                 void* stream);
+int obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps, int kp_stride,
+                           const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp, int map_stride,
+                           int frame_id, double diag, double* d_out, const int32_t* d_remap, void* stream);
+int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                     const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                     const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info, const double* d_H,
+                     const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
+                     const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
+                     int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
+                     const int32_t* d_remap, void* stream);
+
 // RCCL broadcast on the communicator's stream (dist.hip), asynchronous.
 int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);
 int dist_rank(gf_dist* d);

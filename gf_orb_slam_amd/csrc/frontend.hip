@@ -360,25 +360,81 @@ struct MapArrays {
     int32_t* upd;
 };
 
-__global__ __launch_bounds__(256) void k_fe_gather(FeDev D, MapArrays G, MapArrays L, int32_t* lnmp) {
+// Per-point rows of one map array, W 32-bit words per point, for the local
+// points [k0, k0 + np) of a stream: gather (dst local <- src map point lm[k])
+// or scatter (dst map point lm[k] <- src local). Eight independent loads in
+// flight per thread before the stores: a plain per-element loop leaves the
+// copy latency-bound at ~1.3 TB/s.
+template <int W>
+__device__ __forceinline__ void copy_rows(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                          const int32_t* __restrict__ lm, long long o, int k0, int np, bool gather) {
+    constexpr int U = 8;
+    const int t = threadIdx.x, nw = np * W;
+    for (int w0 = t; w0 < nw; w0 += 256 * U) {
+        uint32_t v[U];
+        long long at[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int w = w0 + u * 256;
+            at[u] = -1;
+            if (w < nw) {
+                const int p = w / W, e = w - p * W, k = k0 + p;
+                const long long g = o + lm[k], l = o + k;
+                v[u] = src[(gather ? g : l) * W + e];
+                at[u] = (gather ? l : g) * W + e;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (at[u] >= 0) dst[at[u]] = v[u];
+    }
+}
+
+constexpr int ROWS_PER_BLOCK = 32;
+
+template <int W, typename T>
+__device__ __forceinline__ void rows(T* dst, const T* src, const int32_t* lm, long long o, int k0, int np,
+                                     bool gather) {
+    copy_rows<W>(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src), lm, o, k0, np, gather);
+}
+
+// The local map's rows (grid: point chunks x streams).
+__global__ __launch_bounds__(256) void k_fe_gather_rows(FeDev D, MapArrays G, MapArrays L) {
+    const int b = blockIdx.y, k0 = blockIdx.x * ROWS_PER_BLOCK;
+    const int n = D.nlm[b];
+    if (k0 >= n) return;
+    const int np = min(ROWS_PER_BLOCK, n - k0);
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    rows<sizeof(gf_map_point) / 4>((gf_map_point*)L.map, G.map, lm, o, k0, np, true);
+    rows<8>((uint8_t*)L.desc, G.desc, lm, o, k0, np, true);
+    rows<3>((float*)L.pos, G.pos, lm, o, k0, np, true);
+    rows<sizeof(gf_mp_view) / 4>(L.views, G.views, lm, o, k0, np, true);
+    rows<1>(L.upd, G.upd, lm, o, k0, np, true);
+}
+
+// The local map's visibility and updateAtFrameId back to the stream's map
+// points (H / ObsMat / u_proj are written in map order through the remap).
+__global__ __launch_bounds__(256) void k_fe_scatter_rows(FeDev D, MapArrays G, MapArrays L) {
+    const int b = blockIdx.y, k0 = blockIdx.x * ROWS_PER_BLOCK;
+    const int n = D.nlm[b];
+    if (k0 >= n) return;
+    const int np = min(ROWS_PER_BLOCK, n - k0);
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    rows<sizeof(gf_mp_view) / 4>(G.views, L.views, lm, o, k0, np, false);
+    rows<1>(G.upd, L.upd, lm, o, k0, np, false);
+}
+
+// Index conversion for the step (one workgroup per stream): g2l of the local
+// points, the frame's matches to local indices (a match outside the local map
+// is dropped; UpdateReference puts every matched point's keyframes in it).
+__global__ __launch_bounds__(256) void k_fe_gather(FeDev D, int32_t* lnmp) {
     const int b = blockIdx.x, t = threadIdx.x;
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    for (int k = t; k < n; k += 256) {
-        const long long g = o + lm[k], l = o + k;
-        ((gf_map_point*)L.map)[l] = G.map[g];
-        reinterpret_cast<uint4*>((uint8_t*)L.desc + 32 * l)[0] = reinterpret_cast<const uint4*>(G.desc + 32 * g)[0];
-        reinterpret_cast<uint4*>((uint8_t*)L.desc + 32 * l)[1] = reinterpret_cast<const uint4*>(G.desc + 32 * g)[1];
-        for (int c = 0; c < 3; c++) ((float*)L.pos)[3 * l + c] = G.pos[3 * g + c];
-        L.views[l] = G.views[g];
-        L.uv[2 * l] = G.uv[2 * g];
-        L.uv[2 * l + 1] = G.uv[2 * g + 1];
-        L.upd[l] = G.upd[g];
-        D.g2l[g] = k;
-    }
-    for (int e = t; e < 14 * n; e += 256) L.H[14 * o + e] = G.H[14 * (o + lm[e / 14]) + e % 14];
-    for (int e = t; e < 49 * n; e += 256) L.info[49 * o + e] = G.info[49 * (o + lm[e / 49]) + e % 49];
+    for (int k = t; k < n; k += 256) D.g2l[o + lm[k]] = k;
     if (t == 0) {
         lnmp[b] = n;
         stat(D, GF_ST_NLOCAL)[b] = n;
@@ -395,23 +451,13 @@ __global__ __launch_bounds__(256) void k_fe_gather(FeDev D, MapArrays G, MapArra
     }
 }
 
-// Scatter: the local map's observability state and visibility back to the
-// stream's map points, matches and mLeftMapPoints back to map indices.
-__global__ __launch_bounds__(256) void k_fe_scatter(FeDev D, MapArrays G, MapArrays L) {
+// Matches and mLeftMapPoints back to map indices, g2l reset.
+__global__ __launch_bounds__(256) void k_fe_scatter(FeDev D) {
     const int b = blockIdx.x, t = threadIdx.x;
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    for (int k = t; k < n; k += 256) {
-        const long long g = o + lm[k], l = o + k;
-        G.views[g] = L.views[l];
-        G.uv[2 * g] = L.uv[2 * l];
-        G.uv[2 * g + 1] = L.uv[2 * l + 1];
-        G.upd[g] = L.upd[l];
-        D.g2l[g] = -1;
-    }
-    for (int e = t; e < 14 * n; e += 256) G.H[14 * (o + lm[e / 14]) + e % 14] = L.H[14 * o + e];
-    for (int e = t; e < 49 * n; e += 256) G.info[49 * (o + lm[e / 49]) + e % 49] = L.info[49 * o + e];
+    for (int k = t; k < n; k += 256) D.g2l[o + lm[k]] = -1;
     const long long ko = (long long)b * D.cap;
     const int nk = D.nkp[b];
     for (int i = t; i < nk; i += 256) {
@@ -558,22 +604,30 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_discard_outliers_dev(ctx, B, D.kp2mp, D.outl, D.nkp, cap, D.budget, col(GF_ST_FOUND),
                                   col(GF_ST_TO_MATCH), s));
     const MapArrays WM{D.map, fe->wdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
+    // keyframe graphs: H / ObsMat / u_proj stay in map order (the local map's
+    // point q is map point lmp[q]); the other per-point arrays are gathered
+    const int32_t* rmp = D.refmap ? D.lmp : nullptr;
     if (D.refmap) {
         // TrackLocalMap -> UpdateReference (Tracking.cc:2745, 3689-3852): local
         // keyframes and mvpLocalMapPoints from this frame's matches
         FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp, cap, fe->lkf, fe->nlkf,
                                           gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
+        {
+            GF_PROF(ctx, s, "k_fe_gather_rows");
+            k_fe_gather_rows<<<dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s>>>(D, fe->gm, WM);
+            GF_HIP(hipGetLastError());
+        }
         GF_PROF(ctx, s, "k_fe_gather");
-        k_fe_gather<<<B, 256, 0, s>>>(D, fe->gm, WM, fe->w_nmp);
+        k_fe_gather<<<B, 256, 0, s>>>(D, fe->w_nmp);
         GF_HIP(hipGetLastError());
     }
     // TrackLocalMap -> SearchReferencePointsInFrustum
     if (D.gf) {
         FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, s));
-        FE_RC(gf_obs_frame_info_dev(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp, cap, D.kp2mp, D.outl, fe->mp_pos, D.nmp,
-                                    M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, s));
-        FE_RC(gf_obs_accumulate_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
-                                            fe->base, s));
+        FE_RC(gf::obs_frame_info(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp, cap, D.kp2mp, D.outl, fe->mp_pos, D.nmp,
+                                 M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, rmp, s));
+        FE_RC(gf::obs_accumulate_matched(ctx, B, D.kp2mp, D.nkp, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
+                                         fe->base, rmp, s));
     }
     FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
     {
@@ -589,13 +643,12 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         GF_HIP(hipGetLastError());
     }
     if (D.gf) {
-        FE_RC(gf_obs_map_info_dev(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
-                                  fe->mp_info, fe->mp_uv, fe->mp_updated, s));
-        FE_RC(gf_obs_active_match_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
-                                      fe->mp_info,
-                                      fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2, col(GF_ST_TO_MATCH), 1.f,
-                                      0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score, D.left, D.nleft,
-                                      col(GF_ST_LOCAL), col(GF_ST_LDETS), s));
+        FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
+                               fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s));
+        FE_RC(gf::obs_active_match(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
+                                   fe->mp_info, fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2,
+                                   col(GF_ST_TO_MATCH), 1.f, 0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score,
+                                   D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s));
     }
     FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, 1.f, 0.8f,
                                D.kp2mp, D.score, D.nm2, s));
@@ -610,8 +663,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.gf) {
         // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz)
         FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, s));
-        FE_RC(gf_obs_map_info_dev(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
-                                  fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, s));
+        FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
+                               fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, s));
         // SearchAdditionalMatchesInFrame
         FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview, s));
         {
@@ -623,8 +676,13 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                         0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA), s));
     }
     if (D.refmap) {
+        {
+            GF_PROF(ctx, s, "k_fe_scatter_rows");
+            k_fe_scatter_rows<<<dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s>>>(D, fe->gm, WM);
+            GF_HIP(hipGetLastError());
+        }
         GF_PROF(ctx, s, "k_fe_scatter");
-        k_fe_scatter<<<B, 256, 0, s>>>(D, fe->gm, WM);
+        k_fe_scatter<<<B, 256, 0, s>>>(D);
         GF_HIP(hipGetLastError());
     }
     {
@@ -856,9 +914,6 @@ static int fe_enable_covis(gf_frontend* fe) {
     A_(32 * B * M, wdesc);
     A_(12 * B * M, fe->mp_pos);
     A_(sizeof(gf_mp_view) * B * M, D.views);
-    A_(8 * 14 * B * M, fe->mp_H);
-    A_(8 * 49 * B * M, fe->mp_info);
-    A_(8 * B * M, fe->mp_uv);
     A_(4 * B * M, D.upd);
     A_(4 * B, fe->w_nmp);
     A_(4 * B * M, D.lmp);

@@ -275,6 +275,7 @@ struct ActiveArgs {
     int32_t* nleft;
     int32_t* nmatched;
     int32_t* nldet;  // [F] logDet evaluations (optional)
+    const int32_t* remap;  // [F][mp_cap] map index of local point q for info / H (null: q itself)
     int32_t* err;
     const struct OnePre* pre;  // [F][mp_cap] one-point results against the starting claims
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
@@ -597,12 +598,12 @@ __device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst&
 
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
-                           const int* cell_start, const int* items, const int* claim, const gf_keypoint* K,
-                           const uint8_t* D) {
+                           const int32_t* rmp, const int* cell_start, const int* items, const int* claim,
+                           const gf_keypoint* K, const uint8_t* D) {
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
-        C.score[c] = logdet_sum(cur, info + 49LL * q, 1.0);
+        C.score[c] = logdet_sum(cur, info + 49LL * (rmp ? rmp[q] : q), 1.0);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
@@ -953,6 +954,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     int last_npop = 0;
     const double* info = A.info + (long long)f * A.mp_cap * 49;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
+    const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
 
     for (int round = 0; round < num_to_match; ++round) {
         const int sz = min(S, N);
@@ -1017,7 +1019,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, rmp, cell_start, items, claim, K, D);
         evald = nc;
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
@@ -1046,7 +1048,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             }
             if (rep < nc && rep >= evald) {
                 AM_T(4);
-                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, rmp, cell_start, items, claim, K, D);
                 evald = nc;
                 AM_T(3);
             }
@@ -1201,7 +1203,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
         int oct_b = 0;
         if (!exh && lane < 49) {
-            const double* Hq = Hm + 14LL * lmk[C.slot[top]];
+            const int qt = lmk[C.slot[top]];
+            const double* Hq = Hm + 14LL * (rmp ? rmp[qt] : qt);
             const int i = lane / 7, jj = lane % 7;
             h_i = Hq[i];
             h_j = Hq[jj];
@@ -1491,6 +1494,20 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
                             const float* level_sigma2, const int32_t* d_num_to_match, float th, float nnratio,
                             gf_rng* d_rng, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_left, int32_t* d_nleft,
                             int32_t* d_nmatched, int32_t* d_nldet, void* stream) {
+    return gf::obs_active_match(ctx, fi, nframes, d_kps, d_desc, d_n, kp_cap, d_views, d_mp_desc, d_updated, d_info,
+                                d_H, d_m, mp_cap, d_base, level_sigma2, d_num_to_match, th, nnratio, d_rng, d_kp2mp,
+                                d_score, d_left, d_nleft, d_nmatched, d_nldet, nullptr, stream);
+}
+
+}  // extern "C"
+
+int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                         const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                         const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info, const double* d_H,
+                         const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
+                         const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
+                         int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
+                         const int32_t* d_remap, void* stream) {
     GF_CHECK(ctx && fi && level_sigma2, GF_ERR_ARG, "null arg");
     GF_CHECK(kp_cap <= KP_MAX && mp_cap <= 32767, GF_ERR_UNSUPPORTED, "frame exceeds active-matching limits");
     GF_CHECK(fi->nlevels >= 1 && fi->nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
@@ -1521,6 +1538,7 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
     A.nleft = d_nleft;
     A.nmatched = d_nmatched;
     A.nldet = d_nldet;
+    A.remap = d_remap;
     void* err;
     int rc = gf::ws_get(ctx, 30, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
@@ -1565,6 +1583,8 @@ int gf_obs_active_match_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, c
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
+
+extern "C" {
 
 int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const double* d_score, const int32_t* d_n,
                          int cap, int k, double sample_scale, int mode, gf_rng* d_rng, int32_t* d_out,
@@ -1825,7 +1845,8 @@ __global__ void k_obs_frame_info(gf_obs_camera cam, const double* __restrict__ X
                                  const int32_t* __restrict__ nkps, int kp_stride, const int32_t* __restrict__ kp2mp,
                                  const uint8_t* __restrict__ outl, const float* __restrict__ mpos,
                                  const int32_t* __restrict__ nmp, int map_stride, LevelTab sig, int nlevels,
-                                 double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv) {
+                                 double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
+                                 const int32_t* __restrict__ remap) {
     const int f = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nkps[f]) return;
@@ -1841,10 +1862,11 @@ __global__ void k_obs_frame_info(gf_obs_camera cam, const double* __restrict__ X
     double M[49];
     for (int e = 0; e < 49; e++) M[e] = 0;
     add_info_block(H, (double)sig.v[oc], M);
-    uv[2 * g] = p[0];
-    uv[2 * g + 1] = p[1];
-    for (int e = 0; e < 14; e++) Hout[14 * g + e] = H[e];
-    for (int e = 0; e < 49; e++) info[49 * g + e] = M[e];
+    const long long w = remap ? (long long)f * map_stride + remap[g] : g;
+    uv[2 * w] = p[0];
+    uv[2 * w + 1] = p[1];
+    for (int e = 0; e < 14; e++) Hout[14 * w + e] = H[e];
+    for (int e = 0; e < 49; e++) info[49 * w + e] = M[e];
 }
 
 // batchInfoMat_Map (Observability.cc:556-644): skip points already updated
@@ -1855,7 +1877,7 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
                                const int32_t* __restrict__ nmp, int map_stride, int check_viz,
                                const gf_mp_view* __restrict__ views, int32_t* __restrict__ upd_id, int frame_id,
                                double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
-                               uint8_t* __restrict__ updated_out) {
+                               uint8_t* __restrict__ updated_out, const int32_t* __restrict__ remap) {
     const int f = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= map_stride) return;
@@ -1874,10 +1896,11 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
             double M[49];
             for (int e = 0; e < 49; e++) M[e] = 0;
             add_info_block(H, 1.0, M);
-            uv[2 * g] = p[0];
-            uv[2 * g + 1] = p[1];
-            for (int e = 0; e < 14; e++) Hout[14 * g + e] = H[e];
-            for (int e = 0; e < 49; e++) info[49 * g + e] = M[e];
+            const long long w = remap ? (long long)f * map_stride + remap[g] : g;
+            uv[2 * w] = p[0];
+            uv[2 * w + 1] = p[1];
+            for (int e = 0; e < 14; e++) Hout[14 * w + e] = H[e];
+            for (int e = 0; e < 49; e++) info[49 * w + e] = M[e];
             u = frame_id;
             upd_id[g] = u;
         }
@@ -1892,7 +1915,8 @@ __global__ __launch_bounds__(64) void k_obs_accumulate_matched(const int32_t* __
                                                                const double* __restrict__ info,
                                                                const int32_t* __restrict__ upd_id,
                                                                const int32_t* __restrict__ nmp, int map_stride,
-                                                               int frame_id, double diag, double* __restrict__ out) {
+                                                               int frame_id, double diag, double* __restrict__ out,
+                                                               const int32_t* __restrict__ remap) {
     __shared__ int list[KP_MAX];
     const int f = blockIdx.x, lane = threadIdx.x;
     const int n = min(nkps[f], KP_MAX), m = nmp[f];
@@ -1903,7 +1927,8 @@ __global__ __launch_bounds__(64) void k_obs_accumulate_matched(const int32_t* __
         int mp = i < n ? kp2mp[(long long)f * kp_stride + i] : -1;
         const bool on = mp >= 0 && mp < m && upd_id[(long long)f * map_stride + mp] == frame_id;
         const unsigned long long msk = __ballot(on);
-        if (on) list[cnt + __popcll(msk & ((1ull << lane) - 1ull))] = mp;
+        if (on)
+            list[cnt + __popcll(msk & ((1ull << lane) - 1ull))] = remap ? remap[(long long)f * map_stride + mp] : mp;
         cnt += __popcll(msk);
     }
     __syncthreads();
@@ -1927,13 +1952,11 @@ __global__ __launch_bounds__(64) void k_obs_accumulate_matched(const int32_t* __
 
 }  // namespace
 
-extern "C" {
-
-int gf_obs_frame_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv,
-                          const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
-                          const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
-                          const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
-                          void* stream) {
+int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv,
+                       const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
+                       const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
+                       const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
+                       const int32_t* d_remap, void* stream) {
     GF_CHECK(ctx && cam && level_sigma2, GF_ERR_ARG, "null arg");
     if (nframes <= 0 || kp_stride <= 0) return GF_OK;
     GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
@@ -1945,38 +1968,66 @@ int gf_obs_frame_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, co
     GF_PROF(ctx, s, "k_obs_frame_info");
     k_obs_frame_info<<<dim3((kp_stride + 127) / 128, nframes), 128, 0, s>>>(
         *cam, d_Xv, d_kps, d_nkps, kp_stride, d_kp2mp, d_outlier, d_map_pos, d_nmp, map_stride, t, nlevels, d_H,
-        d_info, d_uv);
+        d_info, d_uv, d_remap);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
 
-int gf_obs_map_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
-                        const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
-                        int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv,
-                        uint8_t* d_updated, void* stream) {
+int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
+                     const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
+                     int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated,
+                     const int32_t* d_remap, void* stream) {
     GF_CHECK(ctx && cam, GF_ERR_ARG, "null arg");
     if (nframes <= 0 || map_stride <= 0) return GF_OK;
     GF_CHECK(d_Xv && d_map_pos && d_nmp && d_upd_id && d_H && d_info && d_uv, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_map_info");
     k_obs_map_info<<<dim3((map_stride + 127) / 128, nframes), 128, 0, s>>>(
-        *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated);
+        *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated,
+        d_remap);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
 
-int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
-                                  int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
-                                  int map_stride, int frame_id, double diag, double* d_out, void* stream) {
+int gf::obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
+                               int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
+                               int map_stride, int frame_id, double diag, double* d_out, const int32_t* d_remap,
+                               void* stream) {
     GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
     if (nframes <= 0) return GF_OK;
     GF_CHECK(d_kp2mp && d_nkps && d_info && d_upd_id && d_nmp && d_out, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_accumulate");
     k_obs_accumulate_matched<<<nframes, 64, 0, s>>>(d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
-                                                    frame_id, diag, d_out);
+                                                    frame_id, diag, d_out, d_remap);
     GF_HIP(hipGetLastError());
     return GF_OK;
+}
+
+extern "C" {
+
+int gf_obs_frame_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv,
+                          const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
+                          const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
+                          const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
+                          void* stream) {
+    return gf::obs_frame_info(ctx, cam, nframes, d_Xv, d_kps, d_nkps, kp_stride, d_kp2mp, d_outlier, d_map_pos, d_nmp,
+                              map_stride, level_sigma2, nlevels, d_H, d_info, d_uv, nullptr, stream);
+}
+
+int gf_obs_map_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
+                        const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
+                        int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv,
+                        uint8_t* d_updated, void* stream) {
+    return gf::obs_map_info(ctx, cam, nframes, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id,
+                            frame_id, d_H, d_info, d_uv, d_updated, nullptr, stream);
+}
+
+int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
+                                  int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
+                                  int map_stride, int frame_id, double diag, double* d_out, void* stream) {
+    return gf::obs_accumulate_matched(ctx, nframes, d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
+                                      frame_id, diag, d_out, nullptr, stream);
 }
 
 }  // extern "C"

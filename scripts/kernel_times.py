@@ -1,7 +1,8 @@
 """Per-kernel device time of one front-end group alone (no overlapping
 groups): B sequences of the bench workload, HIP events per launch.
-Usage: python scripts/kernel_times.py [B] [steps] [stale]  (stale map-descriptor
-fraction, default 0.93: the bench's config-2 regime)"""
+Usage: python scripts/kernel_times.py [B] [steps] [stale] [fixed]  (stale
+map-descriptor fraction, default 0.82 with keyframe maps + UpdateReference as
+the bench runs them, 0.93 with fixed local maps when `fixed` is given)"""
 import json
 import os
 import sys
@@ -15,14 +16,22 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-stale = float(sys.argv[3]) if len(sys.argv) > 3 else 0.93
+fixed = len(sys.argv) > 4 and sys.argv[4] == "fixed"
+stale = float(sys.argv[3]) if len(sys.argv) > 3 else (0.93 if fixed else 0.82)
 W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=stale)
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
-maps = W.build_maps(lambda im: ex(im), 2000, device="cuda")
-fe = FrontEnd("euroc", 1000, B, 2000, 100)
+M = 2000 if fixed else 2100
+if fixed:
+    maps = [(m[0], m[1]) for m in W.build_maps(lambda im: ex(im), M, device="cuda")]
+else:
+    maps = [(g["mp"], g["desc"], g["graph"]) for g in W.build_global_maps(lambda im: ex(im), M, device="cuda")]
+fe = FrontEnd("euroc", 1000, B, M, 100)
 for b in range(B):
-    fe.set_map(b, *maps[W.scene_of[b]])
+    m = maps[W.scene_of[b]]
+    fe.set_map(b, m[0], m[1])
+    if len(m) > 2:
+        fe.set_covis(b, m[2])
     fe.set_rng(b, 1 + b)
 fe.set_source(frames, W.scene_of, W.phase)
 T, V = W.boot_state()

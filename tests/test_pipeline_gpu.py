@@ -230,23 +230,26 @@ def test_budgets_match_oracle(match_s, select_s):
 def test_bench_shape_parity():
     """The timed configuration itself: 1024 streams in 2 groups of 512 (as
     bench.py runs them, each group on its own context / HIP stream, launches
-    interleaved, extraction stages chained by gf_frontend_set_gate), streams
-    {0, 255, 511} of each group checked for 2 steps."""
+    interleaved, extraction stages chained by gf_frontend_set_gate, keyframe
+    maps of 2100 points with UpdateReference every frame), streams {0, 255,
+    511} of each group checked for 2 steps."""
     import torch
 
     from gf_orb_slam_amd.pipeline import FrontEnd, chain_extraction
 
-    G, Bg = 2, 512
-    W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5, stale_desc=0.93)
+    G, Bg, M = 2, 512, 2100
+    W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5, stale_desc=0.82)
     frames = W.render_all("cuda").contiguous()
-    maps = W.build_maps(lambda im: O.extract(im), 2000)
+    gmaps = W.build_global_maps(lambda im: O.extract(im), M)
     T, V = W.boot_state()
     fes = []
     for g in range(G):
         sl = slice(g * Bg, (g + 1) * Bg)
-        fe = FrontEnd("euroc", 1000, Bg, 2000, 100)
+        fe = FrontEnd("euroc", 1000, Bg, M, 100)
         for b in range(Bg):
-            fe.set_map(b, *maps[W.scene_of[g * Bg + b]])
+            gm = gmaps[W.scene_of[g * Bg + b]]
+            fe.set_map(b, gm["mp"], gm["desc"])
+            fe.set_covis(b, gm["graph"])
             fe.set_rng(b, 1 + g * Bg + b)
         fe.set_source(frames, W.scene_of[sl], W.phase[sl])
         fe.bootstrap(T[sl], V[sl], 0.0)
@@ -263,15 +266,57 @@ def test_bench_shape_parity():
         for g, fe in enumerate(fes):
             dev = C.read_state(fe)
             for b in check:
-                ch = C.Chain("euroc", 1000, 2000, 100)
+                ch = C.Chain("euroc", 1000, M, 100)
                 ch.load_from(states[g], b)
+                ch.set_covis(gmaps[W.scene_of[g * Bg + b]]["graph"])
                 ch.step(_img(W, fr, g * Bg + b, k))
                 _compare(dev, ch, b, f"group {g} step {k}: ")
             if k == 2:  # the timed regime: active matching on most streams
                 assert (dev["stats"][3] == 3).mean() >= 0.8
+                nl = dev["stats"][C.STATS.index("nlocal")]
+                assert (nl > 1500).all() and (nl <= M).all() and len(np.unique(nl)) > 1, nl
             states[g] = dev
     for fe in fes:
         fe.close()
+
+
+@pytest.mark.gpu
+def test_graph_replay_equals_eager_with_update_reference():
+    """A captured step with keyframe graphs (UpdateReference, local-map
+    gather / scatter inside the graph) replays to the eager state."""
+    import torch
+
+    from gf_orb_slam_amd.pipeline import FrontEnd
+
+    B, M = 3, 2100
+    W = scene.Workload("euroc", B, n_scenes=2, period=32, seed=6, stale_desc=0.82)
+    frames = W.render_all("cuda").contiguous()
+    gmaps = W.build_global_maps(lambda im: O.extract(im), M)
+    T, V = W.boot_state()
+    fes = []
+    for _ in range(2):
+        fe = FrontEnd("euroc", 1000, B, M, 100)
+        for b in range(B):
+            gm = gmaps[W.scene_of[b]]
+            fe.set_map(b, gm["mp"], gm["desc"])
+            fe.set_covis(b, gm["graph"])
+            fe.set_rng(b, 11 + b)
+        fe.set_source(frames, W.scene_of, W.phase)
+        fe.bootstrap(T, V, 0.0)
+        fes.append(fe)
+    fe, fe2 = fes
+    fe2.step()
+    fe2.capture_graph()
+    fe.step()
+    for _ in range(4):
+        fe.step()
+        fe2.step()
+    torch.cuda.synchronize()
+    a, b = C.read_state(fe), C.read_state(fe2)
+    for k in ("kp2mp", "Tcw", "mp_info", "rng", "views", "stats", "map"):
+        assert np.array_equal(a[k], b[k]), k
+    for f in fes:
+        f.close()
 
 
 @pytest.mark.gpu
