@@ -277,6 +277,10 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 #endif
 #define BT_R (BT_H + 6)   // source rows
 #define BT_SW (BT_W + 8)  // source row: 72 bytes = 18 dwords, x = X0 - 4 .. X0 + 67
+// LDS pitch of a source row: 24 dwords, so rows two apart (the two 16-lane
+// halves of a ds_read_b32 group in the row and compass passes) sit 16 banks
+// apart (mod 32): conflict-free, where the 18-dword pitch made them 2-way
+#define BT_SP 96
 #define BT_NQ (BT_H / 32) // row blocks of 32 per thread (quad x 2 rows each)
 #define BT_U32 ((BT_R / 2) * BT_W > BT_W * BT_H / 2 ? (BT_R / 2) * BT_W : BT_W * BT_H / 2)
 
@@ -303,7 +307,7 @@ __device__ __forceinline__ uint32_t bytes02(uint32_t w) { return __builtin_amdgc
 __device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
-    __shared__ __align__(16) uint8_t src[BT_R][BT_SW];
+    __shared__ __align__(16) uint8_t src[BT_R][BT_SP];
     // the row sums (rows 2p | 2p+1 << 16) are dead once the column pass has
     // read them; the candidate list, written after the scan's barriers, reuses them
     __shared__ __align__(16) uint32_t u32buf[BT_U32];
@@ -359,10 +363,11 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
                 }
             }
         }
-        uint32_t* s32 = reinterpret_cast<uint32_t*>(&src[0][0]) + lr * NQD + lq;
+        uint32_t* s32 = reinterpret_cast<uint32_t*>(&src[0][0]) + lr * (BT_SP / 4) + lq;
 #pragma unroll
         for (int k = 0; k < NI; k++)
-            if (lr < LR && lr + LR * k < BT_R) s32[LR * NQD * k] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            if (lr < LR && lr + LR * k < BT_R)
+                s32[LR * (BT_SP / 4) * k] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
     }
     __syncthreads();
     // taps round(256 * gaussian(7, sigma 2)) = 18 34 49 55 49 34 18
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     for (int i = tid; i < nc; i += 256) {
         const int q = cand[i], py = q >> 6, px = q & 63;
         int c[16];
-        circle_vals(&src[0][0], BT_SW, px + 4, py + 3, c);
+        circle_vals(&src[0][0], BT_SP, px + 4, py + 3, c);
         const int M = fast_max_arc(src[py + 3][px + 4], c);  // corner iff M > th; map entry S + 1 = M
         sc8[q] = M > map_th ? (uint8_t)M : 0;
     }
