@@ -369,6 +369,9 @@ def main():
                     help="stream groups per GPU, each a front end on its own HIP stream (their kernels overlap)")
     ap.add_argument("--no-gate", action="store_true",
                     help="let the groups' extraction stages overlap (default: chained, one at a time)")
+    ap.add_argument("--track-priority", action="store_true",
+                    help="each group's tracking kernels on a high-priority stream of their own "
+                         "(gf_frontend_set_track_priority; measured slower on MI355X: 70k vs 89k frames/s)")
     ap.add_argument("--camera", default="euroc")
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--gf-budget", type=int, default=100)
@@ -466,6 +469,9 @@ def main():
         fe.bootstrap(T[sl], V[sl], 0.0)
         fes.append(fe)
     gates = [] if args.no_gate else chain_extraction(fes)
+    if args.track_priority and G > 1:
+        for fe in fes:
+            fe.set_track_priority(-100)  # the device's most urgent priority
     map_span = gd.gather_ints(map_cks)
     torch.cuda.synchronize()
     t_su = time.perf_counter() - t_su
@@ -622,6 +628,7 @@ def main():
                                f"motion update, next-frame MAP_INFO prediction, SearchAdditionalMatchesInFrame",
                    "sequences_per_gpu": B, "stream_groups": G, "update_reference": refmap,
                    "extraction_gate": bool(gates),
+                   "tracking_stream_priority": bool(args.track_priority and G > 1),
                    "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
         "startup": startup,
         "roofline": roof,

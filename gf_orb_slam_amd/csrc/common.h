@@ -123,6 +123,15 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
     bx = lid - by * (int)gridDim.x;
 }
 
+// A load through the global address space: global_load_* (counted by vmcnt
+// only) where a generic pointer compiles to flat_load_*, which also counts
+// against lgkmcnt, so the LDS waits of the kernel wait for it too. For
+// device memory only (hipMalloc'd buffers, as all of this library's inputs).
+template <typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+    return *(const __attribute__((address_space(1))) T*)p;
+}
+
 __device__ __forceinline__ int reflect101(int p, int len) {
     // BORDER_REFLECT_101 for the <= 18 px excursions the kernels make.
     if (p < 0) p = -p;

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, co
             if (r < nrows) {
                 const uintptr_t a = (uintptr_t)(S + (long long)(rs + r) * sstride + cs);
                 if (4 * q < (int)(a & 3) + span)  // only dwords that hold a needed byte
-                    v[k] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+                    v[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
             }
         }
 #pragma unroll
@@ -330,44 +330,46 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     {
         // BT_R rows x 18 dwords. Thread (lr, lq) = (tid / 18, tid % 18) owns
         // dword column lq of rows lr, lr + 14, ... (252 threads, 14 rows a
-        // sweep), so its x range, border test and LDS column are fixed. Rows
-        // reflect-101 at the top and bottom (a uniform test per tile). A dword
-        // inside the level row comes as two aligned loads realigned with
-        // v_alignbyte (the level rows are unpadded, so the byte shift varies
-        // by row); the x-border ones byte by byte through reflect-101.
+        // sweep), so its x range and LDS column are fixed. Rows reflect-101 at
+        // the top and bottom (a uniform test per tile); the level rows are
+        // unpadded, so the byte shift varies by row.
         constexpr int NQD = BT_SW / 4, LR = 256 / NQD, NI = (BT_R + LR - 1) / LR;
         const int lr = tid / NQD, lq = tid - lr * NQD;
         const int x0 = X0 - 4 + 4 * lq;
-        const bool xin = x0 >= 0 && x0 + 8 <= w;
         const bool yin = Y0 >= 3 && Y0 + BT_R - 3 <= h;
-        uint32_t lo[NI], hi[NI];
-        int sh[NI];
+        // Every lane loads the two aligned dwords holding its four source bytes
+        // and picks them with one v_perm_b32: inside the row the bytes are
+        // consecutive (the selector is the address's byte shift), at the x
+        // borders they are reflect-101 positions, which span at most 4 bytes
+        // (selector offsets <= 6 from the aligned base). No branch, so all the
+        // stage's loads are in flight together. An aligned dword holding a
+        // byte of the row never crosses a page; the second dword is taken
+        // only when a byte lies in it.
+        uint32_t lo[NI], hi[NI], sel[NI];
+        int pj[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) pj[j] = gfd::reflect101(min(x0 + j, w + 2), w);
+        const int pmin = min(min(pj[0], pj[1]), min(pj[2], pj[3]));
 #pragma unroll
         for (int k = 0; k < NI; k++) {
             const int ry = lr + LR * k;
-            lo[k] = hi[k] = 0u;
-            sh[k] = 0;
+            lo[k] = hi[k] = sel[k] = 0u;
             if (lr < LR && ry < BT_R) {
                 const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                const uint8_t* row = S + (long long)yy * stride;
-                if (xin) {
-                    const uintptr_t a = (uintptr_t)(row + x0);
-                    const uint32_t* al = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-                    sh[k] = (int)(a & 3);
-                    lo[k] = al[0];
-                    hi[k] = al[1];  // bytes x0 + 4 .. x0 + 7 lie inside the row
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++)
-                        lo[k] |= (uint32_t)row[gfd::reflect101(min(x0 + j, w + 2), w)] << (8 * j);
-                }
+                const uintptr_t row = (uintptr_t)(S + (long long)yy * stride);
+                const uintptr_t base = (row + pmin) & ~(uintptr_t)3;
+                const int o0 = (int)(row + pj[0] - base), o1 = (int)(row + pj[1] - base);
+                const int o2 = (int)(row + pj[2] - base), o3 = (int)(row + pj[3] - base);
+                const bool two = max(max(o0, o1), max(o2, o3)) >= 4;
+                sel[k] = (uint32_t)o0 | (uint32_t)o1 << 8 | (uint32_t)o2 << 16 | (uint32_t)o3 << 24;
+                lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(base));
+                hi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(two ? base + 4 : base));
             }
         }
         uint32_t* s32 = reinterpret_cast<uint32_t*>(&src[0][0]) + lr * (BT_SP / 4) + lq;
 #pragma unroll
         for (int k = 0; k < NI; k++)
-            if (lr < LR && lr + LR * k < BT_R)
-                s32[LR * (BT_SP / 4) * k] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+            if (lr < LR && lr + LR * k < BT_R) s32[LR * (BT_SP / 4) * k] = __builtin_amdgcn_perm(hi[k], lo[k], sel[k]);
     }
     __syncthreads();
     // taps round(256 * gaussian(7, sigma 2)) = 18 34 49 55 49 34 18
@@ -454,6 +456,9 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
             const uint32_t e = compass2(bytes02(V), bytes02(Dn), bytes02(Rt), bytes02(U), bytes02(Lt), th2);
             const uint32_t o = compass2(bytes13(V), bytes13(Dn), bytes13(Rt), bytes13(U), bytes13(Lt), th2);
             uint32_t m = ((e >> 15) & 1u) | ((o >> 14) & 2u) | ((e >> 29) & 4u) | ((o >> 28) & 8u);
+#if defined(GF_BLUR_EXP) && GF_BLUR_EXP == 2
+            m &= (uint32_t)(V == 0x12345678u);
+#endif
             const int y = Y0 + r0 + r;
             m &= (y >= 3 && y < h - 3) ? xm : 0u;
             mask |= (int)m << (8 * k + 4 * r);
@@ -469,7 +474,11 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     }
     __syncthreads();
     uint8_t* sc8 = reinterpret_cast<uint8_t*>(&sco[0][0]);
+#if defined(GF_BLUR_EXP) && GF_BLUR_EXP == 1
+    for (int i = tid; i < 0; i += 256) {
+#else
     for (int i = tid; i < nc; i += 256) {
+#endif
         const int q = cand[i], py = q >> 6, px = q & 63;
         int c[16];
         circle_vals(&src[0][0], BT_SP, px + 4, py + 3, c);
@@ -592,7 +601,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
             v[k] = 0;
             if (r < dh) {
                 const uintptr_t a = (uintptr_t)(SC + (long long)r * lw);
-                if (4 * q < (int)(a & 3) + dw) v[k] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+                if (4 * q < (int)(a & 3) + dw) v[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
             }
         }
 #pragma unroll
@@ -617,7 +626,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
         const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
         for (int i = tid; i < ci.w * ci.h; i += 256) {
             const int r = i / ci.w;
-            roi[i] = Sl[(long long)r * sstride + (i - r * ci.w)];
+            roi[i] = gfd::ldg(Sl + (long long)r * sstride + (i - r * ci.w));
         }
         __syncthreads();
         for (int i = tid; i < n; i += 256) {
@@ -988,11 +997,11 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             if (live && i < DS_IC * DS_ICW) {
                 const int r = i / DS_ICW, q = i - r * DS_ICW;
                 const uintptr_t a = (uintptr_t)(Pl + (long long)(y - 15 + r) * stride + x - 15);
-                v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+                v[t] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
             } else if (win && i >= DS_IC * DS_ICW && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
                 const int j = i - DS_IC * DS_ICW, r = j / DS_BLW, q = j - r * DS_BLW;
                 const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * pwl + x - 18);
-                v[t] = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3)[q];
+                v[t] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
             }
         }
 #pragma unroll
@@ -1054,7 +1063,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                     const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
                     t[q] = !live ? 0
                            : inside ? B[(long long)yy * pwl + xx]
-                                    : Pl[(long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w)];
+                                    : gfd::ldg(Pl + (long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w));
                 }
             }
             val |= (t[0] < t[1]) << bit;

@@ -530,6 +530,10 @@ struct gf_frontend {
     bool sourced = false;
     // extraction gate (gf_frontend_set_gate): caller-owned events
     hipEvent_t gate_wait = nullptr, gate_done = nullptr;
+    // tracking stream (gf_frontend_set_track_priority): the kernels after
+    // extraction run on ts, joined back into the context's stream at the end
+    hipStream_t ts = nullptr;
+    hipEvent_t ev_extracted = nullptr, ev_tracked = nullptr;
 };
 
 namespace {
@@ -594,6 +598,12 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
     if (fe->gate_done) GF_HIP(hipEventRecord(fe->gate_done, s));
+    const hipStream_t s_ctx = s;
+    if (fe->ts) {  // fork: tracking on the prioritised stream
+        GF_HIP(hipEventRecord(fe->ev_extracted, s));
+        GF_HIP(hipStreamWaitEvent(fe->ts, fe->ev_extracted, 0));
+        s = fe->ts;
+    }
     // TrackWithMotionModel
     FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
                                  D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp, D.score,
@@ -689,6 +699,10 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         GF_PROF(ctx, s, "k_fe_end");
         k_fe_end<<<B, 256, 0, s>>>(D);
         GF_HIP(hipGetLastError());
+    }
+    if (fe->ts) {  // join: the context's stream sees the whole step
+        GF_HIP(hipEventRecord(fe->ev_tracked, s));
+        GF_HIP(hipStreamWaitEvent(s_ctx, fe->ev_tracked, 0));
     }
     return GF_OK;
 }
@@ -850,6 +864,12 @@ int gf_frontend_destroy(gf_frontend* fe) {
     if (!fe) return GF_OK;
     (void)hipSetDevice(fe->ctx->device);
     (void)hipStreamSynchronize(fe->ctx->stream);
+    if (fe->ts) {
+        (void)hipStreamSynchronize(fe->ts);
+        (void)hipEventDestroy(fe->ev_extracted);
+        (void)hipEventDestroy(fe->ev_tracked);
+        (void)hipStreamDestroy(fe->ts);
+    }
     fe_free(fe);
     delete fe;
     return GF_OK;
@@ -1101,6 +1121,21 @@ int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
     return GF_OK;
 }
 
+int gf_frontend_set_track_priority(gf_frontend* fe, int priority) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot change streams");
+    GF_CHECK(!fe->ts, GF_ERR_ARG, "the tracking stream is already set");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    int least = 0, greatest = 0;
+    GF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const int pr = std::max(std::min(priority, least), greatest);  // lower value = higher priority
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    GF_HIP(hipStreamCreateWithPriority(&fe->ts, hipStreamNonBlocking, pr));
+    GF_HIP(hipEventCreateWithFlags(&fe->ev_extracted, hipEventDisableTiming));
+    GF_HIP(hipEventCreateWithFlags(&fe->ev_tracked, hipEventDisableTiming));
+    return GF_OK;
+}
+
 static int fe_check_covis(gf_frontend* fe) {
     if (!fe->covis_set) return GF_OK;
     for (int b = 0; b < fe->D.B; b++)
@@ -1155,6 +1190,7 @@ int gf_frontend_capture(gf_frontend* fe) {
     // a recorded event in a graph is not the caller's event at replay: the
     // extraction gate would silently stop gating
     GF_CHECK(!fe->gate_wait && !fe->gate_done, GF_ERR_ARG, "a gated front end cannot be captured as a graph");
+    GF_CHECK(!fe->ts, GF_ERR_ARG, "a front end with a tracking stream cannot be captured as a graph");
     GF_HIP(hipSetDevice(fe->ctx->device));
     hipStream_t s = fe->ctx->stream;
     GF_HIP(hipStreamSynchronize(s));

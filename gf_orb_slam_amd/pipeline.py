@@ -209,6 +209,11 @@ class FrontEnd:
         check(lib().gf_frontend_set_gate(self.handle, wait_event.handle if wait_event else None,
                                          done_event.handle if done_event else None))
 
+    def set_track_priority(self, priority: int = -1) -> None:
+        """gf_frontend_set_track_priority: tracking kernels on a stream of HIP
+        priority `priority` (lower = more urgent)."""
+        check(lib().gf_frontend_set_track_priority(self.handle, priority))
+
     def sync(self) -> None:
         check(lib().gf_frontend_sync(self.handle))
 

@@ -862,6 +862,14 @@ typedef struct gf_frontend gf_frontend;
 // A gated front end cannot be captured as a graph (gf_frontend_capture
 // refuses), nor can a captured one be gated.
 int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event);
+// Tracking stream: the step's kernels after extraction run on a stream of
+// their own created with HIP stream priority `priority` (clamped to the
+// device's range; lower = more urgent), forked from and joined back into the
+// context's stream each step, so results and ordering are unchanged. With
+// several front ends on one GPU a high priority lets one front end's
+// latency-bound tracking kernels take compute units ahead of another's
+// extraction kernels. Once per front end; not with gf_frontend_capture.
+int gf_frontend_set_track_priority(gf_frontend* fe, int priority);
 // A hipEvent_t (timing disabled) on the context's device, for the gate.
 int gf_event_create(gf_ctx* ctx, void** event_out);
 int gf_event_destroy(void* event);

@@ -320,6 +320,33 @@ def test_graph_replay_equals_eager_with_update_reference():
 
 
 @pytest.mark.gpu
+def test_track_priority_stream_equals_default():
+    """gf_frontend_set_track_priority: tracking forked onto a high-priority
+    stream and joined back gives the same state as one stream, gated as the
+    bench runs it."""
+    from gf_orb_slam_amd.pipeline import chain_extraction
+
+    runs = []
+    for prio in (False, True):
+        fes = [_setup("euroc", 1000, 4, 2000, 100, stale=0.93, seed=8)[3] for _ in range(2)]
+        chain_extraction(fes)
+        if prio:
+            for fe in fes:
+                fe.set_track_priority(-100)
+        for _ in range(4):
+            for fe in fes:
+                fe.step()
+        for fe in fes:
+            fe.sync()
+        runs.append([C.read_state(fe) for fe in fes])
+        for fe in fes:
+            fe.close()
+    for a, b in zip(*runs):
+        for k in ("kp2mp", "Tcw", "mp_info", "rng", "views", "stats"):
+            assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.gpu
 def test_graph_replay_equals_eager():
     """gf_frontend_capture: a replayed step equals an eager one."""
     W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, 2000, 100)
