@@ -739,15 +739,13 @@ __device__ __forceinline__ double rl0(double v) {  // lane 0's value
     return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
 }
 
-__device__ __forceinline__ int dpp_next(int v) {  // lane i <- lane i + 1 (wave_shl:1)
-    return __builtin_amdgcn_update_dpp(v, v, 0x130, 0xf, 0xf, false);
-}
+// lane i <- lane i + 1 (lane 63 keeps its own). A cross-lane permute: the DPP
+// wavefront shifts (wave_shl) are gone from gfx90a on — the encoding still
+// assembles for gfx950 but moves nothing, so every neighbour compare saw a
+// tie and each round fell back to the heap replay.
+__device__ __forceinline__ int dpp_next(int v) { return __shfl_down(v, 1, 64); }
 
-__device__ __forceinline__ double dpp_next(double v) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)dpp_next((int)(uint32_t)b), hi = (uint32_t)dpp_next((int)(uint32_t)(b >> 32));
-    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
-}
+__device__ __forceinline__ double dpp_next(double v) { return __shfl_down(v, 1, 64); }
 
 // Heap top of the live candidates: the arg-max, unless the maximum is tied
 // or a score is NaN, when std::priority_queue's order is reproduced by
