@@ -228,7 +228,7 @@ def test_budgets_match_oracle(match_s, select_s):
 
 @pytest.mark.gpu
 def test_bench_shape_parity():
-    """The timed configuration itself: 1024 streams in 2 groups of 512 (as
+    """The timed configuration itself: 1024 streams in 4 groups of 256 (as
     bench.py runs them, each group on its own context / HIP stream, launches
     interleaved, extraction stages chained by gf_frontend_set_gate, keyframe
     maps of 2100 points with UpdateReference every frame), streams {0, 255,
@@ -237,7 +237,7 @@ def test_bench_shape_parity():
 
     from gf_orb_slam_amd.pipeline import FrontEnd, chain_extraction
 
-    G, Bg, M = 2, 512, 2100
+    G, Bg, M = 4, 256, 2100
     W = scene.Workload("euroc", G * Bg, n_scenes=8, period=32, seed=5, stale_desc=0.82)
     frames = W.render_all("cuda").contiguous()
     gmaps = W.build_global_maps(lambda im: O.extract(im), M)
