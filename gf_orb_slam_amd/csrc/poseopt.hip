@@ -1,17 +1,18 @@
 // Motion-only pose optimisation on gfx950.
 //
-// One 256-thread workgroup per problem (frame). Per-edge work — projection,
+// One wave (PO_T threads) per problem (frame). Per-edge work — projection,
 // error, Huber weight, the 2x6 pose Jacobian and its 27 contributions to the
-// lower triangle of H and to b — runs one edge per thread, 256 edges at a time
-// (a frame's ~200 matches in one pass); the reductions over edges keep the
-// reference's order: thread k owns accumulator k (21 lower H entries, 6 b
-// entries, robust chi2) and adds the per-edge terms staged in LDS in edge
-// order, exactly as g2o's sequential loop over _activeEdges
-// (sparse_optimizer.cpp:100-114, block_solver.hpp:502-562). The scalar LM
-// logic (lambda schedule, LDLT, exp update, stop rules) runs redundantly on
-// every thread from the shared sums, so no broadcast is needed. The problem
-// is latency-bound (one workgroup per frame, an ordered double-precision sum
-// chain per LM pass), so the edge work is spread over four waves.
+// lower triangle of H and to b — runs one edge per thread, PO_E edges per
+// pass; the reductions over edges keep the reference's order: thread k owns
+// accumulator k (21 lower H entries, 6 b entries, robust chi2) and adds the
+// per-edge terms staged in LDS in edge order, exactly as g2o's sequential
+// loop over _activeEdges (sparse_optimizer.cpp:100-114,
+// block_solver.hpp:502-562). The scalar LM logic (lambda schedule, LDLT, exp
+// update, stop rules) runs redundantly on every thread from the shared sums,
+// so no broadcast is needed. The problem is latency-bound (an ordered
+// double-precision sum chain per LM pass), so the footprint, not the lane
+// count, sets the throughput: small enough to share CUs with the other
+// stream groups' kernels.
 //
 // Reference: Optimizer::PoseOptimization src/Optimizer.cc:279-413,
 // OptimizationAlgorithmLevenberg::solve core/optimization_algorithm_levenberg.cpp:61-189,
@@ -26,9 +27,16 @@ constexpr int PO_NACC = 28;  // 21 lower-triangle H + 6 b + robust chi2
 constexpr int PO_CHI = 27;
 constexpr int PO_SPEC = 4;   // LM trials evaluated together (see k_pose_opt)
 constexpr int PO_ROWS = PO_CHI + PO_SPEC;  // term rows: H, b, one chi2 row per trial
-constexpr int PO_T = 256;    // threads per problem
+// One wave per problem: a frame's edges (tens to a few hundred) go through in
+// passes of PO_E, and the footprint (29 KB of LDS) lets four problems share a
+// CU with the other stream groups' extraction workgroups. (r02 ran 256
+// threads and 256-edge passes: 77 KB, one or two problems per CU.)
+#ifndef PO_THREADS
+#define PO_THREADS 64
+#endif
+constexpr int PO_T = PO_THREADS;  // threads per problem
 #ifndef PO_E
-#define PO_E 256             // edges per pass (a term row's length)
+#define PO_E 64                   // edges per pass (a term row's length)
 #endif
 constexpr int PO_TP = PO_E + 1;  // term row pitch (doubles): accumulator threads read distinct banks
 constexpr int PO_STRIDE_MAX = 8192;
@@ -528,13 +536,13 @@ __global__ __launch_bounds__(64) void k_pose_gather(GatherArgs G) {
 
 int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
     GF_PROF(ctx, s, "k_pose_opt");
-    // more problems than CUs: two per CU (measured 0.49 -> 0.36 ms for 512
-    // problems); a small batch keeps the spill-free one-wave build (B = 1:
-    // 166 vs 182 us)
-    if (nprob > ctx->num_cus)
-        k_pose_opt<2><<<nprob, PO_T, 0, s>>>(A);
-    else
-        k_pose_opt<1><<<nprob, PO_T, 0, s>>>(A);
+    // the spill-free build (256 registers a lane: one wave per SIMD, four
+    // problems per CU); PO_WPS=2 selects the two-per-SIMD build, which spills
+#ifndef PO_WPS
+#define PO_WPS 1
+#endif
+    (void)ctx;
+    k_pose_opt<PO_WPS><<<nprob, PO_T, 0, s>>>(A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
