@@ -25,7 +25,10 @@
 
 namespace {
 
-constexpr int RM_T = 1024;
+#ifndef RM_THREADS
+#define RM_THREADS 1024
+#endif
+constexpr int RM_T = RM_THREADS;
 constexpr int RM_MAXKF = 8192;
 
 struct RefArgs {

@@ -1,7 +1,7 @@
 """Phase cycles of k_active_match (diagnostic build, `make stamp`): one
-front end of B streams in the bench's GF regime (config 2, 0.93 stale map
-descriptors), stamps summed over frames and divided by frame-steps.
-Usage: GF_LIB=gf_orb_slam_amd/diag/libgfslam_am.so python scripts/am_stamps.py [B] [steps]"""
+front end of B streams in the bench's GF regime (config 2: keyframe maps,
+UpdateReference, 0.82 stale map descriptors; `fixed`: fixed maps, 0.93), stamps summed over frames and divided by frame-steps.
+Usage: GF_LIB=gf_orb_slam_amd/diag/libgfslam_am.so python scripts/am_stamps.py [B] [steps] [fixed]"""
 import ctypes
 import json
 import os
@@ -18,13 +18,21 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=0.93)
+fixed = len(sys.argv) > 3 and sys.argv[3] == "fixed"  # else the bench regime: keyframe maps, UpdateReference
+W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=0.93 if fixed else 0.82)
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
-maps = W.build_maps(lambda im: ex(im), 2000, device="cuda")
-fe = FrontEnd("euroc", 1000, B, 2000, 100)
+M = 2000 if fixed else 2100
+if fixed:
+    maps = [(m[0], m[1]) for m in W.build_maps(lambda im: ex(im), M, device="cuda")]
+else:
+    maps = [(g["mp"], g["desc"], g["graph"]) for g in W.build_global_maps(lambda im: ex(im), M, device="cuda")]
+fe = FrontEnd("euroc", 1000, B, M, 100)
 for b in range(B):
-    fe.set_map(b, *maps[W.scene_of[b]])
+    m = maps[W.scene_of[b]]
+    fe.set_map(b, m[0], m[1])
+    if len(m) > 2:
+        fe.set_covis(b, m[2])
     fe.set_rng(b, 1 + b)
 fe.set_source(frames, W.scene_of, W.phase)
 T, V = W.boot_state()
