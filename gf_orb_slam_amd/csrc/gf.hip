@@ -554,7 +554,7 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
         }
         got = __popcll(m);
         if (m) {
-            run = __clzll((long long)m);  // rejected tries after the last acceptance
+            run = __builtin_amdgcn_readfirstlane(__clzll((long long)m));  // rejected tries after the last acceptance
         } else {
             run += 64;
         }
@@ -562,7 +562,7 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
     s = rng_advance(s, o, 64);
     tries += 64;
     __syncthreads();
-    return got;
+    return __builtin_amdgcn_readfirstlane(got);
 }
 
 // One-point state of every pool slot (the k_onepoint_pre result, refreshed
@@ -732,6 +732,13 @@ __device__ __forceinline__ void live_sort(LiveSet<K>& L) {
     }
 }
 
+__device__ __forceinline__ double rlane(double v, int l) {  // lane l's value (l uniform)
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+}
+
 __device__ __forceinline__ double rl0(double v) {  // lane 0's value
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 0);
@@ -801,7 +808,7 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
         *s_res = rheap[0];
     }
     __syncthreads();
-    const int t = *s_res;
+    const int t = __builtin_amdgcn_readfirstlane(*s_res);
     int p = -1;
     for (int i0 = 0; i0 < na && p < 0; i0 += AW) {
         const unsigned long long m = __ballot(i0 + lane < na && al[i0 + lane] == t);
@@ -955,7 +962,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
 
     for (int round = 0; round < num_to_match; ++round) {
-        const int sz = min(S, N);
+        const int sz = __builtin_amdgcn_readfirstlane(min(S, N));
         if (sz == 0) break;  // empty heap: early termination
         // -- draws, ahead of need
         uint32_t sd = rs;
@@ -992,7 +999,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             __syncthreads();
         }
         AM_T(7);
-        if (nsucc_valid && s_nsucc == 0) {  // nothing left to match: the round draws until the draws give out
+        if (nsucc_valid && __builtin_amdgcn_readfirstlane(s_nsucc) == 0) {  // nothing left to match: the round draws until the draws give out
             colvis[lane] = 0ull;
             __syncthreads();
             int nacc = 0, ex = 0;
@@ -1006,8 +1013,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         while (nc < sz && exh_at < 0) {
             if (lane == 0) s_exh = -1;
             __syncthreads();
-            nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
-            exh_at = s_exh;
+            nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+            exh_at = __builtin_amdgcn_readfirstlane(s_exh);
         }
         AM_T(2);
         if (nc < sz) {  // the initial subset could not be completed
@@ -1039,8 +1046,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                 while (rep >= nc && exh_at < 0) {
                     if (lane == 0) s_exh = -1;
                     __syncthreads();
-                    nc += draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef);
-                    exh_at = s_exh;
+                    nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+                    exh_at = __builtin_amdgcn_readfirstlane(s_exh);
                 }
                 AM_T(2);
             }
@@ -1074,6 +1081,78 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                 L.m[r] = L.c[r] >= 0 && C.match[max(L.c[r], 0)] >= 0;
             }
             if (__ballot(tie)) return 0;
+            if constexpr (KR == 1) {
+                // The live set stays in place: lane i keeps its candidate and
+                // its rank (0 = heap top). A pop hands the top's lane to the
+                // replacement: every live score above the replacement moves up
+                // one rank, the others keep theirs, and the replacement takes
+                // the rank a ballot counts. No lane moves, so a pop is a few
+                // ballots and lane reads; the replacements' scores and match
+                // flags come from a 64-candidate window in registers.
+                double& ls = L.s[0];
+                int& lc = L.c[0];
+                int& lm = L.m[0];
+                int rk = lane;  // sorted above: rank = lane
+                const unsigned long long szm = sz >= 64 ? ~0ull : ((1ull << sz) - 1ull);
+                int w0 = -64, wn = 0;  // window start, candidates drawn when it was filled
+                double ws = 0.0;
+                int wm = 0;
+                while (true) {
+                    const int tl = __ffsll((long long)(__ballot(rk == 0) & szm)) - 1;  // the top's lane
+                    top = __builtin_amdgcn_readlane(lc, tl);
+                    if (__builtin_amdgcn_readlane(lm, tl)) {
+                        success = true;
+                        break;
+                    }
+                    const int rep = sz + npop;  // the replacement draw
+                    draw_eval(rep);
+                    if (rep >= nc) {
+                        exh = true;
+                        lc = lane == tl ? -1 : lc;  // the top was popped
+                        break;
+                    }
+                    if (rep >= w0 + 64 || rep >= wn) {
+                        w0 = rep;
+                        wn = nc;
+                        ws = w0 + lane < nc ? C.score[w0 + lane] : 0.0;
+                        wm = w0 + lane < nc ? C.match[w0 + lane] >= 0 : 0;
+                    }
+                    const double x = rlane(ws, rep - w0);
+                    const int xm = __builtin_amdgcn_readlane(wm, rep - w0);
+                    const unsigned long long live = szm & ~(1ull << tl);
+                    if (x != x || (__ballot(ls == x) & live)) {  // a tie: (b) pops it exactly
+                        npop = __builtin_amdgcn_readfirstlane(npop + 1);
+                        for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
+                        __syncthreads();
+                        const bool lv = (live >> lane) & 1ull;
+                        if (lv) {
+                            alv[__popcll(live & ((1ull << lane) - 1ull))] = (int16_t)lc;
+                            C.alive[lc] = 1;
+                        }
+                        if (lane == 0) {
+                            alv[sz - 1] = (int16_t)rep;
+                            C.alive[rep] = 1;
+                        }
+                        __syncthreads();
+                        return 0;
+                    }
+                    const unsigned long long gt = __ballot(ls > x) & live;
+                    rk = (gt >> lane) & 1ull ? rk - 1 : rk;
+                    if (lane == tl) {
+                        ls = x;
+                        lc = rep;
+                        lm = xm;
+                        rk = __popcll(gt);
+                    }
+                    npop = __builtin_amdgcn_readfirstlane(npop + 1);
+                }
+                // alive flags of the candidates that entered: popped 0, live 1
+                for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
+                __syncthreads();
+                if (lane < sz && lc >= 0) C.alive[lc] = 1;
+                __syncthreads();
+                return 1;
+            }
             while (true) {
                 top = __builtin_amdgcn_readlane(L.c[0], 0);
                 if (__builtin_amdgcn_readlane(L.m[0], 0)) {
@@ -1098,7 +1177,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                     rank += __popcll(__ballot(live && L.s[r] > x));
                 }
                 if (t2) {  // hand the live set (positions 1.., then the replacement) to (b)
-                    npop++;
+                    npop = __builtin_amdgcn_readfirstlane(npop + 1);
                     for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
                     __syncthreads();
 #pragma unroll
@@ -1144,7 +1223,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                         L.m[r] = xm;
                     }
                 }
-                npop++;
+                npop = __builtin_amdgcn_readfirstlane(npop + 1);
             }
             // alive flags of the candidates that entered: popped 0, live 1
             for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
@@ -1191,7 +1270,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                     C.alive[rep] = 1;
                     alv[tpos] = (int16_t)rep;  // the replacement takes the popped entry's place
                 }
-                npop++;
+                npop = __builtin_amdgcn_readfirstlane(npop + 1);
                 __syncthreads();
             }
         }
@@ -1242,7 +1321,7 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
             if (!C.alive[c] || c == top) atomicAnd(&pbits[C.slot[c] >> 6], ~(1ull << (C.slot[c] & 63)));
         __syncthreads();
         pool_prefix(P);
-        N -= nrem;
+        N = __builtin_amdgcn_readfirstlane(N - nrem);
         nsucc_valid = false;  // a claim and removed columns: recounted when it may pay off
         last_npop = npop;
         __syncthreads();
