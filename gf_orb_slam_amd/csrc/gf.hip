@@ -196,6 +196,50 @@ __device__ double logdet_sum(const double* a, const double* b, double sign) {
     return 2 * log(v1 * v2);
 }
 
+// logdet_sum(cur, b, +1) reading only what its Cholesky branch reads: b's
+// lower triangle (28 of 49 entries, through the global address space), the
+// factor formed in place, the same arithmetic entry for entry; a matrix that
+// is not positive definite takes logdet_sum's LU fallback on the full b.
+__device__ __forceinline__ double logdet_sum_lower(const double* cur, const double* b) {
+    double X[28];
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) X[i * (i + 1) / 2 + j] = gfd::ldg(b + 7 * i + j);
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) X[i * (i + 1) / 2 + j] = cur[7 * i + j] + X[i * (i + 1) / 2 + j];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        double s = X[j * (j + 1) / 2 + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) s -= X[j * (j + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
+        ok = ok && s > 0;
+        const double d = sqrt(s);
+        X[j * (j + 1) / 2 + j] = d;
+        const double rd = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 7; i++) {
+            double t = X[i * (i + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) t -= X[i * (i + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
+            X[i * (i + 1) / 2 + j] = t * rd;
+        }
+    }
+    if (!ok) return logdet_lu(cur, b, 1.0);
+    double v1 = 1, v2 = 1;  // Armadillo's two-accumulator product of the diagonal
+    v1 *= X[0];
+    v2 *= X[2];
+    v1 *= X[5];
+    v2 *= X[9];
+    v1 *= X[14];
+    v2 *= X[20];
+    v1 *= X[27];
+    return 2 * log(v1 * v2);
+}
+
 // ------------------------------------------------------------- k_obs_info
 __global__ void k_obs_info(gf_obs_camera cam, const double* __restrict__ Xv, const float* __restrict__ pos,
                            const float* __restrict__ sigma2, const int32_t* __restrict__ n, int cap, int check_viz,
@@ -603,7 +647,7 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
-        C.score[c] = logdet_sum(cur, info + 49LL * (rmp ? rmp[q] : q), 1.0);
+        C.score[c] = logdet_sum_lower(cur, info + 49LL * (rmp ? rmp[q] : q));
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
