@@ -576,7 +576,10 @@ __device__ __forceinline__ bool dup_of_lower_lane(int v) {
 // visited this round and not drawn earlier in the batch; accepted columns are
 // marked visited at once (unused ones are unmarked at the round end). A draw
 // fails after MAX_RANDOM_QUERY_TIME rejected tries: *exh_at = tries count then.
-__device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, const Pool& P, int16_t* vis,
+// The batch's start history and words are left in (s0, o0): the round's
+// commit advances the RNG from the batch holding its last call.
+__device__ int draw_batch(uint32_t& s, uint32_t& s0, uint32_t& o0, int& tries, int& run, int N, int round,
+                          const Pool& P, int16_t* vis,
                           const Cands& C, int nc, int* exh_at, const uint32_t (&coef)[31]) {
     const int lane = threadIdx.x;
     const uint32_t o = rng_word(s, coef);
@@ -603,6 +606,8 @@ __device__ int draw_batch(uint32_t& s, int& tries, int& run, int N, int round, c
             run += 64;
         }
     }
+    s0 = s;
+    o0 = o;
     s = rng_advance(s, o, 64);
     tries += 64;
     __syncthreads();
@@ -1011,6 +1016,8 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         // -- draws, ahead of need
         uint32_t sd = rs;
         int tries = 0, run = 0, nc = 0, evald = 0, exh_at = -1;
+        uint32_t bs0 = 0u, bo0 = 0u, bs1 = 0u, bo1 = 0u;  // start history / words of the last two batches
+        int nb = 0;                                      // batches drawn this round
         AM_T(6);
         if (!nsucc_valid && last_npop > sz) {
             // the last round had to pop: count the pool entries that can still be
@@ -1057,7 +1064,16 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         while (nc < sz && exh_at < 0) {
             if (lane == 0) s_exh = -1;
             __syncthreads();
-            nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+            {
+                uint32_t s0, o0;
+                nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
+                                                                    &s_exh, rcoef));
+                bs0 = nb & 1 ? bs0 : s0;
+                bo0 = nb & 1 ? bo0 : o0;
+                bs1 = nb & 1 ? s0 : bs1;
+                bo1 = nb & 1 ? o0 : bo1;
+                nb++;
+            }
             exh_at = __builtin_amdgcn_readfirstlane(s_exh);
         }
         AM_T(2);
@@ -1090,7 +1106,16 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
                 while (rep >= nc && exh_at < 0) {
                     if (lane == 0) s_exh = -1;
                     __syncthreads();
-                    nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+                    {
+                uint32_t s0, o0;
+                nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
+                                                                    &s_exh, rcoef));
+                bs0 = nb & 1 ? bs0 : s0;
+                bo0 = nb & 1 ? bo0 : o0;
+                bs1 = nb & 1 ? s0 : bs1;
+                bo1 = nb & 1 ? o0 : bo1;
+                nb++;
+            }
                     exh_at = __builtin_amdgcn_readfirstlane(s_exh);
                 }
                 AM_T(2);
@@ -1339,7 +1364,12 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         const int T = exh ? exh_at : C.tries[nused - 1];
         for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
         used += T;
-        for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
+        if (T > 0 && (T - 1) / 64 >= nb - 2) {  // the batch holding call T is one of the last two
+            const int b = (T - 1) / 64;
+            rs = (b & 1) ? rng_advance(bs1, bo1, T - 64 * b) : rng_advance(bs0, bo0, T - 64 * b);
+        } else {
+            for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
+        }
         __syncthreads();
         if (exh) break;
         AM_T(5);
