@@ -28,6 +28,9 @@
 #include "select.h"
 
 #define POOL_MAX 4096
+#ifndef AM_SMALL_POOL
+#define AM_SMALL_POOL 1280  // first-pass pool capacity of the two-pass active match (multiple of 64)
+#endif
 #define GF_THREADS 256
 #define MAX_RANDOM_QUERY_TIME 2000
 
@@ -325,6 +328,8 @@ struct ActiveArgs {
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
     int* grid_items;           // [F][kp_cap]
     int pool_cap;              // LDS pool capacity of this launch (<= POOL_MAX)
+    int32_t* ovf;              // [F] two-pass launch: 1 = pool did not fit the first pass's LDS
+    int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
 };
 
 // ---------------------------------------------------------------------------
@@ -878,7 +883,7 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #define AM_T(k) (void)0
 #endif
 
-__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
+__device__ __forceinline__ void active_match_body(const ActiveArgs& A) {
 #ifdef GF_AM_STAMP
     unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -908,6 +913,11 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
 
     const int f = blockIdx.x, lane = threadIdx.x;
+    if (A.pass == 2) {
+        if (A.ovf[f] == 0) return;  // handled by the small-pool pass
+    } else if (A.pass == 1 && lane == 0) {
+        A.ovf[f] = 0;
+    }
     const FrameConst& fc = A.fc;
     const int n = min(A.n[f], A.kp_cap);
     const int m = min(A.m[f], 32767);
@@ -966,8 +976,11 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
         }
         return;
     }
-    if (N > PC) {
-        if (lane == 0) A.err[f] = 2;
+    if (N > PC) {  // nothing written yet: the overflow pass redoes this frame with a full pool
+        if (lane == 0) {
+            if (A.pass == 1) A.ovf[f] = 1;
+            else A.err[f] = 2;
+        }
         return;
     }
     const Pool P{pbits, ppre};
@@ -1423,6 +1436,10 @@ __global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
     }
 }
 
+// the same body under two names, so that profiles tell the small-pool pass
+// from the overflow pass of a two-pass launch
+__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) { active_match_body(A); }
+__global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) { active_match_body(A); }
 
 #undef AM_T
 
@@ -1725,13 +1742,38 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
         k_onepoint_pre<<<nframes, PRE_THREADS, pre_lds, s>>>(A, (OnePre*)pre);
         GF_HIP(hipGetLastError());
     }
-    A.pool_cap = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
-    const size_t am_lds = active_lds_bytes(A.pool_cap, kp_cap);
-    rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, KP_MAX), &mask);
-    if (rc) return rc;
-    GF_PROF(ctx, s, "k_active_match");
-    k_active_match<<<nframes, AW, am_lds, s>>>(A);
-    GF_HIP(hipGetLastError());
+    const int full_pc = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
+    static unsigned long long ovf_mask = 0;
+    if ((rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, KP_MAX), &mask)) ||
+        (rc = set_lds_attr(ctx, (const void*)k_active_match_overflow, active_lds_bytes(POOL_MAX, KP_MAX), &ovf_mask)))
+        return rc;
+    // Two passes when the map list is long: most frames' pools (in-view, updated
+    // points) are far below the list capacity, and a smaller LDS footprint lets
+    // more workgroups of the concurrently running kernels share each CU. Frames
+    // whose pool does not fit return before writing anything and are redone by
+    // the overflow pass with the full capacity.
+    A.pool_cap = full_pc;
+    A.pass = 0;
+    A.ovf = nullptr;
+    if (full_pc > AM_SMALL_POOL) {
+        void* ovf;
+        if ((rc = gf::ws_get(ctx, 39, sizeof(int32_t) * nframes, &ovf))) return rc;
+        A.ovf = (int32_t*)ovf;
+        A.pool_cap = AM_SMALL_POOL;
+        A.pass = 1;
+    }
+    {
+        GF_PROF(ctx, s, "k_active_match");
+        k_active_match<<<nframes, AW, active_lds_bytes(A.pool_cap, kp_cap), s>>>(A);
+        GF_HIP(hipGetLastError());
+    }
+    if (A.pass == 1) {
+        A.pool_cap = full_pc;
+        A.pass = 2;
+        GF_PROF(ctx, s, "k_active_match_overflow");
+        k_active_match_overflow<<<nframes, AW, active_lds_bytes(full_pc, kp_cap), s>>>(A);
+        GF_HIP(hipGetLastError());
+    }
     return GF_OK;
 }
 

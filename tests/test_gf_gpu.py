@@ -114,6 +114,19 @@ def test_active_matching_bit_exact(seed, ntm):
         assert ng > 0 and calls > 0
 
 
+@pytest.mark.parametrize("nmp,frac", [(2500, 0.3), (4000, 1.0)])
+def test_active_matching_two_pass_launch(nmp, frac):
+    """Map lists longer than the first pass's LDS pool (1280) run in two
+    passes: pools that fit finish in the small-pool pass, longer ones return
+    untouched and are redone by the overflow pass (gf.hip obs_active_match)."""
+    case = _active_case(21 + nmp, nmp=nmp, num_to_match=100, frac_updated=frac)
+    views, updated = case[3], case[8]
+    pool = int((views["in_view"].astype(bool) & updated.astype(bool)).sum())
+    assert (pool > 1280) == (nmp == 4000), pool
+    ng, calls = _check_active(*case[:-1], 100, 21 + nmp)
+    assert ng > 0 and calls > 0
+
+
 def test_active_matching_tied_and_nan_scores():
     """Equal log-dets (duplicated information blocks) and NaN scores make the
     std::priority_queue order depend on its history: the device must replay it."""
