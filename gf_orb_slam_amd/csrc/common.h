@@ -57,6 +57,10 @@ struct gf_ctx {
 namespace gf {
 // Device scratch buffer `slot` of at least `bytes` (grow-only, owned by ctx).
 int ws_get(gf_ctx* ctx, int slot, size_t bytes, void** out);
+// record `ev` on the extraction stream after stage `after` (0 resize, 1 blur +
+// FAST map, 2 cells, 3 select, 4 describe) of the extractor's next runs; null
+// clears it (the front end's extraction gate, gf_frontend_set_gate)
+int extract_stage_event(::gf_extractor* ex, void* ev, int after);
 // Host-family helper: copy host -> scratch slot (returns device pointer).
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out);
 

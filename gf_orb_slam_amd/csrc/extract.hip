@@ -1089,6 +1089,8 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
 // ====================================================================== host
 struct gf_extractor {
     gf_ctx* ctx = nullptr;
+    hipEvent_t stage_ev = nullptr;  // gf::extract_stage_event
+    int stage_after = -1;
     int nfeatures = 0, nlevels = 0, fast_th = 20, min_th = 7, width = 0, height = 0, max_batch = 0;
     float scale_factor = 1.2f;
     LevelGeom g{};
@@ -1496,28 +1498,41 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
                                                                       ex->rs_pitch[l], ex->rs_rows[l]);
         }
     }
+    if (ex->stage_ev && ex->stage_after == 0) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_blur_fast");
         k_blur_fast<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g, ex->d_score, ex->fast_th);
     }
+    if (ex->stage_ev && ex->stage_after == 1) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_fast_cells");
         k_fast_cells<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(
             P, g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
     }
+    if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
         k_select<<<dim3(ex->nlevels, nframes), SEL_THREADS, (SEL_THREADS / 64) * sizeof(SelWave), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }
+    if (ex->stage_ev && ex->stage_after == 3) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_describe");
         k_describe<<<dim3((ex->capacity + 7) / 8, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
                                                                           ex->d_lvl_counts, d_kps, d_desc, d_counts,
                                                                           cap);
     }
+    if (ex->stage_ev && ex->stage_after == 4) GF_HIP(hipEventRecord(ex->stage_ev, s));
     GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf::extract_stage_event(gf_extractor* ex, void* ev, int after) {
+    GF_CHECK(ex, GF_ERR_ARG, "null extractor");
+    GF_CHECK(!ev || (after >= 0 && after <= 4), GF_ERR_ARG, "extraction stage must be 0..4");
+    ex->stage_ev = (hipEvent_t)ev;
+    ex->stage_after = ev ? after : -1;
     return GF_OK;
 }
 

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <vector>
 
@@ -530,6 +531,7 @@ struct gf_frontend {
     bool sourced = false;
     // extraction gate (gf_frontend_set_gate): caller-owned events
     hipEvent_t gate_wait = nullptr, gate_done = nullptr;
+    int gate_stage = 4;
     // tracking stream (gf_frontend_set_track_priority): the kernels after
     // extraction run on ts, joined back into the context's stream at the end
     hipStream_t ts = nullptr;
@@ -597,7 +599,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
-    if (fe->gate_done) GF_HIP(hipEventRecord(fe->gate_done, s));
+    if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
     const hipStream_t s_ctx = s;
     if (fe->ts) {  // fork: tracking on the prioritised stream
         GF_HIP(hipEventRecord(fe->ev_extracted, s));
@@ -1118,7 +1120,12 @@ int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
     GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot be gated");
     fe->gate_wait = (hipEvent_t)wait_event;
     fe->gate_done = (hipEvent_t)done_event;
-    return GF_OK;
+    // the next group's extraction may start once this one's stage
+    // GF_GATE_STAGE (0 resize .. 4 describe, the default) is done
+    const char* e = std::getenv("GF_GATE_STAGE");
+    fe->gate_stage = e ? std::max(0, std::min(4, std::atoi(e))) : 4;
+    return gf::extract_stage_event(fe->ex, fe->gate_done && fe->gate_stage < 4 ? done_event : nullptr,
+                                   fe->gate_stage);
 }
 
 int gf_frontend_set_track_priority(gf_frontend* fe, int priority) {

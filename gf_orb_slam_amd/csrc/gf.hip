@@ -31,6 +31,9 @@
 #ifndef AM_SMALL_POOL
 #define AM_SMALL_POOL 1280  // first-pass pool capacity of the two-pass active match (multiple of 64)
 #endif
+#ifndef AM_OVF_GRID
+#define AM_OVF_GRID 64  // workgroups of the overflow pass
+#endif
 #define GF_THREADS 256
 #define MAX_RANDOM_QUERY_TIME 2000
 
@@ -328,7 +331,8 @@ struct ActiveArgs {
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
     int* grid_items;           // [F][kp_cap]
     int pool_cap;              // LDS pool capacity of this launch (<= POOL_MAX)
-    int32_t* ovf;              // [F] two-pass launch: 1 = pool did not fit the first pass's LDS
+    int32_t* ovf;              // two-pass launch: [0] = count, [1 + k] = k-th frame whose pool
+                               // did not fit the first pass's LDS
     int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
 };
 
@@ -883,7 +887,7 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #define AM_T(k) (void)0
 #endif
 
-__device__ __forceinline__ void active_match_body(const ActiveArgs& A) {
+__device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int f) {
 #ifdef GF_AM_STAMP
     unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -912,12 +916,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A) {
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
 
-    const int f = blockIdx.x, lane = threadIdx.x;
-    if (A.pass == 2) {
-        if (A.ovf[f] == 0) return;  // handled by the small-pool pass
-    } else if (A.pass == 1 && lane == 0) {
-        A.ovf[f] = 0;
-    }
+    const int lane = threadIdx.x;
     const FrameConst& fc = A.fc;
     const int n = min(A.n[f], A.kp_cap);
     const int m = min(A.m[f], 32767);
@@ -978,7 +977,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A) {
     }
     if (N > PC) {  // nothing written yet: the overflow pass redoes this frame with a full pool
         if (lane == 0) {
-            if (A.pass == 1) A.ovf[f] = 1;
+            if (A.pass == 1) A.ovf[1 + atomicAdd(A.ovf, 1)] = f;
             else A.err[f] = 2;
         }
         return;
@@ -1438,8 +1437,14 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A) {
 
 // the same body under two names, so that profiles tell the small-pool pass
 // from the overflow pass of a two-pass launch
-__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) { active_match_body(A); }
-__global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) { active_match_body(A); }
+__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) { active_match_body(A, blockIdx.x); }
+
+// overflow pass: a small grid walks the frames the first pass listed (one
+// wave, so the LDS reuse between frames needs no barrier)
+__global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
+    const int cnt = A.ovf[0];
+    for (int k = blockIdx.x; k < cnt; k += gridDim.x) active_match_body(A, A.ovf[1 + k]);
+}
 
 #undef AM_T
 
@@ -1757,7 +1762,8 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.ovf = nullptr;
     if (full_pc > AM_SMALL_POOL) {
         void* ovf;
-        if ((rc = gf::ws_get(ctx, 39, sizeof(int32_t) * nframes, &ovf))) return rc;
+        if ((rc = gf::ws_get(ctx, 39, sizeof(int32_t) * (nframes + 1), &ovf))) return rc;
+        GF_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
         A.ovf = (int32_t*)ovf;
         A.pool_cap = AM_SMALL_POOL;
         A.pass = 1;
@@ -1771,7 +1777,8 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
         A.pool_cap = full_pc;
         A.pass = 2;
         GF_PROF(ctx, s, "k_active_match_overflow");
-        k_active_match_overflow<<<nframes, AW, active_lds_bytes(full_pc, kp_cap), s>>>(A);
+        // few workgroups: the full pool's LDS is only claimed where a frame needs it
+        k_active_match_overflow<<<std::min(nframes, AM_OVF_GRID), AW, active_lds_bytes(full_pc, kp_cap), s>>>(A);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
