@@ -683,11 +683,21 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
 // Lists longer than the LDS buffer fall back to the sequential replay on
 // global memory (gfsel::retain_best_truncate, same result).
 #define SEL_MAX_CELLS 1024
-#define SEL_BUF 1024  // entries per wave
+#define SEL_THREADS 512
+#define SEL_BUF 1024  // entries of wave 0's buffer (cell lists and the level list)
+#ifndef SEL_BUF_CELL
+#define SEL_BUF_CELL 1024  // entries of the other waves' buffers (cell lists only)
+#endif
+// one wave's LDS list and partition scratch; wave 0's is SEL_BUF long, the
+// others' SEL_BUF_CELL (a cell's corners after NMS rarely pass 100), so the
+// workgroup takes 8 + 7 x 2 KB instead of 8 x 8 KB and more fit a CU
 struct SelWave {
-    uint32_t a[SEL_BUF];
-    uint16_t lp[SEL_BUF], rp[SEL_BUF];
+    uint32_t* a;
+    uint16_t *lp, *rp;
+    int cap;
 };
+constexpr size_t sel_wave_bytes(int cap) { return (size_t)cap * (sizeof(uint32_t) + 2 * sizeof(uint16_t)); }
+constexpr size_t SEL_LDS = sel_wave_bytes(SEL_BUF) + (SEL_THREADS / 64 - 1) * sel_wave_bytes(SEL_BUF_CELL);
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -698,7 +708,7 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ int sel_resp(uint32_t e) { return (int)(e >> 24); }
 
 // __unguarded_partition(a + lo, a + hi, a + pivot) with KeypointResponseGreater.
-__device__ int wave_partition(SelWave& W, int lo, int hi, int P) {
+__device__ __forceinline__ int wave_partition(const SelWave& W, int lo, int hi, int P) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = (1ull << lane) - 1ull;
     int nL = 0, nR = 0;
@@ -734,7 +744,7 @@ __device__ int wave_partition(SelWave& W, int lo, int hi, int P) {
 }
 
 // std::nth_element(a, a + nth, a + n) on the wave's LDS list, all lanes.
-__device__ void wave_nth_element(SelWave& W, int nth, int n) {
+__device__ __forceinline__ void wave_nth_element(const SelWave& W, int nth, int n) {
     const int lane = threadIdx.x & 63;
     const gfsel::RespGreater comp;
     if (n == 0 || nth == n) return;
@@ -764,14 +774,14 @@ __device__ void wave_nth_element(SelWave& W, int nth, int n) {
 }
 
 // retainBest(list, keep) + truncation, written to dst[0 .. keep): one wave.
-__device__ void wave_retain_to(SelWave& W, uint32_t* list, int n, int keep, uint32_t* dst) {
+__device__ __forceinline__ void wave_retain_to(const SelWave& W, uint32_t* list, int n, int keep, uint32_t* dst) {
     const int lane = threadIdx.x & 63;
     if (keep <= 0) return;
     if (n <= keep) {
         for (int i = lane; i < n; i += 64) dst[i] = list[i];
         return;
     }
-    if (n > SEL_BUF) {  // sequential replay on global memory
+    if (n > W.cap) {  // sequential replay on global memory
         if (lane == 0) gfsel::retain_best_truncate(list, n, keep, gfsel::RespGreater());
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
@@ -785,7 +795,6 @@ __device__ void wave_retain_to(SelWave& W, uint32_t* list, int n, int keep, uint
     for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
 }
 
-#define SEL_THREADS 512
 __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
                                                 uint32_t* __restrict__ lists, long long list_stride,
                                                 const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
@@ -795,7 +804,15 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
     __shared__ int s_red[2];
     extern __shared__ __align__(16) uint8_t sel_dyn[];
     const int l = blockIdx.x, f = blockIdx.y, wv = threadIdx.x >> 6;
-    SelWave& W = reinterpret_cast<SelWave*>(sel_dyn)[wv];
+    SelWave W;
+    {
+        const int cap = wv == 0 ? SEL_BUF : SEL_BUF_CELL;
+        uint8_t* base = sel_dyn + (wv == 0 ? 0 : sel_wave_bytes(SEL_BUF) + (wv - 1) * sel_wave_bytes(SEL_BUF_CELL));
+        W.a = reinterpret_cast<uint32_t*>(base);
+        W.lp = reinterpret_cast<uint16_t*>(W.a + cap);
+        W.rp = W.lp + cap;
+        W.cap = cap;
+    }
     const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb;
     for (int c = threadIdx.x; c < nc; c += blockDim.x) {
         cnt[c] = counts[(long long)f * g.ncells + cb + c];
@@ -1430,7 +1447,7 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
     GF_HIP(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)((SEL_THREADS / 64) * sizeof(SelWave))));
+                               (int)SEL_LDS));
     GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)ex->fast_lds));
     *out = ex;
@@ -1512,7 +1529,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
-        k_select<<<dim3(ex->nlevels, nframes), SEL_THREADS, (SEL_THREADS / 64) * sizeof(SelWave), s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+        k_select<<<dim3(ex->nlevels, nframes), SEL_THREADS, SEL_LDS, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }
