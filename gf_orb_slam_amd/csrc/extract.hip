@@ -896,10 +896,20 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
     }
     __syncthreads();
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
+    // a cell list longer than a cell wave's buffer that needs a selection
+    // waits for wave 0's (larger) buffer, after wave 0's own cells
+    auto deferred = [&](int c) { return cnt[c] > keep[c] && cnt[c] > SEL_BUF_CELL; };
     for (int c = wv; c < nc; c += SEL_THREADS / 64) {
-        if (!valid[c]) continue;
+        if (!valid[c] || (wv != 0 && deferred(c))) continue;
         uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
         wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
+    }
+    if (wv == 0 && SEL_BUF_CELL < SEL_BUF) {
+        for (int c = 0; c < nc; c++) {
+            if (c % (SEL_THREADS / 64) == 0 || !valid[c] || !deferred(c)) continue;
+            uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+            wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
+        }
     }
     __syncthreads();
     if (wv == 0) {  // the level's retainBest (:750-752)
