@@ -898,7 +898,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
     uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
     // a cell list longer than a cell wave's buffer that needs a selection
     // waits for wave 0's (larger) buffer, after wave 0's own cells
-    auto deferred = [&](int c) { return cnt[c] > keep[c] && cnt[c] > SEL_BUF_CELL; };
+    auto deferred = [&](int c) { return SEL_BUF_CELL < SEL_BUF && cnt[c] > keep[c] && cnt[c] > SEL_BUF_CELL; };
     for (int c = wv; c < nc; c += SEL_THREADS / 64) {
         if (!valid[c] || (wv != 0 && deferred(c))) continue;
         uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
