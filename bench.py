@@ -422,7 +422,7 @@ def main():
     from gf_orb_slam_amd.bow import ORBVocabulary
     from gf_orb_slam_amd.dist import GfDist, checksum, share_world
     from gf_orb_slam_amd.orb import Context
-    from gf_orb_slam_amd.pipeline import STATS, FrontEnd, chain_extraction
+    from gf_orb_slam_amd.pipeline import CK, STATS, FrontEnd, chain_extraction
 
     cam = args.camera
     refmap = not args.fixed_map
@@ -721,20 +721,30 @@ def main():
         for fe in fes:
             fe.sync()
         db = time.perf_counter() - t1
+        caps = {"isInFrustum": 32, "map_info": 64, "active_matching": 128, "no_time_left": 16,
+                "map_info_next": 256, "visibility_pass": 512, "budget_matcher": 1024}
+        last = {k: 0 for k in caps}
+        sofar = []
         for fe in fes:
             st = fe.read("stats")
-            cut_f += int((st[STATS.index("branch")] == 5).sum())
-            cut_s += int((st[STATS.index("flags")] & 16 != 0).sum())
+            for k, bit in caps.items():
+                last[k] += int((st[STATS.index("flags")] & bit != 0).sum())
+            sofar.append(fe.read("clock")[:, CK["sofar"]])
             fe.set_budgets()
         bh = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)
+        sofar = np.concatenate(sofar) / 1e8
         out["budgets_on"] = {"match_s": 0.015, "select_s": round(sel_s, 4), "steps": args.budget_steps,
                              "frames_per_s": round(B * args.budget_steps / db, 1),
                              "ms_per_step": round(db / args.budget_steps * 1e3, 3),
-                             "branch_mix": {"active_matching": int(bh[:, 3].sum()), "budget_cut": int(bh[:, 5].sum()),
+                             "branch_mix": {"active_matching": int(bh[:, 3].sum()),
                                             "leftovers_only": int(bh[:, 1].sum())},
-                             "last_step_cuts": {"isInFrustum": cut_f, "additional_matches": cut_s},
-                             "note": "gf_set_budgets with the reference's budgets, device clock from the step "
-                                     "start of the whole batch; parity mode (+inf) is the headline"}
+                             "frames_cut": int(bh[:, 5].sum()), "frames": int(B * (args.budget_steps + 1)),
+                             "last_step_caps": last,
+                             "timeCost_sofar_ms": {"median": round(float(np.median(sofar)) * 1e3, 3),
+                                                   "max": round(float(sofar.max()) * 1e3, 3)},
+                             "note": "gf_set_budgets with the reference's budgets (abi.h: each cap's timer where "
+                                     "the reference starts it, frame clock after the extraction gate); parity "
+                                     "mode (+inf) is the headline"}
     for fe in fes:
         fe.close()
     if rank == 0 and args.single_stream_steps > 0:

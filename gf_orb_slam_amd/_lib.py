@@ -152,6 +152,7 @@ _PROTOS = {
     "gf_update_reference": [_P, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P],
     "gf_update_reference_dev": [_P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P],
     "gf_frontend_set_gate": [_P, _P, _P],
+    "gf_frontend_set_gate_stage": [_P, ctypes.c_int],
     "gf_frontend_set_track_priority": [_P, ctypes.c_int],
     "gf_event_create": [_P, _P],
     "gf_event_destroy": [_P],

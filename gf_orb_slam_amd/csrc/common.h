@@ -52,6 +52,11 @@ struct gf_ctx {
     // captured graphs (gf_frontend_capture) alive on this context: their
     // kernels hold scratch pointers, so no slot may be reallocated meanwhile
     int ws_pinned = 0;
+    // front ends on this context, and whether one runs its tracking kernels on
+    // a stream of its own (gf_frontend_set_track_priority): its kernels take
+    // the context's scratch slots, so it must be the only front end here
+    int frontends = 0;
+    bool track_stream = false;
 };
 
 namespace gf {
@@ -78,10 +83,53 @@ int obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const dou
                    const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp, const uint8_t* d_outlier,
                    const float* d_map_pos, const int32_t* d_nmp, int map_stride, const float* level_sigma2,
                    int nlevels, double* d_H, double* d_info, float* d_uv, const int32_t* d_remap, void* stream);
+// One stage's time-budget clock in the front end (gf_set_budgets): the timer
+// start of every frame (s_memrealtime ticks), the clock record ([F][stride]
+// int64, GF_FE_CLOCK) and the offset of the stage's elapsed-time array in it.
+// t0 == null: the stage runs without a budget and reads no clock.
+struct StageClock {
+    const unsigned long long* t0 = nullptr;
+    long long* rec = nullptr;
+    long long stride = 0;
+    int off = 0;
+};
+
+// batchInfoMat_Map with its time cap (Observability.cc:564-578) when ck.t0 is
+// set: each 64-point batch reads the clock once and is skipped when 2 x its
+// elapsed time > cap2[f] (2 x the cap in ticks; < 0 skips every batch).
 int obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
                  const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views, int32_t* d_upd_id,
                  int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated, const int32_t* d_remap,
-                 void* stream);
+                 void* stream, const StageClock& ck = StageClock{}, const long long* d_cap2 = nullptr);
+
+// runActiveMapMatching's time cap (Observability.cc:1260, 1366-1370) for the
+// front end: time_for_match = match_ticks - time_Mat_Online - time_Viz, with
+// time_Mat_Online measured from mat_t0[f] (Tracking.cc:3311) to the kernel's
+// start and time_Viz = viz[f]. ck.t0 unused (the kernel starts its own timer).
+struct ActiveClock {
+    const unsigned long long* mat_t0 = nullptr;  // null: no budget
+    const long long* viz = nullptr;
+    long long match_ticks = 0;
+    long long* rec = nullptr;
+    long long stride = 0;
+    int off = 0;    // per-round array
+    int rounds = 0; // its length
+};
+
+// Frame::isInFrustum over a map (d_list null: points < d_m[f]) or over a list,
+// clocked as gf_set_budgets describes when ck.t0 is set: results go to d_alt.
+int frustum_clocked(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw, const gf_map_point* d_mps,
+                    const int32_t* d_m, const int32_t* d_list, const int32_t* d_nlist, int mp_cap,
+                    float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview, const StageClock& ck,
+                    gf_mp_view* d_alt, void* stream);
+// SearchByProjection_Budget (ORBmatcher.cc:276-379) over a list with its clock:
+// d_rest2[f] = 2 x timeCost_rest, ck.t0 = the visibility pass's timer start.
+int match_project_list_budget(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                              const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                              const uint8_t* d_mp_desc, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                              float th, float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches,
+                              const StageClock& ck, const long long* d_rest2, int32_t* d_qres, int32_t* d_old,
+                              int32_t* d_err, void* stream);
 int obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps, int kp_stride,
                            const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp, int map_stride,
                            int frame_id, double diag, double* d_out, const int32_t* d_remap, void* stream);
@@ -91,7 +139,7 @@ int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf
                      const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
                      const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
                      int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
-                     const int32_t* d_remap, void* stream);
+                     const int32_t* d_remap, void* stream, const ActiveClock& ck = ActiveClock{});
 
 // RCCL broadcast on the communicator's stream (dist.hip), asynchronous.
 int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);

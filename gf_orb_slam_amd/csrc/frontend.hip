@@ -87,10 +87,29 @@ struct FeDev {
     int32_t* nm2;    // matches of SearchByProjection(F, local, 1)
     int32_t* stats;  // [GF_FE_NSTAT][B]
     int32_t* hist;   // [B][8] running counters (GF_FE_HIST)
-    // budgets (device clock ticks of 100 MHz; < 0: no budget)
+    // time budgets (gf_set_budgets; device clock ticks of 100 MHz; < 0: no budget)
     long long match_ticks, select_ticks;
-    unsigned long long* t0;
+    long long* clk;        // [B][ck_stride] clock record (GF_FE_CLOCK)
+    long long ck_stride;
+    int ck_R;              // length of the per-round array
+    unsigned long long* t_frame;  // [B] timer_all: the frame's start, after the extraction gate
+    unsigned long long* t_viz0;   // [B] the isInFrustum loop's timer (Tracking.cc:3252)
+    unsigned long long* t_mat0;   // [B] after the loop (Tracking.cc:3311)
+    unsigned long long* t_sel0;   // [B] RunMapPointsSelection / SearchAdditionalMatchesInFrame start
+    long long* viz_time;   // [B] time_Viz
+    long long* cap2_mi;    // [B] 2 x MAP_INFO cap of the active branch
+    long long* rest2;      // [B] 2 x timeCost_rest
+    long long* cap2_sel;   // [B] 2 x MAP_INFO cap of RunMapPointsSelection (-1: skip all)
+    gf_mp_view* vtmp;      // [B][M] clocked isInFrustum results (kept before the cut)
+    int32_t* ncut;         // [B] points the isInFrustum cap moved to mLeftMapPoints
+    int32_t* nlist0;       // [B] mLeftMapPoints size before SearchAdditionalMatchesInFrame
 };
+
+__device__ __forceinline__ long long* ck_rec(const FeDev& D, int b) { return D.clk + (long long)b * D.ck_stride; }
+__device__ __forceinline__ int ck_off_viz(const FeDev& D) { return GF_CK_OFF_VIZ(D.M, D.ck_R); }
+__device__ __forceinline__ int ck_off_mi(const FeDev& D) { return GF_CK_OFF_MI(D.M, D.ck_R); }
+__device__ __forceinline__ int ck_off_sel(const FeDev& D) { return GF_CK_OFF_SEL(D.M, D.ck_R); }
+__device__ __forceinline__ int ck_off_sa(const FeDev& D) { return GF_CK_OFF_SA(D.M, D.ck_R); }
 
 __device__ __forceinline__ int32_t* stat(const FeDev& D, int which) { return D.stats + (long long)which * D.B; }
 
@@ -119,9 +138,19 @@ __global__ __launch_bounds__(256) void k_fe_begin(FeDev D) {
         float o[16];
         mat44(D.V + 16 * b, D.Tcw_last + 16 * b, o);
         for (int i = 0; i < 16; i++) D.Tcw[16 * b + i] = o[i];
-        D.t0[b] = now_ticks();
         for (int s = 0; s < GF_FE_NSTAT; s++)
             if (s != GF_ST_FRAMES) stat(D, s)[b] = 0;
+        D.ncut[b] = 0;
+    }
+    if (D.match_ticks >= 0 || D.select_ticks >= 0) {  // timer_all (Tracking.cc:866) and a fresh record header
+        long long* r = ck_rec(D, b);
+        if (t < GF_CK_HEADER) r[t] = -1;
+        if (t == 0) {
+            r[GF_CK_FLAGS] = (D.match_ticks >= 0 ? 1 : 0) | (D.select_ticks >= 0 ? 2 : 0);
+            r[GF_CK_MATCH] = D.match_ticks;
+            r[GF_CK_SELECT] = D.select_ticks;
+            D.t_frame[b] = now_ticks();
+        }
     }
     const long long o = (long long)b * D.cap;
     for (int i = t; i < D.cap; i += 256) {
@@ -149,9 +178,6 @@ __device__ int compact_in_view(const FeDev& D, int b, int32_t* out) {
 __global__ __launch_bounds__(64) void k_fe_branch(FeDev D) {
     const int b = blockIdx.x, lane = threadIdx.x;
     const int ntm = stat(D, GF_ST_TO_MATCH)[b];
-    // isInFrustum time cap (Tracking.cc:3262-3270): past half of the matching
-    // budget every remaining local point goes to mLeftMapPoints
-    const bool late = D.match_ticks >= 0 && (long long)(now_ticks() - D.t0[b]) > D.match_ticks / 2;
     if (D.gf && ntm <= 0) {
         // mbTrackInView as left by earlier frames (matched points already false)
         const int n = compact_in_view(D, b, D.left1);
@@ -161,36 +187,73 @@ __global__ __launch_bounds__(64) void k_fe_branch(FeDev D) {
             D.nlist_viz[b] = n;
             D.m_frustum[b] = 0;
         }
-    } else if (D.gf && late) {
-        // the cut falls on the first point of the list: every point goes to
-        // mLeftMapPoints (vector(vit, vend)); nToMatch stays 0
-        const int m = D.nmp[b];
-        for (int i = lane; i < m; i += 64) D.left1[(long long)b * D.M + i] = i;
-        if (lane == 0) {
-            stat(D, GF_ST_BRANCH)[b] = 5;
-            stat(D, GF_ST_FLAGS)[b] |= 8;
-            D.nlist[b] = m;
-            D.nlist_viz[b] = m;
-            D.m_frustum[b] = 0;
-        }
     } else if (lane == 0) {
         stat(D, GF_ST_BRANCH)[b] = 0;
         D.nlist[b] = 0;
         D.nlist_viz[b] = 0;
         D.m_frustum[b] = D.nmp[b];
+        if (D.gf && D.match_ticks >= 0) D.t_viz0[b] = now_ticks();  // timer.tic() (Tracking.cc:3252)
     }
 }
 
+// Keypoint-matched map points of a stream (mnLastFrameSeen == mnId) as a bitmap
+// in LDS; M <= 4096.
+__device__ void matched_bits(const FeDev& D, int b, int m, uint32_t* bits) {
+    const int t = threadIdx.x;
+    for (int w = t; w < 128; w += blockDim.x) bits[w] = 0u;
+    __syncthreads();
+    const int n = D.nkp[b];
+    const long long o = (long long)b * D.cap;
+    for (int i = t; i < n; i += blockDim.x) {
+        const int mp = D.kp2mp[o + i];
+        if (mp >= 0 && mp < m) atomicOr(&bits[mp >> 5], 1u << (mp & 31));
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool is_matched(const uint32_t* bits, int i) { return (bits[i >> 5] >> (i & 31)) & 1u; }
+
+// nToMatch and the search branch (Tracking.cc:3305-3343). With a match budget
+// the isInFrustum results are in vtmp with each point's elapsed time in the
+// clock record: the loop stops at the first point not matched this frame whose
+// elapsed > time_total_match / 2 (:3262-3270); the points before it take their
+// results, the rest keep their state and go to mLeftMapPoints in list order,
+// and mvpLocalMapPoints (the search's list) ends at the cut.
 __global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
-    __shared__ int s_cnt;
+    __shared__ int s_cnt, s_cut, s_last;
+    __shared__ uint32_t bits[128];
     const int b = blockIdx.x, t = threadIdx.x;
-    if (t == 0) s_cnt = 0;
+    if (t == 0) {
+        s_cnt = 0;
+        s_cut = INT_MAX;
+        s_last = -1;
+    }
     __syncthreads();
     const int br = stat(D, GF_ST_BRANCH)[b];
+    const bool clocked = D.gf && D.match_ticks >= 0 && br == 0;
+    const int m = D.nmp[b];
+    const long long o = (long long)b * D.M;
+    int cut = m;
+    if (clocked) {
+        matched_bits(D, b, m, bits);
+        const long long* el = ck_rec(D, b) + ck_off_viz(D);
+        for (int i = t; i < m; i += 256) {
+            if (is_matched(bits, i)) continue;  // mnLastFrameSeen == mnId: skipped before the clock
+            if (2 * el[i] > D.match_ticks) atomicMin(&s_cut, i);
+            atomicMax(&s_last, i);
+        }
+        __syncthreads();
+        cut = min(s_cut, m);
+        for (int i = t; i < cut; i += 256) {
+            gf_mp_view v = D.vtmp[o + i];
+            if (is_matched(bits, i)) v.in_view = 0;
+            D.views[o + i] = v;
+        }
+        for (int i = cut + t; i < m; i += 256) D.left1[o + i - cut] = i;
+    }
     if (br == 0) {
-        const int m = D.nmp[b];
         int c = 0;
-        for (int i = t; i < m; i += 256) c += D.views[(long long)b * D.M + i].in_view ? 1 : 0;
+        for (int i = t; i < cut; i += 256) c += D.views[o + i].in_view ? 1 : 0;
         c = gfd::warp_sum(c);
         if ((t & 63) == 0) atomicAdd(&s_cnt, c);
     }
@@ -199,6 +262,19 @@ __global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
     D.m_active[b] = 0;
     D.m_m2[b] = 0;
     if (br != 0) return;
+    if (clocked) {
+        // time_Viz: the last value the loop compared (0 when it compared none)
+        const long long* el = ck_rec(D, b) + ck_off_viz(D);
+        const long long viz = cut < m ? el[cut] : (s_last >= 0 ? el[s_last] : 0);
+        long long* r = ck_rec(D, b);
+        r[GF_CK_VIZ_CUT] = cut;
+        r[GF_CK_VIZ_TIME] = viz;
+        D.viz_time[b] = viz;
+        D.cap2_mi[b] = D.match_ticks - viz;  // (total - time_Viz) / 2, doubled
+        D.ncut[b] = m - cut;
+        stat(D, GF_ST_NCUT)[b] = m - cut;
+        if (cut < m) stat(D, GF_ST_FLAGS)[b] |= 8 | 32;
+    }
     const int n = s_cnt;
     stat(D, GF_ST_IN_VIEW)[b] = n;
     int nb;
@@ -206,23 +282,36 @@ __global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
         nb = 4;
     } else if (!D.gf || n < 400) {  // Tracking.cc:3322
         nb = 2;
-        D.m_m2[b] = D.nmp[b];
+        D.m_m2[b] = cut;
     } else {
         nb = 3;
-        D.m_active[b] = D.nmp[b];
+        D.m_active[b] = cut;
     }
     stat(D, GF_ST_BRANCH)[b] = nb;
+    if (clocked) D.t_mat0[b] = now_ticks();  // timer.tic() (Tracking.cc:3311)
 }
 
 __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
+    __shared__ int s_tail[4096];
     const int b = blockIdx.x, t = threadIdx.x;
     const int br = stat(D, GF_ST_BRANCH)[b];
+    const long long o = (long long)b * D.M;
+    const int ncut = D.ncut[b];
     int n = 0;
-    if (br == 1 || br == 5) {
+    if (br == 1) {
         n = D.nlist[b];
-        for (int i = t; i < n; i += 256) D.left[(long long)b * D.M + i] = D.left1[(long long)b * D.M + i];
-    } else if (br == 3) {
-        n = D.nleft[b];
+        for (int i = t; i < n; i += 256) D.left[o + i] = D.left1[o + i];
+    } else {
+        // mLeftMapPoints: the points the isInFrustum cap cut (Tracking.cc:3265),
+        // then runActiveMapMatching's leftovers (push_back, Observability.cc:1517-1519)
+        const int na = br == 3 ? D.nleft[b] : 0;
+        if (ncut > 0 && na > 0) {
+            for (int i = t; i < na; i += 256) s_tail[i] = D.left[o + i];
+            __syncthreads();
+            for (int i = t; i < na; i += 256) D.left[o + ncut + i] = s_tail[i];
+        }
+        for (int i = t; i < ncut; i += 256) D.left[o + i] = D.left1[o + i];
+        n = ncut + na;
     }
     if (t != 0) return;
     if (br == 2) stat(D, GF_ST_LOCAL)[b] = D.nm2[b];
@@ -238,18 +327,25 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
         Twc[4 * i + 3] = -s;
     }
     Twc[15] = 1.f;
-    float o[16];
-    mat44(D.Tcw + 16 * b, Twc, o);
-    for (int i = 0; i < 16; i++) D.V[16 * b + i] = o[i];
+    float Vn[16];
+    mat44(D.Tcw + 16 * b, Twc, Vn);
+    for (int i = 0; i < 16; i++) D.V[16 * b + i] = Vn[i];
     D.nlist[b] = n;
+    D.nlist0[b] = n;
     stat(D, GF_ST_NLEFT)[b] = n;
-    const bool viz = (br == 1 || br == 5);
-    // SearchByProjection_Budget returns at once without budget (ORBmatcher.cc:281-282)
-    const bool no_time = D.select_ticks >= 0 && (long long)(now_ticks() - D.t0[b]) >= D.select_ticks;
-    D.nlist_viz[b] = (viz && !no_time) ? n : 0;
-    if (no_time) {
-        D.nlist[b] = 0;
-        if (n) stat(D, GF_ST_FLAGS)[b] |= 8 | 16;
+    const bool viz = (br == 1 || ncut > 0);  // mbNeedVizCheck
+    D.nlist_viz[b] = viz ? n : 0;
+    if (D.select_ticks >= 0) {
+        // timeCost_rest = budget - timeCost_sofar (Tracking.cc:866), shared by
+        // RunMapPointsSelection and SearchAdditionalMatchesInFrame, whose
+        // timers start here
+        const unsigned long long now = now_ticks();
+        const long long sofar = (long long)(now - D.t_frame[b]), rest = D.select_ticks - sofar;
+        ck_rec(D, b)[GF_CK_SOFAR] = sofar;
+        D.rest2[b] = 2 * rest;
+        D.cap2_sel[b] = rest > 0 ? 2 * rest : -1;  // <= 0: "too little budget available" (:1727-1731)
+        D.t_sel0[b] = now;
+        if (rest <= 0) stat(D, GF_ST_FLAGS)[b] |= 8 | 16;
     }
 }
 
@@ -258,14 +354,47 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
 // Tracking.cc:3110-3111), so they keep mbTrackInView = false: after the list
 // frustum of a stream that ran the pass, matched points are out of view again.
 // Only the isInFrustum-cut list (branch 5) holds such points.
+// With a select budget the visibility pass is clocked (Tracking.cc:3107-3119):
+// its results are in vtmp, and the pass stops at the first list point not
+// matched before the local-map search whose elapsed > timeCost_rest / 2; the
+// points before it take their results and mLeftMapPoints is erased from there.
 __global__ __launch_bounds__(256) void k_fe_viz_exclude(FeDev D) {
+    __shared__ uint32_t bits[128];
+    __shared__ int s_cut;
     const int b = blockIdx.x, t = threadIdx.x;
-    if (D.nlist_viz[b] <= 0) return;
+    const int nl = D.nlist_viz[b];
+    if (nl <= 0) return;
     const int n = D.nkp[b], m = D.nmp[b];
-    const long long o = (long long)b * D.cap;
-    for (int i = t; i < n; i += 256) {
+    const long long o = (long long)b * D.cap, om = (long long)b * D.M;
+    if (D.select_ticks < 0) {
+        for (int i = t; i < n; i += 256) {
+            const int mp = D.kp2mp[o + i];
+            if (mp >= 0 && mp < m) D.views[om + mp].in_view = 0;
+        }
+        return;
+    }
+    if (t == 0) s_cut = INT_MAX;
+    matched_bits(D, b, m, bits);
+    const long long* el = ck_rec(D, b) + ck_off_sa(D);
+    const long long rest2 = D.rest2[b];
+    const int32_t* L = D.left + om;
+    for (int k = t; k < nl; k += 256)
+        if (!is_matched(bits, L[k]) && 2 * el[k] > rest2) atomicMin(&s_cut, k);
+    __syncthreads();
+    const int cut = min(s_cut, nl);
+    for (int k = t; k < cut; k += 256) D.views[om + L[k]] = D.vtmp[om + L[k]];
+    __syncthreads();
+    for (int i = t; i < n; i += 256) {  // as above: matched points end out of view
         const int mp = D.kp2mp[o + i];
-        if (mp >= 0 && mp < m) D.views[(long long)b * D.M + mp].in_view = 0;
+        if (mp >= 0 && mp < m) D.views[om + mp].in_view = 0;
+    }
+    if (t == 0) {
+        ck_rec(D, b)[GF_CK_SA_CUT] = cut;
+        if (cut < nl) {
+            D.nlist[b] = cut;  // mLeftMapPoints.erase(vit, vend)
+            stat(D, GF_ST_NLEFT)[b] = cut;
+            stat(D, GF_ST_FLAGS)[b] |= 8 | 512;
+        }
     }
 }
 
@@ -301,6 +430,19 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
         for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
         D.t_prev[b] = D.t_cur[b];
         int fl = stat(D, GF_ST_FLAGS)[b];
+        if (D.match_ticks >= 0 || D.select_ticks >= 0) {  // the caps that fired, from the clock record
+            const long long* r = ck_rec(D, b);
+            if (D.match_ticks >= 0 && D.m_active[b] > 0) {
+                for (int w = 0; w * 64 < D.m_active[b]; w++)
+                    if (2 * r[ck_off_mi(D) + w] > D.cap2_mi[b]) fl |= 8 | 64;
+                if (r[GF_CK_AM_CUT] >= 0) fl |= 8 | 128;
+            }
+            if (D.select_ticks >= 0 && D.gf && D.cap2_sel[b] >= 0) {
+                for (int w = 0; w * 64 < D.nmp[b]; w++)
+                    if (2 * r[ck_off_sel(D) + w] > D.cap2_sel[b]) fl |= 8 | 256;
+                if (r[GF_CK_BUDGET_CUT] >= 0) fl |= 8 | 1024;
+            }
+        }
         if (stat(D, GF_ST_M3)[b] < 20) fl |= 1;
         if (stat(D, GF_ST_FOUND)[b] < 10) fl |= 2;
         if (stat(D, GF_ST_INL2)[b] < 15) fl |= 4;
@@ -308,7 +450,8 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
         stat(D, GF_ST_FRAMES)[b] += 1;
         int32_t* h = D.hist + 8LL * b;
         const int br = stat(D, GF_ST_BRANCH)[b];
-        if (br >= 0 && br < 6) h[br] += 1;
+        if (br >= 0 && br < 5) h[br] += 1;
+        if (fl & 8) h[5] += 1;  // a time cap fired
         h[6] += stat(D, GF_ST_LDETS)[b];
         h[7] += stat(D, GF_ST_LOCAL)[b];
         if (b == 0) *D.step += 1;
@@ -523,6 +666,7 @@ struct gf_frontend {
     float* mp_pos = nullptr;
     uint8_t* mp_updated = nullptr;
     int32_t* nview = nullptr;
+    int32_t *qres = nullptr, *qold = nullptr, *merr = nullptr;  // SearchByProjection_Budget scratch
     uint8_t* staging = nullptr;
     const uint8_t** staging_ptrs = nullptr;
     std::vector<void*> allocs;
@@ -591,12 +735,14 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     const gf_frame_info* fi = &fe->fi;
     int32_t* st = D.stats;
     auto col = [&](int c) { return st + (size_t)c * B; };
+    // the frame's clock starts after the extraction gate: waiting behind the
+    // other front ends' extraction is not this frame's time
+    if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
     {
         GF_PROF(ctx, s, "k_fe_begin");
         k_fe_begin<<<B, 256, 0, s>>>(D);
         GF_HIP(hipGetLastError());
     }
-    if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
     if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
@@ -647,8 +793,23 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         k_fe_branch<<<B, 64, 0, s>>>(D);
         GF_HIP(hipGetLastError());
     }
-    FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
-    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+    const bool mclk = D.gf && D.match_ticks >= 0, sclk = D.gf && D.select_ticks >= 0;
+    auto clock = [&](const unsigned long long* t0, int off) {
+        gf::StageClock c;
+        c.t0 = t0;
+        c.rec = D.clk;
+        c.stride = D.ck_stride;
+        c.off = off;
+        return c;
+    };
+    const int R = D.ck_R;
+    if (mclk) {  // the isInFrustum loop on its clock (k_fe_decide applies the cap)
+        FE_RC(gf::frustum_clocked(ctx, fi, B, D.Tcw, D.map, D.m_frustum, nullptr, nullptr, M, 0.5f, D.views,
+                                  fe->nview, clock(D.t_viz0, GF_CK_OFF_VIZ(M, R)), D.vtmp, s));
+    } else {
+        FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
+        FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+    }
     {
         GF_PROF(ctx, s, "k_fe_decide");
         k_fe_decide<<<B, 256, 0, s>>>(D);
@@ -656,11 +817,22 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     }
     if (D.gf) {
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
-                               fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s));
+                               fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s,
+                               mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R)) : gf::StageClock{}, D.cap2_mi));
+        gf::ActiveClock ac;
+        if (mclk) {
+            ac.mat_t0 = D.t_mat0;
+            ac.viz = D.viz_time;
+            ac.match_ticks = D.match_ticks;
+            ac.rec = D.clk;
+            ac.stride = D.ck_stride;
+            ac.off = GF_CK_OFF_AM(M, R);
+            ac.rounds = R;
+        }
         FE_RC(gf::obs_active_match(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
                                    fe->mp_info, fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2,
                                    col(GF_ST_TO_MATCH), 1.f, 0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score,
-                                   D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s));
+                                   D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s, ac));
     }
     FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, 1.f, 0.8f,
                                D.kp2mp, D.score, D.nm2, s));
@@ -676,16 +848,25 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz)
         FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, s));
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
-                               fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, s));
+                               fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, s,
+                               sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel));
         // SearchAdditionalMatchesInFrame
-        FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview, s));
+        if (sclk) {
+            FE_RC(gf::frustum_clocked(ctx, fi, B, D.Tcw, D.map, nullptr, D.left, D.nlist_viz, M, 0.5f, D.views,
+                                      fe->nview, clock(D.t_sel0, GF_CK_OFF_SA(M, R)), D.vtmp, s));
+        } else {
+            FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview,
+                                      s));
+        }
         {
             GF_PROF(ctx, s, "k_fe_viz_exclude");
             k_fe_viz_exclude<<<B, 256, 0, s>>>(D);
             GF_HIP(hipGetLastError());
         }
-        FE_RC(gf_match_project_list_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, M, D.left, D.nlist,
-                                        0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA), s));
+        FE_RC(gf::match_project_list_budget(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, M, D.left,
+                                            D.nlist, 0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA),
+                                            sclk ? clock(D.t_sel0, GF_CK_OFF_BUD(M, R)) : gf::StageClock{},
+                                            D.rest2, fe->qres, fe->qold, fe->merr, s));
     }
     if (D.refmap) {
         {
@@ -717,6 +898,9 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     GF_CHECK(ctx && p && out, GF_ERR_ARG, "null arg");
     GF_CHECK(p->batch > 0 && p->map_cap > 0 && p->map_cap <= 4096, GF_ERR_ARG, "batch / map_cap out of range");
     GF_CHECK(p->nlevels >= 1 && p->nlevels <= 16 && p->dt > 0, GF_ERR_ARG, "bad front-end parameters");
+    GF_CHECK(!ctx->track_stream, GF_ERR_ARG,
+             "the context's front end runs tracking on its own stream (gf_frontend_set_track_priority): "
+             "use another context");
     GF_HIP(hipSetDevice(ctx->device));
     gf_frontend* fe = new gf_frontend();
     fe->ctx = ctx;
@@ -822,7 +1006,24 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     F(-1, uint8_t, (size_t)B * M, fe->mp_updated);
     F(-1, int32_t, B, fe->nview);
     F(-1, int32_t, 1, D.step);
-    F(-1, unsigned long long, B, D.t0);
+    // time budgets: timers, caps and the clock record
+    D.ck_R = std::max(p->gf_budget, 1);
+    D.ck_stride = GF_CK_WORDS((long long)M, (long long)D.ck_R);
+    F(GF_FE_CLOCK, long long, (size_t)B * D.ck_stride, D.clk);
+    F(-1, unsigned long long, B, D.t_frame);
+    F(-1, unsigned long long, B, D.t_viz0);
+    F(-1, unsigned long long, B, D.t_mat0);
+    F(-1, unsigned long long, B, D.t_sel0);
+    F(-1, long long, B, D.viz_time);
+    F(-1, long long, B, D.cap2_mi);
+    F(-1, long long, B, D.rest2);
+    F(-1, long long, B, D.cap2_sel);
+    F(-1, gf_mp_view, (size_t)B * M, D.vtmp);
+    F(-1, int32_t, B, D.ncut);
+    F(-1, int32_t, B, D.nlist0);
+    F(-1, int32_t, (size_t)B * M, fe->qres);
+    F(-1, int32_t, (size_t)B * M, fe->qold);
+    F(-1, int32_t, B, fe->merr);
     // the stream maps; the working arrays alias them until a keyframe graph is set
     fe->gm = MapArrays{map, mdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
     fe->g_nmp = nmp;
@@ -858,6 +1059,7 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     if (hipMemcpy(D.Tcw_last, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(D.V, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(gf::fail(GF_ERR_HIP, "upload poses"));
+    ctx->frontends++;
     *out = fe;
     return GF_OK;
 }
@@ -866,7 +1068,9 @@ int gf_frontend_destroy(gf_frontend* fe) {
     if (!fe) return GF_OK;
     (void)hipSetDevice(fe->ctx->device);
     (void)hipStreamSynchronize(fe->ctx->stream);
+    fe->ctx->frontends--;
     if (fe->ts) {
+        fe->ctx->track_stream = false;
         (void)hipStreamSynchronize(fe->ts);
         (void)hipEventDestroy(fe->ev_extracted);
         (void)hipEventDestroy(fe->ev_tracked);
@@ -1120,18 +1324,26 @@ int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event) {
     GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot be gated");
     fe->gate_wait = (hipEvent_t)wait_event;
     fe->gate_done = (hipEvent_t)done_event;
-    // the next group's extraction may start once this one's stage
-    // GF_GATE_STAGE (0 resize .. 4 describe, the default) is done
-    const char* e = std::getenv("GF_GATE_STAGE");
-    fe->gate_stage = e ? std::max(0, std::min(4, std::atoi(e))) : 4;
     return gf::extract_stage_event(fe->ex, fe->gate_done && fe->gate_stage < 4 ? done_event : nullptr,
                                    fe->gate_stage);
+}
+
+int gf_frontend_set_gate_stage(gf_frontend* fe, int stage) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(stage >= 0 && stage <= 4, GF_ERR_ARG, "gate stage must be 0 (resize) .. 4 (describe)");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot be gated");
+    fe->gate_stage = stage;
+    return gf::extract_stage_event(fe->ex, fe->gate_done && stage < 4 ? (void*)fe->gate_done : nullptr, stage);
 }
 
 int gf_frontend_set_track_priority(gf_frontend* fe, int priority) {
     GF_CHECK(fe, GF_ERR_ARG, "null front end");
     GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end cannot change streams");
     GF_CHECK(!fe->ts, GF_ERR_ARG, "the tracking stream is already set");
+    // the tracking kernels use the context's scratch slots: a second front end
+    // on the context would run its kernels concurrently on the same buffers
+    GF_CHECK(fe->ctx->frontends == 1, GF_ERR_ARG,
+             "a front end with a tracking stream needs a context of its own (another front end shares it)");
     GF_HIP(hipSetDevice(fe->ctx->device));
     int least = 0, greatest = 0;
     GF_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -1140,6 +1352,7 @@ int gf_frontend_set_track_priority(gf_frontend* fe, int priority) {
     GF_HIP(hipStreamCreateWithPriority(&fe->ts, hipStreamNonBlocking, pr));
     GF_HIP(hipEventCreateWithFlags(&fe->ev_extracted, hipEventDisableTiming));
     GF_HIP(hipEventCreateWithFlags(&fe->ev_tracked, hipEventDisableTiming));
+    fe->ctx->track_stream = true;
     return GF_OK;
 }
 

@@ -334,6 +334,7 @@ struct ActiveArgs {
     int32_t* ovf;              // two-pass launch: [0] = count, [1 + k] = k-th frame whose pool
                                // did not fit the first pass's LDS
     int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
+    gf::ActiveClock ck;        // the front end's time cap (ck.mat_t0 null: none)
 };
 
 // ---------------------------------------------------------------------------
@@ -933,6 +934,22 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
     int32_t* left = A.left + (long long)f * A.mp_cap;
     const int num_to_match = A.num_to_match[f];
+    // time cap (Observability.cc:1260, 1275-1277): time_for_match from
+    // time_Mat_Online (Tracking.cc:3311 -> here) and time_Viz; <= 0 is the early exit
+    const bool clocked = A.ck.mat_t0 != nullptr;
+    unsigned long long t_am0 = 0;
+    long long am_cap = 0;
+    long long* rec = clocked ? A.ck.rec + (long long)f * A.ck.stride : nullptr;
+    if (clocked) {
+        t_am0 = __builtin_amdgcn_s_memrealtime();
+        const long long mat = (long long)(t_am0 - A.ck.mat_t0[f]);
+        am_cap = A.ck.match_ticks - mat - A.ck.viz[f];
+        if (lane == 0) {
+            rec[GF_CK_MAT_ONLINE] = mat;
+            rec[GF_CK_AM_CUT] = -1;
+        }
+    }
+    bool cut = false;
     // the keypoint grid comes from k_onepoint_pre (HBM; only rescans read it)
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
@@ -944,7 +961,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     AM_T(0);
 
     // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
-    const bool early = (m == 0 || num_to_match <= 0);
+    const bool early = (m == 0 || num_to_match <= 0 || (clocked && am_cap <= 0));
     int N = 0;
     for (int base = 0; base < m; base += AW) {
         const int i = base + lane;
@@ -1025,6 +1042,36 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     for (int round = 0; round < num_to_match; ++round) {
         const int sz = __builtin_amdgcn_readfirstlane(min(S, N));
         if (sz == 0) break;  // empty heap: early termination
+        if (clocked) {
+            // the time cap, read at the round's start; the reference checks it
+            // after each accepted draw (Observability.cc:1362-1370), so a late
+            // round ends at its first accepted draw: matches so far stand, no
+            // leftovers (the return skips mLeftMapPoints)
+            const long long e = (long long)(__builtin_amdgcn_s_memrealtime() - t_am0);
+            if (lane == 0 && round < A.ck.rounds) rec[A.ck.off + round] = e;
+            if (e > am_cap) {
+                uint32_t sd = rs, s0, o0;
+                int tries = 0, run = 0, nc = 0, exh_at = -1;
+                while (nc < 1 && exh_at < 0) {
+                    if (lane == 0) s_exh = -1;
+                    __syncthreads();
+                    nc = __builtin_amdgcn_readfirstlane(
+                        nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+                    exh_at = __builtin_amdgcn_readfirstlane(s_exh);
+                }
+                // an accepted draw before the draws gave out: the cap fires there;
+                // otherwise the draws gave out first (early termination, :1437)
+                const int T = nc >= 1 ? __builtin_amdgcn_readfirstlane(C.tries[0]) : exh_at;
+                for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
+                used += T;
+                if (nc >= 1) {
+                    cut = true;
+                    if (lane == 0) rec[GF_CK_AM_CUT] = round;
+                }
+                __syncthreads();
+                break;
+            }
+        }
         // -- draws, ahead of need
         uint32_t sd = rs;
         int tries = 0, run = 0, nc = 0, evald = 0, exh_at = -1;
@@ -1415,7 +1462,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     }
     // ---- outputs: claims, left-over pool (alive slots in order), RNG state
     for (int i = lane; i < n; i += AW) kp2mp[i] = claim[i];
-    for (int w = 0; w < 64; w++) {
+    if (cut) N = 0;
+    for (int w = 0; w < 64 && !cut; w++) {
         const unsigned long long bits = pbits[w];
         if (((bits >> lane) & 1ull) && w * 64 + lane < PC)
             left[ppre[w] + __popcll(bits & ((1ull << lane) - 1ull))] = lmk[w * 64 + lane];
@@ -1680,8 +1728,9 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
                          const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
                          const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
                          int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
-                         const int32_t* d_remap, void* stream) {
+                         const int32_t* d_remap, void* stream, const gf::ActiveClock& ck) {
     GF_CHECK(ctx && fi && level_sigma2, GF_ERR_ARG, "null arg");
+    GF_CHECK(!ck.mat_t0 || (ck.viz && ck.rec), GF_ERR_ARG, "bad clock");
     GF_CHECK(kp_cap <= KP_MAX && mp_cap <= 32767, GF_ERR_UNSUPPORTED, "frame exceeds active-matching limits");
     GF_CHECK(fi->nlevels >= 1 && fi->nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
     if (nframes <= 0) return GF_OK;
@@ -1712,6 +1761,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.nmatched = d_nmatched;
     A.nldet = d_nldet;
     A.remap = d_remap;
+    A.ck = ck;
     void* err;
     int rc = gf::ws_get(ctx, 30, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
@@ -2077,9 +2127,19 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
                                const int32_t* __restrict__ nmp, int map_stride, int check_viz,
                                const gf_mp_view* __restrict__ views, int32_t* __restrict__ upd_id, int frame_id,
                                double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
-                               uint8_t* __restrict__ updated_out, const int32_t* __restrict__ remap) {
+                               uint8_t* __restrict__ updated_out, const int32_t* __restrict__ remap,
+                               gf::StageClock ck, const long long* __restrict__ cap2) {
     const int f = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool late = false;
+    if (ck.t0) {  // the time cap, one clock read per 64-point batch (Observability.cc:573-578)
+        const int w = i >> 6;
+        if (w * 64 < nmp[f]) {
+            const long long e = (long long)(__builtin_amdgcn_s_memrealtime() - ck.t0[f]);
+            if ((threadIdx.x & 63) == 0) ck.rec[(long long)f * ck.stride + ck.off + w] = e;
+            late = 2 * e > cap2[f];
+        }
+    }
     if (i >= map_stride) return;
     const long long g = (long long)f * map_stride + i;
     if (i >= nmp[f]) {
@@ -2087,7 +2147,7 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
         return;
     }
     int u = upd_id[g];
-    const bool skip = (u == frame_id) || (!check_viz && views && !views[g].in_view);
+    const bool skip = late || (u == frame_id) || (!check_viz && views && !views[g].in_view);
     if (!skip) {
         const double y[3] = {mpos[3 * g], mpos[3 * g + 1], mpos[3 * g + 2]};
         double H[14];
@@ -2176,15 +2236,16 @@ int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const
 int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
                      const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
                      int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated,
-                     const int32_t* d_remap, void* stream) {
+                     const int32_t* d_remap, void* stream, const gf::StageClock& ck, const long long* d_cap2) {
     GF_CHECK(ctx && cam, GF_ERR_ARG, "null arg");
     if (nframes <= 0 || map_stride <= 0) return GF_OK;
     GF_CHECK(d_Xv && d_map_pos && d_nmp && d_upd_id && d_H && d_info && d_uv, GF_ERR_ARG, "null arg");
+    GF_CHECK(!ck.t0 || (ck.rec && d_cap2 && map_stride <= 4096), GF_ERR_ARG, "bad clock");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_map_info");
     k_obs_map_info<<<dim3((map_stride + 127) / 128, nframes), 128, 0, s>>>(
         *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated,
-        d_remap);
+        d_remap, ck, d_cap2);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -61,6 +61,15 @@ struct MatchArgs {
     const struct SeqPre* pre;  // [F][q_cap] MODE_LAST: each query against the starting claims
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (k_match_seq_pre writes, rescans read)
     int* grid_items;           // [F][kp_cap]
+    // SearchByProjection_Budget's clock (list mode, gf_set_budgets; null: none):
+    // the visibility pass's timer start per frame, 2 x timeCost_rest in ticks,
+    // the clock record and scratch for undoing the claims after the cut
+    const unsigned long long* ck_t0;
+    const long long* ck_rest2;
+    long long* ck_rec;
+    long long ck_stride;
+    int ck_off;       // offset of the per-point array in a stream's record
+    int32_t* ck_old;  // [F][q_cap] score a query's claim overwrote
 };
 
 
@@ -222,7 +231,27 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
 
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], kc);
-    const int nq = min(A.list ? A.nlist[f] : A.m[f], min(A.q_cap, Q_MAX));
+    int nq = min(A.list ? A.nlist[f] : A.m[f], min(A.q_cap, Q_MAX));
+    // SearchByProjection_Budget (ORBmatcher.cc:281-288, 366-371): the budget
+    // left after the visibility pass; none left: return at once
+    const bool clocked = A.ck_t0 != nullptr;
+    __shared__ unsigned long long s_now0;
+    __shared__ long long s_constr2;
+    __shared__ int s_cut;
+    long long* rec = clocked ? A.ck_rec + (long long)f * A.ck_stride : nullptr;
+    if (clocked) {
+        if (tid == 0) {
+            const unsigned long long now0 = __builtin_amdgcn_s_memrealtime();
+            const long long so_far = (long long)(now0 - A.ck_t0[f]);
+            s_now0 = now0;
+            s_constr2 = A.ck_rest2[f] - 2 * so_far;
+            s_cut = INT_MAX;
+            rec[GF_CK_SA_SOFAR] = so_far;
+            rec[GF_CK_BUDGET_CUT] = -1;
+        }
+        __syncthreads();
+        if (s_constr2 <= 0) nq = 0;
+    }
     const gf_keypoint* K = A.kps + (long long)f * A.kp_cap;
     const uint8_t* D = A.desc + (long long)f * A.kp_cap * 32;
     int32_t* kp2mp = A.kp2mp + (long long)f * A.kp_cap;
@@ -268,6 +297,8 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
         if (tid == 0) s_any = 0;
         __syncthreads();
         for (int k = tid; k < nq; k += MATCH_THREADS) {
+            if (clocked && rounds == 0)  // per point, from the matcher's start
+                rec[A.ck_off + k] = (long long)(__builtin_amdgcn_s_memrealtime() - s_now0);
             if (done[k]) continue;
             const Query q = make_query(A, fc, f, k);
             if (!q.valid) continue;
@@ -290,7 +321,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             if (done[k]) continue;
             const Query q = make_query(A, fc, f, k);
             int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
-            bool ok = true;
+            bool ok = true, near = false;
             if (q.valid) {
                 for (int ix = q.cx0; ix <= q.cx1 && ok; ix++) {
                     const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
@@ -301,6 +332,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
                         cand(idx, kx, ky, ko);
                         if (!level_ok(ko, q.minL, q.maxL)) continue;
                         if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
+                        near = true;  // GetFeaturesInArea lists it (claimed or not)
                         if (__hip_atomic_load(&claim[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
                             continue;
                         if (minU[idx] != k) {
@@ -327,17 +359,23 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             }
             done[k] = 1;
             int res = -1;
+            bool reject = false;
             if (q.valid && bestDist <= TH_HIGH) {
-                bool reject = A.mode == MODE_PROJECT && bestLevel == bestLevel2 &&
-                              (float)bestDist > A.nnratio * (float)bestDist2;
+                reject = A.mode == MODE_PROJECT && bestLevel == bestLevel2 &&
+                         (float)bestDist > A.nnratio * (float)bestDist2;
                 if (!reject) {
                     __hip_atomic_store(&claim[bestIdx], q.id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (clocked) A.ck_old[(long long)f * A.q_cap + k] = score[bestIdx];
                     score[bestIdx] = bestDist;
                     atomicAdd(&s_nm, 1);
                     res = bestIdx;
                 }
             }
-            if (A.mode == MODE_LAST) A.qres[(long long)f * A.q_cap + k] = res;
+            if (A.mode == MODE_LAST || clocked) A.qres[(long long)f * A.q_cap + k] = res;
+            // the points that reach SearchByProjection_Budget's clock check
+            // (ORBmatcher.cc:366-371): in view, a non-empty area, not rejected
+            // by the ratio test
+            if (clocked && q.valid && near && !reject) done[k] = 2;
         }
         __syncthreads();
         if (!s_any) break;
@@ -348,6 +386,27 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
         __syncthreads();
     }
 
+    if (clocked) {
+        // the break: the first checked point whose elapsed >= the budget left;
+        // later points' claims are undone (they never ran; claims of earlier
+        // points do not depend on them)
+        __syncthreads();
+        for (int k = tid; k < nq; k += MATCH_THREADS)
+            if (done[k] == 2 && 2 * rec[A.ck_off + k] >= s_constr2) atomicMin(&s_cut, k);
+        __syncthreads();
+        const int c = s_cut;
+        if (c != INT_MAX) {
+            for (int k = c + 1 + tid; k < nq; k += MATCH_THREADS) {
+                const int r = A.qres[(long long)f * A.q_cap + k];
+                if (r < 0) continue;
+                claim[r] = -1;
+                score[r] = A.ck_old[(long long)f * A.q_cap + k];
+                atomicSub(&s_nm, 1);
+            }
+            if (tid == 0) rec[GF_CK_BUDGET_CUT] = c;
+        }
+        __syncthreads();
+    }
     // ---- rotation consistency (ORBmatcher.cc:2146-2190)
     if (A.mode == MODE_LAST && A.check_ori) rotation_filter(A, f, nq, K, claim, score, &s_nm, s_hist, s_keep, MATCH_THREADS);
     for (int i = tid; i < n; i += MATCH_THREADS) kp2mp[i] = claim[i];
@@ -684,15 +743,31 @@ size_t seq_lds_bytes(int kp_cap, int q_cap) {
 }
 
 // ---- Frame::isInFrustum (Frame.cc:166-227), one thread per map point.
+// Clocked form (the front end's time budgets, gf_set_budgets): each point's
+// elapsed time since the loop's timer start ck_t0[f] is written to the clock
+// record at its list position, and the result goes to `alt` (same indexing as
+// views): the front end keeps it only for the points before the cut.
+struct FrustumClock {
+    const unsigned long long* t0;  // null: not clocked
+    long long* rec;
+    long long stride;
+    int off;
+    gf_mp_view* alt;
+};
+
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
                           const int32_t* __restrict__ m, int cap, float viewCosLimit, gf_mp_view* __restrict__ views,
                           int32_t* __restrict__ nview, const int32_t* __restrict__ list,
-                          const int32_t* __restrict__ nlist) {
+                          const int32_t* __restrict__ nlist, FrustumClock ck) {
     const int f = blockIdx.y;
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     const float* T = Tcw + 16 * f;
     int in = 0;
     const bool run = list ? i < nlist[f] : i < m[f];
+    if (run && ck.t0) {
+        ck.rec[(long long)f * ck.stride + ck.off + i] = (long long)(__builtin_amdgcn_s_memrealtime() - ck.t0[f]);
+        views = ck.alt;
+    }
     if (run && list) i = list[(long long)f * cap + i];  // the list's map point
     if (run) {
         gf_mp_view v;
@@ -818,7 +893,8 @@ int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const floa
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, "k_frustum");
     k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
-                                                                   d_views, d_nview, nullptr, nullptr);
+                                                                   d_views, d_nview, nullptr, nullptr,
+                                                                   FrustumClock{});
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -836,7 +912,8 @@ int gf_frustum_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, "k_frustum_list");
     k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, nullptr, mp_cap, view_cos_limit,
-                                                                   d_views, d_nview, d_list, d_nlist);
+                                                                   d_views, d_nview, d_list, d_nlist,
+                                                                   FrustumClock{});
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -1062,3 +1139,66 @@ int gf_descriptor_distance(gf_ctx* ctx, const uint8_t* a, const uint8_t* b, int 
 }
 
 }  // extern "C"
+
+// Front-end forms with the time-budget clocks (frontend.hip, gf_set_budgets).
+int gf::frustum_clocked(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw,
+                        const gf_map_point* d_mps, const int32_t* d_m, const int32_t* d_list, const int32_t* d_nlist,
+                        int mp_cap, float view_cos_limit, gf_mp_view* d_views, int32_t* d_nview,
+                        const gf::StageClock& ck, gf_mp_view* d_alt, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    if (nframes <= 0 || mp_cap <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const FrameConst fc = gf::make_frame_const(fi);
+    GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
+    GF_PROF(ctx, s, d_list ? "k_frustum_list" : "k_frustum");
+    const FrustumClock fk{ck.t0, ck.rec, ck.stride, ck.off, d_alt};
+    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
+                                                                   d_views, d_nview, d_list, d_nlist,
+                                                                   ck.t0 ? fk : FrustumClock{});
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+int gf::match_project_list_budget(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                                  const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                                  const uint8_t* d_mp_desc, int mp_cap, const int32_t* d_list, const int32_t* d_nlist,
+                                  float th, float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches,
+                                  const gf::StageClock& ck, const long long* d_rest2, int32_t* d_qres,
+                                  int32_t* d_old, int32_t* d_err, void* stream) {
+    GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
+    int rc = check_fi(fi);
+    if (rc) return rc;
+    GF_CHECK(kp_cap <= KP_MAX && mp_cap <= Q_MAX, GF_ERR_UNSUPPORTED, "frame exceeds matcher limits (4096 kps, 8192 mps)");
+    if (nframes <= 0) return GF_OK;
+    MatchArgs A{};
+    A.mode = MODE_PROJECT;
+    A.kps = d_kps;
+    A.desc = d_desc;
+    A.n = d_n;
+    A.kp_cap = kp_cap;
+    A.views = d_views;
+    A.qdesc = d_mp_desc;
+    A.m = d_nlist;
+    A.q_cap = mp_cap;
+    A.list = d_list;
+    A.nlist = d_nlist;
+    A.th = th;
+    A.nnratio = nnratio;
+    A.kp2mp = d_kp2mp;
+    A.score = d_score;
+    A.nmatches = d_nmatches;
+    A.err = d_err;
+    if (ck.t0) {
+        GF_CHECK(d_rest2 && d_qres && d_old && ck.rec, GF_ERR_ARG, "null clock arg");
+        A.ck_t0 = ck.t0;
+        A.ck_rest2 = d_rest2;
+        A.ck_rec = ck.rec;
+        A.ck_stride = ck.stride;
+        A.ck_off = ck.off;
+        A.ck_old = d_old;
+        A.qres = d_qres;
+    }
+    return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
+}

@@ -62,11 +62,27 @@ FIELDS = {
     "rng": (28, np.uint8, (ctypes.sizeof(Rng),)),
     "left": (29, np.int32, ("M",)),
     "stats": (30, np.int32, None),  # [NSTAT][B]
-    "hist": (31, np.int32, (8,)),  # running counters: steps per branch [0..5], log-dets [6], local matches [7]
+    "hist": (31, np.int32, (8,)),  # running counters: steps per branch [0..4], steps cut by a time cap [5],
+                                   # log-dets [6], local matches [7]
+    "clock": (32, np.int64, ("CK",)),  # budget clock record of the last step (abi.h GF_CK_*)
 }
 STATS = ["m3", "found", "to_match", "branch", "in_view", "local", "inl1", "inl2", "extra", "nleft", "iter1",
-         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal"]
+         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal", "ncut"]
 NSTAT = len(STATS)
+
+# GF_FE_CLOCK layout (abi.h GF_CK_*): header words, then per-stage elapsed-time
+# arrays; M = map capacity, R = max(gf_budget, 1)
+CK = {"flags": 0, "match": 1, "select": 2, "viz_cut": 3, "viz_time": 4, "mat_online": 5, "am_cut": 6, "sofar": 7,
+      "sa_cut": 8, "sa_sofar": 9, "budget_cut": 10}
+CK_HEADER = 16
+
+
+def ck_offsets(M: int, R: int) -> dict:
+    """Offsets of the clock record's arrays: isInFrustum points, MAP_INFO
+    batches (active branch), active-matching rounds, MAP_INFO batches
+    (kinematic[1]), visibility-pass points, SearchByProjection_Budget points."""
+    return {"viz": CK_HEADER, "mi": CK_HEADER + M, "am": CK_HEADER + M + 64, "sel": CK_HEADER + M + 64 + R,
+            "sa": CK_HEADER + M + 128 + R, "bud": CK_HEADER + 2 * M + 128 + R, "words": CK_HEADER + 3 * M + 128 + R}
 
 
 class FrontendParams(ctypes.Structure):
@@ -86,11 +102,12 @@ class FrontendParams(ctypes.Structure):
                    1 if gf else 0, 1.0 / fps)
 
 
-def field_shape(name: str, B: int, cap: int, M: int):
+def field_shape(name: str, B: int, cap: int, M: int, R: int = 1):
     fid, dt, shp = FIELDS[name]
     if shp is None:
         return fid, dt, (NSTAT, B)
-    return fid, dt, (B,) + tuple(cap if s == "cap" else M if s == "M" else s for s in shp)
+    dims = {"cap": cap, "M": M, "CK": ck_offsets(M, R)["words"]}
+    return fid, dt, (B,) + tuple(dims.get(s, s) for s in shp)
 
 
 class GateEvent:
@@ -129,6 +146,7 @@ class FrontEnd:
         self.params = FrontendParams.make(camera, nfeatures, batch, map_size, gf_budget, gf, fps)
         self.cam = synth.CAMERAS[camera]
         self.B, self.M = batch, map_size
+        self.R = max(gf_budget, 1)
         if ctx is None:
             import torch
 
@@ -209,6 +227,11 @@ class FrontEnd:
         check(lib().gf_frontend_set_gate(self.handle, wait_event.handle if wait_event else None,
                                          done_event.handle if done_event else None))
 
+    def set_gate_stage(self, stage: int) -> None:
+        """gf_frontend_set_gate_stage: record the gate's done event after
+        extraction stage `stage` (0 resize .. 4 describe, the default)."""
+        check(lib().gf_frontend_set_gate_stage(self.handle, int(stage)))
+
     def set_track_priority(self, priority: int = -1) -> None:
         """gf_frontend_set_track_priority: tracking kernels on a stream of HIP
         priority `priority` (lower = more urgent)."""
@@ -222,13 +245,13 @@ class FrontEnd:
 
     # ------------------------------------------------------------ state
     def read(self, name: str) -> np.ndarray:
-        fid, dt, shape = field_shape(name, self.B, self.cap, self.M)
+        fid, dt, shape = field_shape(name, self.B, self.cap, self.M, self.R)
         out = np.zeros(shape, dt)
         check(lib().gf_frontend_read(self.handle, fid, ptr(out), out.nbytes))
         return out
 
     def write(self, name: str, arr: np.ndarray) -> None:
-        fid, dt, shape = field_shape(name, self.B, self.cap, self.M)
+        fid, dt, shape = field_shape(name, self.B, self.cap, self.M, self.R)
         a = np.ascontiguousarray(arr, dt).reshape(shape)
         check(lib().gf_frontend_write(self.handle, fid, ptr(a), a.nbytes))
 

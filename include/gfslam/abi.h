@@ -862,13 +862,21 @@ typedef struct gf_frontend gf_frontend;
 // A gated front end cannot be captured as a graph (gf_frontend_capture
 // refuses), nor can a captured one be gated.
 int gf_frontend_set_gate(gf_frontend* fe, void* wait_event, void* done_event);
+// The extraction stage after which the gate's done event is recorded: 0
+// resize, 1 blur + FAST map, 2 cells, 3 select, 4 describe (the default, the
+// whole extraction). An earlier stage lets the next front end's extraction
+// start sooner (overlapping this one's later stages).
+int gf_frontend_set_gate_stage(gf_frontend* fe, int stage);
 // Tracking stream: the step's kernels after extraction run on a stream of
 // their own created with HIP stream priority `priority` (clamped to the
 // device's range; lower = more urgent), forked from and joined back into the
 // context's stream each step, so results and ordering are unchanged. With
 // several front ends on one GPU a high priority lets one front end's
 // latency-bound tracking kernels take compute units ahead of another's
-// extraction kernels. Once per front end; not with gf_frontend_capture.
+// extraction kernels. Once per front end; not with gf_frontend_capture. The
+// tracking kernels use the context's scratch slots, so the front end must be
+// the only one on its context (GF_ERR_ARG otherwise, and gf_frontend_create
+// then refuses a second front end on that context).
 int gf_frontend_set_track_priority(gf_frontend* fe, int priority);
 // A hipEvent_t (timing disabled) on the context's device, for the gate.
 int gf_event_create(gf_ctx* ctx, void** event_out);
@@ -908,15 +916,18 @@ enum {
     GF_FE_LEFT,         /* [B][M] i32 mLeftMapPoints of the last step       */
     GF_FE_STATS,        /* [GF_FE_NSTAT][B] i32, see GF_ST_*                */
     GF_FE_HIST,         /* [B][8] i32 running counters since the last write:
-                           [0..5] steps per GF_ST_BRANCH value, [6] logDet
-                           evaluations, [7] local-map search matches         */
+                           [0..4] steps per GF_ST_BRANCH value, [5] steps in
+                           which a time cap fired, [6] logDet evaluations,
+                           [7] local-map search matches                      */
+    GF_FE_CLOCK,        /* [B][GF_CK_WORDS(M, budget)] i64 budget clock record
+                           of the last step (see gf_set_budgets)             */
     GF_FE_NFIELDS
 };
 enum {
     GF_ST_M3 = 0,       /* SearchByProjection(Cur, Last) matches            */
     GF_ST_FOUND,        /* nMatchesFound after the outlier discard          */
     GF_ST_TO_MATCH,     /* num_to_match = budget - nMatchesFound            */
-    GF_ST_BRANCH,       /* 1 leftovers only, 2 SearchByProjection, 3 active matching, 4 nothing in view */
+    GF_ST_BRANCH,       /* 1 leftovers only, 2 SearchByProjection, 3 active matching, 4 nToMatch = 0 */
     GF_ST_IN_VIEW,      /* nToMatch                                         */
     GF_ST_LOCAL,        /* matches of the local-map search (M2 or active)   */
     GF_ST_INL1,         /* inliers of the first PoseOptimization            */
@@ -926,11 +937,17 @@ enum {
     GF_ST_ITER1, GF_ST_ITER2, GF_ST_EDGES1, GF_ST_EDGES2,
     GF_ST_FLAGS,        /* 1: M3 < 20 (TrackPreviousFrame fall-back), 2: < 10 after PoseOptimization,
                            4: mnMatchesInliers < 15 (LOST), 8: a time budget cut a loop,
-                           16: the cut fell on SearchAdditionalMatchesInFrame (no time left) */
+                           16: timeCost_rest <= 0 (RunMapPointsSelection and
+                           SearchByProjection_Budget return at once),
+                           32: isInFrustum cap, 64: MAP_INFO cap (active branch),
+                           128: runActiveMapMatching cap, 256: MAP_INFO cap of
+                           RunMapPointsSelection, 512: visibility cap of
+                           SearchAdditionalMatchesInFrame, 1024: SearchByProjection_Budget cap */
     GF_ST_FRAMES,       /* frames tracked                                   */
     GF_ST_LDETS,        /* logDet evaluations of runActiveMapMatching (heap
                            pushes, Observability.cc:1373): SURVEY §8d E_ld  */
     GF_ST_NLOCAL,       /* mvpLocalMapPoints size (keyframe graphs only)    */
+    GF_ST_NCUT,         /* local points the isInFrustum cap moved to mLeftMapPoints */
     GF_FE_NSTAT
 };
 int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);
@@ -985,14 +1002,67 @@ int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes
 /* Size and device pointer of a field. */
 int gf_frontend_field(gf_frontend* fe, int field, size_t* bytes, void** d_ptr);
 
-/* Wall-clock budgets of the reference's time-capped loops, in seconds:
- * match_s = time_total_match (Tracking.cc:3230; the isInFrustum cap at half of
- * it :3262-3270, runActiveMapMatching's cap :1366-1370), select_s = the
- * post-publish budget of SearchAdditionalMatchesInFrame /
- * SearchByProjection_Budget (Tracking.cc:3113-3137, ORBmatcher.cc:366-371).
- * +inf (the default) is parity mode: no loop is cut. Measured on the device
- * clock from the start of the frame's step. */
+/* Wall-clock budgets of the reference's time-capped loops, in seconds; +inf
+ * (the default) is parity mode: no loop is cut and no clock is read.
+ *   match_s  = time_total_match (Tracking.cc:3230, 0.015 in the reference).
+ *   select_s = the post-publish frame budget 1/(0.5 fps) - 0.002
+ *              (Tracking.cc:866, 0.098 at 20 fps); timeCost_rest =
+ *              select_s - timeCost_sofar.
+ * Every cap is the reference's rule on the device's real-time clock
+ * (s_memrealtime, 100 MHz ticks), each timer started where the reference
+ * starts it, at the granularity given:
+ *   isInFrustum loop (Tracking.cc:3251-3270): timer at the loop start; point i
+ *     (skipping points matched this frame) cuts when its elapsed > match/2:
+ *     points i.. go to mLeftMapPoints and leave mvpLocalMapPoints. Per point
+ *     (a wave's 64 points read the clock once). time_Viz = the last value the
+ *     loop compared.
+ *   MAP_INFO build (Tracking.cc:3331 -> Observability.cc:564-578), cap
+ *     (match - time_Viz)/2 on a timer started after the loop (:3311); per
+ *     64-point batch.
+ *   runActiveMapMatching (Tracking.cc:3343-3344 -> Observability.cc:1260,
+ *     1275-1277, 1366-1370), cap match - time_Mat_Online - time_Viz (<= 0:
+ *     the early exit); the clock is read at each round's start and the cut
+ *     takes effect at that round's first accepted draw (where the reference
+ *     first checks in a round): matches so far stand, no leftovers.
+ *   timeCost_sofar from the frame's start (after the extraction gate wait,
+ *     so queueing behind other front ends does not count).
+ *   RunMapPointsSelection (Tracking.cc:1727-1779): returns when
+ *     timeCost_rest <= 0, else MAP_INFO at kinematic[1] capped at
+ *     timeCost_rest; per 64-point batch.
+ *   SearchAdditionalMatchesInFrame (Tracking.cc:3097-3137): visibility pass
+ *     cut at timeCost_rest/2 per list point (mLeftMapPoints erased from
+ *     there); SearchByProjection_Budget (ORBmatcher.cc:281-282, 366-371)
+ *     returns when timeCost_rest - time_so_far <= 0, else breaks after the
+ *     first point that reaches its clock check with elapsed >= that
+ *     (per point, elapsed from the matcher's start).
+ * The elapsed values every rule compared are written to GF_FE_CLOCK, so a
+ * CPU replay can apply the same rules (oracle/chain.cpp) and check the cut
+ * positions rather than be told them. */
 int gf_set_budgets(gf_ctx* ctx, double match_s, double select_s);
+
+/* GF_FE_CLOCK record of one stream (int64 words, ticks of 10 ns; -1 = not
+ * reached). M = map_cap, R = max(gf_budget, 1) (rounds <= num_to_match). */
+enum {
+    GF_CK_FLAGS = 0,    /* bit 0 match budget on, bit 1 select budget on   */
+    GF_CK_MATCH,        /* time_total_match in ticks                        */
+    GF_CK_SELECT,       /* select budget in ticks                           */
+    GF_CK_VIZ_CUT,      /* isInFrustum: position of the cut (list size when none) */
+    GF_CK_VIZ_TIME,     /* time_Viz                                         */
+    GF_CK_MAT_ONLINE,   /* time_Mat_Online                                  */
+    GF_CK_AM_CUT,       /* round at which the active-matching cap fired, -1 none */
+    GF_CK_SOFAR,        /* timeCost_sofar                                   */
+    GF_CK_SA_CUT,       /* visibility pass cut position in mLeftMapPoints (size when none) */
+    GF_CK_SA_SOFAR,     /* time_so_far before SearchByProjection_Budget     */
+    GF_CK_BUDGET_CUT,   /* list position SearchByProjection_Budget broke after, -1 none */
+    GF_CK_HEADER = 16
+};
+#define GF_CK_OFF_VIZ(M, R) (GF_CK_HEADER)                       /* [M] isInFrustum, per list point  */
+#define GF_CK_OFF_MI(M, R) (GF_CK_HEADER + (M))                  /* [64] MAP_INFO batches (active)    */
+#define GF_CK_OFF_AM(M, R) (GF_CK_HEADER + (M) + 64)             /* [R] active-matching rounds        */
+#define GF_CK_OFF_SEL(M, R) (GF_CK_HEADER + (M) + 64 + (R))      /* [64] MAP_INFO batches (kinematic[1]) */
+#define GF_CK_OFF_SA(M, R) (GF_CK_HEADER + (M) + 128 + (R))      /* [M] visibility pass, per list point */
+#define GF_CK_OFF_BUD(M, R) (GF_CK_HEADER + 2 * (M) + 128 + (R)) /* [M] SearchByProjection_Budget    */
+#define GF_CK_WORDS(M, R) (GF_CK_HEADER + 3 * (M) + 128 + (R))
 
 /* ------------------------------------------------ multi-GPU start-up exchange
  * Config 5: one process per GPU, sequences independent,

@@ -12,6 +12,7 @@
 // layouts as the device front end (B = 1), so a test can copy a device
 // stream's state in, run one frame here and compare every field.
 // Parity mode only: the time budgets are infinite.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -48,6 +49,16 @@ int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, co
                              const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
                              int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
 long long orc_last_ldets(void);
+int orc_obs_active_match_capped(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                                const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
+                                const double* info, const double* H, int m, const double* base,
+                                const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
+                                int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched,
+                                const long long* round_el, int nrec, long long cap, int* cut_round);
+int orc_match_project_list(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                           const gf_mp_view* views, const uint8_t* mp_desc, const int32_t* list, int nlist, float th,
+                           float nnratio, int32_t* kp2mp, int32_t* score, int* nmatches, const long long* el,
+                           long long constr2, int* cut);
 int orc_update_reference(const gf_covis_map* M, int32_t* frame_mps, int nkp, int32_t* local_kfs, int* n_local_kfs,
                          int kf_cap, int32_t* local_mps, int* n_local_mps, int mp_cap, int32_t* ref_kf);
 }
@@ -117,9 +128,11 @@ struct orc_chain {
     gf_rng rng{};
     int32_t stats[GF_FE_NSTAT] = {};
     double tm[8] = {};  // stage seconds of the last step
-    // time-budget cuts the next steps take (orc_chain_set_cuts): the device
-    // decides them on its clock and reports them in GF_ST_BRANCH / GF_ST_FLAGS
-    int cut_frustum = 0, cut_select = 0;
+    // time budgets (orc_chain_set_clock): the clock record of the step to
+    // replay (GF_FE_CLOCK of one device stream); the cap rules of
+    // gf_set_budgets run on the elapsed times it holds. Empty: parity mode.
+    std::vector<long long> clk;
+    int ck_R = 1;
     // keyframe graph (orc_chain_set_covis): UpdateReference every step, the
     // frame tracked against the local map gathered from the stream map
     int refmap = 0, g_nkf = 0;
@@ -198,12 +211,19 @@ void field(orc_chain* c, int f, void** ptr, size_t* bytes) {
 
 // batchInfoMat_Map (Observability.cc:556-644) over points i < m of the map:
 // skip those stamped fid and (check_viz == 0) those not in view; stamp the
-// valid ones. Returns updated flags (updateAtFrameId == fid).
-void map_info(orc_chain* c, const double* Xv, int m, int check_viz, int fid, std::vector<uint8_t>* updated) {
+// valid ones. Returns updated flags (updateAtFrameId == fid). With a time cap
+// (bel != null) the 64-point batch w is skipped when 2 x bel[w] > cap2
+// (:573-578 on the device's per-batch clock reads); *late = a batch was.
+void map_info(orc_chain* c, const double* Xv, int m, int check_viz, int fid, std::vector<uint8_t>* updated,
+              const long long* bel = nullptr, long long cap2 = 0, bool* late = nullptr) {
+    if (late) *late = false;
+    if (bel && late)
+        for (int w = 0; w * 64 < m; w++) *late = *late || 2 * bel[w] > cap2;
     // runMatrixBuilding (Observability.cc:646-713): hardware_concurrency equal
     // grains of the point list, one std::thread each (ORC_THREADS overrides)
     auto grain = [&](int lo, int hi) {
         for (int i = lo; i < hi; i++) {
+            if (bel && 2 * bel[i >> 6] > cap2) continue;
             if (c->upd[i] == fid) continue;
             if (!check_viz && !c->views[i].in_view) continue;
             double H[14], info[49];
@@ -270,22 +290,6 @@ void frustum_list(orc_chain* c, const int32_t* list, int n) {
     }
 }
 
-// SearchByProjection(F, vpMapPoints, th) over a list of map points in list
-// order (lists are ascending here, so the sequential loop over the whole map
-// with the non-members masked visits the members in list order).
-int project_list(orc_chain* c, const int32_t* list, int n, float th) {
-    std::vector<gf_mp_view> v(c->nmp);
-    for (int i = 0; i < c->nmp; i++) {
-        v[i] = c->views[i];
-        v[i].in_view = 0;
-    }
-    for (int k = 0; k < n; k++) v[list[k]].in_view = c->views[list[k]].in_view;
-    int nm = 0;
-    orc_match_project(&c->fi, c->kps.data(), c->desc.data(), c->nkp, v.data(), c->map_desc.data(), c->nmp, th, 0.8f,
-                      c->kp2mp.data(), c->score.data(), &nm);
-    return nm;
-}
-
 }  // namespace
 
 extern "C" {
@@ -299,6 +303,7 @@ orc_chain* orc_chain_create(const gf_frontend_params* p) {
     c->cap = 0;
     for (int l = 0; l < p->nlevels; l++) c->cap += fpl[l];
     c->M = p->map_cap;
+    c->ck_R = std::max(p->gf_budget, 1);
     c->fi = gf_frame_info{0, p->width, 0, p->height, p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
     float sf = 1.f;
     for (int l = 0; l < p->nlevels; l++) {
@@ -421,13 +426,15 @@ int orc_chain_bootstrap(orc_chain* c, const uint8_t* img, const float* Tcw, cons
     return GF_OK;
 }
 
-// The budget cuts of the following steps: cut_frustum = the isInFrustum cap
-// fired on the first local point (Tracking.cc:3262-3270, GF_ST_BRANCH 5),
-// cut_select = no time left for SearchAdditionalMatchesInFrame
-// (ORBmatcher.cc:281-282, GF_ST_FLAGS bit 16).
-int orc_chain_set_cuts(orc_chain* c, int cut_frustum, int cut_select) {
-    c->cut_frustum = cut_frustum;
-    c->cut_select = cut_select;
+// The clock record of the next step (n = GF_CK_WORDS(map_cap, max(budget, 1))
+// int64 words; n = 0 clears it: parity mode).
+int orc_chain_set_clock(orc_chain* c, const long long* rec, size_t n) {
+    if (n == 0) {
+        c->clk.clear();
+        return GF_OK;
+    }
+    if (!rec || n != (size_t)GF_CK_WORDS((long long)c->M, (long long)c->ck_R)) return GF_ERR_ARG;
+    c->clk.assign(rec, rec + n);
     return GF_OK;
 }
 
@@ -570,47 +577,83 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     int branch = 0, nlist = 0;
     bool viz = false;
     std::vector<int32_t> list;
+    // time budgets (gf_set_budgets), replayed on the device's clock record
+    const long long* rec = c->clk.empty() ? nullptr : c->clk.data();
+    const int M = c->M, R = c->ck_R;
+    const bool mclk = gf && rec && (rec[GF_CK_FLAGS] & 1), sclk = gf && rec && (rec[GF_CK_FLAGS] & 2);
+    const long long match_t = rec ? rec[GF_CK_MATCH] : 0, select_t = rec ? rec[GF_CK_SELECT] : 0;
+    // mnLastFrameSeen == mnId: the points matched before the local-map search
+    std::vector<uint8_t> seen(c->nmp, 0);
+    for (int i = 0; i < n; i++)
+        if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) seen[c->kp2mp[i]] = 1;
     if (gf && ntm <= 0) {  // :3231-3249, stale mbTrackInView
         for (int i = 0; i < c->nmp; i++)
             if (c->views[i].in_view) list.push_back(i);
         branch = 1;
         viz = true;
-    } else if (gf && c->cut_frustum) {
-        // isInFrustum time cap (:3262-3270) on the first point: mLeftMapPoints =
-        // the whole local map in order, mbNeedVizCheck, nToMatch = 0 (no search)
-        for (int i = 0; i < c->nmp; i++) list.push_back(i);
-        branch = 5;
-        viz = true;
-        st[GF_ST_FLAGS] |= 8;
     } else {
+        // isInFrustum over mvpLocalMapPoints (:3251-3278); with a match budget
+        // the loop stops at the first point not seen this frame whose elapsed
+        // > time_total_match / 2: those points move to mLeftMapPoints and the
+        // list ends there
+        int mlen = c->nmp;
+        long long tviz = 0;
+        if (mclk) {
+            const long long* el = rec + GF_CK_OFF_VIZ(M, R);
+            int last = -1;
+            for (int i = 0; i < c->nmp; i++) {
+                if (seen[i]) continue;
+                tviz = el[i];
+                last = i;
+                if (2 * el[i] > match_t) {
+                    mlen = i;
+                    break;
+                }
+            }
+            if (last < 0) tviz = 0;
+            for (int i = mlen; i < c->nmp; i++) list.push_back(i);
+            if (mlen < c->nmp) {
+                viz = true;
+                st[GF_ST_FLAGS] |= 8 | 32;
+            }
+            st[GF_ST_NCUT] = c->nmp - mlen;
+        }
         int nv = 0;
-        orc_frustum(&c->fi, c->Tcw, c->map.data(), c->nmp, 0.5f, c->views.data(), &nv);
+        orc_frustum(&c->fi, c->Tcw, c->map.data(), mlen, 0.5f, c->views.data(), &nv);
         for (int i = 0; i < n; i++)
             if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
         int nin = 0;
-        for (int i = 0; i < c->nmp; i++) nin += c->views[i].in_view ? 1 : 0;
+        for (int i = 0; i < mlen; i++) nin += c->views[i].in_view ? 1 : 0;
         st[GF_ST_IN_VIEW] = nin;
         if (nin == 0) {
             branch = 4;
         } else if (!gf || nin < 400) {  // :3322-3323
             branch = 2;
             int k = 0;
-            orc_match_project(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(), c->nmp,
+            orc_match_project(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(), mlen,
                               1.f, 0.8f, c->kp2mp.data(), c->score.data(), &k);
             st[GF_ST_LOCAL] = k;
         } else {  // :3329-3343
             branch = 3;
             std::vector<uint8_t> updated;
-            map_info(c, c->Xv, c->nmp, 0, 1, &updated);
+            bool late = false;
+            // MAP_INFO capped at (time_total_match - time_Viz) / 2 (:3331)
+            map_info(c, c->Xv, mlen, 0, 1, &updated, mclk ? rec + GF_CK_OFF_MI(M, R) : nullptr, match_t - tviz,
+                     &late);
+            if (late) st[GF_ST_FLAGS] |= 8 | 64;
             std::vector<int32_t> left(c->M);
-            int nleft = 0, nmatched = 0;
-            orc_obs_active_match_rng(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(),
-                                     updated.data(), c->mp_info.data(), c->mp_H.data(), c->nmp, c->base,
-                                     c->level_sigma2, ntm, 1.f, 0.8f, &c->rng, c->kp2mp.data(), c->score.data(),
-                                     left.data(), &nleft, &nmatched);
+            int nleft = 0, nmatched = 0, cut_round = -1;
+            // capped at time_total_match - time_Mat_Online - time_Viz (:3343-3344)
+            orc_obs_active_match_capped(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(),
+                                        c->map_desc.data(), updated.data(), c->mp_info.data(), c->mp_H.data(), mlen,
+                                        c->base, c->level_sigma2, ntm, 1.f, 0.8f, &c->rng, c->kp2mp.data(),
+                                        c->score.data(), left.data(), &nleft, &nmatched,
+                                        mclk ? rec + GF_CK_OFF_AM(M, R) : nullptr, R,
+                                        mclk ? match_t - rec[GF_CK_MAT_ONLINE] - tviz : 0, &cut_round);
+            if (cut_round >= 0) st[GF_ST_FLAGS] |= 8 | 128;
             st[GF_ST_LOCAL] = nmatched;
             st[GF_ST_LDETS] = (int32_t)orc_last_ldets();
-            list.assign(left.begin(), left.begin() + nleft);
+            list.insert(list.end(), left.begin(), left.begin() + nleft);  // push_back after the cut points
         }
     }
     st[GF_ST_BRANCH] = branch;
@@ -621,32 +664,58 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     float LastTwc[16];
     twc_of(c->Tcw_last, LastTwc);
     mat44(c->Tcw, LastTwc, c->V);
-    nlist = (int)list.size();
-    for (int k = 0; k < nlist; k++) c->left[k] = list[k];
-    st[GF_ST_NLEFT] = nlist;
     if (gf) {
+        // timeCost_rest (:866) for RunMapPointsSelection and SearchAdditionalMatchesInFrame
+        const long long rest = sclk ? select_t - rec[GF_CK_SOFAR] : 0;
+        if (sclk && rest <= 0) st[GF_ST_FLAGS] |= 8 | 16;
         // predictPWLSVec(dt, 2) and RunMapPointsSelection at kinematic[1] (:795-800, :1717-1779)
         twc_of(c->Tcw, Twc);
         orc_obs_update(c->t_prev, c->Tcw_last, c->t_cur, Twc, c->Xv);
         gf_kine kin[2];
         orc_obs_predict(c->Xv, c->t_cur - c->t_prev, 2, kin);
         std::memcpy(c->Xv_next, kin[1].Xv, sizeof(c->Xv_next));
-        map_info(c, c->Xv_next, c->nmp, 1, 2, nullptr);
+        if (!sclk || rest > 0) {  // "too little budget available" (:1727-1731)
+            bool late = false;
+            map_info(c, c->Xv_next, c->nmp, 1, 2, nullptr, sclk ? rec + GF_CK_OFF_SEL(M, R) : nullptr, 2 * rest,
+                     &late);
+            if (late) st[GF_ST_FLAGS] |= 8 | 256;
+        }
         lap(5);
-        // SearchAdditionalMatchesInFrame (:3097-3145); without time left
-        // SearchByProjection_Budget returns at once (ORBmatcher.cc:281-282)
-        if (c->cut_select) {
-            if (nlist) st[GF_ST_FLAGS] |= 8 | 16;
-        } else {
+        // SearchAdditionalMatchesInFrame (:3097-3145)
+        if (!list.empty()) {
             if (viz) {
-                frustum_list(c, list.data(), nlist);
-                // matched points are skipped by the visibility pass (mnLastFrameSeen, :3110-3111)
+                // the visibility pass, capped at timeCost_rest / 2 per point (:3107-3119)
+                int cut = (int)list.size();
+                if (sclk) {
+                    const long long* el = rec + GF_CK_OFF_SA(M, R);
+                    for (int k = 0; k < (int)list.size(); k++)
+                        if (!seen[list[k]] && 2 * el[k] > 2 * rest) {
+                            cut = k;
+                            break;
+                        }
+                }
+                frustum_list(c, list.data(), cut);
+                // points seen this frame are skipped by the pass (mnLastFrameSeen, :3110-3111)
                 for (int i = 0; i < n; i++)
                     if (c->kp2mp[i] >= 0 && c->kp2mp[i] < c->nmp) c->views[c->kp2mp[i]].in_view = 0;
+                if (cut < (int)list.size()) {
+                    list.resize(cut);  // mLeftMapPoints.erase(vit, vend)
+                    st[GF_ST_FLAGS] |= 8 | 512;
+                }
             }
-            st[GF_ST_EXTRA] = project_list(c, list.data(), nlist, 0.8f);
+            // SearchByProjection_Budget(F, mLeftMapPoints, 0.8, rest - time_so_far)
+            int k = 0, bcut = -1;
+            orc_match_project_list(&c->fi, c->kps.data(), c->desc.data(), n, c->views.data(), c->map_desc.data(),
+                                   list.data(), (int)list.size(), 0.8f, 0.8f, c->kp2mp.data(), c->score.data(), &k,
+                                   sclk ? rec + GF_CK_OFF_BUD(M, R) : nullptr,
+                                   sclk ? 2 * rest - 2 * rec[GF_CK_SA_SOFAR] : 0, &bcut);
+            if (bcut >= 0) st[GF_ST_FLAGS] |= 8 | 1024;
+            st[GF_ST_EXTRA] = k;
         }
     }
+    nlist = (int)list.size();
+    for (int k = 0; k < nlist; k++) c->left[k] = list[k];
+    st[GF_ST_NLEFT] = nlist;
     if (c->refmap) {  // the local map's state back to the stream map, indices back to map indices
         const int nl = (int)lmp.size();
         for (int k = 0; k < nl; k++) {

@@ -468,12 +468,24 @@ int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uin
                       const gf_mp_view* views, const uint8_t* mp_desc, int m, float th, float nnratio,
                       int32_t* kp2mp, int32_t* score, int* nmatches);
 
+// The time cap of runActiveMapMatching (Observability.cc:1260, 1275-1277,
+// 1362-1370) replayed on elapsed times the device measured: round_el[i] is
+// the elapsed time at round i's start, cap = time_for_match (same ticks);
+// a round with round_el > cap ends at its first accepted draw, returning
+// without leftovers. null round_el: no cap.
+struct AmCap {
+    const long long* round_el = nullptr;
+    int nrec = 0;
+    long long cap = 0;
+    int* cut_round = nullptr;
+};
+
 // runActiveMapMatching, Observability.cc:1249-1524 (FRAME_INFO_MATRIX).
 static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
                         const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
                         const double* H, int m, const double* base, const float* level_sigma2, int num_to_match,
                         float th, float nnratio, int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft,
-                        int* nmatched);
+                        int* nmatched, const AmCap& tc = AmCap{});
 
 int orc_obs_active_match(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
                          const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
@@ -505,15 +517,16 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
                         const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated, const double* info,
                         const double* H, int m, const double* base, const float* level_sigma2, int num_to_match,
                         float th, float nnratio, int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft,
-                        int* nmatched) {
+                        int* nmatched, const AmCap& tc) {
     *nleft = 0;
     *nmatched = 0;
     orc::g_ldets = 0;
+    if (tc.cut_round) *tc.cut_round = -1;
     auto push_left_all = [&]() {
         for (int i = 0; i < m; i++)
             if (views[i].in_view) left[(*nleft)++] = i;
     };
-    if (m == 0 || num_to_match <= 0) {
+    if (m == 0 || num_to_match <= 0 || (tc.round_el && tc.cap <= 0)) {
         push_left_all();
         return GF_OK;
     }
@@ -540,6 +553,7 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
         std::priority_queue<SP> heap;
         std::vector<int> removeIdx;
         size_t numHit = 0, numRndQue = 0, szActual = std::min(szLazier, lmkIdx.size());
+        const bool late = tc.round_el && szActual > 0 && (int)i < tc.nrec && tc.round_el[i] > tc.cap;
         while (numHit < szActual) {
             size_t j = 0;
             numRndQue = 0;
@@ -554,6 +568,11 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
             if (numRndQue >= 2000) break;
             int q = lmkIdx[j];
             ++numHit;
+            if (late) {  // reach max time cap: return nMatched (:1366-1370)
+                if (tc.cut_round) *tc.cut_round = (int)i;
+                *nmatched = nMatched;
+                return GF_OK;
+            }
             double M[49];
             for (int k = 0; k < 49; k++) M[k] = cur[k] + info[49 * (size_t)q + k];
             heap.push(SP{q, orc::logdet7(M)});
@@ -607,6 +626,26 @@ static int active_match(orc::Rand& R, const gf_frame_info* fi, const gf_keypoint
     for (int q : lmkIdx) left[(*nleft)++] = q;
     *nmatched = nMatched;
     return GF_OK;
+}
+
+// The same under the time cap (the front end's budgets, gf_set_budgets).
+int orc_obs_active_match_capped(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                                const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
+                                const double* info, const double* H, int m, const double* base,
+                                const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
+                                int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched,
+                                const long long* round_el, int nrec, long long cap, int* cut_round) {
+    orc::Rand R;
+    R.load(*rng);
+    AmCap tc;
+    tc.round_el = round_el;
+    tc.nrec = nrec;
+    tc.cap = cap;
+    tc.cut_round = cut_round;
+    int rc = active_match(R, fi, kps, desc, n, views, mp_desc, updated, info, H, m, base, level_sigma2, num_to_match,
+                          th, nnratio, kp2mp, score, left, nleft, nmatched, tc);
+    R.save(*rng);
+    return rc;
 }
 
 // Max-volume selection: 1 baseline, 2 lazier selection, 3 automatic (deletion if 2k > n)

@@ -267,6 +267,63 @@ int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uin
     return GF_OK;
 }
 
+// ORBmatcher::SearchByProjection_Budget(F, vpMapPoints, th, time_constr)
+// (ORBmatcher.cc:276-379) over the map points list[0 .. nlist) in list order
+// (views / mp_desc indexed by map point). el (optional) holds the elapsed
+// time the device measured at each list point and constr2 = 2 x time_constr
+// in the same ticks: constr2 <= 0 returns at once (:281-282); otherwise the
+// loop breaks after the first point that reaches the clock check (in view, a
+// non-empty area, not rejected by the ratio test) with 2 el >= constr2
+// (:366-371). *cut = that list position, -1 when the loop ran to the end.
+int orc_match_project_list(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                           const gf_mp_view* views, const uint8_t* mp_desc, const int32_t* list, int nlist, float th,
+                           float nnratio, int32_t* kp2mp, int32_t* score, int* nmatches, const long long* el,
+                           long long constr2, int* cut) {
+    *nmatches = 0;
+    if (cut) *cut = -1;
+    if (el && constr2 <= 0) return GF_OK;
+    orc::FrameGrid G(fi, kps, n);
+    int nm = 0;
+    const bool bFactor = th != 1.0;
+    for (int k = 0; k < nlist; k++) {
+        const int q = list[k];
+        const gf_mp_view& v = views[q];
+        if (!v.in_view) continue;
+        const int pl = v.level;
+        float r = orc::radius_by_viewing_cos(v.view_cos);
+        if (bFactor) r *= th;
+        std::vector<int> near = G.area(v.u, v.v, r * G.scales[pl], pl - 1, pl);
+        if (near.empty()) continue;
+        int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
+        for (int idx : near) {
+            if (kp2mp[idx] >= 0) continue;
+            const int dist = orc::descriptor_distance(mp_desc + 32 * (size_t)q, desc + 32 * (size_t)idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = kps[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kps[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= orc::TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            kp2mp[bestIdx] = q;
+            score[bestIdx] = bestDist;
+            nm++;
+        }
+        if (el && 2 * el[k] >= constr2) {
+            if (cut) *cut = k;
+            break;
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
 // ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, th), :2081-2202
 int orc_match_lastframe(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n, const float* Tcw,
                         const gf_keypoint* last_kps, const uint8_t* last_desc, const int32_t* last_kp2mp,

@@ -31,7 +31,7 @@ def _orc():
         o.orc_chain_bootstrap.argtypes = [_P, _P, _P, _P, ctypes.c_double]
         o.orc_chain_step.argtypes = [_P, _P]
         o.orc_chain_timings.argtypes = [_P, _P]
-        o.orc_chain_set_cuts.argtypes = [_P, ctypes.c_int, ctypes.c_int]
+        o.orc_chain_set_clock.argtypes = [_P, _P, ctypes.c_size_t]
         o.orc_chain_set_covis.argtypes = [_P, _P]
         o._chain_declared = True
     return o
@@ -50,6 +50,7 @@ class Chain:
         self.h = _orc().orc_chain_create(ctypes.byref(self.params))
         self.cap = _orc().orc_chain_capacity(self.h)
         self.M = map_size
+        self.R = max(gf_budget, 1)
 
     def __del__(self):
         try:
@@ -82,19 +83,25 @@ class Chain:
         assert _orc().orc_chain_step(self.h, _p(img)) == 0
 
     def read(self, name: str) -> np.ndarray:
-        fid, dt, shape = field_shape(name, 1, self.cap, self.M)
+        fid, dt, shape = field_shape(name, 1, self.cap, self.M, self.R)
         out = np.zeros(shape, dt)
         assert _orc().orc_chain_read(self.h, fid, _p(out), out.nbytes) == 0, name
         return out[:, 0] if name == "stats" else out[0]
 
     def write(self, name: str, arr):
-        fid, dt, shape = field_shape(name, 1, self.cap, self.M)
+        fid, dt, shape = field_shape(name, 1, self.cap, self.M, self.R)
         a = np.ascontiguousarray(np.asarray(arr, dt).reshape(shape))
         assert _orc().orc_chain_write(self.h, fid, _p(a), a.nbytes) == 0, name
 
-    def set_cuts(self, frustum: bool, select: bool):
-        """Take the time-budget cuts the device took (GF_ST_BRANCH 5 / GF_ST_FLAGS bit 16)."""
-        assert _orc().orc_chain_set_cuts(self.h, int(frustum), int(select)) == 0
+    def set_clock(self, rec):
+        """The device's clock record (GF_FE_CLOCK of one stream) for the next
+        step: the chain applies the reference's time caps to the elapsed times
+        it holds (None: parity mode)."""
+        if rec is None:
+            assert _orc().orc_chain_set_clock(self.h, None, 0) == 0
+            return
+        self._clk = np.ascontiguousarray(rec, np.int64)
+        assert _orc().orc_chain_set_clock(self.h, _p(self._clk), self._clk.size) == 0
 
     def timings(self) -> np.ndarray:
         """Seconds of the last step's stages: extract, motion-model tracking,

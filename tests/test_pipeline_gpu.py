@@ -16,6 +16,7 @@ import pytest
 import oracle_chain as C
 import oracle_lib as O
 from gf_orb_slam_amd import scene
+from gf_orb_slam_amd.pipeline import CK, STATS, ck_offsets
 
 EXACT = ["kps", "desc", "nkp", "kp2mp", "score", "outlier", "last_kps", "last_desc", "last_nkp", "last_kp2mp",
          "last_outlier", "last_pos", "views", "mp_upd", "rng", "t_prev", "t_cur"]
@@ -184,45 +185,107 @@ def test_update_reference_in_step(stale, budget):
     fe.close()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("match_s,select_s", [(0.0, 0.0), (0.0, 1e9), (1e9, 0.0), (1e9, 1e9), (4e-4, 6e-4)])
-def test_budgets_match_oracle(match_s, select_s):
-    """gf_set_budgets (Tracking.cc:3230, 3262-3270; ORBmatcher.cc:276-282,
-    366-371). Budget 0 reproduces the reference's early exits: the isInFrustum
-    cap fires on the first local point (every point to mLeftMapPoints,
-    nToMatch = 0: branch 5) and SearchByProjection_Budget returns at once
-    (no additional matches, flag 16). A finite budget cuts at the pass
-    boundary the device clock decides; the oracle chain takes the cut the
-    device reports and the whole state must stay identical. A budget far
-    above the step time is parity mode."""
-    W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, 2000, 100, stale=0.93)
-    fe.set_budgets(match_s, select_s)
+FLAG_CAPS = 8 | 16 | 32 | 64 | 128 | 256 | 512 | 1024  # GF_ST_FLAGS bits of the time caps
+
+
+def _budget_steps(fe, W, frames, B, M, budget, nsteps, set_budgets=None, check=None):
+    """Step the device, and for every checked stream replay the step on the
+    oracle chain from the state before it, handing the chain only the clock
+    record the device wrote (the chain decides every cut itself). Returns the
+    per-(step, stream) stats and clock records."""
     dev = C.read_state(fe)
-    cuts = []
-    for k in range(1, 7):
+    out = []
+    for k in range(1, nsteps + 1):
+        if set_budgets:
+            set_budgets(k, dev)
         before = dev
         fe.step()
         dev = C.read_state(fe)
-        for b in range(4):
-            br, fl = int(dev["stats"][3, b]), int(dev["stats"][14, b])
-            ch = C.Chain("euroc", 1000, 2000, 100)
+        for b in (range(B) if check is None else check):
+            ch = C.Chain("euroc", 1000, M, budget)
             ch.load_from(before, b)
-            ch.set_cuts(br == 5, fl & 16 != 0)
+            ch.set_clock(dev["clock"][b])
             ch.step(_img(W, frames, b, k))
-            _compare(dev, ch, b, f"budgets ({match_s}, {select_s}) step {k}: ")
-            cuts.append((br == 5, fl & 16 != 0, int(dev["stats"][8, b]), int(dev["stats"][2, b])))
-    cf = np.array([c[0] for c in cuts])
-    cs = np.array([c[1] for c in cuts])
-    extra = np.array([c[2] for c in cuts])
-    ntm = np.array([c[3] for c in cuts])
+            _compare(dev, ch, b, f"budgets step {k}: ")
+            out.append((dev["stats"][:, b].copy(), dev["clock"][b].copy()))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("match_s,select_s", [(0.0, 0.0), (0.0, 1e9), (1e9, 0.0), (1e9, 1e9), (0.015, 0.098)])
+def test_budgets_match_oracle(match_s, select_s):
+    """gf_set_budgets: the reference's time caps on the device clock
+    (Tracking.cc:866, 3251-3344, 1727-1779, 3097-3137; Observability.cc:
+    564-578, 1260-1370; ORBmatcher.cc:276-371). The oracle chain is not told
+    where a cut fell: it applies each cap rule to the elapsed times the device
+    recorded (GF_FE_CLOCK) and must reach the same state. Budget 0 cuts the
+    isInFrustum loop at its first unmatched point (every local point after it
+    to mLeftMapPoints) and leaves SearchAdditionalMatchesInFrame no time; the
+    reference's own budgets (15 ms match, 98 ms post-publish at 20 fps) cut
+    nothing at the device's step times."""
+    M = 2000
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, M, 100, stale=0.93)
+    fe.set_budgets(match_s, select_s)
+    res = _budget_steps(fe, W, frames, 4, M, 100, 6)
+    fl = np.array([st[STATS.index("flags")] for st, _ in res])
+    ntm = np.array([st[STATS.index("to_match")] for st, _ in res])
+    extra = np.array([st[STATS.index("extra")] for st, _ in res])
+    ncut = np.array([st[STATS.index("ncut")] for st, _ in res])
     if match_s == 0.0:
-        assert cf[ntm > 0].all() and not cf[ntm <= 0].any()
+        assert (fl[ntm > 0] & 32).all() and (ncut[ntm > 0] > 0).all() and not (fl[ntm <= 0] & 32).any()
     if select_s == 0.0:
-        assert (extra == 0).all() and cs.any()
-    if match_s == 1e9:
-        assert not cf.any()
-    if select_s == 1e9:
-        assert not cs.any()
+        assert (fl & 16).all() and (extra == 0).all()
+    if match_s >= 1e9:
+        assert not (fl & (32 | 64 | 128)).any()
+    if select_s >= 1e9:
+        assert not (fl & (16 | 256 | 512 | 1024)).any()
+    if (match_s, select_s) == (0.015, 0.098):
+        assert not (fl & FLAG_CAPS).any(), "the reference's budgets cut a loop at device step times"
+    fe.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["match", "select"])
+def test_budget_cut_positions(which):
+    """Budgets below one frame's stage time, calibrated on this box's clock:
+    the isInFrustum cap (match) or the post-publish caps (select) fire inside
+    their loops, and the oracle chain, applying the reference's rules to the
+    device-recorded elapsed times, cuts at the same positions (stats, leftovers
+    and every state field identical)."""
+    # a wide batch spreads each loop's clock reads over many waves and
+    # workgroups, so cuts fall inside the loops; 16 streams are replayed
+    M, B = 2000, 128
+    check = list(range(0, B, 8)) + [B - 1]
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, B, M, 100, stale=0.93)
+    off = ck_offsets(M, 100)
+    sofar_seen = []
+
+    def calibrate(k, dev):
+        if k == 1:  # measure: budgets far above the step records every clock, cuts nothing
+            fe.set_budgets(1e9, 1e9)
+            return
+        clk = dev["clock"]
+        sofar_seen.append(int(np.median(clk[:, CK["sofar"]])))
+        if which == "match":
+            m = dev["nmp"]
+            el = np.concatenate([clk[b, off["viz"]:off["viz"] + m[b]] for b in range(B)])
+            el = el[el >= 0]
+            fe.set_budgets(2 * float(np.quantile(el, 0.1 * k)) / 1e8, 1e9)
+        else:  # timeCost_rest swept around the post-publish stages' time (tens of microseconds each)
+            fe.set_budgets(1e9, (sofar_seen[-1] + 1000 * ((k - 2) % 8) + 500 * ((k - 2) // 8)) / 1e8)
+
+    nsteps = 9 if which == "match" else 18
+    res = _budget_steps(fe, W, frames, B, M, 100, nsteps, calibrate, check)
+    fl = np.array([st[STATS.index("flags")] for st, _ in res[len(check):]])
+    if which == "match":
+        ncut = np.array([st[STATS.index("ncut")] for st, _ in res[len(check):]])
+        assert (fl & 32).any(), "no isInFrustum cut at a budget below the loop's time"
+        print("isInFrustum cuts:", int((fl & 32).astype(bool).sum()), "of", len(fl), "frames; mid-list:",
+              int(((ncut > 0) & (ncut < 1900)).sum()))
+    else:
+        print("post-publish caps:", {bit: int((fl & bit).astype(bool).sum()) for bit in (16, 256, 512, 1024)},
+              "timeCost_sofar ticks:", sofar_seen)
+        assert (fl & (16 | 256 | 512 | 1024)).any(), "no post-publish cap fired"
     fe.close()
 
 
