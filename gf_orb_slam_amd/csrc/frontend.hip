@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.h"
+#include "undist.h"
 
 namespace {
 
@@ -727,6 +728,14 @@ void fe_free(gf_frontend* fe) {
         if (_rc) return _rc;       \
     } while (0)
 
+// mvKeysUn (Frame::UndistortKeyPoints, Frame.cc:389-423): in place, the
+// keypoints' other fields kept; nothing to do when k1 == 0 (a copy there).
+int fe_undistort(gf_frontend* fe, hipStream_t s) {
+    if (fe->p.dist[0] == 0.f) return GF_OK;
+    const float K[4] = {fe->p.fx, fe->p.fy, fe->p.cx, fe->p.cy};
+    return gf_undistort_keypoints_dev(fe->ctx, fe->D.B, K, fe->p.dist, fe->D.kps, fe->D.nkp, fe->D.cap, fe->D.kps, s);
+}
+
 // The tracking step after the frame source pointers are set.
 int fe_track(gf_frontend* fe, hipStream_t s) {
     gf_ctx* ctx = fe->ctx;
@@ -746,6 +755,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
     if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
+    FE_RC(fe_undistort(fe, s));
     const hipStream_t s_ctx = s;
     if (fe->ts) {  // fork: tracking on the prioritised stream
         GF_HIP(hipEventRecord(fe->ev_extracted, s));
@@ -913,10 +923,13 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     }
     gf_extractor_capacity(fe->ex, &fe->cap);
     const int B = p->batch, cap = fe->cap, M = p->map_cap;
-    // Frame tables: bounds of the undistorted image (k1 = 0: the image,
-    // Frame.cc:470-476), mvScaleFactors as float products, mvLevelSigma2 and
+    // Frame tables: bounds of the undistorted image (Frame::ComputeImageBounds,
+    // Frame.cc:425-493), mvScaleFactors as float products, mvLevelSigma2 and
     // mvInvLevelSigma2 (ORBextractor.cc:474-478, Frame.cc:93-98).
-    fe->fi = gf_frame_info{0, p->width, 0, p->height, p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
+    const float K[4] = {p->fx, p->fy, p->cx, p->cy};
+    int bnd[4];
+    gfu::image_bounds(K, p->dist, p->width, p->height, bnd);
+    fe->fi = gf_frame_info{bnd[0], bnd[1], bnd[2], bnd[3], p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
     float sf = 1.f;
     for (int l = 0; l < p->nlevels; l++) {
         if (l) sf = sf * p->scale_factor;
@@ -931,12 +944,12 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     oc.cy = p->cy;
     oc.nrows = p->height;
     oc.ncols = p->width;
-    oc.min_x = 0;
-    oc.max_x = p->width;
-    oc.min_y = 0;
-    oc.max_y = p->height;
-    oc.bound_x = (int)((p->width - 0) * 0.1);
-    oc.bound_y = (int)((p->height - 0) * 0.1);
+    oc.min_x = bnd[0];
+    oc.max_x = bnd[1];
+    oc.min_y = bnd[2];
+    oc.max_y = bnd[3];
+    oc.bound_x = (int)((bnd[1] - bnd[0]) * 0.1);
+    oc.bound_y = (int)((bnd[3] - bnd[2]) * 0.1);
     oc.bound_depth = 0.f;
     FeDev& D = fe->D;
     D.B = B;
@@ -1294,6 +1307,7 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
     GF_HIP(hipMemcpyAsync(D.score, s999.data(), 4 * s999.size(), hipMemcpyHostToDevice, s));
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
                                   s));
+    FE_RC(fe_undistort(fe, s));
     // the first frame is matched against the whole stream map (with keyframe
     // graphs too: a local map needs the matches of a tracked frame)
     FE_RC(gf_frustum_dev(ctx, &fe->fi, B, D.Tcw, fe->gm.map, fe->g_nmp, M, 0.5f, fe->gm.views, fe->nview, s));

@@ -9,33 +9,13 @@
 // it f64 in OpenCV's expression order (compiled without contraction).
 #include "common.h"
 
+#include "undist.h"
+
 namespace {
 
-struct UndistCoef {
-    double fx, fy, ifx, ify, cx, cy;
-    double k[5];  // k1 k2 p1 p2 k3
-};
-
-__device__ __forceinline__ void undistort_point(const UndistCoef& c, float xf, float yf, float& xo, float& yo) {
-    double x = (double)xf, y = (double)yf;
-    x = (x - c.cx) * c.ifx;
-    y = (y - c.cy) * c.ify;
-    // the identity tilt: x0 = 1 * x (exact)
-    const double x0 = x, y0 = y;
-    for (int j = 0; j < 5; j++) {
-        const double r2 = x * x + y * y;
-        // the rational-model numerator is 1 + ((0 r2 + 0) r2 + 0) r2 = 1 exactly
-        const double icdist = 1.0 / (1 + ((c.k[4] * r2 + c.k[1]) * r2 + c.k[0]) * r2);
-        const double deltaX = 2 * c.k[2] * x * y + c.k[3] * (r2 + 2 * x * x);
-        const double deltaY = c.k[2] * (r2 + 2 * y * y) + 2 * c.k[3] * x * y;
-        x = (x0 - deltaX) * icdist;
-        y = (y0 - deltaY) * icdist;
-    }
-    // RR = K: xx = fx x + 0 y + cx, yy = 0 x + fy y + cy, ww = 1 / (0 x + 0 y + 1)
-    const double xx = c.fx * x + c.cx, yy = c.fy * y + c.cy;
-    xo = (float)xx;
-    yo = (float)yy;
-}
+using gfu::UndistCoef;
+using gfu::make_coef;
+using gfu::undistort_point;
 
 __global__ void k_undistort(UndistCoef c, int copy_only, const gf_keypoint* __restrict__ in, const int32_t* __restrict__ n,
                             int cap, gf_keypoint* __restrict__ out) {
@@ -44,18 +24,6 @@ __global__ void k_undistort(UndistCoef c, int copy_only, const gf_keypoint* __re
     gf_keypoint kp = in[(long long)f * cap + i];
     if (!copy_only) undistort_point(c, kp.x, kp.y, kp.x, kp.y);
     out[(long long)f * cap + i] = kp;
-}
-
-UndistCoef make_coef(const float K[4], const float dist[5]) {
-    UndistCoef c;
-    c.fx = (double)K[0];
-    c.fy = (double)K[1];
-    c.cx = (double)K[2];
-    c.cy = (double)K[3];
-    c.ifx = 1. / c.fx;
-    c.ify = 1. / c.fy;
-    for (int i = 0; i < 5; i++) c.k[i] = (double)dist[i];
-    return c;
 }
 
 }  // namespace

@@ -92,14 +92,17 @@ class FrontendParams(ctypes.Structure):
                 ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
                 ("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int32),
                 ("fast_th", ctypes.c_int32), ("batch", ctypes.c_int32), ("map_cap", ctypes.c_int32),
-                ("gf_budget", ctypes.c_int32), ("gf", ctypes.c_int32), ("dt", ctypes.c_double)]
+                ("gf_budget", ctypes.c_int32), ("gf", ctypes.c_int32), ("dt", ctypes.c_double),
+                ("dist", ctypes.c_float * 5)]
 
     @classmethod
     def make(cls, camera: str, nfeatures: int, batch: int, map_cap: int, gf_budget: int, gf: bool = True,
-             fps: float = 20.0, nlevels: int = 8, scale_factor: float = 1.2, fast_th: int = 20):
+             fps: float = 20.0, nlevels: int = 8, scale_factor: float = 1.2, fast_th: int = 20, dist=None):
+        """dist: Camera.k1 k2 p1 p2 [k3] (None / k1 = 0: keypoints used as extracted)."""
         w, h, fx, fy, cx, cy = synth.CAMERAS[camera]
+        d = list(dist or ()) + [0.0] * (5 - len(dist or ()))
         return cls(w, h, fx, fy, cx, cy, nfeatures, scale_factor, nlevels, fast_th, batch, map_cap, gf_budget,
-                   1 if gf else 0, 1.0 / fps)
+                   1 if gf else 0, 1.0 / fps, (ctypes.c_float * 5)(*d))
 
 
 def field_shape(name: str, B: int, cap: int, M: int, R: int = 1):
@@ -142,8 +145,8 @@ class FrontEnd:
     """B independent streams, one frame each per step."""
 
     def __init__(self, camera: str = "euroc", nfeatures: int = 1000, batch: int = 1, map_size: int = 2000,
-                 gf_budget: int = 100, gf: bool = True, fps: float = 20.0, ctx: Context | None = None):
-        self.params = FrontendParams.make(camera, nfeatures, batch, map_size, gf_budget, gf, fps)
+                 gf_budget: int = 100, gf: bool = True, fps: float = 20.0, ctx: Context | None = None, dist=None):
+        self.params = FrontendParams.make(camera, nfeatures, batch, map_size, gf_budget, gf, fps, dist=dist)
         self.cam = synth.CAMERAS[camera]
         self.B, self.M = batch, map_size
         self.R = max(gf_budget, 1)

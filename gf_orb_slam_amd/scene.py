@@ -99,29 +99,39 @@ class Scene:
             best[ok], pid[ok], A[ok], Bc[ok] = lam[ok], k, a[ok], b[ok]
         return best, pid, A, Bc
 
-    def backproject(self, Tcw: np.ndarray, x: np.ndarray, y: np.ndarray, cam) -> tuple:
-        """World points of pixels (x, y) seen from Tcw; valid mask."""
+    def backproject(self, Tcw: np.ndarray, x: np.ndarray, y: np.ndarray, cam, dist=None) -> tuple:
+        """World points of pixels (x, y) seen from Tcw; valid mask. dist: the
+        pixels are in a distorted image (radial-tangential k1 k2 p1 p2 [k3])."""
         _, _, fx, fy, cx, cy = cam
         T = np.asarray(Tcw, np.float64)
         R, t = T[:3, :3], T[:3, 3]
         C = -R.T @ t
-        dc = np.stack([(x - cx) / fx, (y - cy) / fy, np.ones_like(x, dtype=np.float64)], 1)
+        xn, yn = (x - cx) / fx, (y - cy) / fy
+        if dist is not None:
+            xn, yn = synth.undistort_normalized(xn, yn, dist)
+        dc = np.stack([xn, yn, np.ones_like(x, dtype=np.float64)], 1)
         dw = dc @ R  # R^T d
         lam, pid, _, _ = self.intersect(C, dw)
         X = C + lam[:, None] * dw
         return X, pid >= 0
 
-    def render(self, Tcws, cam, device="cpu"):
-        """u8 frames [N][H][W] for N poses (torch on `device`)."""
+    def render(self, Tcws, cam, device="cpu", dist=None):
+        """u8 frames [N][H][W] for N poses (torch on `device`); dist: a
+        distorted image (radial-tangential k1 k2 p1 p2 [k3])."""
         import torch
         import torch.nn.functional as Fn
 
         w, h, fx, fy, cx, cy = cam
         dev = torch.device(device)
         tex = torch.from_numpy(self.textures).to(dev).float()[:, None]  # [P,1,T,T]
-        ys, xs = torch.meshgrid(torch.arange(h, device=dev, dtype=torch.float32),
-                                torch.arange(w, device=dev, dtype=torch.float32), indexing="ij")
-        dc = torch.stack([(xs - cx) / fx, (ys - cy) / fy, torch.ones_like(xs)], -1).reshape(-1, 3)
+        if dist is None:
+            ys, xs = torch.meshgrid(torch.arange(h, device=dev, dtype=torch.float32),
+                                    torch.arange(w, device=dev, dtype=torch.float32), indexing="ij")
+            dc = torch.stack([(xs - cx) / fx, (ys - cy) / fy, torch.ones_like(xs)], -1).reshape(-1, 3)
+        else:  # each pixel's ray through the ideal (undistorted) normalised point
+            ys, xs = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
+            xn, yn = synth.undistort_normalized((xs - cx) / fx, (ys - cy) / fy, dist)
+            dc = torch.from_numpy(np.stack([xn, yn, np.ones_like(xn)], -1).reshape(-1, 3).astype(np.float32)).to(dev)
         out = []
         o = torch.from_numpy(self.o).float().to(dev)
         u = torch.from_numpy(self.u).float().to(dev)
@@ -174,7 +184,8 @@ def velocity(T_prev: np.ndarray, T_cur: np.ndarray) -> np.ndarray:
 
 # ------------------------------------------------------------- local map
 def build_map(scene: Scene, cam, extract, period: int, traj_seed: int, n_map: int, seed: int,
-              n_kf: int = 8, nlevels: int = 8, scale: float = 1.2, device="cpu", stale_desc: float = 0.0):
+              n_kf: int = 8, nlevels: int = 8, scale: float = 1.2, device="cpu", stale_desc: float = 0.0,
+              dist=None):
     """Map points from n_kf keyframes along the loop: every keypoint of a
     keyframe back-projected onto the scene (duplicates within 2 cm merged,
     first keyframe wins), the keyframe descriptor, normal and the
@@ -201,21 +212,21 @@ def build_map(scene: Scene, cam, extract, period: int, traj_seed: int, n_map: in
         sf.append(np.float32(sf[-1] * np.float32(scale)))
     sf = np.array(sf, np.float32)
     poses = [trajectory_pose(k * period / n_kf, period, traj_seed) for k in range(n_kf)]
-    imgs = scene.render(poses, cam, device).cpu().numpy()
+    imgs = scene.render(poses, cam, device, dist=dist).cpu().numpy()
     Xs, Ds, Ns, dmin, dmax = [], [], [], [], []
     for T, img in zip(poses, imgs):
         k, d = extract(img)
-        X, ok = scene.backproject(T, k["x"].astype(np.float64), k["y"].astype(np.float64), cam)
+        X, ok = scene.backproject(T, k["x"].astype(np.float64), k["y"].astype(np.float64), cam, dist=dist)
         C = -T[:3, :3].astype(np.float64).T @ T[:3, 3].astype(np.float64)
         X, d, oc = X[ok], d[ok], k["octave"][ok]
         PC = (X - C).astype(np.float32)
-        dist = np.sqrt((PC.astype(np.float64) ** 2).sum(1)).astype(np.float32)
+        dpc = np.sqrt((PC.astype(np.float64) ** 2).sum(1)).astype(np.float32)
         Xs.append(X)
         Ds.append(d)
-        Ns.append(PC / dist[:, None])
+        Ns.append(PC / dpc[:, None])
         lvl = sf[oc]
-        dmin.append((np.float32(1.0) / np.float32(scale)) * dist / lvl)
-        dmax.append(np.float32(scale) * dist * sf[nlevels - 1 - oc])
+        dmin.append((np.float32(1.0) / np.float32(scale)) * dpc / lvl)
+        dmax.append(np.float32(scale) * dpc * sf[nlevels - 1 - oc])
     X = np.concatenate(Xs)
     D = np.concatenate(Ds)
     keys = np.floor(X / 0.02).astype(np.int64)
@@ -352,8 +363,9 @@ class Workload:
 
     def __init__(self, camera: str, batch: int, n_scenes: int = 8, period: int = 32, seed: int = 0,
                  phase_stride: int = 5, tex_size: int = 1024, scenes: list | None = None, phase_offset: int = 0,
-                 stale_desc: float = 0.0):
+                 stale_desc: float = 0.0, dist=None):
         self.cam = synth.CAMERAS[camera]
+        self.dist = dist  # radial-tangential coefficients of distorted renders (None: pinhole)
         self.stale_desc = stale_desc
         self.B, self.S, self.period, self.seed = batch, min(n_scenes, batch), period, seed
         self.scenes = scenes if scenes is not None else [Scene(seed * 1000 + s, tex_size) for s in range(self.S)]
@@ -368,7 +380,7 @@ class Workload:
         frames = []
         for s, sc in enumerate(self.scenes):
             poses = [trajectory_pose(k, self.period, self.traj_seed[s]) for k in range(self.period)]
-            frames.append(sc.render(poses, self.cam, device))
+            frames.append(sc.render(poses, self.cam, device, dist=self.dist))
         return torch.stack(frames)
 
     def gt_pose(self, stream: int, step: int) -> np.ndarray:
@@ -391,4 +403,5 @@ class Workload:
 
     def build_maps(self, extract, n_map: int, device="cpu"):
         return [build_map(sc, self.cam, extract, self.period, self.traj_seed[s], n_map, self.seed * 7919 + s,
-                          device=device, stale_desc=self.stale_desc) for s, sc in enumerate(self.scenes)]
+                          device=device, stale_desc=self.stale_desc, dist=self.dist)
+                for s, sc in enumerate(self.scenes)]

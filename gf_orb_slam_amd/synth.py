@@ -14,6 +14,29 @@ CAMERAS = {
     "euroc": (752, 480, 457.3, 457.3, 367.215, 248.375),
     "tum": (640, 480, 525.0, 525.0, 319.5, 239.5),
 }
+# radial-tangential coefficients k1 k2 p1 p2 of real cameras (the public
+# EuRoC MAV cam0 and TUM fr2 calibrations), for distorted renders
+DISTORTION = {
+    "euroc": (-0.28340811, 0.07395907, 0.00019359, 1.76187114e-05),
+    "tum": (0.231222, -0.784899, -0.003257, -0.000105, 0.917205),
+}
+
+
+def undistort_normalized(xd, yd, dist, iters: int = 20):
+    """Ideal normalised coordinates of distorted normalised ones (fixed-point
+    inversion of the radial-tangential model, float64; for rendering and map
+    building only — the tracked keypoints go through cv::undistortPoints'
+    restatement in the library)."""
+    k1, k2, p1, p2, k3 = (list(dist) + [0.0] * 5)[:5]
+    x, y = xd.copy(), yd.copy()
+    for _ in range(iters):
+        r2 = x * x + y * y
+        rad = 1 + ((k3 * r2 + k2) * r2 + k1) * r2
+        dx = 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+        dy = p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+        x = (xd - dx) / rad
+        y = (yd - dy) / rad
+    return x, y
 
 
 def frame_seed(stream: int, frame: int) -> int:

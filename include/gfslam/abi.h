@@ -840,7 +840,7 @@ int gf_views_exclude_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2m
  * graph. Time budgets follow gf_set_budgets of the context (+inf = parity). */
 typedef struct gf_frontend_params {
     int32_t width, height;
-    float fx, fy, cx, cy;       /* Camera.fx/fy/cx/cy; k1 = 0 (undistortion is a copy) */
+    float fx, fy, cx, cy;       /* Camera.fx/fy/cx/cy                             */
     int32_t nfeatures;          /* ORBextractor.nFeatures */
     float scale_factor;         /* ORBextractor.scaleFactor */
     int32_t nlevels;            /* ORBextractor.nLevels */
@@ -850,6 +850,14 @@ typedef struct gf_frontend_params {
     int32_t gf_budget;          /* num_good_inlier_predef (main.cc GF budget) */
     int32_t gf;                 /* 1 GOOD_FEATURE_MAP_MATCHING, 0 ORB-SLAM baseline matching */
     double dt;                  /* frame period 1 / Camera.fps (timestamps t_k = t_0 + k dt) */
+    float dist[5];              /* Camera.k1 k2 p1 p2 [k3] (mDistCoef). k1 != 0: every
+                                   frame's keypoints are undistorted after extraction
+                                   (Frame::UndistortKeyPoints, Frame.cc:389-423) and the
+                                   image bounds mnMinX..mnMaxY come from the undistorted
+                                   corners and edge midpoints (Frame.cc:425-493); they
+                                   set the projection bounds, the keypoint grid and the
+                                   observability margins (Tracking.cc:876-877).
+                                   k1 == 0: keypoints as extracted, bounds = the image. */
 } gf_frontend_params;
 typedef struct gf_frontend gf_frontend;
 

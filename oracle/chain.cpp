@@ -49,6 +49,8 @@ int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, co
                              const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
                              int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
 long long orc_last_ldets(void);
+int orc_undistort_keypoints(const float K[4], const float dist[5], const gf_keypoint* in, int n, gf_keypoint* out);
+int orc_frame_bounds(const float K[4], const float dist[5], int w, int h, int b[4]);
 int orc_obs_active_match_capped(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
                                 const gf_mp_view* views, const uint8_t* mp_desc, const uint8_t* updated,
                                 const double* info, const double* H, int m, const double* base,
@@ -304,7 +306,11 @@ orc_chain* orc_chain_create(const gf_frontend_params* p) {
     for (int l = 0; l < p->nlevels; l++) c->cap += fpl[l];
     c->M = p->map_cap;
     c->ck_R = std::max(p->gf_budget, 1);
-    c->fi = gf_frame_info{0, p->width, 0, p->height, p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
+    // Frame::ComputeImageBounds (Frame.cc:425-493)
+    const float K[4] = {p->fx, p->fy, p->cx, p->cy};
+    int bnd[4];
+    orc_frame_bounds(K, p->dist, p->width, p->height, bnd);
+    c->fi = gf_frame_info{bnd[0], bnd[1], bnd[2], bnd[3], p->fx, p->fy, p->cx, p->cy, p->nlevels, p->scale_factor};
     float sf = 1.f;
     for (int l = 0; l < p->nlevels; l++) {
         if (l) sf = sf * p->scale_factor;
@@ -318,12 +324,13 @@ orc_chain* orc_chain_create(const gf_frontend_params* p) {
     oc.cy = p->cy;
     oc.nrows = p->height;
     oc.ncols = p->width;
-    oc.min_x = 0;
-    oc.max_x = p->width;
-    oc.min_y = 0;
-    oc.max_y = p->height;
-    oc.bound_x = (int)(p->width * 0.1);
-    oc.bound_y = (int)(p->height * 0.1);
+    oc.min_x = bnd[0];
+    oc.max_x = bnd[1];
+    oc.min_y = bnd[2];
+    oc.max_y = bnd[3];
+    // mBoundXInFrame / mBoundYInFrame (Tracking.cc:876-877)
+    oc.bound_x = (int)((bnd[1] - bnd[0]) * 0.1);
+    oc.bound_y = (int)((bnd[3] - bnd[2]) * 0.1);
     oc.bound_depth = 0.f;
     const size_t cap = c->cap, M = c->M;
     c->kps.assign(cap, gf_keypoint{});
@@ -391,6 +398,9 @@ static int extract(orc_chain* c, const uint8_t* img) {
     int rc = orc_extract(img, c->p.width, c->p.height, c->p.width, c->p.nfeatures, c->p.scale_factor, c->p.nlevels,
                          c->p.fast_th, c->kps.data(), c->desc.data(), c->cap, &n);
     c->nkp = n;
+    // mvKeysUn (Frame::UndistortKeyPoints, Frame.cc:389-423; a copy when k1 == 0)
+    const float K[4] = {c->p.fx, c->p.fy, c->p.cx, c->p.cy};
+    if (rc == GF_OK) orc_undistort_keypoints(K, c->p.dist, c->kps.data(), n, c->kps.data());
     return rc;
 }
 

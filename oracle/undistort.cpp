@@ -5,6 +5,8 @@
 // OpenCV 3.4's cvUndistortPointsInternal (imgproc/src/undistort.cpp) for that
 // call — TermCriteria(COUNT, 5): five iterations, identity tilt, RR = K —
 // keeping its expression order. Parity unpinned against OpenCV itself.
+#include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 
@@ -37,5 +39,40 @@ extern "C" int orc_undistort_keypoints(const float K[4], const float dist[5], co
         out[i].x = (float)(xx * ww);
         out[i].y = (float)(yy * ww);
     }
+    return GF_OK;
+}
+
+// Frame::ComputeImageBounds (Frame.cc:425-493): the four corners and four edge
+// midpoints undistorted, the int bounds compared with the float coordinates
+// as the reference writes it; b = {mnMinX, mnMaxX, mnMinY, mnMaxY}. k1 == 0:
+// the image (:486-492).
+extern "C" int orc_frame_bounds(const float K[4], const float dist[5], int w, int h, int b[4]) {
+    if (dist[0] == 0.f) {
+        b[0] = 0;
+        b[1] = w;
+        b[2] = 0;
+        b[3] = h;
+        return GF_OK;
+    }
+    gf_keypoint p[8];
+    std::memset(p, 0, sizeof(p));
+    const float xs[8] = {0.0f, (float)w, 0.0f, (float)w, 0.0f, float(w) / 2.0f, float(w) / 2.0f, (float)w};
+    const float ys[8] = {0.0f, 0.0f, (float)h, (float)h, float(h) / 2.0f, 0.0f, (float)h, float(h) / 2.0f};
+    for (int i = 0; i < 8; i++) {
+        p[i].x = xs[i];
+        p[i].y = ys[i];
+    }
+    orc_undistort_keypoints(K, dist, p, 8, p);
+    int mnMinX = INT_MAX, mnMaxX = INT_MIN, mnMinY = INT_MAX, mnMaxY = INT_MIN;
+    for (int i = 0; i < 8; i++) {
+        if (mnMinX > p[i].x) mnMinX = (int)std::floor(p[i].x);
+        if (mnMinY > p[i].y) mnMinY = (int)std::floor(p[i].y);
+        if (mnMaxX < p[i].x) mnMaxX = (int)std::ceil(p[i].x);
+        if (mnMaxY < p[i].y) mnMaxY = (int)std::ceil(p[i].y);
+    }
+    b[0] = mnMinX;
+    b[1] = mnMaxX;
+    b[2] = mnMinY;
+    b[3] = mnMaxY;
     return GF_OK;
 }

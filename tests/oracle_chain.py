@@ -45,8 +45,8 @@ class Chain:
     """One stream of the front end on the CPU oracle."""
 
     def __init__(self, camera: str, nfeatures: int, map_size: int, gf_budget: int, gf: bool = True,
-                 fps: float = 20.0):
-        self.params = FrontendParams.make(camera, nfeatures, 1, map_size, gf_budget, gf, fps)
+                 fps: float = 20.0, dist=None):
+        self.params = FrontendParams.make(camera, nfeatures, 1, map_size, gf_budget, gf, fps, dist=dist)
         self.h = _orc().orc_chain_create(ctypes.byref(self.params))
         self.cap = _orc().orc_chain_capacity(self.h)
         self.M = map_size

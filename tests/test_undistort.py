@@ -62,3 +62,20 @@ def test_undistort_gpu_bit_exact(K, D):
     g = undistort_keypoints(k, K, D)
     o = O.undistort_keypoints(k, K, D)
     assert g.tobytes() == o.tobytes()
+
+
+def test_oracle_frame_bounds():
+    """Frame::ComputeImageBounds (Frame.cc:425-493): with EuRoC's barrel
+    distortion the undistorted corners lie outside the image, so the bounds
+    widen; k1 = 0 gives the image."""
+    import ctypes
+
+    o = O.orc()
+    b = (ctypes.c_int * 4)()
+    K = (ctypes.c_float * 4)(*EUROC_K)
+    D = (ctypes.c_float * 5)(*(list(EUROC_D) + [0.0]))
+    assert o.orc_frame_bounds(K, D, 752, 480, b) == 0
+    mnMinX, mnMaxX, mnMinY, mnMaxY = list(b)
+    assert mnMinX < 0 and mnMaxX > 752 and mnMinY < 0 and mnMaxY > 480
+    Z = (ctypes.c_float * 5)(0, 0.1, 0, 0, 0)
+    assert o.orc_frame_bounds(K, Z, 752, 480, b) == 0 and list(b) == [0, 752, 0, 480]
