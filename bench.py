@@ -332,6 +332,102 @@ def lba_leg(batch: int, repeats: int = 3, cpu: bool = True) -> dict:
     return out
 
 
+# ------------------------------------------------------------- config 3 leg
+def config3_leg(local: int, batch: int, groups: int, steps: int, warmup: int) -> dict:
+    """BASELINE config 3 (TUM RGB-D 640x480, 2000 features, GF budget 160 +
+    PoseOptimization) on this GPU: `batch` rendered sequences in `groups`
+    gated front ends, 3000-point keyframe-built local maps with 93% stale
+    descriptors (the GF regime: runActiveMapMatching on most frames), timed
+    like the headline; the dominant §8d-priced kernel's roofline."""
+    import torch
+
+    from gf_orb_slam_amd import ORBextractor, scene
+    from gf_orb_slam_amd.orb import Context
+    from gf_orb_slam_amd.pipeline import STATS, FrontEnd, chain_extraction
+
+    cam, nfeat, budget, nmap, stale = "tum", 2000, 160, 3000, 0.93
+    B, G = batch, max(1, groups)
+    Bg = B // G
+    W = scene.Workload(cam, B, n_scenes=8, period=32, seed=1, stale_desc=stale)
+    ex = ORBextractor(nfeat, 1.2, 8, 1, 20)
+    maps = W.build_maps(lambda im: ex(im), nmap, device=f"cuda:{local}")
+    frames = W.render_all(f"cuda:{local}").contiguous()
+    T, V = W.boot_state()
+    fes = []
+    for g in range(G):
+        sl = slice(g * Bg, (g + 1) * Bg)
+        fe = FrontEnd(cam, nfeat, Bg, nmap, budget, ctx=Context(local))
+        for b in range(Bg):
+            fe.set_map(b, *maps[W.scene_of[g * Bg + b]])
+            fe.set_rng(b, 7 + g * Bg + b)
+        fe.set_source(frames, W.scene_of[sl], W.phase[sl])
+        fe.bootstrap(T[sl], V[sl], 0.0)
+        fes.append(fe)
+    gates = chain_extraction(fes)
+    for _ in range(warmup):
+        for fe in fes:
+            fe.step()
+    for fe in fes:
+        fe.sync()
+        fe.write("hist", np.zeros((fe.B, 8), np.int32))
+        fe.prof_enable(True)
+        fe.prof_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        for fe in fes:
+            fe.step()
+    for fe in fes:
+        fe.sync()
+    dt = time.perf_counter() - t0
+    prof = {}
+    for fe in fes:
+        for k, (ms, cnt) in fe.prof_report().items():
+            a = prof.setdefault(k, [0.0, 0])
+            a[0] += ms
+            a[1] += cnt
+        fe.prof_enable(False)
+    th = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)
+    st = [fe.stats() for fe in fes]
+    final = {k: np.concatenate([x[k] for x in st]) for k in STATS}
+    for fe in fes:
+        fe.close()
+    del gates
+    kb = kernel_bytes(cam, nfeat)
+    ldets = float(th[:, 6].sum())
+    work = {"k_resize": kb["k_resize"] * Bg, "k_blur_fast": kb["k_blur_fast"] * Bg,
+            "k_describe": kb["k_describe"] * Bg}
+    if "k_active_match" in prof:
+        work["k_active_match"] = 224.0 * ldets / max(prof["k_active_match"][1], 1)
+    priced = {}
+    for k, units in work.items():
+        if k not in prof:
+            continue
+        ms = prof[k][0] / prof[k][1]
+        if k == "k_active_match" and "k_active_match_overflow" in prof:
+            ms = (prof[k][0] + prof["k_active_match_overflow"][0]) / prof[k][1]
+        ach = units / (ms / 1e3) / 1e9
+        priced[k] = {"kernel": k, "bound": "hbm", "achieved": round(ach, 3), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(ach / 8000.0, 6), "algorithmic_bytes_per_launch": units,
+                     "avg_launch_ms": round(ms, 4), "launches": prof[k][1]}
+    dom = max(priced, key=lambda k: prof[k][0])
+    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
+                 if k in prof)
+    return {"workload": f"config 3: tum 640x480, {nfeat} feats, GF budget {budget}, {nmap}-point keyframe-built "
+                        f"local maps ({stale:.2f} stale descriptors), {B} sequences in {G} gated groups, "
+                        f"PoseOptimization twice per frame",
+            "frames_per_s": round(B * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+            "warmup": warmup, "roofline": {**priced[dom], "others": {k: v for k, v in priced.items() if k != dom}},
+            "extraction_algorithmic_GBps": round(kb["extract_total"] * B * steps / (ext_ms / 1e3) / 1e9, 1)
+            if ext_ms else None,
+            "branch_mix_timed": {"leftovers_only": int(th[:, 1].sum()), "search_by_projection": int(th[:, 2].sum()),
+                                 "active_matching": int(th[:, 3].sum()), "nothing_to_match": int(th[:, 4].sum())},
+            "logdets_per_frame": round(ldets / (B * steps), 1),
+            "mean_inliers": round(float(final["inl2"].mean()), 1),
+            "lost_frames_last_step": int((final["flags"] & 4 != 0).sum()),
+            "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1]} for k, v in prof.items()}}
+
+
 # ------------------------------------------------------------- main
 def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, device: int, stale: float,
                 refmap: bool, n_kf: int):
@@ -398,6 +494,9 @@ def main():
                     help="also time the step with the reference's time budgets on (gf_set_budgets)")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="also time one group with the frames handed over from host memory")
+    ap.add_argument("--config3-steps", type=int, default=10,
+                    help="also time BASELINE config 3 (TUM 640x480, 2000 feats, GF 160; 0: skip)")
+    ap.add_argument("--config3-batch", type=int, default=1024)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -549,6 +648,22 @@ def main():
         ei = float((nedges * iters).sum()) / (2 * G)
         work["k_pose_opt"] = ("f64", 160.0 * ei, "160 flop x edges x LM iterations (%.0f edge-iterations per "
                                                   "launch, last timed step)" % ei)
+    # matchers (SURVEY §8d B_match = 48 M + 36 C + 8 N per frame, C = area
+    # candidates counted on the device, GF_ST_CAND_*), from the last timed step
+    nkp_last = np.concatenate([fe.read("nkp") for fe in fes]).astype(np.float64)
+    m2_q = np.where(final["branch"] == 2, final["nlocal"] if refmap else args.map, 0).astype(np.float64)
+    b_m3 = 48.0 * nkp_last + 36.0 * final["cand_last"] + 8.0 * nkp_last
+    b_proj = 48.0 * (m2_q + final["nleft"]) + 36.0 * final["cand_proj"] + 2 * 8.0 * nkp_last
+    if "k_match_lastframe" in prof:
+        work["k_match_lastframe"] = ("hbm", float(b_m3.sum()) / G,
+                                     "48 M + 36 C + 8 N per frame: SearchByProjection(Cur, Last), M = last-frame "
+                                     "keypoints, C = %.0f area candidates per frame (device-counted), last timed step"
+                                     % float(final["cand_last"].mean()))
+    if "k_match_project" in prof:
+        work["k_match_project"] = ("hbm", float(b_proj.sum()) / (2 * G),
+                                   "48 M + 36 C + 8 N per frame over SearchByProjection(F, local) and "
+                                   "SearchByProjection_Budget (two launches per step), C = %.0f area candidates per "
+                                   "frame, last timed step" % float(final["cand_proj"].mean()))
     PEAK = {"hbm": (8000.0, "GB/s"), "f64": (78.6, "TFLOP/s")}
 
     def price(k, ms_avg, traffic=None):
@@ -575,6 +690,11 @@ def main():
                                                  / max(prof["k_active_match_overflow"][1], 1), 4),
             "timing_note": "avg_launch_ms = small-pool pass + overflow pass (k_active_match_overflow) per step "
                            "and group; rocprof lists them as two kernels"})
+    if "k_match_lastframe" in priced and "k_match_seq_pre" in prof:
+        # the per-query precompute and the ordered pass are one SearchByProjection(Cur, Last)
+        ms_pair = (prof["k_match_lastframe"][0] + prof["k_match_seq_pre"][0]) / prof["k_match_lastframe"][1]
+        priced["k_match_lastframe"] = price("k_match_lastframe", ms_pair)
+        priced["k_match_lastframe"]["timing_note"] = "avg_launch_ms = k_match_seq_pre + k_match_seq per launch"
     for k in priced:
         if work[k][0] == "f64":
             priced[k]["peak_note"] = "FP64 peak (AMD spec, vector = matrix on MI355X); this kernel is f64 VALU"
@@ -792,6 +912,8 @@ def main():
         fe.close()
     if rank == 0 and args.lba_batch > 0:
         out["local_ba"] = lba_leg(args.lba_batch, cpu=not args.no_cpu_baseline)
+    if rank == 0 and world == 1 and args.config3_steps > 0:
+        out["config3"] = config3_leg(local, args.config3_batch, G, args.config3_steps, 3)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam, args.nfeatures, args.map, args.gf_budget, 20.0, maps, W,
                                            frames.cpu().numpy(), budget_s=args.cpu_seconds)

@@ -141,6 +141,17 @@ int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf
                      int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
                      const int32_t* d_remap, void* stream, const ActiveClock& ck = ActiveClock{});
 
+// Candidate counting for the front end's matcher calls (SURVEY §8d B_match's
+// C): while a CandidateCount lives on this thread, every projection-matcher
+// launch (match.hip) adds each frame's window candidate count (the
+// GetFeaturesInArea sizes) to d_counts[f].
+struct CandidateCount {
+    int32_t* prev;
+    explicit CandidateCount(int32_t* d_counts);
+    ~CandidateCount();
+};
+int32_t* candidate_counts();
+
 // RCCL broadcast on the communicator's stream (dist.hip), asynchronous.
 int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);
 int dist_rank(gf_dist* d);

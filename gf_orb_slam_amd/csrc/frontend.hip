@@ -763,9 +763,13 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         s = fe->ts;
     }
     // TrackWithMotionModel
-    FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
-                                 D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp, D.score,
-                                 col(GF_ST_M3), fe->scratch, s));
+    {
+        gf::CandidateCount cc(col(GF_ST_CAND_LAST));
+        FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
+                                     D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp,
+                                     D.score, col(GF_ST_M3), fe->scratch, s));
+    }
+    gf::CandidateCount cc(col(GF_ST_CAND_PROJ));  // the projection searches below
     FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
                                  fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
                                  col(GF_ST_ITER1), col(GF_ST_EDGES1), s));

@@ -70,6 +70,9 @@ struct MatchArgs {
     long long ck_stride;
     int ck_off;       // offset of the per-point array in a stream's record
     int32_t* ck_old;  // [F][q_cap] score a query's claim overwrote
+    // candidates the windows list (GetFeaturesInArea sizes), added to
+    // ncand[f] (SURVEY §8d B_match's C); null: not counted
+    int32_t* ncand;
 };
 
 
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     int* claim = items + kc;                // kc
     int* minU = claim + kc;                 // kc
     uint8_t* done = (uint8_t*)(minU + kc);  // min(q_cap, Q_MAX)
-    __shared__ int s_any, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
+    __shared__ int s_any, s_nm, s_hist[HISTO_LENGTH], s_keep[3], s_cand;
 
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], kc);
@@ -284,6 +287,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
 
     if (tid == 0) {
         s_nm = 0;
+        s_cand = 0;
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
     build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, minU, MATCH_THREADS);
@@ -322,6 +326,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             const Query q = make_query(A, fc, f, k);
             int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
             bool ok = true, near = false;
+            int ncq = 0;
             if (q.valid) {
                 for (int ix = q.cx0; ix <= q.cx1 && ok; ix++) {
                     const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
@@ -333,6 +338,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
                         if (!level_ok(ko, q.minL, q.maxL)) continue;
                         if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
                         near = true;  // GetFeaturesInArea lists it (claimed or not)
+                        ncq++;
                         if (__hip_atomic_load(&claim[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
                             continue;
                         if (minU[idx] != k) {
@@ -357,6 +363,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
                 s_any = 1;
                 continue;
             }
+            if (A.ncand && ncq && !clocked) atomicAdd(&s_cand, ncq);
             done[k] = 1;
             int res = -1;
             bool reject = false;
@@ -405,12 +412,33 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             }
             if (tid == 0) rec[GF_CK_BUDGET_CUT] = c;
         }
+        if (A.ncand) {  // the candidates of the points that ran (the list up to the break)
+            const int nrun = c == INT_MAX ? nq : c + 1;
+            for (int k = tid; k < nrun; k += MATCH_THREADS) {
+                const Query q = make_query(A, fc, f, k);
+                if (!q.valid) continue;
+                int ncq = 0;
+                for (int ix = q.cx0; ix <= q.cx1; ix++) {
+                    const int s0 = cell_start[ix * GRID_ROWS + q.cy0], e0 = cell_start[ix * GRID_ROWS + q.cy1 + 1];
+                    for (int t = s0; t < e0; t++) {
+                        float kx, ky;
+                        int ko;
+                        cand(items[t], kx, ky, ko);
+                        ncq += level_ok(ko, q.minL, q.maxL) && fabsf(kx - q.x) <= q.r && fabsf(ky - q.y) <= q.r;
+                    }
+                }
+                if (ncq) atomicAdd(&s_cand, ncq);
+            }
+        }
         __syncthreads();
     }
     // ---- rotation consistency (ORBmatcher.cc:2146-2190)
     if (A.mode == MODE_LAST && A.check_ori) rotation_filter(A, f, nq, K, claim, score, &s_nm, s_hist, s_keep, MATCH_THREADS);
     for (int i = tid; i < n; i += MATCH_THREADS) kp2mp[i] = claim[i];
-    if (tid == 0) A.nmatches[f] = s_nm;
+    if (tid == 0) {
+        A.nmatches[f] = s_nm;
+        if (A.ncand) A.ncand[f] += s_cand;  // launches on one stream: no race
+    }
 }
 
 // ---- Per-query precompute for the wave-sequential matcher (SearchByProjection
@@ -469,6 +497,10 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
     // the sequential loop's tie order.
     const int g = tid & (SEQ_PRE_G - 1);
     constexpr unsigned long long NONE = ~0ull;
+    __shared__ int s_cand;
+    if (tid == 0) s_cand = 0;
+    __syncthreads();
+    int na = 0;  // this lane's area candidates (GetFeaturesInArea), for B_match's C
     for (int k0 = 0; k0 < nq; k0 += SEQ_PRE_THREADS / SEQ_PRE_G) {
         const int k = k0 + tid / SEQ_PRE_G;
         const bool live = k < nq;
@@ -484,9 +516,9 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
                     const int idx = items[t];
                     const float4 kp = X[idx];
                     const int oct = __float_as_int(kp.z);
-                    if (!level_ok(oct, q.minL, q.maxL) || fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r ||
-                        claim[idx] >= 0)
-                        continue;
+                    if (!level_ok(oct, q.minL, q.maxL) || fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
+                    na++;
+                    if (claim[idx] >= 0) continue;
                     const int dist = hamming32(q.d, DD + (long long)idx * 32);
                     nc++;
                     const unsigned long long kk = ((unsigned long long)dist << 48) |
@@ -529,6 +561,12 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
             r.ncand = q.valid ? (int16_t)min(nc, 5) : (int16_t)0;
             out[(long long)f * A.q_cap + k] = r;
         }
+    }
+    if (A.ncand) {
+        na = gfd::warp_sum(na);
+        if ((tid & 63) == 0 && na) atomicAdd(&s_cand, na);
+        __syncthreads();
+        if (tid == 0) A.ncand[f] += s_cand;
     }
 }
 
@@ -853,7 +891,16 @@ static int check_fi(const gf_frame_info* fi) {
     return GF_OK;
 }
 
-static int launch_match(gf_ctx* ctx, const MatchArgs& A, const FrameConst& fc, int nframes, hipStream_t s) {
+namespace {
+thread_local int32_t* tl_ncand = nullptr;
+}
+gf::CandidateCount::CandidateCount(int32_t* d_counts) : prev(tl_ncand) { tl_ncand = d_counts; }
+gf::CandidateCount::~CandidateCount() { tl_ncand = prev; }
+int32_t* gf::candidate_counts() { return tl_ncand; }
+
+static int launch_match(gf_ctx* ctx, const MatchArgs& A0, const FrameConst& fc, int nframes, hipStream_t s) {
+    MatchArgs A = A0;
+    A.ncand = tl_ncand;
     static unsigned long long attr_mask = 0;
     if (!(attr_mask & (1ull << ctx->device))) {
         GF_HIP(hipFuncSetAttribute((const void*)k_match, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));

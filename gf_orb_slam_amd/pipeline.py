@@ -67,7 +67,7 @@ FIELDS = {
     "clock": (32, np.int64, ("CK",)),  # budget clock record of the last step (abi.h GF_CK_*)
 }
 STATS = ["m3", "found", "to_match", "branch", "in_view", "local", "inl1", "inl2", "extra", "nleft", "iter1",
-         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal", "ncut"]
+         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal", "ncut", "cand_last", "cand_proj"]
 NSTAT = len(STATS)
 
 # GF_FE_CLOCK layout (abi.h GF_CK_*): header words, then per-stage elapsed-time

@@ -956,6 +956,10 @@ enum {
                            pushes, Observability.cc:1373): SURVEY §8d E_ld  */
     GF_ST_NLOCAL,       /* mvpLocalMapPoints size (keyframe graphs only)    */
     GF_ST_NCUT,         /* local points the isInFrustum cap moved to mLeftMapPoints */
+    GF_ST_CAND_LAST,    /* SearchByProjection(Cur, Last): area candidates (GetFeaturesInArea
+                           sizes; SURVEY §8d B_match's C)                   */
+    GF_ST_CAND_PROJ,    /* the same for SearchByProjection(F, local) and
+                           SearchByProjection_Budget together              */
     GF_FE_NSTAT
 };
 int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);

@@ -49,6 +49,7 @@ int orc_obs_active_match_rng(const gf_frame_info* fi, const gf_keypoint* kps, co
                              const float* level_sigma2, int num_to_match, float th, float nnratio, gf_rng* rng,
                              int32_t* kp2mp, int32_t* score, int32_t* left, int* nleft, int* nmatched);
 long long orc_last_ldets(void);
+long long orc_cand_take(void);
 int orc_undistort_keypoints(const float K[4], const float dist[5], const gf_keypoint* in, int n, gf_keypoint* out);
 int orc_frame_bounds(const float K[4], const float dist[5], int w, int h, int b[4]);
 int orc_obs_active_match_capped(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
@@ -494,10 +495,12 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     lap(0);
     const int n = c->nkp;
     int nm = 0;
+    orc_cand_take();
     orc_match_lastframe(&c->fi, c->kps.data(), c->desc.data(), n, c->Tcw, c->last_kps.data(), c->last_desc.data(),
                         c->last_kp2mp.data(), c->last_outl.data(), c->last_pos.data(), c->last_nkp, 15.f, 1,
                         c->kp2mp.data(), c->score.data(), &nm);
     st[GF_ST_M3] = nm;
+    st[GF_ST_CAND_LAST] = (int32_t)orc_cand_take();
     pose(c, &st[GF_ST_INL1], &st[GF_ST_ITER1], &st[GF_ST_EDGES1]);
     int found = 0;
     for (int i = 0; i < n; i++)
@@ -726,6 +729,7 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     nlist = (int)list.size();
     for (int k = 0; k < nlist; k++) c->left[k] = list[k];
     st[GF_ST_NLEFT] = nlist;
+    st[GF_ST_CAND_PROJ] = (int32_t)orc_cand_take();  // M2 and SearchByProjection_Budget (the one-point scans do not count)
     if (c->refmap) {  // the local map's state back to the stream map, indices back to map indices
         const int nl = (int)lmp.size();
         for (int k = 0; k < nl; k++) {

@@ -128,6 +128,10 @@ static inline void transform(const float* T, const float* P, float* Pc) {
 }
 
 int g_gemm_mode = 0;
+// area candidates (Frame::GetFeaturesInArea sizes) of the projection matchers
+// since the last orc_cand_take(): SURVEY §8d B_match's C, counted as the
+// device counts it
+long long g_cand = 0;
 
 // ORBmatcher::SearchByProjection_OnePoint (ORBmatcher.h:71-145) over a grid
 // built once per frame (runActiveMapMatching's one-point matches).
@@ -175,6 +179,12 @@ int one_point(const OnePointGrid* g, const gf_mp_view& v, const uint8_t* mp_desc
 extern "C" {
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return orc::descriptor_distance(a, b); }
+
+long long orc_cand_take(void) {
+    const long long c = orc::g_cand;
+    orc::g_cand = 0;
+    return c;
+}
 
 // docs/ORACLE_ASSUMPTIONS.md A1 (sensitivity runs only; 0 = parity)
 void orc_set_gemm_mode(int mode) { orc::g_gemm_mode = mode; }
@@ -240,6 +250,7 @@ int orc_match_project(const gf_frame_info* fi, const gf_keypoint* kps, const uin
         float r = orc::radius_by_viewing_cos(v.view_cos);
         if (bFactor) r *= th;
         std::vector<int> near = G.area(v.u, v.v, r * G.scales[pl], pl - 1, pl);
+        orc::g_cand += (long long)near.size();  // B_match's C
         if (near.empty()) continue;
         int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
         for (int idx : near) {
@@ -293,6 +304,7 @@ int orc_match_project_list(const gf_frame_info* fi, const gf_keypoint* kps, cons
         float r = orc::radius_by_viewing_cos(v.view_cos);
         if (bFactor) r *= th;
         std::vector<int> near = G.area(v.u, v.v, r * G.scales[pl], pl - 1, pl);
+        orc::g_cand += (long long)near.size();
         if (near.empty()) continue;
         int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
         for (int idx : near) {
@@ -346,6 +358,7 @@ int orc_match_lastframe(const gf_frame_info* fi, const gf_keypoint* kps, const u
         int oct = last_kps[i].octave;
         float radius = th * G.scales[oct];
         std::vector<int> idx2 = G.area(u, v, radius, oct - 1, oct + 1);
+        orc::g_cand += (long long)idx2.size();  // B_match's C
         if (idx2.empty()) continue;
         int bestDist = INT_MAX, bestIdx2 = -1;
         for (int i2 : idx2) {
