@@ -174,6 +174,7 @@ _PROTOS = {
     "gf_dist_bcast_map": [_P, _P, _I],
     "gf_vocab_download": [_P, _P, _P, _P, _P],
     "gf_select_map_points": [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "gf_select_pool": [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "gf_initialize": [_P, _P, _F, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P],
     "gf_initialize_dev": [_P, _P, _F, _I, _I, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P],
     "gf_initialize_batch_dev": [_P, _I, _P, _F, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],

@@ -451,7 +451,7 @@ bool Observability::runMatrixBuilding(size_t mat_type, double, bool, bool check_
     } else if (mat_type == MAP_INFO_MATRIX) {  // batchInfoMat_Map (Observability.cc:556-644)
         if (!mMapPoints) return false;
         for (MapPoint* p : *mMapPoints) {
-            if (!p || p->isBad()) continue;
+            if (!p) continue;  // batchInfoMat_Map tests the pointer only (:584)
             if (p->updateAtFrameId == (long)mnFrameId) continue;
             if (!check_viz && !p->mbTrackInView) continue;
             pts.push_back(p);
@@ -479,6 +479,7 @@ bool Observability::runMatrixBuilding(size_t mat_type, double, bool, bool check_
         p->v_proj = uv[2 * i + 1];
         std::memcpy(p->H_meas, &H[14 * (size_t)i], sizeof(p->H_meas));
         std::memcpy(p->ObsMat, &info[49 * (size_t)i], sizeof(p->ObsMat));
+        p->hasObsMat = true;
         if (frame) {
             p->ObsScore = pFrame->mvpMatchScore[kp[i]];
         } else {
@@ -534,45 +535,33 @@ bool Observability::setSelction_Number(size_t num_good_inlier, int greedy_mtd, d
     if (kinematic.size() < 2) return false;
     mKineIdx = 1;
     mMapPoints = mapPoints;
-    std::vector<int> idx;
-    std::vector<float> pos;
+    // MAP_INFO_MATRIX with the visibility check (:1039 -> batchInfoMat_Map
+    // :556-644): points updated this frame keep their blocks and scores, the
+    // others are rebuilt at kinematic[1] (ObsScore 1, stamped) or, not
+    // visible, get ObsScore -1
+    runMatrixBuilding(MAP_INFO_MATRIX, time_for_select / 2.0, true, true);
+    // lmkSelectPool: ObsScore >= 0 with a block, in list order (:1046-1058)
+    std::vector<size_t> pidx;
+    std::vector<double> pinfo, pscore;
     for (size_t i = 0; i < mapPoints->size(); i++) {
-        MapPoint* p = (*mapPoints)[i];
-        if (!p || p->isBad()) continue;
-        idx.push_back((int)i);
-        float x[3];
-        p->GetWorldPos(x);
-        pos.insert(pos.end(), x, x + 3);
+        const MapPoint* p = (*mapPoints)[i];
+        if (!p || !(p->ObsScore >= 0) || !p->hasObsMat) continue;
+        pidx.push_back(i);
+        pinfo.insert(pinfo.end(), p->ObsMat, p->ObsMat + 49);
+        pscore.push_back(p->ObsScore);
     }
     mpVec->clear();
-    const int n = (int)idx.size();
+    const int n = (int)pidx.size();
     if (n == 0) return true;
-    const gf_obs_camera cam = cam_now();
     std::vector<int32_t> out(n);
     int nout = 0;
-    check(gf_select_map_points(Context(), &cam, kinematic[1].Xv, pos.data(), n, (int)num_good_inlier, greedy_mtd,
-                               (int)mNumThreads, &rng_, out.data(), &nout));
-    // the MAP_INFO_MATRIX blocks of the selection (ObsMat at kinematic[1])
-    std::vector<float> spos(3 * (size_t)std::max(nout, 1));
-    for (int j = 0; j < nout; j++) std::memcpy(&spos[3 * (size_t)j], &pos[3 * (size_t)out[j]], 12);
-    std::vector<double> H(14 * (size_t)std::max(nout, 1)), info(49 * (size_t)std::max(nout, 1));
-    std::vector<float> uv(2 * (size_t)std::max(nout, 1));
-    std::vector<uint8_t> valid(std::max(nout, 1));
-    if (nout)
-        check(gf_obs_build_info(Context(), &cam, kinematic[1].Xv, spos.data(), nullptr, nout, 1, H.data(), info.data(),
-                                uv.data(), valid.data()));
+    check(gf_select_pool(Context(), pinfo.data(), pscore.data(), n, (int)num_good_inlier, greedy_mtd,
+                         (int)mNumThreads, &rng_, out.data(), &nout));
     for (int j = 0; j < nout; j++) {
         GoodPoint g;
-        g.idx = (size_t)idx[out[j]];
-        g.obs_score = 1.0;  // batchInfoMat_Map: ObsScore = 1 for a visible point
-        std::memcpy(g.obs_block.data(), &info[49 * (size_t)j], sizeof(double) * 49);
-        MapPoint* p = (*mapPoints)[g.idx];
-        std::memcpy(p->ObsMat, g.obs_block.data(), sizeof(p->ObsMat));
-        std::memcpy(p->H_meas, &H[14 * (size_t)j], sizeof(p->H_meas));
-        p->u_proj = uv[2 * j];
-        p->v_proj = uv[2 * j + 1];
-        p->ObsScore = 1.0;
-        p->updateAtFrameId = (long)mnFrameId;
+        g.idx = pidx[out[j]];
+        g.obs_score = pscore[out[j]];
+        std::memcpy(g.obs_block.data(), &pinfo[49 * (size_t)out[j]], sizeof(double) * 49);
         mpVec->push_back(g);
     }
     return true;

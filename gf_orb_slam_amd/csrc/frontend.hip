@@ -681,6 +681,12 @@ struct gf_frontend {
     // extraction run on ts, joined back into the context's stream at the end
     hipStream_t ts = nullptr;
     hipEvent_t ev_extracted = nullptr, ev_tracked = nullptr;
+    // a captured step forks RunMapPointsSelection's prediction (updatePWLSVec,
+    // MAP_INFO at kinematic[1]) from SearchAdditionalMatchesInFrame, as
+    // Tracking.cc:884-891 runs them on two threads: two graph branches
+    bool fork_post = false;
+    hipStream_t fork_s = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 namespace {
@@ -859,11 +865,21 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         GF_HIP(hipGetLastError());
     }
     if (D.gf) {
-        // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz)
-        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, s));
+        // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz);
+        // in a captured step a branch of its own beside SearchAdditionalMatchesInFrame
+        // (no shared data: the prediction writes Xv / H / ObsMat / u_proj / stamps,
+        // the search reads views, descriptors and keypoints)
+        hipStream_t sp = s;
+        if (fe->fork_post) {
+            GF_HIP(hipEventRecord(fe->ev_fork, s));
+            GF_HIP(hipStreamWaitEvent(fe->fork_s, fe->ev_fork, 0));
+            sp = fe->fork_s;
+        }
+        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, sp));
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
-                               fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, s,
+                               fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, sp,
                                sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel));
+        if (fe->fork_post) GF_HIP(hipEventRecord(fe->ev_join, sp));
         // SearchAdditionalMatchesInFrame
         if (sclk) {
             FE_RC(gf::frustum_clocked(ctx, fi, B, D.Tcw, D.map, nullptr, D.left, D.nlist_viz, M, 0.5f, D.views,
@@ -881,6 +897,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                             D.nlist, 0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA),
                                             sclk ? clock(D.t_sel0, GF_CK_OFF_BUD(M, R)) : gf::StageClock{},
                                             D.rest2, fe->qres, fe->qold, fe->merr, s));
+        if (fe->fork_post) GF_HIP(hipStreamWaitEvent(s, fe->ev_join, 0));  // thread_Select.join()
     }
     if (D.refmap) {
         {
@@ -1086,6 +1103,12 @@ int gf_frontend_destroy(gf_frontend* fe) {
     (void)hipSetDevice(fe->ctx->device);
     (void)hipStreamSynchronize(fe->ctx->stream);
     fe->ctx->frontends--;
+    if (fe->fork_s) {
+        (void)hipStreamSynchronize(fe->fork_s);
+        (void)hipEventDestroy(fe->ev_fork);
+        (void)hipEventDestroy(fe->ev_join);
+        (void)hipStreamDestroy(fe->fork_s);
+    }
     if (fe->ts) {
         fe->ctx->track_stream = false;
         (void)hipStreamSynchronize(fe->ts);
@@ -1438,10 +1461,17 @@ int gf_frontend_capture(gf_frontend* fe) {
     fe->D.select_ticks = ticks(fe->ctx->select_budget_s);
     const bool prof = fe->ctx->prof;
     fe->ctx->prof = false;  // no event records inside the graph
+    if (!fe->fork_s) {
+        GF_HIP(hipStreamCreateWithFlags(&fe->fork_s, hipStreamNonBlocking));
+        GF_HIP(hipEventCreateWithFlags(&fe->ev_fork, hipEventDisableTiming));
+        GF_HIP(hipEventCreateWithFlags(&fe->ev_join, hipEventDisableTiming));
+    }
+    fe->fork_post = true;
     GF_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = fe_track(fe, s);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(s, &g);
+    fe->fork_post = false;
     fe->ctx->prof = prof;
     if (rc) {
         if (g) (void)hipGraphDestroy(g);

@@ -1983,12 +1983,55 @@ int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n
     return GF_OK;
 }
 
-// Observability::setSelction_Number over map points (Observability.cc:
-// 1021-1247): MAP_INFO_MATRIX with the visibility check on the device, the
-// visible pool in list order, then the greedy of greedy_mtd on the device
-// (k_maxvol); mode 3 splits a large pool into threadNeeded chunks as the
-// reference does (:1086-1160), run in chunk order on the caller's rand()
-// stream, and finishes with an automatic pass over the merged selections.
+// Observability::setSelction_Number's greedy stage over a prepared pool
+// (lmkSelectPool, Observability.cc:1072-1160): greedy_mtd 1 / 2 on the pool,
+// 3 splits a large pool into threadNeeded chunks as the reference does
+// (:1086-1160), run in chunk order on the caller's rand() stream, then an
+// automatic pass over the merged selections (which keep their scores).
+int gf_select_pool(gf_ctx* ctx, const double* info, const double* score, int n, int k, int greedy_mtd,
+                   int max_threads, gf_rng* rng, int32_t* out_idx, int* nout) {
+    GF_CHECK(ctx && rng && nout, GF_ERR_ARG, "null arg");
+    GF_CHECK(greedy_mtd >= 1 && greedy_mtd <= 3, GF_ERR_ARG, "greedy_mtd must be 1, 2 or 3");
+    *nout = 0;
+    const int P = n;
+    if (P <= 0) return GF_OK;
+    GF_CHECK(info && score && out_idx, GF_ERR_ARG, "null arg");
+    const double scale = 6.0;  // random_sample_scale of the map overload (:1035)
+    int rc;
+    int T = 1;
+    if (greedy_mtd == 3 && !((float)P - 1.2f * (float)k <= 10 || P < 2 * 1000))
+        T = std::max(1, std::min((int)std::lround((float)P / 1000.f), max_threads));
+    if (T == 1) return gf_maxvol_select(ctx, info, score, P, k, scale, greedy_mtd, rng, out_idx, nout);
+    const int kpar = (int)std::ceil((float)k / (float)T * 1.2f);
+    const int npar = (int)std::ceil((float)P / (float)T);
+    std::vector<int> merged;
+    for (int t = 0; t < T; t++) {
+        const int lo = t * npar, hi = std::min(P, (t + 1) * npar);
+        if (hi <= lo) continue;
+        std::vector<int32_t> o(hi - lo);
+        int no = 0;
+        rc = gf_maxvol_select(ctx, &info[49 * (size_t)lo], &score[lo], hi - lo, kpar, scale, 3, rng, o.data(), &no);
+        if (rc) return rc;
+        for (int q = 0; q < no; q++) merged.push_back(lo + o[q]);
+    }
+    const int Mg = (int)merged.size();
+    std::vector<double> minfo(49 * (size_t)std::max(Mg, 1)), mscore(std::max(Mg, 1));
+    for (int j = 0; j < Mg; j++) {
+        memcpy(&minfo[49 * (size_t)j], &info[49 * (size_t)merged[j]], 49 * sizeof(double));
+        mscore[j] = score[merged[j]];
+    }
+    std::vector<int32_t> o(std::max(Mg, 1));
+    int no = 0;
+    rc = gf_maxvol_select(ctx, minfo.data(), mscore.data(), Mg, k, scale, 3, rng, o.data(), &no);
+    if (rc) return rc;
+    for (int q = 0; q < no; q++) out_idx[(*nout)++] = merged[o[q]];
+    return GF_OK;
+}
+
+// Observability::setSelction_Number over fresh map points (Observability.cc:
+// 1021-1247): MAP_INFO_MATRIX with the visibility check on the device (no
+// point updated this frame), the visible pool in list order with ObsScore 1,
+// then gf_select_pool.
 int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv, const float* pos, int n, int k,
                          int greedy_mtd, int max_threads, gf_rng* rng, int32_t* out_idx, int* nout) {
     GF_CHECK(ctx && cam && Xv && rng && nout, GF_ERR_ARG, "null arg");
@@ -2007,37 +2050,10 @@ int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv
     const int P = (int)pool.size();
     std::vector<double> pinfo(49 * (size_t)std::max(P, 1)), pscore(std::max(P, 1), 1.0);
     for (int j = 0; j < P; j++) memcpy(&pinfo[49 * (size_t)j], &info[49 * (size_t)pool[j]], 49 * sizeof(double));
-    const double scale = 6.0;  // random_sample_scale of the map overload (:1035)
     std::vector<int32_t> sel(std::max(P, 1));
     int ns = 0;
-    int T = 1;
-    if (greedy_mtd == 3 && !((float)P - 1.2f * (float)k <= 10 || P < 2 * 1000))
-        T = std::max(1, std::min((int)std::lround((float)P / 1000.f), max_threads));
-    if (T == 1) {
-        rc = gf_maxvol_select(ctx, pinfo.data(), pscore.data(), P, k, scale, greedy_mtd, rng, sel.data(), &ns);
-        if (rc) return rc;
-    } else {
-        const int kpar = (int)std::ceil((float)k / (float)T * 1.2f);
-        const int npar = (int)std::ceil((float)P / (float)T);
-        std::vector<int> merged;
-        for (int t = 0; t < T; t++) {
-            const int lo = t * npar, hi = std::min(P, (t + 1) * npar);
-            if (hi <= lo) continue;
-            std::vector<int32_t> o(hi - lo);
-            int no = 0;
-            rc = gf_maxvol_select(ctx, &pinfo[49 * (size_t)lo], &pscore[lo], hi - lo, kpar, scale, 3, rng, o.data(), &no);
-            if (rc) return rc;
-            for (int q = 0; q < no; q++) merged.push_back(lo + o[q]);
-        }
-        const int Mg = (int)merged.size();
-        std::vector<double> minfo(49 * (size_t)std::max(Mg, 1)), mscore(std::max(Mg, 1), 1.0);
-        for (int j = 0; j < Mg; j++) memcpy(&minfo[49 * (size_t)j], &pinfo[49 * (size_t)merged[j]], 49 * sizeof(double));
-        std::vector<int32_t> o(std::max(Mg, 1));
-        int no = 0;
-        rc = gf_maxvol_select(ctx, minfo.data(), mscore.data(), Mg, k, scale, 3, rng, o.data(), &no);
-        if (rc) return rc;
-        for (int q = 0; q < no; q++) sel[ns++] = merged[o[q]];
-    }
+    rc = gf_select_pool(ctx, pinfo.data(), pscore.data(), P, k, greedy_mtd, max_threads, rng, sel.data(), &ns);
+    if (rc) return rc;
     for (int q = 0; q < ns; q++) out_idx[(*nout)++] = pool[sel[q]];
     return GF_OK;
 }

@@ -289,6 +289,15 @@ int gf_obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint*
 int gf_maxvol_select(gf_ctx* ctx, const double* info, const double* score, int n, int k, double sample_scale,
                      int mode, gf_rng* rng, int32_t* out_idx, int* nout);
 
+/* The greedy stage alone, over a prepared pool (lmkSelectPool,
+ * Observability.cc:1046-1160): n blocks info [n][49] with their ObsScore
+ * values, k = num_good_inlier; out_idx = pool positions selected (greedy_mtd
+ * 3 splits large pools into threadNeeded chunks, run in chunk order on rng).
+ * What setSelction_Number runs after MAP_INFO_MATRIX has left points updated
+ * this frame (e.g. by FRAME_INFO_MATRIX) with their own blocks and scores. */
+int gf_select_pool(gf_ctx* ctx, const double* info, const double* score, int n, int k, int greedy_mtd,
+                   int max_threads, gf_rng* rng, int32_t* out_idx, int* nout);
+
 /* Observability::setSelction_Number(num_good_inlier, greedy_mtd, time,
  * mapPoints, mpVec) (Observability.cc:1021-1247; test/test_GoodMap.cpp drives
  * it): MAP_INFO_MATRIX with the visibility check (mKineIdx = 1: Xv is the

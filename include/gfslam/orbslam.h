@@ -86,6 +86,7 @@ struct MapPoint {
     /* written by Observability (MapPoint.h: H_meas, ObsMat, u/v_proj, ...) */
     double H_meas[14] = {};
     double ObsMat[49] = {};
+    bool hasObsMat = false; /* ObsMat.n_rows > 0 (an arma::mat set by a build) */
     float u_proj = 0, v_proj = 0;
     double ObsScore = 0;
     long updateAtFrameId = -1;

@@ -664,9 +664,60 @@ int orc_maxvol_select(const double* info, const double* score, int n, int k, dou
 // 1), the pool of visible points in list order, then greedy_mtd 1 (baseline),
 // 2 (lazier) or 3 (automatic, split over threadNeeded chunks when the pool is
 // large: :1086-1160; the chunks run in chunk order on one rand() stream).
+// setSelction_Number's greedy stage over a prepared pool (lmkSelectPool,
+// Observability.cc:1072-1160): greedy_mtd 1 / 2 on the pool; 3 splits a
+// large pool into threadNeeded chunks (:1086-1160) run in chunk order on one
+// rand() stream (the reference runs them on threads sharing std::rand: an
+// ordering assumption, docs/ORACLE_ASSUMPTIONS.md), then an automatic pass
+// over the merged selections, which keep their pool scores (:1141-1146).
+int orc_select_pool(const double* info, const double* score, int P, int k, int greedy_mtd, int max_threads,
+                    gf_rng* rng, int32_t* out_idx, int* nout) {
+    *nout = 0;
+    if (greedy_mtd < 1 || greedy_mtd > 3) return GF_ERR_ARG;
+    if (P <= 0) return GF_OK;
+    orc::Rand R;
+    R.load(*rng);
+    const double scale = 6.0;
+    if (greedy_mtd == 1 || greedy_mtd == 2) {
+        maxvol_select(R, info, score, P, k, scale, greedy_mtd, out_idx, nout);
+    } else {
+        int T = 1;
+        if (!((float)P - 1.2f * (float)k <= 10 || P < 2 * 1000)) T = std::min((int)std::lround((float)P / 1000.f), max_threads);
+        T = std::max(T, 1);
+        if (T == 1) {
+            maxvol_select(R, info, score, P, k, scale, 3, out_idx, nout);
+        } else {
+            const int kpar = (int)std::ceil((float)k / (float)T * 1.2f);
+            const int npar = (int)std::ceil((float)P / (float)T);
+            std::vector<int> merged;  // pool positions, chunk by chunk
+            for (int t = 0; t < T; t++) {
+                const int lo = t * npar, hi = std::min(P, (t + 1) * npar);
+                if (hi <= lo) continue;
+                std::vector<int32_t> o(hi - lo);
+                int no = 0;
+                maxvol_select(R, &info[49 * (size_t)lo], &score[lo], hi - lo, kpar, scale, 3, o.data(), &no);
+                for (int q = 0; q < no; q++) merged.push_back(lo + o[q]);
+            }
+            const int Mg = (int)merged.size();
+            std::vector<double> minfo(49 * (size_t)std::max(Mg, 1)), mscore(std::max(Mg, 1));
+            for (int j = 0; j < Mg; j++) {
+                std::memcpy(&minfo[49 * (size_t)j], &info[49 * (size_t)merged[j]], 49 * sizeof(double));
+                mscore[j] = score[merged[j]];
+            }
+            std::vector<int32_t> o(std::max(Mg, 1));
+            int no = 0;
+            maxvol_select(R, minfo.data(), mscore.data(), Mg, k, scale, 3, o.data(), &no);
+            for (int q = 0; q < no; q++) out_idx[(*nout)++] = merged[o[q]];
+        }
+    }
+    R.save(*rng);
+    return GF_OK;
+}
+
 int orc_select_map_points(const gf_obs_camera* cam, const double* Xv, const float* pos, int n, int k,
                           int greedy_mtd, int max_threads, gf_rng* rng, int32_t* out_idx, int* nout) {
     *nout = 0;
+    if (greedy_mtd < 1 || greedy_mtd > 3) return GF_ERR_ARG;
     std::vector<double> H(14 * (size_t)std::max(n, 1)), info(49 * (size_t)std::max(n, 1));
     std::vector<float> uv(2 * (size_t)std::max(n, 1));
     std::vector<uint8_t> valid(std::max(n, 1));
@@ -677,46 +728,11 @@ int orc_select_map_points(const gf_obs_camera* cam, const double* Xv, const floa
     const int P = (int)pool.size();
     std::vector<double> pinfo(49 * (size_t)std::max(P, 1)), pscore(std::max(P, 1), 1.0);
     for (int j = 0; j < P; j++) std::memcpy(&pinfo[49 * (size_t)j], &info[49 * (size_t)pool[j]], 49 * sizeof(double));
-    orc::Rand R;
-    R.load(*rng);
-    const double scale = 6.0;
     std::vector<int32_t> sel(std::max(P, 1));
     int ns = 0;
-    if (greedy_mtd == 1 || greedy_mtd == 2) {
-        maxvol_select(R, pinfo.data(), pscore.data(), P, k, scale, greedy_mtd, sel.data(), &ns);
-    } else if (greedy_mtd == 3) {
-        int T = 1;
-        if (!((float)P - 1.2f * (float)k <= 10 || P < 2 * 1000)) T = std::min((int)std::lround((float)P / 1000.f), max_threads);
-        T = std::max(T, 1);
-        if (T == 1) {
-            maxvol_select(R, pinfo.data(), pscore.data(), P, k, scale, 3, sel.data(), &ns);
-        } else {
-            const int kpar = (int)std::ceil((float)k / (float)T * 1.2f);
-            const int npar = (int)std::ceil((float)P / (float)T);
-            std::vector<int> merged;  // pool positions, chunk by chunk
-            for (int t = 0; t < T; t++) {
-                const int lo = t * npar, hi = std::min(P, (t + 1) * npar);
-                if (hi <= lo) continue;
-                std::vector<int32_t> o(hi - lo);
-                int no = 0;
-                maxvol_select(R, &pinfo[49 * (size_t)lo], &pscore[lo], hi - lo, kpar, scale, 3, o.data(), &no);
-                for (int q = 0; q < no; q++) merged.push_back(lo + o[q]);
-            }
-            const int Mg = (int)merged.size();
-            std::vector<double> minfo(49 * (size_t)std::max(Mg, 1)), mscore(std::max(Mg, 1), 1.0);
-            for (int j = 0; j < Mg; j++)
-                std::memcpy(&minfo[49 * (size_t)j], &pinfo[49 * (size_t)merged[j]], 49 * sizeof(double));
-            std::vector<int32_t> o(std::max(Mg, 1));
-            int no = 0;
-            maxvol_select(R, minfo.data(), mscore.data(), Mg, k, scale, 3, o.data(), &no);
-            for (int q = 0; q < no; q++) sel[ns++] = merged[o[q]];
-        }
-    } else {
-        return GF_ERR_ARG;
-    }
+    int rc = orc_select_pool(pinfo.data(), pscore.data(), P, k, greedy_mtd, max_threads, rng, sel.data(), &ns);
     for (int q = 0; q < ns; q++) out_idx[(*nout)++] = pool[sel[q]];
-    R.save(*rng);
-    return GF_OK;
+    return rc;
 }
 
 static int maxvol_select(orc::Rand& R, const double* info, const double* score, int n, int k, double sample_scale,

@@ -181,7 +181,32 @@ int main(int argc, char** argv) {
         sel.srand(9);
         std::vector<GoodPoint> good;
         const bool no_time = sel.setSelction_Number(300, 3, 0.0, &local, &good);
+        // points updated this frame before the selection (FRAME_INFO_MATRIX of
+        // matched points: their own block and score) keep them: every 7th
+        // local point with a scaled identity block and score 0.5, every 11th
+        // with ObsScore -1 (no pool entry)
+        sel.mnFrameId = 5;
+        for (size_t i = 0; i < local.size(); i++) {
+            MapPoint* q = local[i];
+            if (i % 7 == 3) {
+                q->updateAtFrameId = 5;
+                for (int e = 0; e < 49; e++) q->ObsMat[e] = (e % 8 == 0) ? 1e3 * (1 + (double)(i % 5)) : 0.0;
+                q->hasObsMat = true;
+                q->ObsScore = 0.5;
+            } else if (i % 11 == 4) {
+                q->updateAtFrameId = 5;
+                q->ObsScore = -1.0;
+            }
+        }
         const bool ok = sel.setSelction_Number(300, 3, 1.0, &local, &good);
+        std::vector<double> lscore;
+        std::vector<int32_t> lstamp;
+        for (MapPoint* q : local) {
+            lscore.push_back(q->ObsScore);
+            lstamp.push_back((int32_t)q->updateAtFrameId);
+        }
+        dump(dir + "/select_scores.f64", lscore.data(), lscore.size());
+        dump(dir + "/select_stamps.i32", lstamp.data(), lstamp.size());
         std::vector<int32_t> gidx;
         for (const GoodPoint& g : good) gidx.push_back((int32_t)g.idx);
         dump(dir + "/select.i32", gidx.data(), gidx.size());

@@ -137,17 +137,37 @@ def test_dropin_frontend_matches_oracle(tmp_path):
     ocam = ObsCamera.for_tracking(*(float(np.float32(v)) for v in (fx, fy, cx, cy)), w, h)
     ks = O.obs_predict(xv, 0.05, 2)
     xv1 = np.array(ks[1].Xv[:])
-    sel = np.zeros(len(mps), np.int32)
-    nsel = ctypes.c_int()
+    # batchInfoMat_Map (:556-644) over the local list: every 7th point was
+    # updated this frame (its own block, score 0.5), every 11th too with score
+    # -1; the others are rebuilt at kinematic[1], visible ones into the pool
+    # (score 1, stamped), invisible ones get score -1 (stamp unchanged)
     pos = np.ascontiguousarray(mps["pos"], np.float32)
-    assert O.orc().orc_select_map_points(ctypes.byref(ocam), O._p(xv1), O._p(pos), len(pos), 300, 3, 8,
-                                         ctypes.byref(Rng.seeded(9)), O._p(sel), ctypes.byref(nsel)) == 0
+    n = len(pos)
+    _, blk_all, _, valid = O.obs_build_info(ocam, xv1, pos, None, 1)
+    blk_all = blk_all.reshape(n, 49)
+    pre = np.array([i % 7 == 3 for i in range(n)])
+    pre_neg = np.array([(i % 7 != 3) and (i % 11 == 4) for i in range(n)])
+    fresh = ~pre & ~pre_neg
+    score = np.where(pre, 0.5, np.where(pre_neg, -1.0, np.where(valid.astype(bool), 1.0, -1.0)))
+    pool = np.nonzero(score >= 0)[0]
+    pinfo = np.ascontiguousarray(np.where(pre[pool, None], 0.0, blk_all[pool]))
+    for j, i in enumerate(pool):
+        if pre[i]:
+            pinfo[j, [0, 8, 16, 24, 32, 40, 48]] = 1e3 * (1 + (i % 5))
+    pscore = np.ascontiguousarray(score[pool])
+    sel = np.zeros(len(pool), np.int32)
+    nsel = ctypes.c_int()
+    assert O.orc().orc_select_pool(O._p(pinfo), O._p(pscore), len(pool), 300, 3, 8, ctypes.byref(Rng.seeded(9)),
+                                   O._p(sel), ctypes.byref(nsel)) == 0
     assert no_time == 0 and ok == 1
     gsel = rd("select.i32", np.int32)
-    assert len(gsel) == nsel.value == 300 and np.array_equal(gsel, sel[:nsel.value])
-    _, blk, _, _ = O.obs_build_info(ocam, xv1, pos[gsel], None, 1)
-    np.testing.assert_allclose(rd("select_blocks.f64", np.float64).reshape(-1, 49), blk.reshape(-1, 49), rtol=1e-9,
-                               atol=1e-12)
+    assert len(gsel) == nsel.value == 300 and np.array_equal(gsel, pool[sel[:nsel.value]])
+    np.testing.assert_allclose(rd("select_blocks.f64", np.float64).reshape(-1, 49), pinfo[sel[:nsel.value]],
+                               rtol=1e-9, atol=1e-12)
+    assert np.array_equal(rd("select_scores.f64", np.float64), score)
+    stamps = rd("select_stamps.i32", np.int32)
+    assert (stamps[pre | pre_neg] == 5).all() and (stamps[fresh & valid.astype(bool)] == 5).all()
+    assert (stamps[fresh & ~valid.astype(bool)] != 5).all()
 
 
 SEQ_BIN = os.path.join(ROOT, "tests", "cpp", "sequence_driver")
