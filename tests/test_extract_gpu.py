@@ -86,6 +86,25 @@ def test_fast_threshold_edges(fast_th):
     assert np.array_equal(dg, do)
 
 
+@pytest.mark.parametrize("nf", [200, 1000])
+def test_long_cell_lists(nf):
+    """Dense corners: uniform noise whose contrast ramps across the image,
+    so a cell's corner list after NMS spans from none to thousands (cells of
+    tens of thousands of pixels at 200 features). Lists longer than the
+    selection's per-wave LDS buffers (k_select: SEL_BUF = SEL_BUF_CELL = 1024
+    entries; with -DSEL_BUF_CELL=256 lists of 257..1024 wait for wave 0's
+    buffer) take the sequential replay in global memory; the cut must match
+    the oracle's retainBest either way (ORBextractor.cc:647-651, 750-752)."""
+    rng = np.random.default_rng(21)
+    h, w = 480, 752
+    amp = np.linspace(0, 255, w)[None, :]
+    img = (128 + (rng.random((h, w)) - 0.5) * amp).clip(0, 255).astype(np.uint8)
+    kg, dg = ORBextractor(nf, 1.2, 8, 1, 20)(img)
+    ko, do = O.extract(img, nfeatures=nf)
+    assert kg.tobytes() == ko.tobytes(), _diff_report(kg, ko)
+    assert np.array_equal(dg, do)
+
+
 def test_flat_image_no_keypoints():
     img = np.full((480, 640), 77, np.uint8)
     kg, dg = ORBextractor(1000)(img)
