@@ -1171,38 +1171,38 @@ int ba_launch_step(gf_ba_plan* P, hipStream_t s) {
         ggemm((P->max_items + BA_SW - 1) / BA_SW, B), gred((P->max_ss + 255) / 256, B);
     {
         GF_PROF(P->ctx, s, "k_ba_linearize");
-        k_ba_linearize<<<gpt, BA_T, 0, s>>>(A);
+        GF_LAUNCH(k_ba_linearize, gpt, BA_T, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_poses");
-        k_ba_poses<<<gpose, BA_PT, 0, s>>>(A);
+        GF_LAUNCH(k_ba_poses, gpose, BA_PT, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_schur_pts");
-        k_ba_schur_pts<<<gedge, BA_T, 0, s>>>(A);
+        GF_LAUNCH(k_ba_schur_pts, gedge, BA_T, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_gemm");
         if (P->sparse_gemm)
-            k_ba_spgemm<<<ggemm, 64 * BA_SW, 0, s>>>(A);
+            GF_LAUNCH(k_ba_spgemm, ggemm, 64 * BA_SW, 0, s, A);
         else
-            k_ba_gemm<<<dim3(P->max_split, B), 64 * BA_GW, ba_gemm_lds(P->max_npad), s>>>(A);
+            GF_LAUNCH(k_ba_gemm, dim3(P->max_split, B), 64 * BA_GW, ba_gemm_lds(P->max_npad), s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_gemm_reduce");
-        k_ba_gemm_reduce<<<gred, 256, 0, s>>>(A);
+        GF_LAUNCH(k_ba_gemm_reduce, gred, 256, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_solve");
-        k_ba_solve<<<B, BA_ST, 0, s>>>(A);
+        GF_LAUNCH(k_ba_solve, B, BA_ST, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_update");
-        k_ba_update<<<gpt, BA_T, 0, s>>>(A);
+        GF_LAUNCH(k_ba_update, gpt, BA_T, 0, s, A);
     }
     {
         GF_PROF(P->ctx, s, "k_ba_decide");
-        k_ba_decide<<<B, 1024, 0, s>>>(A);
+        GF_LAUNCH(k_ba_decide, B, 1024, 0, s, A);
     }
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -1539,7 +1539,7 @@ int gf_ba_plan_solve_stop(gf_ba_plan* P, void* stream, const volatile uint8_t* s
     GF_HIP(hipMemsetAsync(P->A.panel, 0, P->panel_doubles * sizeof(double), s));
     {
         GF_PROF(P->ctx, s, "k_ba_init");
-        k_ba_init<<<P->nprob, 256, 0, s>>>(P->A);
+        GF_LAUNCH(k_ba_init, P->nprob, 256, 0, s, P->A);
         GF_HIP(hipGetLastError());
     }
     int n = 0;
@@ -1563,7 +1563,7 @@ int gf_ba_plan_solve_stop(gf_ba_plan* P, void* stream, const volatile uint8_t* s
     }
     {
         GF_PROF(P->ctx, s, "k_ba_finish");
-        k_ba_finish<<<P->nprob, 256, 0, s>>>(P->A);
+        GF_LAUNCH(k_ba_finish, P->nprob, 256, 0, s, P->A);
         GF_HIP(hipGetLastError());
     }
     GF_HIP(hipStreamSynchronize(s));

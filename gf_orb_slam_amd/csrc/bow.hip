@@ -682,12 +682,12 @@ int gf_bow_transform_dev(gf_vocab* v, int nframes, const uint8_t* d_desc, const 
     const VocabDev V = vdev(v);
     {
         GF_PROF(v->ctx, s, "k_bow_descend");
-        k_bow_descend<<<dim3((cap + 255) / 256, nframes), 256, 0, s>>>(V, d_desc, d_n, cap, levelsup, wid, wv, nid);
+        GF_LAUNCH(k_bow_descend, dim3((cap + 255) / 256, nframes), 256, 0, s, V, d_desc, d_n, cap, levelsup, wid, wv, nid);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(v->ctx, s, "k_bow_build");
-        k_bow_build<<<nframes, 256, 0, s>>>(V, d_n, cap, wid, wv, nid, d_words, d_values, d_nwords, d_fv_nodes,
+        GF_LAUNCH(k_bow_build, nframes, 256, 0, s, V, d_n, cap, wid, wv, nid, d_words, d_values, d_nwords, d_fv_nodes,
                                             d_fv_start, d_fv_feats, d_nfv);
         GF_HIP(hipGetLastError());
     }
@@ -759,7 +759,7 @@ int gf_match_bow_dev(gf_ctx* ctx, int mode, float nnratio, int check_ori, int np
     if (rc) return rc;
     GF_HIP(hipMemcpyAsync(dp, P.data(), sizeof(BowPair) * npairs, hipMemcpyHostToDevice, s));
     GF_PROF(ctx, s, "k_match_bow");
-    k_match_bow<<<npairs, 256, 0, s>>>((const BowPair*)dp, mode, nnratio, check_ori, d_nmatches);
+    GF_LAUNCH(k_match_bow, npairs, 256, 0, s, (const BowPair*)dp, mode, nnratio, check_ori, d_nmatches);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -862,7 +862,7 @@ int gf_search_for_triangulation_dev(gf_ctx* ctx, int check_ori, int npairs, cons
     if (rc) return rc;
     GF_HIP(hipMemcpyAsync(dp, T.data(), sizeof(TriPair) * npairs, hipMemcpyHostToDevice, s));
     GF_PROF(ctx, s, "k_search_tri");
-    k_search_tri<<<npairs, TRI_THREADS, 0, s>>>((const TriPair*)dp, check_ori, d_nmatches);
+    GF_LAUNCH(k_search_tri, npairs, TRI_THREADS, 0, s, (const TriPair*)dp, check_ori, d_nmatches);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -1,9 +1,12 @@
 // Shared runtime pieces of libgfslam: error capture, context, device helpers.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gfslam/abi.h"
@@ -45,6 +48,7 @@ struct gf_ctx {
     double match_budget_s = __builtin_inf(), select_budget_s = __builtin_inf();
     std::vector<gf::ProfEntry> prof_entries;
     std::vector<hipEvent_t> event_pool;
+    std::vector<hipEvent_t> prof_spent;  // stop events of multi-launch scopes that are not read
     // grow-only device scratch for the host-family wrappers (one slot per use)
     static const int kSlots = 64;
     void* ws[kSlots] = {};
@@ -157,17 +161,38 @@ int dist_bcast(gf_dist* d, void* buf, size_t bytes, int root);
 int dist_rank(gf_dist* d);
 gf_ctx* dist_ctx(gf_dist* d);
 
-// RAII bracket for one kernel launch when profiling is on.
+// Per-kernel timing when profiling is on (gf_prof_enable): a ProfScope names
+// the launches made while it is the innermost open scope on this thread
+// (GF_LAUNCH). Their start / stop events are taken from the kernels' own
+// dispatch timestamps (hipExtLaunchKernel), not recorded on the stream
+// around them, so a kernel waiting for compute units held by another stream's
+// kernels does not count that wait (the figure rocprof reports). A scope
+// with several launches spans the first one's start to the last one's end.
 struct ProfScope {
     gf_ctx* ctx;
     hipStream_t s;
     int idx = -1;
+    ProfScope* prev = nullptr;
+    hipEvent_t first = nullptr, last = nullptr;
     ProfScope(gf_ctx* c, hipStream_t st, const char* name);
     ~ProfScope();
 };
+// The events of the next launch in the innermost scope (false: not profiling).
+bool prof_launch_events(hipEvent_t* start, hipEvent_t* stop);
+
+template <typename... KArgs, typename... Args>
+inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipStream_t s, Args&&... args) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof_launch_events(&e0, &e1))
+        hipExtLaunchKernelGGL(k, grid, block, (std::uint32_t)lds, s, e0, e1, 0, static_cast<KArgs>(args)...);
+    else
+        k<<<grid, block, lds, s>>>(std::forward<Args>(args)...);
+}
 }  // namespace gf
 
 #define GF_PROF(ctx, stream, name) ::gf::ProfScope _gf_prof_scope((ctx), (stream), (name))
+// kernel<<<grid, block, lds, stream>>>(args...), timed by the innermost GF_PROF scope
+#define GF_LAUNCH(kernel, grid, block, lds, stream, ...) ::gf::launch(kernel, grid, block, lds, stream, __VA_ARGS__)
 
 // Device-side helpers ------------------------------------------------------
 namespace gfd {

@@ -1520,7 +1520,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
         for (int l = 1; l < ex->nlevels; l++) {
             const size_t lds = (((size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l] + 15) & ~(size_t)15) +
                                RS_H * sizeof(int2) + 8;
-            k_resize<<<dim3(ex->rs_tiles[l], nframes), 256, lds, s>>>(P, g, l, ex->d_xtab + ex->xtab_off[l],
+            GF_LAUNCH(k_resize, dim3(ex->rs_tiles[l], nframes), 256, lds, s, P, g, l, ex->d_xtab + ex->xtab_off[l],
                                                                       ex->d_ytab + ex->ytab_off[l], ex->rs_tiles_x[l],
                                                                       ex->rs_pitch[l], ex->rs_rows[l]);
         }
@@ -1528,25 +1528,25 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     if (ex->stage_ev && ex->stage_after == 0) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_blur_fast");
-        k_blur_fast<<<dim3(ex->max_tiles, nframes), 256, 0, s>>>(P, g, ex->d_score, ex->fast_th);
+        GF_LAUNCH(k_blur_fast, dim3(ex->max_tiles, nframes), 256, 0, s, P, g, ex->d_score, ex->fast_th);
     }
     if (ex->stage_ev && ex->stage_after == 1) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_fast_cells");
-        k_fast_cells<<<dim3(g.ncells, nframes), 256, ex->fast_lds, s>>>(
+        GF_LAUNCH(k_fast_cells, dim3(g.ncells, nframes), 256, ex->fast_lds, s, 
             P, g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
     }
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
-        k_select<<<dim3(ex->nlevels, nframes), SEL_THREADS, SEL_LDS, s>>>(g, ex->d_cells, ex->d_lists, ex->list_stride,
+        GF_LAUNCH(k_select, dim3(ex->nlevels, nframes), SEL_THREADS, SEL_LDS, s, g, ex->d_cells, ex->d_lists, ex->list_stride,
                                                             ex->d_counts, ex->d_lvl, ex->lvl_stride,
                                                             ex->d_lvl_counts);
     }
     if (ex->stage_ev && ex->stage_after == 3) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_describe");
-        k_describe<<<dim3((ex->capacity + 7) / 8, nframes), 256, 0, s>>>(P, g, ex->d_lvl, ex->lvl_stride,
+        GF_LAUNCH(k_describe, dim3((ex->capacity + 7) / 8, nframes), 256, 0, s, P, g, ex->d_lvl, ex->lvl_stride,
                                                                           ex->d_lvl_counts, d_kps, d_desc, d_counts,
                                                                           cap);
     }

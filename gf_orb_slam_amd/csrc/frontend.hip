@@ -755,7 +755,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
     {
         GF_PROF(ctx, s, "k_fe_begin");
-        k_fe_begin<<<B, 256, 0, s>>>(D);
+        GF_LAUNCH(k_fe_begin, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
@@ -792,11 +792,11 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                           gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
         {
             GF_PROF(ctx, s, "k_fe_gather_rows");
-            k_fe_gather_rows<<<dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s>>>(D, fe->gm, WM);
+            GF_LAUNCH(k_fe_gather_rows, dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM);
             GF_HIP(hipGetLastError());
         }
         GF_PROF(ctx, s, "k_fe_gather");
-        k_fe_gather<<<B, 256, 0, s>>>(D, fe->w_nmp);
+        GF_LAUNCH(k_fe_gather, B, 256, 0, s, D, fe->w_nmp);
         GF_HIP(hipGetLastError());
     }
     // TrackLocalMap -> SearchReferencePointsInFrustum
@@ -810,7 +810,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
     {
         GF_PROF(ctx, s, "k_fe_branch");
-        k_fe_branch<<<B, 64, 0, s>>>(D);
+        GF_LAUNCH(k_fe_branch, B, 64, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     const bool mclk = D.gf && D.match_ticks >= 0, sclk = D.gf && D.select_ticks >= 0;
@@ -832,7 +832,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     }
     {
         GF_PROF(ctx, s, "k_fe_decide");
-        k_fe_decide<<<B, 256, 0, s>>>(D);
+        GF_LAUNCH(k_fe_decide, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     if (D.gf) {
@@ -861,7 +861,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                  col(GF_ST_ITER2), col(GF_ST_EDGES2), s));
     {
         GF_PROF(ctx, s, "k_fe_post");
-        k_fe_post<<<B, 256, 0, s>>>(D);
+        GF_LAUNCH(k_fe_post, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     if (D.gf) {
@@ -890,7 +890,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         }
         {
             GF_PROF(ctx, s, "k_fe_viz_exclude");
-            k_fe_viz_exclude<<<B, 256, 0, s>>>(D);
+            GF_LAUNCH(k_fe_viz_exclude, B, 256, 0, s, D);
             GF_HIP(hipGetLastError());
         }
         FE_RC(gf::match_project_list_budget(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, M, D.left,
@@ -902,16 +902,16 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.refmap) {
         {
             GF_PROF(ctx, s, "k_fe_scatter_rows");
-            k_fe_scatter_rows<<<dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s>>>(D, fe->gm, WM);
+            GF_LAUNCH(k_fe_scatter_rows, dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM);
             GF_HIP(hipGetLastError());
         }
         GF_PROF(ctx, s, "k_fe_scatter");
-        k_fe_scatter<<<B, 256, 0, s>>>(D);
+        GF_LAUNCH(k_fe_scatter, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_fe_end");
-        k_fe_end<<<B, 256, 0, s>>>(D);
+        GF_LAUNCH(k_fe_end, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     if (fe->ts) {  // join: the context's stream sees the whole step
@@ -1321,12 +1321,12 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
     GF_HIP(hipMemcpyAsync(D.V, V, sizeof(float) * 16 * B, hipMemcpyHostToDevice, s));
     GF_HIP(hipMemcpyAsync(D.t_cur, t.data(), sizeof(double) * B, hipMemcpyHostToDevice, s));
     if (!host) {
-        k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(D);
+        GF_LAUNCH(k_fe_boot_begin, (B + 63) / 64, 64, 0, s, D);
         GF_HIP(hipGetLastError());
     } else {  // the step counter still advances: a sourced step after a host bootstrap continues the loop
         FeDev Dh = D;
         Dh.src_mode = 0;
-        k_fe_boot_begin<<<(B + 63) / 64, 64, 0, s>>>(Dh);
+        GF_LAUNCH(k_fe_boot_begin, (B + 63) / 64, 64, 0, s, Dh);
         GF_HIP(hipGetLastError());
     }
     GF_HIP(hipMemsetAsync(D.kp2mp, 0xff, sizeof(int32_t) * B * cap, s));
@@ -1340,7 +1340,7 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
     FE_RC(gf_frustum_dev(ctx, &fe->fi, B, D.Tcw, fe->gm.map, fe->g_nmp, M, 0.5f, fe->gm.views, fe->nview, s));
     FE_RC(gf_match_project_dev(ctx, &fe->fi, B, D.kps, D.desc, D.nkp, cap, fe->gm.views, fe->gm.desc, fe->g_nmp, M,
                                1.f, 0.8f, D.kp2mp, D.score, fe->scratch, s));
-    k_fe_boot_end<<<B, 256, 0, s>>>(D);
+    GF_LAUNCH(k_fe_boot_end, B, 256, 0, s, D);
     GF_HIP(hipGetLastError());
     GF_HIP(hipStreamSynchronize(s));
     return GF_OK;

@@ -1691,7 +1691,7 @@ int gf_obs_build_info_dev(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, co
     if (nframes <= 0 || cap <= 0) return GF_OK;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_info");
-    k_obs_info<<<dim3((cap + 127) / 128, nframes), 128, 0, s>>>(*cam, d_Xv, d_pos, d_sigma2, d_n, cap, check_viz, d_H,
+    GF_LAUNCH(k_obs_info, dim3((cap + 127) / 128, nframes), 128, 0, s, *cam, d_Xv, d_pos, d_sigma2, d_n, cap, check_viz, d_H,
                                                                  d_info, d_uv, d_valid);
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -1703,7 +1703,7 @@ int gf_obs_accumulate_dev(gf_ctx* ctx, int nframes, const double* d_info, const 
     if (nframes <= 0) return GF_OK;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_accumulate");
-    k_obs_accumulate<<<nframes, 64, 0, s>>>(d_info, d_flag, d_n, cap, diag, d_out);
+    GF_LAUNCH(k_obs_accumulate, nframes, 64, 0, s, d_info, d_flag, d_n, cap, diag, d_out);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -1794,7 +1794,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     }
     {
         GF_PROF(ctx, s, "k_onepoint_pre");
-        k_onepoint_pre<<<nframes, PRE_THREADS, pre_lds, s>>>(A, (OnePre*)pre);
+        GF_LAUNCH(k_onepoint_pre, nframes, PRE_THREADS, pre_lds, s, A, (OnePre*)pre);
         GF_HIP(hipGetLastError());
     }
     const int full_pc = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
@@ -1820,7 +1820,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     }
     {
         GF_PROF(ctx, s, "k_active_match");
-        k_active_match<<<nframes, AW, active_lds_bytes(A.pool_cap, kp_cap), s>>>(A);
+        GF_LAUNCH(k_active_match, nframes, AW, active_lds_bytes(A.pool_cap, kp_cap), s, A);
         GF_HIP(hipGetLastError());
     }
     if (A.pass == 1) {
@@ -1828,7 +1828,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
         A.pass = 2;
         GF_PROF(ctx, s, "k_active_match_overflow");
         // few workgroups: the full pool's LDS is only claimed where a frame needs it
-        k_active_match_overflow<<<std::min(nframes, AM_OVF_GRID), AW, active_lds_bytes(full_pc, kp_cap), s>>>(A);
+        GF_LAUNCH(k_active_match_overflow, std::min(nframes, AM_OVF_GRID), AW, active_lds_bytes(full_pc, kp_cap), s, A);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
@@ -1850,7 +1850,7 @@ int gf_maxvol_select_dev(gf_ctx* ctx, int npools, const double* d_info, const do
     if (rc) return rc;
     A.err = (int32_t*)err;
     GF_PROF(ctx, s, "k_maxvol");
-    k_maxvol<<<npools, GF_THREADS, 0, s>>>(A);
+    GF_LAUNCH(k_maxvol, npools, GF_THREADS, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -1892,7 +1892,7 @@ int gf_logdet(gf_ctx* ctx, const double* M, int n, double* out) {
         return rc;
     {
         GF_PROF(ctx, ctx->stream, "k_logdet");
-        k_logdet<<<(n + 127) / 128, 128, 0, ctx->stream>>>((const double*)dM, n, (double*)dO);
+        GF_LAUNCH(k_logdet, (n + 127) / 128, 128, 0, ctx->stream, (const double*)dM, n, (double*)dO);
     }
     GF_HIP(hipGetLastError());
     GF_HIP(hipMemcpyAsync(out, dO, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
@@ -2089,7 +2089,7 @@ extern "C" int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_pre
     GF_CHECK(d_t_prev && d_Tcw_prev && d_t_cur && d_Tcw_cur && d_Xv, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_update");
-    k_obs_update<<<(nframes + 63) / 64, 64, 0, s>>>(nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv,
+    GF_LAUNCH(k_obs_update, (nframes + 63) / 64, 64, 0, s, nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv,
                                                     d_Xv_next);
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -2242,7 +2242,7 @@ int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const
     for (int i = 0; i < nlevels; i++) t.v[i] = level_sigma2[i];
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_frame_info");
-    k_obs_frame_info<<<dim3((kp_stride + 127) / 128, nframes), 128, 0, s>>>(
+    GF_LAUNCH(k_obs_frame_info, dim3((kp_stride + 127) / 128, nframes), 128, 0, s, 
         *cam, d_Xv, d_kps, d_nkps, kp_stride, d_kp2mp, d_outlier, d_map_pos, d_nmp, map_stride, t, nlevels, d_H,
         d_info, d_uv, d_remap);
     GF_HIP(hipGetLastError());
@@ -2259,7 +2259,7 @@ int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const d
     GF_CHECK(!ck.t0 || (ck.rec && d_cap2 && map_stride <= 4096), GF_ERR_ARG, "bad clock");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_map_info");
-    k_obs_map_info<<<dim3((map_stride + 127) / 128, nframes), 128, 0, s>>>(
+    GF_LAUNCH(k_obs_map_info, dim3((map_stride + 127) / 128, nframes), 128, 0, s, 
         *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated,
         d_remap, ck, d_cap2);
     GF_HIP(hipGetLastError());
@@ -2275,7 +2275,7 @@ int gf::obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp,
     GF_CHECK(d_kp2mp && d_nkps && d_info && d_upd_id && d_nmp && d_out, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_accumulate");
-    k_obs_accumulate_matched<<<nframes, 64, 0, s>>>(d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
+    GF_LAUNCH(k_obs_accumulate_matched, nframes, 64, 0, s, d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
                                                     frame_id, diag, d_out, d_remap);
     GF_HIP(hipGetLastError());
     return GF_OK;

@@ -1070,27 +1070,27 @@ static int init_launch(gf_ctx* ctx, int nprob, const float K[9], float sigma, in
     hipStream_t s = (hipStream_t)stream;
     {
         GF_PROF(ctx, s, "k_init_prepare");
-        k_init_prepare<<<dim3(3, nprob), IN_BIG, 0, s>>>(Bt);
+        GF_LAUNCH(k_init_prepare, dim3(3, nprob), IN_BIG, 0, s, Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_hyp");
-        k_init_hyp<<<dim3(2 * iterations, nprob), IN_T, 0, s>>>(Bt);
+        GF_LAUNCH(k_init_hyp, dim3(2 * iterations, nprob), IN_T, 0, s, Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_decide");
-        k_init_decide<<<dim3(1, nprob), IN_BIG, 0, s>>>(Bt);
+        GF_LAUNCH(k_init_decide, dim3(1, nprob), IN_BIG, 0, s, Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_checkrt");
-        k_init_checkrt<<<dim3(8, nprob), IN_T, 0, s>>>(Bt);
+        GF_LAUNCH(k_init_checkrt, dim3(8, nprob), IN_T, 0, s, Bt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_init_finish");
-        k_init_finish<<<dim3(1, nprob), IN_BIG, 0, s>>>(Bt);
+        GF_LAUNCH(k_init_finish, dim3(1, nprob), IN_BIG, 0, s, Bt);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;

@@ -230,12 +230,12 @@ int gf_distinctive_descriptors_dev(gf_ctx* ctx, int nmp, const uint8_t* d_desc, 
     GF_HIP(hipMemsetAsync(d_best, 0xff, 4 * (size_t)nmp, s));
     if (total > 0) {
         GF_PROF(ctx, s, "k_distinctive_rows");
-        k_distinctive_rows<<<(total + 255) / 256, 256, 0, s>>>(d_desc, d_offsets, nmp, total, (uint32_t*)d_best);
+        GF_LAUNCH(k_distinctive_rows, (total + 255) / 256, 256, 0, s, d_desc, d_offsets, nmp, total, (uint32_t*)d_best);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_distinctive_pick");
-        k_distinctive_pick<<<(2 * nmp + 255) / 256, 256, 0, s>>>(d_desc, d_offsets, nmp, d_best, d_out_desc);
+        GF_LAUNCH(k_distinctive_pick, (2 * nmp + 255) / 256, 256, 0, s, d_desc, d_offsets, nmp, d_best, d_out_desc);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
@@ -306,7 +306,7 @@ int gf_fuse_dev(gf_ctx* ctx, const gf_frame_info* fi, int nprob, const gf_fuse_p
     if (rc) return rc;
     GF_HIP(hipMemcpyAsync(dp, P.data(), sizeof(FuseProb) * nprob, hipMemcpyHostToDevice, s));
     GF_PROF(ctx, s, "k_fuse");
-    k_fuse<<<nprob, MATCH_THREADS, fuse_lds_bytes(nmax), s>>>(gf::make_frame_const(fi), (const FuseProb*)dp);
+    GF_LAUNCH(k_fuse, nprob, MATCH_THREADS, fuse_lds_bytes(nmax), s, gf::make_frame_const(fi), (const FuseProb*)dp);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -913,14 +913,14 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A0, const FrameConst& fc, 
     if (A.mode == MODE_LAST) {  // few queries, wide windows: wave-sequential in the reference order
         {
             GF_PROF(ctx, s, "k_match_seq_pre");
-            k_match_seq_pre<<<nframes, SEQ_PRE_THREADS, seq_pre_lds_bytes(A.kp_cap), s>>>(A, fc, (SeqPre*)A.pre);
+            GF_LAUNCH(k_match_seq_pre, nframes, SEQ_PRE_THREADS, seq_pre_lds_bytes(A.kp_cap), s, A, fc, (SeqPre*)A.pre);
             GF_HIP(hipGetLastError());
         }
         GF_PROF(ctx, s, "k_match_lastframe");
-        k_match_seq<<<nframes, SEQ_THREADS, seq_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
+        GF_LAUNCH(k_match_seq, nframes, SEQ_THREADS, seq_lds_bytes(A.kp_cap, A.q_cap), s, A, fc);
     } else {  // many queries, narrow windows: claim-resolution rounds
         GF_PROF(ctx, s, "k_match_project");
-        k_match<<<nframes, MATCH_THREADS, match_lds_bytes(A.kp_cap, A.q_cap), s>>>(A, fc);
+        GF_LAUNCH(k_match, nframes, MATCH_THREADS, match_lds_bytes(A.kp_cap, A.q_cap), s, A, fc);
     }
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -939,7 +939,7 @@ int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const floa
     FrameConst fc = gf::make_frame_const(fi);
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, "k_frustum");
-    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
+    GF_LAUNCH(k_frustum, dim3((mp_cap + 255) / 256, nframes), 256, 0, s, fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
                                                                    d_views, d_nview, nullptr, nullptr,
                                                                    FrustumClock{});
     GF_HIP(hipGetLastError());
@@ -958,7 +958,7 @@ int gf_frustum_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const
     FrameConst fc = gf::make_frame_const(fi);
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, "k_frustum_list");
-    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, nullptr, mp_cap, view_cos_limit,
+    GF_LAUNCH(k_frustum, dim3((mp_cap + 255) / 256, nframes), 256, 0, s, fc, d_Tcw, d_mps, nullptr, mp_cap, view_cos_limit,
                                                                    d_views, d_nview, d_list, d_nlist,
                                                                    FrustumClock{});
     GF_HIP(hipGetLastError());
@@ -1178,7 +1178,7 @@ int gf_descriptor_distance(gf_ctx* ctx, const uint8_t* a, const uint8_t* b, int 
     if ((rc = gf::ws_upload(ctx, 0, a, 32 * (size_t)n, &dA)) || (rc = gf::ws_upload(ctx, 1, b, 32 * (size_t)n, &dB)) ||
         (rc = gf::ws_get(ctx, 2, 4 * (size_t)n, &dO)))
         return rc;
-    k_hamming<<<(n + 255) / 256, 256, 0, ctx->stream>>>((const uint8_t*)dA, (const uint8_t*)dB, n, (int32_t*)dO);
+    GF_LAUNCH(k_hamming, (n + 255) / 256, 256, 0, ctx->stream, (const uint8_t*)dA, (const uint8_t*)dB, n, (int32_t*)dO);
     GF_HIP(hipGetLastError());
     GF_HIP(hipMemcpyAsync(dist, dO, 4 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
     GF_HIP(hipStreamSynchronize(ctx->stream));
@@ -1201,7 +1201,7 @@ int gf::frustum_clocked(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, d_list ? "k_frustum_list" : "k_frustum");
     const FrustumClock fk{ck.t0, ck.rec, ck.stride, ck.off, d_alt};
-    k_frustum<<<dim3((mp_cap + 255) / 256, nframes), 256, 0, s>>>(fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
+    GF_LAUNCH(k_frustum, dim3((mp_cap + 255) / 256, nframes), 256, 0, s, fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
                                                                    d_views, d_nview, d_list, d_nlist,
                                                                    ck.t0 ? fk : FrustumClock{});
     GF_HIP(hipGetLastError());

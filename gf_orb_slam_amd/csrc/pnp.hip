@@ -819,18 +819,18 @@ int gf_pnp_iterate_dev(gf_ctx* ctx, int nprob, const float* d_p3d, const float* 
     const Cam cam{(double)K[0], (double)K[1], (double)K[2], (double)K[3]};
     {
         GF_PROF(ctx, s, "k_pnp_draw");
-        k_pnp_draw<<<(nprob + 63) / 64, 64, 0, s>>>(nprob, d_state, d_rng, n_iterations, lcap, (int32_t*)draws, cap);
+        GF_LAUNCH(k_pnp_draw, (nprob + 63) / 64, 64, 0, s, nprob, d_state, d_rng, n_iterations, lcap, (int32_t*)draws, cap);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_pnp_hyp");
-        k_pnp_hyp<<<dim3((lcap + 63) / 64, nprob), 64, 0, s>>>(d_p3d, d_p2d, d_sigma2, cap, cam, d_state, n_iterations,
+        GF_LAUNCH(k_pnp_hyp, dim3((lcap + 63) / 64, nprob), 64, 0, s, d_p3d, d_p2d, d_sigma2, cap, cam, d_state, n_iterations,
                                                                lcap, (const int32_t*)draws, (double*)rt, (int32_t*)cnt);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(ctx, s, "k_pnp_scan");
-        k_pnp_scan<<<nprob, 256, 0, s>>>(d_p3d, d_p2d, d_sigma2, cap, cam, d_state, d_best_mask, n_iterations, lcap,
+        GF_LAUNCH(k_pnp_scan, nprob, 256, 0, s, d_p3d, d_p2d, d_sigma2, cap, cam, d_state, d_best_mask, n_iterations, lcap,
                                          (const double*)rt, (const int32_t*)cnt, (double*)work, d_rng, d_Tcw, d_inliers,
                                          d_ninliers, d_flags);
         GF_HIP(hipGetLastError());

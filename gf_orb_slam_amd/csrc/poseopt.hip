@@ -542,7 +542,7 @@ int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
 #define PO_WPS 1
 #endif
     (void)ctx;
-    k_pose_opt<PO_WPS><<<nprob, PO_T, 0, s>>>(A);
+    GF_LAUNCH(k_pose_opt<PO_WPS>, nprob, PO_T, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -612,7 +612,7 @@ int gf_pose_opt_frames_dev(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keyp
     G.nedges = (int32_t*)ne;
     {
         GF_PROF(ctx, s, "k_pose_gather");
-        k_pose_gather<<<nframes, 64, 0, s>>>(G);
+        GF_LAUNCH(k_pose_gather, nframes, 64, 0, s, G);
         GF_HIP(hipGetLastError());
     }
     PoseArgs A{};

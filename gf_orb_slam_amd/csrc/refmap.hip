@@ -244,7 +244,7 @@ int gf_update_reference_dev(gf_ctx* ctx, const gf_covis_map* d_map, int nframes,
     A.first_stride = m.nmp;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_update_reference");
-    k_update_reference<<<nframes, RM_T, 0, s>>>(A);
+    GF_LAUNCH(k_update_reference, nframes, RM_T, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -276,7 +276,7 @@ int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap
     A.ref_kf = d_ref_kf;
     A.first = d_first;
     GF_PROF(ctx, s, "k_update_reference");
-    k_update_reference<<<nframes, RM_T, 0, s>>>(A);
+    GF_LAUNCH(k_update_reference, nframes, RM_T, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -43,6 +43,8 @@ static hipEvent_t pool_event(gf_ctx* ctx) {
     return e;
 }
 
+static thread_local ProfScope* tl_scope = nullptr;
+
 ProfScope::ProfScope(gf_ctx* c, hipStream_t st, const char* name) : ctx(c), s(st) {
     if (!ctx || !ctx->prof) return;
     for (size_t i = 0; i < ctx->prof_entries.size(); i++)
@@ -51,21 +53,39 @@ ProfScope::ProfScope(gf_ctx* c, hipStream_t st, const char* name) : ctx(c), s(st
         ctx->prof_entries.push_back(ProfEntry{name, {}, {}});
         idx = (int)ctx->prof_entries.size() - 1;
     }
-    hipEvent_t e = pool_event(ctx);
-    if (!e) {
-        idx = -1;
-        return;
-    }
-    (void)hipEventRecord(e, s);
-    ctx->prof_entries[idx].start.push_back(e);
+    prev = tl_scope;
+    tl_scope = this;
 }
 
 ProfScope::~ProfScope() {
     if (idx < 0) return;
-    hipEvent_t e = pool_event(ctx);
-    if (!e) return;
-    (void)hipEventRecord(e, s);
-    ctx->prof_entries[idx].stop.push_back(e);
+    tl_scope = prev;
+    if (first && last) {
+        ctx->prof_entries[idx].start.push_back(first);
+        ctx->prof_entries[idx].stop.push_back(last);
+    }
+}
+
+bool prof_launch_events(hipEvent_t* start, hipEvent_t* stop) {
+    ProfScope* sc = tl_scope;
+    if (!sc || sc->idx < 0) return false;
+    hipEvent_t e = pool_event(sc->ctx);
+    if (!e) return false;
+    if (!sc->first) {
+        hipEvent_t e0 = pool_event(sc->ctx);
+        if (!e0) {
+            sc->ctx->event_pool.push_back(e);
+            return false;
+        }
+        sc->first = e0;
+        *start = e0;
+    } else {
+        *start = nullptr;
+        sc->ctx->prof_spent.push_back(sc->last);  // only the scope's last stop is read; pooled at reset
+    }
+    sc->last = e;
+    *stop = e;
+    return true;
 }
 
 int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out) {
@@ -123,6 +143,7 @@ int gf_ctx_destroy(gf_ctx* ctx) {
         for (auto ev : e.stop) (void)hipEventDestroy(ev);
     }
     for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
+    for (auto ev : ctx->prof_spent) (void)hipEventDestroy(ev);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return GF_OK;
@@ -148,6 +169,8 @@ int gf_prof_reset(gf_ctx* ctx) {
         for (auto ev : e.start) ctx->event_pool.push_back(ev);
         for (auto ev : e.stop) ctx->event_pool.push_back(ev);
     }
+    for (auto ev : ctx->prof_spent) ctx->event_pool.push_back(ev);
+    ctx->prof_spent.clear();
     ctx->prof_entries.clear();
     return GF_OK;
 }

@@ -120,7 +120,7 @@ int gf_motion_predict_dev(gf_ctx* ctx, int nframes, const float* d_velocity, con
     GF_CHECK(d_velocity && d_Tcw_last && d_Tcw, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_motion_predict");
-    k_motion_predict<<<(nframes + 63) / 64, 64, 0, s>>>(nframes, d_velocity, d_Tcw_last, d_Tcw);
+    GF_LAUNCH(k_motion_predict, (nframes + 63) / 64, 64, 0, s, nframes, d_velocity, d_Tcw_last, d_Tcw);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -132,7 +132,7 @@ int gf_discard_outliers_dev(gf_ctx* ctx, int nframes, int32_t* d_kp2mp, uint8_t*
     GF_CHECK(d_kp2mp && d_outlier && d_nkps && kp_stride > 0, GF_ERR_ARG, "bad arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_discard_outliers");
-    k_discard_outliers<<<nframes, 64, 0, s>>>(d_kp2mp, d_outlier, d_nkps, kp_stride, budget, d_nmatches,
+    GF_LAUNCH(k_discard_outliers, nframes, 64, 0, s, d_kp2mp, d_outlier, d_nkps, kp_stride, budget, d_nmatches,
                                               d_num_to_match);
     GF_HIP(hipGetLastError());
     return GF_OK;
@@ -161,7 +161,7 @@ int gf_matched_gather_dev(gf_ctx* ctx, int nframes, const gf_keypoint* d_kps, co
     G.n = d_n;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_matched_gather");
-    k_matched_gather<<<nframes, 64, 0, s>>>(G);
+    GF_LAUNCH(k_matched_gather, nframes, 64, 0, s, G);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -174,7 +174,7 @@ int gf_views_exclude_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2m
     GF_CHECK(d_kp2mp && d_nkps && d_views && d_nmp, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_views_exclude");
-    k_views_exclude<<<nframes, 64, 0, s>>>(d_kp2mp, d_nkps, kp_stride, d_views, mp_stride, d_nmp);
+    GF_LAUNCH(k_views_exclude, nframes, 64, 0, s, d_kp2mp, d_nkps, kp_stride, d_views, mp_stride, d_nmp);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -37,7 +37,7 @@ int gf_undistort_keypoints_dev(gf_ctx* ctx, int nframes, const float K[4], const
     if (nframes <= 0 || cap <= 0) return GF_OK;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_undistort");
-    k_undistort<<<dim3((cap + 255) / 256, nframes), 256, 0, s>>>(make_coef(K, dist), dist[0] == 0.f ? 1 : 0, d_in,
+    GF_LAUNCH(k_undistort, dim3((cap + 255) / 256, nframes), 256, 0, s, make_coef(K, dist), dist[0] == 0.f ? 1 : 0, d_in,
                                                                  d_n, cap, d_out);
     GF_HIP(hipGetLastError());
     return GF_OK;
