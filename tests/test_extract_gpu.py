@@ -86,11 +86,11 @@ def test_fast_threshold_edges(fast_th):
     assert np.array_equal(dg, do)
 
 
-@pytest.mark.parametrize("nf", [200, 1000])
+@pytest.mark.parametrize("nf", [500, 1000])
 def test_long_cell_lists(nf):
     """Dense corners: uniform noise whose contrast ramps across the image,
     so a cell's corner list after NMS spans from none to thousands (cells of
-    tens of thousands of pixels at 200 features). Lists longer than the
+    twenty thousand pixels at 500 features). Lists longer than the
     selection's per-wave LDS buffers (k_select: SEL_BUF = SEL_BUF_CELL = 1024
     entries; with -DSEL_BUF_CELL=256 lists of 257..1024 wait for wave 0's
     buffer) take the sequential replay in global memory; the cut must match
