@@ -494,11 +494,19 @@ def main():
                     help="also time the step with the reference's time budgets on (gf_set_budgets)")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="also time one group with the frames handed over from host memory")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (0: the environment's; HIP's default is 4, so with more "
+                         "streams than queues two streams share one and a kernel can wait behind the other's)")
+    ap.add_argument("--no-prof-timed", action="store_true",
+                    help="time the headline steps without the per-kernel HIP events; the kernel table then comes "
+                         "from a profiled pass of the same steps right after")
     ap.add_argument("--config3-steps", type=int, default=10,
                     help="also time BASELINE config 3 (TUM 640x480, 2000 feats, GF 160; 0: skip)")
     ap.add_argument("--config3-batch", type=int, default=1024)
     args = ap.parse_args()
 
+    if args.hw_queues > 0:  # before anything initialises the HIP runtime
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # launch one process per GPU before anything touches the GPU
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
@@ -594,7 +602,7 @@ def main():
     for fe in fes:
         fe.sync()
         fe.write("hist", np.zeros((fe.B, 8), np.int32))  # running counters of the timed region
-        fe.prof_enable(True)  # HIP events around every launch on its group's stream
+        fe.prof_enable(not args.no_prof_timed)  # per-launch HIP events (dispatch timestamps, GF_LAUNCH)
         fe.prof_reset()
     torch.cuda.synchronize()
     if world > 1:
@@ -614,6 +622,17 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
+    stats = [fe.stats() for fe in fes]
+    final = {k: np.concatenate([s[k] for s in stats]) for k in STATS}
+    thist = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)  # [B][8] over the timed steps
+    if args.no_prof_timed:  # the kernel table from a profiled pass of the same steps
+        for fe in fes:
+            fe.prof_enable(True)
+        for _ in range(args.steps):
+            for fe in fes:
+                fe.step()
+        for fe in fes:
+            fe.sync()
     prof = {}
     for fe in fes:
         for k, (ms, cnt) in fe.prof_report().items():
@@ -621,9 +640,6 @@ def main():
             a[0] += ms
             a[1] += cnt
         fe.prof_enable(False)
-    stats = [fe.stats() for fe in fes]
-    final = {k: np.concatenate([s[k] for s in stats]) for k in STATS}
-    thist = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)  # [B][8] over the timed steps
     mix = thist[:, :6].sum(0)
     ldets_total = float(thist[:, 6].sum())
     local_total = float(thist[:, 7].sum())
