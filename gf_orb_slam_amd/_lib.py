@@ -147,6 +147,14 @@ _PROTOS = {
     "gf_frontend_set_map": [_P, _I, _P, _P, _I],
     "gf_frontend_set_rng": [_P, _I, ctypes.c_uint32],
     "gf_frontend_set_covis": [_P, _I, _P],
+    "gf_kfdb_create": [_P, _P, _P],
+    "gf_kfdb_destroy": [_P],
+    "gf_frontend_set_kfdb": [_P, _I, _P],
+    "gf_frontend_set_vocab": [_P, _P],
+    "gf_window_search": [_P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _F, _I, _P, _P],
+    "gf_search_frames": [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _F, _P, _P, _P],
+    "gf_search_kf_projection": [_P, _P, _P, _P, _I, _P, _P, _P, _I, _P, _P, _I, _P, _F, _I, _I, _P, _P, _P],
+    "gf_reloc_candidates": [_P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_uint32, _P, _P, _P],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
     "gf_update_reference": [_P, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P],

@@ -64,8 +64,9 @@ __device__ __forceinline__ int ham_regs(const uint32_t* f, const uint8_t* nd) {
 __global__ __launch_bounds__(256) void k_bow_descend(VocabDev V, const uint8_t* __restrict__ desc,
                                                      const int32_t* __restrict__ nfeat, int cap, int levelsup,
                                                      int32_t* __restrict__ wid, double* __restrict__ wval,
-                                                     int32_t* __restrict__ nid) {
+                                                     int32_t* __restrict__ nid, const int32_t* __restrict__ gate) {
     const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    if (gate && !gate[f]) return;
     if (i >= min(nfeat[f], cap)) return;
     const size_t g = (size_t)f * cap + i;
     uint32_t x[8];
@@ -140,12 +141,13 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __
                                                    const int32_t* __restrict__ nid, int32_t* __restrict__ words,
                                                    double* __restrict__ values, int32_t* __restrict__ nwords,
                                                    int32_t* __restrict__ fv_nodes, int32_t* __restrict__ fv_start,
-                                                   int32_t* __restrict__ fv_feats, int32_t* __restrict__ nfv) {
+                                                   int32_t* __restrict__ fv_feats, int32_t* __restrict__ nfv,
+                                                   const int32_t* __restrict__ gate) {
     __shared__ unsigned long long kw[BOW_MAX], kn[BOW_MAX];
     __shared__ double vals[BOW_MAX];
     __shared__ int tmp[4], s_m;
     const int f = blockIdx.x, tid = threadIdx.x;
-    const int n = min(nfeat[f], cap);
+    const int n = gate && !gate[f] ? 0 : min(nfeat[f], cap);
     const size_t g0 = (size_t)f * cap;
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
@@ -269,10 +271,7 @@ __device__ void rotation_filter(int nm, const uint8_t* rbin, const int* rec, int
     __syncthreads();
 }
 
-struct BowPair {
-    gf_bow_side a, b;
-    int32_t* out;
-};
+using BowPair = gf::BowPairDev;
 
 // (d1, position of d1, d2) of a stream, reduced across the wave: the winner
 // has the smaller d1 (ties: earlier position); second = min(winner d2, loser d1)
@@ -583,6 +582,11 @@ VocabDev vdev(const gf_vocab* v) {
 
 }  // namespace
 
+static int bow_transform_impl(gf_vocab* v, int nframes, const uint8_t* d_desc, const int32_t* d_n,
+                              const int32_t* d_gate, int cap, int levelsup, int32_t* d_words, double* d_values,
+                              int32_t* d_nwords, int32_t* d_fv_nodes, int32_t* d_fv_start, int32_t* d_fv_feats,
+                              int32_t* d_nfv, void* tmp, void* stream);
+
 extern "C" {
 
 int gf_vocab_destroy(gf_vocab* v) {
@@ -668,31 +672,66 @@ int gf_bow_transform_dev(gf_vocab* v, int nframes, const uint8_t* d_desc, const 
                          int32_t* d_fv_start, int32_t* d_fv_feats, int32_t* d_nfv, void* stream) {
     GF_CHECK(v, GF_ERR_ARG, "null vocab");
     if (nframes <= 0) return GF_OK;
+    void* tmp;
+    int rc = gf::ws_get(v->ctx, 48, (size_t)nframes * std::max(cap, 1) * 16, &tmp);
+    if (rc) return rc;
+    return bow_transform_impl(v, nframes, d_desc, d_n, nullptr, cap, levelsup, d_words, d_values, d_nwords, d_fv_nodes,
+                              d_fv_start, d_fv_feats, d_nfv, tmp, stream);
+}
+
+}  // extern "C"
+
+// Scratch of nframes x cap x 16 bytes: the caller's (a front end's own
+// buffer: the context's slot 48 is also the batched PnP's work buffer).
+static int bow_transform_impl(gf_vocab* v, int nframes, const uint8_t* d_desc, const int32_t* d_n,
+                              const int32_t* d_gate, int cap, int levelsup, int32_t* d_words, double* d_values,
+                              int32_t* d_nwords, int32_t* d_fv_nodes, int32_t* d_fv_start, int32_t* d_fv_feats,
+                              int32_t* d_nfv, void* tmp, void* stream) {
     GF_CHECK(d_desc && d_n && d_words && d_values && d_nwords && d_fv_nodes && d_fv_start && d_fv_feats && d_nfv,
              GF_ERR_ARG, "null arg");
     GF_CHECK(cap > 0 && cap <= BOW_MAX, GF_ERR_UNSUPPORTED, "cap must be in 1..4096");
     GF_CHECK(v->nnodes > 1, GF_ERR_ARG, "empty vocabulary");
     hipStream_t s = (hipStream_t)stream;
-    void* tmp;
-    int rc = gf::ws_get(v->ctx, 48, (size_t)nframes * cap * 16, &tmp);
-    if (rc) return rc;
     int32_t* wid = (int32_t*)tmp;
     int32_t* nid = wid + (size_t)nframes * cap;
     double* wv = (double*)(nid + (size_t)nframes * cap);
     const VocabDev V = vdev(v);
     {
         GF_PROF(v->ctx, s, "k_bow_descend");
-        GF_LAUNCH(k_bow_descend, dim3((cap + 255) / 256, nframes), 256, 0, s, V, d_desc, d_n, cap, levelsup, wid, wv, nid);
+        GF_LAUNCH(k_bow_descend, dim3((cap + 255) / 256, nframes), 256, 0, s, V, d_desc, d_n, cap, levelsup, wid, wv, nid,
+                  d_gate);
         GF_HIP(hipGetLastError());
     }
     {
         GF_PROF(v->ctx, s, "k_bow_build");
         GF_LAUNCH(k_bow_build, nframes, 256, 0, s, V, d_n, cap, wid, wv, nid, d_words, d_values, d_nwords, d_fv_nodes,
-                                            d_fv_start, d_fv_feats, d_nfv);
+                  d_fv_start, d_fv_feats, d_nfv, d_gate);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
 }
+
+int gf::bow_transform_gated(gf_vocab* voc, int nframes, const uint8_t* d_desc, const int32_t* d_n,
+                            const int32_t* d_gate, int cap, int levelsup, int32_t* d_words, double* d_values,
+                            int32_t* d_nwords, int32_t* d_fv_nodes, int32_t* d_fv_start, int32_t* d_fv_feats,
+                            int32_t* d_nfv, void* tmp, void* stream) {
+    GF_CHECK(voc, GF_ERR_ARG, "null vocab");
+    if (nframes <= 0) return GF_OK;
+    return bow_transform_impl(voc, nframes, d_desc, d_n, d_gate, cap, levelsup, d_words, d_values, d_nwords,
+                              d_fv_nodes, d_fv_start, d_fv_feats, d_nfv, tmp, stream);
+}
+
+int gf::match_bow_pairs(gf_ctx* ctx, int mode, float nnratio, int check_ori, int npairs, const gf::BowPairDev* d_pairs,
+                        int32_t* d_nmatches, void* stream) {
+    if (npairs <= 0) return GF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    GF_PROF(ctx, s, "k_match_bow");
+    GF_LAUNCH(k_match_bow, npairs, 256, 0, s, d_pairs, mode, nnratio, check_ori, d_nmatches);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
+extern "C" {
 
 int gf_bow_transform(gf_vocab* v, const uint8_t* desc, int n, int levelsup, int32_t* words, double* values,
                      int* nwords, int32_t* fv_nodes, int32_t* fv_start, int32_t* fv_feats, int* nfv) {

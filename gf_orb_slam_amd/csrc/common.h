@@ -136,7 +136,37 @@ int match_project_list_budget(gf_ctx* ctx, const gf_frame_info* fi, int nframes,
                               int32_t* d_err, void* stream);
 int obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps, int kp_stride,
                            const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp, int map_stride,
-                           int frame_id, double diag, double* d_out, const int32_t* d_remap, void* stream);
+                           int frame_id, double diag, double* d_out, const int32_t* d_remap, void* stream,
+                           const int32_t* d_gate = nullptr);
+// gf_obs_update_dev for the frames with d_gate[f] != 0 (null: all)
+int obs_update_gated(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev, const double* d_t_cur,
+                     const float* d_Tcw_cur, double* d_Xv, double* d_Xv_next, const int32_t* d_gate, void* stream);
+// gf_pose_opt_frames_dev; a frame with d_gate[f] < gate_min is not optimised
+// at all (its pose, flags and counts untouched)
+int pose_opt_frames_gated(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_keypoint* d_kps, const int32_t* d_nkps,
+                          int kp_stride, const int32_t* d_kp2mp, const gf_map_point* d_map, int map_stride,
+                          const float* inv_sigma2, int nlevels, float fx, float fy, float cx, float cy,
+                          uint8_t* d_outlier, int32_t* d_ninliers, int32_t* d_iterations, int32_t* d_nedges,
+                          const int32_t* d_gate, int gate_min, void* stream);
+// gf_match_project_dev with a window factor per frame (d_th[f], the th of
+// SearchByProjection(F, vpMapPoints, th))
+int match_project_th(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                     const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                     const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, const float* d_th, float nnratio,
+                     int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream);
+// gf_bow_transform_dev over the frames with d_gate[f] != 0 (others: empty vectors)
+int bow_transform_gated(gf_vocab* voc, int nframes, const uint8_t* d_desc, const int32_t* d_n, const int32_t* d_gate,
+                        int cap, int levelsup, int32_t* d_words, double* d_values, int32_t* d_nwords,
+                        int32_t* d_fv_nodes, int32_t* d_fv_start, int32_t* d_fv_feats, int32_t* d_nfv, void* d_tmp,
+                        void* stream);  // d_tmp: nframes x cap x 16 bytes
+// One ORBmatcher::SearchByBoW pair whose description already lives in device
+// memory (gf_match_bow_dev copies host-built pairs).
+struct BowPairDev {
+    gf_bow_side a, b;
+    int32_t* out;
+};
+int match_bow_pairs(gf_ctx* ctx, int mode, float nnratio, int check_ori, int npairs, const BowPairDev* d_pairs,
+                    int32_t* d_nmatches, void* stream);
 int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
                      const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
                      const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info, const double* d_H,

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.h"
+#include "reloc.h"
 #include "undist.h"
 
 namespace {
@@ -104,6 +105,19 @@ struct FeDev {
     gf_mp_view* vtmp;      // [B][M] clocked isInFrustum results (kept before the cut)
     int32_t* ncut;         // [B] points the isInFrustum cap moved to mLeftMapPoints
     int32_t* nlist0;       // [B] mLeftMapPoints size before SearchAdditionalMatchesInFrame
+    // the tracking state machine (GF_FE_TRACK) and the per-stream gates of its stages
+    int32_t* track;        // [B][GF_TR_N]
+    int32_t* m3_nlast;     // [B] last-frame points SearchByProjection(Cur, Last) projects (0 off the motion model)
+    int32_t* rl_gate;      // [B] 1: Relocalisation this step
+    int32_t* nkp_tl;       // [B] keypoints TrackLocalMap sees (0: it does not run)
+    int32_t* nkp_fi;       // [B] keypoints of its FRAME_INFO_MATRIX pass
+    int32_t* gate_tl;      // [B] TrackLocalMap runs
+    int32_t* gate_fi;      // [B] its updatePWLSVec + FRAME_INFO_MATRIX run (not within 2 frames of a relocalisation)
+    int32_t* gate_post;    // [B] the frame ends WORKING: motion model, prediction, post-publish block
+    int32_t* nmp_post;     // [B] RunMapPointsSelection's points (0 when the frame is lost)
+    int32_t* nmp_step;     // [B] without keyframe graphs: the map's size when TrackLocalMap runs, else 0
+    float* th_m2;          // [B] SearchByProjection(F, local, th): 5 within 2 frames of a relocalisation (:3318-3320)
+    int max_frames;        // mMaxFrames
 };
 
 __device__ __forceinline__ long long* ck_rec(const FeDev& D, int b) { return D.clk + (long long)b * D.ck_stride; }
@@ -135,9 +149,26 @@ __global__ __launch_bounds__(256) void k_fe_begin(FeDev D) {
             const int idx = (int)(((long long)D.phase[b] + k) % D.period);
             D.ptrs[b] = D.bases[b] + (long long)idx * D.frame_stride;
         }
-        D.t_cur[b] = D.t_prev[b] + D.dt;
+        D.t_cur[b] = D.t_cur[b] + D.dt;  // mCurrentFrame.mTimeStamp (mLastFrame's may be older after a loss)
+        // the initial estimate's path (Tracking.cc:602-628): LOST -> Relocalisation;
+        // a velocity and >= 2 frames since a relocalisation -> TrackWithMotionModel
+        // (mTcw = mVelocity * mLastFrame.mTcw, :1519); else TrackPreviousFrame
+        // (mTcw = mLastFrame.mTcw, :1353); a fresh Frame's mTcw is empty (zeros)
+        int32_t* T = D.track + (size_t)b * GF_TR_N;
+        T[GF_TR_QUERY] += 1;  // mnId
+        const int since = min(T[GF_TR_SINCE] + 1, 1 << 30);
+        T[GF_TR_SINCE] = since;
+        const int path = T[GF_TR_STATE] == 1 ? 3 : (T[GF_TR_VEL] && since >= 2) ? 0 : 2;
+        T[GF_TR_PATH] = path;
+        T[GF_TR_OK] = 0;
+        D.m3_nlast[b] = path == 0 ? D.last_nkp[b] : 0;
+        D.rl_gate[b] = path == 3;
         float o[16];
-        mat44(D.V + 16 * b, D.Tcw_last + 16 * b, o);
+        if (path == 0) {
+            mat44(D.V + 16 * b, D.Tcw_last + 16 * b, o);
+        } else {
+            for (int i = 0; i < 16; i++) o[i] = path == 2 ? D.Tcw_last[16 * b + i] : 0.f;
+        }
         for (int i = 0; i < 16; i++) D.Tcw[16 * b + i] = o[i];
         for (int s = 0; s < GF_FE_NSTAT; s++)
             if (s != GF_ST_FRAMES) stat(D, s)[b] = 0;
@@ -179,7 +210,14 @@ __device__ int compact_in_view(const FeDev& D, int b, int32_t* out) {
 __global__ __launch_bounds__(64) void k_fe_branch(FeDev D) {
     const int b = blockIdx.x, lane = threadIdx.x;
     const int ntm = stat(D, GF_ST_TO_MATCH)[b];
-    if (D.gf && ntm <= 0) {
+    if (!D.gate_tl[b]) {  // no TrackLocalMap: the initial estimate failed
+        if (lane == 0) {
+            stat(D, GF_ST_BRANCH)[b] = 5;
+            D.nlist[b] = 0;
+            D.nlist_viz[b] = 0;
+            D.m_frustum[b] = 0;
+        }
+    } else if (D.gf && ntm <= 0) {
         // mbTrackInView as left by earlier frames (matched points already false)
         const int n = compact_in_view(D, b, D.left1);
         if (lane == 0) {
@@ -281,7 +319,7 @@ __global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
     int nb;
     if (n == 0) {
         nb = 4;
-    } else if (!D.gf || n < 400) {  // Tracking.cc:3322
+    } else if (!D.gf || n < 400 || D.th_m2[b] != 1.f) {  // Tracking.cc:3318-3323
         nb = 2;
         D.m_m2[b] = cut;
     } else {
@@ -316,6 +354,25 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
     }
     if (t != 0) return;
     if (br == 2) stat(D, GF_ST_LOCAL)[b] = D.nm2[b];
+    // TrackLocalMap's verdict (Tracking.cc:2819-2824), mState (:713-716)
+    int32_t* T = D.track + (size_t)b * GF_TR_N;
+    bool ok = false;
+    if (D.gate_tl[b]) {
+        const int inl = stat(D, GF_ST_INL2)[b];
+        ok = !(T[GF_TR_SINCE] < D.max_frames && inl < 25) && inl >= 15;
+        if (!ok) stat(D, GF_ST_FLAGS)[b] |= 16384;
+    }
+    T[GF_TR_STATE] = ok ? 0 : 1;
+    T[GF_TR_VEL] = ok ? 1 : 0;  // mVelocity = cv::Mat() when lost
+    D.gate_post[b] = ok;
+    D.nmp_post[b] = ok ? D.nmp[b] : 0;
+    stat(D, GF_ST_NLEFT)[b] = n;
+    if (!ok) {  // no post-publish block: the leftovers stay unsearched
+        D.nlist[b] = 0;
+        D.nlist0[b] = 0;
+        D.nlist_viz[b] = 0;
+        return;
+    }
     // motion model (Tracking.cc:729-738): LastTwc from mLastFrame.mTcw, mVelocity = mTcw * LastTwc
     const float* L = D.Tcw_last + 16 * b;
     float Twc[16] = {0};
@@ -333,7 +390,6 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
     for (int i = 0; i < 16; i++) D.V[16 * b + i] = Vn[i];
     D.nlist[b] = n;
     D.nlist0[b] = n;
-    stat(D, GF_ST_NLEFT)[b] = n;
     const bool viz = (br == 1 || ncut > 0);  // mbNeedVizCheck
     D.nlist_viz[b] = viz ? n : 0;
     if (D.select_ticks >= 0) {
@@ -401,7 +457,8 @@ __global__ __launch_bounds__(256) void k_fe_viz_exclude(FeDev D) {
 
 __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
     const int b = blockIdx.x, t = threadIdx.x;
-    const int n = D.nkp[b];
+    const bool working = D.gate_post[b];  // mState == WORKING (Tracking.cc:854)
+    const int n = working ? D.nkp[b] : 0;
     const long long o = (long long)b * D.cap;
     for (int i = t; i < n; i += 256) {
         int mp = D.kp2mp[o + i];
@@ -427,9 +484,11 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
     const int m = D.gnmp[b];
     for (int i = t; i < m; i += 256) D.gupd[(long long)b * D.M + i] -= 1;
     if (t == 0) {
-        D.last_nkp[b] = n;
-        for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
-        D.t_prev[b] = D.t_cur[b];
+        if (working) {  // mLastFrame = Frame(mCurrentFrame) (:910)
+            D.last_nkp[b] = n;
+            for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
+            D.t_prev[b] = D.t_cur[b];
+        }
         int fl = stat(D, GF_ST_FLAGS)[b];
         if (D.match_ticks >= 0 || D.select_ticks >= 0) {  // the caps that fired, from the clock record
             const long long* r = ck_rec(D, b);
@@ -444,9 +503,9 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
                 if (r[GF_CK_BUDGET_CUT] >= 0) fl |= 8 | 1024;
             }
         }
-        if (stat(D, GF_ST_M3)[b] < 20) fl |= 1;
-        if (stat(D, GF_ST_FOUND)[b] < 10) fl |= 2;
-        if (stat(D, GF_ST_INL2)[b] < 15) fl |= 4;
+        const int32_t* T = D.track + (size_t)b * GF_TR_N;
+        if (T[GF_TR_PATH] == 1) fl |= stat(D, GF_ST_M3)[b] < 20 ? 1 : 2;  // TrackWithMotionModel failed
+        if (D.gate_tl[b] && stat(D, GF_ST_INL2)[b] < 15) fl |= 4;
         stat(D, GF_ST_FLAGS)[b] = fl;
         stat(D, GF_ST_FRAMES)[b] += 1;
         int32_t* h = D.hist + 8LL * b;
@@ -486,6 +545,12 @@ __global__ __launch_bounds__(256) void k_fe_boot_end(FeDev D) {
         D.last_nkp[b] = n;
         for (int i = 0; i < 16; i++) D.Tcw_last[16 * b + i] = D.Tcw[16 * b + i];
         D.t_prev[b] = D.t_cur[b];
+        int32_t* T = D.track + (size_t)b * GF_TR_N;  // WORKING, a velocity, no relocalisation so far
+        T[GF_TR_STATE] = 0;
+        T[GF_TR_VEL] = 1;
+        T[GF_TR_SINCE] = 1 << 30;
+        T[GF_TR_PATH] = 0;
+        T[GF_TR_OK] = 1;
         if (b == 0) *D.step += 1;
     }
 }
@@ -586,7 +651,7 @@ __global__ __launch_bounds__(256) void k_fe_gather(FeDev D, int32_t* lnmp) {
     }
     __syncthreads();
     const long long ko = (long long)b * D.cap;
-    const int nk = D.nkp[b];
+    const int nk = D.nkp_tl[b];
     for (int i = t; i < nk; i += 256) {
         const int mp = D.kp2mp[ko + i];
         if (mp < 0) continue;
@@ -604,7 +669,7 @@ __global__ __launch_bounds__(256) void k_fe_scatter(FeDev D) {
     const int32_t* lm = D.lmp + o;
     for (int k = t; k < n; k += 256) D.g2l[o + lm[k]] = -1;
     const long long ko = (long long)b * D.cap;
-    const int nk = D.nkp[b];
+    const int nk = D.nkp_tl[b];
     for (int i = t; i < nk; i += 256) {
         const int l = D.kp2mp[ko + i];
         if (l >= 0) D.kp2mp[ko + i] = lm[l];
@@ -687,6 +752,17 @@ struct gf_frontend {
     bool fork_post = false;
     hipStream_t fork_s = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // track-loss paths (reloc.hip): their arguments; relocalisation needs a
+    // vocabulary and a keyframe database on some stream (rl_on)
+    gf::TrackLossArgs TL{};
+    gf_vocab* voc = nullptr;
+    bool rl_alloc = false, rl_on = false;
+    std::vector<gf::KfdbDev> h_kfdb;
+    gf::KfdbDev* d_kfdb = nullptr;
+    std::vector<int32_t> h_kfc;
+    int32_t* d_kfc = nullptr;
+    std::vector<std::vector<int32_t>> h_slots;  // per stream: the graph's slots per keyframe
+    void* bow_tmp = nullptr;
 };
 
 namespace {
@@ -768,19 +844,33 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         GF_HIP(hipStreamWaitEvent(fe->ts, fe->ev_extracted, 0));
         s = fe->ts;
     }
-    // TrackWithMotionModel
+    // TrackWithMotionModel (the streams on the motion model; the others project
+    // no last-frame point), PoseOptimization when >= 20 matches (:1559)
     {
         gf::CandidateCount cc(col(GF_ST_CAND_LAST));
         FE_RC(gf_match_lastframe_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.Tcw, D.last_kps, D.last_desc,
-                                     D.last_kp2mp, D.last_outl, D.last_pos, D.last_nkp, cap, 15.f, 1, D.kp2mp,
+                                     D.last_kp2mp, D.last_outl, D.last_pos, D.m3_nlast, cap, 15.f, 1, D.kp2mp,
                                      D.score, col(GF_ST_M3), fe->scratch, s));
     }
     gf::CandidateCount cc(col(GF_ST_CAND_PROJ));  // the projection searches below
-    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
-                                 fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
-                                 col(GF_ST_ITER1), col(GF_ST_EDGES1), s));
+    FE_RC(gf::pose_opt_frames_gated(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
+                                    fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
+                                    col(GF_ST_ITER1), col(GF_ST_EDGES1), col(GF_ST_M3), 20, s));
     FE_RC(gf_discard_outliers_dev(ctx, B, D.kp2mp, D.outl, D.nkp, cap, D.budget, col(GF_ST_FOUND),
                                   col(GF_ST_TO_MATCH), s));
+    // Relocalisation of the LOST streams: ComputeBoW, the keyframe database's
+    // candidates, SearchByBoW per candidate (Tracking.cc:3861-3922)
+    if (fe->rl_on) {
+        const gf::TrackLossArgs& TL = fe->TL;
+        FE_RC(gf::bow_transform_gated(fe->voc, B, D.desc, D.nkp, D.rl_gate, cap, 4, (int32_t*)TL.words,
+                                      (double*)TL.values, (int32_t*)TL.nwords, (int32_t*)TL.fv_nodes,
+                                      (int32_t*)TL.fv_start, (int32_t*)TL.fv_feats, (int32_t*)TL.nfv, fe->bow_tmp, s));
+        FE_RC(gf::reloc_candidates(ctx, TL, s));
+        FE_RC(gf::match_bow_pairs(ctx, 0, 0.75f, 1, B * TL.ncs, TL.pairs, TL.bow_nm, s));
+    }
+    // the motion model's failure test, TrackPreviousFrame, the relocalisation
+    // loop, and the gates of the TrackLocalMap stages below
+    FE_RC(gf::track_loss(ctx, fe->TL, s));
     const MapArrays WM{D.map, fe->wdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
     // keyframe graphs: H / ObsMat / u_proj stay in map order (the local map's
     // point q is map point lmp[q]); the other per-point arrays are gathered
@@ -788,7 +878,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.refmap) {
         // TrackLocalMap -> UpdateReference (Tracking.cc:2745, 3689-3852): local
         // keyframes and mvpLocalMapPoints from this frame's matches
-        FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp, cap, fe->lkf, fe->nlkf,
+        FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp_tl, cap, fe->lkf, fe->nlkf,
                                           gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
         {
             GF_PROF(ctx, s, "k_fe_gather_rows");
@@ -801,13 +891,13 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     }
     // TrackLocalMap -> SearchReferencePointsInFrustum
     if (D.gf) {
-        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, s));
-        FE_RC(gf::obs_frame_info(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp, cap, D.kp2mp, D.outl, fe->mp_pos, D.nmp,
-                                 M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, rmp, s));
-        FE_RC(gf::obs_accumulate_matched(ctx, B, D.kp2mp, D.nkp, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
-                                         fe->base, rmp, s));
+        FE_RC(gf::obs_update_gated(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, D.gate_fi, s));
+        FE_RC(gf::obs_frame_info(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp_fi, cap, D.kp2mp, D.outl, fe->mp_pos,
+                                 D.nmp, M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, rmp, s));
+        FE_RC(gf::obs_accumulate_matched(ctx, B, D.kp2mp, D.nkp_tl, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
+                                         fe->base, rmp, s, D.gate_tl));
     }
-    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp_tl, cap, D.views, D.nmp, M, s));
     {
         GF_PROF(ctx, s, "k_fe_branch");
         GF_LAUNCH(k_fe_branch, B, 64, 0, s, D);
@@ -828,7 +918,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                   fe->nview, clock(D.t_viz0, GF_CK_OFF_VIZ(M, R)), D.vtmp, s));
     } else {
         FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
-        FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp, cap, D.views, D.nmp, M, s));
+        FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp_tl, cap, D.views, D.nmp, M, s));
     }
     {
         GF_PROF(ctx, s, "k_fe_decide");
@@ -854,11 +944,11 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                    col(GF_ST_TO_MATCH), 1.f, 0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score,
                                    D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s, ac));
     }
-    FE_RC(gf_match_project_dev(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, 1.f, 0.8f,
+    FE_RC(gf::match_project_th(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, D.th_m2, 0.8f,
                                D.kp2mp, D.score, D.nm2, s));
-    FE_RC(gf_pose_opt_frames_dev(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
-                                 fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL2),
-                                 col(GF_ST_ITER2), col(GF_ST_EDGES2), s));
+    FE_RC(gf::pose_opt_frames_gated(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
+                                    fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL2),
+                                    col(GF_ST_ITER2), col(GF_ST_EDGES2), D.gate_tl, 1, s));
     {
         GF_PROF(ctx, s, "k_fe_post");
         GF_LAUNCH(k_fe_post, B, 256, 0, s, D);
@@ -875,8 +965,9 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
             GF_HIP(hipStreamWaitEvent(fe->fork_s, fe->ev_fork, 0));
             sp = fe->fork_s;
         }
-        FE_RC(gf_obs_update_dev(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, sp));
-        FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp, M, 1, nullptr, D.upd, 2,
+        FE_RC(gf::obs_update_gated(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, fe->Xv_next, D.gate_post,
+                                   sp));
+        FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp_post, M, 1, nullptr, D.upd, 2,
                                fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, sp,
                                sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel));
         if (fe->fork_post) GF_HIP(hipEventRecord(fe->ev_join, sp));
@@ -1058,11 +1149,36 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     F(-1, int32_t, (size_t)B * M, fe->qres);
     F(-1, int32_t, (size_t)B * M, fe->qold);
     F(-1, int32_t, B, fe->merr);
+    // the tracking state machine, its gates and the track-loss scratch
+    F(GF_FE_TRACK, int32_t, (size_t)B * GF_TR_N, D.track);
+    gf_reloc_kf* rkf = nullptr;
+    F(GF_FE_RELOC, gf_reloc_kf, (size_t)B * gf::RL_NC, rkf);
+    F(-1, int32_t, B, D.m3_nlast);
+    F(-1, int32_t, B, D.rl_gate);
+    F(-1, int32_t, B, D.nkp_tl);
+    F(-1, int32_t, B, D.nkp_fi);
+    F(-1, int32_t, B, D.gate_tl);
+    F(-1, int32_t, B, D.gate_fi);
+    F(-1, int32_t, B, D.gate_post);
+    F(-1, int32_t, B, D.nmp_post);
+    F(-1, int32_t, B, D.nmp_step);
+    F(-1, float, B, D.th_m2);
+    F(-1, int32_t, B, fe->d_kfc);
+    gf::TrackLossArgs& TL = fe->TL;
+    F(-1, int32_t, (size_t)B * gf::grid_ints(cap), TL.grid);
+    F(-1, int32_t, (size_t)B * cap, TL.rec);
+    F(-1, gf_pose_edge, (size_t)B * cap, TL.edges);
+    F(-1, int32_t, (size_t)B * cap, TL.edge_kp);
+    F(-1, uint8_t, (size_t)B * cap, TL.eoutl);
+    F(-1, double, (size_t)3 * B * cap, TL.pwork);
+    F(-1, int32_t, (size_t)4 * B, TL.pint);
+    D.max_frames = p->max_frames > 0 ? p->max_frames : (int)(18.0 / (30.0 * p->dt) + 1e-6);  // 18 * fps / 30
     // the stream maps; the working arrays alias them until a keyframe graph is set
     fe->gm = MapArrays{map, mdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
     fe->g_nmp = nmp;
     fe->wdesc = mdesc;
     fe->w_nmp = nmp;
+    D.nmp = D.nmp_step;  // TrackLocalMap sees no map on a stream whose initial estimate failed
     D.gmap = map;
     D.gnmp = nmp;
     D.gupd = D.upd;
@@ -1093,6 +1209,49 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     if (hipMemcpy(D.Tcw_last, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(D.V, I.data(), I.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(gf::fail(GF_ERR_HIP, "upload poses"));
+    fe->h_kfc.assign(B, -1);  // no keyframe graph: the map is assumed to hold > 5 keyframes
+    if (hipMemcpy(fe->d_kfc, fe->h_kfc.data(), 4 * (size_t)B, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(gf::fail(GF_ERR_HIP, "upload keyframe counts"));
+    fe->h_kfdb.assign(B, gf::KfdbDev{});
+    TL.B = B;
+    TL.cap = cap;
+    TL.M = M;
+    TL.budget = p->gf_budget;
+    TL.nlevels = p->nlevels;
+    TL.fc = gf::make_frame_const(&fe->fi);
+    for (int l = 0; l < 16; l++) {
+        TL.inv_sigma2[l] = fe->inv_sigma2[l];
+        TL.level_sigma2[l] = fe->level_sigma2[l];
+    }
+    TL.kps = D.kps;
+    TL.desc = D.desc;
+    TL.nkp = D.nkp;
+    TL.kp2mp = D.kp2mp;
+    TL.score = D.score;
+    TL.outl = D.outl;
+    TL.Tcw = D.Tcw;
+    TL.last_kps = D.last_kps;
+    TL.last_desc = D.last_desc;
+    TL.last_nkp = D.last_nkp;
+    TL.last_kp2mp = D.last_kp2mp;
+    TL.last_pos = D.last_pos;
+    TL.Tcw_last = D.Tcw_last;
+    TL.gmap = map;
+    TL.gdesc = mdesc;
+    TL.track = D.track;
+    TL.stats = D.stats;
+    TL.rng = rng;
+    TL.kf_count = fe->d_kfc;
+    TL.gnmp = nmp;
+    TL.nkp_tl = D.nkp_tl;
+    TL.nkp_fi = D.nkp_fi;
+    TL.gate_tl = D.gate_tl;
+    TL.gate_fi = D.gate_fi;
+    TL.th_m2 = D.th_m2;
+    TL.nmp_step = D.nmp_step;
+    TL.rkf = rkf;
+    TL.rl_gate = D.rl_gate;
+    TL.ncs = 1;
     ctx->frontends++;
     *out = fe;
     return GF_OK;
@@ -1206,6 +1365,8 @@ static int fe_enable_covis(gf_frontend* fe) {
     fe->wdesc = wdesc;
     D.refmap = 1;
     fe->covis_set = 1;
+    fe->TL.covis = fe->d_covis;
+    fe->h_slots.assign(B, {});
     return GF_OK;
 }
 
@@ -1267,6 +1428,93 @@ int gf_frontend_set_covis(gf_frontend* fe, int stream, const gf_covis_map* g) {
     GF_HIP(up(d.mp_obs, g->mp_obs, 4 * no));
     GF_HIP(hipMemcpy(fe->d_covis + b, &d, sizeof(d), hipMemcpyHostToDevice));
     fe->has_covis[b] = 1;
+    // KeyFramesInMap() for TrackPreviousFrame's octave floor; a keyframe
+    // database set earlier indexed the old graph
+    fe->h_kfc[b] = nkf;
+    GF_HIP(hipMemcpy(fe->d_kfc + b, &fe->h_kfc[b], 4, hipMemcpyHostToDevice));
+    fe->h_slots[b].resize(nkf);
+    for (int k = 0; k < nkf; k++) fe->h_slots[b][k] = g->kf_mp_off[k + 1] - g->kf_mp_off[k];
+    if (fe->rl_alloc && fe->h_kfdb[b].nkf) FE_RC(gf_frontend_set_kfdb(fe, stream, nullptr));
+    return GF_OK;
+}
+
+static int fe_enable_reloc(gf_frontend* fe) {
+    FeDev& D = fe->D;
+    gf::TrackLossArgs& TL = fe->TL;
+    const size_t B = D.B, cap = D.cap, NC = gf::RL_NC;
+    int rc;
+    void* p;
+#define A_(bytes, dst)                                 \
+    if ((rc = fe_alloc(fe, (bytes), &p))) return rc; \
+    dst = (decltype(dst))p;
+    A_(sizeof(gf::KfdbDev) * B, fe->d_kfdb);
+    A_(4 * B * cap, TL.words);
+    A_(8 * B * cap, TL.values);
+    A_(4 * B, TL.nwords);
+    A_(4 * B * cap, TL.fv_nodes);
+    A_(4 * B * (cap + 1), TL.fv_start);
+    A_(4 * B * cap, TL.fv_feats);
+    A_(4 * B, TL.nfv);
+    A_(16 * B * cap, fe->bow_tmp);
+    A_(sizeof(gf::BowPairDev) * B * NC, TL.pairs);
+    A_(4 * B * NC * cap, TL.bow_out);
+    A_(4 * B * NC, TL.bow_nm);
+    A_(4 * B * NC, TL.cands);
+    A_(4 * B, TL.ncand);
+    A_(sizeof(gf_pnp_state) * B * NC, TL.pst);
+    A_(B * NC * cap, TL.pbest);
+    A_(12 * B * cap, TL.p3d);
+    A_(8 * B * cap, TL.p2d);
+    A_(4 * B * cap, TL.psig);
+    A_(4 * B * cap, TL.pidx);
+    A_(B * cap, TL.pinl);
+    A_(4 * B * gf::RL_LCAP * 8, TL.pdraws);
+    A_(8 * B * gf::RL_LCAP * 12, TL.prt);
+    A_(4 * B * gf::RL_LCAP, TL.pcnt);
+    A_(8 * B * cap * gf::RL_WORK, TL.pwk);
+    A_(4 * B * 16, TL.ptcw);
+    A_(4 * B * 2, TL.pflags);
+#undef A_
+    TL.kfdb = fe->d_kfdb;
+    fe->rl_alloc = true;
+    return GF_OK;
+}
+
+int gf_frontend_set_kfdb(gf_frontend* fe, int stream, gf_kfdb* db) {
+    GF_CHECK(fe && stream >= 0 && stream < fe->D.B, GF_ERR_ARG, "bad stream");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set keyframe databases before capturing a graph");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    gf::KfdbDev v{};
+    if (db) {
+        v = gf::kfdb_dev(db);
+        GF_CHECK(fe->covis_set && fe->has_covis[stream], GF_ERR_ARG,
+                 "a keyframe database needs the stream's keyframe graph (gf_frontend_set_covis)");
+        GF_CHECK(v.nkf == fe->h_kfc[stream], GF_ERR_ARG, "the database and the keyframe graph differ in keyframes");
+        std::vector<int32_t> off(v.nkf + 1);
+        GF_HIP(hipMemcpy(off.data(), v.kp_off, 4 * off.size(), hipMemcpyDeviceToHost));
+        for (int k = 0; k < v.nkf; k++)
+            GF_CHECK(off[k + 1] - off[k] == fe->h_slots[stream][k], GF_ERR_ARG,
+                     "keyframe " + std::to_string(k) + ": keypoints and graph slots differ");
+    }
+    if (!fe->rl_alloc) FE_RC(fe_enable_reloc(fe));
+    fe->h_kfdb[stream] = v;
+    GF_HIP(hipMemcpy(fe->d_kfdb + stream, &v, sizeof(v), hipMemcpyHostToDevice));
+    GF_HIP(hipMemset(fe->TL.rkf + (size_t)stream * gf::RL_NC, 0, sizeof(gf_reloc_kf) * gf::RL_NC));
+    int ncs = 1;
+    for (const gf::KfdbDev& k : fe->h_kfdb) ncs = std::max(ncs, k.nkf);
+    fe->TL.ncs = ncs;
+    fe->rl_on = fe->voc && ncs > 0 && std::any_of(fe->h_kfdb.begin(), fe->h_kfdb.end(),
+                                                  [](const gf::KfdbDev& k) { return k.nkf > 0; });
+    return GF_OK;
+}
+
+int gf_frontend_set_vocab(gf_frontend* fe, gf_vocab* voc) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set the vocabulary before capturing a graph");
+    fe->voc = voc;
+    fe->rl_on = fe->voc && std::any_of(fe->h_kfdb.begin(), fe->h_kfdb.end(),
+                                       [](const gf::KfdbDev& k) { return k.nkf > 0; });
     return GF_OK;
 }
 

@@ -2068,9 +2068,11 @@ int gf_select_map_points(gf_ctx* ctx, const gf_obs_camera* cam, const double* Xv
 namespace {
 __global__ void k_obs_update(int nframes, const double* __restrict__ t_prev, const float* __restrict__ Tcw_prev,
                              const double* __restrict__ t_cur, const float* __restrict__ Tcw_cur,
-                             double* __restrict__ Xv, double* __restrict__ Xv_next) {
+                             double* __restrict__ Xv, double* __restrict__ Xv_next,
+                             const int32_t* __restrict__ gate) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= nframes) return;
+    if (gate && !gate[f]) return;
     float Twc[16];
     gfkine::get_Twc(Tcw_cur + 16 * f, Twc);
     gfkine::obs_update(t_prev[f], Tcw_prev + 16 * f, t_cur[f], Twc, Xv + 13 * f);
@@ -2088,9 +2090,16 @@ extern "C" int gf_obs_update_dev(gf_ctx* ctx, int nframes, const double* d_t_pre
     if (nframes <= 0) return GF_OK;
     GF_CHECK(d_t_prev && d_Tcw_prev && d_t_cur && d_Tcw_cur && d_Xv, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
+    return gf::obs_update_gated(ctx, nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv, d_Xv_next, nullptr, s);
+}
+
+int gf::obs_update_gated(gf_ctx* ctx, int nframes, const double* d_t_prev, const float* d_Tcw_prev,
+                         const double* d_t_cur, const float* d_Tcw_cur, double* d_Xv, double* d_Xv_next,
+                         const int32_t* d_gate, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_update");
     GF_LAUNCH(k_obs_update, (nframes + 63) / 64, 64, 0, s, nframes, d_t_prev, d_Tcw_prev, d_t_cur, d_Tcw_cur, d_Xv,
-                                                    d_Xv_next);
+              d_Xv_next, d_gate);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -2192,9 +2201,11 @@ __global__ __launch_bounds__(64) void k_obs_accumulate_matched(const int32_t* __
                                                                const int32_t* __restrict__ upd_id,
                                                                const int32_t* __restrict__ nmp, int map_stride,
                                                                int frame_id, double diag, double* __restrict__ out,
-                                                               const int32_t* __restrict__ remap) {
+                                                               const int32_t* __restrict__ remap,
+                                                               const int32_t* __restrict__ gate) {
     __shared__ int list[KP_MAX];
     const int f = blockIdx.x, lane = threadIdx.x;
+    if (gate && !gate[f]) return;
     const int n = min(nkps[f], KP_MAX), m = nmp[f];
     // the contributing map points in keypoint order (ballot compaction)
     int cnt = 0;
@@ -2269,14 +2280,14 @@ int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const d
 int gf::obs_accumulate_matched(gf_ctx* ctx, int nframes, const int32_t* d_kp2mp, const int32_t* d_nkps,
                                int kp_stride, const double* d_info, const int32_t* d_upd_id, const int32_t* d_nmp,
                                int map_stride, int frame_id, double diag, double* d_out, const int32_t* d_remap,
-                               void* stream) {
+                               void* stream, const int32_t* d_gate) {
     GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
     if (nframes <= 0) return GF_OK;
     GF_CHECK(d_kp2mp && d_nkps && d_info && d_upd_id && d_nmp && d_out, GF_ERR_ARG, "null arg");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_obs_accumulate");
     GF_LAUNCH(k_obs_accumulate_matched, nframes, 64, 0, s, d_kp2mp, d_nkps, kp_stride, d_info, d_upd_id, d_nmp, map_stride,
-                                                    frame_id, diag, d_out, d_remap);
+              frame_id, diag, d_out, d_remap, d_gate);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -51,6 +51,7 @@ struct MatchArgs {
     const float* last_pos;
     const float* Tcw;  // [F][16]
     float th, nnratio;
+    const float* th_per;  // MODE_PROJECT: th per frame (null: th)
     int check_ori;
     // in/out
     int32_t* kp2mp;
@@ -97,7 +98,8 @@ __device__ Query make_query(const MatchArgs& A, const FrameConst& fc, int f, int
         if (!v.in_view) return q;
         const int pl = min(max(v.level, 0), fc.nlevels - 1);
         float r = v.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
-        if (A.th != 1.0) r *= A.th;
+        const float th = A.th_per ? A.th_per[f] : A.th;
+        if (th != 1.0) r *= th;
         q.r = r * fc.scales[pl];
         q.x = v.u;
         q.y = v.v;
@@ -926,6 +928,11 @@ static int launch_match(gf_ctx* ctx, const MatchArgs& A0, const FrameConst& fc, 
     return GF_OK;
 }
 
+static int project_impl(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                        const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                        const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, float th, const float* d_th,
+                        float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream);
+
 extern "C" {
 
 int gf_frustum_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const float* d_Tcw, const gf_map_point* d_mps,
@@ -969,6 +976,24 @@ int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
                          const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
                          const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, float th, float nnratio,
                          int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream) {
+    return project_impl(ctx, fi, nframes, d_kps, d_desc, d_n, kp_cap, d_views, d_mp_desc, d_m, mp_cap, th, nullptr,
+                        nnratio, d_kp2mp, d_score, d_nmatches, stream);
+}
+
+}  // extern "C"
+
+int gf::match_project_th(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                         const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                         const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, const float* d_th, float nnratio,
+                         int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream) {
+    return project_impl(ctx, fi, nframes, d_kps, d_desc, d_n, kp_cap, d_views, d_mp_desc, d_m, mp_cap, 1.f, d_th,
+                        nnratio, d_kp2mp, d_score, d_nmatches, stream);
+}
+
+static int project_impl(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
+                        const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
+                        const uint8_t* d_mp_desc, const int32_t* d_m, int mp_cap, float th, const float* d_th,
+                        float nnratio, int32_t* d_kp2mp, int32_t* d_score, int32_t* d_nmatches, void* stream) {
     GF_CHECK(ctx, GF_ERR_ARG, "null ctx");
     int rc = check_fi(fi);
     if (rc) return rc;
@@ -985,6 +1010,7 @@ int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.m = d_m;
     A.q_cap = mp_cap;
     A.th = th;
+    A.th_per = d_th;
     A.nnratio = nnratio;
     A.kp2mp = d_kp2mp;
     A.score = d_score;
@@ -995,6 +1021,8 @@ int gf_match_project_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.err = (int32_t*)err;
     return launch_match(ctx, A, gf::make_frame_const(fi), nframes, (hipStream_t)stream);
 }
+
+extern "C" {
 
 int gf_match_project_list_dev(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
                               const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,

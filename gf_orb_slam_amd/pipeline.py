@@ -28,6 +28,8 @@ from .matcher import MAP_POINT_DTYPE, MP_VIEW_DTYPE
 from .observability import Rng
 from .orb import KEYPOINT_DTYPE, Context
 
+RELOC_KF_DTYPE = np.dtype([("query", "<u4"), ("words", "<i4"), ("score", "<f4")])  # gf_reloc_kf
+
 # gf_frontend field ids (abi.h GF_FE_*): name -> (id, dtype, per-stream shape
 # with "cap" = keypoint capacity and "M" = map capacity)
 FIELDS = {
@@ -65,9 +67,16 @@ FIELDS = {
     "hist": (31, np.int32, (8,)),  # running counters: steps per branch [0..4], steps cut by a time cap [5],
                                    # log-dets [6], local matches [7]
     "clock": (32, np.int64, ("CK",)),  # budget clock record of the last step (abi.h GF_CK_*)
+    "track": (33, np.int32, (8,)),  # tracking state (abi.h GF_TR_*)
+    "reloc": (34, RELOC_KF_DTYPE, (64,)),  # keyframes' relocalisation-query state (gf_reloc_kf)
 }
 STATS = ["m3", "found", "to_match", "branch", "in_view", "local", "inl1", "inl2", "extra", "nleft", "iter1",
-         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal", "ncut", "cand_last", "cand_proj"]
+         "iter2", "edges1", "edges2", "flags", "frames", "ldets", "nlocal", "ncut", "cand_last", "cand_proj",
+         "tpf", "ncand", "reloc", "ransac"]
+# GF_FE_TRACK columns and path codes
+TR = {"state": 0, "vel": 1, "since": 2, "path": 3, "query": 4, "ok": 5}
+PATHS = {0: "motion model", 1: "previous frame after the motion model", 2: "previous frame", 3: "relocalisation"}
+
 NSTAT = len(STATS)
 
 # GF_FE_CLOCK layout (abi.h GF_CK_*): header words, then per-stage elapsed-time
@@ -93,7 +102,7 @@ class FrontendParams(ctypes.Structure):
                 ("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int32),
                 ("fast_th", ctypes.c_int32), ("batch", ctypes.c_int32), ("map_cap", ctypes.c_int32),
                 ("gf_budget", ctypes.c_int32), ("gf", ctypes.c_int32), ("dt", ctypes.c_double),
-                ("dist", ctypes.c_float * 5)]
+                ("dist", ctypes.c_float * 5), ("max_frames", ctypes.c_int32)]
 
     @classmethod
     def make(cls, camera: str, nfeatures: int, batch: int, map_cap: int, gf_budget: int, gf: bool = True,
@@ -101,8 +110,9 @@ class FrontendParams(ctypes.Structure):
         """dist: Camera.k1 k2 p1 p2 [k3] (None / k1 = 0: keypoints used as extracted)."""
         w, h, fx, fy, cx, cy = synth.CAMERAS[camera]
         d = list(dist or ()) + [0.0] * (5 - len(dist or ()))
+        # mMaxFrames = 18 * camera_fps / 30 (Tracking.cc:153; int of a double)
         return cls(w, h, fx, fy, cx, cy, nfeatures, scale_factor, nlevels, fast_th, batch, map_cap, gf_budget,
-                   1 if gf else 0, 1.0 / fps, (ctypes.c_float * 5)(*d))
+                   1 if gf else 0, 1.0 / fps, (ctypes.c_float * 5)(*d), int(18 * fps / 30))
 
 
 def field_shape(name: str, B: int, cap: int, M: int, R: int = 1):
@@ -205,6 +215,19 @@ class FrontEnd:
     def set_rng(self, stream: int, seed: int) -> None:
         check(lib().gf_frontend_set_rng(self.handle, stream, ctypes.c_uint32(seed)))
 
+    def set_vocab(self, vocab) -> None:
+        """gf_frontend_set_vocab: Frame::ComputeBoW's vocabulary for
+        relocalisation (a bow.ORBVocabulary, kept alive here)."""
+        self._vocab = vocab
+        check(lib().gf_frontend_set_vocab(self.handle, vocab.handle if vocab is not None else None))
+
+    def set_kfdb(self, stream: int, db) -> None:
+        """gf_frontend_set_kfdb: the stream's keyframe database (a
+        KeyframeDB over the same keyframes as its graph; None detaches)."""
+        self._kfdbs = getattr(self, "_kfdbs", {})
+        self._kfdbs[stream] = db
+        check(lib().gf_frontend_set_kfdb(self.handle, stream, db.device(self.ctx) if db is not None else None))
+
     def bootstrap(self, Tcw: np.ndarray, V: np.ndarray, t0: float = 0.0) -> None:
         T = np.ascontiguousarray(Tcw, np.float32).reshape(self.B, 16)
         Vv = np.ascontiguousarray(V, np.float32).reshape(self.B, 16)
@@ -297,3 +320,69 @@ def make_workload_frontend(camera: str, nfeatures: int, batch: int, map_size: in
     T, V = workload.boot_state()
     fe.bootstrap(T, V, 0.0)
     return fe
+
+
+class KeyframeDBArrays(ctypes.Structure):
+    """gf_keyframe_db."""
+
+    _fields_ = [("nkf", ctypes.c_int32)] + [(k, ctypes.c_void_p) for k in
+                                           ("kp_off", "kps", "desc", "bow_off", "bow_words", "bow_values", "fv_off",
+                                            "fv_nodes", "fv_start", "fv_feats")]
+
+
+class KeyframeDB:
+    """The keyframes of a map as Relocalisation reads them (abi.h
+    gf_keyframe_db): per keyframe its keypoints, descriptors, BowVector and
+    FeatureVector (KeyFrame::ComputeBoW, levelsup 4). `transform(desc)` gives
+    (words, values, FeatureVector) — the library's ORBVocabulary.transform on
+    the device, or a CPU restatement in the oracle tests."""
+
+    def __init__(self, kf_kps: list, kf_desc: list, transform):
+        from .orb import KEYPOINT_DTYPE
+
+        self.nkf = len(kf_kps)
+        kps = [np.ascontiguousarray(k, KEYPOINT_DTYPE) for k in kf_kps]
+        desc = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in kf_desc]
+        self.kp_off = np.zeros(self.nkf + 1, np.int32)
+        self.kp_off[1:] = np.cumsum([len(k) for k in kps])
+        self.kps = np.concatenate(kps) if kps else np.zeros(0, KEYPOINT_DTYPE)
+        self.desc = np.ascontiguousarray(np.concatenate(desc) if desc else np.zeros((0, 32), np.uint8))
+        bw, bv, fn, fs, ff = [], [], [], [0], []
+        self.bow_off = np.zeros(self.nkf + 1, np.int32)
+        self.fv_off = np.zeros(self.nkf + 1, np.int32)
+        for k, d in enumerate(desc):
+            w, v, fv = transform(d)
+            bw.append(np.asarray(w, np.int32))
+            bv.append(np.asarray(v, np.float64))
+            self.bow_off[k + 1] = self.bow_off[k] + len(w)
+            fn.append(np.asarray(fv.nodes, np.int32))
+            base = fs[-1]
+            fs.extend((base + np.asarray(fv.start[1:], np.int64)).tolist())
+            ff.append(np.asarray(fv.feats, np.int32))
+            self.fv_off[k + 1] = self.fv_off[k] + len(fv.nodes)
+        cat = lambda xs, dt: np.ascontiguousarray(np.concatenate(xs) if xs else np.zeros(0, dt), dt)
+        self.bow_words, self.bow_values = cat(bw, np.int32), cat(bv, np.float64)
+        self.fv_nodes, self.fv_feats = cat(fn, np.int32), cat(ff, np.int32)
+        self.fv_start = np.ascontiguousarray(fs, np.int32)
+        self._dev = {}
+
+    def struct(self) -> KeyframeDBArrays:
+        a = [self.kp_off, self.kps, self.desc, self.bow_off, self.bow_words, self.bow_values, self.fv_off,
+             self.fv_nodes, self.fv_start, self.fv_feats]
+        return KeyframeDBArrays(self.nkf, *[x.ctypes.data if x.size else None for x in a])
+
+    def device(self, ctx):
+        """The gf_kfdb handle on ctx (created once, shared by the streams)."""
+        key = id(ctx)
+        if key not in self._dev:
+            h = ctypes.c_void_p()
+            check(lib().gf_kfdb_create(ctx.handle, ctypes.byref(self.struct()), ctypes.byref(h)))
+            self._dev[key] = h
+        return self._dev[key]
+
+    def __del__(self):
+        try:
+            for h in self._dev.values():
+                lib().gf_kfdb_destroy(h)
+        except Exception:
+            pass

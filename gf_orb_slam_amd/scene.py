@@ -272,7 +272,9 @@ def build_global_map(scene: Scene, cam, extract, period: int, traj_seed: int, g_
     an observation of it (one slot per keyframe and point), else a new point
     (its keyframe's descriptor, normal and UpdateNormalAndDepth distances, as
     build_map). At most g_cap points are kept (a seeded subset, in a seeded
-    order: the map's point indices); slots of dropped points are NULL.
+    order: the map's point indices); slots of dropped points are NULL. The
+    keyframes' keypoints and descriptors (kf_kps / kf_desc, slot order) feed
+    the relocalisation keyframe database (pipeline.KeyframeDB).
     Keyframes are in creation order (= ascending KeyFrame*); each keyframe's
     covisible keyframes sharing >= min_shared points, by weight descending
     (ties: later keyframe first), are mvpOrderedConnectedKeyFrames
@@ -289,8 +291,11 @@ def build_global_map(scene: Scene, cam, extract, period: int, traj_seed: int, g_
     key_to_pt = {}
     X_l, D_l, N_l, dmin_l, dmax_l = [], [], [], [], []
     slots = []  # per keyframe: point id per keypoint slot (-1 = NULL)
+    kf_kps, kf_desc = [], []
     for T, img in zip(poses, imgs):
         k, d = extract(img)
+        kf_kps.append(k)
+        kf_desc.append(d)
         X, ok = scene.backproject(T, k["x"].astype(np.float64), k["y"].astype(np.float64), cam)
         C = -T[:3, :3].astype(np.float64).T @ T[:3, 3].astype(np.float64)
         sl = np.full(len(k), -1, np.int64)
@@ -355,7 +360,7 @@ def build_global_map(scene: Scene, cam, extract, period: int, traj_seed: int, g_
                  kf_cov_off=kf_cov_off, kf_cov=np.array([b for c in cov for b in c], np.int32),
                  mp_bad=np.zeros(G, np.uint8), mp_obs_off=mp_obs_off,
                  mp_obs=np.array([k for o in obs for k in o], np.int32))
-    return dict(mp=mp, desc=desc, graph=graph, kf_Tcw=np.stack(poses))
+    return dict(mp=mp, desc=desc, graph=graph, kf_Tcw=np.stack(poses), kf_kps=kf_kps, kf_desc=kf_desc)
 
 
 class Workload:

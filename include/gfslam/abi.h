@@ -841,9 +841,31 @@ int gf_views_exclude_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2m
  *     th 0.8), outliers set NULL, mLastFrame = Frame(mCurrentFrame) (:901-910).
  * The local map (UpdateReference, :3689-3852) is the map set with
  * gf_frontend_set_map, in that order; keyframe insertion and local mapping
- * are outside the path. Track-loss fall-backs (TrackPreviousFrame,
- * relocalisation) are not modelled: the step flags them in GF_FE_STATS and
- * continues. updateAtFrameId stamps are stored relative to the current frame
+ * are outside the path. The tracking state machine of GrabImage
+ * (:602-644, 652-716, 854-911) runs per stream (GF_FE_TRACK):
+ *   WORKING with a velocity and >= 2 frames since a relocalisation:
+ *     TrackWithMotionModel; it fails on < 20 matches (:1559) or < 10 after
+ *     the outlier discard (:1641), and TrackPreviousFrame (:1325-1404) runs;
+ *   WORKING otherwise: TrackPreviousFrame (WindowSearch 200 from the upper
+ *     half of the pyramid, then 100 at any level, PoseOptimization,
+ *     SearchByProjection(Last, Cur, 15 or 50), PoseOptimization);
+ *   LOST: Relocalisation (:3854-4031) against the stream's keyframe
+ *     database (gf_frontend_set_kfdb; none: the frame stays LOST):
+ *     ComputeBoW, DetectRelocalisationCandidates, SearchByBoW(0.75) per
+ *     candidate (>= 15), P4P RANSAC iterate(5) rounds over the candidates
+ *     (0.99, 10, 300, 4, 0.5, 5.991) with PoseOptimization and the
+ *     SearchByProjection(F, KF, found, 10 / 3, 100 / 64) refinements, until
+ *     one pose keeps >= 50 inliers.
+ *   A frame whose initial estimate succeeded runs TrackLocalMap (the
+ *   SearchByProjection window is 5 and FRAME_INFO_MATRIX is skipped for two
+ *   frames after a relocalisation, :3162, :3318-3320); it fails on < 25
+ *   inliers within mMaxFrames of a relocalisation or < 15 (:2819-2824). A
+ *   failed frame sets LOST, clears the velocity and skips the post-publish
+ *   block: mLastFrame stays the last tracked frame.
+ * Assumed of the map: >= 6 keyframes (KeyFramesInMap() >= 4 for the motion
+ * model, > 5 for WindowSearch's octave floor; the keyframe graph's count when
+ * one is set) and frames past the initial TIME_INIT_TRACKING window.
+ * updateAtFrameId stamps are stored relative to the current frame
  * (the frame being tracked is 1, the next 2; every step shifts them by -1),
  * so a step has no per-frame host argument and can be replayed as a HIP
  * graph. Time budgets follow gf_set_budgets of the context (+inf = parity). */
@@ -867,6 +889,9 @@ typedef struct gf_frontend_params {
                                    set the projection bounds, the keypoint grid and the
                                    observability margins (Tracking.cc:876-877).
                                    k1 == 0: keypoints as extracted, bounds = the image. */
+    int32_t max_frames;         /* mMaxFrames = 18 * Camera.fps / 30 (Tracking.cc:153), the
+                                   window of TrackLocalMap's stricter inlier rule after a
+                                   relocalisation; 0: derived from dt */
 } gf_frontend_params;
 typedef struct gf_frontend gf_frontend;
 
@@ -938,8 +963,30 @@ enum {
                            [7] local-map search matches                      */
     GF_FE_CLOCK,        /* [B][GF_CK_WORDS(M, budget)] i64 budget clock record
                            of the last step (see gf_set_budgets)             */
+    GF_FE_TRACK,        /* [B][GF_TR_N] i32 tracking state, see GF_TR_*     */
+    GF_FE_RELOC,        /* [B][64] gf_reloc_kf: keyframes' relocalisation-query
+                           state (mnRelocQuery / mnRelocWords / mRelocScore) */
     GF_FE_NFIELDS
 };
+enum {
+    GF_TR_STATE = 0,    /* mState after the step: 0 WORKING, 1 LOST          */
+    GF_TR_VEL,          /* 1: mVelocity holds a motion, 0: empty              */
+    GF_TR_SINCE,        /* mnId - mnLastRelocFrameId (saturates at 1 << 30)  */
+    GF_TR_PATH,         /* initial estimate of the last step: 0 TrackWithMotionModel,
+                           1 TrackPreviousFrame after it failed, 2 TrackPreviousFrame,
+                           3 Relocalisation                                  */
+    GF_TR_QUERY,        /* mnId of the last frame (the keyframe database's query id) */
+    GF_TR_OK,           /* bOK of the last step's initial estimate           */
+    GF_TR_N = 8
+};
+/* KeyFrame::mnRelocQuery / mnRelocWords / mRelocScore of one keyframe of a
+ * stream's database (KeyFrame.h:163-165; the reference leaves mRelocScore
+ * uninitialised, here it starts at 0). */
+typedef struct gf_reloc_kf {
+    uint32_t query;
+    int32_t words;
+    float score;
+} gf_reloc_kf;
 enum {
     GF_ST_M3 = 0,       /* SearchByProjection(Cur, Last) matches            */
     GF_ST_FOUND,        /* nMatchesFound after the outlier discard          */
@@ -959,7 +1006,10 @@ enum {
                            32: isInFrustum cap, 64: MAP_INFO cap (active branch),
                            128: runActiveMapMatching cap, 256: MAP_INFO cap of
                            RunMapPointsSelection, 512: visibility cap of
-                           SearchAdditionalMatchesInFrame, 1024: SearchByProjection_Budget cap */
+                           SearchAdditionalMatchesInFrame, 1024: SearchByProjection_Budget cap,
+                           2048: TrackPreviousFrame ran, 4096: Relocalisation ran,
+                           8192: the initial estimate failed (no TrackLocalMap),
+                           16384: TrackLocalMap failed, 32768: relocalised */
     GF_ST_FRAMES,       /* frames tracked                                   */
     GF_ST_LDETS,        /* logDet evaluations of runActiveMapMatching (heap
                            pushes, Observability.cc:1373): SURVEY §8d E_ld  */
@@ -969,6 +1019,10 @@ enum {
                            sizes; SURVEY §8d B_match's C)                   */
     GF_ST_CAND_PROJ,    /* the same for SearchByProjection(F, local) and
                            SearchByProjection_Budget together              */
+    GF_ST_TPF,          /* TrackPreviousFrame's final nmatches (lmk_num_initTrack) */
+    GF_ST_NCAND,        /* relocalisation candidates (DetectRelocalisationCandidates) */
+    GF_ST_RELOC,        /* relocalisation: nGood of the last pose it optimised */
+    GF_ST_RANSAC,       /* relocalisation: PnPsolver::iterate calls           */
     GF_FE_NSTAT
 };
 int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* params, gf_frontend** out);
@@ -984,6 +1038,76 @@ int gf_frontend_set_source(gf_frontend* fe, const uint8_t* const* d_bases, const
  * mvpLocalMapPoints order. Resets that stream's observability state. */
 int gf_frontend_set_map(gf_frontend* fe, int stream, const gf_map_point* mps, const uint8_t* desc, int m);
 int gf_frontend_set_rng(gf_frontend* fe, int stream, uint32_t seed);
+/* ----------------------------------------- keyframe database (relocalisation)
+ * The keyframes of a stream's map as Relocalisation reads them: per keyframe
+ * its undistorted keypoints and descriptors (mvKeysUn, mDescriptors; slot i of
+ * the keyframe graph's kf_mp is keypoint i), its BowVector (words ascending,
+ * values) and FeatureVector (nodes ascending; node g's keypoints are
+ * fv_feats[fv_start[g] .. fv_start[g + 1]), offsets absolute over all
+ * keyframes, fv_start has fv_off[nkf] + 1 entries), all from
+ * KeyFrame::ComputeBoW with the front end's vocabulary (levelsup 4). The
+ * inverted file (KeyFrameDatabase::add, KeyFrameDatabase.cc:39-45) is built
+ * from the BowVectors, keyframes in index order (= insertion order).
+ * gf_kfdb_create uploads a database once (device resident; several streams
+ * over one scene share it); gf_frontend_set_kfdb attaches it to a stream,
+ * whose keyframe graph (gf_frontend_set_covis, same nkf and slot counts)
+ * supplies the map points, isBad flags and covisibility. */
+typedef struct gf_keyframe_db {
+    int32_t nkf;
+    const int32_t* kp_off;      /* [nkf + 1] keypoint offsets                 */
+    const gf_keypoint* kps;     /* [kp_off[nkf]]                              */
+    const uint8_t* desc;        /* [kp_off[nkf]][32]                          */
+    const int32_t* bow_off;     /* [nkf + 1]                                  */
+    const int32_t* bow_words;   /* [bow_off[nkf]]                             */
+    const double* bow_values;   /* [bow_off[nkf]]                             */
+    const int32_t* fv_off;      /* [nkf + 1] FeatureVector nodes per keyframe */
+    const int32_t* fv_nodes;    /* [fv_off[nkf]]                              */
+    const int32_t* fv_start;    /* [fv_off[nkf] + 1]                          */
+    const int32_t* fv_feats;    /* [fv_start[fv_off[nkf]]] keyframe-local keypoint indices */
+} gf_keyframe_db;
+typedef struct gf_kfdb gf_kfdb;
+int gf_kfdb_create(gf_ctx* ctx, const gf_keyframe_db* db, gf_kfdb** out);
+int gf_kfdb_destroy(gf_kfdb* db);
+/* NULL detaches (Relocalisation then finds no candidate). The stream's
+ * keyframes' query state (GF_FE_RELOC) is reset. */
+int gf_frontend_set_kfdb(gf_frontend* fe, int stream, gf_kfdb* db);
+/* The vocabulary of Frame::ComputeBoW for relocalisation (mpORBVocabulary);
+ * the caller keeps it alive while the front end steps. */
+int gf_frontend_set_vocab(gf_frontend* fe, gf_vocab* voc);
+/* The track-loss matchers of the step, one problem per call (host arrays,
+ * synchronous; at most 4096 keypoints a frame and map points):
+ * gf_window_search: ORBmatcher::WindowSearch(F1, F2, window,
+ *   vpMapPointMatches2, min_level, max_level) (ORBmatcher.cc:979-1086) with
+ *   ORBmatcher(nnratio, check_ori); F1 = keypoints / descriptors / map point
+ *   per keypoint (-1 NULL) of the last frame, F2 the current frame; out (n2)
+ *   = vpMapPointMatches2; max_level = INT_MAX for none.
+ * gf_search_frames: ORBmatcher::SearchByProjection(F1, F2, window,
+ *   vpMapPointMatches2) (:1089-1168): F1's map points (world positions pos1)
+ *   projected with Tcw2; kp2mp / score (n2) are F2.mvpMapPoints /
+ *   mvpMatchScore, in and out.
+ * gf_search_kf_projection: ORBmatcher::SearchByProjection(F, pKF,
+ *   sAlreadyFound, th, ORBdist) (:2204-2336): the keyframe's slots (kf_mp,
+ *   its keypoints for the angle) against the frame at Tcw; found = a byte per
+ *   map point (sAlreadyFound); kp2mp / score in and out.
+ * gf_reloc_candidates: KeyFrameDatabase::DetectRelocalisationCandidates
+ *   (KeyFrameDatabase.cc:198-308) for a frame's BowVector against db's
+ *   keyframes (kf_bad optional; cov_off / cov = mvpOrderedConnectedKeyFrames);
+ *   query = the frame's mnId (!= 0); state (db->nkf entries) persists across
+ *   queries as the keyframes' fields do. */
+int gf_window_search(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps2, const uint8_t* desc2, int n2,
+                     const gf_keypoint* kps1, const uint8_t* desc1, const int32_t* mp1, int n1, int window,
+                     int min_level, int max_level, float nnratio, int check_ori, int32_t* out, int* nmatches);
+int gf_search_frames(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps2, const uint8_t* desc2, int n2,
+                     const float* Tcw2, const gf_keypoint* kps1, const uint8_t* desc1, const int32_t* mp1,
+                     const float* pos1, int n1, int window, float nnratio, int32_t* kp2mp, int32_t* score,
+                     int* nmatches);
+int gf_search_kf_projection(gf_ctx* ctx, const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                            const float* Tcw, const gf_keypoint* kf_kps, const int32_t* kf_mp, int nslots,
+                            const gf_map_point* mps, const uint8_t* mp_desc, int nmp, const uint8_t* found, float th,
+                            int orb_dist, int check_ori, int32_t* kp2mp, int32_t* score, int* nmatches);
+int gf_reloc_candidates(gf_ctx* ctx, const int32_t* words, const double* values, int nwords, const gf_keyframe_db* db,
+                        const uint8_t* kf_bad, const int32_t* cov_off, const int32_t* cov, uint32_t query,
+                        gf_reloc_kf* state, int32_t* cands, int* ncand);
 /* The keyframe graph of one stream's map (host arrays, gf_covis_map over the
  * map set with gf_frontend_set_map: g->nmp must equal its size; at most 64
  * keyframes, 64 x keypoint-capacity slots and observations). Once any stream

@@ -329,4 +329,105 @@ int orc_search_triangulation(int check_ori, const int32_t* a_nodes, const int32_
     return GF_OK;
 }
 
+
+// L1Scoring::score (DBoW2 ScoringObject.cpp): over the words both BowVectors
+// hold, in ascending word order, score += |v - w| - |v| - |w|; -score / 2.
+double orc_bow_score_l1(const int32_t* w1, const double* v1, int n1, const int32_t* w2, const double* v2, int n2) {
+    double score = 0;
+    int i = 0, j = 0;
+    while (i < n1 && j < n2) {
+        if (w1[i] == w2[j]) {
+            const double vi = v1[i], wi = v2[j];
+            score += std::fabs(vi - wi) - std::fabs(vi) - std::fabs(wi);
+            i++;
+            j++;
+        } else if (w1[i] < w2[j]) {
+            i = (int)(std::lower_bound(w1 + i, w1 + n1, w2[j]) - w1);
+        } else {
+            j = (int)(std::lower_bound(w2 + j, w2 + n2, w1[i]) - w2);
+        }
+    }
+    return -score / 2.0;
+}
+
+// KeyFrameDatabase::DetectRelocalisationCandidates (KeyFrameDatabase.cc:198-308)
+// for one frame (BowVector words / values, nwords entries) against nkf
+// keyframes: BowVector CSR bow_off / bow_words / bow_values, the inverted file
+// (mvInvertedFile: per word the non-bad keyframes in insertion order, here
+// ascending keyframe index; kf_bad may be null), the first 10 of
+// mvpOrderedConnectedKeyFrames (cov_off / cov), and the keyframes'
+// mnRelocQuery / mnRelocWords / mRelocScore, which persist across queries
+// (a keyframe sharing words but not scored keeps an older score, :272-281).
+// query = the frame's mnId (never 0). Candidates in the reference's order.
+int orc_reloc_candidates(const int32_t* words, const double* values, int nwords, int nkf, const uint8_t* kf_bad,
+                         const int32_t* bow_off, const int32_t* bow_words, const double* bow_values,
+                         const int32_t* cov_off, const int32_t* cov, uint32_t query, uint32_t* reloc_query,
+                         int32_t* reloc_words, float* reloc_score, int32_t* cands, int* ncand) {
+    *ncand = 0;
+    // the inverted file: word -> keyframes (ascending)
+    std::map<int, std::vector<int>> inv;
+    for (int k = 0; k < nkf; k++) {
+        if (kf_bad && kf_bad[k]) continue;
+        for (int e = bow_off[k]; e < bow_off[k + 1]; e++) inv[bow_words[e]].push_back(k);
+    }
+    std::vector<int> sharing;  // lKFsSharingWords
+    for (int i = 0; i < nwords; i++) {
+        auto it = inv.find(words[i]);
+        if (it == inv.end()) continue;
+        for (int k : it->second) {
+            if (reloc_query[k] != query) {
+                reloc_words[k] = 0;
+                reloc_query[k] = query;
+                sharing.push_back(k);
+            }
+            reloc_words[k]++;
+        }
+    }
+    if (sharing.empty()) return GF_OK;
+    int maxCommonWords = 0;
+    for (int k : sharing)
+        if (reloc_words[k] > maxCommonWords) maxCommonWords = reloc_words[k];
+    const int minCommonWords = maxCommonWords * 0.8f;
+    std::vector<std::pair<float, int>> scored;  // lScoreAndMatch
+    for (int k : sharing) {
+        if (reloc_words[k] > minCommonWords) {
+            const float si = (float)orc_bow_score_l1(words, values, nwords, bow_words + bow_off[k], bow_values + bow_off[k],
+                                                     bow_off[k + 1] - bow_off[k]);
+            reloc_score[k] = si;
+            scored.push_back({si, k});
+        }
+    }
+    if (scored.empty()) return GF_OK;
+    std::vector<std::pair<float, int>> acc;  // lAccScoreAndMatch
+    float bestAccScore = 0;
+    for (auto& sk : scored) {
+        const int k = sk.second;
+        float bestScore = sk.first, accScore = bestScore;
+        int pBest = k;
+        const int nn = std::min(10, cov_off[k + 1] - cov_off[k]);  // GetBestCovisibilityKeyFrames(10)
+        for (int j = 0; j < nn; j++) {
+            const int k2 = cov[cov_off[k] + j];
+            if (reloc_query[k2] != query) continue;
+            accScore += reloc_score[k2];
+            if (reloc_score[k2] > bestScore) {
+                pBest = k2;
+                bestScore = reloc_score[k2];
+            }
+        }
+        acc.push_back({accScore, pBest});
+        if (accScore > bestAccScore) bestAccScore = accScore;
+    }
+    const float minScoreToRetain = 0.75f * bestAccScore;
+    std::vector<char> added(nkf, 0);
+    int nc = 0;
+    for (auto& a : acc) {
+        if (a.first > minScoreToRetain && !added[a.second]) {
+            cands[nc++] = a.second;
+            added[a.second] = 1;
+        }
+    }
+    *ncand = nc;
+    return GF_OK;
+}
+
 }  // extern "C"

@@ -504,4 +504,195 @@ int orc_fuse(const gf_frame_info* fi, const float* Tcw, const float* Ow, const g
     return GF_OK;
 }
 
+
+// ORBmatcher::WindowSearch(F1, F2, windowSize, vpMapPointMatches2, minScaleLevel,
+// maxScaleLevel) (ORBmatcher.cc:979-1086) for the matcher TrackPreviousFrame
+// builds (ORBmatcher(0.9, true), Tracking.cc:1331): F1 = the last frame (its
+// undistorted keypoints, descriptors and map points, -1 = NULL), F2 = the
+// current frame. out (n2 entries) = vpMapPointMatches2. max_level = INT_MAX:
+// no maximum. Sequential claims; the ratio test compares int with the float
+// product (:1046); rotation bins as the reference computes them (:1052-1059).
+int orc_window_search(const gf_frame_info* fi, const gf_keypoint* kps2, const uint8_t* desc2, int n2,
+                      const gf_keypoint* kps1, const uint8_t* desc1, const int32_t* mp1, int n1, int window,
+                      int min_level, int max_level, float nnratio, int check_ori, int32_t* out, int* nmatches) {
+    orc::FrameGrid G(fi, kps2, n2);
+    for (int i = 0; i < n2; i++) out[i] = -1;
+    std::vector<int> rotHist[orc::HISTO_LENGTH];
+    const float factor = 1.0f / orc::HISTO_LENGTH;
+    const bool bMinLevel = min_level > 0, bMaxLevel = max_level < INT_MAX;
+    int nm = 0;
+    for (int i1 = 0; i1 < n1; i1++) {
+        if (mp1[i1] < 0) continue;
+        const gf_keypoint& kp1 = kps1[i1];
+        const int level1 = kp1.octave;
+        if (bMinLevel && level1 < min_level) continue;
+        if (bMaxLevel && level1 > max_level) continue;
+        const std::vector<int> idx2 = G.area(kp1.x, kp1.y, (float)window, level1, level1);
+        if (idx2.empty()) continue;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int i2 : idx2) {
+            if (out[i2] >= 0) continue;
+            const int dist = orc::descriptor_distance(desc1 + 32 * (size_t)i1, desc2 + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if ((float)bestDist <= (float)bestDist2 * nnratio && bestDist <= orc::TH_HIGH) {
+            out[bestIdx2] = mp1[i1];
+            nm++;
+            if (check_ori) {
+                float rot = kp1.angle - kps2[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == orc::HISTO_LENGTH) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    if (check_ori) {
+        int sizes[orc::HISTO_LENGTH], i1, i2, i3;
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) sizes[b] = (int)rotHist[b].size();
+        orc::three_maxima(sizes, orc::HISTO_LENGTH, i1, i2, i3);
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int j : rotHist[b]) {
+                out[j] = -1;
+                nm--;
+            }
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchByProjection(Frame& F1, Frame& F2, windowSize,
+// vpMapPointMatches2) (ORBmatcher.cc:1089-1168): F1's map points (world
+// positions pos1) not already among F2's matches (the set is taken at entry,
+// :1092) projected with F2's pose, without a depth or bounds test, into a
+// same-level window; best < ratio x second (floats, :1155) and <= TH_HIGH.
+// kp2mp / score (n2 entries) are F2.mvpMapPoints in and vpMapPointMatches2 /
+// mvpMatchScore out.
+int orc_search_frames(const gf_frame_info* fi, const gf_keypoint* kps2, const uint8_t* desc2, int n2, const float* Tcw2,
+                      const gf_keypoint* kps1, const uint8_t* desc1, const int32_t* mp1, const float* pos1, int n1,
+                      int window, float nnratio, int32_t* kp2mp, int32_t* score, int* nmatches) {
+    orc::FrameGrid G(fi, kps2, n2);
+    std::vector<int> found;
+    for (int i = 0; i < n2; i++)
+        if (kp2mp[i] >= 0) found.push_back(kp2mp[i]);
+    std::sort(found.begin(), found.end());
+    int nm = 0;
+    for (int i1 = 0; i1 < n1; i1++) {
+        const int mp = mp1[i1];
+        if (mp < 0 || std::binary_search(found.begin(), found.end(), mp)) continue;
+        const int level1 = kps1[i1].octave;
+        float Pc[3];
+        orc::transform(Tcw2, pos1 + 3 * (size_t)i1, Pc);
+        const float invzc2 = (float)(1.0 / (double)Pc[2]);
+        const float u2 = fi->fx * Pc[0] * invzc2 + fi->cx;
+        const float v2 = fi->fy * Pc[1] * invzc2 + fi->cy;
+        const std::vector<int> idx2 = G.area(u2, v2, (float)window, level1, level1);
+        if (idx2.empty()) continue;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int i2 : idx2) {
+            if (kp2mp[i2] >= 0) continue;
+            const int dist = orc::descriptor_distance(desc1 + 32 * (size_t)i1, desc2 + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if ((float)bestDist <= (float)bestDist2 * nnratio && bestDist <= orc::TH_HIGH) {
+            kp2mp[bestIdx2] = mp;
+            score[bestIdx2] = bestDist;
+            nm++;
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
+// ORBmatcher::SearchByProjection(Frame& F, KeyFrame* pKF, sAlreadyFound, th,
+// ORBdist) (ORBmatcher.cc:2204-2336), Relocalisation's ORBmatcher(0.9, true):
+// the keyframe's map points in slot order (kf_mp, -1 = NULL) not marked in
+// `found` (a byte per map point) projected with the frame's pose; image bounds,
+// the predicted level from the invariance distance (lower_bound of the scale
+// factors), a window th x scale over levels [pred - 1, pred + 1]; the nearest
+// unclaimed keypoint within ORBdist claims; rotation bins from the keyframe
+// keypoint's angle. kp2mp / score are the frame's mvpMapPoints / mvpMatchScore.
+int orc_search_kf_projection(const gf_frame_info* fi, const gf_keypoint* kps, const uint8_t* desc, int n,
+                             const float* Tcw, const gf_keypoint* kf_kps, const int32_t* kf_mp, int nslots,
+                             const gf_map_point* mps, const uint8_t* mp_desc, const uint8_t* found, float th,
+                             int orb_dist, int check_ori, int32_t* kp2mp, int32_t* score, int* nmatches) {
+    orc::FrameGrid G(fi, kps, n);
+    float Ow[3];  // -Rcw^T tcw (:2210)
+    for (int c = 0; c < 3; c++) Ow[c] = -orc::dot3(Tcw[0 * 4 + c], Tcw[3], Tcw[1 * 4 + c], Tcw[7], Tcw[2 * 4 + c], Tcw[11]);
+    std::vector<int> rotHist[orc::HISTO_LENGTH];
+    const float factor = 1.0f / orc::HISTO_LENGTH;
+    int nm = 0;
+    for (int i = 0; i < nslots; i++) {
+        const int mp = kf_mp[i];
+        if (mp < 0 || found[mp]) continue;
+        const gf_map_point& P = mps[mp];
+        float Pc[3];
+        orc::transform(Tcw, P.pos, Pc);
+        const float invzc = (float)(1.0 / (double)Pc[2]);
+        const float u = fi->fx * Pc[0] * invzc + fi->cx;
+        const float v = fi->fy * Pc[1] * invzc + fi->cy;
+        if (u < fi->min_x || u > fi->max_x) continue;
+        if (v < fi->min_y || v > fi->max_y) continue;
+        const float minDistance = P.min_dist;
+        const float PO[3] = {P.pos[0] - Ow[0], P.pos[1] - Ow[1], P.pos[2] - Ow[2]};
+        const float dist3D = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+        const float ratio = dist3D / minDistance;
+        const int lb = (int)(std::lower_bound(G.scales.begin(), G.scales.end(), ratio) - G.scales.begin());
+        const int nPredictedLevel = std::min(lb, fi->nlevels - 1);
+        const float radius = th * G.scales[nPredictedLevel];
+        const std::vector<int> idx2 = G.area(u, v, radius, nPredictedLevel - 1, nPredictedLevel + 1);
+        if (idx2.empty()) continue;
+        int bestDist = INT_MAX, bestIdx2 = -1;
+        for (int i2 : idx2) {
+            if (kp2mp[i2] >= 0) continue;
+            const int dist = orc::descriptor_distance(mp_desc + 32 * (size_t)mp, desc + 32 * (size_t)i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+        if (bestDist <= orb_dist) {
+            kp2mp[bestIdx2] = mp;
+            score[bestIdx2] = bestDist;
+            nm++;
+            if (check_ori) {
+                float rot = kf_kps[i].angle - kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == orc::HISTO_LENGTH) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    if (check_ori) {
+        int sizes[orc::HISTO_LENGTH], i1, i2, i3;
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) sizes[b] = (int)rotHist[b].size();
+        orc::three_maxima(sizes, orc::HISTO_LENGTH, i1, i2, i3);
+        for (int b = 0; b < orc::HISTO_LENGTH; b++) {
+            if (b == i1 || b == i2 || b == i3) continue;
+            for (int j : rotHist[b]) {
+                kp2mp[j] = -1;
+                score[j] = 999;
+                nm--;
+            }
+        }
+    }
+    *nmatches = nm;
+    return GF_OK;
+}
+
 }  // extern "C"

@@ -600,6 +600,17 @@ struct Rand {  // glibc random_r TYPE_3: the process-wide std::rand()
         std::memset(state, 0, sizeof(state));
         initstate_r(s, state, sizeof(state), &rd);
     }
+    void load(const gf_rng& g) {  // a saved std::rand() state (gf_rng)
+        seed(1);
+        for (int i = 0; i < 31; i++) rd.state[i] = g.state[i];
+        rd.fptr = rd.state + g.f;
+        rd.rptr = rd.state + g.r;
+    }
+    void save(gf_rng& g) const {
+        for (int i = 0; i < 31; i++) g.state[i] = rd.state[i];
+        g.f = (int32_t)(rd.fptr - rd.state);
+        g.r = (int32_t)(rd.rptr - rd.state);
+    }
     int next() {
         int32_t r;
         random_r(&rd, &r);
@@ -639,6 +650,96 @@ int orc_pnp_init(int n, const gf_pnp_params* p, gf_pnp_state* st) {
     return GF_OK;
 }
 
+}  // extern "C"
+
+namespace orc_pnp {
+
+// One PnPsolver::iterate(n_iter, bNoMore, vbInliers, nInliers) call (:137-230)
+// on a solver state; draws from R (DUtils::Random::RandomInt over std::rand()),
+// *calls counts them. Outputs T (zeros unless found), inl (n), ninl, flags.
+static void iterate_call(const float* p3d, const float* p2d, const float* sigma2, int n, const float K[4],
+                         gf_pnp_state& st, uint8_t* best_mask, int n_iter, Rand& R, int* calls, float* T,
+                         uint8_t* inl, int32_t* ninliers, int32_t* flags) {
+    const double fu = K[0], fv = K[1], uc = K[2], vc = K[3];
+    std::vector<float> max_err(n);
+    for (int i = 0; i < n; i++) max_err[i] = sigma2[i] * st.th2;  // :126-128
+    std::vector<uint8_t> best(best_mask, best_mask + n), cur(n, 0), refined(n, 0);
+    std::vector<int> avail(std::max(n, 1));
+    EPnP E;
+    E.fu = fu;
+    E.fv = fv;
+    E.uc = uc;
+    E.vc = vc;
+    for (int i = 0; i < 16; i++) T[i] = 0.f;
+    for (int i = 0; i < n; i++) inl[i] = 0;
+    int fl = 0, ninl = 0;
+    if (n < st.min_inliers) {  // :145-149
+        *flags = GF_PNP_NOMORE;
+        *ninliers = 0;
+        return;
+    }
+    int cur_it = 0;
+    bool done = false;
+    while (st.iterations < st.max_iterations || cur_it < n_iter) {
+        cur_it++;
+        st.iterations++;
+        E.reset(st.min_set);
+        for (int i = 0; i < n; i++) avail[i] = i;  // vAvailableIndices = mvAllIndices
+        int size = n;
+        for (int i = 0; i < st.min_set; i++) {
+            const int randi = R.random_int(0, size - 1);
+            (*calls)++;
+            const int idx = avail[randi];
+            E.add(p3d[3 * idx], p3d[3 * idx + 1], p3d[3 * idx + 2], p2d[2 * idx], p2d[2 * idx + 1]);
+            avail[idx] = avail[size - 1];  // :171, index idx as the reference writes it
+            size--;
+        }
+        double Ri[3][3], ti[3];
+        E.compute_pose(Ri, ti);
+        const int inl_i = check_inliers(p3d, p2d, max_err.data(), n, Ri, ti, uc, vc, fu, fv, cur.data());
+        if (inl_i >= st.min_inliers) {
+            if (inl_i > st.best_inliers) {
+                best = cur;
+                st.best_inliers = inl_i;
+                to_Tcw(Ri, ti, st.best_Tcw);
+            }
+            // Refine :232-277
+            int K2 = 0;
+            for (int i = 0; i < n; i++) K2 += best[i];
+            E.reset(K2);
+            for (int i = 0; i < n; i++)
+                if (best[i]) E.add(p3d[3 * i], p3d[3 * i + 1], p3d[3 * i + 2], p2d[2 * i], p2d[2 * i + 1]);
+            double Rr[3][3], tr[3];
+            E.compute_pose(Rr, tr);
+            const int nref = check_inliers(p3d, p2d, max_err.data(), n, Rr, tr, uc, vc, fu, fv, refined.data());
+            if (nref > st.min_inliers) {
+                to_Tcw(Rr, tr, T);
+                for (int i = 0; i < n; i++) inl[i] = refined[i];
+                ninl = nref;
+                fl = GF_PNP_FOUND | GF_PNP_REFINED;
+                done = true;
+                break;
+            }
+        }
+    }
+    if (!done && st.iterations >= st.max_iterations) {  // :213-227
+        fl = GF_PNP_NOMORE;
+        if (st.best_inliers >= st.min_inliers) {
+            ninl = st.best_inliers;
+            for (int i = 0; i < n; i++) inl[i] = best[i];
+            for (int i = 0; i < 16; i++) T[i] = st.best_Tcw[i];
+            fl |= GF_PNP_FOUND;
+        }
+    }
+    std::memcpy(best_mask, best.data(), (size_t)n);
+    *flags = fl;
+    *ninliers = ninl;
+}
+
+}  // namespace orc_pnp
+
+extern "C" {
+
 // A sequence of iterate() calls on one solver of n correspondences with
 // std::srand(seed) before the first: call c runs n_iter[c] iterations; its
 // outputs land at Tcw[c*16], inliers[c*n], ninliers[c], flags[c];
@@ -652,85 +753,27 @@ int orc_pnp_run(const float* p3d, const float* p2d, const float* sigma2, int n, 
     Rand R;
     R.seed(seed);
     int calls = 0;
-    const double fu = K[0], fv = K[1], uc = K[2], vc = K[3];
-    std::vector<float> max_err(n);
-    for (int i = 0; i < n; i++) max_err[i] = sigma2[i] * st.th2;  // :126-128
-    std::vector<uint8_t> best(n, 0), cur(n, 0), refined(n, 0);
-    std::vector<int> avail(std::max(n, 1));
-    EPnP E;
-    E.fu = fu;
-    E.fv = fv;
-    E.uc = uc;
-    E.vc = vc;
+    std::vector<uint8_t> best(std::max(n, 1), 0);
     for (int c = 0; c < ncalls; c++) {
-        float* T = Tcw + 16 * c;
-        uint8_t* inl = inliers + (size_t)n * c;
-        for (int i = 0; i < 16; i++) T[i] = 0.f;
-        for (int i = 0; i < n; i++) inl[i] = 0;
-        int fl = 0, ninl = 0;
-        if (n < st.min_inliers) {  // :145-149
-            flags[c] = GF_PNP_NOMORE;
-            ninliers[c] = 0;
-            rand_calls[c] = calls;
-            continue;
-        }
-        int cur_it = 0;
-        bool done = false;
-        while (st.iterations < st.max_iterations || cur_it < n_iter[c]) {
-            cur_it++;
-            st.iterations++;
-            E.reset(st.min_set);
-            for (int i = 0; i < n; i++) avail[i] = i;  // vAvailableIndices = mvAllIndices
-            int size = n;
-            for (int i = 0; i < st.min_set; i++) {
-                const int randi = R.random_int(0, size - 1);
-                calls++;
-                const int idx = avail[randi];
-                E.add(p3d[3 * idx], p3d[3 * idx + 1], p3d[3 * idx + 2], p2d[2 * idx], p2d[2 * idx + 1]);
-                avail[idx] = avail[size - 1];  // :171, index idx as the reference writes it
-                size--;
-            }
-            double Ri[3][3], ti[3];
-            E.compute_pose(Ri, ti);
-            const int inl_i = check_inliers(p3d, p2d, max_err.data(), n, Ri, ti, uc, vc, fu, fv, cur.data());
-            if (inl_i >= st.min_inliers) {
-                if (inl_i > st.best_inliers) {
-                    best = cur;
-                    st.best_inliers = inl_i;
-                    to_Tcw(Ri, ti, st.best_Tcw);
-                }
-                // Refine :232-277
-                int K2 = 0;
-                for (int i = 0; i < n; i++) K2 += best[i];
-                E.reset(K2);
-                for (int i = 0; i < n; i++)
-                    if (best[i]) E.add(p3d[3 * i], p3d[3 * i + 1], p3d[3 * i + 2], p2d[2 * i], p2d[2 * i + 1]);
-                double Rr[3][3], tr[3];
-                E.compute_pose(Rr, tr);
-                const int nref = check_inliers(p3d, p2d, max_err.data(), n, Rr, tr, uc, vc, fu, fv, refined.data());
-                if (nref > st.min_inliers) {
-                    to_Tcw(Rr, tr, T);
-                    for (int i = 0; i < n; i++) inl[i] = refined[i];
-                    ninl = nref;
-                    fl = GF_PNP_FOUND | GF_PNP_REFINED;
-                    done = true;
-                    break;
-                }
-            }
-        }
-        if (!done && st.iterations >= st.max_iterations) {  // :213-227
-            fl = GF_PNP_NOMORE;
-            if (st.best_inliers >= st.min_inliers) {
-                ninl = st.best_inliers;
-                for (int i = 0; i < n; i++) inl[i] = best[i];
-                for (int i = 0; i < 16; i++) T[i] = st.best_Tcw[i];
-                fl |= GF_PNP_FOUND;
-            }
-        }
-        flags[c] = fl;
-        ninliers[c] = ninl;
+        iterate_call(p3d, p2d, sigma2, n, K, st, best.data(), n_iter[c], R, &calls, Tcw + 16 * c,
+                     inliers + (size_t)n * c, &ninliers[c], &flags[c]);
         rand_calls[c] = calls;
     }
+    return GF_OK;
+}
+
+// One iterate() call on a saved solver state (gf_pnp_iterate's contract):
+// rng is the std::rand() state (advanced by the draws made), best_mask
+// (mvbBestInliers) persists with the state.
+int orc_pnp_iterate(const float* p3d, const float* p2d, const float* sigma2, const float K[4], gf_pnp_state* st,
+                    uint8_t* best_mask, int n_iterations, gf_rng* rng, float* Tcw, uint8_t* inliers, int32_t* ninliers,
+                    int32_t* flags) {
+    using namespace orc_pnp;
+    Rand R;
+    R.load(*rng);
+    int calls = 0;
+    iterate_call(p3d, p2d, sigma2, st->n, K, *st, best_mask, n_iterations, R, &calls, Tcw, inliers, ninliers, flags);
+    R.save(*rng);
     return GF_OK;
 }
 

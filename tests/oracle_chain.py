@@ -33,6 +33,9 @@ def _orc():
         o.orc_chain_timings.argtypes = [_P, _P]
         o.orc_chain_set_clock.argtypes = [_P, _P, ctypes.c_size_t]
         o.orc_chain_set_covis.argtypes = [_P, _P]
+        o.orc_chain_set_kfdb.argtypes = [_P, _P]
+        o.orc_chain_set_vocab.argtypes = [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          _P, _P, _P, _P]
         o._chain_declared = True
     return o
 
@@ -68,6 +71,20 @@ class Chain:
 
         self._g = graph if isinstance(graph, CovisGraph) else CovisGraph(**graph)
         assert _orc().orc_chain_set_covis(self.h, ctypes.byref(self._g.struct())) == 0
+
+    def set_kfdb(self, db):
+        """The keyframe database (pipeline.KeyframeDB over the graph's keyframes; None: none)."""
+        self._db = db
+        assert _orc().orc_chain_set_kfdb(self.h, ctypes.byref(db.struct()) if db is not None else None) == 0
+
+    def set_vocab(self, tree: dict):
+        """The vocabulary tree arrays (bow.read_vocabulary / synth.synth_vocabulary layout)."""
+        self._voc = {k: np.ascontiguousarray(tree[k], dt) for k, dt in
+                     (("parent", np.int32), ("desc", np.uint8), ("weight", np.float64), ("is_leaf", np.uint8))}
+        v = self._voc
+        assert _orc().orc_chain_set_vocab(self.h, tree["k"], tree["L"], tree["scoring"], tree["weighting"],
+                                          len(v["parent"]), _p(v["parent"]), _p(v["desc"]), _p(v["weight"]),
+                                          _p(v["is_leaf"])) == 0
 
     def set_rng(self, seed: int):
         _orc().orc_chain_set_rng(self.h, ctypes.c_uint32(seed))
@@ -116,7 +133,8 @@ class Chain:
         return {k: int(s[i]) for i, k in enumerate(STATS)}
 
     STATE = ["last_kps", "last_desc", "last_nkp", "last_kp2mp", "last_outlier", "last_pos", "Tcw_last", "velocity",
-             "t_prev", "map", "map_desc", "nmp", "views", "mp_H", "mp_info", "mp_uv", "mp_upd", "rng"]
+             "t_prev", "t_cur", "map", "map_desc", "nmp", "views", "mp_H", "mp_info", "mp_uv", "mp_upd", "rng",
+             "track", "reloc"]
 
     def load_from(self, dev_state: dict, b: int):
         """Copy stream b's carried-over state (FrontEnd.read outputs) in."""

@@ -346,3 +346,70 @@ def initialize(K, kps1, kps2, matches12, rng_state, sigma=1.0, iterations=200, m
     rc = f(_p(Kf), sigma, iterations, min_triangulated, _p(k1), len(k1), _p(k2), len(k2), _p(m), _p(rng_state),
            _p(res), _p(p3d), _p(tri))
     return rc, res, p3d, tri
+
+
+def window_search(info, kps2, desc2, kps1, desc1, mp1, window, min_level, max_level=2**31 - 1, nnratio=0.9,
+                  check_ori=True):
+    """ORBmatcher::WindowSearch on the CPU oracle -> (nmatches, out[n2])."""
+    k2, d2 = np.ascontiguousarray(kps2, KEYPOINT_DTYPE), np.ascontiguousarray(desc2, np.uint8)
+    k1, d1 = np.ascontiguousarray(kps1, KEYPOINT_DTYPE), np.ascontiguousarray(desc1, np.uint8)
+    m1 = np.ascontiguousarray(mp1, np.int32)
+    out = np.zeros(max(len(k2), 1), np.int32)
+    nm = ctypes.c_int()
+    o = orc()
+    o.orc_window_search(ctypes.byref(info), _p(k2), _p(d2), len(k2), _p(k1), _p(d1), _p(m1), len(k1), window,
+                        min_level, max_level, ctypes.c_float(nnratio), int(check_ori), _p(out), ctypes.byref(nm))
+    return nm.value, out[:len(k2)].copy()
+
+
+def search_frames(info, kps2, desc2, Tcw2, kps1, desc1, mp1, pos1, window, kp2mp, score, nnratio=0.9):
+    """ORBmatcher::SearchByProjection(F1, F2, window, ...) on the CPU oracle ->
+    (nmatches, kp2mp, score)."""
+    k2, d2 = np.ascontiguousarray(kps2, KEYPOINT_DTYPE), np.ascontiguousarray(desc2, np.uint8)
+    k1, d1 = np.ascontiguousarray(kps1, KEYPOINT_DTYPE), np.ascontiguousarray(desc1, np.uint8)
+    m1, p1 = np.ascontiguousarray(mp1, np.int32), np.ascontiguousarray(pos1, np.float32)
+    T = np.ascontiguousarray(Tcw2, np.float32).reshape(16)
+    km, sc = np.array(kp2mp, np.int32), np.array(score, np.int32)
+    nm = ctypes.c_int()
+    o = orc()
+    o.orc_search_frames(ctypes.byref(info), _p(k2), _p(d2), len(k2), _p(T), _p(k1), _p(d1), _p(m1), _p(p1), len(k1),
+                        window, ctypes.c_float(nnratio), _p(km), _p(sc), ctypes.byref(nm))
+    return nm.value, km, sc
+
+
+def search_kf_projection(info, kps, desc, Tcw, kf_kps, kf_mp, mps, mp_desc, found, th, orb_dist, kp2mp, score,
+                         check_ori=True):
+    """ORBmatcher::SearchByProjection(F, KF, sAlreadyFound, th, ORBdist) on the
+    CPU oracle -> (nmatches, kp2mp, score)."""
+    k, d = np.ascontiguousarray(kps, KEYPOINT_DTYPE), np.ascontiguousarray(desc, np.uint8)
+    kk, km_ = np.ascontiguousarray(kf_kps, KEYPOINT_DTYPE), np.ascontiguousarray(kf_mp, np.int32)
+    m, md = np.ascontiguousarray(mps), np.ascontiguousarray(mp_desc, np.uint8)
+    f = np.ascontiguousarray(found, np.uint8)
+    T = np.ascontiguousarray(Tcw, np.float32).reshape(16)
+    km, sc = np.array(kp2mp, np.int32), np.array(score, np.int32)
+    nm = ctypes.c_int()
+    o = orc()
+    o.orc_search_kf_projection(ctypes.byref(info), _p(k), _p(d), len(k), _p(T), _p(kk), _p(km_), len(kk), _p(m),
+                               _p(md), _p(f), ctypes.c_float(th), orb_dist, int(check_ori), _p(km), _p(sc),
+                               ctypes.byref(nm))
+    return nm.value, km, sc
+
+
+def reloc_candidates(words, values, db, kf_bad, cov_off, cov, query, state):
+    """KeyFrameDatabase::DetectRelocalisationCandidates on the CPU oracle; db a
+    pipeline.KeyframeDB, state a RELOC_KF_DTYPE array (updated in place) ->
+    candidates."""
+    w, v = np.ascontiguousarray(words, np.int32), np.ascontiguousarray(values, np.float64)
+    nkf = db.nkf
+    rq = np.ascontiguousarray(state["query"][:nkf], np.uint32)
+    rw = np.ascontiguousarray(state["words"][:nkf], np.int32)
+    rs = np.ascontiguousarray(state["score"][:nkf], np.float32)
+    kb = np.ascontiguousarray(kf_bad if kf_bad is not None else np.zeros(nkf), np.uint8)
+    co, cv = np.ascontiguousarray(cov_off, np.int32), np.ascontiguousarray(cov, np.int32)
+    out = np.zeros(64, np.int32)
+    nc = ctypes.c_int()
+    o = orc()
+    o.orc_reloc_candidates(_p(w), _p(v), len(w), nkf, _p(kb), _p(db.bow_off), _p(db.bow_words), _p(db.bow_values),
+                           _p(co), _p(cv), ctypes.c_uint32(query), _p(rq), _p(rw), _p(rs), _p(out), ctypes.byref(nc))
+    state["query"][:nkf], state["words"][:nkf], state["score"][:nkf] = rq, rw, rs
+    return out[:nc.value].copy()
