@@ -222,8 +222,12 @@ EXACT = ["kps", "desc", "nkp", "kp2mp", "score", "outlier", "last_kps", "last_de
 
 
 def _compare(dev, ch, b, prefix):
+    n = int(ch.read("nkp"))
     for k in EXACT:
-        assert np.array_equal(dev[k][b], ch.read(k)), f"{prefix}{k} differs (stream {b})"
+        a, o = dev[k][b], ch.read(k)
+        if k in ("kps", "desc"):  # a frame with fewer keypoints leaves the device buffer's tail as it was
+            a, o = a[:n], o[:n]
+        assert np.array_equal(a, o), f"{prefix}{k} differs (stream {b})"
     nl = int(ch.stats()["nleft"])
     assert np.array_equal(dev["left"][b][:nl], ch.read("left")[:nl]), f"{prefix}leftovers differ (stream {b})"
     for k in ("Tcw", "velocity", "Tcw_last"):
