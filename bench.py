@@ -49,6 +49,7 @@ def kernel_bytes(camera: str, nfeat: int) -> dict:
         "k_resize": (P - P7) + (P - P0),  # read level l-1, write level l
         "k_blur_fast": 3 * P,             # read every level, write blurred level + FAST score map
         "k_describe": 60 * nfeat,         # 32 B descriptor + 28 B keypoint out
+        "k_describe_planes": 2 * P + 60 * nfeat,  # + both planes read once (IC_Angle level, rBRIEF blurred level)
         "extract_total": (P - P7) + (P - P0) + P + 2 * P + 60 * nfeat,
     }
 
@@ -442,7 +443,7 @@ def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, de
     ex = ORBextractor(nfeat, 1.2, 8, 1, 20)
     if refmap:
         gm = W0.build_global_maps(lambda im: ex(im), nmap, n_kf=n_kf, device=f"cuda:{device}")
-        return W0.scenes, [(g["mp"], g["desc"], g["graph"]) for g in gm]
+        return W0.scenes, [(g["mp"], g["desc"], g["graph"], g["kf_kps"], g["kf_desc"]) for g in gm]
     return W0.scenes, W0.build_maps(lambda im: ex(im), nmap, device=f"cuda:{device}")
 
 
@@ -503,6 +504,9 @@ def main():
     ap.add_argument("--config3-steps", type=int, default=10,
                     help="also time BASELINE config 3 (TUM 640x480, 2000 feats, GF 160; 0: skip)")
     ap.add_argument("--config3-batch", type=int, default=1024)
+    ap.add_argument("--no-reloc", action="store_true",
+                    help="no keyframe databases: a lost stream stays LOST (the step then skips the BoW / candidate "
+                         "launches); default: every stream relocalises against its scene's keyframes")
     args = ap.parse_args()
 
     if args.hw_queues > 0:  # before anything initialises the HIP runtime
@@ -529,7 +533,7 @@ def main():
     from gf_orb_slam_amd.bow import ORBVocabulary
     from gf_orb_slam_amd.dist import GfDist, checksum, share_world
     from gf_orb_slam_amd.orb import Context
-    from gf_orb_slam_amd.pipeline import CK, STATS, FrontEnd, chain_extraction
+    from gf_orb_slam_amd.pipeline import CK, STATS, TR, FrontEnd, KeyframeDB, chain_extraction
 
     cam = args.camera
     refmap = not args.fixed_map
@@ -555,6 +559,11 @@ def main():
     voc = gd.bcast_vocab(voc, 0)
     voc_ck = voc.checksum()
     voc_span = gd.gather_ints([voc_ck])
+    # Relocalisation's keyframe databases: KeyFrame::ComputeBoW of every keyframe
+    # with the broadcast vocabulary (one database per scene, shared by its streams)
+    dbs = None
+    if refmap and not args.no_reloc:
+        dbs = [KeyframeDB(m[3], m[4], voc.transform) for m in maps]
     W = scene.Workload(cam, B, n_scenes=S, period=args.period, seed=0, scenes=scenes, phase_offset=3 * rank)
     frames = W.render_all(f"cuda:{local}").contiguous()
     T, V = W.boot_state()
@@ -570,6 +579,10 @@ def main():
         for b in range(Bg):  # keyframe graphs: host-side, from the world blob
             load_map(fe, b, maps[W.scene_of[g * Bg + b]], with_points=False)
         map_cks.append(checksum(fe.read("map")) ^ checksum(fe.read("map_desc")))
+        if dbs is not None:
+            fe.set_vocab(voc)
+            for b in range(Bg):
+                fe.set_kfdb(b, dbs[W.scene_of[g * Bg + b]])
         for b in range(Bg):
             fe.set_rng(b, 1 + rank * B + g * Bg + b)
         fe.set_source(frames, W.scene_of[sl], W.phase[sl])
@@ -625,6 +638,7 @@ def main():
     stats = [fe.stats() for fe in fes]
     final = {k: np.concatenate([s[k] for s in stats]) for k in STATS}
     thist = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)  # [B][8] over the timed steps
+    trk = np.concatenate([fe.read("track") for fe in fes])  # GF_FE_TRACK after the timed steps
     if args.no_prof_timed:  # the kernel table from a profiled pass of the same steps
         for fe in fes:
             fe.prof_enable(True)
@@ -706,6 +720,15 @@ def main():
                                                  / max(prof["k_active_match_overflow"][1], 1), 4),
             "timing_note": "avg_launch_ms = small-pool pass + overflow pass (k_active_match_overflow) per step "
                            "and group; rocprof lists them as two kernels"})
+    if "k_describe" in priced:
+        # §8d prices describe at its outputs; the stage must also read the
+        # level and the blurred level around every keypoint: the planes once
+        bp = kb["k_describe_planes"] * Bg
+        ms_d = priced["k_describe"]["avg_launch_ms"]
+        priced["k_describe"]["with_planes_read"] = {
+            "algorithmic_bytes_per_launch": bp, "achieved": round(bp / (ms_d / 1e3) / 1e9, 2), "unit": "GB/s",
+            "frac": round(bp / (ms_d / 1e3) / 1e9 / 8000.0, 6),
+            "work": "%d frames x (2 P + 60 N): the IC_Angle level and the rBRIEF blurred level read once" % Bg}
     if "k_match_lastframe" in priced and "k_match_seq_pre" in prof:
         # the per-query precompute and the ordered pass are one SearchByProjection(Cur, Last)
         ms_pair = (prof["k_match_lastframe"][0] + prof["k_match_seq_pre"][0]) / prof["k_match_lastframe"][1]
@@ -799,6 +822,11 @@ def main():
                                           "budget_cut": int(mix[5])},
                      "branch_mix_warmup": {"leftovers_only": int(hist[1]), "search_by_projection": int(hist[2]),
                                            "active_matching": int(hist[3]), "nothing_in_view": int(hist[4])},
+                     "keyframe_databases": dbs is not None,
+                     "streams_lost_at_end": int((trk[:, TR["state"]] == 1).sum()),
+                     "last_step_paths": {p: int((trk[:, TR["path"]] == i).sum()) for i, p in
+                                         enumerate(["motion_model", "previous_frame_fallback", "previous_frame",
+                                                    "relocalisation"])},
                      "mean_local_map_points": round(local_mean, 1),
                      "mean_inliers": round(float(final["inl2"].mean()), 1),
                      "mean_last_frame_matches": round(float(final["m3"].mean()), 1),

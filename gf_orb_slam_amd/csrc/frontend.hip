@@ -207,8 +207,22 @@ __device__ int compact_in_view(const FeDev& D, int b, int32_t* out) {
     return cnt;
 }
 
+// mbTrackInView = false for the points the frame already matched (the
+// mnLastFrameSeen = mnId / mbTrackInView = false loop of
+// SearchReferencePointsInFrustum, Tracking.cc:3194-3208).
+__device__ __forceinline__ void exclude_matched(const FeDev& D, int b) {
+    const int n = D.nkp_tl[b], m = D.nmp[b];
+    const long long ko = (long long)b * D.cap, o = (long long)b * D.M;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int mp = D.kp2mp[ko + i];
+        if (mp >= 0 && mp < m) D.views[o + mp].in_view = 0;
+    }
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(64) void k_fe_branch(FeDev D) {
     const int b = blockIdx.x, lane = threadIdx.x;
+    exclude_matched(D, b);
     const int ntm = stat(D, GF_ST_TO_MATCH)[b];
     if (!D.gate_tl[b]) {  // no TrackLocalMap: the initial estimate failed
         if (lane == 0) {
@@ -270,6 +284,7 @@ __global__ __launch_bounds__(256) void k_fe_decide(FeDev D) {
     __syncthreads();
     const int br = stat(D, GF_ST_BRANCH)[b];
     const bool clocked = D.gf && D.match_ticks >= 0 && br == 0;
+    if (br == 0 && !clocked) exclude_matched(D, b);  // after the unclocked isInFrustum pass
     const int m = D.nmp[b];
     const long long o = (long long)b * D.M;
     int cut = m;
@@ -608,39 +623,11 @@ __device__ __forceinline__ void rows(T* dst, const T* src, const int32_t* lm, lo
     copy_rows<W>(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src), lm, o, k0, np, gather);
 }
 
-// The local map's rows (grid: point chunks x streams).
-__global__ __launch_bounds__(256) void k_fe_gather_rows(FeDev D, MapArrays G, MapArrays L) {
-    const int b = blockIdx.y, k0 = blockIdx.x * ROWS_PER_BLOCK;
-    const int n = D.nlm[b];
-    if (k0 >= n) return;
-    const int np = min(ROWS_PER_BLOCK, n - k0);
-    const long long o = (long long)b * D.M;
-    const int32_t* lm = D.lmp + o;
-    rows<sizeof(gf_map_point) / 4>((gf_map_point*)L.map, G.map, lm, o, k0, np, true);
-    rows<8>((uint8_t*)L.desc, G.desc, lm, o, k0, np, true);
-    rows<3>((float*)L.pos, G.pos, lm, o, k0, np, true);
-    rows<sizeof(gf_mp_view) / 4>(L.views, G.views, lm, o, k0, np, true);
-    rows<1>(L.upd, G.upd, lm, o, k0, np, true);
-}
-
-// The local map's visibility and updateAtFrameId back to the stream's map
-// points (H / ObsMat / u_proj are written in map order through the remap).
-__global__ __launch_bounds__(256) void k_fe_scatter_rows(FeDev D, MapArrays G, MapArrays L) {
-    const int b = blockIdx.y, k0 = blockIdx.x * ROWS_PER_BLOCK;
-    const int n = D.nlm[b];
-    if (k0 >= n) return;
-    const int np = min(ROWS_PER_BLOCK, n - k0);
-    const long long o = (long long)b * D.M;
-    const int32_t* lm = D.lmp + o;
-    rows<sizeof(gf_mp_view) / 4>(G.views, L.views, lm, o, k0, np, false);
-    rows<1>(G.upd, L.upd, lm, o, k0, np, false);
-}
-
-// Index conversion for the step (one workgroup per stream): g2l of the local
-// points, the frame's matches to local indices (a match outside the local map
-// is dropped; UpdateReference puts every matched point's keyframes in it).
-__global__ __launch_bounds__(256) void k_fe_gather(FeDev D, int32_t* lnmp) {
-    const int b = blockIdx.x, t = threadIdx.x;
+// Index conversion for the step: g2l of the local points, the frame's matches
+// to local indices (a match outside the local map is dropped; UpdateReference
+// puts every matched point's keyframes in it).
+__device__ void gather_index(const FeDev& D, int b, int32_t* lnmp) {
+    const int t = threadIdx.x;
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
@@ -662,8 +649,8 @@ __global__ __launch_bounds__(256) void k_fe_gather(FeDev D, int32_t* lnmp) {
 }
 
 // Matches and mLeftMapPoints back to map indices, g2l reset.
-__global__ __launch_bounds__(256) void k_fe_scatter(FeDev D) {
-    const int b = blockIdx.x, t = threadIdx.x;
+__device__ void scatter_index(const FeDev& D, int b) {
+    const int t = threadIdx.x;
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
@@ -676,6 +663,46 @@ __global__ __launch_bounds__(256) void k_fe_scatter(FeDev D) {
     }
     const int nl = stat(D, GF_ST_NLEFT)[b];
     for (int j = t; j < nl; j += 256) D.left[o + j] = lm[D.left[o + j]];
+}
+
+// The local map (grid: 1 + point chunks x streams): workgroup 0 converts the
+// indices, the others gather the local map's rows from the stream's map.
+__global__ __launch_bounds__(256) void k_fe_gather(FeDev D, MapArrays G, MapArrays L, int32_t* lnmp) {
+    const int b = blockIdx.y;
+    if (blockIdx.x == 0) {
+        gather_index(D, b, lnmp);
+        return;
+    }
+    const int k0 = (blockIdx.x - 1) * ROWS_PER_BLOCK;
+    const int n = D.nlm[b];
+    if (k0 >= n) return;
+    const int np = min(ROWS_PER_BLOCK, n - k0);
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    rows<sizeof(gf_map_point) / 4>((gf_map_point*)L.map, G.map, lm, o, k0, np, true);
+    rows<8>((uint8_t*)L.desc, G.desc, lm, o, k0, np, true);
+    rows<3>((float*)L.pos, G.pos, lm, o, k0, np, true);
+    rows<sizeof(gf_mp_view) / 4>(L.views, G.views, lm, o, k0, np, true);
+    rows<1>(L.upd, G.upd, lm, o, k0, np, true);
+}
+
+// Back to the stream's map: workgroup 0 converts the indices, the others
+// scatter the local map's visibility and updateAtFrameId (H / ObsMat /
+// u_proj are written in map order through the remap).
+__global__ __launch_bounds__(256) void k_fe_scatter(FeDev D, MapArrays G, MapArrays L) {
+    const int b = blockIdx.y;
+    if (blockIdx.x == 0) {
+        scatter_index(D, b);
+        return;
+    }
+    const int k0 = (blockIdx.x - 1) * ROWS_PER_BLOCK;
+    const int n = D.nlm[b];
+    if (k0 >= n) return;
+    const int np = min(ROWS_PER_BLOCK, n - k0);
+    const long long o = (long long)b * D.M;
+    const int32_t* lm = D.lmp + o;
+    rows<sizeof(gf_mp_view) / 4>(G.views, L.views, lm, o, k0, np, false);
+    rows<1>(G.upd, L.upd, lm, o, k0, np, false);
 }
 
 __global__ void k_fe_boot_begin(FeDev D) {
@@ -856,8 +883,6 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf::pose_opt_frames_gated(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
                                     fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
                                     col(GF_ST_ITER1), col(GF_ST_EDGES1), col(GF_ST_M3), 20, s));
-    FE_RC(gf_discard_outliers_dev(ctx, B, D.kp2mp, D.outl, D.nkp, cap, D.budget, col(GF_ST_FOUND),
-                                  col(GF_ST_TO_MATCH), s));
     // Relocalisation of the LOST streams: ComputeBoW, the keyframe database's
     // candidates, SearchByBoW per candidate (Tracking.cc:3861-3922)
     if (fe->rl_on) {
@@ -868,8 +893,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         FE_RC(gf::reloc_candidates(ctx, TL, s));
         FE_RC(gf::match_bow_pairs(ctx, 0, 0.75f, 1, B * TL.ncs, TL.pairs, TL.bow_nm, s));
     }
-    // the motion model's failure test, TrackPreviousFrame, the relocalisation
-    // loop, and the gates of the TrackLocalMap stages below
+    // the motion model's outlier discard and failure test, TrackPreviousFrame,
+    // the relocalisation loop, and the gates of the TrackLocalMap stages below
     FE_RC(gf::track_loss(ctx, fe->TL, s));
     const MapArrays WM{D.map, fe->wdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
     // keyframe graphs: H / ObsMat / u_proj stay in map order (the local map's
@@ -880,13 +905,9 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         // keyframes and mvpLocalMapPoints from this frame's matches
         FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp_tl, cap, fe->lkf, fe->nlkf,
                                           gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
-        {
-            GF_PROF(ctx, s, "k_fe_gather_rows");
-            GF_LAUNCH(k_fe_gather_rows, dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM);
-            GF_HIP(hipGetLastError());
-        }
         GF_PROF(ctx, s, "k_fe_gather");
-        GF_LAUNCH(k_fe_gather, B, 256, 0, s, D, fe->w_nmp);
+        GF_LAUNCH(k_fe_gather, dim3(1 + (M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM,
+                  fe->w_nmp);
         GF_HIP(hipGetLastError());
     }
     // TrackLocalMap -> SearchReferencePointsInFrustum
@@ -897,7 +918,6 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         FE_RC(gf::obs_accumulate_matched(ctx, B, D.kp2mp, D.nkp_tl, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
                                          fe->base, rmp, s, D.gate_tl));
     }
-    FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp_tl, cap, D.views, D.nmp, M, s));
     {
         GF_PROF(ctx, s, "k_fe_branch");
         GF_LAUNCH(k_fe_branch, B, 64, 0, s, D);
@@ -918,7 +938,6 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                   fe->nview, clock(D.t_viz0, GF_CK_OFF_VIZ(M, R)), D.vtmp, s));
     } else {
         FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
-        FE_RC(gf_views_exclude_matched_dev(ctx, B, D.kp2mp, D.nkp_tl, cap, D.views, D.nmp, M, s));
     }
     {
         GF_PROF(ctx, s, "k_fe_decide");
@@ -991,13 +1010,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         if (fe->fork_post) GF_HIP(hipStreamWaitEvent(s, fe->ev_join, 0));  // thread_Select.join()
     }
     if (D.refmap) {
-        {
-            GF_PROF(ctx, s, "k_fe_scatter_rows");
-            GF_LAUNCH(k_fe_scatter_rows, dim3((M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM);
-            GF_HIP(hipGetLastError());
-        }
         GF_PROF(ctx, s, "k_fe_scatter");
-        GF_LAUNCH(k_fe_scatter, B, 256, 0, s, D);
+        GF_LAUNCH(k_fe_scatter, dim3(1 + (M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM);
         GF_HIP(hipGetLastError());
     }
     {

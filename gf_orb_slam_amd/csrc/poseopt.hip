@@ -43,15 +43,15 @@ struct GatherArgs {
     gf_pose_edge* edges;
     int32_t* edge_kp;
     int32_t* nedges;
-    // optional gate: frame f is not optimised at all (nedges = -1) when
-    // gate[f] < gate_min
+    // optional gate: frame f is not optimised at all (nedges = 0, the
+    // optimisation skipped) when gate[f] < gate_min
     const int32_t* gate;
     int gate_min;
 };
 
-// Ordered compaction of the matched keypoints of one frame (one wave).
-__global__ __launch_bounds__(64) void k_pose_gather(GatherArgs G) {
-    const int f = blockIdx.x, l = threadIdx.x;
+// Ordered compaction of the matched keypoints of frame f (one wave).
+__device__ __forceinline__ void gather_frame(const GatherArgs& G, int f) {
+    const int l = threadIdx.x;
     if (G.gate && G.gate[f] < G.gate_min) {
         if (l == 0) G.nedges[f] = 0;
         return;
@@ -83,6 +83,16 @@ __global__ __launch_bounds__(64) void k_pose_gather(GatherArgs G) {
         cnt += __popcll(m);
     }
     if (l == 0) G.nedges[f] = cnt;
+}
+
+// One wave per frame: its edges in keypoint order, then PoseOptimization on
+// them (the gather and the LM in one launch: no launch gap between them on a
+// single sequence's chain).
+template <int WPS>
+__global__ __launch_bounds__(PO_T, WPS) void k_pose_opt_frames(GatherArgs G, PoseArgs A) {
+    gather_frame(G, blockIdx.x);
+    __syncthreads();  // the edges (global memory) visible to the whole wave
+    pose_opt_problem(A, blockIdx.x);
 }
 
 int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
@@ -175,11 +185,6 @@ int gf::pose_opt_frames_gated(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_k
     G.edges = (gf_pose_edge*)edges;
     G.edge_kp = (int32_t*)ekp;
     G.nedges = (int32_t*)ne;
-    {
-        GF_PROF(ctx, s, "k_pose_gather");
-        GF_LAUNCH(k_pose_gather, nframes, 64, 0, s, G);
-        GF_HIP(hipGetLastError());
-    }
     PoseArgs A{};
     A.edges = G.edges;
     A.nedges = G.nedges;
@@ -198,7 +203,10 @@ int gf::pose_opt_frames_gated(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_k
     A.kp_stride = kp_stride;
     A.gate = d_gate;
     A.gate_min = gate_min;
-    return launch_pose(ctx, nframes, A, s);
+    GF_PROF(ctx, s, "k_pose_opt");
+    GF_LAUNCH(k_pose_opt_frames<PO_WPS>, nframes, PO_T, 0, s, G, A);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
 }
 
 extern "C" {

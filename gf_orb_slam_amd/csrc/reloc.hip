@@ -6,8 +6,9 @@
 //                 (KeyFrameDatabase.cc:198-308) on the frame's BowVector and
 //                 the stream's database, then one ORBmatcher::SearchByBoW
 //                 pair per candidate (k_match_bow runs them, bow.hip);
-//   k_track_loss  one wave per stream: TrackWithMotionModel's failure test
-//                 (Tracking.cc:1559, 1641), TrackPreviousFrame (:1325-1404)
+//   k_track_loss  one wave per stream: TrackWithMotionModel's outlier
+//                 discard and failure test (Tracking.cc:1550-1563, 1559,
+//                 1641), TrackPreviousFrame (:1325-1404)
 //                 with WindowSearch (ORBmatcher.cc:979-1086) and
 //                 SearchByProjection(F1, F2, window) (:1089-1168), or the
 //                 relocalisation loop (:3884-4031): EPnP RANSAC iterate(5) per
@@ -32,7 +33,7 @@
 #include "reloc.h"
 
 struct gf_kfdb {
-    gf_ctx* ctx = nullptr;
+    int device = 0;  // the context's device (the context may go first)
     gf::KfdbDev dev{};
     std::vector<void*> allocs;
 };
@@ -668,6 +669,27 @@ __global__ __launch_bounds__(TL_T) void k_track_loss(gf::TrackLossArgs A) {
     const int b = blockIdx.x, lane = threadIdx.x, cap = A.cap;
     int32_t* T = A.track + (size_t)b * GF_TR_N;
     int path = T[GF_TR_PATH];
+    {  // TrackWithMotionModel's outlier discard (Tracking.cc:1550-1563): nMatchesFound, num_to_match
+        const int n = A.nkp[b];
+        int32_t* km = A.kp2mp + (size_t)b * cap;
+        uint8_t* ou = A.outl + (size_t)b * cap;
+        int c = 0;
+        for (int i = lane; i < n; i += TL_T)
+            if (km[i] >= 0) {
+                if (ou[i]) {
+                    km[i] = -1;
+                    ou[i] = 0;
+                } else {
+                    c++;
+                }
+            }
+        c = gfd::warp_sum(c);
+        if (lane == 0) {
+            stat_of(A, GF_ST_FOUND)[b] = c;
+            stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
+        }
+        __syncthreads();
+    }
     if (path == 0) {  // TrackWithMotionModel: < 20 matches (:1559) or < 10 after the discard (:1641)
         const bool ok = stat_of(A, GF_ST_M3)[b] >= 20 && stat_of(A, GF_ST_FOUND)[b] >= 10;
         if (ok) {
@@ -1148,7 +1170,7 @@ int gf_kfdb_create(gf_ctx* ctx, const gf_keyframe_db* db, gf_kfdb** out) {
     }
     GF_HIP(hipSetDevice(ctx->device));
     gf_kfdb* d = new gf_kfdb();
-    d->ctx = ctx;
+    d->device = ctx->device;
     auto up = [&](const void* src, size_t bytes) -> void* {
         void* p = nullptr;
         if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) return nullptr;
@@ -1193,7 +1215,7 @@ int gf_kfdb_create(gf_ctx* ctx, const gf_keyframe_db* db, gf_kfdb** out) {
 
 int gf_kfdb_destroy(gf_kfdb* d) {
     if (!d) return GF_OK;
-    (void)hipSetDevice(d->ctx->device);
+    (void)hipSetDevice(d->device);
     (void)hipDeviceSynchronize();
     for (void* p : d->allocs) (void)hipFree(p);
     delete d;

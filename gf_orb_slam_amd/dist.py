@@ -126,7 +126,10 @@ class TorchComm:
 # ------------------------------------------------------------- packing
 def pack_world(scenes, maps) -> np.ndarray:
     """Scenes (Scene.pack) and per-scene maps in one blob: (points,
-    descriptors) or (points, descriptors, keyframe graph arrays)."""
+    descriptors), (points, descriptors, keyframe graph arrays) or with the
+    keyframes' keypoints and descriptors too (the relocalisation database's
+    inputs): (points, descriptors, graph, kf_kps, kf_desc)."""
+    from .orb import KEYPOINT_DTYPE
     from .localmap import _ARRAYS
     from .matcher import MAP_POINT_DTYPE
 
@@ -137,12 +140,19 @@ def pack_world(scenes, maps) -> np.ndarray:
         sb = sc.pack()
         mb = np.ascontiguousarray(mp, MAP_POINT_DTYPE).view(np.uint8).reshape(-1)
         db = np.ascontiguousarray(d, np.uint8).reshape(-1)
-        hdr = np.array([sb.nbytes, len(mp), 0 if g is None else 1], np.int64).view(np.uint8)
+        kf = len(m) > 4
+        hdr = np.array([sb.nbytes, len(mp), 0 if g is None else (2 if kf else 1)], np.int64).view(np.uint8)
         parts += [hdr, sb, mb, db]
         if g is not None:
             for k, dt in _ARRAYS:
                 a = np.ascontiguousarray(g[k], dt).reshape(-1)
                 parts += [np.array([len(a)], np.int64).view(np.uint8), a.view(np.uint8)]
+        if kf:
+            parts.append(np.array([len(m[3])], np.int64).view(np.uint8))
+            for kp, de in zip(m[3], m[4]):
+                kp = np.ascontiguousarray(kp, KEYPOINT_DTYPE)
+                parts += [np.array([len(kp)], np.int64).view(np.uint8), kp.view(np.uint8),
+                          np.ascontiguousarray(de, np.uint8).reshape(-1)]
     return np.concatenate([np.array([len(scenes)], np.int64).view(np.uint8)] + parts)
 
 
@@ -151,6 +161,7 @@ def unpack_world(blob: np.ndarray):
     from .scene import Scene
 
     from .localmap import _ARRAYS
+    from .orb import KEYPOINT_DTYPE
 
     S = int(blob[:8].view(np.int64)[0])
     o = 8
@@ -172,7 +183,20 @@ def unpack_world(blob: np.ndarray):
                 nb = n * np.dtype(dt).itemsize
                 g[k] = blob[o:o + nb].copy().view(dt)
                 o += nb
-            maps.append((mp, d, g))
+            if hg == 2:
+                nkf = int(blob[o:o + 8].view(np.int64)[0])
+                o += 8
+                kps, des = [], []
+                for _ in range(nkf):
+                    n = int(blob[o:o + 8].view(np.int64)[0])
+                    o += 8
+                    kps.append(blob[o:o + n * KEYPOINT_DTYPE.itemsize].copy().view(KEYPOINT_DTYPE))
+                    o += n * KEYPOINT_DTYPE.itemsize
+                    des.append(blob[o:o + 32 * n].copy().reshape(n, 32))
+                    o += 32 * n
+                maps.append((mp, d, g, kps, des))
+            else:
+                maps.append((mp, d, g))
         else:
             maps.append((mp, d))
     return scenes, maps

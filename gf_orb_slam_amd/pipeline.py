@@ -377,12 +377,12 @@ class KeyframeDB:
         if key not in self._dev:
             h = ctypes.c_void_p()
             check(lib().gf_kfdb_create(ctx.handle, ctypes.byref(self.struct()), ctypes.byref(h)))
-            self._dev[key] = h
-        return self._dev[key]
+            self._dev[key] = (ctx, h)  # the context outlives the handle
+        return self._dev[key][1]
 
     def __del__(self):
         try:
-            for h in self._dev.values():
+            for _, h in self._dev.values():
                 lib().gf_kfdb_destroy(h)
         except Exception:
             pass

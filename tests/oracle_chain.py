@@ -134,7 +134,7 @@ class Chain:
 
     STATE = ["last_kps", "last_desc", "last_nkp", "last_kp2mp", "last_outlier", "last_pos", "Tcw_last", "velocity",
              "t_prev", "t_cur", "map", "map_desc", "nmp", "views", "mp_H", "mp_info", "mp_uv", "mp_upd", "rng",
-             "track", "reloc"]
+             "track", "reloc", "Xv", "Xv_next", "base"]  # the last three persist through a lost frame
 
     def load_from(self, dev_state: dict, b: int):
         """Copy stream b's carried-over state (FrontEnd.read outputs) in."""
