@@ -429,6 +429,66 @@ def config3_leg(local: int, batch: int, groups: int, steps: int, warmup: int) ->
             "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1]} for k, v in prof.items()}}
 
 
+# ------------------------------------------------------------- kernel table
+def _under_profiler() -> bool:
+    """True inside a rocprofv3 (or older rocprof) run: no nested profiler."""
+    return (any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+            or "rocprof" in os.environ.get("LD_PRELOAD", ""))
+
+
+def _kname(raw: str) -> str:
+    return raw.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
+
+
+def rocprof_kernel_table(args) -> tuple:
+    """Per-kernel dispatch durations of the headline timed region from a
+    rocprofv3 kernel trace of this script run as a child process (the same
+    workload and step counts, the other legs off, no HIP events in the timed
+    region): HIP events on a stream that shares a hardware queue with the
+    other groups' streams count the wait behind their kernels, the dispatch
+    timestamps do not. The timed region is the dispatches from the first
+    k_fe_begin of the timed steps to the last k_fe_end of them (one per group
+    and step). -> ({kernel: [durations ns]}, queues used, note)."""
+    import glob
+    import shutil
+    import tempfile
+
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return None, None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="gf_bench_kt_", dir="/tmp")
+    child = sys.argv[1:] + ["--kernels-child", "--no-prof-timed", "--no-cpu-baseline", "--single-stream-steps", "0",
+                            "--lba-batch", "0", "--config3-steps", "0", "--pcie-steps", "0", "--budget-steps", "0",
+                            "--isolated-steps", "0", "--kernel-times", "events"]
+    cmd = [exe, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+           os.path.abspath(__file__)] + child
+    try:
+        r = subprocess.run(cmd, cwd=d, env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
+                           stderr=subprocess.PIPE, timeout=600)
+    except subprocess.TimeoutExpired:
+        return None, None, "rocprofv3 child timed out"
+    tr = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    if r.returncode != 0 or not tr:
+        return None, None, "rocprofv3 child failed (exit %d): %s" % (r.returncode, r.stderr.decode()[-300:])
+    import csv
+
+    rows = list(csv.DictReader(open(tr[0])))
+    shutil.rmtree(d, ignore_errors=True)
+    G, W, K = max(1, args.groups), args.warmup, args.steps
+    beg = sorted(int(x["Start_Timestamp"]) for x in rows if _kname(x["Kernel_Name"]) == "k_fe_begin")
+    end = sorted(int(x["End_Timestamp"]) for x in rows if _kname(x["Kernel_Name"]) == "k_fe_end")
+    if len(beg) < (W + K) * G or len(end) < (W + K) * G:
+        return None, None, "timed region not found in the trace"
+    t0, t1 = beg[W * G], end[(W + K) * G - 1]
+    acc, queues = {}, set()
+    for x in rows:
+        a, b = int(x["Start_Timestamp"]), int(x["End_Timestamp"])
+        if a >= t0 and b <= t1:
+            acc.setdefault(_kname(x["Kernel_Name"]), []).append(b - a)
+            queues.add(x.get("Queue_Id"))
+    return acc, len(queues), None
+
+
 # ------------------------------------------------------------- main
 def build_world(cam: str, B: int, S: int, period: int, nfeat: int, nmap: int, device: int, stale: float,
                 refmap: bool, n_kf: int):
@@ -504,6 +564,10 @@ def main():
     ap.add_argument("--config3-steps", type=int, default=10,
                     help="also time BASELINE config 3 (TUM 640x480, 2000 feats, GF 160; 0: skip)")
     ap.add_argument("--config3-batch", type=int, default=1024)
+    ap.add_argument("--kernel-times", choices=("rocprof", "events"), default="rocprof",
+                    help="source of the per-kernel table: a rocprofv3 kernel trace of the same steps in a child "
+                         "process (default, one GPU, not under a profiler) or the HIP events of the timed region")
+    ap.add_argument("--kernels-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-reloc", action="store_true",
                     help="no keyframe databases: a lost stream stays LOST (the step then skips the BoW / candidate "
                          "launches); default: every stream relocalises against its scene's keyframes")
@@ -521,6 +585,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
+    ktab, kqueues, knote = None, None, "HIP events (--kernel-times events)"
+    if args.kernel_times == "rocprof" and not args.kernels_child:
+        if world > 1:
+            knote = "HIP events (rocprofv3 child only at one GPU)"
+        elif _under_profiler():
+            knote = "HIP events (this run is itself under a profiler)"
+        else:  # a child process, started before this one touches the GPU
+            ktab, kqueues, knote = rocprof_kernel_table(args)
+            knote = knote or "rocprofv3 kernel trace of the same steps (child process)"
 
     import torch
     import torch.distributed as dist
@@ -635,6 +708,11 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
+    if args.kernels_child:  # the profiled child ends with the timed region
+        print(json.dumps({"kernels_child": True, "ms_per_step": round(dt / args.steps * 1e3, 3)}))
+        for fe in fes:
+            fe.close()
+        return
     stats = [fe.stats() for fe in fes]
     final = {k: np.concatenate([s[k] for s in stats]) for k in STATS}
     thist = np.concatenate([fe.read("hist") for fe in fes]).astype(np.int64)  # [B][8] over the timed steps
@@ -737,8 +815,28 @@ def main():
     for k in priced:
         if work[k][0] == "f64":
             priced[k]["peak_note"] = "FP64 peak (AMD spec, vector = matrix on MI355X); this kernel is f64 VALU"
-    top = max(prof, key=lambda k: prof[k][0])
-    dom = max(priced, key=lambda k: prof[k][0])
+    # the rocprof dispatch durations of the same steps (child process), per
+    # launch of each priced kernel's HIP-event scope
+    rp = {k: (sum(v) / 1e6, len(v)) for k, v in ktab.items()} if ktab else None
+    SCOPE = {"k_active_match": ["k_active_match", "k_active_match_overflow"],
+             "k_match_lastframe": ["k_match_seq", "k_match_seq_pre"], "k_match_project": ["k_match"],
+             "k_pose_opt": ["k_pose_opt_frames"]}
+
+    def rp_total(k):
+        return sum(rp[n][0] for n in SCOPE.get(k, [k]) if n in rp) if rp else 0.0
+
+    if rp:
+        for k, e in priced.items():
+            if rp_total(k) > 0:
+                ms_r = rp_total(k) / prof[k][1]
+                e["avg_launch_ms_rocprof"] = round(ms_r, 4)
+                e["events_over_rocprof"] = round(e["avg_launch_ms"] / ms_r, 3)
+    if rp:
+        top = max(rp, key=lambda k: rp[k][0])
+        dom = max(priced, key=rp_total)
+    else:
+        top = max(prof, key=lambda k: prof[k][0])
+        dom = max(priced, key=lambda k: prof[k][0])
     traffic_src = None
     for cand in ("r03",):  # PMC traffic measured on this round's build and workload only
         try:
@@ -754,16 +852,18 @@ def main():
     roof = dict(priced[dom])
     roof["traffic_source"] = traffic_src
     roof["frames_per_launch"] = Bg
-    roof["dominant_by"] = "total HIP-event time over the timed region among the SURVEY §8d-priced kernels"
-    if top != dom:
-        roof["largest_kernel"] = {"kernel": top, "avg_launch_ms": round(prof[top][0] / prof[top][1], 4)}
+    roof["dominant_by"] = ("total rocprof dispatch time" if rp else "total HIP-event time") + \
+        " over the timed region among the SURVEY §8d-priced kernels"
+    tab = rp if rp else {k: tuple(v) for k, v in prof.items()}
+    if top not in SCOPE.get(dom, [dom]):
+        roof["largest_kernel"] = {"kernel": top, "avg_launch_ms": round(tab[top][0] / tab[top][1], 4)}
     roof["other_kernels"] = {k: v for k, v in priced.items() if k != dom}
-    ext_ms = sum(prof[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
-                 if k in prof)
+    ext_ms = sum(tab[k][0] for k in ("k_resize", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
+                 if k in tab)
     ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
-    gf_kernels = [k for k in prof if k.startswith(("k_obs", "k_onepoint", "k_active"))]
-    gf_ms = sum(prof[k][0] for k in gf_kernels)
-    all_ms = sum(v[0] for v in prof.values())
+    gf_kernels = [k for k in tab if k.startswith(("k_obs", "k_onepoint", "k_active"))]
+    gf_ms = sum(tab[k][0] for k in gf_kernels)
+    all_ms = sum(v[0] for v in tab.values())
     pose_ms = prof.get("k_pose_opt", (0.0, 1))
     pose_avg_ms = pose_ms[0] / max(pose_ms[1], 1)
     mean_iters = float(iters.mean())
@@ -815,8 +915,9 @@ def main():
                       "share_of_kernel_time": round(gf_ms / all_ms, 4) if all_ms else None,
                       "logdets_per_frame": round(ldets_total / nfr, 1),
                       "active_matches_per_frame": round(local_total / nfr, 2),
-                      "note": "HIP-event time of the GF kernels (FRAME_INFO / MAP_INFO builds, one-point "
-                              "precompute, runActiveMapMatching) over all kernel time; groups overlap"},
+                      "note": ("rocprof dispatch" if rp else "HIP-event") + " time of the GF kernels (FRAME_INFO / "
+                              "MAP_INFO builds, one-point precompute, runActiveMapMatching) over all kernel time; "
+                              "groups overlap"},
         "tracking": {"branch_mix_timed": {"leftovers_only": int(mix[1]), "search_by_projection": int(mix[2]),
                                           "active_matching": int(mix[3]), "nothing_in_view": int(mix[4]),
                                           "budget_cut": int(mix[5])},
@@ -837,12 +938,17 @@ def main():
                      "lost_frames_last_step": int((final["flags"] & 4 != 0).sum())},
         "extraction_stage": {"ms_per_frame": round(ext_ms / (B * args.steps), 5),
                              "algorithmic_GBps": round(ext_bw, 2) if ext_bw else None},
-        "kernels_note": f"HIP events per launch over the timed region; each launch covers one group ({Bg} sequences)"
-                        f" and the {G} groups' launches overlap (extraction stages chained one group at a time"
-                        f" when extraction_gate), so ms_per_step sums exceed the wall time per step",
+        "kernels_note": f"{knote}: per dispatch over the timed region; each launch covers one group ({Bg} "
+                        f"sequences) and the {G} groups' launches overlap (extraction stages chained one group at a "
+                        f"time when extraction_gate), so ms_per_step sums exceed the wall time per step"
+                        + (f"; the child's timed region used {kqueues} hardware queues" if kqueues else ""),
         "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1],
-                        "ms_per_step": round(v[0] / args.steps, 4)} for k, v in prof.items()},
+                        "ms_per_step": round(v[0] / args.steps, 4)} for k, v in sorted(tab.items(),
+                                                                                     key=lambda kv: -kv[1][0])},
     }
+    if rp:  # the HIP-event scopes of this run (they include queue waits behind other streams' kernels)
+        out["kernels_hip_events"] = {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1]}
+                                     for k, v in prof.items()}
     if args.isolated_steps > 0:
         # the priced kernel with one group running alone (after the timed
         # region): in the timed region the other groups' tracking kernels share

@@ -980,9 +980,11 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
     __shared__ DescLds sh_all[8];
-    __shared__ uint32_t sh_pat[256];  // the rBRIEF pattern, one dword per test
-    __shared__ int sh_umax[16];       // IC_Angle's umax (a lane-indexed read)
-    sh_pat[threadIdx.x] = c_pattern8[threadIdx.x];
+    // the rBRIEF pattern, one dword per test, bit-major (test 8 i + bit at
+    // bit * 32 + i): the 32 lanes of a half read 32 consecutive dwords
+    __shared__ uint32_t sh_pat[256];
+    __shared__ int sh_umax[16];  // IC_Angle's umax (a lane-indexed read)
+    sh_pat[(threadIdx.x & 7) * 32 + (threadIdx.x >> 3)] = c_pattern8[threadIdx.x];
     if (threadIdx.x < 16) sh_umax[threadIdx.x] = c_umax[threadIdx.x];
     __syncthreads();
     int bx, f;
@@ -1078,7 +1080,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
             int t[2];
 #pragma unroll
             for (int q = 0; q < 2; q++) {
-                const uint32_t pt = sh_pat[hl * 8 + bit] >> (16 * q);
+                const uint32_t pt = sh_pat[bit * 32 + hl] >> (16 * q);
                 const float px = (float)(int8_t)(pt & 0xff), py = (float)(int8_t)((pt >> 8) & 0xff);
                 const int ry = __float2int_rn(px * b + py * a);
                 const int rx = __float2int_rn(px * a - py * b);
