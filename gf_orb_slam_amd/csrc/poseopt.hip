@@ -88,12 +88,17 @@ __device__ __forceinline__ void gather_frame(const GatherArgs& G, int f) {
 // One wave per frame: its edges in keypoint order, then PoseOptimization on
 // them (the gather and the LM in one launch: no launch gap between them on a
 // single sequence's chain).
-template <int WPS>
-__global__ __launch_bounds__(PO_T, WPS) void k_pose_opt_frames(GatherArgs G, PoseArgs A) {
-    gather_frame(G, blockIdx.x);
-    __syncthreads();  // the edges (global memory) visible to the whole wave
-    pose_opt_problem(A, blockIdx.x);
+template <int WPS, int NT>
+__global__ __launch_bounds__(NT, WPS) void k_pose_opt_frames(GatherArgs G, PoseArgs A) {
+    if (threadIdx.x < 64) gather_frame(G, blockIdx.x);
+    __syncthreads();  // the edges (global memory) visible to the whole workgroup
+    pose_opt_problem<NT>(A, blockIdx.x);
 }
+
+// Batches up to this size run a problem per 256-thread workgroup (the LM
+// trials' edge passes on four waves): the single-sequence chain is one
+// wave's instruction stream, and with few problems the CUs are free.
+constexpr int PO_WIDE_MAX = 64;
 
 int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
     GF_PROF(ctx, s, "k_pose_opt");
@@ -204,7 +209,10 @@ int gf::pose_opt_frames_gated(gf_ctx* ctx, int nframes, float* d_Tcw, const gf_k
     A.gate = d_gate;
     A.gate_min = gate_min;
     GF_PROF(ctx, s, "k_pose_opt");
-    GF_LAUNCH(k_pose_opt_frames<PO_WPS>, nframes, PO_T, 0, s, G, A);
+    if (nframes <= PO_WIDE_MAX)
+        GF_LAUNCH((k_pose_opt_frames<1, 256>), nframes, 256, 0, s, G, A);
+    else
+        GF_LAUNCH((k_pose_opt_frames<PO_WPS, PO_T>), nframes, PO_T, 0, s, G, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

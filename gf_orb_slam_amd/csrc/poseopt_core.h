@@ -187,17 +187,22 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
 // in edge order, lanes 0..26 trial 0's H and b terms. When trial 0 is
 // accepted (most LM iterations) the next iteration's linearisation is
 // already in sh_sum — the same arithmetic g2o's next computeActiveErrors +
-// buildSystem at that estimate performs.
+// buildSystem at that estimate performs. With NT = 256 (a problem per
+// workgroup, for small batches) wave s evaluates trial s, so the trials'
+// edge passes run on four SIMDs instead of one after another.
+template <int NT>
 __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[PO_TP],
                                             double* sh_sum) {
     double acc = 0.0;
+    const int w = NT > 64 ? L.l >> 6 : 0, ll = NT > 64 ? L.l & 63 : L.l;
     for (int base = 0; base < L.n; base += PO_E) {
-        const int e = base + L.l;
-        if (L.l < PO_E && e < L.n) {
+        const int e = base + ll;
+        if (ll < PO_E && e < L.n && w < S) {
             const double info = L.info[e];
 #pragma unroll
             for (int s = 0; s < PO_SPEC; s++) {
                 if (s >= S) break;
+                if (NT > 64 && s != w) continue;
                 double pc[3], r0, r1;
                 edge_error(L, T[s], e, pc, r0, r1);
                 const double chi2 = r0 * (info * r0) + r1 * (info * r1);
@@ -242,7 +247,9 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
     __syncthreads();
 }
 
-// k_pose_opt's body: problem p by one wave (PO_T threads).
+// k_pose_opt's body: problem p by NT threads (one wave, or four with the
+// trials' passes split over them).
+template <int NT = PO_T>
 __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
     if (A.gate && A.gate[p] < A.gate_min) return;
     __shared__ double term[PO_ROWS][PO_TP];
@@ -260,7 +267,7 @@ __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
     L.n = min(max(A.nedges[p], 0), A.stride);
     if (L.n <= PO_LDS_EDGES) {
         const gf_pose_edge* src = A.edges + (size_t)p * A.stride;
-        for (int e = L.l; e < L.n; e += PO_T) sh_edges[e] = src[e];
+        for (int e = L.l; e < L.n; e += NT) sh_edges[e] = src[e];
         L.E = sh_edges;
         L.info = sh_info;
         __syncthreads();
@@ -287,7 +294,7 @@ __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
         for (int i = 0; i < 3; i++) T.t[i] = (double)Tp[4 * i + 3];
         gfse3::normalize(T.r);
     }
-    for (int e = L.l; e < L.n; e += PO_T) {
+    for (int e = L.l; e < L.n; e += NT) {
         L.info[e] = (double)L.E[e].inv_sigma2;
         ou[e] = 0;
     }
@@ -376,7 +383,7 @@ __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
                 }
                 __syncthreads();
                 PO_ST(3);
-                pass_trials(L, sh_T, S, term, sh_sum);
+                pass_trials<NT>(L, sh_T, S, term, sh_sum);
                 PO_ST(4);
                 for (int s2 = 0; s2 < S; s2++) {
                     const bool ok = sh_ok[s2];
@@ -422,7 +429,7 @@ __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
         // the last evaluated estimate, recomputed at the current one for
         // flagged edges.
         int nb = 0;
-        for (int base = 0; base < L.n; base += PO_T) {
+        for (int base = 0; base < L.n; base += NT) {
             const int e = base + L.l;
             bool bad = false;
             if (e < L.n) {
@@ -471,7 +478,7 @@ __device__ __forceinline__ void pose_opt_problem(const PoseArgs& A, int p) {
 #endif
     }
     if (A.kp_outl)
-        for (int e = L.l; e < L.n; e += PO_T)
+        for (int e = L.l; e < L.n; e += NT)
             A.kp_outl[(size_t)p * A.kp_stride + A.edge_kp[(size_t)p * A.stride + e]] = ou[e];
 }
 

@@ -376,7 +376,7 @@ __device__ int pose_wave(const gf::TrackLossArgs& A, int b) {
     P.edge_kp = ek;
     P.kp_outl = A.outl + (size_t)b * cap;
     P.kp_stride = cap;
-    gfpose::pose_opt_problem(P, 0);
+    gfpose::pose_opt_problem<64>(P, 0);
     __syncthreads();
     return pi[1];
 }
