@@ -194,21 +194,21 @@ template <int NT>
 __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[PO_TP],
                                             double* sh_sum) {
     double acc = 0.0;
-    const int w = NT > 64 ? L.l >> 6 : 0, ll = NT > 64 ? L.l & 63 : L.l;
+    const int wv = NT > 64 ? L.l >> 6 : 0, ll = NT > 64 ? L.l & 63 : L.l;
     for (int base = 0; base < L.n; base += PO_E) {
         const int e = base + ll;
-        if (ll < PO_E && e < L.n && w < S) {
+        if (ll < PO_E && e < L.n && wv < S) {
             const double info = L.info[e];
 #pragma unroll
             for (int s = 0; s < PO_SPEC; s++) {
                 if (s >= S) break;
-                if (NT > 64 && s != w) continue;
+                if (NT > 64 && s != wv) continue;
                 double pc[3], r0, r1;
                 edge_error(L, T[s], e, pc, r0, r1);
                 const double chi2 = r0 * (info * r0) + r1 * (info * r1);
                 double rho0, rho1;
                 robustify(chi2, L.delta, L.dsqr, rho0, rho1);
-                term[PO_CHI + s][L.l] = rho0;
+                term[PO_CHI + s][ll] = rho0;
                 if (s == 0) {
                     const double x = pc[0], y = pc[1], z = pc[2], z2 = z * z;
                     double J0[6], J1[6];
@@ -230,9 +230,9 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
 #pragma unroll
                     for (int a = 0; a < 6; a++)
 #pragma unroll
-                        for (int b = 0; b <= a; b++) term[k++][L.l] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
+                        for (int b = 0; b <= a; b++) term[k++][ll] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
 #pragma unroll
-                    for (int a = 0; a < 6; a++) term[21 + a][L.l] = J0[a] * o0 + J1[a] * o1;
+                    for (int a = 0; a < 6; a++) term[21 + a][ll] = J0[a] * o0 + J1[a] * o1;
                 }
             }
         }
