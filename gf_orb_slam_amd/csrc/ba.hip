@@ -784,17 +784,36 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
                 for (int a2 = c; a2 < 6; a2++) sL[tri(k0 + a2) + k0 + c] = Db[a2][c];
             }
         }
-        // trailing update: R_ij -= L_i,k0+m L_j,k0+m, m = 0..5, for k0+6 <= j <= i
-        const int ntr = tri(nrow);
-        for (int e = tid; e < ntr; e += BA_ST) {
-            int ii = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
-            while (tri(ii + 1) <= e) ii++;
-            while (tri(ii) > e) ii--;
-            const int jj = e - tri(ii), i = k0 + 6 + ii, j = k0 + 6 + jj;
-            double Rv = sL[tri(i) + j];
+        // trailing update: R_ij -= L_i,k0+m L_j,k0+m, m = 0..5, for k0+6 <= j <= i.
+        // Lane l of every wave keeps the panel rows j = k0 + 6 + l + 64 q in
+        // registers; wave w takes rows i = k0 + 6 + w, + 16, ... and reads
+        // each row's six panel values once (a broadcast), so an element costs
+        // one LDS read and one write instead of thirteen accesses.
+        {
+            double Lj[(BA_MAXN + 63) / 64][6];
 #pragma unroll
-            for (int m = 0; m < 6; m++) Rv = Rv - sL[tri(i) + k0 + m] * sL[tri(j) + k0 + m];
-            sL[tri(i) + j] = Rv;
+            for (int q = 0; q < (BA_MAXN + 63) / 64; q++) {
+                const int j = k0 + 6 + lane + 64 * q;
+#pragma unroll
+                for (int m = 0; m < 6; m++) Lj[q][m] = j < n ? sL[tri(j) + k0 + m] : 0.0;
+            }
+            for (int ii = w; ii < nrow; ii += BA_ST / 64) {
+                const int i = k0 + 6 + ii;
+                double Li[6];
+#pragma unroll
+                for (int m = 0; m < 6; m++) Li[m] = sL[tri(i) + k0 + m];
+#pragma unroll
+                for (int q = 0; q < (BA_MAXN + 63) / 64; q++) {
+                    const int jj = lane + 64 * q;
+                    if (jj <= ii) {
+                        const int j = k0 + 6 + jj;
+                        double Rv = sL[tri(i) + j];
+#pragma unroll
+                        for (int m = 0; m < 6; m++) Rv = Rv - Li[m] * Lj[q][m];
+                        sL[tri(i) + j] = Rv;
+                    }
+                }
+            }
         }
         __syncthreads();
         if (s_fail) break;

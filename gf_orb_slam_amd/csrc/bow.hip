@@ -136,7 +136,7 @@ __device__ int block_excl_scan(int v, int* tmp, int& total) {  // 256 threads
     return base + x - v;
 }
 
-__global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __restrict__ nfeat, int cap,
+__global__ __launch_bounds__(256) void k_bow_build(VocabDev V, int nframes, const int32_t* __restrict__ nfeat, int cap,
                                                    const int32_t* __restrict__ wid, const double* __restrict__ wval,
                                                    const int32_t* __restrict__ nid, int32_t* __restrict__ words,
                                                    double* __restrict__ values, int32_t* __restrict__ nwords,
@@ -146,8 +146,20 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __
     __shared__ unsigned long long kw[BOW_MAX], kn[BOW_MAX];
     __shared__ double vals[BOW_MAX];
     __shared__ int tmp[4], s_m;
-    const int f = blockIdx.x, tid = threadIdx.x;
-    const int n = gate && !gate[f] ? 0 : min(nfeat[f], cap);
+    __shared__ double s_norm;
+    const int tid = threadIdx.x;
+    // a small grid walks the frames: with a gate most frames are off, and a
+    // workgroup per frame would hold this kernel's LDS across the whole chip
+    for (int f = blockIdx.x; f < nframes; f += gridDim.x) {
+    if (gate && !gate[f]) {  // empty vectors
+        if (tid == 0) {
+            nwords[f] = 0;
+            nfv[f] = 0;
+            fv_start[(size_t)f * (cap + 1)] = 0;
+        }
+        continue;
+    }
+    const int n = min(nfeat[f], cap);
     const size_t g0 = (size_t)f * cap;
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
@@ -184,7 +196,6 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __
     }
     total = base;
     __syncthreads();
-    __shared__ double s_norm;
     if (tid == 0) {
         double norm = 0.0;
         if (V.scoring == 5) {  // DOT_PRODUCT: no normalisation; TF / TF_IDF divide by the size
@@ -218,6 +229,8 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, const int32_t* __
     if (tid == 0) {
         nfv[f] = base;
         fv_start[(size_t)f * (cap + 1) + base] = m;
+    }
+    __syncthreads();  // the LDS goes to the next frame
     }
 }
 
@@ -285,19 +298,26 @@ __device__ __forceinline__ void top2_merge(int& d1, int& p1, int& d2, int od1, i
     }
 }
 
-__global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ pairs, int mode, float nnratio,
-                                                   int check_ori, int32_t* __restrict__ nmatches) {
+__global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ pairs, int npairs, int mode,
+                                                   float nnratio, int check_ori, int32_t* __restrict__ nmatches) {
     __shared__ uint8_t claimed[BOW_MAX];
     __shared__ int2 common[BOW_MAX];
     __shared__ int rec[BOW_MAX];
     __shared__ uint8_t rbin[BOW_MAX];
     __shared__ int s_nc, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
-    const BowPair P = pairs[blockIdx.x];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    // a small grid walks the pairs (the step's pair list is mostly the empty
+    // pairs of streams that do not relocalise)
+    for (int pi = blockIdx.x; pi < npairs; pi += gridDim.x) {
+    const BowPair P = pairs[pi];
     const gf_bow_side& A = P.a;
     const gf_bow_side& B = P.b;
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const int nout = mode == 0 ? B.n : A.n;
     for (int i = tid; i < nout; i += 256) P.out[i] = -1;
+    if (A.nfv == 0 || B.nfv == 0) {  // no common node: no match
+        if (tid == 0) nmatches[pi] = 0;
+        continue;
+    }
     for (int i = tid; i < B.n; i += 256) claimed[i] = 0;
     if (tid == 0) s_nc = s_nm = 0;
     if (tid < HISTO_LENGTH) s_hist[tid] = 0;
@@ -365,7 +385,9 @@ __global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ p
     __syncthreads();
     const int nm = s_nm;
     if (check_ori) rotation_filter(nm, rbin, rec, P.out, s_hist, s_keep, &s_nm);
-    if (tid == 0) nmatches[blockIdx.x] = s_nm;
+    if (tid == 0) nmatches[pi] = s_nm;
+    __syncthreads();  // the LDS goes to the next pair
+    }
 }
 
 // SearchForTriangulation (ORBmatcher.cc:1426-1588): same node walk as
@@ -704,8 +726,8 @@ static int bow_transform_impl(gf_vocab* v, int nframes, const uint8_t* d_desc, c
     }
     {
         GF_PROF(v->ctx, s, "k_bow_build");
-        GF_LAUNCH(k_bow_build, nframes, 256, 0, s, V, d_n, cap, wid, wv, nid, d_words, d_values, d_nwords, d_fv_nodes,
-                  d_fv_start, d_fv_feats, d_nfv, d_gate);
+        GF_LAUNCH(k_bow_build, std::min(nframes, d_gate ? 32 : nframes), 256, 0, s, V, nframes, d_n, cap, wid, wv, nid,
+                  d_words, d_values, d_nwords, d_fv_nodes, d_fv_start, d_fv_feats, d_nfv, d_gate);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
@@ -726,7 +748,7 @@ int gf::match_bow_pairs(gf_ctx* ctx, int mode, float nnratio, int check_ori, int
     if (npairs <= 0) return GF_OK;
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_match_bow");
-    GF_LAUNCH(k_match_bow, npairs, 256, 0, s, d_pairs, mode, nnratio, check_ori, d_nmatches);
+    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, 0, s, d_pairs, npairs, mode, nnratio, check_ori, d_nmatches);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -798,7 +820,8 @@ int gf_match_bow_dev(gf_ctx* ctx, int mode, float nnratio, int check_ori, int np
     if (rc) return rc;
     GF_HIP(hipMemcpyAsync(dp, P.data(), sizeof(BowPair) * npairs, hipMemcpyHostToDevice, s));
     GF_PROF(ctx, s, "k_match_bow");
-    GF_LAUNCH(k_match_bow, npairs, 256, 0, s, (const BowPair*)dp, mode, nnratio, check_ori, d_nmatches);
+    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, 0, s, (const BowPair*)dp, npairs, mode, nnratio, check_ori,
+              d_nmatches);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -98,7 +98,9 @@ __global__ __launch_bounds__(NT, WPS) void k_pose_opt_frames(GatherArgs G, PoseA
 // Batches up to this size run a problem per 256-thread workgroup (the LM
 // trials' edge passes on four waves): the single-sequence chain is one
 // wave's instruction stream, and with few problems the CUs are free.
-constexpr int PO_WIDE_MAX = 64;
+#ifndef PO_WIDE_MAX
+#define PO_WIDE_MAX 64
+#endif
 
 int launch_pose(gf_ctx* ctx, int nprob, const PoseArgs& A, hipStream_t s) {
     GF_PROF(ctx, s, "k_pose_opt");
