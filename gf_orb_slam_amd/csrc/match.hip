@@ -210,9 +210,12 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
 // beside other kernels' workgroups on a CU. With MATCH_STAGE it also stages
 // the frame's keypoint positions / octaves (float4) and descriptors (48 B a
 // keypoint; the candidate loops then read no global memory) when that stays
-// within MATCH_STAGE_LDS.
+// within MATCH_STAGE_LDS. Off by default since r04: in the 4-group step the
+// staged workgroup's extra ~60 KB of LDS keeps the other groups' extraction
+// workgroups off its CU (A/B, one box: 101.2k vs 100.1k / 100.3k frames/s,
+// profiles/r04/ab4_*.json).
 #ifndef MATCH_STAGE
-#define MATCH_STAGE 1
+#define MATCH_STAGE 0
 #endif
 #define MATCH_STAGE_LDS (96 * 1024)
 __host__ __device__ __forceinline__ size_t match_base_lds(int kp_cap, int q_cap) {
