@@ -961,9 +961,15 @@ __device__ float fast_atan2f(float y, float x) {
 #define DS_BL 37
 #define DS_BLW 10   // dwords per window row (37 bytes at any alignment)
 #define DS_LOADS ((DS_IC * DS_ICW + DS_BL * DS_BLW + 63) / 64)
-struct DescLds {
+// rBRIEF samples read as aligned 8-byte words (ds_read_b64 banks over 64
+// dwords, not 32: the half-wave's pseudo-random sample positions collide on a
+// bank half as often) with the byte picked by a shift
+#ifndef DESC_B64
+#define DESC_B64 0
+#endif
+struct __align__(8) DescLds {
+    uint32_t bl[DS_BL * DS_BLW];  // first: 8-byte aligned (1480 B)
     uint32_t ic[DS_IC * DS_ICW];
-    uint32_t bl[DS_BL * DS_BLW];
     uint8_t ic_sh[DS_IC];
 };
 
@@ -1086,7 +1092,13 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
                 const int rx = __float2int_rn(px * a - py * b);
                 if (win) {
                     const int r = ry + 18;
+#if DESC_B64
+                    const int a = r * (4 * DS_BLW) + bsh + rx + 18;
+                    const uint64_t w8 = *reinterpret_cast<const uint64_t*>(bl8 + (a & ~7));
+                    t[q] = (int)((w8 >> (8 * (a & 7))) & 0xffu);
+#else
                     t[q] = bl8[r * (4 * DS_BLW) + bsh + rx + 18];
+#endif
                 } else {
                     const int xx = x + rx, yy = y + ry;
                     const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;

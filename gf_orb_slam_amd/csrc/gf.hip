@@ -509,13 +509,17 @@ struct OnePre {  // one-point result against the frame's starting claims
 };
 
 // One 1024-thread workgroup per frame: the keypoint grid, the keypoints'
-// (x, y, octave) and (up to 2048 keypoints) their descriptors in LDS, then
+// (x, y, octave) (and, up to PRE_DESC_LDS_MAX keypoints, their descriptors) in LDS, then
 // one thread per in-view map point runs the one-point scan. The active
 // matcher takes these results until a claim hits one of their holders.
 #ifndef PRE_THREADS
 #define PRE_THREADS 1024
 #endif
-#define PRE_DESC_LDS_MAX 2048
+// descriptors staged in LDS up to this capacity; 0 since r04 (see
+// SEQ_PRE_DESC_MAX in match.hip)
+#ifndef PRE_DESC_LDS_MAX
+#define PRE_DESC_LDS_MAX 0
+#endif
 __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OnePre* __restrict__ out) {
     extern __shared__ __align__(16) uint8_t smem[];
     const int f = blockIdx.x, tid = threadIdx.x;

@@ -465,7 +465,13 @@ struct SeqPre {
 #ifndef SEQ_PRE_THREADS
 #define SEQ_PRE_THREADS 1024
 #endif
-#define SEQ_PRE_DESC_MAX 2048
+// descriptors staged in LDS up to this capacity; 0 since r04 (A/B in the
+// 4-group step: 103.0k vs 101.8k / 101.4k frames/s with k_onepoint_pre's
+// likewise: the smaller workgroups leave room for the other groups'
+// extraction, the descriptor reads hit L2; profiles/r04/ab5_*.json)
+#ifndef SEQ_PRE_DESC_MAX
+#define SEQ_PRE_DESC_MAX 0
+#endif
 #define SEQ_PRE_G 4  // lanes per query
 __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,
                                                                    SeqPre* __restrict__ out) {
