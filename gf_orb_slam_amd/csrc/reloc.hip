@@ -664,11 +664,15 @@ __device__ void set_gates(const gf::TrackLossArgs& A, int b, bool ok, int since)
     if (A.nmp_step) A.nmp_step[b] = ok ? A.gnmp[b] : 0;
 }
 
-__global__ __launch_bounds__(TL_T) void k_track_loss(gf::TrackLossArgs A) {
-    __shared__ TLShared S;
+// The steady-state part of the step's track-loss stage, one light wave per
+// stream: TrackWithMotionModel's outlier discard and failure test. A stream
+// that passes gets its TrackLocalMap gates (GF_TR_OK = 1); the others (the
+// motion model failed, or the stream is on TrackPreviousFrame or LOST) are
+// left to k_track_loss with GF_TR_OK = 0 and GF_TR_PATH set.
+__global__ __launch_bounds__(TL_T) void k_track_gate(gf::TrackLossArgs A) {
     const int b = blockIdx.x, lane = threadIdx.x, cap = A.cap;
     int32_t* T = A.track + (size_t)b * GF_TR_N;
-    int path = T[GF_TR_PATH];
+    const int path = T[GF_TR_PATH];
     {  // TrackWithMotionModel's outlier discard (Tracking.cc:1550-1563): nMatchesFound, num_to_match
         const int n = A.nkp[b];
         int32_t* km = A.kp2mp + (size_t)b * cap;
@@ -684,47 +688,60 @@ __global__ __launch_bounds__(TL_T) void k_track_loss(gf::TrackLossArgs A) {
                 }
             }
         c = gfd::warp_sum(c);
+        if (path == 0) {  // TrackWithMotionModel: < 20 matches (:1559) or < 10 after the discard (:1641)
+            const bool ok = stat_of(A, GF_ST_M3)[b] >= 20 && c >= 10;
+            if (ok) {
+                if (lane == 0) {
+                    stat_of(A, GF_ST_FOUND)[b] = c;
+                    stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
+                    T[GF_TR_OK] = 1;
+                    set_gates(A, b, true, T[GF_TR_SINCE]);
+                }
+                return;
+            }
+            // fall back to TrackPreviousFrame
+            for (int i = lane; i < n; i += TL_T) km[i] = -1;
+            if (lane < 16) A.Tcw[16 * (size_t)b + lane] = A.Tcw_last[16 * (size_t)b + lane];
+        }
+        if (lane == 0) {
+            T[GF_TR_OK] = 0;
+            if (path == 0) T[GF_TR_PATH] = 1;
+        }
+    }
+}
+
+// TrackPreviousFrame or the relocalisation loop for the streams k_track_gate
+// left (GF_TR_OK = 0): a small grid of one-wave workgroups walks the streams,
+// since each workgroup holds a whole SIMD's registers and most steps have no
+// such stream.
+__global__ __launch_bounds__(TL_T) void k_track_loss(gf::TrackLossArgs A) {
+    __shared__ TLShared S;
+    const int lane = threadIdx.x, cap = A.cap;
+    for (int b = blockIdx.x; b < A.B; b += gridDim.x) {
+        int32_t* T = A.track + (size_t)b * GF_TR_N;
+        if (T[GF_TR_OK]) continue;
+        const int path = T[GF_TR_PATH];
+        const bool ok = path == 3 ? relocalise(A, b, S) : track_previous_frame(A, b, S);
+        // nMatchesFound / num_to_match of the frame's matches (Tracking.cc:3195-3228)
+        const int n = A.nkp[b];
+        int c = 0;
+        for (int i = lane; i < n; i += TL_T) c += A.kp2mp[(size_t)b * cap + i] >= 0;
+        c = gfd::warp_sum(c);
         if (lane == 0) {
             stat_of(A, GF_ST_FOUND)[b] = c;
             stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
-        }
-        __syncthreads();
-    }
-    if (path == 0) {  // TrackWithMotionModel: < 20 matches (:1559) or < 10 after the discard (:1641)
-        const bool ok = stat_of(A, GF_ST_M3)[b] >= 20 && stat_of(A, GF_ST_FOUND)[b] >= 10;
-        if (ok) {
-            if (lane == 0) {
-                T[GF_TR_OK] = 1;
-                set_gates(A, b, true, T[GF_TR_SINCE]);
+            T[GF_TR_OK] = ok;
+            int fl = stat_of(A, GF_ST_FLAGS)[b];
+            fl |= path == 3 ? 4096 : 2048;
+            if (!ok) fl |= 8192;
+            if (path == 3 && ok) {
+                fl |= 32768;
+                T[GF_TR_SINCE] = 0;  // mnLastRelocFrameId = mCurrentFrame.mnId
             }
-            return;
+            stat_of(A, GF_ST_FLAGS)[b] = fl;
+            set_gates(A, b, ok, T[GF_TR_SINCE]);
         }
-        path = 1;  // fall back to TrackPreviousFrame
-        const int n = A.nkp[b];
-        for (int i = lane; i < n; i += TL_T) A.kp2mp[(size_t)b * cap + i] = -1;
-        if (lane < 16) A.Tcw[16 * (size_t)b + lane] = A.Tcw_last[16 * (size_t)b + lane];
-        __syncthreads();
-    }
-    const bool ok = path == 3 ? relocalise(A, b, S) : track_previous_frame(A, b, S);
-    // nMatchesFound / num_to_match of the frame's matches (Tracking.cc:3195-3228)
-    const int n = A.nkp[b];
-    int c = 0;
-    for (int i = lane; i < n; i += TL_T) c += A.kp2mp[(size_t)b * cap + i] >= 0;
-    c = gfd::warp_sum(c);
-    if (lane == 0) {
-        stat_of(A, GF_ST_FOUND)[b] = c;
-        stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
-        T[GF_TR_PATH] = path;
-        T[GF_TR_OK] = ok;
-        int fl = stat_of(A, GF_ST_FLAGS)[b];
-        fl |= path == 3 ? 4096 : 2048;
-        if (!ok) fl |= 8192;
-        if (path == 3 && ok) {
-            fl |= 32768;
-            T[GF_TR_SINCE] = 0;  // mnLastRelocFrameId = mCurrentFrame.mnId
-        }
-        stat_of(A, GF_ST_FLAGS)[b] = fl;
-        set_gates(A, b, ok, T[GF_TR_SINCE]);
+        __syncthreads();  // the LDS goes to the next stream
     }
 }
 
@@ -974,8 +991,13 @@ int gf::reloc_candidates(gf_ctx* ctx, const TrackLossArgs& A, hipStream_t s) {
 }
 
 int gf::track_loss(gf_ctx* ctx, const TrackLossArgs& A, hipStream_t s) {
+    {
+        GF_PROF(ctx, s, "k_track_gate");
+        GF_LAUNCH(k_track_gate, A.B, TL_T, 0, s, A);
+        GF_HIP(hipGetLastError());
+    }
     GF_PROF(ctx, s, "k_track_loss");
-    GF_LAUNCH(k_track_loss, A.B, TL_T, 0, s, A);
+    GF_LAUNCH(k_track_loss, std::min(A.B, 64), TL_T, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
