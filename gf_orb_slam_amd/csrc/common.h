@@ -77,7 +77,7 @@ int ws_upload(gf_ctx* ctx, int slot, const void* host, size_t bytes, void** out)
 int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap, int nframes, int32_t* d_frame_mps,
                             const int32_t* d_nkps, int stride, int32_t* d_local_kfs, int32_t* d_n_local_kfs,
                             int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap, int32_t* d_ref_kf,
-                            int32_t* d_first, hipStream_t s);
+                            int32_t* d_first, int kf_max, hipStream_t s);
 
 // The observability passes with the map-point state (H / ObsMat / u_proj) kept
 // in map order while the step runs over a local map: local point q of frame f

@@ -904,7 +904,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         // TrackLocalMap -> UpdateReference (Tracking.cc:2745, 3689-3852): local
         // keyframes and mvpLocalMapPoints from this frame's matches
         FE_RC(gf::update_reference_frames(ctx, fe->d_covis, M, B, D.kp2mp, D.nkp_tl, cap, fe->lkf, fe->nlkf,
-                                          gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first, s));
+                                          gf_frontend::KF_CAP, D.lmp, D.nlm, M, fe->ref_kf, fe->rm_first,
+                                          gf_frontend::KF_CAP, s));
         GF_PROF(ctx, s, "k_fe_gather");
         GF_LAUNCH(k_fe_gather, dim3(1 + (M + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK, B), 256, 0, s, D, fe->gm, WM,
                   fe->w_nmp);

@@ -528,8 +528,7 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
     if (m == 0 || A.num_to_match[f] <= 0) return;  // k_active_match takes its early exit
     float4* X = (float4*)smem;                  // kp_cap
     int* cell_start = (int*)(X + A.kp_cap);     // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;      // NCELLS
-    int* items = cursor + NCELLS;               // kp_cap
+    int* items = cell_start + NCELLS + 1;       // kp_cap
     int* claim = items + A.kp_cap;              // kp_cap
     int* scratch = claim + A.kp_cap;            // kp_cap
     uint8_t* Ds = (uint8_t*)(scratch + A.kp_cap);  // 32 x kp_cap when kp_cap <= PRE_DESC_LDS_MAX
@@ -543,7 +542,7 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
     if (dl)
         for (int i = tid; i < 2 * n; i += PRE_THREADS)
             reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
-    build_grid(A.fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
+    build_grid(A.fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, items, claim, scratch,
                PRE_THREADS);
     for (int c = tid; c < NCELLS + 1; c += PRE_THREADS) A.grid_cs[(long long)f * (NCELLS + 1) + c] = cell_start[c];
     for (int i = tid; i < n; i += PRE_THREADS) A.grid_items[(long long)f * A.kp_cap + i] = items[i];
@@ -556,7 +555,7 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
 }
 
 size_t onepoint_pre_lds_bytes(int kp_cap) {
-    return 16 * (size_t)kp_cap + sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kp_cap) +
+    return 16 * (size_t)kp_cap + sizeof(int) * (NCELLS + 1 + 3 * (size_t)kp_cap) +
            (kp_cap <= PRE_DESC_LDS_MAX ? 32 * (size_t)kp_cap : 0);
 }
 

@@ -124,13 +124,12 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_fuse(FrameConst fc, const Fus
     const FuseProb& P = probs[blockIdx.x];
     const int n = P.n, tid = threadIdx.x;
     int* cell_start = lds;                 // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1; // NCELLS
-    int* items = cursor + NCELLS;          // n
+    int* items = cell_start + NCELLS + 1;  // n
     int* slot = items + n;                 // n: KF map point, then the first adder of an empty slot
     int* scratch = slot + n;               // n
     __shared__ int s_nf;
     if (tid == 0) s_nf = 0;
-    build_grid(fc, P.kps, n, P.kf_mp, cell_start, cursor, items, slot, scratch, MATCH_THREADS);
+    build_grid(fc, P.kps, n, P.kf_mp, cell_start, items, slot, scratch, MATCH_THREADS);
     // slot[k] = the first candidate (list order) that chose the empty slot k; INT_MAX = none
     for (int i = tid; i < n; i += MATCH_THREADS) slot[i] = INT_MAX;
     __syncthreads();
@@ -215,7 +214,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_fuse(FrameConst fc, const Fus
     if (tid == 0) *P.nfused = s_nf;
 }
 
-size_t fuse_lds_bytes(int n) { return sizeof(int) * ((size_t)2 * NCELLS + 1 + 3 * (size_t)n); }
+size_t fuse_lds_bytes(int n) { return sizeof(int) * ((size_t)NCELLS + 1 + 3 * (size_t)n); }
 
 }  // namespace
 

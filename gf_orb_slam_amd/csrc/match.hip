@@ -220,7 +220,7 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
 #define MATCH_STAGE_LDS (96 * 1024)
 __host__ __device__ __forceinline__ size_t match_base_lds(int kp_cap, int q_cap) {
     const int kc = kp_cap < KP_MAX ? kp_cap : KP_MAX, qc = q_cap < Q_MAX ? q_cap : Q_MAX;
-    return (sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kc) + (size_t)qc + 15) & ~(size_t)15;
+    return (sizeof(int) * (NCELLS + 1 + 3 * (size_t)kc) + (size_t)qc + 15) & ~(size_t)15;
 }
 __host__ __device__ __forceinline__ bool match_stage(int kp_cap, int q_cap) {
     return MATCH_STAGE && match_base_lds(kp_cap, q_cap) + 48 * (size_t)kp_cap <= MATCH_STAGE_LDS;
@@ -230,8 +230,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     extern __shared__ __align__(16) int lds[];
     const int kc = min(A.kp_cap, KP_MAX);
     int* cell_start = lds;                  // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;  // NCELLS
-    int* items = cursor + NCELLS;           // kc
+    int* items = cell_start + NCELLS + 1;   // kc
     int* claim = items + kc;                // kc
     int* minU = claim + kc;                 // kc
     uint8_t* done = (uint8_t*)(minU + kc);  // min(q_cap, Q_MAX)
@@ -295,7 +294,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
         s_cand = 0;
         for (int b = 0; b < HISTO_LENGTH; b++) s_hist[b] = 0;
     }
-    build_grid(fc, K, n, kp2mp, cell_start, cursor, items, claim, minU, MATCH_THREADS);
+    build_grid(fc, K, n, kp2mp, cell_start, items, claim, minU, MATCH_THREADS);
     for (int k = tid; k < nq; k += MATCH_THREADS) done[k] = 0;
     __syncthreads();
 
@@ -481,8 +480,7 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
     const int nq = min(A.m[f], Q_MAX);
     float4* X = (float4*)smem;                  // kp_cap: x, y, octave
     int* cell_start = (int*)(X + A.kp_cap);     // NCELLS + 1
-    int* cursor = cell_start + NCELLS + 1;      // NCELLS
-    int* items = cursor + NCELLS;               // kp_cap
+    int* items = cell_start + NCELLS + 1;       // kp_cap
     int* claim = items + A.kp_cap;              // kp_cap
     int* scratch = claim + A.kp_cap;            // kp_cap
     uint8_t* Ds = (uint8_t*)(scratch + A.kp_cap);  // 32 x kp_cap when kp_cap <= SEQ_PRE_DESC_MAX
@@ -496,8 +494,7 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
     if (dl)
         for (int i = tid; i < 2 * n; i += SEQ_PRE_THREADS)
             reinterpret_cast<uint4*>(Ds)[i] = reinterpret_cast<const uint4*>(D)[i];
-    build_grid(fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, cursor, items, claim, scratch,
-               SEQ_PRE_THREADS);
+    build_grid(fc, K, n, A.kp2mp + (long long)f * A.kp_cap, cell_start, items, claim, scratch, SEQ_PRE_THREADS);
     for (int c = tid; c < NCELLS + 1; c += SEQ_PRE_THREADS) A.grid_cs[(long long)f * (NCELLS + 1) + c] = cell_start[c];
     for (int i = tid; i < n; i += SEQ_PRE_THREADS) A.grid_items[(long long)f * A.kp_cap + i] = items[i];
     const uint8_t* DD = dl ? (const uint8_t*)Ds : D;
@@ -582,7 +579,7 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
 }
 
 size_t seq_pre_lds_bytes(int kp_cap) {
-    return 16 * (size_t)kp_cap + sizeof(int) * (2 * NCELLS + 1 + 3 * (size_t)kp_cap) +
+    return 16 * (size_t)kp_cap + sizeof(int) * (NCELLS + 1 + 3 * (size_t)kp_cap) +
            (kp_cap <= SEQ_PRE_DESC_MAX ? 32 * (size_t)kp_cap : 0);
 }
 

@@ -46,7 +46,17 @@ struct RefArgs {
     int mp_cap;
     int32_t* ref_kf;
     int32_t* first;  // [nframes][nmp] scratch
+    int kfc;         // keyframe capacity of the launch's maps (sizes the LDS)
 };
+
+// LDS of k_update_reference for maps of at most kfc keyframes: votes / slot
+// offsets [kfc + 1], local keyframes [kfc], marks [kfc]. (Sized per launch:
+// the front end's graphs hold at most 64 keyframes, and a fixed 8192-keyframe
+// footprint, 74 KB, kept the other stream groups' workgroups off the CU.)
+size_t rm_lds_bytes(int kfc) {
+    const size_t a = ((size_t)(kfc + 1) * 4 + 15) & ~(size_t)15, b = ((size_t)kfc * 4 + 15) & ~(size_t)15;
+    return a + b + (size_t)kfc;
+}
 
 // exclusive scan over the workgroup (16 waves); total returned in `total`
 __device__ int scan_1024(int v, int* tmp, int& total) {
@@ -72,9 +82,10 @@ __device__ int scan_1024(int v, int* tmp, int& total) {
 }
 
 __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
-    __shared__ int cnt[RM_MAXKF + 1];  // votes, then the slot offsets of the local keyframes
-    __shared__ int lkf[RM_MAXKF];   // local keyframes
-    __shared__ uint8_t mark[RM_MAXKF];
+    extern __shared__ __align__(16) uint8_t rm_lds[];
+    int* cnt = reinterpret_cast<int*>(rm_lds);  // votes, then the slot offsets of the local keyframes
+    int* lkf = reinterpret_cast<int*>(rm_lds + (((size_t)(A.kfc + 1) * 4 + 15) & ~(size_t)15));  // local keyframes
+    uint8_t* mark = reinterpret_cast<uint8_t*>(lkf) + (((size_t)A.kfc * 4 + 15) & ~(size_t)15);
     __shared__ int tmp[RM_T / 64];
     __shared__ unsigned long long s_best;
     __shared__ int s_nl;
@@ -207,6 +218,17 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     if (tid == 0) A.n_local_mps[f] = nm;
 }
 
+// dynamic LDS above 64 KB (maps of more than ~5400 keyframes) needs the attribute
+int rm_lds_attr(gf_ctx* ctx) {
+    static unsigned long long mask = 0;
+    if (!(mask & (1ull << ctx->device))) {
+        GF_HIP(hipFuncSetAttribute((const void*)k_update_reference, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)rm_lds_bytes(RM_MAXKF)));
+        mask |= 1ull << ctx->device;
+    }
+    return GF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -242,9 +264,11 @@ int gf_update_reference_dev(gf_ctx* ctx, const gf_covis_map* d_map, int nframes,
     A.ref_kf = d_ref_kf;
     A.first = (int32_t*)first;
     A.first_stride = m.nmp;
+    A.kfc = std::max(m.nkf, 1);
     hipStream_t s = (hipStream_t)stream;
+    if ((rc = rm_lds_attr(ctx))) return rc;
     GF_PROF(ctx, s, "k_update_reference");
-    GF_LAUNCH(k_update_reference, nframes, RM_T, 0, s, A);
+    GF_LAUNCH(k_update_reference, nframes, RM_T, rm_lds_bytes(A.kfc), s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -254,14 +278,17 @@ int gf_update_reference_dev(gf_ctx* ctx, const gf_covis_map* d_map, int nframes,
 namespace gf {
 // UpdateReference for B frames each against its own map: d_maps is a device
 // array of B gf_covis_map whose arrays are device pointers, every map with at
-// most nmp_cap points and RM_MAXKF keyframes (the front end's per-stream
+// most nmp_cap points and kf_max keyframes (the front end's per-stream
 // keyframe graphs); d_first is scratch of B * nmp_cap ints.
 int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap, int nframes, int32_t* d_frame_mps,
                             const int32_t* d_nkps, int stride, int32_t* d_local_kfs, int32_t* d_n_local_kfs,
                             int kf_cap, int32_t* d_local_mps, int32_t* d_n_local_mps, int mp_cap, int32_t* d_ref_kf,
-                            int32_t* d_first, hipStream_t s) {
+                            int32_t* d_first, int kf_max, hipStream_t s) {
     if (nframes <= 0) return GF_OK;
+    GF_CHECK(kf_max >= 0 && kf_max <= RM_MAXKF, GF_ERR_UNSUPPORTED, "more than 8192 keyframes");
+    if (int rc = rm_lds_attr(ctx)) return rc;
     RefArgs A{};
+    A.kfc = std::max(kf_max, 1);
     A.maps = d_maps;
     A.first_stride = nmp_cap;
     A.frame_mps = d_frame_mps;
@@ -276,7 +303,7 @@ int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap
     A.ref_kf = d_ref_kf;
     A.first = d_first;
     GF_PROF(ctx, s, "k_update_reference");
-    GF_LAUNCH(k_update_reference, nframes, RM_T, 0, s, A);
+    GF_LAUNCH(k_update_reference, nframes, RM_T, rm_lds_bytes(A.kfc), s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

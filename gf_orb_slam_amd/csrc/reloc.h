@@ -12,9 +12,9 @@ constexpr int RL_NC = 64;     // relocalisation candidate slots per stream (the 
 constexpr int RL_LCAP = 300;  // PnP hypotheses one iterate() call can need (mRansacMaxIts <= 300)
 constexpr int RL_WORK = 12;   // doubles per correspondence of the PnP refine buffer (pnp_core.h kWork)
 
-// Frame grid scratch per stream: cell_start [NCELLS + 1], cursor [NCELLS],
-// items / scratch / claim [cap] each.
-__host__ __device__ inline size_t grid_ints(int cap) { return 2 * (size_t)NCELLS + 1 + 3 * (size_t)cap; }
+// Frame grid scratch per stream: cell_start [NCELLS + 1], items / scratch /
+// claim [cap] each.
+__host__ __device__ inline size_t grid_ints(int cap) { return (size_t)NCELLS + 1 + 3 * (size_t)cap; }
 
 // Device view of a keyframe database (gf_kfdb) plus its inverted file.
 struct KfdbDev {

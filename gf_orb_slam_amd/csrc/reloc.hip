@@ -496,11 +496,10 @@ struct TLShared {
 __device__ GridView frame_grid(const gf::TrackLossArgs& A, int b) {
     int32_t* g = A.grid + (size_t)b * gf::grid_ints(A.cap);
     int* cs = g;
-    int* cursor = cs + NCELLS + 1;
-    int* items = cursor + NCELLS;
+    int* items = cs + NCELLS + 1;
     int* claim = items + A.cap;
     int* scratch = claim + A.cap;
-    build_grid(A.fc, A.kps + (size_t)b * A.cap, A.nkp[b], A.kp2mp + (size_t)b * A.cap, cs, cursor, items, claim,
+    build_grid(A.fc, A.kps + (size_t)b * A.cap, A.nkp[b], A.kp2mp + (size_t)b * A.cap, cs, items, claim,
                scratch, TL_T);
     return GridView{cs, items};
 }
@@ -935,11 +934,10 @@ struct UnitArgs {
 
 __device__ GridView unit_grid(const UnitArgs& U) {
     int* cs = U.grid;
-    int* cursor = cs + NCELLS + 1;
-    int* items = cursor + NCELLS;
+    int* items = cs + NCELLS + 1;
     int* claim = items + U.n2;
     int* scratch = claim + U.n2;
-    build_grid(U.fc, U.K2, U.n2, U.kp2mp, cs, cursor, items, claim, scratch, TL_T);
+    build_grid(U.fc, U.K2, U.n2, U.kp2mp, cs, items, claim, scratch, TL_T);
     return GridView{cs, items};
 }
 
