@@ -460,7 +460,7 @@ def rocprof_kernel_table(args) -> tuple:
     child = sys.argv[1:] + ["--kernels-child", "--no-prof-timed", "--no-cpu-baseline", "--single-stream-steps", "0",
                             "--lba-batch", "0", "--config3-steps", "0", "--pcie-steps", "0", "--budget-steps", "0",
                             "--isolated-steps", "0", "--kernel-times", "events"]
-    cmd = [exe, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+    cmd = [exe, "--kernel-trace", "--stats", "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
            os.path.abspath(__file__)] + child
     try:
         r = subprocess.run(cmd, cwd=d, env=dict(os.environ, TMPDIR="/tmp"), stdout=subprocess.DEVNULL,
@@ -473,6 +473,11 @@ def rocprof_kernel_table(args) -> tuple:
     import csv
 
     rows = list(csv.DictReader(open(tr[0])))
+    keep = getattr(args, "kernel_trace_dir", None)
+    if keep:  # the child's rocprof files (its --stats summary and trace) beside the bench output
+        os.makedirs(keep, exist_ok=True)
+        for f_ in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True):
+            shutil.copy(f_, os.path.join(keep, os.path.basename(f_)))
     shutil.rmtree(d, ignore_errors=True)
     G, W, K = max(1, args.groups), args.warmup, args.steps
     beg = sorted(int(x["Start_Timestamp"]) for x in rows if _kname(x["Kernel_Name"]) == "k_fe_begin")
@@ -486,6 +491,14 @@ def rocprof_kernel_table(args) -> tuple:
         if a >= t0 and b <= t1:
             acc.setdefault(_kname(x["Kernel_Name"]), []).append(b - a)
             queues.add(x.get("Queue_Id"))
+    if keep:  # the timed region's table (the figures `kernels` reports), as scripts/trace_timed.py writes it
+        tot = sum(sum(v) for v in acc.values())
+        with open(os.path.join(keep, "kernel_stats_timed.csv"), "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+            for k, v in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
+                w.writerow([k, len(v), sum(v), round(sum(v) / len(v), 1), round(100.0 * sum(v) / tot, 2), min(v),
+                            max(v)])
     return acc, len(queues), None
 
 
@@ -567,6 +580,9 @@ def main():
     ap.add_argument("--kernel-times", choices=("rocprof", "events"), default="rocprof",
                     help="source of the per-kernel table: a rocprofv3 kernel trace of the same steps in a child "
                          "process (default, one GPU, not under a profiler) or the HIP events of the timed region")
+    ap.add_argument("--kernel-trace-dir", default=None,
+                    help="keep the rocprofv3 child's files (kernel trace, --stats summary, the timed region's "
+                         "kernel_stats_timed.csv) in this directory")
     ap.add_argument("--kernels-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-reloc", action="store_true",
                     help="no keyframe databases: a lost stream stays LOST (the step then skips the BoW / candidate "

@@ -683,7 +683,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
 // Lists longer than the LDS buffer fall back to the sequential replay on
 // global memory (gfsel::retain_best_truncate, same result).
 #define SEL_MAX_CELLS 1024
+#ifndef SEL_THREADS
 #define SEL_THREADS 512
+#endif
 #define SEL_BUF 1024  // entries of wave 0's buffer (cell lists and the level list)
 #ifndef SEL_BUF_CELL
 #define SEL_BUF_CELL 1024  // entries of the other waves' buffers (cell lists only)
