@@ -83,10 +83,14 @@ int update_reference_frames(gf_ctx* ctx, const gf_covis_map* d_maps, int nmp_cap
 // in map order while the step runs over a local map: local point q of frame f
 // reads and writes entry remap[f * map_stride + q] (null: q itself). The
 // extern "C" gf_obs_*_dev entry points are these with remap = null (gf.hip).
+// d_info_lt (optional, [F][map_stride][32] doubles): the writers also store
+// each ObsMat's lower triangle packed there, and obs_active_match's log-dets
+// read it (logdet_sum_lower_packed) instead of the 49-entry block.
 int obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const gf_keypoint* d_kps,
                    const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp, const uint8_t* d_outlier,
                    const float* d_map_pos, const int32_t* d_nmp, int map_stride, const float* level_sigma2,
-                   int nlevels, double* d_H, double* d_info, float* d_uv, const int32_t* d_remap, void* stream);
+                   int nlevels, double* d_H, double* d_info, float* d_uv, const int32_t* d_remap, void* stream,
+                   double* d_info_lt = nullptr);
 // One stage's time-budget clock in the front end (gf_set_budgets): the timer
 // start of every frame (s_memrealtime ticks), the clock record ([F][stride]
 // int64, GF_FE_CLOCK) and the offset of the stage's elapsed-time array in it.
@@ -104,7 +108,8 @@ struct StageClock {
 int obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
                  const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views, int32_t* d_upd_id,
                  int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated, const int32_t* d_remap,
-                 void* stream, const StageClock& ck = StageClock{}, const long long* d_cap2 = nullptr);
+                 void* stream, const StageClock& ck = StageClock{}, const long long* d_cap2 = nullptr,
+                 double* d_info_lt = nullptr);
 
 // runActiveMapMatching's time cap (Observability.cc:1260, 1366-1370) for the
 // front end: time_for_match = match_ticks - time_Mat_Online - time_Viz, with
@@ -173,7 +178,8 @@ int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf
                      const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
                      const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
                      int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
-                     const int32_t* d_remap, void* stream, const ActiveClock& ck = ActiveClock{});
+                     const int32_t* d_remap, void* stream, const ActiveClock& ck = ActiveClock{},
+                     const double* d_info_lt = nullptr);
 
 // Candidate counting for the front end's matcher calls (SURVEY §8d B_match's
 // C): while a CandidateCount lives on this thread, every projection-matcher

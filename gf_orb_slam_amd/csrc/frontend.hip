@@ -755,6 +755,7 @@ struct gf_frontend {
     double* base = nullptr;
     double* mp_H = nullptr;
     double* mp_info = nullptr;
+    double* mp_info_lt = nullptr;  // [B][M][32]: the packed lower triangle of every mp_info block
     float* mp_uv = nullptr;
     float* mp_pos = nullptr;
     uint8_t* mp_updated = nullptr;
@@ -915,7 +916,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.gf) {
         FE_RC(gf::obs_update_gated(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, D.gate_fi, s));
         FE_RC(gf::obs_frame_info(ctx, &fe->ocam, B, fe->Xv, D.kps, D.nkp_fi, cap, D.kp2mp, D.outl, fe->mp_pos,
-                                 D.nmp, M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, rmp, s));
+                                 D.nmp, M, fe->level_sigma2, fe->p.nlevels, fe->mp_H, fe->mp_info, fe->mp_uv, rmp, s,
+                                 fe->mp_info_lt));
         FE_RC(gf::obs_accumulate_matched(ctx, B, D.kp2mp, D.nkp_tl, cap, fe->mp_info, D.upd, D.nmp, M, 1, 1e-5,
                                          fe->base, rmp, s, D.gate_tl));
     }
@@ -948,7 +950,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
     if (D.gf) {
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
                                fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s,
-                               mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R)) : gf::StageClock{}, D.cap2_mi));
+                               mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R)) : gf::StageClock{}, D.cap2_mi,
+                               fe->mp_info_lt));
         gf::ActiveClock ac;
         if (mclk) {
             ac.mat_t0 = D.t_mat0;
@@ -962,7 +965,7 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         FE_RC(gf::obs_active_match(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
                                    fe->mp_info, fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2,
                                    col(GF_ST_TO_MATCH), 1.f, 0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score,
-                                   D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s, ac));
+                                   D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s, ac, fe->mp_info_lt));
     }
     FE_RC(gf::match_project_th(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, D.th_m2, 0.8f,
                                D.kp2mp, D.score, D.nm2, s));
@@ -989,7 +992,8 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
                                    sp));
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp_post, M, 1, nullptr, D.upd, 2,
                                fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, sp,
-                               sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel));
+                               sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel,
+                               fe->mp_info_lt));
         if (fe->fork_post) GF_HIP(hipEventRecord(fe->ev_join, sp));
         // SearchAdditionalMatchesInFrame
         if (sclk) {
@@ -1126,6 +1130,11 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     F(GF_FE_BASE, double, (size_t)B * 49, fe->base);
     F(GF_FE_MP_H, double, (size_t)B * M * 14, fe->mp_H);
     F(GF_FE_MP_INFO, double, (size_t)B * M * 49, fe->mp_info);
+    {
+        void* lt = nullptr;
+        if ((rc = fe_alloc(fe, sizeof(double) * (size_t)B * M * 32, &lt))) return bail(rc);
+        fe->mp_info_lt = (double*)lt;
+    }
     F(GF_FE_MP_UV, float, (size_t)B * M * 2, fe->mp_uv);
     F(GF_FE_MP_UPD, int32_t, (size_t)B * M, D.upd);
     gf_rng* rng = nullptr;
@@ -1778,6 +1787,15 @@ int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes
     GF_HIP(hipSetDevice(fe->ctx->device));
     GF_HIP(hipStreamSynchronize(fe->ctx->stream));
     GF_HIP(hipMemcpy(fe->field_ptr[field], host, bytes, hipMemcpyHostToDevice));
+    if (field == GF_FE_MP_INFO) {  // keep the packed lower triangles the active matcher reads
+        const size_t n = bytes / (49 * sizeof(double));
+        const double* b = (const double*)host;
+        std::vector<double> lt(32 * n, 0.0);
+        for (size_t q = 0; q < n; q++)
+            for (int i = 0; i < 7; i++)
+                for (int j = 0; j <= i; j++) lt[32 * q + i * (i + 1) / 2 + j] = b[49 * q + 7 * i + j];
+        GF_HIP(hipMemcpy(fe->mp_info_lt, lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     if (field == GF_FE_MAP) {  // keep the float3 position copy the Jacobian kernels read
         const size_t n = bytes / sizeof(gf_map_point);
         const gf_map_point* m = (const gf_map_point*)host;

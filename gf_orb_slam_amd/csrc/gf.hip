@@ -246,6 +246,57 @@ __device__ __forceinline__ double logdet_sum_lower(const double* cur, const doub
     return 2 * log(v1 * v2);
 }
 
+// logdet_sum_lower on a packed lower triangle: lt[i (i + 1) / 2 + j] = b[7 i + j]
+// (the front end keeps this 256-B copy of every ObsMat beside the 49-entry
+// block: the Cholesky's 28 entries are then two cache lines, not the four the
+// full block's rows spread them over). The LU fallback reads the full b.
+__device__ __forceinline__ double logdet_sum_lower_packed(const double* cur, const double* lt, const double* b) {
+    double X[28];
+    const double* a = static_cast<const double*>(__builtin_assume_aligned(lt, 256));  // 32-double records
+#pragma unroll
+    for (int k = 0; k < 28; k++) X[k] = gfd::ldg(a + k);
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) X[i * (i + 1) / 2 + j] = cur[7 * i + j] + X[i * (i + 1) / 2 + j];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 7; j++) {
+        double s = X[j * (j + 1) / 2 + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) s -= X[j * (j + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
+        ok = ok && s > 0;
+        const double d = sqrt(s);
+        X[j * (j + 1) / 2 + j] = d;
+        const double rd = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 7; i++) {
+            double t = X[i * (i + 1) / 2 + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) t -= X[i * (i + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
+            X[i * (i + 1) / 2 + j] = t * rd;
+        }
+    }
+    if (!ok) return logdet_lu(cur, b, 1.0);
+    double v1 = 1, v2 = 1;  // Armadillo's two-accumulator product of the diagonal
+    v1 *= X[0];
+    v2 *= X[2];
+    v1 *= X[5];
+    v2 *= X[9];
+    v1 *= X[14];
+    v2 *= X[20];
+    v1 *= X[27];
+    return 2 * log(v1 * v2);
+}
+
+// the packed lower triangle of a 7x7 block (logdet_sum_lower_packed's layout)
+__device__ __forceinline__ void store_lower_packed(const double* M, double* lt) {
+#pragma unroll
+    for (int i = 0; i < 7; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) lt[i * (i + 1) / 2 + j] = M[7 * i + j];
+}
+
 // ------------------------------------------------------------- k_obs_info
 __global__ void k_obs_info(gf_obs_camera cam, const double* __restrict__ Xv, const float* __restrict__ pos,
                            const float* __restrict__ sigma2, const int32_t* __restrict__ n, int cap, int check_viz,
@@ -334,6 +385,7 @@ struct ActiveArgs {
     int32_t* ovf;              // two-pass launch: [0] = count, [1 + k] = k-th frame whose pool
                                // did not fit the first pass's LDS
     int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
+    const double* info_lt;     // null, or the packed lower triangles of info ([F][mp_cap][32])
     gf::ActiveClock ck;        // the front end's time cap (ck.mat_t0 null: none)
 };
 
@@ -660,12 +712,15 @@ __device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst&
 
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
+                           const double* info_lt,
                            const int32_t* rmp, const int* cell_start, const int* items, const int* claim,
                            const gf_keypoint* K, const uint8_t* D) {
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
-        C.score[c] = logdet_sum_lower(cur, info + 49LL * (rmp ? rmp[q] : q));
+        const long long qi = rmp ? rmp[q] : q;
+        C.score[c] = info_lt ? logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi)
+                             : logdet_sum_lower(cur, info + 49LL * qi);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
@@ -1039,6 +1094,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     bool nsucc_valid = true;        // s_nsucc counts the matchable pool slots
     int last_npop = 0;
     const double* info = A.info + (long long)f * A.mp_cap * 49;
+    const double* info_lt = A.info_lt ? A.info_lt + (long long)f * A.mp_cap * 32 : nullptr;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
 
@@ -1146,7 +1202,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, rmp, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K, D);
         evald = nc;
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
@@ -1184,7 +1240,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             if (rep < nc && rep >= evald) {
                 AM_T(4);
-                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, rmp, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K, D);
                 evald = nc;
                 AM_T(3);
             }
@@ -1731,7 +1787,8 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
                          const int32_t* d_m, int mp_cap, const double* d_base, const float* level_sigma2,
                          const int32_t* d_num_to_match, float th, float nnratio, gf_rng* d_rng, int32_t* d_kp2mp,
                          int32_t* d_score, int32_t* d_left, int32_t* d_nleft, int32_t* d_nmatched, int32_t* d_nldet,
-                         const int32_t* d_remap, void* stream, const gf::ActiveClock& ck) {
+                         const int32_t* d_remap, void* stream, const gf::ActiveClock& ck,
+                         const double* d_info_lt) {
     GF_CHECK(ctx && fi && level_sigma2, GF_ERR_ARG, "null arg");
     GF_CHECK(!ck.mat_t0 || (ck.viz && ck.rec), GF_ERR_ARG, "bad clock");
     GF_CHECK(kp_cap <= KP_MAX && mp_cap <= 32767, GF_ERR_UNSUPPORTED, "frame exceeds active-matching limits");
@@ -1748,6 +1805,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.mp_desc = d_mp_desc;
     A.updated = d_updated;
     A.info = d_info;
+    A.info_lt = d_info_lt;
     A.H = d_H;
     A.m = d_m;
     A.mp_cap = mp_cap;
@@ -2124,7 +2182,7 @@ __global__ void k_obs_frame_info(gf_obs_camera cam, const double* __restrict__ X
                                  const uint8_t* __restrict__ outl, const float* __restrict__ mpos,
                                  const int32_t* __restrict__ nmp, int map_stride, LevelTab sig, int nlevels,
                                  double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
-                                 const int32_t* __restrict__ remap) {
+                                 const int32_t* __restrict__ remap, double* __restrict__ info_lt) {
     const int f = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nkps[f]) return;
@@ -2145,6 +2203,7 @@ __global__ void k_obs_frame_info(gf_obs_camera cam, const double* __restrict__ X
     uv[2 * w + 1] = p[1];
     for (int e = 0; e < 14; e++) Hout[14 * w + e] = H[e];
     for (int e = 0; e < 49; e++) info[49 * w + e] = M[e];
+    if (info_lt) store_lower_packed(M, info_lt + 32 * w);
 }
 
 // batchInfoMat_Map (Observability.cc:556-644): skip points already updated
@@ -2156,7 +2215,7 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
                                const gf_mp_view* __restrict__ views, int32_t* __restrict__ upd_id, int frame_id,
                                double* __restrict__ Hout, double* __restrict__ info, float* __restrict__ uv,
                                uint8_t* __restrict__ updated_out, const int32_t* __restrict__ remap,
-                               gf::StageClock ck, const long long* __restrict__ cap2) {
+                               gf::StageClock ck, const long long* __restrict__ cap2, double* __restrict__ info_lt) {
     const int f = blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     bool late = false;
@@ -2189,6 +2248,7 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
             uv[2 * w + 1] = p[1];
             for (int e = 0; e < 14; e++) Hout[14 * w + e] = H[e];
             for (int e = 0; e < 49; e++) info[49 * w + e] = M[e];
+            if (info_lt) store_lower_packed(M, info_lt + 32 * w);
             u = frame_id;
             upd_id[g] = u;
         }
@@ -2246,7 +2306,7 @@ int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const
                        const gf_keypoint* d_kps, const int32_t* d_nkps, int kp_stride, const int32_t* d_kp2mp,
                        const uint8_t* d_outlier, const float* d_map_pos, const int32_t* d_nmp, int map_stride,
                        const float* level_sigma2, int nlevels, double* d_H, double* d_info, float* d_uv,
-                       const int32_t* d_remap, void* stream) {
+                       const int32_t* d_remap, void* stream, double* d_info_lt) {
     GF_CHECK(ctx && cam && level_sigma2, GF_ERR_ARG, "null arg");
     if (nframes <= 0 || kp_stride <= 0) return GF_OK;
     GF_CHECK(nlevels >= 1 && nlevels <= 16, GF_ERR_ARG, "nlevels out of range");
@@ -2258,7 +2318,7 @@ int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const
     GF_PROF(ctx, s, "k_obs_frame_info");
     GF_LAUNCH(k_obs_frame_info, dim3((kp_stride + 127) / 128, nframes), 128, 0, s, 
         *cam, d_Xv, d_kps, d_nkps, kp_stride, d_kp2mp, d_outlier, d_map_pos, d_nmp, map_stride, t, nlevels, d_H,
-        d_info, d_uv, d_remap);
+        d_info, d_uv, d_remap, d_info_lt);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -2266,7 +2326,8 @@ int gf::obs_frame_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const
 int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const double* d_Xv, const float* d_map_pos,
                      const int32_t* d_nmp, int map_stride, int check_viz, const gf_mp_view* d_views,
                      int32_t* d_upd_id, int frame_id, double* d_H, double* d_info, float* d_uv, uint8_t* d_updated,
-                     const int32_t* d_remap, void* stream, const gf::StageClock& ck, const long long* d_cap2) {
+                     const int32_t* d_remap, void* stream, const gf::StageClock& ck, const long long* d_cap2,
+                     double* d_info_lt) {
     GF_CHECK(ctx && cam, GF_ERR_ARG, "null arg");
     if (nframes <= 0 || map_stride <= 0) return GF_OK;
     GF_CHECK(d_Xv && d_map_pos && d_nmp && d_upd_id && d_H && d_info && d_uv, GF_ERR_ARG, "null arg");
@@ -2275,7 +2336,7 @@ int gf::obs_map_info(gf_ctx* ctx, const gf_obs_camera* cam, int nframes, const d
     GF_PROF(ctx, s, "k_obs_map_info");
     GF_LAUNCH(k_obs_map_info, dim3((map_stride + 127) / 128, nframes), 128, 0, s, 
         *cam, d_Xv, d_map_pos, d_nmp, map_stride, check_viz, d_views, d_upd_id, frame_id, d_H, d_info, d_uv, d_updated,
-        d_remap, ck, d_cap2);
+        d_remap, ck, d_cap2, d_info_lt);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
