@@ -687,8 +687,14 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
 #define SEL_THREADS 512
 #endif
 #define SEL_BUF 1024  // entries of wave 0's buffer (cell lists and the level list)
+// entries of the other waves' buffers (cell lists only). 512 since r04: the
+// workgroup's LDS drops from 77 to 49 KB, so it fits beside the tracking
+// kernels' workgroups (k_select 0.46 -> 0.38 ms per launch in the step,
+// 101.1-101.8k -> 101.4-102.4k frames/s, profiles/r04/ab8_*.json, ab9_*.json);
+// the rare cell list above 512 entries that needs a cut waits for wave 0's
+// 1024-entry buffer (exact either way; the c256 build's tests cover it)
 #ifndef SEL_BUF_CELL
-#define SEL_BUF_CELL 1024  // entries of the other waves' buffers (cell lists only)
+#define SEL_BUF_CELL 512
 #endif
 // one wave's LDS list and partition scratch; wave 0's is SEL_BUF long, the
 // others' SEL_BUF_CELL (a cell's corners after NMS rarely pass 100), so the
