@@ -539,6 +539,9 @@ def main():
                     help="stream groups per GPU, each a front end on its own HIP stream (their kernels overlap; 4 x 256 measured best in r03: 95.9k vs 89.5k frames/s for 2 x 512)")
     ap.add_argument("--no-gate", action="store_true",
                     help="let the groups' extraction stages overlap (default: chained, one at a time)")
+    ap.add_argument("--gate-stage", type=int, default=None,
+                    help="extraction stage after which the gate releases the next group (0 resize .. 4 describe; "
+                         "default: the library's, after describe)")
     ap.add_argument("--track-priority", action="store_true",
                     help="each group's tracking kernels on a high-priority stream of their own "
                          "(gf_frontend_set_track_priority; measured slower on MI355X: 70k vs 89k frames/s)")
@@ -678,6 +681,9 @@ def main():
         fe.bootstrap(T[sl], V[sl], 0.0)
         fes.append(fe)
     gates = [] if args.no_gate else chain_extraction(fes)
+    if args.gate_stage is not None and gates:
+        for fe in fes:
+            fe.set_gate_stage(args.gate_stage)
     if args.track_priority and G > 1:
         for fe in fes:
             fe.set_track_priority(-100)  # the device's most urgent priority
