@@ -28,6 +28,9 @@
 #include "select.h"
 
 #define POOL_MAX 4096
+#ifndef AM_CAND_CAP
+#define AM_CAND_CAP 384  // first-pass capacity for a round's drawn candidates
+#endif
 #ifndef AM_SMALL_POOL
 #define AM_SMALL_POOL 1280  // first-pass pool capacity of the two-pass active match (multiple of 64)
 #endif
@@ -382,6 +385,7 @@ struct ActiveArgs {
     int* grid_cs;              // [F][NCELLS + 1] keypoint grid CSR (written by k_onepoint_pre)
     int* grid_items;           // [F][kp_cap]
     int pool_cap;              // LDS pool capacity of this launch (<= POOL_MAX)
+    int cand_cap;              // LDS capacity for a round's drawn candidates (<= pool_cap)
     int32_t* ovf;              // two-pass launch: [0] = count, [1 + k] = k-th frame whose pool
                                // did not fit the first pass's LDS
     int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
@@ -954,23 +958,28 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     // sized for this launch: PC = pool capacity (map-list capacity rounded to 64,
     // at most POOL_MAX), claims for kp_cap keypoints
     const int PC = A.pool_cap;
-    double* c_score = (double*)smem;                                       // PC
-    unsigned long long* pbits = (unsigned long long*)(c_score + PC);       // 64
+    // CC: a round's drawn candidates (sz + pops + the last batch's spare
+    // draws, usually ~100); a frame whose round would draw past CC returns
+    // before writing its outputs and the overflow pass redoes it (as a pool
+    // past PC does)
+    const int CC = A.cand_cap;
+    double* c_score = (double*)smem;                                       // CC
+    unsigned long long* pbits = (unsigned long long*)(c_score + CC);       // 64
     int* claim = (int*)(pbits + 64);                                       // kp_cap
     int* ppre = claim + A.kp_cap;                                          // 65 (+3 pad)
-    int32_t* c_tries = ppre + 68;                                          // PC
-    int16_t* lmk = (int16_t*)(c_tries + PC);                               // PC: map point of each slot
+    int32_t* c_tries = ppre + 68;                                          // CC
+    int16_t* lmk = (int16_t*)(c_tries + CC);                               // PC: map point of each slot
     int16_t* vis = lmk + PC;                                               // PC: lmkVisited per slot
-    int16_t* c_slot = vis + PC;                                            // PC
-    int16_t* c_match = c_slot + PC;                                        // PC
-    int16_t* c_dist = c_match + PC;                                        // PC
-    int16_t* rheap = c_dist + PC;                                          // PC: replay heap
+    int16_t* c_slot = vis + PC;                                            // CC
+    int16_t* c_match = c_slot + CC;                                        // CC
+    int16_t* c_dist = c_match + CC;                                        // CC
+    int16_t* rheap = c_dist + CC;                                          // PC: replay heap
     int16_t* sm_match = rheap + PC;                                        // PC: one-point state per slot
     int16_t* sm_dist = sm_match + PC;                                      // PC
     int16_t* sm_h1 = sm_dist + PC;                                         // PC
     int16_t* sm_h2 = sm_h1 + PC;                                           // PC
     int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
-    uint8_t* c_alive = (uint8_t*)(alv + PC);                               // PC
+    uint8_t* c_alive = (uint8_t*)(alv + PC);                               // CC
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
@@ -1008,6 +1017,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         }
     }
     bool cut = false;
+    bool cabort = false;  // a round would draw past CC: the overflow pass redoes the frame
     // the keypoint grid comes from k_onepoint_pre (HBM; only rescans read it)
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
@@ -1180,6 +1190,10 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             break;
         }
         while (nc < sz && exh_at < 0) {
+            if (CC < N && nc + 64 > CC) {  // the batch could write past the candidate arrays
+                cabort = true;
+                break;
+            }
             if (lane == 0) s_exh = -1;
             __syncthreads();
             {
@@ -1195,6 +1209,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             exh_at = __builtin_amdgcn_readfirstlane(s_exh);
         }
         AM_T(2);
+        if (cabort) break;
         if (nc < sz) {  // the initial subset could not be completed
             nld += nc;
             for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
@@ -1222,6 +1237,10 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             if (rep >= nc && exh_at < 0) {
                 AM_T(4);
                 while (rep >= nc && exh_at < 0) {
+                    if (CC < N && nc + 64 > CC) {  // past the candidate arrays: the overflow pass takes the frame
+                        cabort = true;
+                        break;
+                    }
                     if (lane == 0) s_exh = -1;
                     __syncthreads();
                     {
@@ -1293,6 +1312,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     }
                     const int rep = sz + npop;  // the replacement draw
                     draw_eval(rep);
+                    if (cabort) return 1;
                     if (rep >= nc) {
                         exh = true;
                         lc = lane == tl ? -1 : lc;  // the top was popped
@@ -1348,6 +1368,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 }
                 const int rep = sz + npop;  // the replacement draw
                 draw_eval(rep);
+                if (cabort) return 1;
                 if (rep >= nc) {
                     exh = true;
                     break;
@@ -1449,6 +1470,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (lane == 0) C.alive[top] = 0;  // heapSubset.pop()
                 const int rep = sz + npop;       // the replacement draw
                 draw_eval(rep);
+                if (cabort) break;
                 if (rep >= nc) {
                     exh = true;
                     break;
@@ -1462,6 +1484,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
         }
         AM_T(4);
+        if (cabort) break;
         // the successful top's H row and its keypoint's octave, loaded now so
         // that their latency overlaps the commit below
         double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
@@ -1519,6 +1542,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         __syncthreads();
         AM_T(6);
     }
+    if (cabort) {  // (the scores written at this attempt's claims are the redo's too: same arithmetic)
+        if (lane == 0) {
+            if (A.pass == 1) A.ovf[1 + atomicAdd(A.ovf, 1)] = f;
+            else A.err[f] = 3;
+        }
+        return;
+    }
     // ---- outputs: claims, left-over pool (alive slots in order), RNG state
     for (int i = lane; i < n; i += AW) kp2mp[i] = claim[i];
     if (cut) N = 0;
@@ -1555,9 +1585,9 @@ __global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
 
 #undef AM_T
 
-size_t active_lds_bytes(int pool_cap, int kp_cap) {
-    return sizeof(double) * pool_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) +
-           sizeof(int32_t) * pool_cap + sizeof(int16_t) * 11 * (size_t)pool_cap + pool_cap;
+size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap) {
+    return sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) + sizeof(int32_t) * cand_cap +
+           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap;
 }
 
 // ------------------------------------------------------------- max-volume selection
@@ -1860,36 +1890,42 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     }
     const int full_pc = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
     static unsigned long long ovf_mask = 0;
-    if ((rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, KP_MAX), &mask)) ||
-        (rc = set_lds_attr(ctx, (const void*)k_active_match_overflow, active_lds_bytes(POOL_MAX, KP_MAX), &ovf_mask)))
+    if ((rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX), &mask)) ||
+        (rc = set_lds_attr(ctx, (const void*)k_active_match_overflow, active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX),
+                           &ovf_mask)))
         return rc;
     // Two passes when the map list is long: most frames' pools (in-view, updated
     // points) are far below the list capacity, and a smaller LDS footprint lets
     // more workgroups of the concurrently running kernels share each CU. Frames
     // whose pool does not fit return before writing anything and are redone by
     // the overflow pass with the full capacity.
-    A.pool_cap = full_pc;
+    A.pool_cap = A.cand_cap = full_pc;
     A.pass = 0;
     A.ovf = nullptr;
-    if (full_pc > AM_SMALL_POOL) {
+    // with a time budget the candidate arrays stay full size (an attempt cut
+    // short by them would have spent clock time the redo does not see)
+    const int cand_small = ck.mat_t0 ? std::min(full_pc, AM_SMALL_POOL) : std::min(full_pc, AM_CAND_CAP);
+    if (full_pc > AM_SMALL_POOL || cand_small < full_pc) {
         void* ovf;
         if ((rc = gf::ws_get(ctx, 39, sizeof(int32_t) * (nframes + 1), &ovf))) return rc;
         GF_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));
         A.ovf = (int32_t*)ovf;
-        A.pool_cap = AM_SMALL_POOL;
+        A.pool_cap = std::min(full_pc, AM_SMALL_POOL);
+        A.cand_cap = cand_small;
         A.pass = 1;
     }
     {
         GF_PROF(ctx, s, "k_active_match");
-        GF_LAUNCH(k_active_match, nframes, AW, active_lds_bytes(A.pool_cap, kp_cap), s, A);
+        GF_LAUNCH(k_active_match, nframes, AW, active_lds_bytes(A.pool_cap, A.cand_cap, kp_cap), s, A);
         GF_HIP(hipGetLastError());
     }
     if (A.pass == 1) {
-        A.pool_cap = full_pc;
+        A.pool_cap = A.cand_cap = full_pc;
         A.pass = 2;
         GF_PROF(ctx, s, "k_active_match_overflow");
         // few workgroups: the full pool's LDS is only claimed where a frame needs it
-        GF_LAUNCH(k_active_match_overflow, std::min(nframes, AM_OVF_GRID), AW, active_lds_bytes(full_pc, kp_cap), s, A);
+        GF_LAUNCH(k_active_match_overflow, std::min(nframes, AM_OVF_GRID), AW,
+                  active_lds_bytes(full_pc, full_pc, kp_cap), s, A);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
