@@ -28,8 +28,11 @@
 #include "select.h"
 
 #define POOL_MAX 4096
+#ifndef AM_ONE_PASS_MAX
+#define AM_ONE_PASS_MAX 64  // batches up to this size take the one-pass launch
+#endif
 #ifndef AM_CAND_CAP
-#define AM_CAND_CAP 384  // first-pass capacity for a round's drawn candidates
+#define AM_CAND_CAP 640  // first-pass capacity for a round's drawn candidates
 #endif
 #ifndef AM_SMALL_POOL
 #define AM_SMALL_POOL 1280  // first-pass pool capacity of the two-pass active match (multiple of 64)
@@ -1905,7 +1908,9 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     // with a time budget the candidate arrays stay full size (an attempt cut
     // short by them would have spent clock time the redo does not see)
     const int cand_small = ck.mat_t0 ? std::min(full_pc, AM_SMALL_POOL) : std::min(full_pc, AM_CAND_CAP);
-    if (full_pc > AM_SMALL_POOL || cand_small < full_pc) {
+    // (a small batch runs one pass at full capacity: the LDS is free, and a
+    // redone frame would double a single sequence's latency)
+    if (nframes > AM_ONE_PASS_MAX && (full_pc > AM_SMALL_POOL || cand_small < full_pc)) {
         void* ovf;
         if ((rc = gf::ws_get(ctx, 39, sizeof(int32_t) * (nframes + 1), &ovf))) return rc;
         GF_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), s));

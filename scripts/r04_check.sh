@@ -8,6 +8,7 @@ mkdir -p $R/gpurun_out
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || exit 10
 GF_LIB=$R/gf_orb_slam_amd/diag/libgfslam_c256.so timeout -k 10 200 python -u -m pytest tests/test_extract_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_c256_$TAG.log 2>&1 || exit 14
+GF_LIB=$R/gf_orb_slam_amd/diag/libgfslam_am2p.so timeout -k 10 600 python -u -m pytest tests/test_gf_gpu.py tests/test_pipeline_gpu.py -m gpu -x -v --timeout 500 --timeout-method thread > gpurun_out/pytest_am2p_$TAG.log 2>&1 || exit 15
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit 13
 timeout -k 10 600 python bench.py ${BENCH_ARGS} --kernel-trace-dir $R/gpurun_out/ktrace_$TAG > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 11
 export TMPDIR=/tmp
