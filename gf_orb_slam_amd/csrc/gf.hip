@@ -38,7 +38,7 @@
 #define AM_SMALL_POOL 1280  // first-pass pool capacity of the two-pass active match (multiple of 64)
 #endif
 #ifndef AM_OVF_GRID
-#define AM_OVF_GRID 64  // workgroups of the overflow pass
+#define AM_OVF_GRID 256  // workgroups of the overflow pass (at most)
 #endif
 #define GF_THREADS 256
 #define MAX_RANDOM_QUERY_TIME 2000
@@ -1928,7 +1928,10 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
         A.pool_cap = A.cand_cap = full_pc;
         A.pass = 2;
         GF_PROF(ctx, s, "k_active_match_overflow");
-        // few workgroups: the full pool's LDS is only claimed where a frame needs it
+        // a workgroup per listed frame up to AM_OVF_GRID (the ones past the
+        // list's count exit at once): with long maps (config 3) every frame's
+        // pool is past the first pass's, and 64 workgroups walked 256 frames
+        // four deep (7.7 ms of the step)
         GF_LAUNCH(k_active_match_overflow, std::min(nframes, AM_OVF_GRID), AW,
                   active_lds_bytes(full_pc, full_pc, kp_cap), s, A);
         GF_HIP(hipGetLastError());
