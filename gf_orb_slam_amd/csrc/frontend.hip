@@ -1133,7 +1133,9 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     {
         void* lt = nullptr;
         if ((rc = fe_alloc(fe, sizeof(double) * (size_t)B * M * 32, &lt))) return bail(rc);
+#ifndef GF_NO_PACKED_INFO
         fe->mp_info_lt = (double*)lt;
+#endif
     }
     F(GF_FE_MP_UV, float, (size_t)B * M * 2, fe->mp_uv);
     F(GF_FE_MP_UPD, int32_t, (size_t)B * M, D.upd);
