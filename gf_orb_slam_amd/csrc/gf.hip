@@ -208,54 +208,14 @@ __device__ double logdet_sum(const double* a, const double* b, double sign) {
     return 2 * log(v1 * v2);
 }
 
-// logdet_sum(cur, b, +1) reading only what its Cholesky branch reads: b's
-// lower triangle (28 of 49 entries, through the global address space), the
-// factor formed in place, the same arithmetic entry for entry; a matrix that
-// is not positive definite takes logdet_sum's LU fallback on the full b.
-__device__ __forceinline__ double logdet_sum_lower(const double* cur, const double* b) {
-    double X[28];
-#pragma unroll
-    for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) X[i * (i + 1) / 2 + j] = gfd::ldg(b + 7 * i + j);
-#pragma unroll
-    for (int i = 0; i < 7; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) X[i * (i + 1) / 2 + j] = cur[7 * i + j] + X[i * (i + 1) / 2 + j];
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-        double s = X[j * (j + 1) / 2 + j];
-#pragma unroll
-        for (int k = 0; k < j; k++) s -= X[j * (j + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
-        ok = ok && s > 0;
-        const double d = sqrt(s);
-        X[j * (j + 1) / 2 + j] = d;
-        const double rd = 1.0 / d;
-#pragma unroll
-        for (int i = j + 1; i < 7; i++) {
-            double t = X[i * (i + 1) / 2 + j];
-#pragma unroll
-            for (int k = 0; k < j; k++) t -= X[i * (i + 1) / 2 + k] * X[j * (j + 1) / 2 + k];
-            X[i * (i + 1) / 2 + j] = t * rd;
-        }
-    }
-    if (!ok) return logdet_lu(cur, b, 1.0);
-    double v1 = 1, v2 = 1;  // Armadillo's two-accumulator product of the diagonal
-    v1 *= X[0];
-    v2 *= X[2];
-    v1 *= X[5];
-    v2 *= X[9];
-    v1 *= X[14];
-    v2 *= X[20];
-    v1 *= X[27];
-    return 2 * log(v1 * v2);
-}
 
-// logdet_sum_lower on a packed lower triangle: lt[i (i + 1) / 2 + j] = b[7 i + j]
-// (the front end keeps this 256-B copy of every ObsMat beside the 49-entry
-// block: the Cholesky's 28 entries are then two cache lines, not the four the
-// full block's rows spread them over). The LU fallback reads the full b.
+// logdet_sum(cur, b) (the summed block's logdet) for a matrix the Cholesky
+// accepts, reading b's lower triangle from its packed record lt[i (i + 1) / 2
+// + j] = b[7 i + j] (kept beside every ObsMat: the Cholesky's 28 entries are
+// then two cache lines, not the four the full block's rows spread them over);
+// the factor is formed in place, the same arithmetic entry for entry as the
+// reference's; a matrix that is not positive definite takes logdet_sum's LU
+// fallback on the full b.
 __device__ __forceinline__ double logdet_sum_lower_packed(const double* cur, const double* lt, const double* b) {
     double X[28];
     const double* a = static_cast<const double*>(__builtin_assume_aligned(lt, 256));  // 32-double records
@@ -301,6 +261,16 @@ __device__ __forceinline__ void store_lower_packed(const double* M, double* lt) 
     for (int i = 0; i < 7; i++)
 #pragma unroll
         for (int j = 0; j <= i; j++) lt[i * (i + 1) / 2 + j] = M[7 * i + j];
+}
+
+// The packed records of [F][cap] information blocks, for callers of the
+// active matcher that keep only the full blocks (the C-ABI entry points).
+__global__ __launch_bounds__(256) void k_pack_info(const double* __restrict__ info, int cap,
+                                                   double* __restrict__ lt) {
+    const int q = blockIdx.x * 256 + threadIdx.x, f = blockIdx.y;
+    if (q >= cap) return;
+    const size_t g = (size_t)f * cap + q;
+    store_lower_packed(info + 49 * g, lt + 32 * g);
 }
 
 // ------------------------------------------------------------- k_obs_info
@@ -726,8 +696,7 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
         const int sl = C.slot[c];
         const int q = lmk[sl];
         const long long qi = rmp ? rmp[q] : q;
-        C.score[c] = info_lt ? logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi)
-                             : logdet_sum_lower(cur, info + 49LL * qi);
+        C.score[c] = logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
@@ -1107,7 +1076,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     bool nsucc_valid = true;        // s_nsucc counts the matchable pool slots
     int last_npop = 0;
     const double* info = A.info + (long long)f * A.mp_cap * 49;
-    const double* info_lt = A.info_lt ? A.info_lt + (long long)f * A.mp_cap * 32 : nullptr;
+    const double* info_lt = A.info_lt + (long long)f * A.mp_cap * 32;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
 
@@ -1838,6 +1807,17 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.mp_desc = d_mp_desc;
     A.updated = d_updated;
     A.info = d_info;
+    if (!d_info_lt) {  // the packed records the matcher reads, built here
+        void* lt = nullptr;
+        int rc0 = gf::ws_get(ctx, 20, sizeof(double) * 32 * (size_t)nframes * std::max(mp_cap, 1), &lt);
+        if (rc0) return rc0;
+        if (mp_cap > 0) {
+            GF_PROF(ctx, s, "k_pack_info");
+            GF_LAUNCH(k_pack_info, dim3((mp_cap + 255) / 256, nframes), 256, 0, s, d_info, mp_cap, (double*)lt);
+            GF_HIP(hipGetLastError());
+        }
+        d_info_lt = (const double*)lt;
+    }
     A.info_lt = d_info_lt;
     A.H = d_H;
     A.m = d_m;
