@@ -28,6 +28,9 @@
 #include "select.h"
 
 #define POOL_MAX 4096
+#ifndef AM_CC
+#define AM_CC 1  // first-pass candidate arrays apart from the pool (0: sized with it, no abort checks)
+#endif
 #ifndef AM_ONE_PASS_MAX
 #define AM_ONE_PASS_MAX 64  // batches up to this size take the one-pass launch
 #endif
@@ -934,7 +937,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     // draws, usually ~100); a frame whose round would draw past CC returns
     // before writing its outputs and the overflow pass redoes it (as a pool
     // past PC does)
+#if AM_CC
     const int CC = A.cand_cap;
+#else
+    const int CC = PC;
+#endif
     double* c_score = (double*)smem;                                       // CC
     unsigned long long* pbits = (unsigned long long*)(c_score + CC);       // 64
     int* claim = (int*)(pbits + 64);                                       // kp_cap
@@ -1162,7 +1169,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             break;
         }
         while (nc < sz && exh_at < 0) {
-            if (CC < N && nc + 64 > CC) {  // the batch could write past the candidate arrays
+            if (AM_CC && CC < N && nc + 64 > CC) {  // the batch could write past the candidate arrays
                 cabort = true;
                 break;
             }
@@ -1209,7 +1216,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             if (rep >= nc && exh_at < 0) {
                 AM_T(4);
                 while (rep >= nc && exh_at < 0) {
-                    if (CC < N && nc + 64 > CC) {  // past the candidate arrays: the overflow pass takes the frame
+                    if (AM_CC && CC < N && nc + 64 > CC) {
+                        // past the candidate arrays: no draw, so the pop loop
+                        // ends as on exhausted draws (no claim, no global write
+                        // follows) and the round loop stops at the check after
+                        // it; the overflow pass takes the frame
                         cabort = true;
                         break;
                     }
@@ -1284,7 +1295,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     }
                     const int rep = sz + npop;  // the replacement draw
                     draw_eval(rep);
-                    if (cabort) return 1;
                     if (rep >= nc) {
                         exh = true;
                         lc = lane == tl ? -1 : lc;  // the top was popped
@@ -1340,7 +1350,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 }
                 const int rep = sz + npop;  // the replacement draw
                 draw_eval(rep);
-                if (cabort) return 1;
                 if (rep >= nc) {
                     exh = true;
                     break;
@@ -1442,7 +1451,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (lane == 0) C.alive[top] = 0;  // heapSubset.pop()
                 const int rep = sz + npop;       // the replacement draw
                 draw_eval(rep);
-                if (cabort) break;
                 if (rep >= nc) {
                     exh = true;
                     break;
@@ -1887,7 +1895,7 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     A.ovf = nullptr;
     // with a time budget the candidate arrays stay full size (an attempt cut
     // short by them would have spent clock time the redo does not see)
-    const int cand_small = ck.mat_t0 ? std::min(full_pc, AM_SMALL_POOL) : std::min(full_pc, AM_CAND_CAP);
+    const int cand_small = (ck.mat_t0 || !AM_CC) ? std::min(full_pc, AM_SMALL_POOL) : std::min(full_pc, AM_CAND_CAP);
     // (a small batch runs one pass at full capacity: the LDS is free, and a
     // redone frame would double a single sequence's latency)
     if (nframes > AM_ONE_PASS_MAX && (full_pc > AM_SMALL_POOL || cand_small < full_pc)) {
