@@ -28,8 +28,13 @@
 #include "select.h"
 
 #define POOL_MAX 4096
+// AM_CC 1: the first pass's candidate arrays apart from its pool (AM_CAND_CAP
+// entries; a frame whose round would draw past them is redone by the overflow
+// pass). Off by default: the LDS it saves (50.7 -> 38.6 KB) did not move the
+// headline, and the extra state slowed one frame's pop chain by a fifth
+// (single sequence 1.28 -> 1.40 ms, profiles/r04/sp2_*.json).
 #ifndef AM_CC
-#define AM_CC 1  // first-pass candidate arrays apart from the pool (0: sized with it, no abort checks)
+#define AM_CC 0
 #endif
 #ifndef AM_ONE_PASS_MAX
 #define AM_ONE_PASS_MAX 64  // batches up to this size take the one-pass launch

@@ -121,8 +121,8 @@ def test_active_matching_two_pass_launch(nmp, frac):
     untouched and are redone by the overflow pass (gf.hip obs_active_match).
     Batches up to AM_ONE_PASS_MAX frames take one full-capacity pass, so the
     two-pass launch of this single frame runs in the diagnostic build
-    libgfslam_am2p (AM_ONE_PASS_MAX=0, AM_CAND_CAP=96: also most rounds past
-    the first pass's candidate arrays; scripts/r04_check.sh runs it)."""
+    libgfslam_am2p (AM_ONE_PASS_MAX=0, AM_CC=1, AM_CAND_CAP=96: also most rounds
+    past the first pass's candidate arrays; scripts/r04_check.sh runs it)."""
     case = _active_case(21 + nmp, nmp=nmp, num_to_match=100, frac_updated=frac)
     views, updated = case[3], case[8]
     pool = int((views["in_view"].astype(bool) & updated.astype(bool)).sum())
