@@ -586,6 +586,10 @@ def main():
     ap.add_argument("--kernel-trace-dir", default=None,
                     help="keep the rocprofv3 child's files (kernel trace, --stats summary, the timed region's "
                          "kernel_stats_timed.csv) in this directory")
+    ap.add_argument("--enqueue", choices=("step", "split", "ring"), default="step",
+                    help="host launch order of a step over the stream groups: each group's whole step in turn "
+                         "(step), every group's extraction before any tracking (split, pipeline.step_all), or "
+                         "group g's extraction before g - 1's tracking (ring, pipeline.GatedRing)")
     ap.add_argument("--kernels-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-reloc", action="store_true",
                     help="no keyframe databases: a lost stream stays LOST (the step then skips the BoW / candidate "
@@ -625,7 +629,7 @@ def main():
     from gf_orb_slam_amd.bow import ORBVocabulary
     from gf_orb_slam_amd.dist import GfDist, checksum, share_world
     from gf_orb_slam_amd.orb import Context
-    from gf_orb_slam_amd.pipeline import CK, STATS, TR, FrontEnd, KeyframeDB, chain_extraction
+    from gf_orb_slam_amd.pipeline import CK, STATS, TR, FrontEnd, KeyframeDB, chain_extraction, GatedRing, step_all
 
     cam = args.camera
     refmap = not args.fixed_map
@@ -700,9 +704,16 @@ def main():
     # ---- warm-up
     hist = np.zeros(6, np.int64)
     lost = 0
+    ring = GatedRing(fes) if args.enqueue == "ring" else None
     for _ in range(args.warmup):
-        for fe in fes:
-            fe.step()
+        if ring is not None:
+            ring.step()
+            ring.finish()
+        elif args.enqueue == "split":
+            step_all(fes)
+        else:
+            for fe in fes:
+                fe.step()
         for fe in fes:
             st = fe.read("stats")
             hist += np.bincount(st[STATS.index("branch")], minlength=6)[:6]
@@ -716,10 +727,30 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    t_call = np.zeros((args.steps, G))  # host seconds inside each gf_frontend_step (enqueue only)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        for fe in fes:
-            fe.step()
+    for k in range(args.steps):
+        if args.enqueue == "split":
+            for g, fe in enumerate(fes):
+                tc = time.perf_counter()
+                fe.step_extract()
+                t_call[k, g] = time.perf_counter() - tc
+            for g, fe in enumerate(fes):
+                tc = time.perf_counter()
+                fe.step_track()
+                t_call[k, g] += time.perf_counter() - tc
+        elif args.enqueue == "ring":
+            tc = time.perf_counter()
+            ring.step()
+            t_call[k, :] = (time.perf_counter() - tc) / G
+        else:
+            for g, fe in enumerate(fes):
+                tc = time.perf_counter()
+                fe.step()
+                t_call[k, g] = time.perf_counter() - tc
+    if ring is not None:
+        ring.finish()
+    t_enq = time.perf_counter() - t0
     for fe in fes:
         fe.sync()
     torch.cuda.synchronize()
@@ -927,10 +958,15 @@ def main():
                                f"(FRAME_INFO, isInFrustum, MAP_INFO, runActiveMapMatching), PoseOptimization, "
                                f"motion update, next-frame MAP_INFO prediction, SearchAdditionalMatchesInFrame",
                    "sequences_per_gpu": B, "stream_groups": G, "update_reference": refmap,
-                   "extraction_gate": bool(gates),
+                   "extraction_gate": bool(gates), "enqueue": args.enqueue,
                    "tracking_stream_priority": bool(args.track_priority and G > 1),
                    "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
         "startup": startup,
+        "host_enqueue": {"ms_per_step": round(t_enq / args.steps * 1e3, 3),
+                         "call_ms_avg": [round(float(x) * 1e3, 3) for x in t_call.mean(axis=0)],
+                         "call_ms_max": round(float(t_call.max()) * 1e3, 3),
+                         "note": "host time inside gf_frontend_step per group (launches only): close to "
+                                 "ms_per_step means the host, not the GPU, paces the steps"},
         "roofline": roof,
         "pose_opt": {"ms_per_iter": round(pose_avg_ms / max(mean_iters, 1e-9), 5),
                      "avg_launch_ms": round(pose_avg_ms, 4), "mean_iterations": round(mean_iters, 2),

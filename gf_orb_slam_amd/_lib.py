@@ -157,6 +157,8 @@ _PROTOS = {
     "gf_reloc_candidates": [_P, _P, _P, _I, _P, _P, _P, _P, ctypes.c_uint32, _P, _P, _P],
     "gf_frontend_bootstrap": [_P, _P, _P, _D],
     "gf_frontend_step": [_P],
+    "gf_frontend_step_extract": [_P],
+    "gf_frontend_step_track": [_P],
     "gf_update_reference": [_P, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P],
     "gf_update_reference_dev": [_P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P, _I, _P, _P],
     "gf_frontend_set_gate": [_P, _P, _P],

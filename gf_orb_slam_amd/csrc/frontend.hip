@@ -769,6 +769,7 @@ struct gf_frontend {
     bool sourced = false;
     // extraction gate (gf_frontend_set_gate): caller-owned events
     hipEvent_t gate_wait = nullptr, gate_done = nullptr;
+    bool extracted = false;  // gf_frontend_step_extract ran, gf_frontend_step_track not yet
     int gate_stage = 4;
     // tracking stream (gf_frontend_set_track_priority): the kernels after
     // extraction run on ts, joined back into the context's stream at the end
@@ -846,26 +847,32 @@ int fe_undistort(gf_frontend* fe, hipStream_t s) {
     return gf_undistort_keypoints_dev(fe->ctx, fe->D.B, K, fe->p.dist, fe->D.kps, fe->D.nkp, fe->D.cap, fe->D.kps, s);
 }
 
-// The tracking step after the frame source pointers are set.
-int fe_track(gf_frontend* fe, hipStream_t s) {
+// The step's first part: the extraction gate, Frame construction (ORB
+// extraction, undistortion).
+int fe_extract(gf_frontend* fe, hipStream_t s) {
+    FeDev& D = fe->D;
+    // the frame's clock starts after the extraction gate: waiting behind the
+    // other front ends' extraction is not this frame's time
+    if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
+    {
+        GF_PROF(fe->ctx, s, "k_fe_begin");
+        GF_LAUNCH(k_fe_begin, D.B, 256, 0, s, D);
+        GF_HIP(hipGetLastError());
+    }
+    FE_RC(gf_orb_extract_ptrs_dev(fe->ex, D.B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp,
+                                  D.cap, s));
+    if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
+    return fe_undistort(fe, s);
+}
+
+// The step's second part: tracking on the extracted frame.
+int fe_track_frame(gf_frontend* fe, hipStream_t s) {
     gf_ctx* ctx = fe->ctx;
     FeDev& D = fe->D;
     const int B = D.B, cap = D.cap, M = D.M;
     const gf_frame_info* fi = &fe->fi;
     int32_t* st = D.stats;
     auto col = [&](int c) { return st + (size_t)c * B; };
-    // the frame's clock starts after the extraction gate: waiting behind the
-    // other front ends' extraction is not this frame's time
-    if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
-    {
-        GF_PROF(ctx, s, "k_fe_begin");
-        GF_LAUNCH(k_fe_begin, B, 256, 0, s, D);
-        GF_HIP(hipGetLastError());
-    }
-    FE_RC(gf_orb_extract_ptrs_dev(fe->ex, B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp, cap,
-                                  s));
-    if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
-    FE_RC(fe_undistort(fe, s));
     const hipStream_t s_ctx = s;
     if (fe->ts) {  // fork: tracking on the prioritised stream
         GF_HIP(hipEventRecord(fe->ev_extracted, s));
@@ -1029,6 +1036,12 @@ int fe_track(gf_frontend* fe, hipStream_t s) {
         GF_HIP(hipStreamWaitEvent(s_ctx, fe->ev_tracked, 0));
     }
     return GF_OK;
+}
+
+// The tracking step after the frame source pointers are set.
+int fe_track(gf_frontend* fe, hipStream_t s) {
+    FE_RC(fe_extract(fe, s));
+    return fe_track_frame(fe, s);
 }
 
 }  // namespace
@@ -1680,6 +1693,7 @@ static int fe_check_covis(gf_frontend* fe) {
 
 int gf_frontend_step(gf_frontend* fe) {
     GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
     GF_CHECK(fe->sourced || fe->D.src_mode == 2, GF_ERR_ARG, "no frame source set");
     FE_RC(fe_check_covis(fe));
     GF_HIP(hipSetDevice(fe->ctx->device));
@@ -1698,6 +1712,29 @@ int gf_frontend_step(gf_frontend* fe) {
     fe->D.match_ticks = mt;
     fe->D.select_ticks = stt;
     return fe_track(fe, fe->ctx->stream);
+}
+
+int gf_frontend_step_extract(gf_frontend* fe) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(fe->sourced || fe->D.src_mode == 2, GF_ERR_ARG, "no frame source set");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "a captured front end steps as one graph (gf_frontend_step)");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
+    FE_RC(fe_check_covis(fe));
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    auto ticks = [](double s) -> long long { return std::isfinite(s) && s >= 0 ? (long long)(s * 1e8) : -1; };
+    fe->D.match_ticks = ticks(fe->ctx->match_budget_s);
+    fe->D.select_ticks = ticks(fe->ctx->select_budget_s);
+    FE_RC(fe_extract(fe, fe->ctx->stream));
+    fe->extracted = true;
+    return GF_OK;
+}
+
+int gf_frontend_step_track(gf_frontend* fe) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(fe->extracted, GF_ERR_ARG, "no extracted frame (gf_frontend_step_extract first)");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    fe->extracted = false;
+    return fe_track_frame(fe, fe->ctx->stream);
 }
 
 int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {

@@ -138,6 +138,42 @@ class GateEvent:
             pass
 
 
+def step_all(fes: list) -> None:
+    """One step of every front end, from one host thread: every extraction
+    is enqueued before any tracking, so a gated front end's extraction is
+    never queued behind the host's launches of another's tracking."""
+    for fe in fes:
+        fe.step_extract()
+    for fe in fes:
+        fe.step_track()
+
+
+class GatedRing:
+    """Steps gated front ends (chain_extraction) from one host thread in the
+    launch order that keeps the gate's hand-over short: front end g's
+    extraction is enqueued right after g - 1's, before g - 1's tracking, and
+    the last front end's tracking is held until the next step's first
+    extraction is enqueued (call finish() before reading results)."""
+
+    def __init__(self, fes: list):
+        self.fes = list(fes)
+        self._held = None  # the front end whose tracking is not enqueued yet
+
+    def step(self) -> None:
+        prev = self._held
+        for fe in self.fes:
+            fe.step_extract()
+            if prev is not None:
+                prev.step_track()
+            prev = fe
+        self._held = prev
+
+    def finish(self) -> None:
+        if self._held is not None:
+            self._held.step_track()
+            self._held = None
+
+
 def chain_extraction(fes: list) -> list:
     """Gate the front ends' extraction stages into a ring: front end g waits
     for g - 1's extraction (g = 0 for the last one's, previous step), so the
@@ -236,6 +272,14 @@ class FrontEnd:
     # ------------------------------------------------------------ steps
     def step(self) -> None:
         check(lib().gf_frontend_step(self.handle))
+
+    def step_extract(self) -> None:
+        """gf_frontend_step_extract: the step's extraction gate and Frame
+        construction only (step_track completes the step)."""
+        check(lib().gf_frontend_step_extract(self.handle))
+
+    def step_track(self) -> None:
+        check(lib().gf_frontend_step_track(self.handle))
 
     def step_host(self, imgs: np.ndarray) -> None:
         imgs = np.ascontiguousarray(imgs, np.uint8)

@@ -1131,6 +1131,13 @@ int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, dou
 int gf_frontend_bootstrap_host(gf_frontend* fe, const uint8_t* imgs, const float* Tcw, const float* V, double t0);
 /* One frame per stream from the source (asynchronous on the context stream). */
 int gf_frontend_step(gf_frontend* fe);
+/* gf_frontend_step in two calls: the extraction gate and Frame construction
+ * (ORB extraction, undistortion; the Frame(...) of Tracking.cc:521), then tracking (Track()). Lets a caller stepping several
+ * gated front ends from one thread enqueue every front end's extraction before
+ * any tracking. Each call fails with GF_ERR_ARG out of order; gf_frontend_step
+ * fails while an extracted frame awaits tracking. Not for captured front ends. */
+int gf_frontend_step_extract(gf_frontend* fe);
+int gf_frontend_step_track(gf_frontend* fe);
 /* Same with the B frames taken from host memory ([B][height][width] u8):
  * the PCIe copy is part of the step. */
 int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs);

@@ -439,6 +439,51 @@ def test_track_priority_stream_equals_default():
 
 
 @pytest.mark.gpu
+def test_split_step_and_ring_order_equal_step():
+    """gf_frontend_step_extract + gf_frontend_step_track, and GatedRing's
+    launch order over gated front ends, give the state plain gated steps
+    give; the split calls fail out of order."""
+    from gf_orb_slam_amd.pipeline import GatedRing, chain_extraction, step_all
+
+    runs = []
+    for mode in ("step", "split", "ring"):
+        fes = [_setup("euroc", 1000, 4, 2000, 100, stale=0.93, seed=8)[3] for _ in range(3)]
+        chain_extraction(fes)
+        ring = GatedRing(fes)
+        for _ in range(4):
+            if mode == "step":
+                for fe in fes:
+                    fe.step()
+            elif mode == "split":
+                step_all(fes)
+            else:
+                ring.step()
+        ring.finish()
+        if mode == "split":
+            with pytest.raises(RuntimeError):
+                fes[0].step_track()  # nothing extracted
+            fes[0].step_extract()
+            for bad in (fes[0].step_extract, fes[0].step):
+                with pytest.raises(RuntimeError):
+                    bad()  # the extracted frame is not tracked yet
+            fes[0].step_track()
+        for fe in fes:
+            fe.sync()
+        st = [C.read_state(fe) for fe in fes]
+        if mode == "split":  # one step more on front end 0: drop it from the comparison
+            st[0] = None
+        runs.append(st)
+        for fe in fes:
+            fe.close()
+    for mode, run in zip(("split", "ring"), runs[1:]):
+        for g, (a, b) in enumerate(zip(runs[0], run)):
+            if b is None:
+                continue
+            for k in ("kp2mp", "Tcw", "mp_info", "rng", "views", "stats"):
+                assert np.array_equal(a[k], b[k]), (mode, g, k)
+
+
+@pytest.mark.gpu
 def test_graph_replay_equals_eager():
     """gf_frontend_capture: a replayed step equals an eager one."""
     W, frames, maps, fe, T, V = _setup("euroc", 1000, 4, 2000, 100)
