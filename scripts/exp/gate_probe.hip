@@ -5,6 +5,8 @@
 //   mode 1: event (timing off), B's wait enqueued before K2
 //   mode 2: event (timing on),  B's wait enqueued after K2
 //   mode 3: hipStreamWriteValue32 after K1 / hipStreamWaitValue32 on B, after K2
+//           (the word from hipExtMallocWithFlags(hipMallocSignalMemory))
+//   mode 4: as 3, the word written by a one-wave kernel (release store)
 // Build: hipcc --offload-arch=gfx950 -O2 gate_probe.hip -o gate_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -18,6 +20,10 @@ __global__ void k_spin(unsigned long long* stamp, int slot, long long ticks) {
         stamp[2 * slot] = t0;
         stamp[2 * slot + 1] = wall_clock64();
     }
+}
+
+__global__ void k_signal(uint32_t* w, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(w, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #define CK(x)                                                                    \
@@ -35,13 +41,14 @@ int main() {
     CK(hipStreamCreateWithFlags(&b, hipStreamNonBlocking));
     unsigned long long* st;
     CK(hipMalloc(&st, 64 * sizeof(unsigned long long)));
-    uint32_t* flag;
-    CK(hipMalloc(&flag, 4));
-    CK(hipMemset(flag, 0, 4));
+    uint32_t* flag = nullptr;
+    const hipError_t fe_ = hipExtMallocWithFlags((void**)&flag, 8, hipMallocSignalMemory);
+    if (fe_ != hipSuccess) printf("signal memory: %s\n", hipGetErrorString(fe_));
+    if (flag) CK(hipMemset(flag, 0, 8));
     hipEvent_t ev_nt, ev_t;
     CK(hipEventCreateWithFlags(&ev_nt, hipEventDisableTiming));
     CK(hipEventCreate(&ev_t));
-    for (int mode = 0; mode < 4; mode++) {
+    for (int mode = 0; mode < (flag ? 5 : 3); mode++) {
         for (int rep = 0; rep < 3; rep++) {
             CK(hipDeviceSynchronize());
             CK(hipMemset(st, 0, 64 * 8));
@@ -51,6 +58,8 @@ int main() {
             k_spin<<<1, 64, 0, a>>>(st, 0, 100000);  // K1: 1 ms
             if (mode == 3)
                 CK(hipStreamWriteValue32(a, flag, val, 0));
+            else if (mode == 4)
+                k_signal<<<1, 64, 0, a>>>(flag, val);
             else
                 CK(hipEventRecord(ev, a));
             if (mode == 1) {
@@ -61,7 +70,7 @@ int main() {
             if (mode == 0 || mode == 2) {
                 CK(hipStreamWaitEvent(b, ev, 0));
                 k_spin<<<1, 64, 0, b>>>(st, 2, 100);
-            } else if (mode == 3) {
+            } else if (mode >= 3) {
                 CK(hipStreamWaitValue32(b, flag, val, hipStreamWaitValueGte, 0xffffffffu));
                 k_spin<<<1, 64, 0, b>>>(st, 2, 100);
             }

@@ -3,7 +3,7 @@
 # step | split | ring), the headline rate and the extraction-gate hand-over gaps from
 # the rocprof child's kernel trace (scripts/gate_gaps.py).
 set -o pipefail
-timeout -k 10 60 ./scripts/exp/gate_probe > gpurun_out/gate_probe.log 2>&1 || exit 10
+timeout -k 10 60 ./scripts/exp/gate_probe > gpurun_out/gate_probe.log 2>&1; echo probe rc $?
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 Q="--no-cpu-baseline --single-stream-steps 0 --lba-batch 0 --config3-steps 0 --pcie-steps 0 --budget-steps 0 --isolated-steps 0"
