@@ -671,7 +671,11 @@ __global__ __launch_bounds__(256) void k_ba_gemm_reduce(BAArena A) {
 // poses decouple with x = 0. Blocked LL^T with one 6x6 block per pose (two
 // barriers per pose), substitutions one pose block at a time on one wave —
 // all in the oracle's operation order (see below).
-constexpr int BA_ST = 1024;
+#ifndef BA_SOLVE_THREADS
+#define BA_SOLVE_THREADS 1024
+#endif
+constexpr int BA_ST = BA_SOLVE_THREADS;
+static_assert(BA_ST >= BA_MAXN && BA_ST % 64 == 0, "k_ba_solve: one thread per panel row");
 
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
