@@ -225,6 +225,19 @@ __device__ __forceinline__ int fast_max_arc(int v, const int c[16]) {
     return max((int)mx.x, (int)mx.y);
 }
 
+// Exclusive scan of one int per thread across one wave (total: the wave's sum).
+__device__ __forceinline__ int wave_scan_excl(int v, int& total) {
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
 // Exclusive scan of one int per thread across a 256-thread workgroup.
 __device__ int block_scan_256(int v, int* tmp, int& total) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -519,10 +532,11 @@ __device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buf
 // values replaced by 0 afterwards) and each row's base offset is read one
 // step before the row itself, so a row step issues its reads together and
 // waits once, not once per read.
+template <int NWV>
 __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* rsh, int pitch, uint32_t* bits, int dw,
                                              int dh, int th) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int ya = wv * dh / 4, yb = (wv + 1) * dh / 4;
+    const int ya = wv * dh / NWV, yb = (wv + 1) * dh / NWV;
     int cnt = 0;
     // rows outside the window read row dh, a row of zeros with rsh[dh] = 0
     auto rowi = [&](int y) -> int { return (y >= 0 && y < dh) ? y : dh; };
@@ -566,7 +580,23 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
     return cnt;  // this wave's survivors
 }
 
-__global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
+// FC_THREADS: workgroup size (64: one wave per cell, no workgroup barrier)
+#ifndef FC_THREADS
+#define FC_THREADS 256
+#endif
+constexpr int FC_NT = FC_THREADS, FC_NW = FC_THREADS / 64;
+static_assert(FC_NT == 64 || FC_NT == 256, "k_fast_cells: one wave or four");
+__device__ __forceinline__ void fc_sync() {
+    if constexpr (FC_NT == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
                                                     const CellInfo* __restrict__ cells, uint32_t* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
@@ -592,11 +622,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
     // the window as aligned dwords (a cell window is a few hundred dwords: two
     // loads per thread in flight before the LDS writes)
     constexpr int FC_LB = 2;
-    for (int i0 = 0; i0 < dh * ndw; i0 += 256 * FC_LB) {
+    for (int i0 = 0; i0 < dh * ndw; i0 += FC_NT * FC_LB) {
         uint32_t v[FC_LB];
 #pragma unroll
         for (int k = 0; k < FC_LB; k++) {
-            const int i = i0 + 256 * k + tid;
+            const int i = i0 + FC_NT * k + tid;
             const int r = i / ndw, q = i - r * ndw;
             v[k] = 0;
             if (r < dh) {
@@ -606,51 +636,60 @@ __global__ __launch_bounds__(256) void k_fast_cells(Planes P, LevelGeom g, const
         }
 #pragma unroll
         for (int k = 0; k < FC_LB; k++) {
-            const int i = i0 + 256 * k + tid;
+            const int i = i0 + FC_NT * k + tid;
             if (i < dh * ndw) reinterpret_cast<uint32_t*>(sc)[i] = v[k];
         }
     }
-    for (int r = tid; r < dh; r += 256) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)r * lw) & 3);
+    for (int r = tid; r < dh; r += FC_NT) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)r * lw) & 3);
     if (tid == 0) rsh[dh] = 0;
-    for (int i = tid; i < ndw; i += 256) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
-    for (int i = tid; i < nwords; i += 256) bits[i] = 0;
-    __syncthreads();
-    int c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, fast_th);
+    for (int i = tid; i < ndw; i += FC_NT) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
+    for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
+    fc_sync();
+    int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, fast_th);
     if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
-    __syncthreads();
-    int total = s_cnt[0][0] + s_cnt[0][1] + s_cnt[0][2] + s_cnt[0][3];
+    fc_sync();
+    int total = 0;
+#pragma unroll
+    for (int k = 0; k < FC_NW; k++) total += s_cnt[0][k];
     if (total <= 3) {  // ORBextractor.cc:623-628: retry with the minimum threshold
         // the ROI (window + 3-px ring margin) of the unblurred level to LDS
         uint8_t* roi = reinterpret_cast<uint8_t*>(bits + ((nwords + 3) & ~3));
         int sstride;
         const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
-        for (int i = tid; i < ci.w * ci.h; i += 256) {
+        for (int i = tid; i < ci.w * ci.h; i += FC_NT) {
             const int r = i / ci.w;
             roi[i] = gfd::ldg(Sl + (long long)r * sstride + (i - r * ci.w));
         }
-        __syncthreads();
-        for (int i = tid; i < n; i += 256) {
+        fc_sync();
+        for (int i = tid; i < n; i += FC_NT) {
             const int y = i / dw, x = i - y * dw;
             int c[16];
             circle_vals(roi, ci.w, x + 3, y + 3, c);
             const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
             sc[y * pitch + rsh[y] + x] = M > min_th ? (uint8_t)M : 0;
         }
-        for (int i = tid; i < nwords; i += 256) bits[i] = 0;
-        __syncthreads();
-        c = cell_nms_bits(sc, rsh, pitch, bits, dw, dh, min_th);
+        for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
+        fc_sync();
+        c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, min_th);
         if ((tid & 63) == 0) s_cnt[1][tid >> 6] = c;
-        __syncthreads();
-        total = s_cnt[1][0] + s_cnt[1][1] + s_cnt[1][2] + s_cnt[1][3];
+        fc_sync();
+        total = 0;
+#pragma unroll
+        for (int k = 0; k < FC_NW; k++) total += s_cnt[1][k];
     }
     uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
     const int X0 = ci.x0 + 3, Y0 = ci.y0 + 3;
     int base = 0;
-    for (int w0 = 0; w0 < nwords; w0 += 256) {
+    for (int w0 = 0; w0 < nwords; w0 += FC_NT) {
         const int i = w0 + tid;
         uint32_t word = i < nwords ? bits[i] : 0u;
         int tot;
-        int off = base + block_scan_256(__popc(word), scan_tmp, tot);
+        int off;
+        if constexpr (FC_NT == 64) {
+            off = base + wave_scan_excl(__popc(word), tot);
+        } else {
+            off = base + block_scan_256(__popc(word), scan_tmp, tot);
+        }
         while (word) {
             const int p = 32 * i + __ffs(word) - 1;
             word &= word - 1;
@@ -1555,7 +1594,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     if (ex->stage_ev && ex->stage_after == 1) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_fast_cells");
-        GF_LAUNCH(k_fast_cells, dim3(g.ncells, nframes), 256, ex->fast_lds, s, 
+        GF_LAUNCH(k_fast_cells, dim3(g.ncells, nframes), FC_NT, ex->fast_lds, s, 
             P, g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
     }
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
