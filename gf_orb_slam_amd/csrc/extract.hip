@@ -585,7 +585,26 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
 #define FC_THREADS 256
 #endif
 constexpr int FC_NT = FC_THREADS, FC_NW = FC_THREADS / 64;
-static_assert(FC_NT == 64 || FC_NT == 256, "k_fast_cells: one wave or four");
+static_assert(FC_NT == 64 || FC_NT == 256 || FC_NT == 512, "k_fast_cells: 1, 4 or 8 waves");
+
+// Exclusive scan of one int per thread across an NW-wave workgroup.
+template <int NW>
+__device__ int block_scan_nw(int v, int* tmp, int& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int wt;
+    const int x = wave_scan_excl(v, wt);
+    if (lane == 0) tmp[wid] = wt;
+    __syncthreads();
+    int base = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        base += i < wid ? tmp[i] : 0;
+        total += tmp[i];
+    }
+    __syncthreads();
+    return base + x;
+}
 __device__ __forceinline__ void fc_sync() {
     if constexpr (FC_NT == 64) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -601,8 +620,8 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ int s_cnt[2][4];
-    __shared__ int scan_tmp[4];
+    __shared__ int s_cnt[2][FC_NW];
+    __shared__ int scan_tmp[FC_NW];
     int cid, f;
     gfd::xcd_block(cid, f);
     const int tid = threadIdx.x;
@@ -688,7 +707,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         if constexpr (FC_NT == 64) {
             off = base + wave_scan_excl(__popc(word), tot);
         } else {
-            off = base + block_scan_256(__popc(word), scan_tmp, tot);
+            off = base + block_scan_nw<FC_NW>(__popc(word), scan_tmp, tot);
         }
         while (word) {
             const int p = 32 * i + __ffs(word) - 1;

@@ -5,6 +5,8 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 V=${V:-fc64}
+timeout -k 10 300 python -u -m pytest tests/test_extract_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/fc_pytest_product.log 2>&1 || exit 13
+tail -1 gpurun_out/fc_pytest_product.log
 GF_LIB=$R/gf_orb_slam_amd/diag/libgfslam_$V.so timeout -k 10 300 python -u -m pytest tests/test_extract_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/fc_pytest_$V.log 2>&1 || exit 12
 tail -1 gpurun_out/fc_pytest_$V.log
 Q="--no-cpu-baseline --single-stream-steps 0 --lba-batch 0 --config3-steps 0 --pcie-steps 0 --budget-steps 0 --isolated-steps 0"
