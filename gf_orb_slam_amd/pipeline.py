@@ -162,6 +162,9 @@ class GatedRing:
     def step(self) -> None:
         prev = self._held
         for fe in self.fes:
+            if prev is fe:  # one front end: its frame is tracked before the next is extracted
+                prev.step_track()
+                prev = None
             fe.step_extract()
             if prev is not None:
                 prev.step_track()
