@@ -522,10 +522,6 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 // pixel); survivors set their bit in an LDS bit array (bit = row-major pixel
 // index). Listing: a workgroup scan over the popcounts of the bit words.
 // (Cell windows are at most ~40 px wide, so one strip.)
-// FC_HALF_WAVE: NMS of a window at most 32 px wide on half-waves (below)
-#ifndef FC_HALF_WAVE
-#define FC_HALF_WAVE 0
-#endif
 __device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buffer value at th
     const int S = m - 1;  // entries are S + 1 for corners at the map threshold, 0 otherwise
     return S >= th ? S : 0;
@@ -544,49 +540,6 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
     int cnt = 0;
     // rows outside the window read row dh, a row of zeros with rsh[dh] = 0
     auto rowi = [&](int y) -> int { return (y >= 0 && y < dh) ? y : dh; };
-#if FC_HALF_WAVE
-    // a window at most 32 wide (the usual ~31-px cell): the wave's two halves
-    // take the two halves of its rows, lane & 31 = column, so no lane idles
-    // past the window's edge
-    if (dw <= 32) {
-        const int ym = (ya + yb + 1) >> 1, hi = lane >> 5, x = lane & 31;
-        const int ys = hi ? ym : ya, ye = hi ? yb : ym, nst = ym - ya;
-        const bool okc = x < dw;
-        const int ml = -(int)(x >= 1 && x - 1 < dw), mc = -(int)okc, mr = -(int)(x + 1 < dw);
-        const int cl = min(max(x - 1, 0), dw - 1), cc = min(x, dw - 1), cr = min(x + 1, dw - 1);
-        auto row3 = [&](int b, int& v0, int& v1, int& v2) {
-            const uint8_t* r = sc + b;
-            const int r0 = r[cl], r1 = r[cc], r2 = r[cr];
-            v0 = nms_at(r0, th) & ml;
-            v1 = nms_at(r1, th) & mc;
-            v2 = nms_at(r2, th) & mr;
-        };
-        int u0, u1, u2, c0, c1, c2, d0, d1, d2;
-        {
-            const int i0 = rowi(ys - 1), i1 = rowi(ys), i2 = rowi(ys + 1);
-            row3(i0 * pitch + rsh[i0], u0, u1, u2);
-            row3(i1 * pitch + rsh[i1], c0, c1, c2);
-            row3(i2 * pitch + rsh[i2], d0, d1, d2);
-        }
-        int ie = rowi(ys + 2), se = rsh[ie];
-        for (int t = 0; t < nst; t++) {
-            const int y = ys + t;
-            int e0, e1, e2;
-            row3(ie * pitch + se, e0, e1, e2);  // row y + 2, read one step ahead
-            const int in = rowi(y + 3), sn = rsh[in];
-            const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
-            const bool keep = okc && y < ye && c1 != 0 && c1 > mx;
-            if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
-            cnt += __popcll(__ballot(keep));
-            u0 = c0, u1 = c1, u2 = c2;
-            c0 = d0, c1 = d1, c2 = d2;
-            d0 = e0, d1 = e1, d2 = e2;
-            ie = in;
-            se = sn;
-        }
-        return cnt;
-    }
-#endif
     for (int x0 = 0; x0 < dw; x0 += 64) {
         const int x = x0 + lane;
         const bool okc = x < dw;
