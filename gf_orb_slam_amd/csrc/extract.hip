@@ -285,6 +285,10 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 // out as one dword per quad and row. The planes are pitched to 64 B, so a
 // quad past the level's right edge writes the row padding.
 #define BT_W 64
+// BT_SKIP_PAST: waves of a tile's column / compass pass skip rows past the level
+#ifndef BT_SKIP_PAST
+#define BT_SKIP_PAST 0
+#endif
 #ifndef BT_H
 #define BT_H 64
 #endif
@@ -441,6 +445,11 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 #pragma unroll
     for (int k = 0; k < BT_NQ; k++) {
         const int r0 = 2 * (tid >> 4) + 32 * k;
+#if BT_SKIP_PAST
+        // a wave whose eight rows all lie past the level's last row has no
+        // output, no candidate and no score to write (wave-uniform)
+        if (Y0 + 32 * k + 8 * (tid >> 6) >= h) continue;
+#endif
         // column pass: row pairs r0 / 2 .. + 3 (rows r0 .. r0 + 7) give output
         // rows r0 and r0 + 1, four v_dot2_u32_u16 per pixel (the rounding bias
         // as the accumulator's start)
