@@ -287,7 +287,7 @@ __device__ int block_scan_256(int v, int* tmp, int& total) {
 #define BT_W 64
 // BT_SKIP_PAST: waves of a tile's column / compass pass skip rows past the level
 #ifndef BT_SKIP_PAST
-#define BT_SKIP_PAST 0
+#define BT_SKIP_PAST 1
 #endif
 #ifndef BT_H
 #define BT_H 64
