@@ -429,6 +429,65 @@ def config3_leg(local: int, batch: int, groups: int, steps: int, warmup: int) ->
             "kernels": {k: {"avg_ms": round(v[0] / max(v[1], 1), 4), "launches": v[1]} for k, v in prof.items()}}
 
 
+# ------------------------------------------------------------- output line
+LINE_CAP = 8000
+
+
+def compact_line(out: dict, detail: str) -> str:
+    """The one JSON line the driver parses: the contract fields, the dominant
+    kernel's roofline plus up to four other priced kernels as flat entries, the
+    CPU baseline, a few scalar legs. Everything else is in `detail`."""
+    roof = out.get("roofline", {})
+    keep = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "timing", "avg_launch_ms",
+            "avg_launch_ms_events", "algorithmic_bytes_per_launch", "algorithmic_flops_per_launch", "launches")
+    r = {k: roof[k] for k in keep if k in roof}
+    r["frames_per_launch"] = roof.get("frames_per_launch")
+    others = roof.get("other_kernels", {})
+    order = sorted(others, key=lambda k: -others[k].get("avg_launch_ms", 0))[:4]
+    r["others"] = {k: {f: others[k].get(f) for f in ("bound", "achieved", "unit", "frac", "avg_launch_ms",
+                                                       "traffic")} for k in order}
+    cb = out.get("cpu_baseline")
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype")}
+    line["data"] = "synthetic: rendered EuRoC-like sequences, keyframe maps; no dataset"
+    c = out["config"]
+    line["config"] = {"workload": "config 2: euroc 752x480, 1000 feats, GF budget 100, full GrabImage step "
+                                  "(extract, match, GF select, 2x PoseOptimization) with UpdateReference",
+                      "sequences_per_gpu": c.get("sequences_per_gpu"), "stream_groups": c.get("stream_groups"),
+                      "parallelism": c.get("parallelism")}
+    line["roofline"] = r
+    if cb:
+        line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind")}
+        line["cpu_baseline"]["sample"] = cb.get("sample", "")[:200]
+        if "all_cores" in cb:
+            line["cpu_baseline"]["all_cores"] = {k: cb["all_cores"].get(k) for k in ("value", "cores")}
+    extra = {}
+    if "single_stream" in out:
+        extra["single_stream_ms_per_frame"] = out["single_stream"].get("ms_per_frame")
+    if "pose_opt" in out:
+        extra["pose_opt_ms_per_iter"] = out["pose_opt"].get("ms_per_iter")
+    lba = out.get("local_ba", {})
+    if "batch_1" in lba:
+        extra["local_ba_ms_per_window"] = lba["batch_1"].get("ms_per_batch")
+    if "config3" in out:
+        extra["config3_frames_per_s"] = out["config3"].get("frames_per_s")
+    if "budgets_on" in out:
+        extra["budgets_on_frames_per_s"] = out["budgets_on"].get("frames_per_s")
+    line["legs"] = extra
+    line["detail"] = detail
+    s = json.dumps(line)
+    if len(s) > LINE_CAP:  # never exceed the cap: drop the optional parts first
+        for drop in ("legs", "others"):
+            if drop == "others":
+                line["roofline"].pop("others", None)
+            else:
+                line.pop(drop, None)
+            s = json.dumps(line)
+            if len(s) <= LINE_CAP:
+                break
+    return s
+
+
 # ------------------------------------------------------------- kernel table
 def _under_profiler() -> bool:
     """True inside a rocprofv3 (or older rocprof) run: no nested profiler."""
@@ -591,6 +650,9 @@ def main():
                          "(step), every group's extraction before any tracking (split, pipeline.step_all), or "
                          "group g's extraction before g - 1's tracking (ring, pipeline.GatedRing)")
     ap.add_argument("--kernels-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--detail-out", default=None,
+                    help="file for the full measurement record (per-kernel tables, legs); the stdout line is the "
+                         "compact contract line (<= 8 KB) and names this file (default gpurun_out/bench_detail.json)")
     ap.add_argument("--no-reloc", action="store_true",
                     help="no keyframe databases: a lost stream stays LOST (the step then skips the BoW / candidate "
                          "launches); default: every stream relocalises against its scene's keyframes")
@@ -837,8 +899,36 @@ def main():
                 ("algorithmic_bytes_per_launch" if kind == "hbm" else "algorithmic_flops_per_launch"): units,
                 "work": what, "avg_launch_ms": round(ms_avg, 4), "launches": prof[k][1]}
 
-    priced = {k: price(k, prof[k][0] / prof[k][1]) for k in work if k in prof}
-    if "k_active_match" in priced and "k_active_match_overflow" in prof:
+    # the rocprof dispatch durations of the same steps (child process), per
+    # launch of each priced kernel's HIP-event scope: DESIGN §5 takes them as
+    # the honest per-kernel times (HIP events also count queue waits behind
+    # other streams' kernels), so every `frac` is priced from them when present
+    rp = {k: (sum(v) / 1e6, len(v)) for k, v in ktab.items()} if ktab else None
+    SCOPE = {"k_active_match": ["k_active_match", "k_active_match_overflow"],
+             "k_match_lastframe": ["k_match_seq", "k_match_seq_pre"], "k_match_project": ["k_match"],
+             "k_pose_opt": ["k_pose_opt_frames"]}
+
+    def rp_total(k):
+        return sum(rp[n][0] for n in SCOPE.get(k, [k]) if n in rp) if rp else 0.0
+
+    if rp:
+        priced = {}
+        for k in work:
+            if k in prof and rp_total(k) > 0:
+                ev = prof[k][0] / prof[k][1]
+                if k == "k_active_match" and "k_active_match_overflow" in prof:
+                    ev = (prof[k][0] + prof["k_active_match_overflow"][0]) / prof[k][1]
+                if k == "k_match_lastframe" and "k_match_seq_pre" in prof:
+                    ev = (prof[k][0] + prof["k_match_seq_pre"][0]) / prof[k][1]
+                priced[k] = price(k, rp_total(k) / prof[k][1])
+                priced[k].update({"timing": "rocprof", "avg_launch_ms_events": round(ev, 4),
+                                  "events_over_rocprof": round(ev / (rp_total(k) / prof[k][1]), 3),
+                                  "rocprof_kernels": SCOPE.get(k, [k])})
+    else:
+        priced = {k: price(k, prof[k][0] / prof[k][1]) for k in work if k in prof}
+        for k in priced:
+            priced[k]["timing"] = "hip_events"
+    if rp is None and "k_active_match" in priced and "k_active_match_overflow" in prof:
         # two-pass launch (gf.hip obs_active_match): the log-dets counted per
         # frame include the frames the overflow pass redid, so the rate is
         # priced over both passes' time per launch pair
@@ -860,7 +950,7 @@ def main():
             "algorithmic_bytes_per_launch": bp, "achieved": round(bp / (ms_d / 1e3) / 1e9, 2), "unit": "GB/s",
             "frac": round(bp / (ms_d / 1e3) / 1e9 / 8000.0, 6),
             "work": "%d frames x (2 P + 60 N): the IC_Angle level and the rBRIEF blurred level read once" % Bg}
-    if "k_match_lastframe" in priced and "k_match_seq_pre" in prof:
+    if rp is None and "k_match_lastframe" in priced and "k_match_seq_pre" in prof:
         # the per-query precompute and the ordered pass are one SearchByProjection(Cur, Last)
         ms_pair = (prof["k_match_lastframe"][0] + prof["k_match_seq_pre"][0]) / prof["k_match_lastframe"][1]
         priced["k_match_lastframe"] = price("k_match_lastframe", ms_pair)
@@ -868,22 +958,6 @@ def main():
     for k in priced:
         if work[k][0] == "f64":
             priced[k]["peak_note"] = "FP64 peak (AMD spec, vector = matrix on MI355X); this kernel is f64 VALU"
-    # the rocprof dispatch durations of the same steps (child process), per
-    # launch of each priced kernel's HIP-event scope
-    rp = {k: (sum(v) / 1e6, len(v)) for k, v in ktab.items()} if ktab else None
-    SCOPE = {"k_active_match": ["k_active_match", "k_active_match_overflow"],
-             "k_match_lastframe": ["k_match_seq", "k_match_seq_pre"], "k_match_project": ["k_match"],
-             "k_pose_opt": ["k_pose_opt_frames"]}
-
-    def rp_total(k):
-        return sum(rp[n][0] for n in SCOPE.get(k, [k]) if n in rp) if rp else 0.0
-
-    if rp:
-        for k, e in priced.items():
-            if rp_total(k) > 0:
-                ms_r = rp_total(k) / prof[k][1]
-                e["avg_launch_ms_rocprof"] = round(ms_r, 4)
-                e["events_over_rocprof"] = round(e["avg_launch_ms"] / ms_r, 3)
     if rp:
         top = max(rp, key=lambda k: rp[k][0])
         dom = max(priced, key=rp_total)
@@ -1144,7 +1218,15 @@ def main():
                     "pinned; whole_host_linear scales that figure linearly to all %d physical cores of the "
                     "node (an extrapolation, not a measurement)" % phys}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        detail = args.detail_out or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+            with open(detail, "w") as fh:
+                json.dump(out, fh, indent=1)
+        except OSError as e:
+            detail = f"(not written: {e})"
+        line = compact_line(out, os.path.relpath(detail, ROOT) if os.path.isabs(detail) else detail)
+        print(line, flush=True)
     gd.close()
     if world > 1:
         dist.destroy_process_group()

@@ -178,6 +178,11 @@ _PROTOS = {
     "gf_dist_init": [_P, _I, _I, _P, _P],
     "gf_dist_destroy": [_P],
     "gf_dist_info": [_P, _P, _P],
+    "gf_dist_channel_create": [_I, _P],
+    "gf_dist_channel_destroy": [_P],
+    "gf_dist_init_loopback": [_P, _I, _P, _P],
+    "gf_dist_init_host": [_P, _I, _I, _P, _P, _P],
+    "gf_dist_transport": [_P, _P],
     "gf_dist_bcast": [_P, _P, _S, _I],
     "gf_dist_allreduce": [_P, _P, _S, _I],
     "gf_dist_bcast_vocab": [_P, _P, _I],

@@ -109,6 +109,7 @@ struct FeDev {
     int32_t* track;        // [B][GF_TR_N]
     int32_t* m3_nlast;     // [B] last-frame points SearchByProjection(Cur, Last) projects (0 off the motion model)
     int32_t* rl_gate;      // [B] 1: Relocalisation this step
+    const int32_t* kfc;    // [B] KeyFramesInMap() of the stream's keyframe graph (-1: no graph, assumed > 5)
     int32_t* nkp_tl;       // [B] keypoints TrackLocalMap sees (0: it does not run)
     int32_t* nkp_fi;       // [B] keypoints of its FRAME_INFO_MATRIX pass
     int32_t* gate_tl;      // [B] TrackLocalMap runs
@@ -152,13 +153,15 @@ __global__ __launch_bounds__(256) void k_fe_begin(FeDev D) {
         D.t_cur[b] = D.t_cur[b] + D.dt;  // mCurrentFrame.mTimeStamp (mLastFrame's may be older after a loss)
         // the initial estimate's path (Tracking.cc:602-628): LOST -> Relocalisation;
         // a velocity and >= 2 frames since a relocalisation -> TrackWithMotionModel
-        // (mTcw = mVelocity * mLastFrame.mTcw, :1519); else TrackPreviousFrame
-        // (mTcw = mLastFrame.mTcw, :1353); a fresh Frame's mTcw is empty (zeros)
+        // (mTcw = mVelocity * mLastFrame.mTcw, :1519) unless the map holds fewer
+        // than 4 keyframes (:602); else TrackPreviousFrame (mTcw = mLastFrame.mTcw,
+        // :1353); a fresh Frame's mTcw is empty (zeros)
         int32_t* T = D.track + (size_t)b * GF_TR_N;
         T[GF_TR_QUERY] += 1;  // mnId
         const int since = min(T[GF_TR_SINCE] + 1, 1 << 30);
         T[GF_TR_SINCE] = since;
-        const int path = T[GF_TR_STATE] == 1 ? 3 : (T[GF_TR_VEL] && since >= 2) ? 0 : 2;
+        const int kfc = D.kfc[b];
+        const int path = T[GF_TR_STATE] == 1 ? 3 : (T[GF_TR_VEL] && since >= 2 && !(kfc >= 0 && kfc < 4)) ? 0 : 2;
         T[GF_TR_PATH] = path;
         T[GF_TR_OK] = 0;
         D.m3_nlast[b] = path == 0 ? D.last_nkp[b] : 0;
@@ -1281,6 +1284,7 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     TL.stats = D.stats;
     TL.rng = rng;
     TL.kf_count = fe->d_kfc;
+    D.kfc = fe->d_kfc;
     TL.gnmp = nmp;
     TL.nkp_tl = D.nkp_tl;
     TL.nkp_fi = D.nkp_fi;
@@ -1540,20 +1544,28 @@ int gf_frontend_set_kfdb(gf_frontend* fe, int stream, gf_kfdb* db) {
     fe->h_kfdb[stream] = v;
     GF_HIP(hipMemcpy(fe->d_kfdb + stream, &v, sizeof(v), hipMemcpyHostToDevice));
     GF_HIP(hipMemset(fe->TL.rkf + (size_t)stream * gf::RL_NC, 0, sizeof(gf_reloc_kf) * gf::RL_NC));
+    GF_HIP(hipMemset(fe->TL.ncand + stream, 0, 4));  // no candidates of an earlier database survive
     int ncs = 1;
     for (const gf::KfdbDev& k : fe->h_kfdb) ncs = std::max(ncs, k.nkf);
     fe->TL.ncs = ncs;
     fe->rl_on = fe->voc && ncs > 0 && std::any_of(fe->h_kfdb.begin(), fe->h_kfdb.end(),
                                                   [](const gf::KfdbDev& k) { return k.nkf > 0; });
+    fe->TL.rl_on = fe->rl_on;
     return GF_OK;
 }
 
 int gf_frontend_set_vocab(gf_frontend* fe, gf_vocab* voc) {
     GF_CHECK(fe, GF_ERR_ARG, "null front end");
     GF_CHECK(!fe->exec, GF_ERR_ARG, "set the vocabulary before capturing a graph");
+    if (fe->rl_alloc) {  // candidates computed with another vocabulary are not this step's
+        GF_HIP(hipSetDevice(fe->ctx->device));
+        GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+        GF_HIP(hipMemset(fe->TL.ncand, 0, 4 * (size_t)fe->D.B));
+    }
     fe->voc = voc;
     fe->rl_on = fe->voc && std::any_of(fe->h_kfdb.begin(), fe->h_kfdb.end(),
                                        [](const gf::KfdbDev& k) { return k.nkf > 0; });
+    fe->TL.rl_on = fe->rl_on;
     return GF_OK;
 }
 
@@ -1587,11 +1599,13 @@ static int fe_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, doubl
 int gf_frontend_bootstrap(gf_frontend* fe, const float* Tcw, const float* V, double t0) {
     GF_CHECK(fe && Tcw && V, GF_ERR_ARG, "null arg");
     GF_CHECK(fe->sourced, GF_ERR_ARG, "no frame source set");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
     return fe_bootstrap(fe, Tcw, V, t0, false);
 }
 
 int gf_frontend_bootstrap_host(gf_frontend* fe, const uint8_t* imgs, const float* Tcw, const float* V, double t0) {
     GF_CHECK(fe && imgs && Tcw && V, GF_ERR_ARG, "null arg");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
     GF_HIP(hipSetDevice(fe->ctx->device));
     FE_RC(fe_staging(fe, imgs));
     return fe_bootstrap(fe, Tcw, V, t0, true);
@@ -1739,6 +1753,7 @@ int gf_frontend_step_track(gf_frontend* fe) {
 
 int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
     GF_CHECK(fe && imgs, GF_ERR_ARG, "null arg");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
     FE_RC(fe_check_covis(fe));
     GF_HIP(hipSetDevice(fe->ctx->device));
     FeDev& D = fe->D;
@@ -1758,6 +1773,7 @@ int gf_frontend_step_host(gf_frontend* fe, const uint8_t* imgs) {
 
 int gf_frontend_capture(gf_frontend* fe) {
     GF_CHECK(fe && fe->sourced, GF_ERR_ARG, "capture needs a frame source");
+    GF_CHECK(!fe->extracted, GF_ERR_ARG, "the extracted frame has not been tracked (gf_frontend_step_track)");
     FE_RC(fe_check_covis(fe));
     // a recorded event in a graph is not the caller's event at replay: the
     // extraction gate would silently stop gating

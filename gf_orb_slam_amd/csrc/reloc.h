@@ -81,6 +81,7 @@ struct TrackLossArgs {
     int32_t* pint;        // [B][4] nedges, inliers, iterations
     // relocalisation (kfdb null: no stream has a database)
     const KfdbDev* kfdb;        // [B] (nkf 0: none)
+    int rl_on;                  // the step computes candidates (a vocabulary and some database set)
     const gf_covis_map* covis;  // [B] the streams' keyframe graphs (device)
     gf_reloc_kf* rkf;           // [B][RL_NC]
     const int32_t* rl_gate;     // [B] 1: the stream relocalises this step

@@ -555,10 +555,11 @@ __device__ bool track_previous_frame(const gf::TrackLossArgs& A, int b, TLShared
 __device__ bool relocalise(const gf::TrackLossArgs& A, int b, TLShared& S) {
     const int lane = threadIdx.x, cap = A.cap;
     if (!A.kfdb) return false;
+    const gf::KfdbDev db = A.kfdb[b];
+    if (db.nkf <= 0 || !A.rl_on) return false;  // no database, or no candidates computed this step
     const int nc = A.ncand[b];
     if (nc <= 0) return false;
     const gf_covis_map cv = A.covis[b];
-    const gf::KfdbDev db = A.kfdb[b];
     const int32_t* cand = A.cands + (size_t)b * gf::RL_NC;
     const int n = A.nkp[b];
     int32_t* kp2mp = A.kp2mp + (size_t)b * cap;

@@ -22,15 +22,84 @@ def checksum(a: np.ndarray) -> int:
     return zlib.crc32(np.ascontiguousarray(a).view(np.uint8).reshape(-1).tobytes()) & 0xFFFFFFFF
 
 
-class GfDist:
-    """An RCCL communicator of libgfslam (gf_dist_*) on one context's device.
-    The 128-byte unique id travels over the torch.distributed group `pg`."""
+TRANSPORTS = {"rccl": 0, "loopback": 1, "host": 2}
 
-    def __init__(self, ctx, rank: int, world: int, pg=None):
+# gf_dist_host_fn (abi.h): int fn(void* user, int op, void* host_buf, size_t bytes, int root)
+HOST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+
+
+class LoopbackChannel:
+    """gf_dist_channel: the meeting point of `world` loopback ranks, each a
+    host thread of this process with its own context (abi.h)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.handle = ctypes.c_void_p()
+        check(lib().gf_dist_channel_create(world, ctypes.byref(self.handle)))
+
+    def close(self) -> None:
+        if self.handle:
+            lib().gf_dist_channel_destroy(self.handle)
+            self.handle = None
+
+
+def _gloo_host_fn(pg):
+    """The host-staged transport's collective over a torch.distributed group
+    (gloo): broadcast of bytes from root, or an in-place all-reduce of
+    doubles (abi.h GF_DIST_OP_*)."""
+    import torch
+    import torch.distributed as dist
+
+    ops = {1: dist.ReduceOp.SUM, 2: dist.ReduceOp.MAX, 3: dist.ReduceOp.MIN}
+
+    def fn(user, op, buf, nbytes, root):
+        try:
+            if nbytes == 0:
+                return 0
+            a = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(buf))
+            if op == 0:
+                dist.broadcast(torch.from_numpy(a), src=root, group=pg)
+            else:
+                dist.all_reduce(torch.from_numpy(a.view(np.float64)), op=ops[op], group=pg)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the library as a failed collective
+            import traceback
+
+            traceback.print_exc()
+            return 1
+
+    return HOST_FN(fn)
+
+
+class GfDist:
+    """A communicator of libgfslam (gf_dist_*) on one context's device.
+
+    transport "rccl" (the product path): an RCCL communicator, the 128-byte
+    unique id handed out over the torch.distributed group `pg`. "loopback":
+    ranks are threads of this process meeting in `channel` (a LoopbackChannel)
+    — one GPU runs the receiving side of every exchange. "host": host-staged
+    collectives over the torch.distributed group `pg` (gloo), for processes
+    sharing one GPU."""
+
+    def __init__(self, ctx, rank: int, world: int, pg=None, transport: str = "rccl", channel=None):
+        self.ctx, self.rank, self.world = ctx, rank, world
+        self.transport = transport
+        self.handle = ctypes.c_void_p()
+        if transport == "loopback":
+            if channel is None or channel.world != world:
+                raise ValueError("loopback ranks need a LoopbackChannel of the same world size")
+            self._channel = channel
+            check(lib().gf_dist_init_loopback(ctx.handle, rank, channel.handle, ctypes.byref(self.handle)))
+            return
+        if transport == "host":
+            self._fn = _gloo_host_fn(pg)  # kept alive for the communicator's lifetime
+            check(lib().gf_dist_init_host(ctx.handle, rank, world, self._fn, None, ctypes.byref(self.handle)))
+            return
+        if transport != "rccl":
+            raise ValueError(f"unknown transport {transport!r}")
         import torch
         import torch.distributed as dist
 
-        self.ctx, self.rank, self.world = ctx, rank, world
         uid = np.zeros(128, np.uint8)
         if rank == 0:
             check(lib().gf_dist_unique_id(uid.ctypes.data_as(ctypes.c_void_p)))
@@ -38,9 +107,13 @@ class GfDist:
             t = torch.from_numpy(uid).to(f"cuda:{ctx.device}")
             dist.broadcast(t, src=0, group=pg)
             uid = t.cpu().numpy()
-        self.handle = ctypes.c_void_p()
         check(lib().gf_dist_init(ctx.handle, rank, world, uid.ctypes.data_as(ctypes.c_void_p),
                                  ctypes.byref(self.handle)))
+
+    def transport_kind(self) -> int:
+        k = ctypes.c_int()
+        check(lib().gf_dist_transport(self.handle, ctypes.byref(k)))
+        return k.value
 
     def bcast_array(self, a: np.ndarray | None, root: int = 0) -> np.ndarray:
         """Broadcast a host byte array through a device buffer (size first)."""
@@ -141,6 +214,8 @@ def pack_world(scenes, maps) -> np.ndarray:
         mb = np.ascontiguousarray(mp, MAP_POINT_DTYPE).view(np.uint8).reshape(-1)
         db = np.ascontiguousarray(d, np.uint8).reshape(-1)
         kf = len(m) > 4
+        if kf and g is None:  # the keyframe section is read only after a graph (header flag 2)
+            raise ValueError("keyframe keypoints / descriptors need the keyframe graph (maps[2])")
         hdr = np.array([sb.nbytes, len(mp), 0 if g is None else (2 if kf else 1)], np.int64).view(np.uint8)
         parts += [hdr, sb, mb, db]
         if g is not None:

@@ -1230,6 +1230,28 @@ int gf_dist_unique_id(uint8_t* id);
 int gf_dist_init(gf_ctx* ctx, int rank, int world, const uint8_t* id, gf_dist** out);
 int gf_dist_destroy(gf_dist* d);
 int gf_dist_info(gf_dist* d, int* rank, int* world);
+/* Other transports behind the same entry points (gf_dist_bcast / _allreduce /
+ * _bcast_vocab / _bcast_map work unchanged on them):
+ * - loopback: the ranks are host threads of one process, each with its own
+ *   context, meeting in a channel of `world` ranks; a broadcast is a
+ *   rendezvous and a device-to-device copy from the root's buffer, an
+ *   all-reduce a rank-ordered host reduction. Every rank's call blocks until
+ *   all ranks have made the same call (120 s timeout, then GF_ERR_HIP and a
+ *   broken channel). One GPU runs the receiving side of config 5 this way.
+ * - host-staged: device -> host, fn(user, op, host_buf, bytes, root) does the
+ *   collective on host memory (op GF_DIST_OP_BCAST from root; GF_DIST_OP_SUM /
+ *   _MAX / _MIN in place over bytes / 8 doubles, root -1) and returns 0,
+ *   host -> device. For processes that share a GPU (a gloo group). */
+enum { GF_DIST_RCCL = 0, GF_DIST_LOOPBACK = 1, GF_DIST_HOST = 2 };
+enum { GF_DIST_OP_BCAST = 0, GF_DIST_OP_SUM = 1, GF_DIST_OP_MAX = 2, GF_DIST_OP_MIN = 3 };
+typedef struct gf_dist_channel gf_dist_channel;
+typedef int (*gf_dist_host_fn)(void* user, int op, void* host_buf, size_t bytes, int root);
+int gf_dist_channel_create(int world, gf_dist_channel** out);
+int gf_dist_channel_destroy(gf_dist_channel* ch);
+int gf_dist_init_loopback(gf_ctx* ctx, int rank, gf_dist_channel* ch, gf_dist** out);
+int gf_dist_init_host(gf_ctx* ctx, int rank, int world, gf_dist_host_fn fn, void* user, gf_dist** out);
+/* GF_DIST_RCCL / _LOOPBACK / _HOST */
+int gf_dist_transport(gf_dist* d, int* transport);
 /* Device buffer broadcast from root. */
 int gf_dist_bcast(gf_dist* d, void* d_buf, size_t bytes, int root);
 /* In-place all-reduce of n doubles: op 0 sum, 1 max, 2 min. */

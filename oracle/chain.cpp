@@ -782,7 +782,10 @@ int orc_chain_step(orc_chain* c, const uint8_t* img) {
     // the initial estimate's path (Tracking.cc:602-628)
     T[GF_TR_QUERY] += 1;  // mnId
     T[GF_TR_SINCE] = std::min(T[GF_TR_SINCE] + 1, 1 << 30);
-    int path = T[GF_TR_STATE] == 1 ? 3 : (T[GF_TR_VEL] && T[GF_TR_SINCE] >= 2) ? 0 : 2;
+    // TrackWithMotionModel needs >= 4 keyframes in the map (KeyFramesInMap, :602;
+    // no keyframe graph: the map is assumed to hold more)
+    const int kfc0 = c->refmap ? c->g_nkf : -1;
+    int path = T[GF_TR_STATE] == 1 ? 3 : (T[GF_TR_VEL] && T[GF_TR_SINCE] >= 2 && !(kfc0 >= 0 && kfc0 < 4)) ? 0 : 2;
     c->t_cur = c->t_cur + c->p.dt;  // mCurrentFrame.mTimeStamp
     if (path == 0)
         mat44(c->V, c->Tcw_last, c->Tcw);  // TrackWithMotionModel :1519

@@ -306,3 +306,56 @@ def test_motion_model_miss_falls_back_to_previous_frame():
         print(row)
     assert any(r[2] in (1, 2) for r in log), "TrackPreviousFrame never ran"
     fe.close()
+
+
+def test_lost_after_database_detached():
+    """A stream relocalises (blank frames 3-4), then its keyframe graph is set
+    again (gf_frontend_set_covis detaches the keyframe database) and it loses
+    track a second time (blank frames 9-10): with no database the stream stays
+    LOST, and no relocalisation may reuse the first loss's candidates (they
+    index the detached database). Free-running and copied-in against the oracle
+    chain, whose database is detached at the same step."""
+    B, G = 3, 2600
+    voc = synth.synth_vocabulary_fast(11, k=10, L=5)
+    W0 = scene.Workload("euroc", B, n_scenes=3, period=32, seed=4)
+    blank = [(W0.scene_of[b], (W0.phase[b] + k) % 32) for b in range(B) for k in (3, 4, 9, 10)]
+    W, fr, gmaps, dbs, fe, T, V, dvoc = _scene_setup(B, G, 4, voc, blank=blank)
+    free = []
+    for b in range(B):
+        s = W.scene_of[b]
+        ch = _chain(gmaps[s], dbs[s], voc, G)
+        ch.set_rng(7 + b)
+        ch.bootstrap(fr[s, W.phase[b] % W.period], T[b], V[b])
+        free.append(ch)
+    dev = C.read_state(fe)
+    detach_after = 7
+    relocalised, lost_late = 0, 0
+    for k in range(1, 13):
+        if k == detach_after + 1:
+            for b in range(B):
+                fe.set_covis(b, gmaps[W.scene_of[b]]["graph"])
+                free[b].set_covis(gmaps[W.scene_of[b]]["graph"])
+                free[b].set_kfdb(None)
+            dev = C.read_state(fe)
+        before = dev
+        fe.step()
+        dev = C.read_state(fe)
+        for b in range(B):
+            s = W.scene_of[b]
+            img = fr[s, (W.phase[b] + k) % W.period]
+            ch = _chain(gmaps[s], dbs[s] if k <= detach_after else None, voc, G)
+            ch.load_from(before, b)
+            ch.write("reloc", before["reloc"][b])
+            ch.step(img)
+            _compare(dev, ch, b, f"step {k}: ")
+            free[b].step(img)
+            _compare(dev, free[b], b, f"free-running step {k}: ")
+            st = {n: int(dev["stats"][i, b]) for i, n in enumerate(STATS)}
+            if k <= detach_after and st["flags"] & 32768:
+                relocalised += 1
+            if k > detach_after:
+                assert not st["flags"] & 32768, f"step {k}: stream {b} relocalised without a database"
+                lost_late += int(dev["track"][b][TR["state"]] == 1)
+    assert relocalised > 0, "no stream relocalised before the database was detached"
+    assert lost_late > 0, "no stream lost track after the database was detached"
+    fe.close()
