@@ -114,8 +114,14 @@ class ORBextractor:
 
     def __call__(self, image: np.ndarray, mask=None):
         """Returns (keypoints: KEYPOINT_DTYPE[N], descriptors: uint8[N, 32])."""
+        # The reference takes a CV_8UC1 mask (ORBextractor.cc:775-778) and builds
+        # mvMaskPyramid from it (:929-993), but the per-cell FAST call never
+        # receives cellMask (:614-621): a mask does not change the outputs. It
+        # is accepted and checked the same way, then not used.
         if mask is not None and getattr(mask, "size", 0):
-            raise NotImplementedError("masks are not used on the tracking path (Frame.cc:59 passes cv::Mat())")
+            m = np.asarray(mask)
+            if m.dtype != np.uint8 or m.ndim != 2:
+                raise ValueError("mask must be an 8-bit single-channel image (CV_8UC1)")
         if image is None or image.size == 0:
             return np.zeros(0, KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8)
         image = np.ascontiguousarray(image, dtype=np.uint8)

@@ -198,9 +198,16 @@ public:
     ORBextractor(const ORBextractor&) = delete;
     ORBextractor& operator=(const ORBextractor&) = delete;
 
-    /* operator()(image, mask, keypoints, descriptors) (ORBextractor.cc:769-875);
-     * the reference ignores the mask, so it is not taken here. */
+    /* operator()(image, mask, keypoints, descriptors) (ORBextractor.cc:769-875).
+     * The reference builds mvMaskPyramid from a mask (:929-993) but never hands
+     * cellMask to FAST (:614-621), so a mask does not change the outputs: the
+     * overload with a mask takes it and extracts as without one. */
     void operator()(const ImageView& image, std::vector<KeyPoint>& keypoints, Descriptors& descriptors);
+    void operator()(const ImageView& image, const ImageView& mask, std::vector<KeyPoint>& keypoints,
+                    Descriptors& descriptors) {
+        (void)mask;
+        operator()(image, keypoints, descriptors);
+    }
 
     int GetLevels() const { return nlevels; }
     float GetScaleFactor() const { return (float)scaleFactor; }
