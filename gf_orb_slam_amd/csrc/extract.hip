@@ -64,7 +64,8 @@ struct LevelGeom {
 struct CellInfo {
     int level, x0, y0, w, h, valid;
     long long cap_off;
-    int cap, pad;
+    int cap;
+    int band;  // 0: the window fits k_fast_cells' LDS; else rows per band of k_fast_cells_band
 };
 
 struct Planes {
@@ -84,6 +85,74 @@ __device__ __forceinline__ const uint8_t* level_plane(const Planes& P, const Lev
     }
     stride = g.w[l];
     return P.pyr + (long long)f * g.slab + g.off[l];
+}
+
+// Keypoint list entries of the cell and level lists.
+// FAST_SCORE (1): u32 score << 24 | y << 12 | x, the score the FAST map holds.
+// HARRIS_SCORE (0): u64 key << 32 | y << 12 | x, key = HarrisResponses' float
+// response (ORBextractor.cc:86-127, 667-670) as an order-preserving int32, so
+// retainBest's float comparisons (KeypointResponseGreater) are key comparisons.
+template <typename E>
+struct Ent;
+template <>
+struct Ent<uint32_t> {
+    __host__ __device__ static int key(uint32_t e) { return (int)(e >> 24); }
+    __device__ static float response(uint32_t e) { return (float)(e >> 24); }
+};
+template <>
+struct Ent<uint64_t> {
+    __host__ __device__ static int key(uint64_t e) { return (int)(uint32_t)(e >> 32); }
+    __device__ static float response(uint64_t e) {
+        const int k = key(e);
+        return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff);
+    }
+};
+template <typename E>
+struct EntGreater {  // KeypointResponseGreater on list entries
+    __host__ __device__ bool operator()(E a, E b) const { return Ent<E>::key(a) > Ent<E>::key(b); }
+};
+__device__ __forceinline__ int float_key(float v) {
+    int b = __float_as_int(v);
+    if (b == (int)0x80000000) b = 0;  // -0 == +0
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+
+// HarrisResponses(cellImage, kps, blockSize 7, HARRIS_K 0.04) for one
+// keypoint at level pixel (cx, cy) (ORBextractor.cc:86-127): integer
+// gradient moments over the 7x7 block, then the reference's float expression
+// in its evaluation order (no contraction: -ffp-contract=off).
+__device__ float harris_response(const uint8_t* Pl, int step, int cx, int cy) {
+    const uint8_t* ptr0 = Pl + (long long)(cy - 3) * step + (cx - 3);
+    int a = 0, b = 0, c = 0;
+    for (int i = 0; i < 7; i++) {
+        const uint8_t* p = ptr0 + (long long)i * step;
+#pragma unroll
+        for (int j = 0; j < 7; j++, p++) {
+            const int Ix = (p[1] - p[-1]) * 2 + (p[-step + 1] - p[-step - 1]) + (p[step + 1] - p[step - 1]);
+            const int Iy = (p[step] - p[-step]) * 2 + (p[step - 1] - p[-step - 1]) + (p[step + 1] - p[-step + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    }
+    float scale = (1 << 2) * 7 * 255.0f;
+    scale = 1.0f / scale;
+    const float scale_sq_sq = scale * scale * scale * scale;
+    const float harris_k = 0.04f;
+    return ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+}
+
+// The list entry of a corner at level pixel (X, Y) with FAST score S.
+template <typename E>
+__device__ __forceinline__ E cell_entry(int S, int X, int Y, const Planes& P, const LevelGeom& g, int f, int l) {
+    if constexpr (sizeof(E) == 4) {
+        return ((uint32_t)S << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
+    } else {
+        int step;
+        const uint8_t* Pl = level_plane(P, g, f, l, step);
+        return ((uint64_t)(uint32_t)float_key(harris_response(Pl, step, X, Y)) << 32) | ((uint64_t)Y << 12) |
+               (uint64_t)X;
+    }
 }
 
 // -------------------------------------------------------------- k_resize
@@ -541,14 +610,24 @@ __device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buf
 // values replaced by 0 afterwards) and each row's base offset is read one
 // step before the row itself, so a row step issues its reads together and
 // waits once, not once per read.
-template <int NWV>
+// BAND: sc holds only window rows [lo, lo + nr) (row nr is the zero row) and
+// the rows [yA, yB) of the window are suppressed (k_fast_cells_band).
+template <int NWV, bool BAND = false>
 __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* rsh, int pitch, uint32_t* bits, int dw,
-                                             int dh, int th) {
+                                             int dh, int th, int yA = 0, int yB = 0, int lo = 0, int nr = 0) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int ya = wv * dh / NWV, yb = (wv + 1) * dh / NWV;
+    const int ya = BAND ? yA + wv * (yB - yA) / NWV : wv * dh / NWV;
+    const int yb = BAND ? yA + (wv + 1) * (yB - yA) / NWV : (wv + 1) * dh / NWV;
     int cnt = 0;
     // rows outside the window read row dh, a row of zeros with rsh[dh] = 0
-    auto rowi = [&](int y) -> int { return (y >= 0 && y < dh) ? y : dh; };
+    auto rowi = [&](int y) -> int {
+        if constexpr (BAND) {
+            const int r = y - lo;
+            return (y >= 0 && y < dh && r >= 0 && r < nr) ? r : nr;
+        } else {
+            return (y >= 0 && y < dh) ? y : dh;
+        }
+    };
     for (int x0 = 0; x0 < dw; x0 += 64) {
         const int x = x0 + lane;
         const bool okc = x < dw;
@@ -624,8 +703,9 @@ __device__ __forceinline__ void fc_sync() {
     }
 }
 
+template <typename E>
 __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
-                                                    const CellInfo* __restrict__ cells, uint32_t* __restrict__ lists,
+                                                    const CellInfo* __restrict__ cells, E* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
     extern __shared__ __align__(16) uint8_t smem[];
@@ -635,6 +715,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     gfd::xcd_block(cid, f);
     const int tid = threadIdx.x;
     const CellInfo ci = cells[cid];
+    if (ci.band) return;  // a window past this kernel's LDS: k_fast_cells_band
     const int dw = ci.w - 6, dh = ci.h - 6;
     if (!ci.valid || dw <= 0 || dh <= 0) {  // degenerate ROI: FAST finds nothing
         if (tid == 0) counts[(long long)f * g.ncells + cid] = 0;
@@ -705,7 +786,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
 #pragma unroll
         for (int k = 0; k < FC_NW; k++) total += s_cnt[1][k];
     }
-    uint32_t* out = lists + (long long)f * list_stride + ci.cap_off;
+    E* out = lists + (long long)f * list_stride + ci.cap_off;
     const int X0 = ci.x0 + 3, Y0 = ci.y0 + 3;
     int base = 0;
     for (int w0 = 0; w0 < nwords; w0 += FC_NT) {
@@ -722,8 +803,111 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
             const int p = 32 * i + __ffs(word) - 1;
             word &= word - 1;
             const int y = p / dw, x = p - y * dw;
-            out[off++] = ((uint32_t)(sc[y * pitch + rsh[y] + x] - 1) << 24) | ((uint32_t)(Y0 + y) << 12) |
-                         (uint32_t)(X0 + x);
+            out[off++] = cell_entry<E>(sc[y * pitch + rsh[y] + x] - 1, X0 + x, Y0 + y, P, g, f, l);
+        }
+        base += tot;
+    }
+    if (tid == 0) counts[(long long)f * g.ncells + cid] = total;
+}
+
+// One 256-thread workgroup per (large cell, frame): a cell window whose score
+// rows (and, for the minimum-threshold retry, ROI rows) do not fit
+// k_fast_cells' LDS — small nFeatures make few, large cells (ORBextractor.cc
+// :540-560 grids any level). The same FAST / NMS / listing as k_fast_cells,
+// with the window walked in bands of ci.band rows: each band's rows plus one
+// halo row either side go to LDS (the halo rows are what the 3x3 NMS of the
+// band's edge rows reads), the survivor bits of the whole window stay in LDS,
+// and the listing reads each survivor's score again from the map (or
+// recomputes it from the level on the retry pass).
+template <typename E>
+__global__ __launch_bounds__(256) void k_fast_cells_band(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
+                                                         const CellInfo* __restrict__ cells,
+                                                         const int* __restrict__ band_ids, E* __restrict__ lists,
+                                                         long long list_stride, int* __restrict__ counts, int fast_th,
+                                                         int min_th) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ int s_cnt[4];
+    __shared__ int scan_tmp[4];
+    const int cid = band_ids[blockIdx.x], f = blockIdx.y, tid = threadIdx.x;
+    const CellInfo ci = cells[cid];
+    const int dw = ci.w - 6, dh = ci.h - 6, BH = ci.band;
+    const int n = dw * dh, nwords = (n + 31) >> 5;
+    const int ndw = (dw + 6) >> 2, pitch = 4 * ndw;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
+    uint8_t* sc = smem + 16 * ((nwords + 3) / 4);              // (BH + 3) rows x pitch
+    uint8_t* rsh = sc + (BH + 3) * pitch;                      // BH + 3 row shifts
+    uint8_t* roi = rsh + ((BH + 3 + 15) & ~15);                // (BH + 8) ROI rows x ci.w (retry)
+    const int l = ci.level, lw = g.pw[l];
+    const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
+    int sstride;
+    const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
+    int total = 0, pass = 0;
+    for (; pass < 2; pass++) {
+        const int th = pass ? min_th : fast_th;
+        for (int i = tid; i < nwords; i += 256) bits[i] = 0;
+        total = 0;
+        for (int yb = 0; yb < dh; yb += BH) {
+            const int ye = min(yb + BH, dh), lo = max(yb - 1, 0), hi = min(ye + 1, dh), nr = hi - lo;
+            __syncthreads();  // the previous band's NMS reads are done
+            if (pass == 0) {
+                for (int i = tid; i < nr * ndw; i += 256) {
+                    const int r = i / ndw, q = i - r * ndw;
+                    const uintptr_t a = (uintptr_t)(SC + (long long)(lo + r) * lw);
+                    uint32_t v = 0;
+                    if (4 * q < (int)(a & 3) + dw) v = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
+                    reinterpret_cast<uint32_t*>(sc)[i] = v;
+                }
+                for (int r = tid; r < nr; r += 256) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)(lo + r) * lw) & 3);
+            } else {
+                // window row y's circle lies in ROI rows y .. y + 6
+                const int rr = nr + 6;
+                for (int i = tid; i < rr * ci.w; i += 256) {
+                    const int r = i / ci.w;
+                    roi[i] = gfd::ldg(Sl + (long long)(lo + r) * sstride + (i - r * ci.w));
+                }
+                __syncthreads();
+                for (int i = tid; i < nr * dw; i += 256) {
+                    const int y = i / dw, x = i - y * dw;
+                    int c[16];
+                    circle_vals(roi, ci.w, x + 3, y + 3, c);
+                    const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
+                    sc[y * pitch + x] = M > min_th ? (uint8_t)M : 0;
+                }
+                for (int r = tid; r < nr; r += 256) rsh[r] = 0;
+            }
+            if (tid == 0) rsh[nr] = 0;
+            for (int i = tid; i < ndw; i += 256) reinterpret_cast<uint32_t*>(sc + nr * pitch)[i] = 0u;
+            __syncthreads();
+            const int c = cell_nms_bits<4, true>(sc, rsh, pitch, bits, dw, dh, th, yb, ye, lo, nr);
+            if ((tid & 63) == 0) s_cnt[tid >> 6] = c;
+            __syncthreads();
+            total += s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        }
+        if (total > 3) break;  // else ORBextractor.cc:623-628: retry with the minimum threshold
+    }
+    if (pass == 2) pass = 1;
+    __syncthreads();
+    E* out = lists + (long long)f * list_stride + ci.cap_off;
+    const int X0 = ci.x0 + 3, Y0 = ci.y0 + 3;
+    int base = 0;
+    for (int w0 = 0; w0 < nwords; w0 += 256) {
+        const int i = w0 + tid;
+        uint32_t word = i < nwords ? bits[i] : 0u;
+        int tot;
+        int off = base + block_scan_nw<4>(__popc(word), scan_tmp, tot);
+        while (word) {
+            const int p = 32 * i + __ffs(word) - 1;
+            word &= word - 1;
+            const int y = p / dw, x = p - y * dw;
+            int S;
+            if (pass == 0) {
+                S = SC[(long long)y * lw + x] - 1;
+            } else {
+                int c[16];
+                circle_vals(Sl, sstride, x + 3, y + 3, c);
+                S = fast_max_arc(Sl[(long long)(y + 3) * sstride + x + 3], c) - 1;
+            }
+            out[off++] = cell_entry<E>(S, X0 + x, Y0 + y, P, g, f, l);
         }
         base += tot;
     }
@@ -766,13 +950,16 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
 // one wave's LDS list and partition scratch; wave 0's is SEL_BUF long, the
 // others' SEL_BUF_CELL (a cell's corners after NMS rarely pass 100), so the
 // workgroup takes 8 + 7 x 2 KB instead of 8 x 8 KB and more fit a CU
+template <typename E>
 struct SelWave {
-    uint32_t* a;
+    E* a;
     uint16_t *lp, *rp;
     int cap;
 };
-constexpr size_t sel_wave_bytes(int cap) { return (size_t)cap * (sizeof(uint32_t) + 2 * sizeof(uint16_t)); }
-constexpr size_t SEL_LDS = sel_wave_bytes(SEL_BUF) + (SEL_THREADS / 64 - 1) * sel_wave_bytes(SEL_BUF_CELL);
+template <typename E>
+constexpr size_t sel_wave_bytes(int cap) { return (size_t)cap * (sizeof(E) + 2 * sizeof(uint16_t)); }
+template <typename E>
+constexpr size_t sel_lds() { return sel_wave_bytes<E>(SEL_BUF) + (SEL_THREADS / 64 - 1) * sel_wave_bytes<E>(SEL_BUF_CELL); }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -780,10 +967,12 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int sel_resp(uint32_t e) { return (int)(e >> 24); }
+template <typename E>
+__device__ __forceinline__ int sel_resp(E e) { return Ent<E>::key(e); }
 
 // __unguarded_partition(a + lo, a + hi, a + pivot) with KeypointResponseGreater.
-__device__ __forceinline__ int wave_partition(const SelWave& W, int lo, int hi, int P) {
+template <typename E>
+__device__ __forceinline__ int wave_partition(const SelWave<E>& W, int lo, int hi, int P) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = (1ull << lane) - 1ull;
     int nL = 0, nR = 0;
@@ -808,7 +997,7 @@ __device__ __forceinline__ int wave_partition(const SelWave& W, int lo, int hi, 
     }
     for (int k = lane; k < ks; k += 64) {
         const int x = W.lp[k], y = W.rp[k];
-        const uint32_t ax = W.a[x], ay = W.a[y];
+        const E ax = W.a[x], ay = W.a[y];
         W.a[x] = ay;
         W.a[y] = ax;
     }
@@ -819,9 +1008,10 @@ __device__ __forceinline__ int wave_partition(const SelWave& W, int lo, int hi, 
 }
 
 // std::nth_element(a, a + nth, a + n) on the wave's LDS list, all lanes.
-__device__ __forceinline__ void wave_nth_element(const SelWave& W, int nth, int n) {
+template <typename E>
+__device__ __forceinline__ void wave_nth_element(const SelWave<E>& W, int nth, int n) {
     const int lane = threadIdx.x & 63;
-    const gfsel::RespGreater comp;
+    const EntGreater<E> comp;
     if (n == 0 || nth == n) return;
     int first = 0, last = n;
     int depth = 2 * gfsel::lg_(n);
@@ -849,7 +1039,8 @@ __device__ __forceinline__ void wave_nth_element(const SelWave& W, int nth, int 
 }
 
 // retainBest(list, keep) + truncation, written to dst[0 .. keep): one wave.
-__device__ __forceinline__ void wave_retain_to(const SelWave& W, uint32_t* list, int n, int keep, uint32_t* dst) {
+template <typename E>
+__device__ __forceinline__ void wave_retain_to(const SelWave<E>& W, E* list, int n, int keep, E* dst) {
     const int lane = threadIdx.x & 63;
     if (keep <= 0) return;
     if (n <= keep) {
@@ -857,7 +1048,7 @@ __device__ __forceinline__ void wave_retain_to(const SelWave& W, uint32_t* list,
         return;
     }
     if (n > W.cap) {  // sequential replay on global memory
-        if (lane == 0) gfsel::retain_best_truncate(list, n, keep, gfsel::RespGreater());
+        if (lane == 0) gfsel::retain_best_truncate(list, n, keep, EntGreater<E>());
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -870,20 +1061,22 @@ __device__ __forceinline__ void wave_retain_to(const SelWave& W, uint32_t* list,
     for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
 }
 
+template <typename E>
 __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
-                                                uint32_t* __restrict__ lists, long long list_stride,
-                                                const int* __restrict__ counts, uint32_t* __restrict__ lvl_lists,
+                                                E* __restrict__ lists, long long list_stride,
+                                                const int* __restrict__ counts, E* __restrict__ lvl_lists,
                                                 long long lvl_stride, int* __restrict__ lvl_counts) {
     __shared__ int cnt[SEL_MAX_CELLS], keep[SEL_MAX_CELLS], off[SEL_MAX_CELLS + 1];
     __shared__ char valid[SEL_MAX_CELLS];
     __shared__ int s_red[2];
     extern __shared__ __align__(16) uint8_t sel_dyn[];
     const int l = blockIdx.x, f = blockIdx.y, wv = threadIdx.x >> 6;
-    SelWave W;
+    SelWave<E> W;
     {
         const int cap = wv == 0 ? SEL_BUF : SEL_BUF_CELL;
-        uint8_t* base = sel_dyn + (wv == 0 ? 0 : sel_wave_bytes(SEL_BUF) + (wv - 1) * sel_wave_bytes(SEL_BUF_CELL));
-        W.a = reinterpret_cast<uint32_t*>(base);
+        uint8_t* base =
+            sel_dyn + (wv == 0 ? 0 : sel_wave_bytes<E>(SEL_BUF) + (wv - 1) * sel_wave_bytes<E>(SEL_BUF_CELL));
+        W.a = reinterpret_cast<E*>(base);
         W.lp = reinterpret_cast<uint16_t*>(W.a + cap);
         W.rp = W.lp + cap;
         W.cap = cap;
@@ -970,19 +1163,19 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
         }
     }
     __syncthreads();
-    uint32_t* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
+    E* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
     // a cell list longer than a cell wave's buffer that needs a selection
     // waits for wave 0's (larger) buffer, after wave 0's own cells
     auto deferred = [&](int c) { return SEL_BUF_CELL < SEL_BUF && cnt[c] > keep[c] && cnt[c] > SEL_BUF_CELL; };
     for (int c = wv; c < nc; c += SEL_THREADS / 64) {
         if (!valid[c] || (wv != 0 && deferred(c))) continue;
-        uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+        E* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
         wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
     }
     if (wv == 0 && SEL_BUF_CELL < SEL_BUF) {
         for (int c = 0; c < nc; c++) {
             if (c % (SEL_THREADS / 64) == 0 || !valid[c] || !deferred(c)) continue;
-            uint32_t* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
+            E* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
             wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
         }
     }
@@ -995,7 +1188,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellI
             wave_nth_element(W, nd - 1, total);
             for (int i = threadIdx.x; i < nd; i += 64) L[i] = W.a[i];
         } else if (threadIdx.x == 0) {
-            gfsel::retain_best_truncate(L, total, nd, gfsel::RespGreater());
+            gfsel::retain_best_truncate(L, total, nd, EntGreater<E>());
         }
         if (threadIdx.x == 0)
             lvl_counts[(long long)f * g.nlevels + l] = (nd < 0 || total <= nd) ? total : nd;
@@ -1056,7 +1249,8 @@ __device__ __forceinline__ int half_sum(int v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const uint32_t* __restrict__ lvl_lists,
+template <typename E>
+__global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E* __restrict__ lvl_lists,
                                                   long long lvl_stride, const int* __restrict__ lvl_counts,
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
@@ -1089,8 +1283,8 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
     if (__ballot(l >= 0) == 0) return;  // whole wave past the last keypoint
     const bool live = l >= 0;
     const int lv = live ? l : 0;
-    const uint32_t e = live ? lvl_lists[(long long)f * lvl_stride + g.lvl_off[lv] + idx] : 0u;
-    const int x = e & 0xfff, y = (e >> 12) & 0xfff, score = e >> 24;
+    const E e = live ? lvl_lists[(long long)f * lvl_stride + g.lvl_off[lv] + idx] : (E)0;
+    const int x = (int)(e & 0xfff), y = (int)((e >> 12) & 0xfff);
     const int w = g.w[lv], h = g.h[lv], pwl = g.pw[lv];
     int stride;
     const uint8_t* Pl = level_plane(P, g, f, lv, stride);
@@ -1193,7 +1387,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const u
         kp.y = l ? (float)y * s : (float)y;
         kp.size = (float)(int)(31 * s);
         kp.angle = angle;
-        kp.response = (float)score;
+        kp.response = Ent<E>::response(e);
         kp.octave = l;
         kp.class_id = -1;
         kps[(long long)f * cap + k] = kp;
@@ -1208,6 +1402,7 @@ struct gf_extractor {
     hipEvent_t stage_ev = nullptr;  // gf::extract_stage_event
     int stage_after = -1;
     int nfeatures = 0, nlevels = 0, fast_th = 20, min_th = 7, width = 0, height = 0, max_batch = 0;
+    bool harris = false;  // scoreType HARRIS_SCORE (0): u64 list entries carrying the Harris response
     float scale_factor = 1.2f;
     LevelGeom g{};
     std::vector<CellInfo> cells;
@@ -1215,6 +1410,9 @@ struct gf_extractor {
     int capacity = 0;
     long long list_stride = 0, lvl_stride = 0;
     size_t fast_lds = 0;
+    size_t band_lds = 0;           // k_fast_cells_band's LDS (0: no large cell)
+    std::vector<int> band_cells;   // cells whose window takes the banded kernel
+    int* d_band = nullptr;
     int max_tiles = 0;
     // device buffers
     uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
@@ -1222,7 +1420,7 @@ struct gf_extractor {
     std::vector<long long> xtab_off, ytab_off;
     std::vector<int> rs_pitch, rs_rows, rs_tiles_x, rs_tiles;
     CellInfo* d_cells = nullptr;
-    uint32_t *d_lists = nullptr, *d_lvl = nullptr;
+    void *d_lists = nullptr, *d_lvl = nullptr;  // uint32_t (FAST) or uint64_t (Harris) entries
     int *d_counts = nullptr, *d_lvl_counts = nullptr;
     // host-family staging
     uint8_t* d_img = nullptr;
@@ -1238,6 +1436,11 @@ static int cv_floor_f(float v) {
     int i = (int)v;
     return i - (i > v);
 }
+
+// k_fast_cells keeps a cell's whole window (score rows, retry ROI, survivor
+// bits) in LDS up to FC_LDS_MAX bytes; larger windows (small nFeatures) run
+// k_fast_cells_band within FC_BAND_LDS.
+constexpr size_t FC_LDS_MAX = 64 * 1024, FC_BAND_LDS = 120 * 1024;
 
 static int plan_extractor(gf_extractor* ex) {
     const int nl = ex->nlevels;
@@ -1292,6 +1495,8 @@ static int plan_extractor(gf_extractor* ex) {
 
     // ComputeKeyPoints cell grids (:540-618).
     ex->cells.clear();
+    ex->band_cells.clear();
+    ex->band_lds = 0;
     long long cap_off = 0, lvl_off = 0;
     size_t max_lds = 0;
     const float imageRatio = (float)g.w[0] / g.h[0];
@@ -1349,9 +1554,23 @@ static int plan_extractor(gf_extractor* ex) {
                         ci.cap_off = cap_off;
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
-                        size_t lds = ((size_t)dh + 1) * (4 * (size_t)((dw + 6) / 4)) + (((size_t)dh + 16) & ~(size_t)15) +
-                                     16 * (((size_t)dw * dh + 127) / 128) + (size_t)ci.w * ci.h;
-                        max_lds = std::max(max_lds, lds);
+                        const size_t pitch = 4 * (size_t)((dw + 6) / 4), bits = 16 * (((size_t)dw * dh + 127) / 128);
+                        size_t lds = ((size_t)dh + 1) * pitch + (((size_t)dh + 16) & ~(size_t)15) + bits +
+                                     (size_t)ci.w * ci.h;
+                        if (lds <= FC_LDS_MAX) {
+                            max_lds = std::max(max_lds, lds);
+                        } else {  // k_fast_cells_band: bands of BH rows (halo rows, ROI rows of the retry)
+                            auto band_lds = [&](size_t bh) {
+                                return bits + (bh + 3) * pitch + ((bh + 3 + 15) & ~(size_t)15) + (bh + 8) * ci.w;
+                            };
+                            size_t bh = std::min<size_t>(dh, 64);
+                            while (bh > 4 && band_lds(bh) > FC_BAND_LDS) bh /= 2;
+                            GF_CHECK(band_lds(bh) <= FC_BAND_LDS, GF_ERR_UNSUPPORTED,
+                                     "cell window too large even for the banded FAST kernel");
+                            ci.band = (int)bh;
+                            ex->band_cells.push_back((int)ex->cells.size());
+                            ex->band_lds = std::max(ex->band_lds, band_lds(bh));
+                        }
                         GF_CHECK(ci.x0 >= 0 && ci.y0 >= 0 && ci.x0 + ci.w <= g.w[l] && ci.y0 + ci.h <= g.h[l],
                                  GF_ERR_ARG, "cell ROI outside level");
                     }
@@ -1367,7 +1586,6 @@ static int plan_extractor(gf_extractor* ex) {
     ex->list_stride = cap_off;
     ex->lvl_stride = lvl_off;
     ex->fast_lds = max_lds;
-    GF_CHECK(max_lds <= 150 * 1024, GF_ERR_UNSUPPORTED, "cell ROI too large for LDS");
     ex->capacity = 0;
     for (int l = 0; l < nl; l++) ex->capacity += ex->feat_per_level[l];
     return GF_OK;
@@ -1404,6 +1622,7 @@ static void free_extractor(gf_extractor* ex) {
     (void)hipFree(ex->d_xtab);
     (void)hipFree(ex->d_ytab);
     (void)hipFree(ex->d_cells);
+    (void)hipFree(ex->d_band);
     (void)hipFree(ex->d_lists);
     (void)hipFree(ex->d_lvl);
     (void)hipFree(ex->d_counts);
@@ -1450,13 +1669,16 @@ static int upload_constants(int device) {
 
 static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* d_kps, uint8_t* d_desc,
                           int32_t* d_counts, int cap, void* stream);
+template <typename E>
+static int select_describe(gf_extractor* ex, int nframes, Planes P, gf_keypoint* d_kps, uint8_t* d_desc,
+                           int32_t* d_counts, int cap, hipStream_t s);
 
 extern "C" {
 
 int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlevels, int score_type, int fast_th,
                         int width, int height, int max_batch, gf_extractor** out) {
     GF_CHECK(ctx && out, GF_ERR_ARG, "null arg");
-    GF_CHECK(score_type == 1, GF_ERR_UNSUPPORTED, "only FAST_SCORE (1) is implemented");
+    GF_CHECK(score_type == 0 || score_type == 1, GF_ERR_ARG, "scoreType: 0 HARRIS_SCORE, 1 FAST_SCORE");
     GF_CHECK(nlevels >= 1 && nlevels <= GF_MAX_LEVELS, GF_ERR_ARG, "nlevels out of range");
     GF_CHECK(nfeatures > 0 && scale_factor > 1.f && width > 0 && height > 0 && max_batch > 0, GF_ERR_ARG,
              "bad extractor parameters");
@@ -1473,6 +1695,7 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     ex->width = width;
     ex->height = height;
     ex->max_batch = max_batch;
+    ex->harris = score_type == 0;
     rc = plan_extractor(ex);
     if (rc) {
         delete ex;
@@ -1491,8 +1714,10 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     ALLOC(ex->d_blur, g.bslab * max_batch);
     ALLOC(ex->d_score, g.bslab * max_batch);
     ALLOC(ex->d_cells, sizeof(CellInfo) * ex->cells.size());
-    ALLOC(ex->d_lists, sizeof(uint32_t) * ex->list_stride * max_batch);
-    ALLOC(ex->d_lvl, sizeof(uint32_t) * ex->lvl_stride * max_batch);
+    const size_t esz = ex->harris ? sizeof(uint64_t) : sizeof(uint32_t);
+    ALLOC(ex->d_lists, esz * ex->list_stride * max_batch);
+    ALLOC(ex->d_lvl, esz * ex->lvl_stride * max_batch);
+    ALLOC(ex->d_band, sizeof(int) * std::max<size_t>(ex->band_cells.size(), 1));
     ALLOC(ex->d_counts, sizeof(int) * g.ncells * max_batch);
     ALLOC(ex->d_lvl_counts, sizeof(int) * nlevels * max_batch);
     ALLOC(ex->d_img, (size_t)width * height);
@@ -1545,10 +1770,24 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
         GF_HIP(hipMemcpy(ex->d_ytab, yall.data(), sizeof(int2) * yall.size(), hipMemcpyHostToDevice));
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
-    GF_HIP(hipFuncSetAttribute((const void*)k_select, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)SEL_LDS));
-    GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)ex->fast_lds));
+    if (!ex->band_cells.empty())
+        GF_HIP(hipMemcpy(ex->d_band, ex->band_cells.data(), sizeof(int) * ex->band_cells.size(),
+                         hipMemcpyHostToDevice));
+    if (ex->harris) {
+        GF_HIP(hipFuncSetAttribute((const void*)k_select<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)sel_lds<uint64_t>()));
+        GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)ex->fast_lds));
+        GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint64_t>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex->band_lds));
+    } else {
+        GF_HIP(hipFuncSetAttribute((const void*)k_select<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)sel_lds<uint32_t>()));
+        GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)ex->fast_lds));
+        GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint32_t>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex->band_lds));
+    }
     *out = ex;
     return GF_OK;
 }
@@ -1620,24 +1859,38 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
         GF_LAUNCH(k_blur_fast, dim3(ex->max_tiles, nframes), 256, 0, s, P, g, ex->d_score, ex->fast_th);
     }
     if (ex->stage_ev && ex->stage_after == 1) GF_HIP(hipEventRecord(ex->stage_ev, s));
+    return ex->harris ? select_describe<uint64_t>(ex, nframes, P, d_kps, d_desc, d_counts, cap, s)
+                      : select_describe<uint32_t>(ex, nframes, P, d_kps, d_desc, d_counts, cap, s);
+}
+
+// k_fast_cells (+ k_fast_cells_band), k_select, k_describe on list entries E.
+template <typename E>
+static int select_describe(gf_extractor* ex, int nframes, Planes P, gf_keypoint* d_kps, uint8_t* d_desc,
+                           int32_t* d_counts, int cap, hipStream_t s) {
+    const LevelGeom& g = ex->g;
+    gf_ctx* ctx = ex->ctx;
+    E* lists = reinterpret_cast<E*>(ex->d_lists);
+    E* lvl = reinterpret_cast<E*>(ex->d_lvl);
     {
         GF_PROF(ctx, s, "k_fast_cells");
-        GF_LAUNCH(k_fast_cells, dim3(g.ncells, nframes), FC_NT, ex->fast_lds, s, 
-            P, g, ex->d_score, ex->d_cells, ex->d_lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
+        GF_LAUNCH(k_fast_cells<E>, dim3(g.ncells, nframes), FC_NT, ex->fast_lds, s, P, g, ex->d_score, ex->d_cells,
+                  lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
+        if (!ex->band_cells.empty())
+            GF_LAUNCH(k_fast_cells_band<E>, dim3((int)ex->band_cells.size(), nframes), 256, ex->band_lds, s, P, g,
+                      ex->d_score, ex->d_cells, ex->d_band, lists, ex->list_stride, ex->d_counts, ex->fast_th,
+                      ex->min_th);
     }
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
-        GF_LAUNCH(k_select, dim3(ex->nlevels, nframes), SEL_THREADS, SEL_LDS, s, g, ex->d_cells, ex->d_lists, ex->list_stride,
-                                                            ex->d_counts, ex->d_lvl, ex->lvl_stride,
-                                                            ex->d_lvl_counts);
+        GF_LAUNCH(k_select<E>, dim3(ex->nlevels, nframes), SEL_THREADS, sel_lds<E>(), s, g, ex->d_cells, lists,
+                  ex->list_stride, ex->d_counts, lvl, ex->lvl_stride, ex->d_lvl_counts);
     }
     if (ex->stage_ev && ex->stage_after == 3) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_describe");
-        GF_LAUNCH(k_describe, dim3((ex->capacity + 7) / 8, nframes), 256, 0, s, P, g, ex->d_lvl, ex->lvl_stride,
-                                                                          ex->d_lvl_counts, d_kps, d_desc, d_counts,
-                                                                          cap);
+        GF_LAUNCH(k_describe<E>, dim3((ex->capacity + 7) / 8, nframes), 256, 0, s, P, g, lvl, ex->lvl_stride,
+                  ex->d_lvl_counts, d_kps, d_desc, d_counts, cap);
     }
     if (ex->stage_ev && ex->stage_after == 4) GF_HIP(hipEventRecord(ex->stage_ev, s));
     GF_HIP(hipGetLastError());

@@ -1062,7 +1062,7 @@ int gf_frontend_create(gf_ctx* ctx, const gf_frontend_params* p, gf_frontend** o
     gf_frontend* fe = new gf_frontend();
     fe->ctx = ctx;
     fe->p = *p;
-    int rc = gf_extractor_create(ctx, p->nfeatures, p->scale_factor, p->nlevels, 1, p->fast_th, p->width, p->height,
+    int rc = gf_extractor_create(ctx, p->nfeatures, p->scale_factor, p->nlevels, p->harris_score ? 0 : 1, p->fast_th, p->width, p->height,
                                  p->batch, &fe->ex);
     if (rc) {
         delete fe;

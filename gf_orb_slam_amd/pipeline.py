@@ -102,17 +102,20 @@ class FrontendParams(ctypes.Structure):
                 ("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int32),
                 ("fast_th", ctypes.c_int32), ("batch", ctypes.c_int32), ("map_cap", ctypes.c_int32),
                 ("gf_budget", ctypes.c_int32), ("gf", ctypes.c_int32), ("dt", ctypes.c_double),
-                ("dist", ctypes.c_float * 5), ("max_frames", ctypes.c_int32)]
+                ("dist", ctypes.c_float * 5), ("max_frames", ctypes.c_int32), ("harris_score", ctypes.c_int32)]
 
     @classmethod
     def make(cls, camera: str, nfeatures: int, batch: int, map_cap: int, gf_budget: int, gf: bool = True,
-             fps: float = 20.0, nlevels: int = 8, scale_factor: float = 1.2, fast_th: int = 20, dist=None):
-        """dist: Camera.k1 k2 p1 p2 [k3] (None / k1 = 0: keypoints used as extracted)."""
+             fps: float = 20.0, nlevels: int = 8, scale_factor: float = 1.2, fast_th: int = 20, dist=None,
+             score_type: int = 1):
+        """dist: Camera.k1 k2 p1 p2 [k3] (None / k1 = 0: keypoints used as extracted);
+        score_type: ORBextractor.nScoreType (1 FAST_SCORE, 0 HARRIS_SCORE)."""
         w, h, fx, fy, cx, cy = synth.CAMERAS[camera]
         d = list(dist or ()) + [0.0] * (5 - len(dist or ()))
         # mMaxFrames = 18 * camera_fps / 30 (Tracking.cc:153; int of a double)
         return cls(w, h, fx, fy, cx, cy, nfeatures, scale_factor, nlevels, fast_th, batch, map_cap, gf_budget,
-                   1 if gf else 0, 1.0 / fps, (ctypes.c_float * 5)(*d), int(18 * fps / 30))
+                   1 if gf else 0, 1.0 / fps, (ctypes.c_float * 5)(*d), int(18 * fps / 30),
+                   1 if score_type == 0 else 0)
 
 
 def field_shape(name: str, B: int, cap: int, M: int, R: int = 1):
@@ -194,8 +197,10 @@ class FrontEnd:
     """B independent streams, one frame each per step."""
 
     def __init__(self, camera: str = "euroc", nfeatures: int = 1000, batch: int = 1, map_size: int = 2000,
-                 gf_budget: int = 100, gf: bool = True, fps: float = 20.0, ctx: Context | None = None, dist=None):
-        self.params = FrontendParams.make(camera, nfeatures, batch, map_size, gf_budget, gf, fps, dist=dist)
+                 gf_budget: int = 100, gf: bool = True, fps: float = 20.0, ctx: Context | None = None, dist=None,
+                 score_type: int = 1):
+        self.params = FrontendParams.make(camera, nfeatures, batch, map_size, gf_budget, gf, fps, dist=dist,
+                                          score_type=score_type)
         self.cam = synth.CAMERAS[camera]
         self.B, self.M = batch, map_size
         self.R = max(gf_budget, 1)

@@ -65,7 +65,7 @@ int gf_prof_report(gf_ctx* ctx, int idx, char* name, int name_cap, double* total
  * src/ORBextractor.cc:464-998): ctor(nfeatures, scaleFactor, nlevels,
  * scoreType, fastTh) and operator()(image, mask=empty, keypoints, descriptors).
  * The geometry (width x height) is fixed at creation: the pyramid, cell grids
- * and per-level quotas are planned once. score_type must be FAST_SCORE (1);
+ * and per-level quotas are planned once. score_type: FAST_SCORE (1) or HARRIS_SCORE (0);
  * HARRIS_SCORE (0) returns GF_ERR_UNSUPPORTED. max_batch bounds nframes of the
  * batched device call. */
 int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlevels,
@@ -892,6 +892,8 @@ typedef struct gf_frontend_params {
     int32_t max_frames;         /* mMaxFrames = 18 * Camera.fps / 30 (Tracking.cc:153), the
                                    window of TrackLocalMap's stricter inlier rule after a
                                    relocalisation; 0: derived from dt */
+    int32_t harris_score;       /* 1: ORBextractor.nScoreType = HARRIS_SCORE (0; Tracking.cc:186),
+                                   0: FAST_SCORE (1, the settings' default) */
 } gf_frontend_params;
 typedef struct gf_frontend gf_frontend;
 

@@ -24,6 +24,8 @@
 #include "oracle_common.h"
 
 extern "C" {
+int orc_extract_st(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
+                   int score_type, int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out);
 int orc_extract(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
                 int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out);
 int orc_extractor_plan(int w, int h, int nfeatures, float scale_factor, int nlevels, int* level_w, int* level_h,
@@ -642,8 +644,9 @@ int orc_chain_set_rng(orc_chain* c, uint32_t seed) {
 
 static int extract(orc_chain* c, const uint8_t* img) {
     int n = 0;
-    int rc = orc_extract(img, c->p.width, c->p.height, c->p.width, c->p.nfeatures, c->p.scale_factor, c->p.nlevels,
-                         c->p.fast_th, c->kps.data(), c->desc.data(), c->cap, &n);
+    int rc = orc_extract_st(img, c->p.width, c->p.height, c->p.width, c->p.nfeatures, c->p.scale_factor,
+                            c->p.nlevels, c->p.harris_score ? 0 : 1, c->p.fast_th, c->kps.data(), c->desc.data(),
+                            c->cap, &n);
     c->nkp = n;
     // mvKeysUn (Frame::UndistortKeyPoints, Frame.cc:389-423; a copy when k1 == 0)
     const float K[4] = {c->p.fx, c->p.fy, c->p.cx, c->p.cy};

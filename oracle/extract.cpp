@@ -24,6 +24,7 @@ struct KP {  // cv::KeyPoint
 
 struct ExtractorPlan {
     int nfeatures, nlevels, fastTh, minTh = 7;
+    int scoreType = 1;  // ORB::HARRIS_SCORE 0, ORB::FAST_SCORE 1 (ORBextractor.h:57)
     double scaleFactor;  // ORBextractor.h:79 stores it as double
     std::vector<float> scale, invScale;
     std::vector<int> featPerLevel;
@@ -306,6 +307,34 @@ static void fast_roi(const Image& im, int x0, int y0, int w, int h, int th, std:
         }
 }
 
+// HarrisResponses(cellImage, keypoints, 7, HARRIS_K), ORBextractor.cc:86-127,
+// called per cell when scoreType == HARRIS_SCORE (:667-670): keypoints are in
+// cell coordinates, the ROI (x0, y0) of the level; every read lies inside the
+// level (the cell ROI starts 13 px in, the block reaches 4 px out).
+static void harris_responses(const Image& im, int x0, int y0, std::vector<KP>& pts) {
+    const int blockSize = 7, r = blockSize / 2;
+    const int step = im.w;
+    float scale = (1 << 2) * blockSize * 255.0f;
+    scale = 1.0f / scale;
+    const float scale_sq_sq = scale * scale * scale * scale;
+    const float harris_k = 0.04f;  // HARRIS_K, ORBextractor.cc:80
+    for (KP& k : pts) {
+        const int bx = cv_round(k.x - r), by = cv_round(k.y - r);
+        const uint8_t* ptr0 = &im.px[(size_t)(y0 + by) * step + (x0 + bx)];
+        int a = 0, b = 0, c = 0;
+        for (int i = 0; i < blockSize; i++)
+            for (int j = 0; j < blockSize; j++) {
+                const uint8_t* ptr = ptr0 + i * step + j;
+                const int Ix = (ptr[1] - ptr[-1]) * 2 + (ptr[-step + 1] - ptr[-step - 1]) + (ptr[step + 1] - ptr[step - 1]);
+                const int Iy = (ptr[step] - ptr[-step]) * 2 + (ptr[step - 1] - ptr[-step - 1]) + (ptr[step + 1] - ptr[-step + 1]);
+                a += Ix * Ix;
+                b += Iy * Iy;
+                c += Ix * Iy;
+            }
+        k.response = ((float)a * b - (float)c * c - harris_k * ((float)a + b) * ((float)a + b)) * scale_sq_sq;
+    }
+}
+
 // KeyPointsFilter::retainBest (OpenCV 3.4 keypoint.cpp): nth_element at
 // n_points-1 with KeypointResponseGreater, then the tie-keeping partition.
 struct RespGreater {
@@ -459,6 +488,7 @@ static void extract(const ExtractorPlan& P, const Image& img, ExtractResult& R) 
                     ck.clear();
                     fast_roi(L, (int)iniX, (int)iniY, (int)hX, (int)hY, P.minTh, ck);
                 }
+                if (P.scoreType == 0) harris_responses(L, (int)iniX, (int)iniY, ck);
                 const int nKeys = (int)ck.size();
                 nTotal[i * levelCols + j] = nKeys;
                 if (nKeys > nfCell) {
@@ -536,9 +566,11 @@ static void extract(const ExtractorPlan& P, const Image& img, ExtractResult& R) 
 // ---------------------------------------------------------------- C API
 extern "C" {
 
-int orc_extract(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
-                int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+int orc_extract_st(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
+                   int score_type, int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
     orc::ExtractorPlan P(nfeatures, scale_factor, nlevels, fast_th);
+    if (score_type != 0 && score_type != 1) return GF_ERR_ARG;
+    P.scoreType = score_type;
     orc::Image im;
     im.w = w;
     im.h = h;
@@ -555,6 +587,11 @@ int orc_extract(const uint8_t* img, int w, int h, int stride, int nfeatures, flo
     }
     if (n) std::memcpy(desc, R.desc.data(), (size_t)n * 32);
     return GF_OK;
+}
+
+int orc_extract(const uint8_t* img, int w, int h, int stride, int nfeatures, float scale_factor, int nlevels,
+                int fast_th, gf_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+    return orc_extract_st(img, w, h, stride, nfeatures, scale_factor, nlevels, 1, fast_th, kps, desc, cap, n_out);
 }
 
 // Plan tables: level sizes (w,h), quotas, scale factors.

@@ -48,8 +48,9 @@ class Chain:
     """One stream of the front end on the CPU oracle."""
 
     def __init__(self, camera: str, nfeatures: int, map_size: int, gf_budget: int, gf: bool = True,
-                 fps: float = 20.0, dist=None):
-        self.params = FrontendParams.make(camera, nfeatures, 1, map_size, gf_budget, gf, fps, dist=dist)
+                 fps: float = 20.0, dist=None, score_type: int = 1):
+        self.params = FrontendParams.make(camera, nfeatures, 1, map_size, gf_budget, gf, fps, dist=dist,
+                                          score_type=score_type)
         self.h = _orc().orc_chain_create(ctypes.byref(self.params))
         self.cap = _orc().orc_chain_capacity(self.h)
         self.M = map_size

@@ -29,15 +29,17 @@ def _p(a):
     return ctypes.c_void_p(a.ctypes.data) if a is not None else None
 
 
-def extract(img: np.ndarray, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20):
+def extract(img: np.ndarray, nfeatures=1000, scale=1.2, nlevels=8, fast_th=20, score_type=1):
+    """ORBextractor(nfeatures, scale, nlevels, score_type, fast_th)(img): score_type
+    1 FAST_SCORE, 0 HARRIS_SCORE (ORBextractor.h:57)."""
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     cap = nfeatures + 64
     kps = np.zeros(cap, KEYPOINT_DTYPE)
     desc = np.zeros((cap, 32), np.uint8)
     n = ctypes.c_int()
-    rc = orc().orc_extract(_p(img), w, h, w, nfeatures, ctypes.c_float(scale), nlevels, fast_th, _p(kps),
-                           _p(desc), cap, ctypes.byref(n))
+    rc = orc().orc_extract_st(_p(img), w, h, w, nfeatures, ctypes.c_float(scale), nlevels, score_type, fast_th,
+                              _p(kps), _p(desc), cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
 

@@ -86,7 +86,46 @@ def test_fast_threshold_edges(fast_th):
     assert np.array_equal(dg, do)
 
 
-@pytest.mark.parametrize("nf", [500, 1000])
+@pytest.mark.parametrize("cam", ["euroc", "tum"])
+@pytest.mark.parametrize("score_type", [1, 0])
+@pytest.mark.parametrize("nf", [150, 200, 250, 500, 1000, 2000])
+def test_nfeatures_and_score_type(nf, score_type, cam):
+    """The reference's nFeatures range and both score types (ORBextractor.h:57,
+    ORBextractor.nScoreType in the settings, Tracking.cc:186): few features
+    make few, large cells (752x480 at 200 features: windows of ~360x150 px at
+    level 0) whose window runs k_fast_cells_band in row bands; HARRIS_SCORE (0)
+    replaces each FAST corner's response by HarrisResponses (ORBextractor.cc
+    :86-127, 667-670) before retainBest. Bit-exact keypoints (responses
+    included) and descriptors. Harris: parity unpinned (no reference fixture;
+    docs/ORACLE_ASSUMPTIONS.md A21)."""
+    img = _frame(cam, 40 + nf % 7)
+    kg, dg = ORBextractor(nf, 1.2, 8, score_type, 20)(img)
+    ko, do = O.extract(img, nfeatures=nf, score_type=score_type)
+    assert len(ko) > 0.8 * nf
+    assert kg.tobytes() == ko.tobytes(), _diff_report(kg, ko)
+    assert np.array_equal(dg, do)
+    if score_type == 0:
+        assert np.any(ko["response"] != np.round(ko["response"]))  # Harris responses, not FAST scores
+
+
+@pytest.mark.parametrize("score_type", [1, 0])
+def test_banded_cells_threshold_fallback(score_type):
+    """Large cells (200 features) on a flat image with weak texture: every
+    banded window falls back to the minimum threshold (the retry pass
+    recomputes the scores band by band from the level) and quotas
+    redistribute (ORBextractor.cc:623-628, 695-721)."""
+    rng = np.random.default_rng(6)
+    img = np.full((480, 752), 128, np.uint8)
+    img += rng.integers(0, 12, img.shape, dtype=np.uint8)
+    img[100:140, 200:260] = 40
+    img[300:330, 500:600] = 200
+    kg, dg = ORBextractor(200, 1.2, 8, score_type, 20)(img)
+    ko, do = O.extract(img, nfeatures=200, score_type=score_type)
+    assert kg.tobytes() == ko.tobytes(), _diff_report(kg, ko)
+    assert np.array_equal(dg, do)
+
+
+@pytest.mark.parametrize("nf", [200, 500, 1000])
 def test_long_cell_lists(nf):
     """Dense corners: uniform noise whose contrast ramps across the image,
     so a cell's corner list after NMS spans from none to thousands (cells of

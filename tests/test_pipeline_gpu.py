@@ -25,15 +25,15 @@ F64 = ["Xv", "Xv_next", "base", "mp_H", "mp_info", "mp_uv"]
 STATE = C.Chain.STATE + ["stats"]
 
 
-def _setup(camera, nfeat, B, nmap, budget, gf=True, seed=3, n_scenes=2, stale=0.0, dist=None):
+def _setup(camera, nfeat, B, nmap, budget, gf=True, seed=3, n_scenes=2, stale=0.0, dist=None, score_type=1):
     import torch
 
     from gf_orb_slam_amd.pipeline import FrontEnd
 
     W = scene.Workload(camera, B, n_scenes=n_scenes, period=32, seed=seed, stale_desc=stale, dist=dist)
     frames = W.render_all("cuda").contiguous()
-    maps = W.build_maps(lambda im: O.extract(im, nfeatures=nfeat), nmap)
-    fe = FrontEnd(camera, nfeat, B, nmap, budget, gf=gf, dist=dist)
+    maps = W.build_maps(lambda im: O.extract(im, nfeatures=nfeat, score_type=score_type), nmap)
+    fe = FrontEnd(camera, nfeat, B, nmap, budget, gf=gf, dist=dist, score_type=score_type)
     for b in range(B):
         fe.set_map(b, *maps[W.scene_of[b]])
         fe.set_rng(b, 1 + seed * 1000 + b)
@@ -86,6 +86,8 @@ CASES = {
     # step): EuRoC cam0's k1 k2 p1 p2, TUM fr2's five coefficients
     "config2_dist": ("euroc", 1000, 4, 2000, 100, True, 0.93, synth.DISTORTION["euroc"]),
     "config3_dist": ("tum", 2000, 3, 3000, 160, True, 0.0, synth.DISTORTION["tum"]),
+    # ORBextractor.nScoreType = HARRIS_SCORE (0) in the settings; 500 features
+    "config2_harris": ("euroc", 500, 3, 2000, 100, True, 0.93, None, 0),
 }
 
 
@@ -94,10 +96,11 @@ CASES = {
 def test_sequence_matches_oracle(case):
     camera, nfeat, B, nmap, budget, gf, stale = CASES[case][:7]
     dist = CASES[case][7] if len(CASES[case]) > 7 else None
-    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf, stale=stale, dist=dist)
+    st = CASES[case][8] if len(CASES[case]) > 8 else 1
+    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf, stale=stale, dist=dist, score_type=st)
     free = []
     for b in range(B):
-        ch = C.Chain(camera, nfeat, nmap, budget, gf, dist=dist)
+        ch = C.Chain(camera, nfeat, nmap, budget, gf, dist=dist, score_type=st)
         ch.set_map(*maps[W.scene_of[b]])
         ch.set_rng(1 + 3 * 1000 + b)
         ch.bootstrap(_img(W, frames, b, 0), T[b], V[b])
@@ -113,7 +116,7 @@ def test_sequence_matches_oracle(case):
         fe.step()
         dev = C.read_state(fe)
         for b in range(B):
-            ch = C.Chain(camera, nfeat, nmap, budget, gf, dist=dist)
+            ch = C.Chain(camera, nfeat, nmap, budget, gf, dist=dist, score_type=st)
             ch.load_from(before, b)
             ch.step(_img(W, frames, b, k))
             _compare(dev, ch, b, f"step {k}: ")
