@@ -100,6 +100,10 @@ struct StageClock {
     long long* rec = nullptr;
     long long stride = 0;
     int off = 0;
+    // test clock (gf_frontend_set_test_clock): the site's (base, slope) pair
+    // (for the budget matcher two pairs: its start, then its points); null:
+    // the device clock
+    const long long* syn = nullptr;
 };
 
 // batchInfoMat_Map with its time cap (Observability.cc:564-578) when ck.t0 is
@@ -123,6 +127,7 @@ struct ActiveClock {
     long long stride = 0;
     int off = 0;    // per-round array
     int rounds = 0; // its length
+    const long long* syn = nullptr;  // test clock: (base, slope) of the start, then of the rounds
 };
 
 // Frame::isInFrustum over a map (d_list null: points < d_m[f]) or over a list,
@@ -232,6 +237,13 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipSt
 
 // Device-side helpers ------------------------------------------------------
 namespace gfd {
+
+// Elapsed ticks at a budget's clock check: the device clock (s_memrealtime,
+// 100 MHz) since t0, or with a test clock (syn = the site's base and slope,
+// gf_frontend_set_test_clock) base + idx * slope for the idx-th check.
+__device__ __forceinline__ long long ck_elapsed(unsigned long long t0, const long long* syn, int idx) {
+    return syn ? syn[0] + (long long)idx * syn[1] : (long long)(__builtin_amdgcn_s_memrealtime() - t0);
+}
 
 // XCD-aware workgroup order (cdna_hip_programming.md T1, bijective form):
 // the dispatcher hands consecutive workgroups to the 8 XCDs in turn, so

@@ -106,6 +106,7 @@ struct FeDev {
     int32_t* ncut;         // [B] points the isInFrustum cap moved to mLeftMapPoints
     int32_t* nlist0;       // [B] mLeftMapPoints size before SearchAdditionalMatchesInFrame
     // the tracking state machine (GF_FE_TRACK) and the per-stream gates of its stages
+    const long long* syn; // test clock [GF_CK_NSITE][2] (gf_frontend_set_test_clock); null: the device clock
     int32_t* track;        // [B][GF_TR_N]
     int32_t* m3_nlast;     // [B] last-frame points SearchByProjection(Cur, Last) projects (0 off the motion model)
     int32_t* rl_gate;      // [B] 1: Relocalisation this step
@@ -415,7 +416,8 @@ __global__ __launch_bounds__(256) void k_fe_post(FeDev D) {
         // RunMapPointsSelection and SearchAdditionalMatchesInFrame, whose
         // timers start here
         const unsigned long long now = now_ticks();
-        const long long sofar = (long long)(now - D.t_frame[b]), rest = D.select_ticks - sofar;
+        const long long sofar = D.syn ? D.syn[2 * GF_CK_SITE_SOFAR] : (long long)(now - D.t_frame[b]);
+        const long long rest = D.select_ticks - sofar;
         ck_rec(D, b)[GF_CK_SOFAR] = sofar;
         D.rest2[b] = 2 * rest;
         D.cap2_sel[b] = rest > 0 ? 2 * rest : -1;  // <= 0: "too little budget available" (:1727-1731)
@@ -793,6 +795,7 @@ struct gf_frontend {
     gf::KfdbDev* d_kfdb = nullptr;
     std::vector<int32_t> h_kfc;
     int32_t* d_kfc = nullptr;
+    long long* d_syn = nullptr;  // gf_frontend_set_test_clock's (base, slope) pairs
     std::vector<std::vector<int32_t>> h_slots;  // per stream: the graph's slots per keyframe
     void* bow_tmp = nullptr;
 };
@@ -937,18 +940,19 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
         GF_HIP(hipGetLastError());
     }
     const bool mclk = D.gf && D.match_ticks >= 0, sclk = D.gf && D.select_ticks >= 0;
-    auto clock = [&](const unsigned long long* t0, int off) {
+    auto clock = [&](const unsigned long long* t0, int off, int site) {
         gf::StageClock c;
         c.t0 = t0;
         c.rec = D.clk;
         c.stride = D.ck_stride;
         c.off = off;
+        c.syn = D.syn ? D.syn + 2 * site : nullptr;
         return c;
     };
     const int R = D.ck_R;
     if (mclk) {  // the isInFrustum loop on its clock (k_fe_decide applies the cap)
         FE_RC(gf::frustum_clocked(ctx, fi, B, D.Tcw, D.map, D.m_frustum, nullptr, nullptr, M, 0.5f, D.views,
-                                  fe->nview, clock(D.t_viz0, GF_CK_OFF_VIZ(M, R)), D.vtmp, s));
+                                  fe->nview, clock(D.t_viz0, GF_CK_OFF_VIZ(M, R), GF_CK_SITE_VIZ), D.vtmp, s));
     } else {
         FE_RC(gf_frustum_dev(ctx, fi, B, D.Tcw, D.map, D.m_frustum, M, 0.5f, D.views, fe->nview, s));
     }
@@ -960,7 +964,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
     if (D.gf) {
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
                                fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s,
-                               mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R)) : gf::StageClock{}, D.cap2_mi,
+                               mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R), GF_CK_SITE_MI) : gf::StageClock{}, D.cap2_mi,
                                fe->mp_info_lt));
         gf::ActiveClock ac;
         if (mclk) {
@@ -971,6 +975,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
             ac.stride = D.ck_stride;
             ac.off = GF_CK_OFF_AM(M, R);
             ac.rounds = R;
+            ac.syn = D.syn ? D.syn + 2 * GF_CK_SITE_AM_START : nullptr;
         }
         FE_RC(gf::obs_active_match(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, fe->mp_updated,
                                    fe->mp_info, fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2,
@@ -1002,13 +1007,13 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
                                    sp));
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv_next, fe->mp_pos, D.nmp_post, M, 1, nullptr, D.upd, 2,
                                fe->mp_H, fe->mp_info, fe->mp_uv, nullptr, rmp, sp,
-                               sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R)) : gf::StageClock{}, D.cap2_sel,
+                               sclk ? clock(D.t_sel0, GF_CK_OFF_SEL(M, R), GF_CK_SITE_SEL) : gf::StageClock{}, D.cap2_sel,
                                fe->mp_info_lt));
         if (fe->fork_post) GF_HIP(hipEventRecord(fe->ev_join, sp));
         // SearchAdditionalMatchesInFrame
         if (sclk) {
             FE_RC(gf::frustum_clocked(ctx, fi, B, D.Tcw, D.map, nullptr, D.left, D.nlist_viz, M, 0.5f, D.views,
-                                      fe->nview, clock(D.t_sel0, GF_CK_OFF_SA(M, R)), D.vtmp, s));
+                                      fe->nview, clock(D.t_sel0, GF_CK_OFF_SA(M, R), GF_CK_SITE_SA), D.vtmp, s));
         } else {
             FE_RC(gf_frustum_list_dev(ctx, fi, B, D.Tcw, D.map, M, D.left, D.nlist_viz, 0.5f, D.views, fe->nview,
                                       s));
@@ -1020,7 +1025,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
         }
         FE_RC(gf::match_project_list_budget(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, M, D.left,
                                             D.nlist, 0.8f, 0.8f, D.kp2mp, D.score, col(GF_ST_EXTRA),
-                                            sclk ? clock(D.t_sel0, GF_CK_OFF_BUD(M, R)) : gf::StageClock{},
+                                            sclk ? clock(D.t_sel0, GF_CK_OFF_BUD(M, R), GF_CK_SITE_SA_SOFAR) : gf::StageClock{},
                                             D.rest2, fe->qres, fe->qold, fe->merr, s));
         if (fe->fork_post) GF_HIP(hipStreamWaitEvent(s, fe->ev_join, 0));  // thread_Select.join()
     }
@@ -1859,6 +1864,25 @@ int gf_frontend_write(gf_frontend* fe, int field, const void* host, size_t bytes
             for (int c = 0; c < 3; c++) pos[3 * i + c] = m[i].pos[c];
         GF_HIP(hipMemcpy((float*)fe->gm.pos, pos.data(), 12 * n, hipMemcpyHostToDevice));
     }
+    return GF_OK;
+}
+
+int gf_frontend_set_test_clock(gf_frontend* fe, const long long* base_slope) {
+    GF_CHECK(fe, GF_ERR_ARG, "null front end");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set the test clock before capturing a graph");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    if (!base_slope) {
+        fe->D.syn = nullptr;
+        return GF_OK;
+    }
+    if (!fe->d_syn) {
+        void* p;
+        FE_RC(fe_alloc(fe, sizeof(long long) * 2 * GF_CK_NSITE, &p));
+        fe->d_syn = (long long*)p;
+    }
+    GF_HIP(hipMemcpy(fe->d_syn, base_slope, sizeof(long long) * 2 * GF_CK_NSITE, hipMemcpyHostToDevice));
+    fe->D.syn = fe->d_syn;
     return GF_OK;
 }
 

@@ -993,7 +993,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     long long* rec = clocked ? A.ck.rec + (long long)f * A.ck.stride : nullptr;
     if (clocked) {
         t_am0 = __builtin_amdgcn_s_memrealtime();
-        const long long mat = (long long)(t_am0 - A.ck.mat_t0[f]);
+        const long long mat = A.ck.syn ? A.ck.syn[0] : (long long)(t_am0 - A.ck.mat_t0[f]);
         am_cap = A.ck.match_ticks - mat - A.ck.viz[f];
         if (lane == 0) {
             rec[GF_CK_MAT_ONLINE] = mat;
@@ -1100,7 +1100,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             // after each accepted draw (Observability.cc:1362-1370), so a late
             // round ends at its first accepted draw: matches so far stand, no
             // leftovers (the return skips mLeftMapPoints)
-            const long long e = (long long)(__builtin_amdgcn_s_memrealtime() - t_am0);
+            const long long e = gfd::ck_elapsed(t_am0, A.ck.syn ? A.ck.syn + 2 : nullptr, round);
             if (lane == 0 && round < A.ck.rounds) rec[A.ck.off + round] = e;
             if (e > am_cap) {
                 uint32_t sd = rs, s0, o0;
@@ -2259,7 +2259,7 @@ __global__ void k_obs_map_info(gf_obs_camera cam, const double* __restrict__ Xv,
     if (ck.t0) {  // the time cap, one clock read per 64-point batch (Observability.cc:573-578)
         const int w = i >> 6;
         if (w * 64 < nmp[f]) {
-            const long long e = (long long)(__builtin_amdgcn_s_memrealtime() - ck.t0[f]);
+            const long long e = gfd::ck_elapsed(ck.t0[f], ck.syn, w);
             if ((threadIdx.x & 63) == 0) ck.rec[(long long)f * ck.stride + ck.off + w] = e;
             late = 2 * e > cap2[f];
         }

@@ -70,6 +70,7 @@ struct MatchArgs {
     long long* ck_rec;
     long long ck_stride;
     int ck_off;       // offset of the per-point array in a stream's record
+    const long long* ck_syn;  // test clock: (base, slope) of the start, then of the points; null: device clock
     int32_t* ck_old;  // [F][q_cap] score a query's claim overwrote
     // candidates the windows list (GetFeaturesInArea sizes), added to
     // ncand[f] (SURVEY §8d B_match's C); null: not counted
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     if (clocked) {
         if (tid == 0) {
             const unsigned long long now0 = __builtin_amdgcn_s_memrealtime();
-            const long long so_far = (long long)(now0 - A.ck_t0[f]);
+            const long long so_far = A.ck_syn ? A.ck_syn[0] : (long long)(now0 - A.ck_t0[f]);
             s_now0 = now0;
             s_constr2 = A.ck_rest2[f] - 2 * so_far;
             s_cut = INT_MAX;
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
         __syncthreads();
         for (int k = tid; k < nq; k += MATCH_THREADS) {
             if (clocked && rounds == 0)  // per point, from the matcher's start
-                rec[A.ck_off + k] = (long long)(__builtin_amdgcn_s_memrealtime() - s_now0);
+                rec[A.ck_off + k] = gfd::ck_elapsed(s_now0, A.ck_syn ? A.ck_syn + 2 : nullptr, k);
             if (done[k]) continue;
             const Query q = make_query(A, fc, f, k);
             if (!q.valid) continue;
@@ -799,6 +800,7 @@ struct FrustumClock {
     long long stride;
     int off;
     gf_mp_view* alt;
+    const long long* syn;  // test clock (base, slope); null: the device clock
 };
 
 __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf_map_point* __restrict__ mps,
@@ -811,7 +813,7 @@ __global__ void k_frustum(FrameConst fc, const float* __restrict__ Tcw, const gf
     int in = 0;
     const bool run = list ? i < nlist[f] : i < m[f];
     if (run && ck.t0) {
-        ck.rec[(long long)f * ck.stride + ck.off + i] = (long long)(__builtin_amdgcn_s_memrealtime() - ck.t0[f]);
+        ck.rec[(long long)f * ck.stride + ck.off + i] = gfd::ck_elapsed(ck.t0[f], ck.syn, i);
         views = ck.alt;
     }
     if (run && list) i = list[(long long)f * cap + i];  // the list's map point
@@ -1234,7 +1236,7 @@ int gf::frustum_clocked(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const
     const FrameConst fc = gf::make_frame_const(fi);
     GF_HIP(hipMemsetAsync(d_nview, 0, sizeof(int32_t) * nframes, s));
     GF_PROF(ctx, s, d_list ? "k_frustum_list" : "k_frustum");
-    const FrustumClock fk{ck.t0, ck.rec, ck.stride, ck.off, d_alt};
+    const FrustumClock fk{ck.t0, ck.rec, ck.stride, ck.off, d_alt, ck.syn};
     GF_LAUNCH(k_frustum, dim3((mp_cap + 255) / 256, nframes), 256, 0, s, fc, d_Tcw, d_mps, d_m, mp_cap, view_cos_limit,
                                                                    d_views, d_nview, d_list, d_nlist,
                                                                    ck.t0 ? fk : FrustumClock{});
@@ -1278,6 +1280,7 @@ int gf::match_project_list_budget(gf_ctx* ctx, const gf_frame_info* fi, int nfra
         A.ck_rec = ck.rec;
         A.ck_stride = ck.stride;
         A.ck_off = ck.off;
+        A.ck_syn = ck.syn;
         A.ck_old = d_old;
         A.qres = d_qres;
     }

@@ -84,6 +84,8 @@ NSTAT = len(STATS)
 CK = {"flags": 0, "match": 1, "select": 2, "viz_cut": 3, "viz_time": 4, "mat_online": 5, "am_cut": 6, "sofar": 7,
       "sa_cut": 8, "sa_sofar": 9, "budget_cut": 10}
 CK_HEADER = 16
+# test-clock sites (abi.h GF_CK_SITE_*)
+CK_SITES = ["viz", "mi", "am_start", "am_round", "sofar", "sel", "sa", "sa_sofar", "bud"]
 
 
 def ck_offsets(M: int, R: int) -> dict:
@@ -320,6 +322,21 @@ class FrontEnd:
 
     def set_budgets(self, match_s: float = float("inf"), select_s: float = float("inf")) -> None:
         check(lib().gf_set_budgets(self.ctx.handle, ctypes.c_double(match_s), ctypes.c_double(select_s)))
+
+    def set_test_clock(self, sites: dict | None) -> None:
+        """gf_frontend_set_test_clock (test-only): each budget check at site s
+        reads base + idx * slope ticks, sites = {name: (base, slope)} over
+        CK_SITES (absent sites read (0, 0)); None restores the device clock."""
+        if sites is None:
+            check(lib().gf_frontend_set_test_clock(self.handle, None))
+            return
+        bad = set(sites) - set(CK_SITES)
+        if bad:
+            raise ValueError(f"unknown clock sites {sorted(bad)}")
+        a = np.zeros((len(CK_SITES), 2), np.int64)
+        for name, (base, slope) in sites.items():
+            a[CK_SITES.index(name)] = (base, slope)
+        check(lib().gf_frontend_set_test_clock(self.handle, ptr(a)))
 
     # ------------------------------------------------------------ state
     def read(self, name: str) -> np.ndarray:

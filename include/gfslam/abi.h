@@ -1217,6 +1217,27 @@ enum {
 #define GF_CK_OFF_SA(M, R) (GF_CK_HEADER + (M) + 128 + (R))      /* [M] visibility pass, per list point */
 #define GF_CK_OFF_BUD(M, R) (GF_CK_HEADER + 2 * (M) + 128 + (R)) /* [M] SearchByProjection_Budget    */
 #define GF_CK_WORDS(M, R) (GF_CK_HEADER + 3 * (M) + 128 + (R))
+/* Test clock (test-only): every budget check reads base + idx * slope ticks
+ * instead of the device clock, idx the check's position at its site (the
+ * isInFrustum list point, the MAP_INFO 64-point batch, the active-matching
+ * round, the SearchByProjection_Budget point; 0 for a site read once). With
+ * it a chosen cap fires at a chosen point, so the budget rules are tested
+ * without wall-clock luck; the clock record (GF_FE_CLOCK) holds the values
+ * read, as with the device clock. base_slope: [GF_CK_NSITE][2] i64 ticks;
+ * NULL restores the device clock. Set before a graph capture. */
+enum {
+    GF_CK_SITE_VIZ = 0,    /* isInFrustum loop, per list point (Tracking.cc:3262) */
+    GF_CK_SITE_MI,         /* MAP_INFO batches of the active branch (Observability.cc:573) */
+    GF_CK_SITE_AM_START,   /* time_Mat_Online at runActiveMapMatching's start (Tracking.cc:3311) */
+    GF_CK_SITE_AM_ROUND,   /* runActiveMapMatching, per round (Observability.cc:1366) */
+    GF_CK_SITE_SOFAR,      /* timeCost_sofar (Tracking.cc:866) */
+    GF_CK_SITE_SEL,        /* RunMapPointsSelection's MAP_INFO batches (Tracking.cc:1779) */
+    GF_CK_SITE_SA,         /* SearchAdditionalMatchesInFrame's visibility pass, per point (:3107-3119) */
+    GF_CK_SITE_SA_SOFAR,   /* time_so_far before SearchByProjection_Budget (:3131) */
+    GF_CK_SITE_BUD,        /* SearchByProjection_Budget, per point (ORBmatcher.cc:366) */
+    GF_CK_NSITE
+};
+int gf_frontend_set_test_clock(gf_frontend* fe, const long long* base_slope);
 
 /* ------------------------------------------------ multi-GPU start-up exchange
  * Config 5: one process per GPU, sequences independent,

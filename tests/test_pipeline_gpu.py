@@ -315,9 +315,78 @@ def test_budget_cut_positions_select():
     caps = {bit: int((fl & bit).astype(bool).sum()) for bit in (16, 256, 512, 1024)}
     print("post-publish caps:", caps, "windows (ticks):", win)
     # the windows are a few microseconds wide against tens of jitter, so a
-    # few of the 119 steps land in them (8 on the r04 box); every step's state
-    # is checked either way
-    assert caps[256] + caps[1024] > 0, "no cap fired inside RunMapPointsSelection or SearchByProjection_Budget"
+    # few of the 119 steps land in them (8 on the r04 box). Every step's state
+    # is checked against the oracle either way (gating); whether a cap fired
+    # depends on the box's clock, so it is reported, not asserted
+    # (test_budget_cut_positions_exact pins every cap on a test clock)
+    if caps[256] + caps[1024] == 0:
+        import warnings
+
+        warnings.warn("no wall-clock cap fired inside RunMapPointsSelection or SearchByProjection_Budget")
+    fe.close()
+
+
+def _sec(ticks):  # seconds that gf_set_budgets turns back into exactly `ticks`
+    return (ticks + 0.5) / 1e8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["viz", "active_round", "map_info_select", "budget_matcher"])
+def test_budget_cut_positions_exact(case):
+    """Each time cap fires at a chosen point, on a test clock
+    (gf_frontend_set_test_clock: the check at position idx of a site reads
+    base + idx * slope ticks, idx = list point / 64-point batch / round). The
+    expected cut follows from the reference's rule alone; the oracle chain,
+    replaying the clock record, must reach the same state.
+    - viz: isInFrustum, el[i] = 10 i, time_total_match 10000: the loop breaks
+      at the first unmatched point with el > 5000, i >= 501 (Tracking.cc
+      :3262-3270);
+    - active_round: rounds read 100 r, time_for_match = 350 (time_Viz and
+      time_Mat_Online 0): round 4 is the first past the cap
+      (Observability.cc:1366-1370);
+    - map_info_select: timeCost_sofar 1000, select budget 1000 + 750:
+      batches read 100 w, batch w is late when 100 w > 750: the first late
+      batch is 8 (Tracking.cc:866, 1779; Observability.cc:573-578);
+    - budget_matcher: timeCost_rest 50, points read 10 k: the first point that
+      reaches the check with 2 * 10 k >= 2 * 50 breaks the loop, k >= 5
+      (ORBmatcher.cc:366-371)."""
+    M, B = 2000, 4
+    W, frames, maps, fe, T, V = _setup("euroc", 1000, B, M, 100, stale=0.93)
+    off = ck_offsets(M, 100)
+    clock = {"viz": ({"viz": (0, 10)}, 10000, 1e9),
+             "active_round": ({"am_round": (0, 100)}, 350, 1e9),
+             "map_info_select": ({"sofar": (1000, 0), "sel": (0, 100)}, 1e9, 1750),
+             "budget_matcher": ({"sofar": (1000, 0), "bud": (0, 10)}, 1e9, 1050)}[case]
+    sites, mt, stt = clock
+    fe.set_test_clock(sites)
+    fe.set_budgets(_sec(mt) if mt < 1e9 else 1e9, _sec(stt) if stt < 1e9 else 1e9)
+    res = _budget_steps(fe, W, frames, B, M, 100, 4)
+    fired = 0
+    for st, rec in res:
+        fl = int(st[STATS.index("flags")])
+        if case == "viz":
+            n = int(rec[CK["viz_cut"]])
+            if st[STATS.index("to_match")] > 0:
+                assert np.array_equal(rec[off["viz"]:off["viz"] + 600], 10 * np.arange(600))
+                assert fl & 32 and 501 <= n < 501 + 100, (fl, n)
+                fired += 1
+        elif case == "active_round":
+            if rec[CK["am_cut"]] >= 0:
+                assert np.array_equal(rec[off["am"]:off["am"] + 5], 100 * np.arange(5))
+                assert fl & 128 and rec[CK["am_cut"]] == 4, (fl, rec[CK["am_cut"]])
+                fired += 1
+        elif case == "map_info_select":
+            assert rec[CK["sofar"]] == 1000
+            assert fl & 256, fl
+            assert np.array_equal(rec[off["sel"]:off["sel"] + 8], 100 * np.arange(8))
+            fired += 1
+        else:
+            nl = int(st[STATS.index("nleft")])
+            if nl > 5 and rec[CK["budget_cut"]] >= 0:
+                assert fl & 1024 and rec[CK["budget_cut"]] >= 5, (fl, rec[CK["budget_cut"]])
+                fired += 1
+    assert fired >= len(res) // 2, f"cap fired in {fired} of {len(res)} stream-steps"
+    fe.set_test_clock(None)
     fe.close()
 
 

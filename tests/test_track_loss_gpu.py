@@ -174,7 +174,7 @@ def test_reloc_candidates_match_oracle():
 
 
 # ---------------------------------------------------------------- the step
-def _scene_setup(B, G, seed, voc, blank=(), jump=()):
+def _scene_setup(B, G, seed, voc, blank=(), jump=(), n_kf=24):
     """Keyframe-graph streams with their databases; frames of scene s at
     indices `blank` (pairs (s, idx)) are uniform grey, and (s, idx, src)
     in `jump` replace a frame with the image at another loop index."""
@@ -190,7 +190,7 @@ def _scene_setup(B, G, seed, voc, blank=(), jump=()):
     src = frames.clone()
     for s, i, j in jump:
         frames[s, i] = src[s, j]
-    gmaps = W.build_global_maps(lambda im: O.extract(im), G)
+    gmaps = W.build_global_maps(lambda im: O.extract(im), G, n_kf=n_kf)
     dvoc = ORBVocabulary(voc)
     dbs = [KeyframeDB(gm["kf_kps"], gm["kf_desc"], dvoc.transform) for gm in gmaps]
     fe = FrontEnd("euroc", 1000, B, G, 100)
@@ -358,4 +358,18 @@ def test_lost_after_database_detached():
                 lost_late += int(dev["track"][b][TR["state"]] == 1)
     assert relocalised > 0, "no stream relocalised before the database was detached"
     assert lost_late > 0, "no stream lost track after the database was detached"
+    fe.close()
+
+
+def test_few_keyframes_track_previous_frame():
+    """A keyframe graph of 3 keyframes: mpMap->KeyFramesInMap() < 4 sends the
+    initial estimate to TrackPreviousFrame every frame, velocity or not
+    (Tracking.cc:602); device and oracle chain agree on every field."""
+    B, G = 2, 2600
+    voc = synth.synth_vocabulary_fast(11, k=10, L=5)
+    W, fr, gmaps, dbs, fe, T, V, dvoc = _scene_setup(B, G, 6, voc, n_kf=3)
+    log = _run(W, fr, gmaps, dbs, fe, T, V, voc, G, 5)
+    paths = [r[2] for r in log]
+    assert all(p in (2, 3) for p in paths), paths  # never the motion model (3: relocalisation after a loss)
+    assert paths.count(2) >= len(paths) // 2, paths
     fe.close()
