@@ -238,6 +238,16 @@ inline void launch(void (*k)(KArgs...), dim3 grid, dim3 block, size_t lds, hipSt
 // Device-side helpers ------------------------------------------------------
 namespace gfd {
 
+// GF_TRACK_PRIO: issue priority (s_setprio) of the tracking stages' latency
+// chains (ordered matcher, pose LM, UpdateReference, one-point precompute)
+// while other groups' extraction waves share their SIMDs.
+#ifndef GF_TRACK_PRIO
+#define GF_TRACK_PRIO 0
+#endif
+__device__ __forceinline__ void track_prio() {
+    if (GF_TRACK_PRIO) __builtin_amdgcn_s_setprio(GF_TRACK_PRIO);
+}
+
 // Elapsed ticks at a budget's clock check: the device clock (s_memrealtime,
 // 100 MHz) since t0, or with a test clock (syn = the site's base and slope,
 // gf_frontend_set_test_clock) base + idx * slope for the idx-th check.

@@ -558,6 +558,7 @@ struct OnePre {  // one-point result against the frame's starting claims
 #define PRE_DESC_LDS_MAX 0
 #endif
 __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OnePre* __restrict__ out) {
+    gfd::track_prio();
     extern __shared__ __align__(16) uint8_t smem[];
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], KP_MAX);
@@ -1557,13 +1558,28 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     }
 }
 
+// AM_PRIO: the wave's issue priority (s_setprio). A frame's rounds are one
+// wave's dependent chain, and in the step it shares its SIMD with other
+// groups' extraction waves; VALU / LDS issue goes to the higher priority,
+// then the older wave, so at the default priority the chain waits behind
+// them (cdna_hip_programming / MI355X_MICROARCH: issue arbitration).
+// Measured r05 (profiles/r05/ab1): priority 3 made the launch slower in the
+// step (1.12-1.15 ms per 256 frames against 0.97 at 0; 3 on every tracking
+// kernel, GF_TRACK_PRIO: 1.03), headline unchanged: off.
+#ifndef AM_PRIO
+#define AM_PRIO 0
+#endif
 // the same body under two names, so that profiles tell the small-pool pass
 // from the overflow pass of a two-pass launch
-__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) { active_match_body(A, blockIdx.x); }
+__global__ __launch_bounds__(AW) void k_active_match(ActiveArgs A) {
+    if (AM_PRIO) __builtin_amdgcn_s_setprio(AM_PRIO);
+    active_match_body(A, blockIdx.x);
+}
 
 // overflow pass: a small grid walks the frames the first pass listed (one
 // wave, so the LDS reuse between frames needs no barrier)
 __global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
+    if (AM_PRIO) __builtin_amdgcn_s_setprio(AM_PRIO);
     const int cnt = A.ovf[0];
     for (int k = blockIdx.x; k < cnt; k += gridDim.x) active_match_body(A, A.ovf[1 + k]);
 }

@@ -228,6 +228,7 @@ __host__ __device__ __forceinline__ bool match_stage(int kp_cap, int q_cap) {
 }
 
 __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst fc) {
+    gfd::track_prio();
     extern __shared__ __align__(16) int lds[];
     const int kc = min(A.kp_cap, KP_MAX);
     int* cell_start = lds;                  // NCELLS + 1
@@ -475,6 +476,7 @@ struct SeqPre {
 #define SEQ_PRE_G 4  // lanes per query
 __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,
                                                                    SeqPre* __restrict__ out) {
+    gfd::track_prio();
     extern __shared__ __align__(16) uint8_t smem[];
     const int f = blockIdx.x, tid = threadIdx.x;
     const int n = min(A.n[f], KP_MAX);
@@ -603,6 +605,7 @@ __device__ __forceinline__ void top2_insert(unsigned long long key, unsigned lon
 }
 
 __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameConst fc) {
+    gfd::track_prio();
     extern __shared__ __align__(16) int lds[];
     // everything the ordered loop touches lives in LDS, so its per-query
     // barrier waits on LDS only (global stores would be drained every query)

@@ -90,6 +90,7 @@ __device__ __forceinline__ void gather_frame(const GatherArgs& G, int f) {
 // single sequence's chain).
 template <int WPS, int NT>
 __global__ __launch_bounds__(NT, WPS) void k_pose_opt_frames(GatherArgs G, PoseArgs A) {
+    gfd::track_prio();
     if (threadIdx.x < 64) gather_frame(G, blockIdx.x);
     __syncthreads();  // the edges (global memory) visible to the whole workgroup
     pose_opt_problem<NT>(A, blockIdx.x);

@@ -82,6 +82,7 @@ __device__ int scan_1024(int v, int* tmp, int& total) {
 }
 
 __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
+    gfd::track_prio();
     extern __shared__ __align__(16) uint8_t rm_lds[];
     int* cnt = reinterpret_cast<int*>(rm_lds);  // votes, then the slot offsets of the local keyframes
     int* lkf = reinterpret_cast<int*>(rm_lds + (((size_t)(A.kfc + 1) * 4 + 15) & ~(size_t)15));  // local keyframes
