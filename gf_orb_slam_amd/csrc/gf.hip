@@ -931,6 +931,46 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #define AM_T(k) (void)0
 #endif
 
+// AM_SLOTS: the heap loop of a round (live set <= 64, no ties) by slot
+// assignment instead of one pop at a time. std::priority_queue pops the
+// largest live score; a failed top is replaced by the next draw, so draw i
+// (i >= 1 after the round's sz initial ones) joins at pop time i. Pops in
+// score order to the earliest free time are a unit-job schedule: an entry of
+// score v joining at time a leaves at the first time t >= a at which every
+// higher entry that joined by t has left, i.e. the first t >= a with
+// x_t <= v (t >= 1) and #{initial > v} + #{x_1..x_t > v} <= t; that is the
+// c-th time at which the draw is not above v, c = #{initial > v} (t = 0 when
+// c = 0). The round ends at the first time whose entry is matchable: T = min
+// over matchable entries of their time, T pops, the entries with time < T
+// popped. One window of up to 64 draws costs one pass of broadcast LDS
+// compares instead of up to 64 dependent pop steps; a tie or NaN hands the
+// round to the exact heap replay as before.
+#ifndef AM_SLOTS
+#define AM_SLOTS 1
+#endif
+// LDS hand-over inside the one-wave workgroup
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// position of the k-th (1-based) set bit of m, 64 if fewer
+__device__ __forceinline__ int kth_bit(unsigned long long m, int k) {
+    if (k <= 0 || __popcll(m) < k) return 64;
+    int pos = 0, r = k - 1;
+#pragma unroll
+    for (int half = 32; half >= 1; half >>= 1) {
+        const int c = __popcll(m & ((1ull << half) - 1ull));
+        if (r >= c) {
+            r -= c;
+            m >>= half;
+            pos += half;
+        }
+    }
+    return pos;
+}
+
 __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int f) {
 #ifdef GF_AM_STAMP
     unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
@@ -968,6 +1008,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
+#if AM_SLOTS
+    __shared__ double s_lsc[64];            // slot_loop: live scores, lane order
+    __shared__ unsigned long long s_rk[2];  // slot_loop: ranks seen (distinctness)
+    __shared__ int16_t s_live[128];         // slot_loop: next live set
+#endif
 
     const int lane = threadIdx.x;
     const FrameConst& fc = A.fc;
@@ -1253,6 +1298,124 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 AM_T(3);
             }
         };
+#if AM_SLOTS
+        // (a') the live set (<= 64, lane j: candidate lc) against the next
+        // window of draws, by slot assignment (AM_SLOTS above). 1: round
+        // decided (success / exh set), 0: leave for (b) with alv / C.alive set.
+        auto slot_loop = [&]() -> int {
+            constexpr int INF = 1 << 20;
+            int lc = lane < sz ? lane : -1;
+            while (true) {
+                const int rep0 = sz + npop;
+                draw_eval(rep0);
+                if (nc - rep0 < 16 && exh_at < 0 && !cabort) draw_eval(nc);  // a useful window
+                if (evald < nc && !cabort) {
+                    eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K,
+                               D);
+                    evald = nc;
+                }
+                if (cabort) {
+                    exh = true;
+                    return 1;
+                }
+                const int W = __builtin_amdgcn_readfirstlane(max(min(nc - rep0, 64), 0));
+                const bool v0 = lc >= 0, v1 = lane < W;
+                const int xc = v1 ? rep0 + lane : -1;
+                const double lv = v0 ? C.score[lc] : 0.0, xv = v1 ? C.score[xc] : 0.0;
+                const bool m0 = v0 && C.match[lc] >= 0, m1 = v1 && C.match[xc] >= 0;
+                s_lsc[lane] = lv;
+                if (lane < 2) s_rk[lane] = 0ull;
+                wave_sync_lds();
+                const bool nan = (v0 && lv != lv) || (v1 && xv != xv);
+                // c = #{live > v}, g = {window draws above v}
+                int c0 = 0, c1 = 0;
+                unsigned long long g0 = 0ull, g1 = 0ull;
+                for (int k0 = 0; k0 < sz; k0 += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int k = k0 + u;
+                        if (k < sz) {
+                            const double lk = s_lsc[k];
+                            c0 += lk > lv;
+                            c1 += lk > xv;
+                        }
+                    }
+                }
+                for (int k0 = 0; k0 < W; k0 += 8) {
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const int k = k0 + u;
+                        if (k < W) {
+                            const double xk = C.score[rep0 + k];
+                            g0 |= (unsigned long long)(xk > lv) << k;
+                            g1 |= (unsigned long long)(xk > xv) << k;
+                        }
+                    }
+                }
+                // distinct scores: every entry's rank (#{entries above}) once
+                const int r0 = c0 + __popcll(g0), r1 = c1 + __popcll(g1);
+                if (v0) atomicOr(&s_rk[r0 >> 6], 1ull << (r0 & 63));
+                if (v1) atomicOr(&s_rk[r1 >> 6], 1ull << (r1 & 63));
+                wave_sync_lds();
+                const bool tie = __popcll(s_rk[0]) + __popcll(s_rk[1]) != sz + W;
+                if (__ballot(nan) || tie) {  // (b) pops the rest exactly
+                    for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
+                    wave_sync_lds();
+                    if (v0) {
+                        alv[__popcll(__ballot(v0) & ((1ull << lane) - 1ull))] = (int16_t)lc;
+                        C.alive[lc] = 1;
+                    }
+                    wave_sync_lds();
+                    return 0;
+                }
+                // leaving times: draw k of the window joins (and may leave) at time k + 1
+                const unsigned long long wm = W >= 64 ? ~0ull : ((1ull << W) - 1ull);
+                const unsigned long long z0 = ~g0 & wm, z1 = ~g1 & wm;
+                const int p0 = !v0 ? INF : c0 == 0 ? 0 : (kth_bit(z0, c0) < 64 ? kth_bit(z0, c0) + 1 : INF);
+                int p1 = INF;
+                if (v1) {
+                    const int t = c1 == 0 ? 0 : (kth_bit(z1, c1) < 64 ? kth_bit(z1, c1) + 1 : INF);
+                    p1 = t >= INF ? INF : max(t, lane + 1);
+                }
+                int T = min(m0 ? p0 : INF, m1 ? p1 : INF);
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) T = min(T, __shfl_xor(T, o, 64));
+                T = __builtin_amdgcn_readfirstlane(T);
+                const bool exhausted = T > W && exh_at >= 0 && rep0 + W >= nc;
+                if (T <= W || exhausted) {
+                    // decided: success at time T, or the draws gave out at time W
+                    // (its top popped too, as the sequential loop does)
+                    const int cut = T <= W ? T : W + 1;  // entries leaving before `cut` are popped
+                    const int np = T <= W ? T : W;
+                    if (T <= W) {
+                        const unsigned long long w0m = __ballot(m0 && p0 == T), w1m = __ballot(m1 && p1 == T);
+                        if (w0m) top = __builtin_amdgcn_readlane(lc, __ffsll((long long)w0m) - 1);
+                        else top = rep0 + __ffsll((long long)w1m) - 1;
+                        success = true;
+                    } else {
+                        exh = true;
+                    }
+                    npop = __builtin_amdgcn_readfirstlane(npop + np);
+                    for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
+                    wave_sync_lds();
+                    if (v0 && p0 >= cut) C.alive[lc] = 1;
+                    if (v1 && lane < np && p1 >= cut) C.alive[xc] = 1;
+                    wave_sync_lds();
+                    return 1;
+                }
+                // W pops (times 0 .. W - 1); the entries still live (time >= W) become the live set
+                const bool k0l = v0 && p0 >= W, k1l = v1 && p1 >= W;
+                const unsigned long long b0 = __ballot(k0l), b1 = __ballot(k1l);
+                const unsigned long long below = (1ull << lane) - 1ull;
+                if (k0l) s_live[__popcll(b0 & below)] = (int16_t)lc;
+                if (k1l) s_live[__popcll(b0) + __popcll(b1 & below)] = (int16_t)xc;
+                wave_sync_lds();
+                lc = lane < sz ? (int)s_live[lane] : -1;
+                npop = __builtin_amdgcn_readfirstlane(npop + W);
+                wave_sync_lds();
+            }
+        };
+#endif
         auto sorted_loop = [&](auto kk) -> int {  // 1: round decided, 0: leave for (b)
             constexpr int KR = decltype(kk)::value;
             LiveSet<KR> L;
@@ -1433,8 +1596,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         };
         const int kreg = (sz + 63) >> 6;
         int decided = 0;
+#if AM_SLOTS
+        if (kreg == 1)
+            decided = slot_loop();
+#else
         if (kreg == 1)
             decided = sorted_loop(std::integral_constant<int, 1>{});
+#endif
         else if (kreg == 2)
             decided = sorted_loop(std::integral_constant<int, 2>{});
         else if (kreg <= 4)
