@@ -1009,7 +1009,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
 #if AM_SLOTS
-    __shared__ double s_lsc[64];            // slot_loop: live scores, lane order
+    __shared__ __align__(16) double s_lsc[64];  // slot_loop: live scores, lane order (-inf past sz)
+    __shared__ __align__(16) double s_xsc[64];  // slot_loop: the window's scores (-inf past W)
     __shared__ unsigned long long s_rk[2];  // slot_loop: ranks seen (distinctness)
     __shared__ int16_t s_live[128];         // slot_loop: next live set
 #endif
@@ -1310,9 +1311,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 draw_eval(rep0);
                 if (nc - rep0 < 16 && exh_at < 0 && !cabort) draw_eval(nc);  // a useful window
                 if (evald < nc && !cabort) {
+                    AM_T(4);
                     eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K,
                                D);
                     evald = nc;
+                    AM_T(3);
                 }
                 if (cabort) {
                     exh = true;
@@ -1323,35 +1326,54 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 const int xc = v1 ? rep0 + lane : -1;
                 const double lv = v0 ? C.score[lc] : 0.0, xv = v1 ? C.score[xc] : 0.0;
                 const bool m0 = v0 && C.match[lc] >= 0, m1 = v1 && C.match[xc] >= 0;
-                s_lsc[lane] = lv;
+                s_lsc[lane] = v0 ? lv : -INFINITY;  // -inf is above nothing
+                s_xsc[lane] = v1 ? xv : -INFINITY;
                 if (lane < 2) s_rk[lane] = 0ull;
                 wave_sync_lds();
                 const bool nan = (v0 && lv != lv) || (v1 && xv != xv);
-                // c = #{live > v}, g = {window draws above v}
+                // c = #{live > v}, g = {window draws above v}: broadcast LDS
+                // reads, 16 scores per batch in flight, no per-entry branch
                 int c0 = 0, c1 = 0;
-                unsigned long long g0 = 0ull, g1 = 0ull;
-                for (int k0 = 0; k0 < sz; k0 += 8) {
+                uint32_t g0l = 0u, g0h = 0u, g1l = 0u, g1h = 0u;
 #pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        const int k = k0 + u;
-                        if (k < sz) {
-                            const double lk = s_lsc[k];
-                            c0 += lk > lv;
-                            c1 += lk > xv;
+                for (int kb = 0; kb < 64; kb += 16) {
+                    if (kb < sz) {
+                        double lk[16];
+#pragma unroll
+                        for (int u = 0; u < 16; u += 2) {
+                            const double2 d2 = *reinterpret_cast<const double2*>(&s_lsc[kb + u]);
+                            lk[u] = d2.x;
+                            lk[u + 1] = d2.y;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 16; u++) {
+                            c0 += lk[u] > lv;
+                            c1 += lk[u] > xv;
+                        }
+                    }
+                    if (kb < W) {
+                        double xk[16];
+#pragma unroll
+                        for (int u = 0; u < 16; u += 2) {
+                            const double2 d2 = *reinterpret_cast<const double2*>(&s_xsc[kb + u]);
+                            xk[u] = d2.x;
+                            xk[u + 1] = d2.y;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 16; u++) {
+                            const int k = kb + u;
+                            if (k < 32) {
+                                g0l |= xk[u] > lv ? 1u << k : 0u;
+                                g1l |= xk[u] > xv ? 1u << k : 0u;
+                            } else {
+                                g0h |= xk[u] > lv ? 1u << (k - 32) : 0u;
+                                g1h |= xk[u] > xv ? 1u << (k - 32) : 0u;
+                            }
                         }
                     }
                 }
-                for (int k0 = 0; k0 < W; k0 += 8) {
-#pragma unroll
-                    for (int u = 0; u < 8; u++) {
-                        const int k = k0 + u;
-                        if (k < W) {
-                            const double xk = C.score[rep0 + k];
-                            g0 |= (unsigned long long)(xk > lv) << k;
-                            g1 |= (unsigned long long)(xk > xv) << k;
-                        }
-                    }
-                }
+                const unsigned long long g0 = (unsigned long long)g0h << 32 | g0l,
+                                         g1 = (unsigned long long)g1h << 32 | g1l;
                 // distinct scores: every entry's rank (#{entries above}) once
                 const int r0 = c0 + __popcll(g0), r1 = c1 + __popcll(g1);
                 if (v0) atomicOr(&s_rk[r0 >> 6], 1ull << (r0 & 63));
