@@ -614,13 +614,22 @@ struct Cands {
 };
 
 // True when a lower lane of the wave holds the same value (the earlier try of
-// a batch on the same column wins): 63 lane reads, no LDS.
-__device__ __forceinline__ bool dup_of_lower_lane(int v) {
+// a batch on the same column wins). Values below 2^nbits: the lanes holding
+// the same value are the intersection, over the bits, of the lanes that agree
+// with this lane on that bit (one ballot per bit: nbits ballots instead of 63
+// lane reads). Called with every lane of the wave active (an inactive lane's
+// bits would read as zeros).
+__device__ __forceinline__ bool dup_of_lower_lane(int v, int nbits) {
     const int lane = threadIdx.x;
-    bool dup = false;
-#pragma unroll
-    for (int k = 0; k < 63; k++) dup |= (k < lane) & (__builtin_amdgcn_readlane(v, k) == v);
-    return dup;
+    unsigned long long same = __ballot(1);
+    for (int b = 0; b < nbits; b++) {
+        const unsigned long long ones = __ballot((v >> b) & 1);
+        same &= ((v >> b) & 1) ? ones : ~ones;
+    }
+    return (same & ((1ull << lane) - 1ull)) != 0ull;
+}
+__device__ __forceinline__ int bits_for(int n) {  // 2^bits_for(n) >= n
+    return n <= 1 ? 1 : 32 - __clz(n - 1);
 }
 
 // One batch of 64 tries: tries are accepted in order when their column was not
@@ -631,13 +640,14 @@ __device__ __forceinline__ bool dup_of_lower_lane(int v) {
 // commit advances the RNG from the batch holding its last call.
 __device__ int draw_batch(uint32_t& s, uint32_t& s0, uint32_t& o0, int& tries, int& run, int N, int round,
                           const Pool& P, int16_t* vis,
-                          const Cands& C, int nc, int* exh_at, const uint32_t (&coef)[31]) {
+                          const Cands& C, int nc, int* exh_at, const uint32_t (&coef)[31], int sbits) {
     const int lane = threadIdx.x;
     const uint32_t o = rng_word(s, coef);
     const int j = (int)((o >> 1) % (uint32_t)N);
     const int sl = pool_select(P, j);
     // an earlier try of this batch that drew the same column wins
-    const bool acc = vis[sl] < round && !dup_of_lower_lane(sl);
+    const bool dup = dup_of_lower_lane(sl, sbits);  // all lanes: no short circuit
+    const bool acc = vis[sl] < round && !dup;
     const unsigned long long m = __ballot(acc);
     const int a0 = m ? __ffsll((long long)m) - 1 : 64;
     int got = 0;
@@ -729,7 +739,8 @@ __device__ void exhaust_draws(uint32_t& sd, int tries, int run, int N, unsigned 
     while (true) {
         const uint32_t o = rng_word(sd, coef);
         const int j = (int)((o >> 1) % (uint32_t)N);
-        const bool acc = !((colvis[j >> 6] >> (j & 63)) & 1ull) && !dup_of_lower_lane(j);
+        const bool dup = dup_of_lower_lane(j, bits_for(N));
+        const bool acc = !((colvis[j >> 6] >> (j & 63)) & 1ull) && !dup;
         const unsigned long long m = __ballot(acc);
         const int a0 = m ? __ffsll((long long)m) - 1 : 64;
         if (run + a0 >= MAX_RANDOM_QUERY_TIME) {
@@ -1099,6 +1110,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         return;
     }
     const Pool P{pbits, ppre};
+    const int sbits = bits_for(N);  // pool slots are < N (they never move)
     {
         const int lo = lane * 64;
         pbits[lane] = N >= lo + 64 ? ~0ull : (N > lo ? ((1ull << (N - lo)) - 1ull) : 0ull);
@@ -1156,7 +1168,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     if (lane == 0) s_exh = -1;
                     __syncthreads();
                     nc = __builtin_amdgcn_readfirstlane(
-                        nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef));
+                        nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef, sbits));
                     exh_at = __builtin_amdgcn_readfirstlane(s_exh);
                 }
                 // an accepted draw before the draws gave out: the cap fires there;
@@ -1230,7 +1242,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             {
                 uint32_t s0, o0;
                 nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
-                                                                    &s_exh, rcoef));
+                                                                    &s_exh, rcoef, sbits));
                 bs0 = nb & 1 ? bs0 : s0;
                 bo0 = nb & 1 ? bo0 : o0;
                 bs1 = nb & 1 ? s0 : bs1;
@@ -1281,7 +1293,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     {
                 uint32_t s0, o0;
                 nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
-                                                                    &s_exh, rcoef));
+                                                                    &s_exh, rcoef, sbits));
                 bs0 = nb & 1 ? bs0 : s0;
                 bo0 = nb & 1 ? bo0 : o0;
                 bs1 = nb & 1 ? s0 : bs1;

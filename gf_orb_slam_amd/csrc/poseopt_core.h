@@ -129,12 +129,69 @@ __device__ __forceinline__ double chain_sum(const double* row, int m, double acc
     return acc;
 }
 
+// PO_MFMA (A/B build, off in the product): buildSystem's H = sum_e J^T W J
+// and b on v_mfma_f64_16x16x4f64 instead of the ordered VALU sums. Per pass
+// each edge writes its two Jacobian rows J_r (6) and (w J_r, o_r) (7) to LDS
+// (the H / b term rows' space); wave 0 then contracts them, four edge rows
+// per MFMA: A[i][k] = J_{r_k}[i], B[k][j] = w J_{r_k}[j] (j < 6), o_{r_k}
+// (j = 6), so D[i][j < 6] = H[i][j] and D[i][6] = b[i], accumulated over the
+// passes in registers. The sums' order is the matrix core's, not the edge
+// order of g2o's buildSystem (block_solver.hpp:502-562).
+#ifndef PO_MFMA
+#define PO_MFMA 0
+#endif
+typedef double po_d4 __attribute__((ext_vector_type(4)));
+constexpr int PO_JB = 6 * 2 * PO_E;  // offset of the (w J, o) rows in the buffer
+
+__device__ __forceinline__ void mfma_store_rows(double* jb, int ll, const double* J0, const double* J1, double w,
+                                                double o0, double o1) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        jb[(2 * ll) * 6 + i] = J0[i];
+        jb[(2 * ll + 1) * 6 + i] = J1[i];
+        jb[PO_JB + (2 * ll) * 7 + i] = J0[i] * w;
+        jb[PO_JB + (2 * ll + 1) * 7 + i] = J1[i] * w;
+    }
+    jb[PO_JB + (2 * ll) * 7 + 6] = o0;
+    jb[PO_JB + (2 * ll + 1) * 7 + 6] = o1;
+}
+
+// wave 0: acc += the pass's m edges (2 m rows)
+__device__ __forceinline__ void mfma_accumulate(const double* jb, int m, int l, po_d4& acc) {
+    const int i = l & 15, kk = l >> 4;
+    for (int t = 0; 4 * t < 2 * m; t++) {
+        const int r = 4 * t + kk;
+        const bool rv = r < 2 * m;
+        const double a = (rv && i < 6) ? jb[r * 6 + i] : 0.0;
+        const double bb = (rv && i < 7) ? jb[PO_JB + r * 7 + i] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+    }
+}
+
+// H lower packed [0, 21) and b [21, 27) from the accumulator: lane l holds
+// D[row (l >> 4) + 4 u][col l & 15] in acc[u]
+__device__ __forceinline__ void mfma_write(const po_d4& acc, int l, double* sh_sum) {
+    const int col = l & 15, rb = l >> 4;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const int row = rb + 4 * u;
+        if (row < 6) {
+            const double v = u == 0 ? acc[0] : u == 1 ? acc[1] : u == 2 ? acc[2] : acc[3];
+            if (col <= row) sh_sum[row * (row + 1) / 2 + col] = v;
+            if (col == 6) sh_sum[21 + row] = v;
+        }
+    }
+}
+
 // computeActiveErrors + activeRobustChi2 (+ buildSystem when `build`) at T.
 // Returns the sums in sh_sum: [0,21) lower H row-major-packed, [21,27) b, 27 chi2.
 __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool build, double (*term)[PO_TP],
                                      double* sh_sum) {
     // (build: the H/b rows too; the chi2 row is PO_CHI)
     double acc = 0.0;
+#if PO_MFMA
+    po_d4 macc = {0.0, 0.0, 0.0, 0.0};
+#endif
     for (int base = 0; base < L.n; base += PO_E) {
         const int e = base + L.l;
         if (L.l < PO_E && e < L.n) {
@@ -162,6 +219,9 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
                 J1[5] = y / z2 * L.fy;
                 const double w = rho1 * info;
                 const double o0 = -(info * r0) * rho1, o1 = -(info * r1) * rho1;
+#if PO_MFMA
+                mfma_store_rows(&term[0][0], L.l, J0, J1, w, o0, o1);
+#else
                 int k = 0;
 #pragma unroll
                 for (int a = 0; a < 6; a++)
@@ -169,16 +229,27 @@ __device__ __forceinline__ void pass(const Lane& L, const gfse3::SE3& T, bool bu
                     for (int b = 0; b <= a; b++) term[k++][L.l] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
 #pragma unroll
                 for (int a = 0; a < 6; a++) term[21 + a][L.l] = J0[a] * o0 + J1[a] * o1;
+#endif
             }
         }
         __syncthreads();
         const int m = min(PO_E, L.n - base);
+#if PO_MFMA
+        if (build && L.l < 64) mfma_accumulate(&term[0][0], m, L.l, macc);
+        if (L.l == PO_CHI) acc = chain_sum(term[L.l], m, acc);
+#else
         if ((build && L.l < PO_NACC) || L.l == PO_CHI) {
             acc = chain_sum(term[L.l], m, acc);
         }
+#endif
         __syncthreads();
     }
+#if PO_MFMA
+    if (build && L.l < 64) mfma_write(macc, L.l, sh_sum);
+    if (L.l == PO_CHI) sh_sum[L.l] = acc;
+#else
     if ((build && L.l < PO_NACC) || L.l == PO_CHI) sh_sum[L.l] = acc;
+#endif
     __syncthreads();
 }
 
@@ -194,6 +265,9 @@ template <int NT>
 __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, int S, double (*term)[PO_TP],
                                             double* sh_sum) {
     double acc = 0.0;
+#if PO_MFMA
+    po_d4 macc = {0.0, 0.0, 0.0, 0.0};
+#endif
     const int wv = NT > 64 ? L.l >> 6 : 0, ll = NT > 64 ? L.l & 63 : L.l;
     for (int base = 0; base < L.n; base += PO_E) {
         const int e = base + ll;
@@ -226,6 +300,9 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
                     J1[5] = y / z2 * L.fy;
                     const double w = rho1 * info;
                     const double o0 = -(info * r0) * rho1, o1 = -(info * r1) * rho1;
+#if PO_MFMA
+                    mfma_store_rows(&term[0][0], ll, J0, J1, w, o0, o1);
+#else
                     int k = 0;
 #pragma unroll
                     for (int a = 0; a < 6; a++)
@@ -233,17 +310,28 @@ __device__ __forceinline__ void pass_trials(const Lane& L, const gfse3::SE3* T, 
                         for (int b = 0; b <= a; b++) term[k++][ll] = (J0[a] * w) * J0[b] + (J1[a] * w) * J1[b];
 #pragma unroll
                     for (int a = 0; a < 6; a++) term[21 + a][ll] = J0[a] * o0 + J1[a] * o1;
+#endif
                 }
             }
         }
         __syncthreads();
         const int m = min(PO_E, L.n - base);
+#if PO_MFMA
+        if (L.l < 64) mfma_accumulate(&term[0][0], m, L.l, macc);
+        if (L.l >= PO_CHI && L.l < PO_CHI + S) acc = chain_sum(term[L.l], m, acc);
+#else
         if (L.l < PO_CHI + S) {
             acc = chain_sum(term[L.l], m, acc);
         }
+#endif
         __syncthreads();
     }
+#if PO_MFMA
+    if (L.l < 64) mfma_write(macc, L.l, sh_sum);
+    if (L.l >= PO_CHI && L.l < PO_CHI + S) sh_sum[L.l] = acc;
+#else
     if (L.l < PO_CHI + S) sh_sum[L.l] = acc;
+#endif
     __syncthreads();
 }
 
