@@ -1193,19 +1193,23 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         if (!nsucc_valid && last_npop > sz) {
             // the last round had to pop: count the pool entries that can still be
             // matched (slots whose holders were claimed are scanned again)
-            // pass 1, loads only: a slot whose holders are unclaimed keeps its result
+            // pass 1, loads only: a slot whose holders are unclaimed keeps its
+            // result. Only "none left" matters, so the walk stops at the first
+            // word holding a known matchable slot (usually the first word)
             bool known = false;
             unsigned long long stale = 0ull;  // bit w: this lane's slot in word w needs a rescan
             for (int w = 0; w < nw0; w++) {
                 const int sl = w * 64 + lane;
-                if (!((pbits[w] >> lane) & 1ull)) continue;
-                const int h1 = sm_h1[sl], h2 = sm_h2[sl];
-                if ((h1 >= 0 && claim[h1] >= 0) || (h2 >= 0 && claim[h2] >= 0))
-                    stale |= 1ull << w;
-                else
-                    known |= sm_match[sl] >= 0;
+                if ((pbits[w] >> lane) & 1ull) {
+                    const int h1 = sm_h1[sl], h2 = sm_h2[sl];
+                    if ((h1 >= 0 && claim[h1] >= 0) || (h2 >= 0 && claim[h2] >= 0))
+                        stale |= 1ull << w;
+                    else
+                        known |= sm_match[sl] >= 0;
+                }
+                if (__ballot(known)) break;
             }
-            int ns = __ballot(known) ? 1 : 0;  // only "none left" matters
+            int ns = __ballot(known) ? 1 : 0;
             // pass 2: rescans, until a matchable slot turns up
             for (int w = 0; w < nw0 && !ns; w++) {
                 int mi = -1;
