@@ -604,6 +604,15 @@ __device__ unsigned long long g_am_stamp[8];
 // Per-round candidate list: the draws of the sequential loop in order (the
 // initial random subset, then one replacement per failed top), produced 64
 // tries at a time ahead of need.
+// The active matcher is one wave per workgroup: its LDS hand-offs need the
+// wave's LDS operations done and ordered, not a workgroup barrier, whose
+// release fence also waits for the wave's outstanding global stores.
+__device__ __forceinline__ void am_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 struct Cands {
     int16_t* slot;   // pool slot drawn
     int32_t* tries;  // rand() calls from the round start up to this acceptance
@@ -671,7 +680,7 @@ __device__ int draw_batch(uint32_t& s, uint32_t& s0, uint32_t& o0, int& tries, i
     o0 = o;
     s = rng_advance(s, o, 64);
     tries += 64;
-    __syncthreads();
+    am_sync();
     return __builtin_amdgcn_readfirstlane(got);
 }
 
@@ -722,7 +731,7 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
         C.dist[c] = (int16_t)md;
         C.alive[c] = 0;
     }
-    __syncthreads();
+    am_sync();
 }
 
 // A round in which no pool entry can be matched any more: every draw fails
@@ -747,7 +756,7 @@ __device__ void exhaust_draws(uint32_t& sd, int tries, int run, int N, unsigned 
             const int k = MAX_RANDOM_QUERY_TIME - run;  // tries of this batch before the draw gives up
             exh_at = tries + k;
             sd = rng_advance(sd, o, k);
-            __syncthreads();
+            am_sync();
             return;
         }
         if (acc) atomicOr(&colvis[j >> 6], 1ull << (j & 63));
@@ -755,7 +764,7 @@ __device__ void exhaust_draws(uint32_t& sd, int tries, int run, int N, unsigned 
         run = m ? __clzll((long long)m) : run + 64;
         sd = rng_advance(sd, o, 64);
         tries += 64;
-        __syncthreads();
+        am_sync();
     }
 }
 
@@ -920,7 +929,7 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
         }
         *s_res = rheap[0];
     }
-    __syncthreads();
+    am_sync();
     const int t = __builtin_amdgcn_readfirstlane(*s_res);
     int p = -1;
     for (int i0 = 0; i0 < na && p < 0; i0 += AW) {
@@ -960,11 +969,7 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #define AM_SLOTS 1
 #endif
 // LDS hand-over inside the one-wave workgroup
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
+__device__ __forceinline__ void wave_sync_lds() { am_sync(); }
 
 // position of the k-th (1-based) set bit of m, 64 if fewer
 __device__ __forceinline__ int kth_bit(unsigned long long m, int k) {
@@ -1067,7 +1072,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
 #pragma unroll
     for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
-    __syncthreads();
+    am_sync();
     AM_T(0);
 
     // ---- pool: in-view, updated map points in list order (Observability.cc:1285-1306)
@@ -1114,7 +1119,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     {
         const int lo = lane * 64;
         pbits[lane] = N >= lo + 64 ? ~0ull : (N > lo ? ((1ull << (N - lo)) - 1ull) : 0ull);
-        __syncthreads();
+        am_sync();
         pool_prefix(P);
     }
     const SlotMatch SM{sm_match, sm_dist, sm_h1, sm_h2};
@@ -1138,7 +1143,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         rs = lane < 31 ? (uint32_t)A.rng[f].state[(f0 + lane) % 31] : 0u;
     }
     int used = 0, nm = 0, nld = 0;  // nld: logDet calls of the reference (one per draw)
-    __syncthreads();
+    am_sync();
     AM_T(1);
 
     const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
@@ -1166,7 +1171,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 int tries = 0, run = 0, nc = 0, exh_at = -1;
                 while (nc < 1 && exh_at < 0) {
                     if (lane == 0) s_exh = -1;
-                    __syncthreads();
+                    am_sync();
                     nc = __builtin_amdgcn_readfirstlane(
                         nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc, &s_exh, rcoef, sbits));
                     exh_at = __builtin_amdgcn_readfirstlane(s_exh);
@@ -1180,7 +1185,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     cut = true;
                     if (lane == 0) rec[GF_CK_AM_CUT] = round;
                 }
-                __syncthreads();
+                am_sync();
                 break;
             }
         }
@@ -1222,12 +1227,12 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             if (lane == 0) s_nsucc = ns;
             nsucc_valid = true;
-            __syncthreads();
+            am_sync();
         }
         AM_T(7);
         if (nsucc_valid && __builtin_amdgcn_readfirstlane(s_nsucc) == 0) {  // nothing left to match: the round draws until the draws give out
             colvis[lane] = 0ull;
-            __syncthreads();
+            am_sync();
             int nacc = 0, ex = 0;
             exhaust_draws(sd, 0, 0, N, colvis, nacc, ex, rcoef);
             nld += nacc;
@@ -1242,7 +1247,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 break;
             }
             if (lane == 0) s_exh = -1;
-            __syncthreads();
+            am_sync();
             {
                 uint32_t s0, o0;
                 nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
@@ -1293,7 +1298,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                         break;
                     }
                     if (lane == 0) s_exh = -1;
-                    __syncthreads();
+                    am_sync();
                     {
                 uint32_t s0, o0;
                 nc = __builtin_amdgcn_readfirstlane(nc + draw_batch(sd, s0, o0, tries, run, N, round, P, vis, C, nc,
@@ -1519,7 +1524,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     if (x != x || (__ballot(ls == x) & live)) {  // a tie: (b) pops it exactly
                         npop = __builtin_amdgcn_readfirstlane(npop + 1);
                         for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
-                        __syncthreads();
+                        am_sync();
                         const bool lv = (live >> lane) & 1ull;
                         if (lv) {
                             alv[__popcll(live & ((1ull << lane) - 1ull))] = (int16_t)lc;
@@ -1529,7 +1534,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                             alv[sz - 1] = (int16_t)rep;
                             C.alive[rep] = 1;
                         }
-                        __syncthreads();
+                        am_sync();
                         return 0;
                     }
                     const unsigned long long gt = __ballot(ls > x) & live;
@@ -1544,9 +1549,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 }
                 // alive flags of the candidates that entered: popped 0, live 1
                 for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
-                __syncthreads();
+                am_sync();
                 if (lane < sz && lc >= 0) C.alive[lc] = 1;
-                __syncthreads();
+                am_sync();
                 return 1;
             }
             while (true) {
@@ -1575,7 +1580,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (t2) {  // hand the live set (positions 1.., then the replacement) to (b)
                     npop = __builtin_amdgcn_readfirstlane(npop + 1);
                     for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
-                    __syncthreads();
+                    am_sync();
 #pragma unroll
                     for (int r = 0; r < KR; r++) {
                         const int p = 64 * r + lane;
@@ -1588,7 +1593,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                         alv[sz - 1] = (int16_t)rep;
                         C.alive[rep] = 1;
                     }
-                    __syncthreads();
+                    am_sync();
                     return 0;
                 }
                 // new[p] = old[p + 1] for p < rank, new[rank] = the replacement
@@ -1623,13 +1628,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             // alive flags of the candidates that entered: popped 0, live 1
             for (int c = lane; c < sz + npop; c += AW) C.alive[c] = 0;
-            __syncthreads();
+            am_sync();
 #pragma unroll
             for (int r = 0; r < KR; r++) {
                 const int p = 64 * r + lane;
                 if (p < sz && !(exh && p == 0)) C.alive[L.c[r]] = 1;  // on exhaustion the top was popped
             }
-            __syncthreads();
+            am_sync();
             return 1;
         };
         const int kreg = (sz + 63) >> 6;
@@ -1651,7 +1656,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     C.alive[c] = 1;
                     alv[c] = (int16_t)c;
                 }
-                __syncthreads();
+                am_sync();
             }
             // (b) general: wave_top over the live list (ties replay the heap)
             while (true) {
@@ -1672,7 +1677,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                     alv[tpos] = (int16_t)rep;  // the replacement takes the popped entry's place
                 }
                 npop = __builtin_amdgcn_readfirstlane(npop + 1);
-                __syncthreads();
+                am_sync();
             }
         }
         AM_T(4);
@@ -1703,7 +1708,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         } else {
             for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
         }
-        __syncthreads();
+        am_sync();
         if (exh) break;
         AM_T(5);
         const int nrem = npop + 1;  // removeIdx: every top tried
@@ -1721,17 +1726,17 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         }
         nm++;
         (void)success;
-        __syncthreads();
+        am_sync();
         if (nrem == N) break;  // went through all map points: the pool stays as left-overs
         // drop the tried columns: popped candidates and the successful top
         for (int c = lane; c < nused; c += AW)
             if (!C.alive[c] || c == top) atomicAnd(&pbits[C.slot[c] >> 6], ~(1ull << (C.slot[c] & 63)));
-        __syncthreads();
+        am_sync();
         pool_prefix(P);
         N = __builtin_amdgcn_readfirstlane(N - nrem);
         nsucc_valid = false;  // a claim and removed columns: recounted when it may pay off
         last_npop = npop;
-        __syncthreads();
+        am_sync();
         AM_T(6);
     }
     if (cabort) {  // (the scores written at this attempt's claims are the redo's too: same arithmetic)
@@ -1751,9 +1756,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     }
     {  // back to the glibc ring: f advanced by the calls made, oldest word at f
         const int f1 = (A.rng[f].f + used) % 31;
-        __syncthreads();
+        am_sync();
         if (lane < 31) A.rng[f].state[(f1 + lane) % 31] = (int32_t)rs;
-        __syncthreads();
+        am_sync();
         if (lane == 0) {
             A.rng[f].f = f1;
             A.rng[f].r = (f1 + 28) % 31;
