@@ -155,88 +155,172 @@ __device__ __forceinline__ E cell_entry(int S, int X, int Y, const Planes& P, co
     }
 }
 
-// -------------------------------------------------------------- k_resize
-// cv::resize INTER_LINEAR, level l from level l-1 (ORBextractor.cc:1063-1068).
-// xtab[dx] = (sx, a0 | a1<<16), ytab[dy] = (sy, b0 | b1<<16) precomputed on
-// the host with OpenCV's float coefficient arithmetic. One 256-thread
-// workgroup per 64 x RS_H output tile: the source rows and columns the tile
-// reads go to LDS as aligned dwords (one batch of loads), then each thread
-// makes one column's outputs in RS_H / 4 rows from LDS. Tall tiles keep more
-// bytes in flight per workgroup: the kernel is bound by load latency, not
-// bandwidth (64-row tiles: 0.42 -> 0.34 ms for the 7 levels of 256 frames).
-#define RS_W 64
-#ifndef RS_H
-#define RS_H 64
-#endif
-#define RS_RPT (RS_H / 4)
-__global__ __launch_bounds__(256) void k_resize(Planes P, LevelGeom g, int l, const int2* __restrict__ xtab,
-                                                const int2* __restrict__ ytab, int tiles_x, int pitch, int max_rows) {
-    extern __shared__ __align__(16) uint32_t rs_lds[];
-    uint8_t* src = reinterpret_cast<uint8_t*>(rs_lds);
-    uint8_t* rsh = src + (size_t)pitch * max_rows;  // byte offset of each row's first needed column
-    // the tile's RS_H y-table entries (a row's entry is the same for a whole wave)
-    int2* yt_s = reinterpret_cast<int2*>(src + (((size_t)pitch * max_rows + max_rows + 15) & ~(size_t)15));
-    int bx, f;
-    gfd::xcd_block(bx, f);
+// -------------------------------------------------------------- k_pyramid
+// cv::resize INTER_LINEAR, level l from level l-1 (ORBextractor.cc:1063-1068),
+// every level in one launch. xtab[dx] = (sx, a0 | a1<<16), ytab[dy] = (sy,
+// b0 | b1<<16) are OpenCV's fixed-point coefficients (2048 = 1.0), made on the
+// host with its float arithmetic.
+// Each level is cut into the same nbx x nby grid of blocks (block k of a
+// level of width w owns columns k w / nbx .. (k + 1) w / nbx - 1). One
+// 256-thread workgroup per (frame, block) takes the level-0 pixels its block
+// column needs through all the levels into LDS once, then makes level 1, 2,
+// ... from the previous level in LDS: at each level the pixels it owns plus
+// the few the next level's owned pixels read beyond them (the required span,
+// PyrSpan.lo .. hi, made on the host from the tables top-down). A pixel is a
+// function of the level below only, so a span pixel recomputed by a
+// neighbouring block is the same byte; only the owner stores it. No
+// workgroup waits for another, and one launch replaces one per level.
+struct PyrSpan {
+    int16_t lo, hi;    // required pixels of the level, inclusive
+    int16_t olo, ohi;  // owned pixels [olo, ohi) (level 0: none)
+};
+struct PyrGeom {
+    int nbx, nby;
+    int rx, ry;     // int2 entries per block-column / block-row record
+    int lds_a;      // bytes of the even levels' buffer (the odd levels' follows)
+    int lds_img;    // bytes of both buffers (the records follow)
+};
+#define PYR_NT 512  // threads per block
+#define PYR_G 4     // output pixels per item (a row's 4 consecutive columns)
+
+__device__ __forceinline__ int pyr_pitch(int span) { return (span + 8 + 3) & ~3; }
+
+// Record of a block column (rows alike): its PyrSpan at each of the nl levels,
+// then for levels 1 .. nl-1 the table entries (sx, a0 | a1 << 16) of its
+// required columns in order. Both records go to LDS with the level-0 pixels,
+// so the level passes wait on LDS only.
+// A level pass: thread t takes column group g = t % ng (PYR_G columns from
+// x0 = lo + PYR_G g) in rows t / ng, + NT / ng, ... (every thread of a group
+// keeps its columns' taps in registers). Per source row: the three LDS dwords
+// from the group's first tap realigned to two (v_alignbyte), each column's tap
+// pair picked as 16-bit lanes (v_perm_b32) and weighted by v_dot2_u32_u16
+// (p0 a0 + p1 a1, exactly the 32-bit sum); then the vertical step as OpenCV's
+// ((b0 (t0 >> 4)) >> 16) + ((b1 (t1 >> 4)) >> 16) + 2 >> 2. The host planned
+// the group width so that a group's taps span at most 7 bytes (scale <= 2 at
+// 4 columns; larger scales take 2 or 1).
+template <int G>
+__global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGeom pg, const int2* __restrict__ xrec,
+                                                    const int2* __restrict__ yrec) {
+    extern __shared__ __align__(16) uint8_t pyr_lds[];
+    int blk, f;
+    gfd::xcd_block(blk, f);
     const int tid = threadIdx.x;
-    const int tx = bx % tiles_x, ty = bx / tiles_x;
-    const int dw = g.w[l], dh = g.h[l], sw = g.w[l - 1], sh = g.h[l - 1];
-    const int X0 = tx * RS_W, Y0 = ty * RS_H;
-    const int xl = min(X0 + RS_W - 1, dw - 1), yl = min(Y0 + RS_H - 1, dh - 1);
-    const int cs = xtab[X0].x, ce = min(xtab[xl].x + 1, sw - 1);
-    const int rs = min(max(ytab[Y0].x, 0), sh - 1), re = min(max(ytab[yl].x + 1, 0), sh - 1);
-    const int nrows = re - rs + 1, span = ce - cs + 1;
-    const int ndw = pitch / 4;  // dwords per LDS row (covers 3 + span bytes)
-    int sstride;
-    const uint8_t* S = level_plane(P, g, f, l - 1, sstride);
-    uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l];
-    // this thread's table entries, fetched alongside the source rows
-    const int x = X0 + (tid & 63), yb = Y0 + RS_RPT * (tid >> 6);
-    const int2 xt = xtab[min(x, xl)];
-    if (tid < RS_H) yt_s[tid] = ytab[min(Y0 + tid, yl)];
-    constexpr int RS_LB = 8;  // dwords per thread per load batch
-    for (int i0 = 0; i0 < nrows * ndw; i0 += 256 * RS_LB) {
-        uint32_t v[RS_LB];
+    const int kx = blk % pg.nbx, ky = blk / pg.nbx;
+    const int nl = g.nlevels;
+    int2* tx = reinterpret_cast<int2*>(pyr_lds + pg.lds_img);
+    int2* ty = tx + pg.rx;
+    auto ld2 = [](const int2* p) {
+        return __builtin_bit_cast(int2, gfd::ldg(reinterpret_cast<const unsigned long long*>(p)));
+    };
+    for (int i = tid; i < pg.rx; i += PYR_NT) tx[i] = ld2(xrec + (long long)kx * pg.rx + i);
+    for (int i = tid; i < pg.ry; i += PYR_NT) ty[i] = ld2(yrec + (long long)ky * pg.ry + i);
+    auto span = [](int2 e) { return __builtin_bit_cast(PyrSpan, e); };
+    {  // level 0: the block's source rectangle, realigned so LDS column 0 is its first column
+        const PyrSpan sx = span(ld2(xrec + (long long)kx * pg.rx)), sy = span(ld2(yrec + (long long)ky * pg.ry));
+        const int w0 = sx.hi - sx.lo + 1, nr = sy.hi - sy.lo + 1, pitch = pyr_pitch(w0), ndw = pitch >> 2;
+        int stride;
+        const uint8_t* S = level_plane(P, g, f, 0, stride);
+        uint32_t* A = reinterpret_cast<uint32_t*>(pyr_lds);
+        constexpr int LB = 8;  // dwords per thread per batch, all in flight
+        for (int i0 = 0; i0 < nr * ndw; i0 += PYR_NT * LB) {
+            uint32_t lo[LB], hi[LB], sh[LB];
 #pragma unroll
-        for (int k = 0; k < RS_LB; k++) {
-            const int i = i0 + 256 * k + tid;
-            const int r = i / ndw, q = i - r * ndw;
-            v[k] = 0;
-            if (r < nrows) {
-                const uintptr_t a = (uintptr_t)(S + (long long)(rs + r) * sstride + cs);
-                if (4 * q < (int)(a & 3) + span)  // only dwords that hold a needed byte
-                    v[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
+            for (int k = 0; k < LB; k++) {
+                const int i = i0 + PYR_NT * k + tid;
+                const int r = i / ndw, q = i - r * ndw;
+                lo[k] = hi[k] = sh[k] = 0u;
+                if (r < nr && 4 * q < w0) {
+                    const uintptr_t a = (uintptr_t)(S + (long long)(sy.lo + r) * stride + sx.lo) + 4 * q;
+                    const uintptr_t al = a & ~(uintptr_t)3;
+                    sh[k] = (uint32_t)(a & 3);
+                    // the second aligned dword only when one of the needed bytes lies in it
+                    const bool two = sh[k] != 0 && 4 * q + 4 - (int)sh[k] < w0;
+                    lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(al));
+                    hi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(two ? al + 4 : al));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < LB; k++) {
+                const int i = i0 + PYR_NT * k + tid;
+                if (i < nr * ndw) A[i] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
             }
         }
-#pragma unroll
-        for (int k = 0; k < RS_LB; k++) {
-            const int i = i0 + 256 * k + tid;
-            if (i < nrows * ndw) rs_lds[i] = v[k];
-        }
     }
-    for (int r = tid; r < nrows; r += 256) rsh[r] = (uint8_t)((uintptr_t)(S + (long long)(rs + r) * sstride + cs) & 3);
     __syncthreads();
-    // thread: column X0 + (tid & 63), rows yb .. yb + RS_RPT - 1 (a wave stores 64 consecutive bytes)
-    if (x > xl) return;
-    // at sx = sw - 1 the table holds a0 = 2048, a1 = 0 (fx clamped to 0), so the
-    // second tap (an in-allocation LDS byte past the span) weighs nothing
-    const int sx = xt.x - cs, a0 = xt.y & 0xffff, a1 = xt.y >> 16;
-    uint8_t* dp = D + (long long)yb * dw + x;
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    int offx = nl, offy = nl;  // the level's first table entry in the records
+    for (int l = 1; l < nl; l++) {
+        const PyrSpan ssx = span(tx[l - 1]), ssy = span(ty[l - 1]);
+        const PyrSpan dsx = span(tx[l]), dsy = span(ty[l]);
+        const uint8_t* src = pyr_lds + ((l - 1) & 1 ? pg.lds_a : 0);
+        uint8_t* dst = pyr_lds + (l & 1 ? pg.lds_a : 0);
+        const int sp = pyr_pitch(ssx.hi - ssx.lo + 1);
+        const int dspan = dsx.hi - dsx.lo + 1, dp = pyr_pitch(dspan), nrow = dsy.hi - dsy.lo + 1;
+        const int ng = (dspan + G - 1) / G, rstep = PYR_NT / ng;
+        const int gi = tid % ng, r00 = tid / ng;
+        const int sh = g.h[l - 1], dw = g.w[l];
+        uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l];
+        // the group's taps: first tap's LDS column c0, per column the byte of its
+        // pair in the realigned 8 bytes and the weights (a0, a1) as u16 lanes
+        const int x0 = dsx.lo + G * gi;
+        int c0 = 0;
+        uint32_t sel[G], wgt[G];
+        unsigned own = 0;
+        if (r00 < rstep) {
+            c0 = tx[offx + G * gi].x - ssx.lo;
 #pragma unroll
-    for (int i = 0; i < RS_RPT; i++, dp += dw) {
-        if (yb + i > yl) continue;  // (no break: the loop stays unrolled, yts in registers)
-        const int2 yt = yt_s[yb - Y0 + i];
-        const int r0 = min(max(yt.x, 0), sh - 1) - rs, r1 = min(max(yt.x + 1, 0), sh - 1) - rs;
-        const int b0 = yt.y & 0xffff, b1 = yt.y >> 16;
-        // the two taps of a row from two aligned LDS dwords (a byte pair at an
-        // odd address would become one misaligned ds_read_u16, a slow path)
-        const int o0 = r0 * pitch + rsh[r0] + sx, o1 = r1 * pitch + rsh[r1] + sx;
-        const uint32_t p0 = __builtin_amdgcn_alignbyte(rs_lds[(o0 >> 2) + 1], rs_lds[o0 >> 2], o0 & 3);
-        const uint32_t p1 = __builtin_amdgcn_alignbyte(rs_lds[(o1 >> 2) + 1], rs_lds[o1 >> 2], o1 & 3);
-        const int t0 = __mul24((int)(p0 & 0xff), a0) + __mul24((int)((p0 >> 8) & 0xff), a1);
-        const int t1 = __mul24((int)(p1 & 0xff), a0) + __mul24((int)((p1 >> 8) & 0xff), a1);
-        const int v = ((__mul24(b0, t0 >> 4) >> 16) + (__mul24(b1, t1 >> 4) >> 16) + 2) >> 2;
-        *dp = (uint8_t)min(max(v, 0), 255);
+            for (int k = 0; k < G; k++) {
+                const int c = G * gi + k;
+                const int2 e = c < dspan ? tx[offx + c] : make_int2(ssx.lo + c0, 0);
+                const uint32_t d = (uint32_t)(e.x - ssx.lo - c0);
+                sel[k] = d | 0x0c00u | (d + 1) << 16 | 0x0c000000u;
+                wgt[k] = (uint32_t)e.y;  // a0 | a1 << 16; 0 past the span
+                own |= (unsigned)(c < dspan && x0 + k >= dsx.olo && x0 + k < dsx.ohi) << k;
+            }
+        }
+        const int cq = c0 >> 2, csh = c0 & 3;
+        for (int r = r00; r < nrow && r00 < rstep; r += rstep) {
+            const int y = dsy.lo + r;
+            const int2 e = ty[offy + r];
+            const int r0 = min(max(e.x, 0), sh - 1) - ssy.lo, r1 = min(max(e.x + 1, 0), sh - 1) - ssy.lo;
+            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + r0 * sp) + cq;
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + r1 * sp) + cq;
+            const uint32_t u0 = s0[0], u1 = s0[1], u2 = s0[2], v0 = s1[0], v1 = s1[1], v2 = s1[2];
+            const uint32_t ua = __builtin_amdgcn_alignbyte(u1, u0, csh), ub = __builtin_amdgcn_alignbyte(u2, u1, csh);
+            const uint32_t va = __builtin_amdgcn_alignbyte(v1, v0, csh), vb = __builtin_amdgcn_alignbyte(v2, v1, csh);
+            const uint32_t b0 = (uint32_t)e.y & 0xffffu, b1 = (uint32_t)e.y >> 16;
+            uint32_t o = 0;
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+                const u16x2 w = __builtin_bit_cast(u16x2, wgt[k]);
+                const uint32_t t0 =
+                    __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(ub, ua, sel[k])), w, 0u, false);
+                const uint32_t t1 =
+                    __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(vb, va, sel[k])), w, 0u, false);
+                const uint32_t v = ((__mul24(b0, t0 >> 4) >> 16) + (__mul24(b1, t1 >> 4) >> 16) + 2) >> 2;
+                o |= min(v, 255u) << (8 * k);
+            }
+            if constexpr (G == 4) {
+                *reinterpret_cast<uint32_t*>(dst + r * dp + G * gi) = o;
+            } else {
+#pragma unroll
+                for (int k = 0; k < G; k++) dst[r * dp + G * gi + k] = (uint8_t)(o >> (8 * k));
+            }
+            if (y >= dsy.olo && y < dsy.ohi && own) {
+                uint8_t* q = D + (long long)y * dw + x0;
+                if (own == (1u << G) - 1u) {
+#pragma unroll
+                    for (int k = 0; k < G; k++) q[k] = (uint8_t)(o >> (8 * k));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < G; k++)
+                        if ((own >> k) & 1u) q[k] = (uint8_t)(o >> (8 * k));
+                }
+            }
+        }
+        offx += dspan;
+        offy += nrow;
+        __syncthreads();
     }
 }
 
@@ -1416,9 +1500,10 @@ struct gf_extractor {
     int max_tiles = 0;
     // device buffers
     uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
-    int2 *d_xtab = nullptr, *d_ytab = nullptr;
-    std::vector<long long> xtab_off, ytab_off;
-    std::vector<int> rs_pitch, rs_rows, rs_tiles_x, rs_tiles;
+    int2 *d_xtab = nullptr, *d_ytab = nullptr;  // k_pyramid's block-column / block-row records
+    PyrGeom pg{};
+    size_t pyr_lds = 0;
+    int pyr_g = PYR_G;  // k_pyramid's columns per item (1 when a 4-column group's taps span more than 7 bytes)
     CellInfo* d_cells = nullptr;
     void *d_lists = nullptr, *d_lvl = nullptr;  // uint32_t (FAST) or uint64_t (Harris) entries
     int *d_counts = nullptr, *d_lvl_counts = nullptr;
@@ -1615,6 +1700,79 @@ static void resize_tables(int sw, int sh, int dw, int dh, std::vector<int2>& xt,
     }
 }
 
+// k_pyramid's blocks: each level cut into the same nbx x nby grid; top-down
+// from the last level, a block's required span at level l is its owned
+// pixels plus the source pixels (both taps) of its required span at l + 1
+// (level 0: the source pixels only). Blocks start near 128 x 96 level-0 px
+// and shrink until every computed span is at most 256 columns and the
+// two LDS buffers (even / odd levels) fit 64 KB.
+static void pyr_axis(const LevelGeom& g, const std::vector<std::vector<int2>>& tabs, bool is_x, int nb,
+                     std::vector<PyrSpan>& out, int& maxspan) {
+    const int nl = g.nlevels;
+    out.assign((size_t)nl * nb, PyrSpan{});
+    maxspan = 0;
+    for (int k = 0; k < nb; k++) {
+        int lo = 0, hi = 0;
+        for (int l = nl - 1; l >= 0; l--) {
+            const int n = is_x ? g.w[l] : g.h[l];
+            int rlo = 0, rhi = 0;
+            if (l < nl - 1) {  // the taps of level l + 1's required span (rows clamped as the kernel clamps them)
+                const std::vector<int2>& t = tabs[l + 1];
+                rlo = std::min(std::max(t[lo].x, 0), n - 1);
+                rhi = std::min(std::max(t[hi].x + 1, 0), n - 1);
+            }
+            PyrSpan s{};
+            if (l >= 1) {
+                const int olo = (int)((long long)k * n / nb), ohi = (int)((long long)(k + 1) * n / nb);
+                s.olo = (int16_t)olo;
+                s.ohi = (int16_t)ohi;
+                lo = l < nl - 1 ? std::min(rlo, olo) : olo;
+                hi = l < nl - 1 ? std::max(rhi, ohi - 1) : ohi - 1;
+                maxspan = std::max(maxspan, hi - lo + 1);
+            } else {
+                lo = rlo;
+                hi = rhi;
+            }
+            s.lo = (int16_t)lo;
+            s.hi = (int16_t)hi;
+            out[(size_t)l * nb + k] = s;
+        }
+    }
+}
+
+static bool pyr_plan(const LevelGeom& g, const std::vector<std::vector<int2>>& xts,
+                     const std::vector<std::vector<int2>>& yts, PyrGeom& pg, std::vector<PyrSpan>& spx,
+                     std::vector<PyrSpan>& spy, size_t& lds) {
+    const int nl = g.nlevels;
+    int nbx = std::max(1, (g.w[0] + 127) / 128), nby = std::max(1, (g.h[0] + 95) / 96);
+    const int nmax = std::min(g.w[nl - 1], g.h[nl - 1]) / 2;  // at least two owned pixels per block and level
+    while (nbx <= nmax && nby <= nmax) {
+        int mx, my;
+        pyr_axis(g, xts, true, nbx, spx, mx);
+        pyr_axis(g, yts, false, nby, spy, my);
+        size_t buf[2] = {0, 0};
+        for (int l = 0; l < nl; l++)
+            for (int kx = 0; kx < nbx; kx++)
+                for (int ky = 0; ky < nby; ky++) {
+                    const PyrSpan& a = spx[(size_t)l * nbx + kx];
+                    const PyrSpan& b = spy[(size_t)l * nby + ky];
+                    const size_t pitch = (size_t)((a.hi - a.lo + 1 + 8 + 3) & ~3);
+                    buf[l & 1] = std::max(buf[l & 1], pitch * (size_t)(b.hi - b.lo + 1));
+                }
+        buf[0] = (buf[0] + 15) & ~(size_t)15;
+        if (mx <= 256 && buf[0] + buf[1] <= 64 * 1024) {
+            pg.nbx = nbx;
+            pg.nby = nby;
+            pg.lds_a = (int)buf[0];
+            lds = buf[0] + buf[1];
+            return true;
+        }
+        if (mx > 256 || (double)g.w[0] / nbx >= (double)g.h[0] / nby) nbx++;
+        else nby++;
+    }
+    return false;
+}
+
 static void free_extractor(gf_extractor* ex) {
     (void)hipFree(ex->d_pyr);
     (void)hipFree(ex->d_blur);
@@ -1724,50 +1882,58 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     ALLOC(ex->d_kps, sizeof(gf_keypoint) * ex->capacity);
     ALLOC(ex->d_desc, 32 * (size_t)ex->capacity);
     ALLOC(ex->d_nout, sizeof(int));
-    // resize tables for levels 1..nl-1
-    std::vector<int2> xall, yall, xt, yt;
-    ex->xtab_off.assign(nlevels, 0);
-    ex->ytab_off.assign(nlevels, 0);
-    ex->rs_pitch.assign(nlevels, 0);
-    ex->rs_rows.assign(nlevels, 0);
-    ex->rs_tiles_x.assign(nlevels, 0);
-    ex->rs_tiles.assign(nlevels, 0);
-    for (int l = 1; l < nlevels; l++) {
-        resize_tables(g.w[l - 1], g.h[l - 1], g.w[l], g.h[l], xt, yt);
-        {  // LDS geometry of k_resize's tiles: widest column span, most source rows
-            const int sw = g.w[l - 1], sh = g.h[l - 1], dw = g.w[l], dh = g.h[l];
-            int maxspan = 1, maxrows = 1;
-            for (int X0 = 0; X0 < dw; X0 += RS_W) {
-                const int xl = std::min(X0 + RS_W - 1, dw - 1);
-                maxspan = std::max(maxspan, std::min(xt[xl].x + 1, sw - 1) - xt[X0].x + 1);
-            }
-            for (int Y0 = 0; Y0 < dh; Y0 += RS_H) {
-                const int yl = std::min(Y0 + RS_H - 1, dh - 1);
-                const int rs = std::min(std::max(yt[Y0].x, 0), sh - 1), re = std::min(std::max(yt[yl].x + 1, 0), sh - 1);
-                maxrows = std::max(maxrows, re - rs + 1);
-            }
-            ex->rs_pitch[l] = ((maxspan + 3) + 3) / 4 * 4;
-            ex->rs_rows[l] = maxrows;
-            ex->rs_tiles_x[l] = (dw + RS_W - 1) / RS_W;
-            ex->rs_tiles[l] = ex->rs_tiles_x[l] * ((dh + RS_H - 1) / RS_H);
-            const size_t lds = (size_t)ex->rs_pitch[l] * maxrows + maxrows + 8;
-            if (lds > 64 * 1024) {
-                free_extractor(ex);
-                delete ex;
-                return gf::fail(GF_ERR_UNSUPPORTED, "scale factor too large for the resize tile");
-            }
-        }
-        ex->xtab_off[l] = (long long)xall.size();
-        ex->ytab_off[l] = (long long)yall.size();
-        xall.insert(xall.end(), xt.begin(), xt.end());
-        yall.insert(yall.end(), yt.begin(), yt.end());
+    // resize tables for levels 1..nl-1, and k_pyramid's block spans
+    std::vector<std::vector<int2>> xts(nlevels), yts(nlevels);
+    for (int l = 1; l < nlevels; l++) resize_tables(g.w[l - 1], g.h[l - 1], g.w[l], g.h[l], xts[l], yts[l]);
+    std::vector<PyrSpan> spx, spy;
+    if (nlevels > 1 && !pyr_plan(g, xts, yts, ex->pg, spx, spy, ex->pyr_lds)) {
+        free_extractor(ex);
+        delete ex;
+        return gf::fail(GF_ERR_UNSUPPORTED, "scale factor too large for the pyramid blocks");
     }
-    ALLOC(ex->d_xtab, sizeof(int2) * std::max<size_t>(xall.size(), 1));
-    ALLOC(ex->d_ytab, sizeof(int2) * std::max<size_t>(yall.size(), 1));
+    // k_pyramid's column groups: PYR_G columns whose taps lie within 8 bytes
+    // of the group's first tap (else one column per item)
+    for (int l = 1; l < nlevels && ex->pyr_g > 1; l++)
+        for (int k = 0; k < ex->pg.nbx; k++) {
+            const PyrSpan& sp = spx[(size_t)l * ex->pg.nbx + k];
+            for (int x0 = sp.lo; x0 <= sp.hi; x0 += PYR_G)
+                if (xts[l][std::min(x0 + PYR_G - 1, (int)sp.hi)].x - xts[l][x0].x + 1 > 7) ex->pyr_g = 1;
+        }
+    // the block-column / block-row records (k_pyramid)
+    std::vector<int2> xrec, yrec;
+    if (nlevels > 1) {
+        auto records = [&](const std::vector<PyrSpan>& sp, const std::vector<std::vector<int2>>& tabs, int nb,
+                           std::vector<int2>& rec) -> int {
+            std::vector<std::vector<int2>> r(nb);
+            size_t stride = 0;
+            for (int k = 0; k < nb; k++) {
+                for (int l = 0; l < nlevels; l++) r[k].push_back(__builtin_bit_cast(int2, sp[(size_t)l * nb + k]));
+                for (int l = 1; l < nlevels; l++) {
+                    const PyrSpan& s = sp[(size_t)l * nb + k];
+                    for (int v = s.lo; v <= s.hi; v++) r[k].push_back(tabs[l][v]);
+                }
+                stride = std::max(stride, r[k].size());
+            }
+            stride = (stride + 1) & ~(size_t)1;
+            rec.assign(stride * nb, make_int2(0, 0));
+            for (int k = 0; k < nb; k++) std::copy(r[k].begin(), r[k].end(), rec.begin() + (size_t)k * stride);
+            return (int)stride;
+        };
+        ex->pg.rx = records(spx, xts, ex->pg.nbx, xrec);
+        ex->pg.ry = records(spy, yts, ex->pg.nby, yrec);
+        ex->pg.lds_img = (int)((ex->pyr_lds + 15) & ~(size_t)15);
+        ex->pyr_lds = ex->pg.lds_img + sizeof(int2) * (size_t)(ex->pg.rx + ex->pg.ry);
+    }
+    ALLOC(ex->d_xtab, sizeof(int2) * std::max<size_t>(xrec.size(), 1));
+    ALLOC(ex->d_ytab, sizeof(int2) * std::max<size_t>(yrec.size(), 1));
 #undef ALLOC
-    if (!xall.empty()) {
-        GF_HIP(hipMemcpy(ex->d_xtab, xall.data(), sizeof(int2) * xall.size(), hipMemcpyHostToDevice));
-        GF_HIP(hipMemcpy(ex->d_ytab, yall.data(), sizeof(int2) * yall.size(), hipMemcpyHostToDevice));
+    if (!xrec.empty()) {
+        GF_HIP(hipMemcpy(ex->d_xtab, xrec.data(), sizeof(int2) * xrec.size(), hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy(ex->d_ytab, yrec.data(), sizeof(int2) * yrec.size(), hipMemcpyHostToDevice));
+        GF_HIP(hipFuncSetAttribute((const void*)k_pyramid<PYR_G>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)ex->pyr_lds));
+        GF_HIP(hipFuncSetAttribute((const void*)k_pyramid<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)ex->pyr_lds));
     }
     GF_HIP(hipMemcpy(ex->d_cells, ex->cells.data(), sizeof(CellInfo) * ex->cells.size(), hipMemcpyHostToDevice));
     if (!ex->band_cells.empty())
@@ -1844,13 +2010,15 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     ex->last = P;
     gf_ctx* ctx = ex->ctx;
     {
-        GF_PROF(ctx, s, "k_resize");
-        for (int l = 1; l < ex->nlevels; l++) {
-            const size_t lds = (((size_t)ex->rs_pitch[l] * ex->rs_rows[l] + ex->rs_rows[l] + 15) & ~(size_t)15) +
-                               RS_H * sizeof(int2) + 8;
-            GF_LAUNCH(k_resize, dim3(ex->rs_tiles[l], nframes), 256, lds, s, P, g, l, ex->d_xtab + ex->xtab_off[l],
-                                                                      ex->d_ytab + ex->ytab_off[l], ex->rs_tiles_x[l],
-                                                                      ex->rs_pitch[l], ex->rs_rows[l]);
+        GF_PROF(ctx, s, "k_pyramid");
+        if (ex->nlevels > 1)
+        {
+            if (ex->pyr_g == PYR_G)
+                GF_LAUNCH(k_pyramid<PYR_G>, dim3(ex->pg.nbx * ex->pg.nby, nframes), PYR_NT, ex->pyr_lds, s, P, g,
+                          ex->pg, ex->d_xtab, ex->d_ytab);
+            else
+                GF_LAUNCH(k_pyramid<1>, dim3(ex->pg.nbx * ex->pg.nby, nframes), PYR_NT, ex->pyr_lds, s, P, g, ex->pg,
+                          ex->d_xtab, ex->d_ytab);
         }
     }
     if (ex->stage_ev && ex->stage_after == 0) GF_HIP(hipEventRecord(ex->stage_ev, s));

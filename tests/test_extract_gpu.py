@@ -29,6 +29,21 @@ def test_pyramid_and_blur_bit_exact(cam, nf, seed):
                                       err_msg=f"blurred level {lvl}")
 
 
+@pytest.mark.parametrize("w,h,scale,nl", [(1241, 376, 1.2, 8), (1920, 1080, 1.2, 8), (640, 480, 1.5, 5),
+                                          (752, 480, 2.0, 4), (800, 600, 3.0, 3), (320, 240, 1.1, 10)])
+def test_pyramid_geometries(w, h, scale, nl):
+    """k_pyramid's block plan (spans, column groups of 4 or 1) on other frame
+    sizes and scale factors: every level and its blur bit-exact."""
+    img = synth.synth_frame(w, h, synth.frame_seed(1, w + nl))
+    ex = ORBextractor(1000, scale, nl, 1, 20)
+    ex(img)
+    for lvl in range(nl):
+        np.testing.assert_array_equal(ex.debug_level(lvl, 0), O.level(img, lvl, 0, scale=scale, nlevels=nl),
+                                      err_msg=f"pyramid level {lvl}")
+        np.testing.assert_array_equal(ex.debug_level(lvl, 1), O.level(img, lvl, 1, scale=scale, nlevels=nl),
+                                      err_msg=f"blurred level {lvl}")
+
+
 def _diff_report(kg, ko):
     n = min(len(kg), len(ko))
     bad = np.nonzero(kg[:n].tobytes() != ko[:n].tobytes())
