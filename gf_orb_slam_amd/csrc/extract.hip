@@ -176,7 +176,7 @@ struct PyrSpan {
 };
 struct PyrGeom {
     int nbx, nby;
-    int rx, ry;     // int2 entries per block-column / block-row record
+    int rx, ry;     // dwords per block-column / block-row record
     int lds_a;      // bytes of the even levels' buffer (the odd levels' follows)
     int lds_img;    // bytes of both buffers (the records follow)
 };
@@ -185,41 +185,52 @@ struct PyrGeom {
 
 __device__ __forceinline__ int pyr_pitch(int span) { return (span + 8 + 3) & ~3; }
 
-// Record of a block column (rows alike): its PyrSpan at each of the nl levels,
-// then for levels 1 .. nl-1 the table entries (sx, a0 | a1 << 16) of its
-// required columns in order. Both records go to LDS with the level-0 pixels,
-// so the level passes wait on LDS only.
-// A level pass: thread t takes column group g = t % ng (PYR_G columns from
-// x0 = lo + PYR_G g) in rows t / ng, + NT / ng, ... (every thread of a group
-// keeps its columns' taps in registers). Per source row: the three LDS dwords
-// from the group's first tap realigned to two (v_alignbyte), each column's tap
-// pair picked as 16-bit lanes (v_perm_b32) and weighted by v_dot2_u32_u16
-// (p0 a0 + p1 a1, exactly the 32-bit sum); then the vertical step as OpenCV's
-// ((b0 (t0 >> 4)) >> 16) + ((b1 (t1 >> 4)) >> 16) + 2 >> 2. The host planned
-// the group width so that a group's taps span at most 7 bytes (scale <= 2 at
-// 4 columns; larger scales take 2 or 1).
+// floor(i / n) for 0 <= i < 2^16, 1 <= n <= 2^10 (rcp is exact enough there)
+__device__ __forceinline__ int pyr_div(int i, float rn) { return (int)(((float)i + 0.5f) * rn); }
+
+// Records, made on the host, staged in LDS with the level-0 pixels (the level
+// passes then wait on LDS only). Block column: the PyrSpan of each of the nl
+// levels (2 dwords), then per level 1 .. nl-1 and column group (G columns
+// from x0 = lo + G g): {c0 | d1 << 16 | d2 << 20 | d3 << 24 | own << 28} and
+// the G weights a0 | a1 << 16; c0 = the first column's left tap in the
+// source span, d_k = column k's left tap past c0, own = the columns this
+// block stores. Block row: spans, then per level and row {r0 | r1 << 16 |
+// own << 31} (source rows in the source span, clamped as OpenCV clamps) and
+// b0 | b1 << 16.
+// A level pass: thread t takes column group g = t % ng in rows t / ng,
+// + NT / ng, ... Per source row: the three LDS dwords from the group's first
+// tap realigned to two (v_alignbyte), each column's tap pair picked as 16-bit
+// lanes (v_perm_b32) and weighted by v_dot2_u32_u16 (p0 a0 + p1 a1, the
+// exact sum); then OpenCV's vertical step ((b0 (t0 >> 4)) >> 16) +
+// ((b1 (t1 >> 4)) >> 16) + 2 >> 2, at most 255 as the weights sum to at most
+// 2049 (checked on the host), so no clamp. The host takes G = 4 when every
+// group's taps lie within 8 bytes of its first (scale <= 2), else G = 1.
 template <int G>
-__global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGeom pg, const int2* __restrict__ xrec,
-                                                    const int2* __restrict__ yrec) {
+__global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGeom pg,
+                                                    const uint32_t* __restrict__ xrec,
+                                                    const uint32_t* __restrict__ yrec) {
     extern __shared__ __align__(16) uint8_t pyr_lds[];
     int blk, f;
     gfd::xcd_block(blk, f);
     const int tid = threadIdx.x;
     const int kx = blk % pg.nbx, ky = blk / pg.nbx;
     const int nl = g.nlevels;
-    int2* tx = reinterpret_cast<int2*>(pyr_lds + pg.lds_img);
-    int2* ty = tx + pg.rx;
-    auto ld2 = [](const int2* p) {
-        return __builtin_bit_cast(int2, gfd::ldg(reinterpret_cast<const unsigned long long*>(p)));
+    uint32_t* tx = reinterpret_cast<uint32_t*>(pyr_lds + pg.lds_img);
+    uint32_t* ty = tx + pg.rx;
+    for (int i = tid; i < pg.rx; i += PYR_NT) tx[i] = gfd::ldg(xrec + (long long)kx * pg.rx + i);
+    for (int i = tid; i < pg.ry; i += PYR_NT) ty[i] = gfd::ldg(yrec + (long long)ky * pg.ry + i);
+    auto span = [](const uint32_t* r, int l) {
+        return __builtin_bit_cast(PyrSpan, make_uint2(r[2 * l], r[2 * l + 1]));
     };
-    for (int i = tid; i < pg.rx; i += PYR_NT) tx[i] = ld2(xrec + (long long)kx * pg.rx + i);
-    for (int i = tid; i < pg.ry; i += PYR_NT) ty[i] = ld2(yrec + (long long)ky * pg.ry + i);
-    auto span = [](int2 e) { return __builtin_bit_cast(PyrSpan, e); };
     {  // level 0: the block's source rectangle, realigned so LDS column 0 is its first column
-        const PyrSpan sx = span(ld2(xrec + (long long)kx * pg.rx)), sy = span(ld2(yrec + (long long)ky * pg.ry));
+        const uint32_t* gx = xrec + (long long)kx * pg.rx;
+        const uint32_t* gy = yrec + (long long)ky * pg.ry;
+        const PyrSpan sx = __builtin_bit_cast(PyrSpan, make_uint2(gfd::ldg(gx), gfd::ldg(gx + 1)));
+        const PyrSpan sy = __builtin_bit_cast(PyrSpan, make_uint2(gfd::ldg(gy), gfd::ldg(gy + 1)));
         const int w0 = sx.hi - sx.lo + 1, nr = sy.hi - sy.lo + 1, pitch = pyr_pitch(w0), ndw = pitch >> 2;
+        const float rn = 1.0f / (float)ndw;
         int stride;
-        const uint8_t* S = level_plane(P, g, f, 0, stride);
+        const uint8_t* S = level_plane(P, g, f, 0, stride) + sx.lo;
         uint32_t* A = reinterpret_cast<uint32_t*>(pyr_lds);
         constexpr int LB = 8;  // dwords per thread per batch, all in flight
         for (int i0 = 0; i0 < nr * ndw; i0 += PYR_NT * LB) {
@@ -227,10 +238,10 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
 #pragma unroll
             for (int k = 0; k < LB; k++) {
                 const int i = i0 + PYR_NT * k + tid;
-                const int r = i / ndw, q = i - r * ndw;
+                const int r = pyr_div(i, rn), q = i - r * ndw;
                 lo[k] = hi[k] = sh[k] = 0u;
                 if (r < nr && 4 * q < w0) {
-                    const uintptr_t a = (uintptr_t)(S + (long long)(sy.lo + r) * stride + sx.lo) + 4 * q;
+                    const uintptr_t a = (uintptr_t)(S + (sy.lo + r) * stride) + 4 * q;
                     const uintptr_t al = a & ~(uintptr_t)3;
                     sh[k] = (uint32_t)(a & 3);
                     // the second aligned dword only when one of the needed bytes lies in it
@@ -248,47 +259,40 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
     }
     __syncthreads();
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    int offx = nl, offy = nl;  // the level's first table entry in the records
+    int offx = 2 * nl, offy = 2 * nl;  // the level's first group / row entry in the records
     for (int l = 1; l < nl; l++) {
-        const PyrSpan ssx = span(tx[l - 1]), ssy = span(ty[l - 1]);
-        const PyrSpan dsx = span(tx[l]), dsy = span(ty[l]);
-        const uint8_t* src = pyr_lds + ((l - 1) & 1 ? pg.lds_a : 0);
-        uint8_t* dst = pyr_lds + (l & 1 ? pg.lds_a : 0);
+        const PyrSpan ssx = span(tx, l - 1), dsx = span(tx, l), dsy = span(ty, l);
+        const uint32_t srcb = (l - 1) & 1 ? pg.lds_a : 0u, dstb = l & 1 ? pg.lds_a : 0u;
         const int sp = pyr_pitch(ssx.hi - ssx.lo + 1);
         const int dspan = dsx.hi - dsx.lo + 1, dp = pyr_pitch(dspan), nrow = dsy.hi - dsy.lo + 1;
         const int ng = (dspan + G - 1) / G, rstep = PYR_NT / ng;
-        const int gi = tid % ng, r00 = tid / ng;
-        const int sh = g.h[l - 1], dw = g.w[l];
-        uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l];
-        // the group's taps: first tap's LDS column c0, per column the byte of its
-        // pair in the realigned 8 bytes and the weights (a0, a1) as u16 lanes
+        const int r00 = pyr_div(tid, 1.0f / (float)ng), gi = tid - r00 * ng;
+        const int dw = g.w[l];
         const int x0 = dsx.lo + G * gi;
-        int c0 = 0;
-        uint32_t sel[G], wgt[G];
-        unsigned own = 0;
+        uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l] + x0;
+        uint32_t sel[G], wgt[G], own = 0, cq = 0, csh = 0;
         if (r00 < rstep) {
-            c0 = tx[offx + G * gi].x - ssx.lo;
+            const uint32_t* gr = tx + offx + (1 + G) * gi;
+            const uint32_t h = gr[0];
+            own = h >> 28;
+            cq = (h & 0xffffu) >> 2;
+            csh = h & 3u;
 #pragma unroll
             for (int k = 0; k < G; k++) {
-                const int c = G * gi + k;
-                const int2 e = c < dspan ? tx[offx + c] : make_int2(ssx.lo + c0, 0);
-                const uint32_t d = (uint32_t)(e.x - ssx.lo - c0);
-                sel[k] = d | 0x0c00u | (d + 1) << 16 | 0x0c000000u;
-                wgt[k] = (uint32_t)e.y;  // a0 | a1 << 16; 0 past the span
-                own |= (unsigned)(c < dspan && x0 + k >= dsx.olo && x0 + k < dsx.ohi) << k;
+                const uint32_t d = k == 0 ? 0u : (h >> (12 + 4 * k)) & 15u;
+                sel[k] = d * 0x00010001u + 0x0c010c00u;  // bytes d, d + 1 as 16-bit lanes
+                wgt[k] = gr[1 + k];
             }
         }
-        const int cq = c0 >> 2, csh = c0 & 3;
+        const uint32_t* rows = ty + offy;
         for (int r = r00; r < nrow && r00 < rstep; r += rstep) {
-            const int y = dsy.lo + r;
-            const int2 e = ty[offy + r];
-            const int r0 = min(max(e.x, 0), sh - 1) - ssy.lo, r1 = min(max(e.x + 1, 0), sh - 1) - ssy.lo;
-            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(src + r0 * sp) + cq;
-            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(src + r1 * sp) + cq;
+            const uint32_t rr = rows[2 * r], bb = rows[2 * r + 1];
+            const uint32_t* s0 = reinterpret_cast<const uint32_t*>(pyr_lds + srcb + (rr & 0x7fffu) * sp) + cq;
+            const uint32_t* s1 = reinterpret_cast<const uint32_t*>(pyr_lds + srcb + ((rr >> 16) & 0x7fffu) * sp) + cq;
             const uint32_t u0 = s0[0], u1 = s0[1], u2 = s0[2], v0 = s1[0], v1 = s1[1], v2 = s1[2];
             const uint32_t ua = __builtin_amdgcn_alignbyte(u1, u0, csh), ub = __builtin_amdgcn_alignbyte(u2, u1, csh);
             const uint32_t va = __builtin_amdgcn_alignbyte(v1, v0, csh), vb = __builtin_amdgcn_alignbyte(v2, v1, csh);
-            const uint32_t b0 = (uint32_t)e.y & 0xffffu, b1 = (uint32_t)e.y >> 16;
+            const uint32_t b0 = bb & 0xffffu, b1 = bb >> 16;
             uint32_t o = 0;
 #pragma unroll
             for (int k = 0; k < G; k++) {
@@ -298,16 +302,16 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
                 const uint32_t t1 =
                     __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, __builtin_amdgcn_perm(vb, va, sel[k])), w, 0u, false);
                 const uint32_t v = ((__mul24(b0, t0 >> 4) >> 16) + (__mul24(b1, t1 >> 4) >> 16) + 2) >> 2;
-                o |= min(v, 255u) << (8 * k);
+                o |= v << (8 * k);
             }
             if constexpr (G == 4) {
-                *reinterpret_cast<uint32_t*>(dst + r * dp + G * gi) = o;
+                *reinterpret_cast<uint32_t*>(pyr_lds + dstb + r * dp + G * gi) = o;
             } else {
 #pragma unroll
-                for (int k = 0; k < G; k++) dst[r * dp + G * gi + k] = (uint8_t)(o >> (8 * k));
+                for (int k = 0; k < G; k++) pyr_lds[dstb + r * dp + G * gi + k] = (uint8_t)(o >> (8 * k));
             }
-            if (y >= dsy.olo && y < dsy.ohi && own) {
-                uint8_t* q = D + (long long)y * dw + x0;
+            if ((rr >> 31) && own) {
+                uint8_t* q = D + (dsy.lo + r) * dw;
                 if (own == (1u << G) - 1u) {
 #pragma unroll
                     for (int k = 0; k < G; k++) q[k] = (uint8_t)(o >> (8 * k));
@@ -318,8 +322,8 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
                 }
             }
         }
-        offx += dspan;
-        offy += nrow;
+        offx += (1 + G) * ng;
+        offy += 2 * nrow;
         __syncthreads();
     }
 }
@@ -1500,7 +1504,7 @@ struct gf_extractor {
     int max_tiles = 0;
     // device buffers
     uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
-    int2 *d_xtab = nullptr, *d_ytab = nullptr;  // k_pyramid's block-column / block-row records
+    uint32_t *d_xtab = nullptr, *d_ytab = nullptr;  // k_pyramid's block-column / block-row records
     PyrGeom pg{};
     size_t pyr_lds = 0;
     int pyr_g = PYR_G;  // k_pyramid's columns per item (1 when a 4-column group's taps span more than 7 bytes)
@@ -1900,36 +1904,87 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
                 if (xts[l][std::min(x0 + PYR_G - 1, (int)sp.hi)].x - xts[l][x0].x + 1 > 7) ex->pyr_g = 1;
         }
     // the block-column / block-row records (k_pyramid)
-    std::vector<int2> xrec, yrec;
+    std::vector<uint32_t> xrec, yrec;
     if (nlevels > 1) {
-        auto records = [&](const std::vector<PyrSpan>& sp, const std::vector<std::vector<int2>>& tabs, int nb,
-                           std::vector<int2>& rec) -> int {
-            std::vector<std::vector<int2>> r(nb);
+        const int G = ex->pyr_g;
+        auto pack = [](const std::vector<std::vector<uint32_t>>& r, std::vector<uint32_t>& rec) -> int {
             size_t stride = 0;
-            for (int k = 0; k < nb; k++) {
-                for (int l = 0; l < nlevels; l++) r[k].push_back(__builtin_bit_cast(int2, sp[(size_t)l * nb + k]));
-                for (int l = 1; l < nlevels; l++) {
-                    const PyrSpan& s = sp[(size_t)l * nb + k];
-                    for (int v = s.lo; v <= s.hi; v++) r[k].push_back(tabs[l][v]);
-                }
-                stride = std::max(stride, r[k].size());
-            }
-            stride = (stride + 1) & ~(size_t)1;
-            rec.assign(stride * nb, make_int2(0, 0));
-            for (int k = 0; k < nb; k++) std::copy(r[k].begin(), r[k].end(), rec.begin() + (size_t)k * stride);
+            for (const auto& v : r) stride = std::max(stride, v.size());
+            stride = (stride + 3) & ~(size_t)3;
+            rec.assign(stride * r.size(), 0u);
+            for (size_t k = 0; k < r.size(); k++) std::copy(r[k].begin(), r[k].end(), rec.begin() + k * stride);
             return (int)stride;
         };
-        ex->pg.rx = records(spx, xts, ex->pg.nbx, xrec);
-        ex->pg.ry = records(spy, yts, ex->pg.nby, yrec);
+        auto head = [&](std::vector<uint32_t>& v, const std::vector<PyrSpan>& sp, int nb, int k) {
+            for (int l = 0; l < nlevels; l++) {
+                const uint2 u = __builtin_bit_cast(uint2, sp[(size_t)l * nb + k]);
+                v.push_back(u.x);
+                v.push_back(u.y);
+            }
+        };
+        bool ok = true;
+        std::vector<std::vector<uint32_t>> rx(ex->pg.nbx), ry(ex->pg.nby);
+        for (int k = 0; k < ex->pg.nbx; k++) {
+            head(rx[k], spx, ex->pg.nbx, k);
+            for (int l = 1; l < nlevels; l++) {
+                const PyrSpan& s = spx[(size_t)l * ex->pg.nbx + k];
+                const PyrSpan& ss = spx[(size_t)(l - 1) * ex->pg.nbx + k];
+                for (int x0 = s.lo; x0 <= s.hi; x0 += G) {
+                    const int c0 = xts[l][x0].x - ss.lo;
+                    uint32_t h = (uint32_t)c0, own = 0;
+                    std::vector<uint32_t> w;
+                    for (int j = 0; j < G; j++) {
+                        const int x = x0 + j;
+                        if (x > s.hi) {
+                            w.push_back(0u);
+                            continue;
+                        }
+                        const int d = xts[l][x].x - ss.lo - c0;
+                        ok = ok && d >= 0 && d <= 6 && c0 >= 0 && c0 < 0x10000;
+                        if (j) h |= (uint32_t)d << (12 + 4 * j);
+                        own |= (uint32_t)(x >= s.olo && x < s.ohi) << j;
+                        const uint32_t a = (uint32_t)xts[l][x].y;
+                        ok = ok && (a & 0xffffu) + (a >> 16) <= 2049;
+                        w.push_back(a);
+                    }
+                    rx[k].push_back(h | own << 28);
+                    rx[k].insert(rx[k].end(), w.begin(), w.end());
+                }
+            }
+        }
+        for (int k = 0; k < ex->pg.nby; k++) {
+            head(ry[k], spy, ex->pg.nby, k);
+            for (int l = 1; l < nlevels; l++) {
+                const PyrSpan& s = spy[(size_t)l * ex->pg.nby + k];
+                const PyrSpan& ss = spy[(size_t)(l - 1) * ex->pg.nby + k];
+                const int sh = g.h[l - 1];
+                for (int y = s.lo; y <= s.hi; y++) {
+                    const int r0 = std::min(std::max(yts[l][y].x, 0), sh - 1) - ss.lo;
+                    const int r1 = std::min(std::max(yts[l][y].x + 1, 0), sh - 1) - ss.lo;
+                    ok = ok && r0 >= 0 && r1 >= 0 && r0 < 0x8000 && r1 < 0x8000;
+                    const uint32_t b = (uint32_t)yts[l][y].y;
+                    ok = ok && (b & 0xffffu) + (b >> 16) <= 2049;
+                    ry[k].push_back((uint32_t)r0 | (uint32_t)r1 << 16 | (uint32_t)(y >= s.olo && y < s.ohi) << 31);
+                    ry[k].push_back(b);
+                }
+            }
+        }
+        if (!ok) {
+            free_extractor(ex);
+            delete ex;
+            return gf::fail(GF_ERR_UNSUPPORTED, "pyramid tables outside the k_pyramid record ranges");
+        }
+        ex->pg.rx = pack(rx, xrec);
+        ex->pg.ry = pack(ry, yrec);
         ex->pg.lds_img = (int)((ex->pyr_lds + 15) & ~(size_t)15);
-        ex->pyr_lds = ex->pg.lds_img + sizeof(int2) * (size_t)(ex->pg.rx + ex->pg.ry);
+        ex->pyr_lds = ex->pg.lds_img + sizeof(uint32_t) * (size_t)(ex->pg.rx + ex->pg.ry);
     }
-    ALLOC(ex->d_xtab, sizeof(int2) * std::max<size_t>(xrec.size(), 1));
-    ALLOC(ex->d_ytab, sizeof(int2) * std::max<size_t>(yrec.size(), 1));
+    ALLOC(ex->d_xtab, sizeof(uint32_t) * std::max<size_t>(xrec.size(), 1));
+    ALLOC(ex->d_ytab, sizeof(uint32_t) * std::max<size_t>(yrec.size(), 1));
 #undef ALLOC
     if (!xrec.empty()) {
-        GF_HIP(hipMemcpy(ex->d_xtab, xrec.data(), sizeof(int2) * xrec.size(), hipMemcpyHostToDevice));
-        GF_HIP(hipMemcpy(ex->d_ytab, yrec.data(), sizeof(int2) * yrec.size(), hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy(ex->d_xtab, xrec.data(), sizeof(uint32_t) * xrec.size(), hipMemcpyHostToDevice));
+        GF_HIP(hipMemcpy(ex->d_ytab, yrec.data(), sizeof(uint32_t) * yrec.size(), hipMemcpyHostToDevice));
         GF_HIP(hipFuncSetAttribute((const void*)k_pyramid<PYR_G>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)ex->pyr_lds));
         GF_HIP(hipFuncSetAttribute((const void*)k_pyramid<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
