@@ -83,7 +83,7 @@ __device__ __forceinline__ const uint8_t* level_plane(const Planes& P, const Lev
         stride = P.stride0;
         return P.ptrs ? P.ptrs[f] : P.img0 + (long long)f * P.fstride0;
     }
-    stride = g.w[l];
+    stride = g.pw[l];  // levels >= 1: rows pitched to 64 B like the blurred planes
     return P.pyr + (long long)f * g.slab + g.off[l];
 }
 
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
         const int dspan = dsx.hi - dsx.lo + 1, dp = pyr_pitch(dspan), nrow = dsy.hi - dsy.lo + 1;
         const int ng = (dspan + G - 1) / G, rstep = PYR_NT / ng;
         const int r00 = pyr_div(tid, 1.0f / (float)ng), gi = tid - r00 * ng;
-        const int dw = g.w[l];
+        const int dw = g.pw[l];
         const int x0 = dsx.lo + G * gi;
         uint8_t* D = P.pyr + (long long)f * g.slab + g.off[l] + x0;
         uint32_t sel[G], wgt[G], own = 0, cq = 0, csh = 0;
@@ -312,7 +312,9 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
             }
             if ((rr >> 31) && own) {
                 uint8_t* q = D + (dsy.lo + r) * dw;
-                if (own == (1u << G) - 1u) {
+                if (G == 4 && own == 0xfu) {  // column groups start at multiples of 4 (host plan): one dword
+                    *reinterpret_cast<uint32_t*>(q) = o;
+                } else if (own == (1u << G) - 1u) {
 #pragma unroll
                     for (int k = 0; k < G; k++) q[k] = (uint8_t)(o >> (8 * k));
                 } else {
@@ -505,8 +507,8 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         // BT_R rows x 18 dwords. Thread (lr, lq) = (tid / 18, tid % 18) owns
         // dword column lq of rows lr, lr + 14, ... (252 threads, 14 rows a
         // sweep), so its x range and LDS column are fixed. Rows reflect-101 at
-        // the top and bottom (a uniform test per tile); the level rows are
-        // unpadded, so the byte shift varies by row.
+        // the top and bottom (a uniform test per tile); in a level-0 image
+        // whose rows are not dword-aligned the byte shift varies by row.
         constexpr int NQD = BT_SW / 4, LR = 256 / NQD, NI = (BT_R + LR - 1) / LR;
         const int lr = tid / NQD, lq = tid - lr * NQD;
         const int x0 = X0 - 4 + 4 * lq;
@@ -524,20 +526,42 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 #pragma unroll
         for (int j = 0; j < 4; j++) pj[j] = gfd::reflect101(min(x0 + j, w + 2), w);
         const int pmin = min(min(pj[0], pj[1]), min(pj[2], pj[3]));
+        if (((uintptr_t)S & 3u) == 0 && (stride & 3) == 0) {
+            // dword-aligned rows (the pitched levels >= 1; level 0 when its
+            // rows are): the byte offsets, the selector and the second dword
+            // are the same in every row, only the row address changes
+            const int pb = pmin & ~3;
+            const int o0 = pj[0] - pb, o1 = pj[1] - pb, o2 = pj[2] - pb, o3 = pj[3] - pb;
+            const bool two = max(max(o0, o1), max(o2, o3)) >= 4;
+            const uint32_t sl = (uint32_t)o0 | (uint32_t)o1 << 8 | (uint32_t)o2 << 16 | (uint32_t)o3 << 24;
 #pragma unroll
-        for (int k = 0; k < NI; k++) {
-            const int ry = lr + LR * k;
-            lo[k] = hi[k] = sel[k] = 0u;
-            if (lr < LR && ry < BT_R) {
-                const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                const uintptr_t row = (uintptr_t)(S + (long long)yy * stride);
-                const uintptr_t base = (row + pmin) & ~(uintptr_t)3;
-                const int o0 = (int)(row + pj[0] - base), o1 = (int)(row + pj[1] - base);
-                const int o2 = (int)(row + pj[2] - base), o3 = (int)(row + pj[3] - base);
-                const bool two = max(max(o0, o1), max(o2, o3)) >= 4;
-                sel[k] = (uint32_t)o0 | (uint32_t)o1 << 8 | (uint32_t)o2 << 16 | (uint32_t)o3 << 24;
-                lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(base));
-                hi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(two ? base + 4 : base));
+            for (int k = 0; k < NI; k++) {
+                const int ry = lr + LR * k;
+                lo[k] = hi[k] = 0u;
+                sel[k] = sl;
+                if (lr < LR && ry < BT_R) {
+                    const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+                    const uint8_t* row = S + yy * stride + pb;
+                    lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(row));
+                    hi[k] = two ? gfd::ldg(reinterpret_cast<const uint32_t*>(row + 4)) : lo[k];
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NI; k++) {
+                const int ry = lr + LR * k;
+                lo[k] = hi[k] = sel[k] = 0u;
+                if (lr < LR && ry < BT_R) {
+                    const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+                    const uintptr_t row = (uintptr_t)(S + (long long)yy * stride);
+                    const uintptr_t base = (row + pmin) & ~(uintptr_t)3;
+                    const int o0 = (int)(row + pj[0] - base), o1 = (int)(row + pj[1] - base);
+                    const int o2 = (int)(row + pj[2] - base), o3 = (int)(row + pj[3] - base);
+                    const bool two = max(max(o0, o1), max(o2, o3)) >= 4;
+                    sel[k] = (uint32_t)o0 | (uint32_t)o1 << 8 | (uint32_t)o2 << 16 | (uint32_t)o3 << 24;
+                    lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(base));
+                    hi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(two ? base + 4 : base));
+                }
             }
         }
         uint32_t* s32 = reinterpret_cast<uint32_t*>(&src[0][0]) + lr * (BT_SP / 4) + lq;
@@ -1047,7 +1071,12 @@ struct SelWave {
 template <typename E>
 constexpr size_t sel_wave_bytes(int cap) { return (size_t)cap * (sizeof(E) + 2 * sizeof(uint16_t)); }
 template <typename E>
-constexpr size_t sel_lds() { return sel_wave_bytes<E>(SEL_BUF) + (SEL_THREADS / 64 - 1) * sel_wave_bytes<E>(SEL_BUF_CELL); }
+constexpr size_t sel_wave_lds() {
+    return sel_wave_bytes<E>(SEL_BUF) + (SEL_THREADS / 64 - 1) * sel_wave_bytes<E>(SEL_BUF_CELL);
+}
+// + the per-cell counts, quotas, offsets and flags of a level (maxnc cells at most)
+template <typename E>
+constexpr size_t sel_lds(int maxnc) { return sel_wave_lds<E>() + sizeof(int) * (3 * (size_t)maxnc + 1) + (size_t)maxnc; }
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1153,12 +1182,16 @@ template <typename E>
 __global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
                                                 E* __restrict__ lists, long long list_stride,
                                                 const int* __restrict__ counts, E* __restrict__ lvl_lists,
-                                                long long lvl_stride, int* __restrict__ lvl_counts) {
-    __shared__ int cnt[SEL_MAX_CELLS], keep[SEL_MAX_CELLS], off[SEL_MAX_CELLS + 1];
-    __shared__ char valid[SEL_MAX_CELLS];
+                                                long long lvl_stride, int* __restrict__ lvl_counts, int maxnc) {
     __shared__ int s_red[2];
     extern __shared__ __align__(16) uint8_t sel_dyn[];
-    const int l = blockIdx.x, f = blockIdx.y, wv = threadIdx.x >> 6;
+    // frames along x: the dispatch takes level 0 (the longest selections) of
+    // every frame first, the short levels fill in behind them
+    const int f = blockIdx.x, l = blockIdx.y, wv = threadIdx.x >> 6;
+    int* cnt = reinterpret_cast<int*>(sel_dyn + sel_wave_lds<E>());
+    int* keep = cnt + maxnc;
+    int* off = keep + maxnc;  // maxnc + 1
+    char* valid = reinterpret_cast<char*>(off + maxnc + 1);
     SelWave<E> W;
     {
         const int cap = wv == 0 ? SEL_BUF : SEL_BUF_CELL;
@@ -1507,6 +1540,7 @@ struct gf_extractor {
     uint32_t *d_xtab = nullptr, *d_ytab = nullptr;  // k_pyramid's block-column / block-row records
     PyrGeom pg{};
     size_t pyr_lds = 0;
+    int sel_maxnc = 0;  // most cells of a level (k_select's per-cell arrays)
     int pyr_g = PYR_G;  // k_pyramid's columns per item (1 when a 4-column group's taps span more than 7 bytes)
     CellInfo* d_cells = nullptr;
     void *d_lists = nullptr, *d_lvl = nullptr;  // uint32_t (FAST) or uint64_t (Harris) entries
@@ -1565,7 +1599,7 @@ static int plan_extractor(gf_extractor* ex) {
                  "level size out of supported range");
         if (l > 0) {
             g.off[l] = off;
-            off += ((long long)g.w[l] * g.h[l] + 255) & ~255LL;
+            off += ((long long)g.pw[l] * g.h[l] + 255) & ~255LL;
         }
         g.boff[l] = boff;
         boff += ((long long)g.pw[l] * g.h[l] + 255) & ~255LL;
@@ -1584,6 +1618,7 @@ static int plan_extractor(gf_extractor* ex) {
 
     // ComputeKeyPoints cell grids (:540-618).
     ex->cells.clear();
+    ex->sel_maxnc = 0;
     ex->band_cells.clear();
     ex->band_lds = 0;
     long long cap_off = 0, lvl_off = 0;
@@ -1600,6 +1635,7 @@ static int plan_extractor(gf_extractor* ex) {
         const int cellH = (int)std::ceil((float)H / levelRows);
         const int nCells = levelRows * levelCols;
         GF_CHECK(nCells <= SEL_MAX_CELLS, GF_ERR_UNSUPPORTED, "too many cells per level");
+        ex->sel_maxnc = std::max(ex->sel_maxnc, nCells);
         g.nfcell[l] = (int)std::ceil((float)nDesired / nCells);
         g.ndesired[l] = nDesired;
         g.cell_begin[l] = (int)ex->cells.size();
@@ -1727,10 +1763,16 @@ static void pyr_axis(const LevelGeom& g, const std::vector<std::vector<int2>>& t
             }
             PyrSpan s{};
             if (l >= 1) {
-                const int olo = (int)((long long)k * n / nb), ohi = (int)((long long)(k + 1) * n / nb);
+                // columns: block boundaries and required spans start at multiples
+                // of 4, so k_pyramid's 4-column groups store aligned dwords
+                const int al = is_x ? 4 : 1;
+                auto bound = [&](int kk) {
+                    return kk >= nb ? n : (int)((long long)kk * n / nb) / al * al;
+                };
+                const int olo = bound(k), ohi = bound(k + 1);
                 s.olo = (int16_t)olo;
                 s.ohi = (int16_t)ohi;
-                lo = l < nl - 1 ? std::min(rlo, olo) : olo;
+                lo = (l < nl - 1 ? std::min(rlo, olo) : olo) / al * al;
                 hi = l < nl - 1 ? std::max(rhi, ohi - 1) : ohi - 1;
                 maxspan = std::max(maxspan, hi - lo + 1);
             } else {
@@ -1935,8 +1977,9 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
                     std::vector<uint32_t> w;
                     for (int j = 0; j < G; j++) {
                         const int x = x0 + j;
-                        if (x > s.hi) {
-                            w.push_back(0u);
+                        if (x > s.hi) {  // past the span: weight 0; past the level's last column the
+                            w.push_back(0u);  // byte lands in the row padding, stored with its group
+                            own |= (uint32_t)(x >= g.w[l] && s.ohi == g.w[l]) << j;
                             continue;
                         }
                         const int d = xts[l][x].x - ss.lo - c0;
@@ -1996,14 +2039,14 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
                          hipMemcpyHostToDevice));
     if (ex->harris) {
         GF_HIP(hipFuncSetAttribute((const void*)k_select<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)sel_lds<uint64_t>()));
+                                   (int)sel_lds<uint64_t>(ex->sel_maxnc)));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)ex->fast_lds));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint64_t>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex->band_lds));
     } else {
         GF_HIP(hipFuncSetAttribute((const void*)k_select<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)sel_lds<uint32_t>()));
+                                   (int)sel_lds<uint32_t>(ex->sel_maxnc)));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)ex->fast_lds));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint32_t>,
@@ -2106,8 +2149,8 @@ static int select_describe(gf_extractor* ex, int nframes, Planes P, gf_keypoint*
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
-        GF_LAUNCH(k_select<E>, dim3(ex->nlevels, nframes), SEL_THREADS, sel_lds<E>(), s, g, ex->d_cells, lists,
-                  ex->list_stride, ex->d_counts, lvl, ex->lvl_stride, ex->d_lvl_counts);
+        GF_LAUNCH(k_select<E>, dim3(nframes, ex->nlevels), SEL_THREADS, sel_lds<E>(ex->sel_maxnc), s, g, ex->d_cells,
+                  lists, ex->list_stride, ex->d_counts, lvl, ex->lvl_stride, ex->d_lvl_counts, ex->sel_maxnc);
     }
     if (ex->stage_ev && ex->stage_after == 3) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
@@ -2178,8 +2221,8 @@ int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, 
         GF_HIP(hipMemcpy2D(out, g.w[0], ex->last.img0 + (long long)frame * ex->last.fstride0, ex->last.stride0, g.w[0],
                            g.h[0], hipMemcpyDeviceToHost));
     } else {
-        GF_HIP(hipMemcpy(out, ex->d_pyr + (long long)frame * g.slab + g.off[level], (size_t)g.w[level] * g.h[level],
-                         hipMemcpyDeviceToHost));
+        GF_HIP(hipMemcpy2D(out, g.w[level], ex->d_pyr + (long long)frame * g.slab + g.off[level], g.pw[level],
+                           g.w[level], g.h[level], hipMemcpyDeviceToHost));
     }
     return GF_OK;
 }
