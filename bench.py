@@ -906,7 +906,8 @@ def main():
     rp = {k: (sum(v) / 1e6, len(v)) for k, v in ktab.items()} if ktab else None
     SCOPE = {"k_active_match": ["k_active_match", "k_active_match_overflow"],
              "k_match_lastframe": ["k_match_seq", "k_match_seq_pre"], "k_match_project": ["k_match"],
-             "k_pose_opt": ["k_pose_opt_frames"]}
+             "k_pose_opt": ["k_pose_opt_frames"], "k_select": ["k_select_cells", "k_select_level"],
+             "k_fast_cells": ["k_fast_cells", "k_fast_cells_band"]}
 
     def rp_total(k):
         return sum(rp[n][0] for n in SCOPE.get(k, [k]) if n in rp) if rp else 0.0
@@ -989,8 +990,8 @@ def main():
     if top not in SCOPE.get(dom, [dom]):
         roof["largest_kernel"] = {"kernel": top, "avg_launch_ms": round(tab[top][0] / tab[top][1], 4)}
     roof["other_kernels"] = {k: v for k, v in priced.items() if k != dom}
-    ext_ms = sum(tab[k][0] for k in ("k_pyramid", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
-                 if k in tab)
+    ext_ms = sum(tab[n][0] for k in ("k_pyramid", "k_blur_fast", "k_fast_cells", "k_select", "k_describe")
+                 for n in (SCOPE.get(k, [k]) if rp else [k]) if n in tab)
     ext_bw = kb["extract_total"] * B * args.steps / (ext_ms / 1e3) / 1e9 if ext_ms else None
     gf_kernels = [k for k in tab if k.startswith(("k_obs", "k_onepoint", "k_active"))]
     gf_ms = sum(tab[k][0] for k in gf_kernels)

@@ -1178,142 +1178,138 @@ __device__ __forceinline__ void wave_retain_to(const SelWave<E>& W, E* list, int
     for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
 }
 
-template <typename E>
-__global__ __launch_bounds__(SEL_THREADS) void k_select(LevelGeom g, const CellInfo* __restrict__ cells,
-                                                E* __restrict__ lists, long long list_stride,
-                                                const int* __restrict__ counts, E* __restrict__ lvl_lists,
-                                                long long lvl_stride, int* __restrict__ lvl_counts, int maxnc) {
-    __shared__ int s_red[2];
-    extern __shared__ __align__(16) uint8_t sel_dyn[];
-    // frames along x: the dispatch takes level 0 (the longest selections) of
-    // every frame first, the short levels fill in behind them
-    const int f = blockIdx.x, l = blockIdx.y, wv = threadIdx.x >> 6;
-    int* cnt = reinterpret_cast<int*>(sel_dyn + sel_wave_lds<E>());
-    int* keep = cnt + maxnc;
-    int* off = keep + maxnc;  // maxnc + 1
-    char* valid = reinterpret_cast<char*>(off + maxnc + 1);
-    SelWave<E> W;
-    {
-        const int cap = wv == 0 ? SEL_BUF : SEL_BUF_CELL;
-        uint8_t* base =
-            sel_dyn + (wv == 0 ? 0 : sel_wave_bytes<E>(SEL_BUF) + (wv - 1) * sel_wave_bytes<E>(SEL_BUF_CELL));
-        W.a = reinterpret_cast<E*>(base);
-        W.lp = reinterpret_cast<uint16_t*>(W.a + cap);
-        W.rp = W.lp + cap;
-        W.cap = cap;
-    }
-    const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb;
-    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
-        cnt[c] = counts[(long long)f * g.ncells + cb + c];
-        valid[c] = (char)cells[cb + c].valid;
-    }
-    __syncthreads();
-    // Quota redistribution, ORBextractor.cc:673-721, by the whole workgroup:
-    // each round is a per-cell map with integer sums (order-free), so the
-    // rounds give the sequential loop's keep[] exactly. Cells skipped by the
-    // ROI loop (valid == 0) keep nTotal = 0, nToRetain = 0, bNoMore = false.
-    // off[c] is the noMore flag until the final prefix sum.
-    {
-        const int nf = g.nfcell[l];
-        if (threadIdx.x == 0) {
-            s_red[0] = 0;  // nToDistribute
-            s_red[1] = 0;  // nNoMore
+// Quota redistribution of one level (ORBextractor.cc:673-721) by one wave:
+// each round is a per-cell map with integer sums (order-free), so the rounds
+// give the sequential loop's nToRetain exactly. Cells skipped by the ROI loop
+// (valid == 0) keep nTotal = 0, nToRetain = 0, bNoMore = false. Leaves keep[c]
+// and off[c] = exclusive prefix of the kept counts (off[nc] = the level's
+// total) in the wave's LDS arrays; cnt[c] = the cell's corner count.
+__device__ void wave_quota(const int* __restrict__ counts, const CellInfo* __restrict__ cells, int nc, int nf,
+                           int* cnt, int* keep, int* off, uint8_t* flag) {
+    const int lane = threadIdx.x & 63;
+    int dist = 0, nomore = 0;
+    for (int c = lane; c < nc; c += 64) {
+        const int n = counts[c];
+        const bool v = cells[c].valid != 0;
+        cnt[c] = v ? n : 0;
+        int k = 0, fl = 0;
+        if (!v) {
+            k = -1;  // not a cell of the ROI loop: no quota, no list
+        } else if (n > nf) {
+            k = nf;
+        } else {
+            k = n;
+            dist += nf - n;
+            fl = 1;
+            nomore++;
         }
-        __syncthreads();
-        int dist = 0, nomore = 0;
-        for (int c = threadIdx.x; c < nc; c += SEL_THREADS) {
-            off[c] = 0;
-            if (!valid[c]) {
-                keep[c] = 0;
-            } else if (cnt[c] > nf) {
-                keep[c] = nf;
+        keep[c] = k;
+        flag[c] = (uint8_t)fl;
+    }
+    int nToDistribute = gfd::warp_sum(dist), nNoMore = gfd::warp_sum(nomore);
+    while (nToDistribute > 0 && nNoMore < nc) {
+        const int nNew = nf + (int)ceilf((float)nToDistribute / (float)(nc - nNoMore));
+        dist = 0;
+        nomore = 0;
+        for (int c = lane; c < nc; c += 64) {
+            if (flag[c]) continue;  // (skipped cells take part: nTotal 0, bNoMore false)
+            const int n = cnt[c];
+            if (n > nNew) {
+                if (keep[c] >= 0) keep[c] = nNew;
             } else {
-                keep[c] = cnt[c];
-                dist += nf - cnt[c];
-                off[c] = 1;
+                if (keep[c] >= 0) keep[c] = n;
+                dist += nNew - n;
+                flag[c] = 1;
                 nomore++;
             }
         }
-        if (dist) atomicAdd(&s_red[0], dist);
-        if (nomore) atomicAdd(&s_red[1], nomore);
-        __syncthreads();
-        int nToDistribute = s_red[0], nNoMore = s_red[1];
-        while (nToDistribute > 0 && nNoMore < nc) {  // uniform: every thread read the same sums
-            const int nNew = nf + (int)ceilf((float)nToDistribute / (float)(nc - nNoMore));
-            __syncthreads();  // all have read s_red
-            if (threadIdx.x == 0) s_red[0] = 0;
-            __syncthreads();
-            dist = 0;
-            nomore = 0;
-            for (int c = threadIdx.x; c < nc; c += SEL_THREADS) {
-                if (off[c]) continue;  // (skipped cells take part: nTotal 0, bNoMore false)
-                if (cnt[c] > nNew) {
-                    keep[c] = nNew;
-                } else {
-                    keep[c] = cnt[c];
-                    dist += nNew - cnt[c];
-                    off[c] = 1;
-                    nomore++;
-                }
-            }
-            if (dist) atomicAdd(&s_red[0], dist);
-            if (nomore) atomicAdd(&s_red[1], nomore);
-            __syncthreads();
-            nToDistribute = s_red[0];
-            nNoMore = s_red[1];
-        }
-        // keep[c] <= cnt[c], so retainBest leaves exactly keep[c] per cell
-        // (:734-736); off = exclusive prefix of the kept counts
-        __syncthreads();
-        if (wv == 0) {
-            const int lane = threadIdx.x & 63;
-            int base = 0;
-            for (int c0 = 0; c0 < nc; c0 += 64) {
-                const int c = c0 + lane;
-                const int v = c < nc && valid[c] ? keep[c] : 0;
-                int x = v;
+        nToDistribute = gfd::warp_sum(dist);
+        nNoMore += gfd::warp_sum(nomore);
+    }
+    // keep[c] <= cnt[c], so retainBest leaves exactly keep[c] per cell (:734-736)
+    int base = 0;
+    for (int c0 = 0; c0 < nc; c0 += 64) {
+        const int c = c0 + lane;
+        const int v = c < nc && keep[c] > 0 ? keep[c] : 0;
+        int x = v;
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) {
-                    const int y = __shfl_up(x, o, 64);
-                    if (lane >= o) x += y;
-                }
-                if (c < nc) off[c] = base + x - v;
-                base += __shfl(x, 63, 64);
-            }
-            if (lane == 0) off[nc] = base;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
+        if (c < nc) off[c] = base + x - v;
+        base += __shfl(x, 63, 64);
     }
-    __syncthreads();
+    if (lane == 0) off[nc] = base;
+    wave_sync();
+}
+
+// retainBest per cell: one wave per (cell, frame), every cell of every level
+// at once (cells of a level no longer queue behind one workgroup's waves).
+// The wave redoes its level's quota (a few integer rounds over the level's
+// cells) and writes its cell's kept entries at the cell's offset in the level
+// list. The level's first cell also records the level total for k_select_level.
+#define SEL_CW 4  // cell waves per workgroup
+template <typename E>
+constexpr size_t sel_cell_wave_lds(int maxnc) {
+    return sel_wave_bytes<E>(SEL_BUF) + sizeof(int) * (3 * (size_t)maxnc + 1) + (((size_t)maxnc + 15) & ~(size_t)15);
+}
+
+template <typename E>
+__global__ __launch_bounds__(64 * SEL_CW) void k_select_cells(LevelGeom g, const CellInfo* __restrict__ cells,
+                                                              E* __restrict__ lists, long long list_stride,
+                                                              const int* __restrict__ counts,
+                                                              E* __restrict__ lvl_lists, long long lvl_stride,
+                                                              int* __restrict__ lvl_counts, int maxnc) {
+    extern __shared__ __align__(16) uint8_t sel_dyn[];
+    const int f = blockIdx.y, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int c = blockIdx.x * SEL_CW + wv;  // cell (all levels, level-major)
+    if (c >= g.ncells) return;               // whole wave
+    uint8_t* base = sel_dyn + (size_t)wv * sel_cell_wave_lds<E>(maxnc);
+    SelWave<E> W;
+    W.a = reinterpret_cast<E*>(base);
+    W.lp = reinterpret_cast<uint16_t*>(W.a + SEL_BUF);
+    W.rp = W.lp + SEL_BUF;
+    W.cap = SEL_BUF;
+    int* cnt = reinterpret_cast<int*>(base + sel_wave_bytes<E>(SEL_BUF));
+    int* keep = cnt + maxnc;
+    int* off = keep + maxnc;  // maxnc + 1
+    uint8_t* flag = reinterpret_cast<uint8_t*>(off + maxnc + 1);
+    const int l = cells[c].level;
+    const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb, ci = c - cb;
+    wave_quota(counts + (long long)f * g.ncells + cb, cells + cb, nc, g.nfcell[l], cnt, keep, off, flag);
     E* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
-    // a cell list longer than a cell wave's buffer that needs a selection
-    // waits for wave 0's (larger) buffer, after wave 0's own cells
-    auto deferred = [&](int c) { return SEL_BUF_CELL < SEL_BUF && cnt[c] > keep[c] && cnt[c] > SEL_BUF_CELL; };
-    for (int c = wv; c < nc; c += SEL_THREADS / 64) {
-        if (!valid[c] || (wv != 0 && deferred(c))) continue;
-        E* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
-        wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
+    if (ci == 0 && lane == 0) lvl_counts[(long long)f * g.nlevels + l] = off[nc];
+    if (keep[ci] > 0) {
+        E* a = lists + (long long)f * list_stride + cells[c].cap_off;
+        wave_retain_to(W, a, cnt[ci], keep[ci], L + off[ci]);
     }
-    if (wv == 0 && SEL_BUF_CELL < SEL_BUF) {
-        for (int c = 0; c < nc; c++) {
-            if (c % (SEL_THREADS / 64) == 0 || !valid[c] || !deferred(c)) continue;
-            E* a = lists + (long long)f * list_stride + cells[cb + c].cap_off;
-            wave_retain_to(W, a, cnt[c], keep[c], L + off[c]);
-        }
+}
+
+// The level's retainBest (:750-752) on the concatenated cell lists: one wave
+// per (frame, level); total from k_select_cells, the cut count back in place.
+template <typename E>
+__global__ __launch_bounds__(64) void k_select_level(LevelGeom g, E* __restrict__ lvl_lists, long long lvl_stride,
+                                                     int* __restrict__ lvl_counts) {
+    extern __shared__ __align__(16) uint8_t sel_dyn[];
+    const int f = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+    SelWave<E> W;
+    W.a = reinterpret_cast<E*>(sel_dyn);
+    W.lp = reinterpret_cast<uint16_t*>(W.a + SEL_BUF);
+    W.rp = W.lp + SEL_BUF;
+    W.cap = SEL_BUF;
+    E* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
+    int* out = lvl_counts + (long long)f * g.nlevels + l;
+    const int total = *out, nd = g.ndesired[l];
+    if (nd >= 0 && total > nd && nd > 0 && total <= SEL_BUF) {
+        for (int i = lane; i < total; i += 64) W.a[i] = L[i];
+        wave_sync();
+        wave_nth_element(W, nd - 1, total);
+        for (int i = lane; i < nd; i += 64) L[i] = W.a[i];
+    } else if (lane == 0) {
+        gfsel::retain_best_truncate(L, total, nd, EntGreater<E>());
     }
-    __syncthreads();
-    if (wv == 0) {  // the level's retainBest (:750-752)
-        const int total = off[nc], nd = g.ndesired[l];
-        if (nd >= 0 && total > nd && nd > 0 && total <= SEL_BUF) {
-            for (int i = threadIdx.x; i < total; i += 64) W.a[i] = L[i];
-            wave_sync();
-            wave_nth_element(W, nd - 1, total);
-            for (int i = threadIdx.x; i < nd; i += 64) L[i] = W.a[i];
-        } else if (threadIdx.x == 0) {
-            gfsel::retain_best_truncate(L, total, nd, EntGreater<E>());
-        }
-        if (threadIdx.x == 0)
-            lvl_counts[(long long)f * g.nlevels + l] = (nd < 0 || total <= nd) ? total : nd;
-    }
+    if (lane == 0) *out = (nd < 0 || total <= nd) ? total : nd;
 }
 
 // -------------------------------------------------------------- k_describe
@@ -2038,15 +2034,15 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
         GF_HIP(hipMemcpy(ex->d_band, ex->band_cells.data(), sizeof(int) * ex->band_cells.size(),
                          hipMemcpyHostToDevice));
     if (ex->harris) {
-        GF_HIP(hipFuncSetAttribute((const void*)k_select<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)sel_lds<uint64_t>(ex->sel_maxnc)));
+        GF_HIP(hipFuncSetAttribute((const void*)k_select_cells<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(SEL_CW * sel_cell_wave_lds<uint64_t>(ex->sel_maxnc))));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint64_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)ex->fast_lds));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint64_t>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)ex->band_lds));
     } else {
-        GF_HIP(hipFuncSetAttribute((const void*)k_select<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)sel_lds<uint32_t>(ex->sel_maxnc)));
+        GF_HIP(hipFuncSetAttribute((const void*)k_select_cells<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(SEL_CW * sel_cell_wave_lds<uint32_t>(ex->sel_maxnc))));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells<uint32_t>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)ex->fast_lds));
         GF_HIP(hipFuncSetAttribute((const void*)k_fast_cells_band<uint32_t>,
@@ -2149,8 +2145,11 @@ static int select_describe(gf_extractor* ex, int nframes, Planes P, gf_keypoint*
     if (ex->stage_ev && ex->stage_after == 2) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_select");
-        GF_LAUNCH(k_select<E>, dim3(nframes, ex->nlevels), SEL_THREADS, sel_lds<E>(ex->sel_maxnc), s, g, ex->d_cells,
-                  lists, ex->list_stride, ex->d_counts, lvl, ex->lvl_stride, ex->d_lvl_counts, ex->sel_maxnc);
+        GF_LAUNCH(k_select_cells<E>, dim3((g.ncells + SEL_CW - 1) / SEL_CW, nframes), 64 * SEL_CW,
+                  SEL_CW * sel_cell_wave_lds<E>(ex->sel_maxnc), s, g, ex->d_cells, lists, ex->list_stride,
+                  ex->d_counts, lvl, ex->lvl_stride, ex->d_lvl_counts, ex->sel_maxnc);
+        GF_LAUNCH(k_select_level<E>, dim3(nframes, ex->nlevels), 64, sel_wave_bytes<E>(SEL_BUF), s, g, lvl,
+                  ex->lvl_stride, ex->d_lvl_counts);
     }
     if (ex->stage_ev && ex->stage_after == 3) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
@@ -2197,6 +2196,17 @@ int gf_orb_extract(gf_extractor* ex, const uint8_t* img, int stride, gf_keypoint
     }
     return GF_OK;
 }
+
+#ifdef GF_SEL_STAMP
+int gf_debug_sel_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sel_stamp), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sel_stamp), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 int gf_extractor_debug_level(gf_extractor* ex, int frame, int level, int which, uint8_t* out, int* w, int* h) {
     GF_CHECK(ex && w && h, GF_ERR_ARG, "null arg");

@@ -17,7 +17,7 @@ for v in ${VARS//,/ }; do
 import json, sys
 d = json.load(open(sys.argv[1]))
 k = d.get("kernels", {})
-pick = {n: k[n]["avg_ms"] for n in ("k_pyramid", "k_active_match", "k_blur_fast", "k_pose_opt_frames", "k_match_seq", "k_update_reference", "k_onepoint_pre", "k_select", "k_fast_cells", "k_describe") if n in k}
+pick = {n: k[n]["avg_ms"] for n in ("k_pyramid", "k_active_match", "k_blur_fast", "k_pose_opt_frames", "k_match_seq", "k_update_reference", "k_onepoint_pre", "k_select", "k_select_cells", "k_select_level", "k_fast_cells", "k_describe") if n in k}
 print(sys.argv[2], "fps", d["value"], "single", d.get("single_stream", {}).get("ms_per_frame"), pick)
 PY
 done
