@@ -712,10 +712,6 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 // pixel); survivors set their bit in an LDS bit array (bit = row-major pixel
 // index). Listing: a workgroup scan over the popcounts of the bit words.
 // (Cell windows are at most ~40 px wide, so one strip.)
-__device__ __forceinline__ int nms_at(int m, int th) {  // map entry -> FAST buffer value at th
-    const int S = m - 1;  // entries are S + 1 for corners at the map threshold, 0 otherwise
-    return S >= th ? S : 0;
-}
 
 // sc: the window rows as loaded (row y at byte y * pitch + rsh[y]). Every LDS
 // read is unconditional (addresses clamped into the window, out-of-window
@@ -745,36 +741,49 @@ __device__ __forceinline__ int cell_nms_bits(const uint8_t* sc, const uint8_t* r
         const bool okc = x < dw;
         // lane masks (all ones inside the window) instead of conditions, so
         // no read is predicated away behind a branch
-        const int ml = -(int)(x >= 1 && x - 1 < dw), mc = -(int)okc, mr = -(int)(x + 1 < dw);
         const int cl = min(max(x - 1, 0), dw - 1), cc = min(x, dw - 1), cr = min(x + 1, dw - 1);
-        auto row3 = [&](int b, int& v0, int& v1, int& v2) {
-            const uint8_t* r = sc + b;
-            const int r0 = r[cl], r1 = r[cc], r2 = r[cr];
-            v0 = nms_at(r0, th) & ml;
-            v1 = nms_at(r1, th) & mc;
-            v2 = nms_at(r2, th) & mr;
+        // The FAST buffer value at th is S = m - 1 where S >= th, else 0 (m: the
+        // map entry S + 1, nonzero only for corners at the map's threshold).
+        // Comparisons between such values are comparisons of m on the entries
+        // with m > max(th, 1) (m = 1 at th = 0 is a score-0 corner: 0), so each
+        // read is one compare against a per-lane bound (255 past the window's
+        // edge: every entry reads 0 there, as FAST's row buffers do).
+        const int t1 = max(th, 1);
+        const int tl = (x >= 1 && x - 1 < dw) ? t1 : 255, tc = okc ? t1 : 255, tr = (x + 1 < dw) ? t1 : 255;
+        struct R3 {
+            int a, b, c;
         };
-        int u0, u1, u2, c0, c1, c2, d0, d1, d2;
+        auto row3 = [&](int b) -> R3 {
+            const uint8_t* r = sc + b;
+            const int va = r[cl], vb = r[cc], vc = r[cr];
+            return R3{va > tl ? va : 0, vb > tc ? vb : 0, vc > tr ? vc : 0};
+        };
+        R3 q[4];
         {
             const int i0 = rowi(ya - 1), i1 = rowi(ya), i2 = rowi(ya + 1);
-            row3(i0 * pitch + rsh[i0], u0, u1, u2);
-            row3(i1 * pitch + rsh[i1], c0, c1, c2);
-            row3(i2 * pitch + rsh[i2], d0, d1, d2);
+            q[0] = row3(i0 * pitch + rsh[i0]);
+            q[1] = row3(i1 * pitch + rsh[i1]);
+            q[2] = row3(i2 * pitch + rsh[i2]);
         }
         int ie = rowi(ya + 2), se = rsh[ie];
-        for (int y = ya; y < yb; y++) {
-            int e0, e1, e2;
-            row3(ie * pitch + se, e0, e1, e2);  // row y + 2, read one step ahead
-            const int in = rowi(y + 3), sn = rsh[in];  // its shift is used next step
-            const int mx = max(max(max(u0, u1), max(u2, c0)), max(max(c2, d0), max(d1, d2)));
-            const bool keep = okc && c1 != 0 && c1 > mx;
+        // rows y - 1, y, y + 1 in q[k], q[k + 1], q[k + 2] (mod 4); row y + 2 is
+        // read into q[k + 3] one step ahead. Unrolled by four so the roles
+        // rotate by register naming, with no moves.
+        auto step = [&](int y, R3& u, R3& c, R3& d, R3& e) {
+            e = row3(ie * pitch + se);
+            const int in = rowi(y + 3);
+            se = rsh[in];
+            ie = in;
+            const int mx = max(max(max(u.a, u.b), max(u.c, c.a)), max(max(c.c, d.a), max(d.b, d.c)));
+            const bool keep = okc && c.b != 0 && c.b > mx;
             if (keep) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
             cnt += __popcll(__ballot(keep));
-            u0 = c0, u1 = c1, u2 = c2;
-            c0 = d0, c1 = d1, c2 = d2;
-            d0 = e0, d1 = e1, d2 = e2;
-            ie = in;
-            se = sn;
+        };
+        for (int y = ya; y < yb; y += 4) {
+            step(y, q[0], q[1], q[2], q[3]);
+            if (y + 1 < yb) step(y + 1, q[1], q[2], q[3], q[0]);
+            if (y + 2 < yb) step(y + 2, q[2], q[3], q[0], q[1]);
+            if (y + 3 < yb) step(y + 3, q[3], q[0], q[1], q[2]);
         }
     }
     return cnt;  // this wave's survivors
