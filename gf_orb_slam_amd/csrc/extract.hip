@@ -41,7 +41,10 @@
 namespace {
 
 __constant__ uint32_t c_pattern8[256];  // test i: (x0, y0, x1, y1) of its two points as int8
-__constant__ int c_umax[16];
+// IC_Angle row weights by |v| (k_describe): [16][8] dwords of bytes u + 15 for
+// |u| <= umax[|v|] (else 0), then [16][8] dwords of the 0/1 patch mask (column
+// c = 4 j + b is u = c - 15; column 31 weighs 0)
+__constant__ uint32_t c_ic_tab[256];
 
 struct LevelGeom {
     int nlevels;
@@ -1384,9 +1387,9 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
     // the rBRIEF pattern, one dword per test, bit-major (test 8 i + bit at
     // bit * 32 + i): the 32 lanes of a half read 32 consecutive dwords
     __shared__ uint32_t sh_pat[256];
-    __shared__ int sh_umax[16];  // IC_Angle's umax (a lane-indexed read)
+    __shared__ uint32_t sh_ictab[256];  // IC_Angle's row weights and masks (c_ic_tab)
     sh_pat[(threadIdx.x & 7) * 32 + (threadIdx.x >> 3)] = c_pattern8[threadIdx.x];
-    if (threadIdx.x < 16) sh_umax[threadIdx.x] = c_umax[threadIdx.x];
+    sh_ictab[threadIdx.x] = c_ic_tab[threadIdx.x];
     __syncthreads();
     int bx, f;
     gfd::xcd_block(bx, f);
@@ -1445,23 +1448,27 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    const uint8_t* ic8 = reinterpret_cast<const uint8_t*>(W.ic);
     const uint8_t* bl8 = reinterpret_cast<const uint8_t*>(W.bl);
 
     // IC_Angle: 31 pixels of the 31x31 square per lane (row hl); pixels outside
     // the circular patch (|u| > umax[|v|]) weigh 0. Integer moments: order-free.
+    // The row's 31 bytes realigned to 8 dwords; sum p and sum (u + 15) p over
+    // the patch as v_dot4_u32_u8 against the row's weight dwords (exact), then
+    // m10 = sum (u + 15) p - 15 sum p.
     int m10 = 0, m01 = 0;
     if (hl < 31) {
-        const int v = hl - 15, d = sh_umax[v < 0 ? -v : v];
-        const uint8_t* row = ic8 + hl * (4 * DS_ICW) + W.ic_sh[hl] + 15;
-        int sum = 0;
+        const int v = hl - 15, av = v < 0 ? -v : v;
+        const uint32_t* row = W.ic + hl * DS_ICW;
+        const uint32_t sh = W.ic_sh[hl];
+        uint32_t s1 = 0, s0 = 0;
 #pragma unroll
-        for (int u = -15; u <= 15; u++) {
-            const int p = (u >= -d && u <= d) ? row[u] : 0;
-            sum += p;
-            m10 += u * p;
+        for (int j = 0; j < 8; j++) {
+            const uint32_t px = __builtin_amdgcn_alignbyte(row[j + 1], row[j], sh);
+            s1 = __builtin_amdgcn_udot4(px, sh_ictab[av * 8 + j], s1, false);
+            s0 = __builtin_amdgcn_udot4(px, sh_ictab[128 + av * 8 + j], s0, false);
         }
-        m01 = v * sum;
+        m10 = (int)s1 - 15 * (int)s0;
+        m01 = v * (int)s0;
     }
     m10 = half_sum(m10);
     m01 = half_sum(m01);
@@ -1871,7 +1878,17 @@ static int upload_constants(int device) {
         umax[v] = v0;
         ++v0;
     }
-    GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax)));
+    {
+        uint32_t tab[256] = {};
+        for (int av = 0; av < 16; av++)
+            for (int c = 0; c < 31; c++) {
+                const int u = c - 15;
+                if (u < -umax[av] || u > umax[av]) continue;
+                tab[av * 8 + c / 4] |= (uint32_t)(u + 15) << (8 * (c % 4));
+                tab[128 + av * 8 + c / 4] |= 1u << (8 * (c % 4));
+            }
+        GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ic_tab), tab, sizeof(tab)));
+    }
     done_mask |= 1ull << device;
     return GF_OK;
 }
