@@ -494,6 +494,8 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
     __shared__ uint32_t nmsb[BT_H][BT_W / 32];  // interior NMS survivors, bit x of row y
     __shared__ int scan_tmp[4];
+    __shared__ int s_ncor;  // tile-interior corners listed for the NMS
+    if (threadIdx.x == 0) s_ncor = 0;  // (ordered by the scan's barriers)
     static_assert(BT_W == 64 && 2 * BT_H <= 256, "k_blur_fast: two NMS words per tile row, one thread each");
     if (threadIdx.x < 2 * BT_H) (&nmsb[0][0])[threadIdx.x] = 0u;  // ordered by the scan's barriers
     uint32_t(*rows2)[BT_W] = reinterpret_cast<uint32_t(*)[BT_W]>(u32buf);
@@ -684,6 +686,12 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     }
     __syncthreads();
     uint8_t* sc8 = reinterpret_cast<uint8_t*>(&sco[0][0]);
+    // corners for the NMS: the candidate list fills u32buf from the bottom, the
+    // corners (a subset) go from the top down, so they meet only when the
+    // candidates take more than half of it; then the NMS walks the candidates
+    const int t1 = max(map_th, 1);
+    const bool clist_on = 2 * nc <= (int)sizeof(u32buf) / 2;
+    uint16_t* clist = reinterpret_cast<uint16_t*>(u32buf) + (sizeof(u32buf) / 2 - 1);
 #if defined(GF_BLUR_EXP) && GF_BLUR_EXP == 1
     for (int i = tid; i < 0; i += 256) {
 #else
@@ -694,6 +702,14 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         circle_vals(&src[0][0], BT_SP, px + 4, py + 3, c);
         const int M = fast_max_arc(src[py + 3][px + 4], c);  // corner iff M > th; map entry S + 1 = M
         sc8[q] = M > map_th ? (uint8_t)M : 0;
+        if (clist_on) {  // the tile-interior corners the NMS below visits, appended from the top of u32buf
+            const bool cor = M > t1 && px >= 1 && px <= BT_W - 2 && py >= 1 && py <= BT_H - 2;
+            const unsigned long long b = __ballot(cor);
+            int base = 0;
+            if ((tid & 63) == 0 && b) base = atomicAdd(&s_ncor, __popcll(b));
+            base = __shfl(base, 0, 64);
+            if (cor) clist[-(base + __popcll(b & ((1ull << (tid & 63)) - 1ull)))] = (uint16_t)q;
+        }
     }
     __syncthreads();
     // 3x3 NMS of the tile's interior corners (pixels 1 .. 62 of the tile in x
@@ -703,9 +719,9 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     // pixels whose neighbours all lie in the window and in one tile, and
     // evaluates the rest itself.
     {
-        const int t1 = max(map_th, 1);
-        for (int i = tid; i < nc; i += 256) {
-            const int q = cand[i], py = q >> 6, px = q & 63;
+        const int ncor = clist_on ? s_ncor : nc;
+        for (int i = tid; i < ncor; i += 256) {
+            const int q = clist_on ? clist[-i] : cand[i], py = q >> 6, px = q & 63;
             const int m = sc8[q];
             if (m > t1 && px >= 1 && px <= BT_W - 2 && py >= 1 && py <= BT_H - 2) {
                 int mx = 0;
