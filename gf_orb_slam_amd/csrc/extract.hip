@@ -485,19 +485,13 @@ __device__ __forceinline__ uint32_t compass2(uint32_t v, uint32_t c0, uint32_t c
 __device__ __forceinline__ uint32_t bytes02(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c020c00u); }
 __device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
 
-__global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score,
-                                                   uint32_t* __restrict__ nms, int map_th) {
+__global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
     __shared__ __align__(16) uint8_t src[BT_R][BT_SP];
     // the row sums (rows 2p | 2p+1 << 16) are dead once the column pass has
     // read them; the candidate list, written after the scan's barriers, reuses them
     __shared__ __align__(16) uint32_t u32buf[BT_U32];
     __shared__ __align__(16) uint32_t sco[BT_H][BT_W / 4];
-    __shared__ uint32_t nmsb[BT_H][BT_W / 32];  // interior NMS survivors, bit x of row y
     __shared__ int scan_tmp[4];
-    __shared__ int s_ncor;  // tile-interior corners listed for the NMS
-    if (threadIdx.x == 0) s_ncor = 0;  // (ordered by the scan's barriers)
-    static_assert(BT_W == 64 && 2 * BT_H <= 256, "k_blur_fast: two NMS words per tile row, one thread each");
-    if (threadIdx.x < 2 * BT_H) (&nmsb[0][0])[threadIdx.x] = 0u;  // ordered by the scan's barriers
     uint32_t(*rows2)[BT_W] = reinterpret_cast<uint32_t(*)[BT_W]>(u32buf);
     uint16_t* cand = reinterpret_cast<uint16_t*>(u32buf);
     int t, f;
@@ -686,12 +680,6 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
     }
     __syncthreads();
     uint8_t* sc8 = reinterpret_cast<uint8_t*>(&sco[0][0]);
-    // corners for the NMS: the candidate list fills u32buf from the bottom, the
-    // corners (a subset) go from the top down, so they meet only when the
-    // candidates take more than half of it; then the NMS walks the candidates
-    const int t1 = max(map_th, 1);
-    const bool clist_on = 2 * nc <= (int)sizeof(u32buf) / 2;
-    uint16_t* clist = reinterpret_cast<uint16_t*>(u32buf) + (sizeof(u32buf) / 2 - 1);
 #if defined(GF_BLUR_EXP) && GF_BLUR_EXP == 1
     for (int i = tid; i < 0; i += 256) {
 #else
@@ -702,40 +690,6 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
         circle_vals(&src[0][0], BT_SP, px + 4, py + 3, c);
         const int M = fast_max_arc(src[py + 3][px + 4], c);  // corner iff M > th; map entry S + 1 = M
         sc8[q] = M > map_th ? (uint8_t)M : 0;
-        if (clist_on) {  // the tile-interior corners the NMS below visits, appended from the top of u32buf
-            const bool cor = M > t1 && px >= 1 && px <= BT_W - 2 && py >= 1 && py <= BT_H - 2;
-            const unsigned long long b = __ballot(cor);
-            int base = 0;
-            if ((tid & 63) == 0 && b) base = atomicAdd(&s_ncor, __popcll(b));
-            base = __shfl(base, 0, 64);
-            if (cor) clist[-(base + __popcll(b & ((1ull << (tid & 63)) - 1ull)))] = (uint16_t)q;
-        }
-    }
-    __syncthreads();
-    // 3x3 NMS of the tile's interior corners (pixels 1 .. 62 of the tile in x
-    // and y, whose eight neighbours the tile holds), as FAST's buffer values
-    // compare: an entry m counts when m > max(th, 1) (m = 1 at th = 0 is a
-    // score-0 corner), else 0. k_fast_cells takes these bits for the window
-    // pixels whose neighbours all lie in the window and in one tile, and
-    // evaluates the rest itself.
-    {
-        const int ncor = clist_on ? s_ncor : nc;
-        for (int i = tid; i < ncor; i += 256) {
-            const int q = clist_on ? clist[-i] : cand[i], py = q >> 6, px = q & 63;
-            const int m = sc8[q];
-            if (m > t1 && px >= 1 && px <= BT_W - 2 && py >= 1 && py <= BT_H - 2) {
-                int mx = 0;
-#pragma unroll
-                for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; dx++) {
-                        if (dx == 0 && dy == 0) continue;
-                        const int n = sc8[q + dy * BT_W + dx];
-                        mx = max(mx, n > t1 ? n : 0);
-                    }
-                if (m > mx) atomicOr(&nmsb[py][px >> 5], 1u << (px & 31));
-            }
-        }
     }
     __syncthreads();
 #pragma unroll
@@ -745,11 +699,6 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
 #pragma unroll
         for (int r = 0; r < 2; r++)
             if (Y0 + r0 + r < h) *reinterpret_cast<uint32_t*>(SC + (long long)r * pw) = sco[r0 + r][qx];
-    }
-    if (tid < 2 * BT_H) {  // the NMS bits: one bit per pixel, rows of pw / 32 words
-        const int r = tid >> 1, wd = tid & 1;
-        if (Y0 + r < h)
-            nms[((long long)f * g.bslab + g.boff[l]) / 32 + (long long)(Y0 + r) * (pw / 32) + X0 / 32 + wd] = nmsb[r][wd];
     }
 }
 
@@ -880,15 +829,13 @@ __device__ __forceinline__ void fc_sync() {
 
 template <typename E>
 __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
-                                                    const uint32_t* __restrict__ nms,
                                                     const CellInfo* __restrict__ cells, E* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ int s_cnt[2][FC_NW];
     __shared__ int scan_tmp[FC_NW];
-    __shared__ int16_t s_srow[64], s_scol[64];  // the window's special rows / columns (see below)
-    __shared__ int s_nsr, s_nsc;
+    __shared__ int s_ncor;
     int cid, f;
     gfd::xcd_block(cid, f);
     const int tid = threadIdx.x;
@@ -931,101 +878,75 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     if (tid == 0) rsh[dh] = 0;
     for (int i = tid; i < ndw; i += FC_NT) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
     for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
-    // Survivors at fast_th. A window pixel whose eight neighbours lie in the
-    // window and in one k_blur_fast tile has the tile's NMS bit (the same map
-    // values, the same rule); the others — the window's edge rows and columns
-    // and the rows / columns on a tile edge (level coordinate 0 or 63 mod 64) —
-    // are evaluated here with the window's rule (outside neighbours read 0).
-    const int X0w = ci.x0 + 3, Y0w = ci.y0 + 3;
-    auto srow = [&](int y) { return y == 0 || y == dh - 1 || ((Y0w + y + 1) & 63) <= 1; };
-    auto scol = [&](int x) { return x == 0 || x == dw - 1 || ((X0w + x + 1) & 63) <= 1; };
+    // Survivors at fast_th, sparse: the window's corners (entries that count
+    // at th: m > max(th, 1), see cell_nms_bits) are listed from a pass over
+    // the window's dwords, then only they compare with their eight neighbours
+    // (the window rule: outside neighbours read 0). A window with more corners
+    // than the list holds runs the dense pass.
     int total = 0;
-    fc_sync();  // the window's map, shifts and zeroed bits
-    if (tid < 64) {  // lists of special rows / columns (ballot compaction on wave 0)
-        int nr = 0, ncl = 0;
-        for (int y0 = 0; y0 < dh; y0 += 64) {
-            const bool sp = y0 + tid < dh && srow(y0 + tid);
-            const unsigned long long b = __ballot(sp);
-            if (sp && nr + __popcll(b & ((1ull << tid) - 1ull)) < 64) s_srow[nr + __popcll(b & ((1ull << tid) - 1ull))] = (int16_t)(y0 + tid);
-            nr += __popcll(b);
-        }
-        for (int x0 = 0; x0 < dw; x0 += 64) {
-            const bool sp = x0 + tid < dw && scol(x0 + tid);
-            const unsigned long long b = __ballot(sp);
-            if (sp && ncl + __popcll(b & ((1ull << tid) - 1ull)) < 64) s_scol[ncl + __popcll(b & ((1ull << tid) - 1ull))] = (int16_t)(x0 + tid);
-            ncl += __popcll(b);
-        }
-        if (tid == 0) {
-            s_nsr = nr;
-            s_nsc = ncl;
-        }
-    }
-    const bool fused = dh <= 64 * 16 && dw <= 64 * 16;  // (lists fit: at most 2 + 2 per 64 rows / columns)
-    if (fused) {
-        // the tile bits of the window rows, special columns masked, special rows skipped
-        const uint32_t* NB = nms + ((long long)f * g.bslab + g.boff[l]) / 32 + (long long)Y0w * (lw / 32);
-        const int nch = (dw + 31) >> 5;
-        for (int it = tid; it < dh * nch; it += FC_NT) {
-            const int y = it / nch, k = it - y * nch;
-            if (srow(y)) continue;
-            const int b = X0w + 32 * k, w0 = b >> 5, sft = b & 31, nb = min(32, dw - 32 * k);
-            const uint32_t* rw = NB + (long long)y * (lw / 32);
-            uint32_t v = gfd::ldg(rw + w0) >> sft;
-            if (sft && sft + nb > 32) v |= gfd::ldg(rw + w0 + 1) << (32 - sft);
-            if (nb < 32) v &= (1u << nb) - 1u;
-            // special columns of this chunk: the window edges, and the columns at
-            // level x = 0 / 63 mod 64 (at most one of each in 32 columns)
-            uint32_t cm = 0;
-            if (k == 0) cm |= 1u;
-            if (dw - 1 - 32 * k < 32) cm |= 1u << (dw - 1 - 32 * k);
-            const int j0 = (64 - ((X0w + 32 * k) & 63)) & 63, j1 = (j0 + 63) & 63;
-            if (j0 < 32) cm |= 1u << j0;
-            if (j1 < 32) cm |= 1u << j1;
-            v &= ~cm;
-            if (v) {
-                const int pp = y * dw + 32 * k;
-                atomicOr(&bits[pp >> 5], v << (pp & 31));
-                if (pp & 31) {
-                    const uint32_t hi = v >> (32 - (pp & 31));
-                    if (hi) atomicOr(&bits[(pp >> 5) + 1], hi);
+    const int t1 = max(fast_th, 1);
+    uint16_t* clist = reinterpret_cast<uint16_t*>(bits + ((nwords + 3) & ~3));  // the retry's ROI area
+    const int ccap = (ci.w * ci.h) >> 1;
+    if (tid == 0) s_ncor = 0;
+    fc_sync();  // the window's map, shifts, zeroed bits and the counter
+    {
+        const float rn = 1.0f / (float)ndw;
+        for (int it0 = 0; it0 < dh * ndw; it0 += FC_NT) {
+            const int it = it0 + tid;
+            uint32_t cm = 0;  // bytes of this dword holding a corner of the window
+            int y = 0, xb = 0;
+            if (it < dh * ndw) {
+                y = (int)(((float)it + 0.5f) * rn);
+                const int q = it - y * ndw;
+                const uint32_t wv = reinterpret_cast<const uint32_t*>(sc)[it];
+                xb = 4 * q - rsh[y];  // window x of the dword's byte 0
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int b = (wv >> (8 * j)) & 0xff, x = xb + j;
+                    cm |= (uint32_t)(b > t1 && x >= 0 && x < dw) << j;
                 }
             }
+            const int nb = __popc(cm);
+            int tot;
+            const int pos = wave_scan_excl(nb, tot);
+            int base = 0;
+            if ((tid & 63) == 0 && tot) base = atomicAdd(&s_ncor, tot);
+            base = __shfl(base, 0, 64) + pos;
+            while (cm) {
+                const int j = __ffs(cm) - 1;
+                cm &= cm - 1;
+                if (base < ccap) clist[base] = (uint16_t)(y * dw + xb + j);
+                base++;
+            }
         }
-        fc_sync();  // (also publishes the special lists)
-        // the special pixels, window rule
-        const int nsr = s_nsr, nsc = s_nsc, t1 = max(fast_th, 1);
+    }
+    fc_sync();
+    const int ncor = s_ncor;
+    if (ncor <= ccap) {
         auto val = [&](int x, int y) -> int {
             if (x < 0 || x >= dw || y < 0 || y >= dh) return 0;
             const int m = sc[y * pitch + rsh[y] + x];
             return m > t1 ? m : 0;
         };
-        for (int it = tid; it < nsr * dw + nsc * dh; it += FC_NT) {
-            int x, y;
-            if (it < nsr * dw) {
-                const int rI = it / dw;
-                y = s_srow[rI];
-                x = it - rI * dw;
-            } else {
-                const int j = it - nsr * dw, cI = j / dh;
-                x = s_scol[cI];
-                y = j - cI * dh;
-                if (srow(y)) continue;  // done in the row pass
+        int c = 0;
+        for (int i0 = 0; i0 < ncor; i0 += FC_NT) {
+            const int i = i0 + tid;
+            bool keep = false;
+            if (i < ncor) {
+                const int p = clist[i], y = p / dw, x = p - y * dw;
+                const int m = val(x, y);
+                int mx = 0;
+#pragma unroll
+                for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; dx++)
+                        if (dx || dy) mx = max(mx, val(x + dx, y + dy));
+                keep = m > mx;
+                if (keep) atomicOr(&bits[p >> 5], 1u << (p & 31));
             }
-            const int m = val(x, y);
-            if (m == 0) continue;
-            int mx = 0;
-#pragma unroll
-            for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                for (int dx = -1; dx <= 1; dx++)
-                    if (dx || dy) mx = max(mx, val(x + dx, y + dy));
-            if (m > mx) atomicOr(&bits[(y * dw + x) >> 5], 1u << ((y * dw + x) & 31));
+            c += __popcll(__ballot(keep));
         }
-        fc_sync();
-        int pc = 0;
-        for (int i = tid; i < nwords; i += FC_NT) pc += __popc(bits[i]);
-        pc = gfd::warp_sum(pc);
-        if ((tid & 63) == 0) s_cnt[0][tid >> 6] = pc;
+        if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
         fc_sync();
     } else {
         const int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, fast_th);
@@ -1699,7 +1620,6 @@ struct gf_extractor {
     int max_tiles = 0;
     // device buffers
     uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_score = nullptr;
-    uint32_t* d_nms = nullptr;  // k_blur_fast's tile-interior NMS bits (one bit per score-map pixel)
     uint32_t *d_xtab = nullptr, *d_ytab = nullptr;  // k_pyramid's block-column / block-row records
     PyrGeom pg{};
     size_t pyr_lds = 0;
@@ -1986,7 +1906,6 @@ static void free_extractor(gf_extractor* ex) {
     (void)hipFree(ex->d_pyr);
     (void)hipFree(ex->d_blur);
     (void)hipFree(ex->d_score);
-    (void)hipFree(ex->d_nms);
     (void)hipFree(ex->d_xtab);
     (void)hipFree(ex->d_ytab);
     (void)hipFree(ex->d_cells);
@@ -2091,7 +2010,6 @@ int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlev
     ALLOC(ex->d_pyr, std::max<long long>(g.slab, 256) * max_batch);
     ALLOC(ex->d_blur, g.bslab * max_batch);
     ALLOC(ex->d_score, g.bslab * max_batch);
-    ALLOC(ex->d_nms, g.bslab / 8 * max_batch);
     ALLOC(ex->d_cells, sizeof(CellInfo) * ex->cells.size());
     const size_t esz = ex->harris ? sizeof(uint64_t) : sizeof(uint32_t);
     ALLOC(ex->d_lists, esz * ex->list_stride * max_batch);
@@ -2297,7 +2215,7 @@ static int extract_planes(gf_extractor* ex, int nframes, Planes P, gf_keypoint* 
     if (ex->stage_ev && ex->stage_after == 0) GF_HIP(hipEventRecord(ex->stage_ev, s));
     {
         GF_PROF(ctx, s, "k_blur_fast");
-        GF_LAUNCH(k_blur_fast, dim3(ex->max_tiles, nframes), 256, 0, s, P, g, ex->d_score, ex->d_nms, ex->fast_th);
+        GF_LAUNCH(k_blur_fast, dim3(ex->max_tiles, nframes), 256, 0, s, P, g, ex->d_score, ex->fast_th);
     }
     if (ex->stage_ev && ex->stage_after == 1) GF_HIP(hipEventRecord(ex->stage_ev, s));
     return ex->harris ? select_describe<uint64_t>(ex, nframes, P, d_kps, d_desc, d_counts, cap, s)
@@ -2314,8 +2232,7 @@ static int select_describe(gf_extractor* ex, int nframes, Planes P, gf_keypoint*
     E* lvl = reinterpret_cast<E*>(ex->d_lvl);
     {
         GF_PROF(ctx, s, "k_fast_cells");
-        GF_LAUNCH(k_fast_cells<E>, dim3(g.ncells, nframes), FC_NT, ex->fast_lds, s, P, g, ex->d_score, ex->d_nms,
-                  ex->d_cells,
+        GF_LAUNCH(k_fast_cells<E>, dim3(g.ncells, nframes), FC_NT, ex->fast_lds, s, P, g, ex->d_score, ex->d_cells,
                   lists, ex->list_stride, ex->d_counts, ex->fast_th, ex->min_th);
         if (!ex->band_cells.empty())
             GF_LAUNCH(k_fast_cells_band<E>, dim3((int)ex->band_cells.size(), nframes), 256, ex->band_lds, s, P, g,
