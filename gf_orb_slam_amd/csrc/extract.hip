@@ -835,7 +835,6 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ int s_cnt[2][FC_NW];
     __shared__ int scan_tmp[FC_NW];
-    __shared__ int s_ncor;
     int cid, f;
     gfd::xcd_block(cid, f);
     const int tid = threadIdx.x;
@@ -878,81 +877,11 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     if (tid == 0) rsh[dh] = 0;
     for (int i = tid; i < ndw; i += FC_NT) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
     for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
-    // Survivors at fast_th, sparse: the window's corners (entries that count
-    // at th: m > max(th, 1), see cell_nms_bits) are listed from a pass over
-    // the window's dwords, then only they compare with their eight neighbours
-    // (the window rule: outside neighbours read 0). A window with more corners
-    // than the list holds runs the dense pass.
-    int total = 0;
-    const int t1 = max(fast_th, 1);
-    uint16_t* clist = reinterpret_cast<uint16_t*>(bits + ((nwords + 3) & ~3));  // the retry's ROI area
-    const int ccap = (ci.w * ci.h) >> 1;
-    if (tid == 0) s_ncor = 0;
-    fc_sync();  // the window's map, shifts, zeroed bits and the counter
-    {
-        const float rn = 1.0f / (float)ndw;
-        for (int it0 = 0; it0 < dh * ndw; it0 += FC_NT) {
-            const int it = it0 + tid;
-            uint32_t cm = 0;  // bytes of this dword holding a corner of the window
-            int y = 0, xb = 0;
-            if (it < dh * ndw) {
-                y = (int)(((float)it + 0.5f) * rn);
-                const int q = it - y * ndw;
-                const uint32_t wv = reinterpret_cast<const uint32_t*>(sc)[it];
-                xb = 4 * q - rsh[y];  // window x of the dword's byte 0
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int b = (wv >> (8 * j)) & 0xff, x = xb + j;
-                    cm |= (uint32_t)(b > t1 && x >= 0 && x < dw) << j;
-                }
-            }
-            const int nb = __popc(cm);
-            int tot;
-            const int pos = wave_scan_excl(nb, tot);
-            int base = 0;
-            if ((tid & 63) == 0 && tot) base = atomicAdd(&s_ncor, tot);
-            base = __shfl(base, 0, 64) + pos;
-            while (cm) {
-                const int j = __ffs(cm) - 1;
-                cm &= cm - 1;
-                if (base < ccap) clist[base] = (uint16_t)(y * dw + xb + j);
-                base++;
-            }
-        }
-    }
     fc_sync();
-    const int ncor = s_ncor;
-    if (ncor <= ccap) {
-        auto val = [&](int x, int y) -> int {
-            if (x < 0 || x >= dw || y < 0 || y >= dh) return 0;
-            const int m = sc[y * pitch + rsh[y] + x];
-            return m > t1 ? m : 0;
-        };
-        int c = 0;
-        for (int i0 = 0; i0 < ncor; i0 += FC_NT) {
-            const int i = i0 + tid;
-            bool keep = false;
-            if (i < ncor) {
-                const int p = clist[i], y = p / dw, x = p - y * dw;
-                const int m = val(x, y);
-                int mx = 0;
-#pragma unroll
-                for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; dx++)
-                        if (dx || dy) mx = max(mx, val(x + dx, y + dy));
-                keep = m > mx;
-                if (keep) atomicOr(&bits[p >> 5], 1u << (p & 31));
-            }
-            c += __popcll(__ballot(keep));
-        }
-        if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
-        fc_sync();
-    } else {
-        const int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, fast_th);
-        if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
-        fc_sync();
-    }
+    int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, fast_th);
+    if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
+    fc_sync();
+    int total = 0;
 #pragma unroll
     for (int k = 0; k < FC_NW; k++) total += s_cnt[0][k];
     if (total <= 3) {  // ORBextractor.cc:623-628: retry with the minimum threshold
@@ -974,7 +903,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         }
         for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
         fc_sync();
-        const int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, min_th);
+        c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, min_th);
         if ((tid & 63) == 0) s_cnt[1][tid >> 6] = c;
         fc_sync();
         total = 0;
