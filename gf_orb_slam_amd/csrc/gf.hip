@@ -718,12 +718,12 @@ __device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst&
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
                            const double* info_lt,
-                           const int32_t* rmp, const int* cell_start, const int* items, const int* claim,
+                           const int32_t* lq, const int* cell_start, const int* items, const int* claim,
                            const gf_keypoint* K, const uint8_t* D) {
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
-        const long long qi = rmp ? rmp[q] : q;
+        const long long qi = lq[sl];  // the slot's info / H row (remapped at the pool build)
         C.score[c] = logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
@@ -1021,6 +1021,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     int16_t* sm_h2 = sm_h1 + PC;                                           // PC
     int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
     uint8_t* c_alive = (uint8_t*)(alv + PC);                               // CC
+    int32_t* lq = (int32_t*)(((uintptr_t)(c_alive + CC) + 3) & ~(uintptr_t)3);  // PC: info / H row of each slot
+    uint8_t* koct = (uint8_t*)(lq + PC);                                   // kp_cap: keypoint octaves
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
@@ -1068,7 +1070,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     // the keypoint grid comes from k_onepoint_pre (HBM; only rescans read it)
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
-    for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
+    for (int i = lane; i < n; i += AW) {
+        claim[i] = kp2mp[i];
+        koct[i] = (uint8_t)K[i].octave;  // the commit's sigma^2 lookup, from LDS
+    }
+    const float sig2l = lane < 16 ? A.sigma2[lane] : 0.f;  // level sigma^2, lane = octave
     uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
 #pragma unroll
     for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
@@ -1081,10 +1087,12 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     for (int base = 0; base < m; base += AW) {
         const int i = base + lane;
         bool in = false, upd = false;
+        int rq = i;
         if (i < m) {
             const long long g = (long long)f * A.mp_cap + i;
             in = A.views[g].in_view;
             upd = A.updated[g];
+            if (A.remap) rq = A.remap[g];  // (loaded beside the flags: no extra round trip)
         }
         const bool take = in && (early || upd);
         const unsigned long long msk = __ballot(take);
@@ -1094,6 +1102,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 left[o] = i;
             } else if (o < PC) {
                 lmk[o] = (int16_t)i;
+                lq[o] = rq;
                 vis[o] = -1;
             }
         }
@@ -1154,7 +1163,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     const double* info = A.info + (long long)f * A.mp_cap * 49;
     const double* info_lt = A.info_lt + (long long)f * A.mp_cap * 32;
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
-    const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
 
     for (int round = 0; round < num_to_match; ++round) {
         const int sz = __builtin_amdgcn_readfirstlane(min(S, N));
@@ -1269,7 +1277,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K, D);
         evald = nc;
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
@@ -1315,7 +1323,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             if (rep < nc && rep >= evald) {
                 AM_T(4);
-                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K, D);
                 evald = nc;
                 AM_T(3);
             }
@@ -1333,7 +1341,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (nc - rep0 < 16 && exh_at < 0 && !cabort) draw_eval(nc);  // a useful window
                 if (evald < nc && !cabort) {
                     AM_T(4);
-                    eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, rmp, cell_start, items, claim, K,
+                    eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K,
                                D);
                     evald = nc;
                     AM_T(3);
@@ -1687,14 +1695,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
         int oct_b = 0;
         if (!exh && lane < 49) {
-            const int qt = lmk[C.slot[top]];
-            const double* Hq = Hm + 14LL * (rmp ? rmp[qt] : qt);
+            const double* Hq = Hm + 14LL * lq[C.slot[top]];
             const int i = lane / 7, jj = lane % 7;
             h_i = Hq[i];
             h_j = Hq[jj];
             h_7i = Hq[7 + i];
             h_7j = Hq[7 + jj];
-            oct_b = K[C.match[top]].octave;
+            oct_b = koct[C.match[top]];
         }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
@@ -1719,7 +1726,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             A.score[(long long)f * A.kp_cap + b] = C.dist[top];
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
-            const double s2 = sqrt((double)A.sigma2[oct_b]);
+            const double s2 = sqrt((double)__shfl(sig2l, oct_b, 64));
             const double w = s2 / (s2 * s2);
             const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
@@ -1799,7 +1806,8 @@ __global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
 
 size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap) {
     return sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) + sizeof(int32_t) * cand_cap +
-           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap;
+           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap + 3 +
+           sizeof(int32_t) * (size_t)pool_cap + (size_t)kp_cap;
 }
 
 // ------------------------------------------------------------- max-volume selection
