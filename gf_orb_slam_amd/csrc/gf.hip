@@ -372,6 +372,7 @@ struct ActiveArgs {
     int pass;                  // 0 = single launch, 1 = small-pool pass, 2 = overflow pass
     const double* info_lt;     // null, or the packed lower triangles of info ([F][mp_cap][32])
     gf::ActiveClock ck;        // the front end's time cap (ck.mat_t0 null: none)
+    int lq_stage;              // 1: each pool slot's info / H row (remap) staged in LDS (when it fits)
 };
 
 // ---------------------------------------------------------------------------
@@ -718,12 +719,13 @@ __device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst&
 __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, const Cands& C, int c0, int c1,
                            const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
                            const double* info_lt,
-                           const int32_t* lq, const int* cell_start, const int* items, const int* claim,
-                           const gf_keypoint* K, const uint8_t* D) {
+                           const uint16_t* lq, const int32_t* rmp, const int* cell_start, const int* items,
+                           const int* claim, const gf_keypoint* K, const uint8_t* D) {
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
-        const long long qi = lq[sl];  // the slot's info / H row (remapped at the pool build)
+        // the slot's info / H row: staged at the pool build (lq_stage), else through the remap
+        const long long qi = A.lq_stage ? (long long)lq[sl] : (rmp ? rmp[q] : q);
         C.score[c] = logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
@@ -1021,8 +1023,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     int16_t* sm_h2 = sm_h1 + PC;                                           // PC
     int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
     uint8_t* c_alive = (uint8_t*)(alv + PC);                               // CC
-    int32_t* lq = (int32_t*)(((uintptr_t)(c_alive + CC) + 3) & ~(uintptr_t)3);  // PC: info / H row of each slot
-    uint8_t* koct = (uint8_t*)(lq + PC);                                   // kp_cap: keypoint octaves
+    uint16_t* lq = (uint16_t*)(((uintptr_t)(c_alive + CC) + 1) & ~(uintptr_t)1);  // PC (lq_stage): info / H row of each slot
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
@@ -1070,11 +1071,15 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     // the keypoint grid comes from k_onepoint_pre (HBM; only rescans read it)
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
-    for (int i = lane; i < n; i += AW) {
-        claim[i] = kp2mp[i];
-        koct[i] = (uint8_t)K[i].octave;  // the commit's sigma^2 lookup, from LDS
-    }
+    for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
     const float sig2l = lane < 16 ? A.sigma2[lane] : 0.f;  // level sigma^2, lane = octave
+    const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
+    // a slot's info / H row: staged at the pool build, or read through the remap
+    auto row_of = [&](int sl) -> long long {
+        if (A.lq_stage) return lq[sl];
+        const int q = lmk[sl];
+        return rmp ? rmp[q] : q;
+    };
     uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
 #pragma unroll
     for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
@@ -1092,7 +1097,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             const long long g = (long long)f * A.mp_cap + i;
             in = A.views[g].in_view;
             upd = A.updated[g];
-            if (A.remap) rq = A.remap[g];  // (loaded beside the flags: no extra round trip)
+            if (A.remap && A.lq_stage) rq = A.remap[g];  // (loaded beside the flags: no extra round trip)
         }
         const bool take = in && (early || upd);
         const unsigned long long msk = __ballot(take);
@@ -1102,7 +1107,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 left[o] = i;
             } else if (o < PC) {
                 lmk[o] = (int16_t)i;
-                lq[o] = rq;
+                if (A.lq_stage) lq[o] = (uint16_t)rq;
                 vis[o] = -1;
             }
         }
@@ -1277,7 +1282,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D);
         evald = nc;
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
@@ -1323,7 +1328,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             if (rep < nc && rep >= evald) {
                 AM_T(4);
-                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D);
                 evald = nc;
                 AM_T(3);
             }
@@ -1341,7 +1346,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (nc - rep0 < 16 && exh_at < 0 && !cabort) draw_eval(nc);  // a useful window
                 if (evald < nc && !cabort) {
                     AM_T(4);
-                    eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, cell_start, items, claim, K,
+                    eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K,
                                D);
                     evald = nc;
                     AM_T(3);
@@ -1695,13 +1700,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
         int oct_b = 0;
         if (!exh && lane < 49) {
-            const double* Hq = Hm + 14LL * lq[C.slot[top]];
+            const double* Hq = Hm + 14LL * row_of(C.slot[top]);
             const int i = lane / 7, jj = lane % 7;
             h_i = Hq[i];
             h_j = Hq[jj];
             h_7i = Hq[7 + i];
             h_7j = Hq[7 + jj];
-            oct_b = koct[C.match[top]];
+            oct_b = K[C.match[top]].octave;
         }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
@@ -1804,11 +1809,12 @@ __global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
 
 #undef AM_T
 
-size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap) {
+size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap, bool lq_stage = false) {
     return sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) + sizeof(int32_t) * cand_cap +
-           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap + 3 +
-           sizeof(int32_t) * (size_t)pool_cap + (size_t)kp_cap;
+           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
+           (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
 }
+constexpr size_t AM_LDS_LIMIT = 160 * 1024;  // gfx950 LDS per workgroup
 
 // ------------------------------------------------------------- max-volume selection
 struct MaxvolArgs {
@@ -2121,10 +2127,14 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     }
     const int full_pc = std::min(((mp_cap + 63) / 64) * 64, POOL_MAX);
     static unsigned long long ovf_mask = 0;
-    if ((rc = set_lds_attr(ctx, (const void*)k_active_match, active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX), &mask)) ||
-        (rc = set_lds_attr(ctx, (const void*)k_active_match_overflow, active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX),
-                           &ovf_mask)))
+    const size_t lds_max = std::min(active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX, true), AM_LDS_LIMIT);
+    if ((rc = set_lds_attr(ctx, (const void*)k_active_match, lds_max, &mask)) ||
+        (rc = set_lds_attr(ctx, (const void*)k_active_match_overflow, lds_max, &ovf_mask)))
         return rc;
+    // the slots' rows go to LDS when the remapped rows fit 16 bits and the launch's LDS allows
+    auto lq_fits = [&](int pc, int cc) {
+        return mp_cap <= 65536 && active_lds_bytes(pc, cc, kp_cap, true) <= AM_LDS_LIMIT;
+    };
     // Two passes when the map list is long: most frames' pools (in-view, updated
     // points) are far below the list capacity, and a smaller LDS footprint lets
     // more workgroups of the concurrently running kernels share each CU. Frames
@@ -2149,7 +2159,8 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     }
     {
         GF_PROF(ctx, s, "k_active_match");
-        GF_LAUNCH(k_active_match, nframes, AW, active_lds_bytes(A.pool_cap, A.cand_cap, kp_cap), s, A);
+        A.lq_stage = lq_fits(A.pool_cap, A.cand_cap) ? 1 : 0;
+        GF_LAUNCH(k_active_match, nframes, AW, active_lds_bytes(A.pool_cap, A.cand_cap, kp_cap, A.lq_stage), s, A);
         GF_HIP(hipGetLastError());
     }
     if (A.pass == 1) {
@@ -2160,8 +2171,9 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
         // list's count exit at once): with long maps (config 3) every frame's
         // pool is past the first pass's, and 64 workgroups walked 256 frames
         // four deep (7.7 ms of the step)
+        A.lq_stage = lq_fits(full_pc, full_pc) ? 1 : 0;
         GF_LAUNCH(k_active_match_overflow, std::min(nframes, AM_OVF_GRID), AW,
-                  active_lds_bytes(full_pc, full_pc, kp_cap), s, A);
+                  active_lds_bytes(full_pc, full_pc, kp_cap, A.lq_stage), s, A);
         GF_HIP(hipGetLastError());
     }
     return GF_OK;
