@@ -1814,7 +1814,9 @@ size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap, bool lq_stage = 
            sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
            (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
 }
-constexpr size_t AM_LDS_LIMIT = 160 * 1024;  // gfx950 LDS per workgroup
+// dynamic LDS bound of the active matcher's launches: the full-capacity
+// footprint without the staged rows (the static arrays take the rest of 160 KB)
+static const size_t AM_LDS_LIMIT = active_lds_bytes(POOL_MAX, POOL_MAX, KP_MAX, false);
 
 // ------------------------------------------------------------- max-volume selection
 struct MaxvolArgs {
