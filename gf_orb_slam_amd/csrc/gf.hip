@@ -1027,7 +1027,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
-    __shared__ float s_sig2[16];           // level sigma^2 (A.sigma2)
 #if AM_SLOTS
     __shared__ __align__(16) double s_lsc[64];  // slot_loop: live scores, lane order (-inf past sz)
     __shared__ __align__(16) double s_xsc[64];  // slot_loop: the window's scores (-inf past W)
@@ -1073,10 +1072,6 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
     for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
-    // level sigma^2 in LDS for the commit (a cross-lane read of a register
-    // held since the kernel start is not safe: the compiler may move it under
-    // a partial exec mask, leaving the source lane's copy stale)
-    if (lane < 16) s_sig2[lane] = A.sigma2[lane];
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
     // a slot's info / H row: staged at the pool build, or read through the remap
     auto row_of = [&](int sl) -> long long {
@@ -1735,7 +1730,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             A.score[(long long)f * A.kp_cap + b] = C.dist[top];
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
-            const double s2 = sqrt((double)s_sig2[oct_b]);
+            const double s2 = sqrt((double)A.sigma2[oct_b]);
             const double w = s2 / (s2 * s2);
             const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
