@@ -601,6 +601,9 @@ size_t onepoint_pre_lds_bytes(int kp_cap) {
 #ifdef GF_AM_STAMP
 __device__ unsigned long long g_am_stamp[8];
 #endif
+#ifdef GF_AM_GUARD
+__device__ unsigned long long g_am_guard[2];  // [0] corrupted sentinel dwords, [1] frames checked
+#endif
 
 // Per-round candidate list: the draws of the sequential loop in order (the
 // initial random subset, then one replacement per failed top), produced 64
@@ -1006,7 +1009,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
 #else
     const int CC = PC;
 #endif
+#ifdef GF_AM_GUARD  // diagnostic build: 256 sentinel bytes below the dynamic arrays, checked at the end
+    uint32_t* guard = (uint32_t*)smem;
+    guard[threadIdx.x] = 0xa5a5a5a5u + threadIdx.x;
+    double* c_score = (double*)(smem + 256);                               // CC
+#else
     double* c_score = (double*)smem;                                       // CC
+#endif
     unsigned long long* pbits = (unsigned long long*)(c_score + CC);       // 64
     int* claim = (int*)(pbits + 64);                                       // kp_cap
     int* ppre = claim + A.kp_cap;                                          // 65 (+3 pad)
@@ -1765,6 +1774,11 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         if (((bits >> lane) & 1ull) && w * 64 + lane < PC)
             left[ppre[w] + __popcll(bits & ((1ull << lane) - 1ull))] = lmk[w * 64 + lane];
     }
+#ifdef GF_AM_GUARD
+    am_sync();
+    if (guard[threadIdx.x] != 0xa5a5a5a5u + threadIdx.x) atomicAdd(&g_am_guard[0], 1ull);
+    if (threadIdx.x == 0) atomicAdd(&g_am_guard[1], 1ull);
+#endif
     {  // back to the glibc ring: f advanced by the calls made, oldest word at f
         const int f1 = (A.rng[f].f + used) % 31;
         am_sync();
@@ -1809,8 +1823,13 @@ __global__ __launch_bounds__(AW) void k_active_match_overflow(ActiveArgs A) {
 #undef AM_T
 
 size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap, bool lq_stage = false) {
-    return sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) + sizeof(int32_t) * cand_cap +
-           sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
+#ifdef GF_AM_GUARD
+    const size_t guard = 256;
+#else
+    const size_t guard = 0;
+#endif
+    return guard + sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) +
+           sizeof(int32_t) * cand_cap + sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
            (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
 }
 // dynamic LDS bound of the active matcher's launches: the full-capacity
@@ -2669,6 +2688,11 @@ int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2
 
 }  // extern "C"
 
+#ifdef GF_AM_GUARD
+extern "C" int gf_debug_am_guard(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_guard), sizeof(unsigned long long) * 2) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef GF_AM_STAMP
 // Diagnostic build only (not in the header): phase cycles of k_active_match.
 extern "C" int gf_debug_am_stamps(unsigned long long* out, int reset) {
