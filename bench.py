@@ -966,18 +966,20 @@ def main():
         top = max(prof, key=lambda k: prof[k][0])
         dom = max(priced, key=lambda k: prof[k][0])
     traffic_src = None
-    for cand in ("r04",):  # PMC traffic measured on this round's build and workload only
+    for cand in ("r05",):  # PMC traffic measured on this round's build and workload only
         try:
             pmc = json.load(open(os.path.join(ROOT, "profiles", cand, "pmc_traffic.json")))
             if pmc.get("batch") == Bg:
                 pk = pmc.get("kernels", {})
                 for k in priced:  # every priced kernel whose dispatches the PMC table holds
-                    if k == "k_pyramid" and pmc.get("round", "r04") == "r04":  # r04 measured the seven-dispatch k_resize
-                        continue
                     names = [n for n in SCOPE.get(k, [k]) if n in pk]
                     if names:
                         priced[k]["traffic"] = round(sum(pk[n]["traffic_bytes"] for n in names))
-                traffic_src = f"profiles/{cand}/pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE per launch)"
+                        priced[k]["traffic_min"] = round(sum(pk[n].get("traffic_bytes_min", pk[n]["traffic_bytes"])
+                                                             for n in names))
+                traffic_src = (f"profiles/{cand}/pmc_traffic.json: traffic = 2 x FETCH_SIZE + WRITE_SIZE per launch "
+                               "(exact for 128-B read requests), traffic_min = FETCH_SIZE + WRITE_SIZE (scattered "
+                               "64-B requests; calibration in that file)")
                 break
         except (OSError, ValueError, KeyError):
             pass

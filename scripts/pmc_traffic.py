@@ -5,6 +5,7 @@ the bytes of coalesced streaming reads, so it is doubled. Writes the table
 bench.py reads for roofline.traffic.
 python scripts/pmc_traffic.py <summary.json> <out.json> <batch> <source text>"""
 import json
+import re
 import sys
 
 summ = json.load(open(sys.argv[1]))
@@ -16,6 +17,7 @@ for k, v in sorted(summ.items()):
     if "FETCH_SIZE" not in v or "WRITE_SIZE" not in v:
         continue
     fb, wb = 2 * v["FETCH_SIZE"] * 1024, v["WRITE_SIZE"] * 1024
+    k = re.sub(r"^void ", "", k).split("<")[0]  # kernel names as bench.py / rocprof tables use them
     out["kernels"][k] = {"fetch_bytes": round(fb), "write_bytes": round(wb), "traffic_bytes": round(fb + wb),
                          "fetch_size_kib_raw": v["FETCH_SIZE"], "write_size_kib_raw": v["WRITE_SIZE"],
                          "grid_size": v.get("grid_size"), "dispatches": v.get("dispatches")}
