@@ -247,6 +247,15 @@ namespace gfd {
 __device__ __forceinline__ void track_prio() {
     if (GF_TRACK_PRIO) __builtin_amdgcn_s_setprio(GF_TRACK_PRIO);
 }
+// GF_EXT_PRIO: the same for the extraction kernels (the groups' extraction
+// stages run one at a time and pace the step; the other groups' tracking
+// waves share their SIMDs)
+#ifndef GF_EXT_PRIO
+#define GF_EXT_PRIO 0
+#endif
+__device__ __forceinline__ void ext_prio() {
+    if (GF_EXT_PRIO) __builtin_amdgcn_s_setprio(GF_EXT_PRIO);
+}
 
 // Elapsed ticks at a budget's clock check: the device clock (s_memrealtime,
 // 100 MHz) since t0, or with a test clock (syn = the site's base and slope,

@@ -212,6 +212,7 @@ template <int G>
 __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGeom pg,
                                                     const uint32_t* __restrict__ xrec,
                                                     const uint32_t* __restrict__ yrec) {
+    gfd::ext_prio();
     extern __shared__ __align__(16) uint8_t pyr_lds[];
     int blk, f;
     gfd::xcd_block(blk, f);
@@ -486,6 +487,7 @@ __device__ __forceinline__ uint32_t bytes02(uint32_t w) { return __builtin_amdgc
 __device__ __forceinline__ uint32_t bytes13(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
 
 __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_t* __restrict__ score, int map_th) {
+    gfd::ext_prio();
     __shared__ __align__(16) uint8_t src[BT_R][BT_SP];
     // the row sums (rows 2p | 2p+1 << 16) are dead once the column pass has
     // read them; the candidate list, written after the scan's barriers, reuses them
@@ -832,6 +834,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
                                                     const CellInfo* __restrict__ cells, E* __restrict__ lists,
                                                     long long list_stride, int* __restrict__ counts, int fast_th,
                                                     int min_th) {
+    gfd::ext_prio();
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ int s_cnt[2][FC_NW];
     __shared__ int scan_tmp[FC_NW];
@@ -949,6 +952,7 @@ __global__ __launch_bounds__(256) void k_fast_cells_band(Planes P, LevelGeom g, 
                                                          const int* __restrict__ band_ids, E* __restrict__ lists,
                                                          long long list_stride, int* __restrict__ counts, int fast_th,
                                                          int min_th) {
+    gfd::ext_prio();
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ int s_cnt[4];
     __shared__ int scan_tmp[4];
@@ -1273,6 +1277,7 @@ __global__ __launch_bounds__(64 * SEL_CW) void k_select_cells(LevelGeom g, const
                                                               const int* __restrict__ counts,
                                                               E* __restrict__ lvl_lists, long long lvl_stride,
                                                               int* __restrict__ lvl_counts, int maxnc) {
+    gfd::ext_prio();
     extern __shared__ __align__(16) uint8_t sel_dyn[];
     const int f = blockIdx.y, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int c = blockIdx.x * SEL_CW + wv;  // cell (all levels, level-major)
@@ -1303,6 +1308,7 @@ __global__ __launch_bounds__(64 * SEL_CW) void k_select_cells(LevelGeom g, const
 template <typename E>
 __global__ __launch_bounds__(64) void k_select_level(LevelGeom g, E* __restrict__ lvl_lists, long long lvl_stride,
                                                      int* __restrict__ lvl_counts) {
+    gfd::ext_prio();
     extern __shared__ __align__(16) uint8_t sel_dyn[];
     const int f = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
     SelWave<E> W;
@@ -1383,6 +1389,7 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
                                                   long long lvl_stride, const int* __restrict__ lvl_counts,
                                                   gf_keypoint* __restrict__ kps, uint8_t* __restrict__ desc,
                                                   int* __restrict__ out_counts, int cap) {
+    gfd::ext_prio();
     __shared__ DescLds sh_all[8];
     // the rBRIEF pattern, one dword per test, bit-major (test 8 i + bit at
     // bit * 32 + i): the 32 lanes of a half read 32 consecutive dwords
