@@ -188,7 +188,9 @@ struct PyrGeom {
 
 __device__ __forceinline__ int pyr_pitch(int span) { return (span + 8 + 3) & ~3; }
 
-// floor(i / n) for 0 <= i < 2^16, 1 <= n <= 2^10 (rcp is exact enough there)
+// floor(i / n) for 0 <= i < 2^20, n >= 1, rn = 1 / n in float: the product's
+// relative error (~2^-22) stays below the 0.5 / n margin the + 0.5 leaves
+// while i < 2^21
 __device__ __forceinline__ int pyr_div(int i, float rn) { return (int)(((float)i + 0.5f) * rn); }
 
 // Records, made on the host, staged in LDS with the level-0 pixels (the level
@@ -863,7 +865,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
 #pragma unroll
         for (int k = 0; k < FC_LB; k++) {
             const int i = i0 + FC_NT * k + tid;
-            const int r = i / ndw, q = i - r * ndw;
+            const int r = pyr_div(i, 1.0f / (float)ndw), q = i - r * ndw;
             v[k] = 0;
             if (r < dh) {
                 const uintptr_t a = (uintptr_t)(SC + (long long)r * lw);
@@ -893,12 +895,12 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         int sstride;
         const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
         for (int i = tid; i < ci.w * ci.h; i += FC_NT) {
-            const int r = i / ci.w;
+            const int r = pyr_div(i, 1.0f / (float)ci.w);
             roi[i] = gfd::ldg(Sl + (long long)r * sstride + (i - r * ci.w));
         }
         fc_sync();
         for (int i = tid; i < n; i += FC_NT) {
-            const int y = i / dw, x = i - y * dw;
+            const int y = pyr_div(i, 1.0f / (float)dw), x = i - y * dw;
             int c[16];
             circle_vals(roi, ci.w, x + 3, y + 3, c);
             const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
@@ -929,7 +931,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         while (word) {
             const int p = 32 * i + __ffs(word) - 1;
             word &= word - 1;
-            const int y = p / dw, x = p - y * dw;
+            const int y = pyr_div(p, 1.0f / (float)dw), x = p - y * dw;
             out[off++] = cell_entry<E>(sc[y * pitch + rsh[y] + x] - 1, X0 + x, Y0 + y, P, g, f, l);
         }
         base += tot;
@@ -979,7 +981,7 @@ __global__ __launch_bounds__(256) void k_fast_cells_band(Planes P, LevelGeom g, 
             __syncthreads();  // the previous band's NMS reads are done
             if (pass == 0) {
                 for (int i = tid; i < nr * ndw; i += 256) {
-                    const int r = i / ndw, q = i - r * ndw;
+                    const int r = pyr_div(i, 1.0f / (float)ndw), q = i - r * ndw;
                     const uintptr_t a = (uintptr_t)(SC + (long long)(lo + r) * lw);
                     uint32_t v = 0;
                     if (4 * q < (int)(a & 3) + dw) v = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
@@ -990,12 +992,12 @@ __global__ __launch_bounds__(256) void k_fast_cells_band(Planes P, LevelGeom g, 
                 // window row y's circle lies in ROI rows y .. y + 6
                 const int rr = nr + 6;
                 for (int i = tid; i < rr * ci.w; i += 256) {
-                    const int r = i / ci.w;
+                    const int r = pyr_div(i, 1.0f / (float)ci.w);
                     roi[i] = gfd::ldg(Sl + (long long)(lo + r) * sstride + (i - r * ci.w));
                 }
                 __syncthreads();
                 for (int i = tid; i < nr * dw; i += 256) {
-                    const int y = i / dw, x = i - y * dw;
+                    const int y = pyr_div(i, 1.0f / (float)dw), x = i - y * dw;
                     int c[16];
                     circle_vals(roi, ci.w, x + 3, y + 3, c);
                     const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
@@ -1026,7 +1028,7 @@ __global__ __launch_bounds__(256) void k_fast_cells_band(Planes P, LevelGeom g, 
         while (word) {
             const int p = 32 * i + __ffs(word) - 1;
             word &= word - 1;
-            const int y = p / dw, x = p - y * dw;
+            const int y = pyr_div(p, 1.0f / (float)dw), x = p - y * dw;
             int S;
             if (pass == 0) {
                 S = SC[(long long)y * lw + x] - 1;
