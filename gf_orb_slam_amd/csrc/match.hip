@@ -546,19 +546,27 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
         }
 #pragma unroll
         for (int o = 1; o < SEQ_PRE_G; o <<= 1) {
-            unsigned long long p[4], m[4];
+            unsigned long long p[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) p[j] = __shfl_xor(key[j], o, 64);
             nc += __shfl_xor(nc, o, 64);
-            // merge two ascending lists, keep the four smallest
-            int a = 0, b = 0;
+            // the four smallest of two ascending lists, ascending: a bitonic
+            // merge with fixed indices (min of one list against the other
+            // reversed, then a two-stage sort), so the lists stay in registers
+            // (a data-dependent merge index put them in scratch memory). Keys
+            // are distinct (they carry the candidate order), so the result is
+            // the merge's.
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const unsigned long long ka = a < 4 ? key[a] : NONE, kb = b < 4 ? p[b] : NONE;
-                if (ka <= kb) { m[j] = ka; a++; } else { m[j] = kb; b++; }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) key[j] = m[j];
+            for (int j = 0; j < 4; j++) key[j] = key[j] < p[3 - j] ? key[j] : p[3 - j];
+            auto cx = [](unsigned long long& x, unsigned long long& y) {
+                const unsigned long long lo = x < y ? x : y, hi = x < y ? y : x;
+                x = lo;
+                y = hi;
+            };
+            cx(key[0], key[2]);
+            cx(key[1], key[3]);
+            cx(key[0], key[1]);
+            cx(key[2], key[3]);
         }
         if (live && g == 0) {
             SeqPre r;
@@ -678,15 +686,22 @@ __global__ __launch_bounds__(SEQ_THREADS) void k_match_seq(MatchArgs A, FrameCon
             const SeqPre pr = spre[qi];
             k = qidx[qi];
             id = pr.id;
-            int j = 0;
-            while (j < 4 && pr.h[j] >= 0 && claim[pr.h[j]] >= 0) j++;
-            const bool known = (j < 4 && pr.h[j] >= 0) || j >= pr.ncand;
+            // j = the first of the four precomputed candidates that is absent or
+            // still unclaimed (4: all claimed). Fixed indices throughout: a
+            // data-dependent index into the record put it in scratch memory.
+            const int h0 = pr.h[0], h1 = pr.h[1], h2 = pr.h[2], h3 = pr.h[3];
+            const bool c0 = h0 >= 0 && claim[max(h0, 0)] >= 0, c1 = h1 >= 0 && claim[max(h1, 0)] >= 0;
+            const bool c2 = h2 >= 0 && claim[max(h2, 0)] >= 0, c3 = h3 >= 0 && claim[max(h3, 0)] >= 0;
+            const int j = !c0 ? 0 : !c1 ? 1 : !c2 ? 2 : !c3 ? 3 : 4;
+            const int hj = j == 0 ? h0 : j == 1 ? h1 : j == 2 ? h2 : j == 3 ? h3 : -1;
+            const int dj = j == 0 ? pr.d[0] : j == 1 ? pr.d[1] : j == 2 ? pr.d[2] : j == 3 ? pr.d[3] : 0;
+            const bool known = (j < 4 && hj >= 0) || j >= pr.ncand;
             rescan = !known;
-            if (known && j < 4 && pr.h[j] >= 0) {
-                pick = pr.h[j];
-                if (j < pr.ncand && pr.d[j] <= TH_HIGH) {
+            if (known && j < 4 && hj >= 0) {
+                pick = hj;
+                if (j < pr.ncand && dj <= TH_HIGH) {
                     res = pick;
-                    dres = pr.d[j];
+                    dres = (int16_t)dj;
                 }
             }
             if (res >= 0) atomicMin(&mk[res], lane);
