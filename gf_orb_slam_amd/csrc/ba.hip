@@ -216,6 +216,36 @@ __device__ __forceinline__ void edge_jac(const double* m, const gfse3::SE3& T, c
     Jc[1][5] = y / z2 * fy;
 }
 
+// BA_EG consecutive edges [le0, le0 + BA_EG) of one point (problem-local,
+// clipped at ee): active flags, measurement records, the keyframe poses of
+// estimate buffer buf and the free-pose columns, every load issued before any
+// of them is used. A point's edge loop pays two memory round trips per group
+// instead of two or three per edge; the edges are still consumed in order.
+constexpr int BA_EG = 4;
+struct BAEdgeGroup {
+    bool act[BA_EG];
+    int col[BA_EG];
+    double m[BA_EG][8];
+    gfse3::SE3 T[BA_EG];
+    __device__ __forceinline__ void load(const BAArena& A, const BADesc& d, int buf, int le0, int ee) {
+        int kf[BA_EG];
+#pragma unroll
+        for (int q = 0; q < BA_EG; q++) {
+            const int ge = d.e0 + min(le0 + q, ee - 1);
+            const uint8_t a = A.e_act[ge];
+            act[q] = le0 + q < ee && a;
+            kf[q] = A.e_kf[ge];
+#pragma unroll
+            for (int k = 0; k < 8; k++) m[q][k] = A.e_meas[(size_t)ge * 8 + k];
+        }
+#pragma unroll
+        for (int q = 0; q < BA_EG; q++) {
+            T[q] = load_T(A, buf, d.kf0 + kf[q]);
+            col[q] = A.kf_col[d.kf0 + kf[q]];
+        }
+    }
+};
+
 // Workgroup sum / max of one double per thread in a fixed order.
 __device__ double block_reduce(double v, double* sh, bool is_max) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -307,41 +337,47 @@ __global__ __launch_bounds__(BA_T) void k_ba_linearize(BAArena A) {
         double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
         int nact = 0;
         const int eb = A.pt_eb[gp], ee = A.pt_ee[gp];
-        for (int le = eb; le < ee; le++) {
-            const int ge = d.e0 + le;
-            if (!A.e_act[ge]) continue;
-            nact++;
-            const int kf = A.e_kf[ge];
-            const double* m = A.e_meas + (size_t)ge * 8;
-            const gfse3::SE3 T = load_T(A, cur, d.kf0 + kf);
-            double pc[3], e0, e1;
-            edge_error(m, T, X, pc, e0, e1);
-            const double info = m[2];
-            double rho0, rho1;
-            huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
-            chi += rho0;
-            double Jp[2][3], Jc[2][6];
-            edge_jac(m, T, pc, Jp, Jc, true);
-            const double w = rho1 * info;
-            const double o0 = -(info * e0) * rho1, o1 = -(info * e1) * rho1;
+        for (int le0 = eb; le0 < ee; le0 += BA_EG) {
+            // one group of edges: their records and poses loaded before the
+            // first edge's arithmetic (two memory round trips per group)
+            BAEdgeGroup g;
+            g.load(A, d, cur, le0, ee);
 #pragma unroll
-            for (int r = 0; r < 3; r++) {
-                b[r] += Jp[0][r] * o0 + Jp[1][r] * o1;
+            for (int q = 0; q < BA_EG; q++) {
+                if (!g.act[q]) continue;
+                const int ge = d.e0 + le0 + q;
+                nact++;
+                const double* m = g.m[q];
+                const gfse3::SE3& T = g.T[q];
+                double pc[3], e0, e1;
+                edge_error(m, T, X, pc, e0, e1);
+                const double info = m[2];
+                double rho0, rho1;
+                huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
+                chi += rho0;
+                double Jp[2][3], Jc[2][6];
+                edge_jac(m, T, pc, Jp, Jc, true);
+                const double w = rho1 * info;
+                const double o0 = -(info * e0) * rho1, o1 = -(info * e1) * rho1;
 #pragma unroll
-                for (int c = 0; c < 3; c++) H[3 * r + c] += (Jp[0][r] * w) * Jp[0][c] + (Jp[1][r] * w) * Jp[1][c];
-            }
-            const int col = A.kf_col[d.kf0 + kf];
-            if (col >= 0) {  // Hpl = B^T W A, also the panel Ht[3 i + c][6 col + r]
-                double* hp = A.Hpl + (size_t)ge * 18;
-                double* Ht = A.panel + d.panel0;
+                for (int r = 0; r < 3; r++) {
+                    b[r] += Jp[0][r] * o0 + Jp[1][r] * o1;
 #pragma unroll
-                for (int r = 0; r < 6; r++)
+                    for (int c = 0; c < 3; c++) H[3 * r + c] += (Jp[0][r] * w) * Jp[0][c] + (Jp[1][r] * w) * Jp[1][c];
+                }
+                const int col = g.col[q];
+                if (col >= 0) {  // Hpl = B^T W A, also the panel Ht[3 i + c][6 col + r]
+                    double* hp = A.Hpl + (size_t)ge * 18;
+                    double* Ht = A.panel + d.panel0;
 #pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        const double v = (Jc[0][r] * w) * Jp[0][c] + (Jc[1][r] * w) * Jp[1][c];
-                        hp[3 * r + c] = v;
-                        Ht[(size_t)(3 * i + c) * d.npad + 6 * col + r] = v;
-                    }
+                    for (int r = 0; r < 6; r++)
+#pragma unroll
+                        for (int c = 0; c < 3; c++) {
+                            const double v = (Jc[0][r] * w) * Jp[0][c] + (Jc[1][r] * w) * Jp[1][c];
+                            hp[3 * r + c] = v;
+                            Ht[(size_t)(3 * i + c) * d.npad + 6 * col + r] = v;
+                        }
+                }
             }
         }
         double* Hg = A.Hll + (size_t)gp * 9;
@@ -375,13 +411,36 @@ __global__ __launch_bounds__(BA_PT) void k_ba_poses(BAArena A) {
     for (int k = 0; k < 27; k++) acc[k] = 0.0;
     int cnt = 0;
     const int j0 = A.f_eptr[d.fe0 + a], j1 = A.f_eptr[d.fe0 + a + 1];
-    for (int j = j0 + (int)threadIdx.x; j < j1; j += BA_PT) {
-        const int ge = d.e0 + A.f_elist[d.pl0 + j];
-        if (!A.e_act[ge]) continue;
+    for (int jg = j0 + (int)threadIdx.x; jg < j1; jg += BA_PT * BA_EG) {
+      // this thread's next BA_EG edges (j = jg, jg + BA_PT, ...): every load
+      // of the group issued before the first edge's arithmetic
+      bool use[BA_EG];
+      double mq[BA_EG][8], Xq[BA_EG][3];
+      {
+        int ge[BA_EG], pt[BA_EG];
+#pragma unroll
+        for (int q = 0; q < BA_EG; q++) ge[q] = d.e0 + A.f_elist[d.pl0 + min(jg + q * BA_PT, j1 - 1)];
+#pragma unroll
+        for (int q = 0; q < BA_EG; q++) {
+            const uint8_t a = A.e_act[ge[q]];
+            use[q] = jg + q * BA_PT < j1 && a;
+            pt[q] = A.e_pt[ge[q]];
+#pragma unroll
+            for (int k = 0; k < 8; k++) mq[q][k] = A.e_meas[(size_t)ge[q] * 8 + k];
+        }
+#pragma unroll
+        for (int q = 0; q < BA_EG; q++) {
+            const double* Xp = ptX_at(A, cur, d.pt0 + pt[q]);
+#pragma unroll
+            for (int k = 0; k < 3; k++) Xq[q][k] = Xp[k];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < BA_EG; q++) {
+        if (!use[q]) continue;
         cnt++;
-        const double* m = A.e_meas + (size_t)ge * 8;
-        const double* Xp = ptX_at(A, cur, d.pt0 + A.e_pt[ge]);
-        const double X[3] = {Xp[0], Xp[1], Xp[2]};
+        const double* m = mq[q];
+        const double* X = Xq[q];
         double pc[3], e0, e1;
         edge_error(m, T, X, pc, e0, e1);
         const double info = m[2];
@@ -398,6 +457,7 @@ __global__ __launch_bounds__(BA_PT) void k_ba_poses(BAArena A) {
             for (int c = 0; c <= r; c++) acc[k++] += (Jc[0][r] * w) * Jc[0][c] + (Jc[1][r] * w) * Jc[1][c];
 #pragma unroll
         for (int r = 0; r < 6; r++) acc[21 + r] += Jc[0][r] * o0 + Jc[1][r] * o1;
+      }
     }
 #pragma unroll
     for (int k = 0; k < 27; k++)
@@ -461,8 +521,10 @@ __global__ __launch_bounds__(BA_T) void k_ba_schur_pts(BAArena A) {
     if (!A.e_act[ge]) return;
     const int i = A.e_pt[ge], gp = d.pt0 + i;
     const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
-    bool first = true;
-    for (int le = A.pt_eb[gp]; le < e; le++) first = first && !A.e_act[d.e0 + le];
+    int earlier = 0;  // an active edge of this point before e (independent loads, no early exit)
+#pragma unroll 8
+    for (int le = A.pt_eb[gp]; le < e; le++) earlier |= A.e_act[d.e0 + le];
+    const bool first = !earlier;
     if (col < 0 && !first) return;
     double D[9], Di[9];
     const double* Hg = A.Hll + (size_t)gp * 9;
@@ -954,17 +1016,31 @@ __global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
             const double* b = A.bl + (size_t)gp * 3;
             if (st.chol_ok) {  // cl = b_l + Hpl^T (-x_p), x_l = Dinv cl
                 double cl[3] = {b[0], b[1], b[2]};
-                for (int le = eb; le < ee; le++) {
-                    const int ge = d.e0 + le;
-                    if (!A.e_act[ge]) continue;
-                    const int col = A.kf_col[d.kf0 + A.e_kf[ge]];
-                    if (col < 0) continue;
-                    const double* H = A.Hpl + (size_t)ge * 18;
-                    const double* xa = A.xp + (size_t)(d.f0 + col) * 6;
-                    for (int c = 0; c < 3; c++) {
-                        double t = H[c] * (-xa[0]);
-                        for (int r = 1; r < 6; r++) t += H[3 * r + c] * (-xa[r]);
-                        cl[c] += t;
+                for (int le0 = eb; le0 < ee; le0 += BA_EG) {  // groups of edges, loads first (BAEdgeGroup)
+                    bool use[BA_EG];
+                    int col[BA_EG];
+                    double H[BA_EG][18], xa[BA_EG][6];
+#pragma unroll
+                    for (int q = 0; q < BA_EG; q++) {
+                        const int ge = d.e0 + min(le0 + q, ee - 1);
+                        const uint8_t a = A.e_act[ge];
+                        col[q] = A.kf_col[d.kf0 + A.e_kf[ge]];
+                        use[q] = le0 + q < ee && a && col[q] >= 0;
+#pragma unroll
+                        for (int k = 0; k < 18; k++) H[q][k] = A.Hpl[(size_t)ge * 18 + k];
+                    }
+#pragma unroll
+                    for (int q = 0; q < BA_EG; q++)
+#pragma unroll
+                        for (int k = 0; k < 6; k++) xa[q][k] = A.xp[(size_t)(d.f0 + max(col[q], 0)) * 6 + k];
+#pragma unroll
+                    for (int q = 0; q < BA_EG; q++) {
+                        if (!use[q]) continue;
+                        for (int c = 0; c < 3; c++) {
+                            double t = H[q][c] * (-xa[q][0]);
+                            for (int r = 1; r < 6; r++) t += H[q][3 * r + c] * (-xa[q][r]);
+                            cl[c] += t;
+                        }
                     }
                 }
                 const double* Di = A.Dinv + (size_t)gp * 9;
@@ -979,19 +1055,23 @@ __global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
         Xn[0] = X[0];
         Xn[1] = X[1];
         Xn[2] = X[2];
-        for (int le = eb; le < ee; le++) {  // errors at the trial estimate
-            const int ge = d.e0 + le;
-            if (!A.e_act[ge]) continue;
-            const double* m = A.e_meas + (size_t)ge * 8;
-            const gfse3::SE3 T = load_T(A, nxt, d.kf0 + A.e_kf[ge]);
-            double pc[3], e0, e1;
-            edge_error(m, T, X, pc, e0, e1);
-            A.e_err[(size_t)ge * 2] = e0;
-            A.e_err[(size_t)ge * 2 + 1] = e1;
-            const double info = m[2];
-            double rho0, rho1;
-            huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
-            chi += rho0;
+        for (int le0 = eb; le0 < ee; le0 += BA_EG) {  // errors at the trial estimate
+            BAEdgeGroup g;
+            g.load(A, d, nxt, le0, ee);
+#pragma unroll
+            for (int q = 0; q < BA_EG; q++) {
+                if (!g.act[q]) continue;
+                const int ge = d.e0 + le0 + q;
+                const double* m = g.m[q];
+                double pc[3], e0, e1;
+                edge_error(m, g.T[q], X, pc, e0, e1);
+                A.e_err[(size_t)ge * 2] = e0;
+                A.e_err[(size_t)ge * 2 + 1] = e1;
+                const double info = m[2];
+                double rho0, rho1;
+                huber(e0 * (info * e0) + e1 * (info * e1), rho0, rho1);
+                chi += rho0;
+            }
         }
     }
     const double cs = block_reduce(chi, sh, false);
@@ -1006,6 +1086,7 @@ __global__ __launch_bounds__(BA_T) void k_ba_update(BAArena A) {
 __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
     __shared__ int s_end, s_cnt;
     __shared__ double s_part[3][BA_MAXPTS / BA_T];
+    __shared__ double s_sum[3];
     const int p = blockIdx.x, tid = threadIdx.x;
     const BADesc d = A.desc[p];
     if (A.st[p].round >= 2) return;
@@ -1015,22 +1096,27 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         s_part[2][w] = A.wg_scale[d.wg0 + w];
     }
     __syncthreads();
+    // the three ordered sums on three threads at once (each in workgroup order,
+    // the pose part of the scale first, as one thread summed them before)
+    if (tid < 3) {
+        double c = tid == 2 ? A.st[p].scale_p : 0.0;
+#pragma unroll 8
+        for (int w = 0; w < d.nwg; w++) c += s_part[tid][w];
+        s_sum[tid] = c;
+    }
+    __syncthreads();
     if (tid == 0 && ba_halted(A, A.st[p])) {  // terminate() before this iteration: optimize() returns
         s_end = 1;
         s_cnt = 0;
     } else if (tid == 0) {
         BAState st = A.st[p];
         if (st.q == 0) {  // activeRobustChi2 at the iteration start
-            double c = 0.0;
-            for (int w = 0; w < d.nwg; w++) c += s_part[0][w];
-            st.currentChi = c;
-            st.iniChi = c;
+            st.currentChi = s_sum[0];
+            st.iniChi = s_sum[0];
         }
-        double tempChi = 0.0;
-        for (int w = 0; w < d.nwg; w++) tempChi += s_part[1][w];
+        double tempChi = s_sum[1];
         if (!st.chol_ok) tempChi = DBL_MAX;
-        double scale = st.scale_p;
-        for (int w = 0; w < d.nwg; w++) scale += s_part[2][w];
+        double scale = s_sum[2];
         scale += 1e-3;
         const double rho = (st.currentChi - tempChi) / scale;
         if (rho > 0 && isfinite(tempChi)) {
@@ -1050,7 +1136,10 @@ __global__ __launch_bounds__(1024) void k_ba_decide(BAArena A) {
         if (rho < 0 && st.q < 10 && !(A.stop && *A.stop)) {  // the trial loop also ends on terminate()
             st.need_lin = 0;  // another trial on the same system
         } else {
-            st.iters[st.round]++;
+            if (st.round == 0)  // (fixed indices: a run-time one puts st in scratch memory)
+                st.iters[0]++;
+            else
+                st.iters[1]++;
             bool term = (st.q == 10 || rho == 0) || (A.stop && *A.stop);
             if (!term) {
                 if ((st.iniChi - st.currentChi) * 1e3 < st.iniChi)
