@@ -740,9 +740,13 @@ constexpr int BA_ST = BA_SOLVE_THREADS;
 static_assert(BA_ST >= BA_MAXN && BA_ST % 64 == 0, "k_ba_solve: one thread per panel row");
 
 __device__ __forceinline__ void wave_lds_sync() {
+#ifdef BA_TRSV_NOFENCE  // diagnostic: code-motion barrier only (one wave's LDS operations run in order)
+    __builtin_amdgcn_wave_barrier();
+#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -804,6 +808,9 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     // srinv[j] = 1 / d_j.
     if (tid == 0) s_fail = 0;
     __syncthreads();
+#ifdef BA_CHOL_PHASES  // diagnostic: s_memtime cycles of (diagonal + panel) and (trailing update) summed over the block steps
+    unsigned long long ph_a = 0, ph_b = 0, ph_t = __builtin_amdgcn_s_memtime();
+#endif
     for (int k0 = 0; k0 < n; k0 += 6) {
         const int nrow = n - k0 - 6;  // panel rows below the block
         double Db[6][6], rb[6];
@@ -841,6 +848,9 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
             }
         }
         __syncthreads();
+#ifdef BA_CHOL_PHASES
+        { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph_a += t - ph_t; ph_t = t; }
+#endif
         if (tid == 0) {  // the block's factor (no one reads these rows before the substitutions)
             if (!ok) s_fail = 1;
 #pragma unroll
@@ -882,12 +892,22 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
             }
         }
         __syncthreads();
+#ifdef BA_CHOL_PHASES
+        { const unsigned long long t = __builtin_amdgcn_s_memtime(); ph_b += t - ph_t; ph_t = t; }
+#endif
         if (s_fail) break;
     }
     const bool fail = s_fail;
     __syncthreads();
     BA_STAMP(2);
+#ifdef BA_CHOL_PHASES
+    if (A.tstamp && tid == 0) {
+        A.tstamp[(size_t)p * 8 + 5] = ph_a;
+        A.tstamp[(size_t)p * 8 + 6] = ph_b;
+    }
+#else
     if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 5] = __builtin_amdgcn_s_memtime();
+#endif
     if (!fail && w == 0) {
         // Substitutions on one wave, one pose block at a time: lane l holds
         // rows l, l + 64, l + 128 in registers; a block's 6 values go through
@@ -966,7 +986,9 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     }
     __syncthreads();
     BA_STAMP(3);
+#ifndef BA_CHOL_PHASES
     if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 6] = __builtin_amdgcn_s_memtime();
+#endif
     if (fail) {  // Solver::_x keeps its previous value
         for (int i = tid; i < n; i += BA_ST) sb[i] = A.xp[(size_t)d.f0 * 6 + i];
     } else {
