@@ -740,13 +740,9 @@ constexpr int BA_ST = BA_SOLVE_THREADS;
 static_assert(BA_ST >= BA_MAXN && BA_ST % 64 == 0, "k_ba_solve: one thread per panel row");
 
 __device__ __forceinline__ void wave_lds_sync() {
-#ifdef BA_TRSV_NOFENCE  // diagnostic: code-motion barrier only (one wave's LDS operations run in order)
-    __builtin_amdgcn_wave_barrier();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {

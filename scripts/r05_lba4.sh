@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU box: pipelined trailing-update variant (BA_TRAIL_PF): parity, phase split, timing against the product.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out/lba4
+D=$PWD/gf_orb_slam_amd/diag
+GF_LIB=$D/libgfslam_pf.so timeout -k 10 300 python -u -m pytest tests/test_lba_gpu.py tests/test_dropin_gpu.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/lba4/pf_pytest.log 2>&1 || { tail -5 gpurun_out/lba4/pf_pytest.log; exit 5; }
+tail -1 gpurun_out/lba4/pf_pytest.log
+GF_LIB=$D/libgfslam_pfph.so timeout -k 10 120 python -u scripts/lba_chol_phases.py > gpurun_out/lba4/pfph.log 2>&1 || exit 6
+GF_LIB=$D/libgfslam_chph.so timeout -k 10 120 python -u scripts/lba_chol_phases.py > gpurun_out/lba4/chph.log 2>&1 || exit 7
+grep chol gpurun_out/lba4/pfph.log gpurun_out/lba4/chph.log
+bash scripts/r05_lba.sh lba4b product,pf,product,pf
