@@ -1,3 +1,5 @@
+# (historical: the BA_TRSV_NOFENCE / BA_TRAIL_PF / BA_TRAIL_RL variants this measured were
+# removed from ba.hip after the measurement; results in profiles/r05/lba/)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out/lba3
 GF_LIB=$PWD/gf_orb_slam_amd/diag/libgfslam_chph.so timeout -k 10 120 python -u scripts/lba_chol_phases.py > gpurun_out/lba3/chph.log 2>&1 || exit 5

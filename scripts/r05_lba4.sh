@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the BA_TRSV_NOFENCE / BA_TRAIL_PF / BA_TRAIL_RL variants this measured were
+# removed from ba.hip after the measurement; results in profiles/r05/lba/)
 # GPU box: pipelined trailing-update variant (BA_TRAIL_PF): parity, phase split, timing against the product.
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out/lba4
