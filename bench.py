@@ -454,10 +454,16 @@ def compact_line(out: dict, detail: str) -> str:
     line["config"] = {"workload": "config 2: euroc 752x480, 1000 feats, GF budget 100, full GrabImage step "
                                   "(extract, match, GF select, 2x PoseOptimization) with UpdateReference",
                       "sequences_per_gpu": c.get("sequences_per_gpu"), "stream_groups": c.get("stream_groups"),
+                      "distinct_frames_per_step": c.get("distinct_frames_per_step"),
                       "parallelism": c.get("parallelism")}
+    if out.get("n_gpus", 1) > 1 or out.get("ranks", {}).get("transport") == "host":
+        line["ranks"] = {k: out["ranks"][k] for k in ("world", "communicator_world", "transport", "devices_used",
+                                                      "frames_per_s", "min_frames_per_s", "max_frames_per_s",
+                                                      "max_over_min_ms")}
+        line["startup_checksums_equal"] = out.get("startup", {}).get("checksums_equal_across_ranks")
     line["roofline"] = r
     if cb:
-        line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind")}
+        line["cpu_baseline"] = {k: cb.get(k) for k in ("value", "unit", "cores", "kind", "vs_published")}
         line["cpu_baseline"]["sample"] = cb.get("sample", "")[:200]
         if "all_cores" in cb:
             line["cpu_baseline"]["all_cores"] = {k: cb["all_cores"].get(k) for k in ("value", "cores")}
@@ -617,7 +623,9 @@ def main():
                     help="fraction of map points with a stale (random) descriptor; the defaults (0.82 keyframe map, "
                          "0.93 fixed map) give config 2's regime of SURVEY §8d: ~60 motion-model matches vs GF "
                          "budget 100, runActiveMapMatching every frame (scene.build_map / build_global_map)")
-    ap.add_argument("--scenes", type=int, default=8)
+    ap.add_argument("--scenes", type=int, default=32,
+                    help="rendered rooms (each its own keyframe map); 32 rooms x 32-frame loops give the 1024 "
+                         "sequences of a step 1024 distinct frames")
     ap.add_argument("--period", type=int, default=32, help="frames per loop of the rendered trajectory")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -649,6 +657,15 @@ def main():
                     help="host launch order of a step over the stream groups: each group's whole step in turn "
                          "(step), every group's extraction before any tracking (split, pipeline.step_all), or "
                          "group g's extraction before g - 1's tracking (ring, pipeline.GatedRing)")
+    ap.add_argument("--dist-transport", choices=("rccl", "host"), default="rccl",
+                    help="start-up exchange of --gpus N > 1: RCCL, one GPU per rank (the product path), or "
+                         "host-staged collectives over a gloo group with the ranks sharing the visible GPUs "
+                         "round-robin (a rehearsal of the N-rank bench path on one GPU)")
+    ap.add_argument("--time-log", default=None,
+                    help="file for Tracking::SaveTimeLog's per-frame stage log of stream 0 (default "
+                         "gpurun_out/time_log.txt); the medians over all streams go to the record")
+    ap.add_argument("--time-log-steps", type=int, default=12,
+                    help="steps run with the stage log on after the timed region (0: skip)")
     ap.add_argument("--kernels-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--detail-out", default=None,
                     help="file for the full measurement record (per-kernel tables, legs); the stdout line is the "
@@ -668,6 +685,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    host_tp = args.dist_transport == "host"
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE={world} does not match --gpus {args.gpus}")
     ktab, kqueues, knote = None, None, "HIP events (--kernel-times events)"
@@ -683,9 +701,17 @@ def main():
     import torch
     import torch.distributed as dist
 
+    # the device of this rank: one per rank (RCCL), or shared round-robin by the
+    # host-staged rehearsal of the N-rank path on fewer GPUs
+    ndev = torch.cuda.device_count()
+    local = local % ndev if host_tp else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if host_tp:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    red_dev = "cpu" if host_tp else "cuda"  # tensors of the timing collectives
 
     from gf_orb_slam_amd import scene, synth
     from gf_orb_slam_amd.bow import ORBVocabulary
@@ -709,7 +735,8 @@ def main():
     t_su = time.perf_counter()
     ctx0 = Context(local)
     with _StdoutToStderr():
-        gd = GfDist(ctx0, rank, world)
+        gd = GfDist(ctx0, rank, world, transport=args.dist_transport)
+    gd_world = gd.info()[1]
     scenes, maps, world_ck, world_span, world_bytes = share_world(
         gd, rank, lambda: build_world(cam, B, S, args.period, args.nfeatures, args.map, local, args.stale_desc,
                                       refmap, args.keyframes))
@@ -723,6 +750,9 @@ def main():
     if refmap and not args.no_reloc:
         dbs = [KeyframeDB(m[3], m[4], voc.transform) for m in maps]
     W = scene.Workload(cam, B, n_scenes=S, period=args.period, seed=0, scenes=scenes, phase_offset=3 * rank)
+    # (scene, phase) pairs of one step: with S * period >= B every sequence of
+    # the step tracks a different frame (no group re-reads another's inputs)
+    distinct = len(set(zip(W.scene_of.tolist(), W.phase.tolist())))
     frames = W.render_all(f"cuda:{local}").contiguous()
     T, V = W.boot_state()
     fes = []
@@ -761,7 +791,8 @@ def main():
                                                     np.all(voc_span[0] == voc_span[1]) and
                                                     np.all(map_span[0] == map_span[1])),
                "world_checksum": world_ck, "vocabulary_checksum": voc_ck, "seconds": round(t_su, 2),
-               "transport": "RCCL (gf_dist_bcast / gf_dist_bcast_vocab / gf_dist_bcast_map)"}
+               "transport": ("RCCL" if not host_tp else "host-staged over gloo")
+                            + " (gf_dist_bcast / gf_dist_bcast_vocab / gf_dist_bcast_map)"}
 
     # ---- warm-up
     hist = np.zeros(6, np.int64)
@@ -819,10 +850,17 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    dt_rank = dt
+    tt = torch.tensor([dt], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     dt = float(tt.item())
+    # every rank's own wall time of the timed steps (the straggler shows here)
+    rank_dt = torch.zeros(world, dtype=torch.float64, device=red_dev)
+    rank_dt[rank] = dt_rank
+    if world > 1:
+        dist.all_reduce(rank_dt, op=dist.ReduceOp.SUM)
+    rank_dt = rank_dt.cpu().numpy()
     if args.kernels_child:  # the profiled child ends with the timed region
         print(json.dumps({"kernels_child": True, "ms_per_step": round(dt / args.steps * 1e3, 3)}))
         for fe in fes:
@@ -925,6 +963,13 @@ def main():
                 priced[k].update({"timing": "rocprof", "avg_launch_ms_events": round(ev, 4),
                                   "events_over_rocprof": round(ev / (rp_total(k) / prof[k][1]), 3),
                                   "rocprof_kernels": SCOPE.get(k, [k])})
+            elif k in prof:  # no rocprof dispatch under this scope's names: HIP events, said so
+                ev = prof[k][0]
+                for extra in {"k_active_match": "k_active_match_overflow",
+                              "k_match_lastframe": "k_match_seq_pre"}.get(k, "").split():
+                    ev += prof.get(extra, (0.0, 0))[0]
+                priced[k] = price(k, ev / prof[k][1])
+                priced[k]["timing"] = "hip_events (no rocprof scope)"
     else:
         priced = {k: price(k, prof[k][0] / prof[k][1]) for k in work if k in prof}
         for k in priced:
@@ -961,7 +1006,7 @@ def main():
             priced[k]["peak_note"] = "FP64 peak (AMD spec, vector = matrix on MI355X); this kernel is f64 VALU"
     if rp:
         top = max(rp, key=lambda k: rp[k][0])
-        dom = max(priced, key=rp_total)
+        dom = max(priced, key=rp_total) if priced else None
     else:
         top = max(prof, key=lambda k: prof[k][0])
         dom = max(priced, key=lambda k: prof[k][0])
@@ -983,6 +1028,8 @@ def main():
                 break
         except (OSError, ValueError, KeyError):
             pass
+    if dom is None:
+        raise RuntimeError("no SURVEY §8d kernel was timed in the step (empty kernel table)")
     roof = dict(priced[dom])
     roof["traffic_source"] = traffic_src
     roof["frames_per_launch"] = Bg
@@ -1037,8 +1084,20 @@ def main():
                    "sequences_per_gpu": B, "stream_groups": G, "update_reference": refmap,
                    "extraction_gate": bool(gates), "enqueue": args.enqueue,
                    "tracking_stream_priority": bool(args.track_priority and G > 1),
-                   "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"},
+                   "parallelism": f"{B} sequences x {world} ranks (one process per GPU)"
+                                  if not host_tp else
+                                  f"{B} sequences x {world} ranks on {min(world, ndev)} GPU(s) "
+                                  f"(host-staged rehearsal of the N-rank path)",
+                   "distinct_frames_per_step": distinct},
         "startup": startup,
+        "ranks": {"world": world, "communicator_world": gd_world, "transport": args.dist_transport,
+                  "devices_used": min(world, ndev) if host_tp else world,
+                  "frames_per_s": [round(B * args.steps / float(x), 1) for x in rank_dt],
+                  "ms_per_step": [round(float(x) / args.steps * 1e3, 3) for x in rank_dt],
+                  "min_frames_per_s": round(B * args.steps / float(rank_dt.max()), 1),
+                  "max_frames_per_s": round(B * args.steps / float(rank_dt.min()), 1),
+                  "max_over_min_ms": round(float(rank_dt.max() / rank_dt.min()), 4),
+                  "note": "each rank's own wall time of the timed steps; `value` uses the max over ranks"},
         "host_enqueue": {"ms_per_step": round(t_enq / args.steps * 1e3, 3),
                          "call_ms_avg": [round(float(x) * 1e3, 3) for x in t_call.mean(axis=0)],
                          "call_ms_max": round(float(t_call.max()) * 1e3, 3),
@@ -1154,6 +1213,35 @@ def main():
                              "note": "gf_set_budgets with the reference's budgets (abi.h: each cap's timer where "
                                      "the reference starts it, frame clock after the extraction gate); parity "
                                      "mode (+inf) is the headline"}
+    if args.time_log_steps > 0:
+        # Tracking::SaveTimeLog's per-frame stage log (gf_frontend_set_time_log),
+        # after the timed region: device-clock stage boundaries of every group
+        from gf_orb_slam_amd.pipeline import TIME_LOG_COLUMNS
+        for fe in fes:
+            fe.set_time_log(args.time_log_steps)
+        for _ in range(args.time_log_steps):
+            for fe in fes:
+                fe.step()
+        logs = [fe.time_log() for fe in fes]
+        tl_file = args.time_log or os.path.join(ROOT, "gpurun_out", "time_log.txt")
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(tl_file)), exist_ok=True)
+            fes[0].save_time_log(tl_file, 0)
+        except OSError as e:
+            tl_file = f"(not written: {e})"
+        med = {}
+        for c in TIME_LOG_COLUMNS[1:]:
+            v = np.concatenate([lg[c].reshape(-1) for lg in logs]).astype(np.float64)
+            med[c] = round(float(np.median(v)) * (1e3 if c.startswith("time_") else 1.0), 4)
+        out["time_log"] = {"file": os.path.relpath(tl_file, ROOT) if os.path.isabs(tl_file) else tl_file,
+                           "steps": args.time_log_steps, "streams": B, "median": med,
+                           "unit": "ms (time_*), landmarks (lmk_*)",
+                           "note": "Tracking::SaveTimeLog columns (Tracking.h:254-280) per frame and stream; stage "
+                                   "boundaries on the device clock, shared by the streams of a group (batched "
+                                   "stages), counts per stream; the groups overlap, so a stage's time includes "
+                                   "the other groups' kernels beside it"}
+        for fe in fes:
+            fe.set_time_log(0)
     for fe in fes:
         fe.close()
     if rank == 0 and args.single_stream_steps > 0:
@@ -1220,6 +1308,15 @@ def main():
             "note": "aggregate = this GPU's frames/s; all_cores = every physical core of the job's CPU share, "
                     "pinned; whole_host_linear scales that figure linearly to all %d physical cores of the "
                     "node (an extrapolation, not a measurement)" % phys}
+        # the reference's own published figure (~11-16 ms per
+        # frame on EuRoC, one tracking thread): the speed-ups against it
+        ss = out.get("single_stream", {}).get("fps")
+        out["cpu_baseline"]["vs_published"] = {
+            "published_ms_per_frame": [11.0, 16.0], "published_frames_per_s": [62.5, 90.9],
+            "single_sequence_speedup": [round(ss / 90.9, 1), round(ss / 62.5, 1)] if ss else None,
+            "aggregate_speedup_one_gpu": [round(fps / world / 90.9, 1), round(fps / world / 62.5, 1)],
+            "note": "GPU figures over the reference's published per-frame latency range (read off its plot, "
+                    "hardware not stated); `value` above is this repo's scalar C++ port timed here"}
     if rank == 0:
         detail = args.detail_out or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
         try:

@@ -175,6 +175,8 @@ _PROTOS = {
     "gf_frontend_field": [_P, _I, _P, _P],
     "gf_set_budgets": [_P, _D, _D],
     "gf_frontend_set_test_clock": [_P, _P],
+    "gf_frontend_set_time_log": [_P, _I],
+    "gf_frontend_read_time_log": [_P, _P, _P, _P],
     "gf_dist_unique_id": [_P],
     "gf_dist_init": [_P, _I, _I, _P, _P],
     "gf_dist_destroy": [_P],

@@ -74,12 +74,17 @@ bool lb_barrier(gf_dist_channel* ch) {
 int lb_post(gf_dist* d, void* buf, size_t bytes) {
     // the buffer's producers on this rank's stream finish first (RCCL orders
     // the broadcast after them on the stream)
-    GF_HIP(hipStreamSynchronize(d->ctx->stream));
+    const hipError_t e = hipStreamSynchronize(d->ctx->stream);
     {
         std::lock_guard<std::mutex> lk(d->ch->m);
         d->ch->ptr[d->rank] = buf;
         d->ch->bytes[d->rank] = bytes;
+        if (e != hipSuccess) {  // the other ranks are released at once instead of timing out
+            d->ch->broken = true;
+            d->ch->cv.notify_all();
+        }
     }
+    if (e != hipSuccess) return gf::fail(GF_ERR_HIP, std::string("loopback transport: ") + hipGetErrorString(e));
     if (!lb_barrier(d->ch)) return gf::fail(GF_ERR_HIP, "loopback transport: a rank did not arrive");
     return GF_OK;
 }
@@ -129,10 +134,13 @@ int lb_allreduce(gf_dist* d, double* buf, size_t n, int op) {
 }
 
 int host_call(gf_dist* d, int op, void* buf, size_t bytes, int root, bool send, bool recv) {
-    GF_HIP(hipStreamSynchronize(d->ctx->stream));
+    // a local HIP failure still joins the collective (the peers would
+    // otherwise wait for the callback's own timeout); the error is returned after it
+    hipError_t e = hipStreamSynchronize(d->ctx->stream);
     if (d->host.size() < bytes) d->host.resize(bytes);
-    if (send && bytes) GF_HIP(hipMemcpy(d->host.data(), buf, bytes, hipMemcpyDeviceToHost));
+    if (e == hipSuccess && send && bytes) e = hipMemcpy(d->host.data(), buf, bytes, hipMemcpyDeviceToHost);
     const int r = d->fn(d->user, op, d->host.data(), bytes, root);
+    if (e != hipSuccess) return gf::fail(GF_ERR_HIP, std::string("host-staged transport: ") + hipGetErrorString(e));
     if (r) return gf::fail(GF_ERR_HIP, "host-staged transport: the collective callback returned " + std::to_string(r));
     if (recv && bytes) GF_HIP(hipMemcpy(buf, d->host.data(), bytes, hipMemcpyHostToDevice));
     return GF_OK;

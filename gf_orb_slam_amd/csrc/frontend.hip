@@ -120,6 +120,10 @@ struct FeDev {
     int32_t* nmp_step;     // [B] without keyframe graphs: the map's size when TrackLocalMap runs, else 0
     float* th_m2;          // [B] SearchByProjection(F, local, th): 5 within 2 frames of a relocalisation (:3318-3320)
     int max_frames;        // mMaxFrames
+    // per-frame stage log (gf_frontend_set_time_log; tl_cap 0: off)
+    int tl_cap;
+    long long* tl_stamp;   // [tl_cap][GF_TL_NSITE] device clock at the stage boundaries
+    gf_time_rec* tl_rec;   // [tl_cap][B]
 };
 
 __device__ __forceinline__ long long* ck_rec(const FeDev& D, int b) { return D.clk + (long long)b * D.ck_stride; }
@@ -538,6 +542,40 @@ __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
     }
 }
 
+// Stage log (logCurrentFrame, Tracking.h:254-280): one boundary of this
+// step, in the ring slot of the step counter (advanced by k_fe_end).
+__global__ __launch_bounds__(64) void k_fe_tstamp(FeDev D, int site) {
+    if (threadIdx.x == 0) {
+        const int slot = *D.step % D.tl_cap;
+        long long* st = D.tl_stamp + (long long)slot * GF_TL_NSITE;
+        if (site == GF_TL_BEGIN)
+            for (int k = 1; k < GF_TL_NSITE; k++) st[k] = 0;  // the boundaries this step does not reach read 0
+        st[site] = (long long)now_ticks();
+    }
+}
+
+// After k_fe_end: the step's end stamp and each stream's counts.
+__global__ __launch_bounds__(64) void k_fe_tlog(FeDev D) {
+    const int step = *D.step - 1;  // k_fe_end advanced the counter
+    const int slot = step % D.tl_cap;
+    for (int b = blockIdx.x * 64 + threadIdx.x; b < D.B; b += gridDim.x * 64) {
+        gf_time_rec r;
+        r.frame_time_stamp = D.t_cur[b];
+        r.path = D.track[(size_t)b * GF_TR_N + GF_TR_PATH];
+        r.branch = stat(D, GF_ST_BRANCH)[b];
+        r.found = stat(D, GF_ST_FOUND)[b];
+        r.tpf = stat(D, GF_ST_TPF)[b];
+        r.local = stat(D, GF_ST_LOCAL)[b];
+        r.inliers = stat(D, GF_ST_INL2)[b];
+        r.extra = stat(D, GF_ST_EXTRA)[b];
+        r.track_map = D.gate_tl[b];
+        r.flags = stat(D, GF_ST_FLAGS)[b];
+        r.step = step;
+        D.tl_rec[(long long)slot * D.B + b] = r;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) D.tl_stamp[(long long)slot * GF_TL_NSITE + GF_TL_END] = (long long)now_ticks();
+}
+
 // Bootstrap: the matched frame becomes the last frame (kp2mp as matched).
 __global__ __launch_bounds__(256) void k_fe_boot_end(FeDev D) {
     const int b = blockIdx.x, t = threadIdx.x;
@@ -796,6 +834,8 @@ struct gf_frontend {
     std::vector<int32_t> h_kfc;
     int32_t* d_kfc = nullptr;
     long long* d_syn = nullptr;  // gf_frontend_set_test_clock's (base, slope) pairs
+    int tl_alloc = 0;            // time-log ring entries allocated
+    int tl_first = 0;            // step counter when the log was switched on
     std::vector<std::vector<int32_t>> h_slots;  // per stream: the graph's slots per keyframe
     void* bow_tmp = nullptr;
 };
@@ -853,6 +893,14 @@ int fe_undistort(gf_frontend* fe, hipStream_t s) {
     return gf_undistort_keypoints_dev(fe->ctx, fe->D.B, K, fe->p.dist, fe->D.kps, fe->D.nkp, fe->D.cap, fe->D.kps, s);
 }
 
+// A stage boundary of the per-frame log (gf_frontend_set_time_log), when on.
+int fe_tstamp(gf_frontend* fe, hipStream_t s, int site) {
+    if (!fe->D.tl_cap) return GF_OK;
+    GF_LAUNCH(k_fe_tstamp, 1, 64, 0, s, fe->D, site);
+    GF_HIP(hipGetLastError());
+    return GF_OK;
+}
+
 // The step's first part: the extraction gate, Frame construction (ORB
 // extraction, undistortion).
 int fe_extract(gf_frontend* fe, hipStream_t s) {
@@ -860,6 +908,7 @@ int fe_extract(gf_frontend* fe, hipStream_t s) {
     // the frame's clock starts after the extraction gate: waiting behind the
     // other front ends' extraction is not this frame's time
     if (fe->gate_wait) GF_HIP(hipStreamWaitEvent(s, fe->gate_wait, 0));
+    FE_RC(fe_tstamp(fe, s, GF_TL_BEGIN));
     {
         GF_PROF(fe->ctx, s, "k_fe_begin");
         GF_LAUNCH(k_fe_begin, D.B, 256, 0, s, D);
@@ -868,7 +917,8 @@ int fe_extract(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf_orb_extract_ptrs_dev(fe->ex, D.B, (const uint8_t* const*)D.ptrs, fe->p.width, D.kps, D.desc, D.nkp,
                                   D.cap, s));
     if (fe->gate_done && fe->gate_stage >= 4) GF_HIP(hipEventRecord(fe->gate_done, s));
-    return fe_undistort(fe, s);
+    FE_RC(fe_undistort(fe, s));
+    return fe_tstamp(fe, s, GF_TL_EXTRACTED);
 }
 
 // The step's second part: tracking on the extracted frame.
@@ -897,6 +947,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
     FE_RC(gf::pose_opt_frames_gated(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.gmap, M, fe->inv_sigma2,
                                     fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL1),
                                     col(GF_ST_ITER1), col(GF_ST_EDGES1), col(GF_ST_M3), 20, s));
+    FE_RC(fe_tstamp(fe, s, GF_TL_MOTION));
     // Relocalisation of the LOST streams: ComputeBoW, the keyframe database's
     // candidates, SearchByBoW per candidate (Tracking.cc:3861-3922)
     if (fe->rl_on) {
@@ -910,6 +961,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
     // the motion model's outlier discard and failure test, TrackPreviousFrame,
     // the relocalisation loop, and the gates of the TrackLocalMap stages below
     FE_RC(gf::track_loss(ctx, fe->TL, s));
+    FE_RC(fe_tstamp(fe, s, GF_TL_INIT_POSE));
     const MapArrays WM{D.map, fe->wdesc, fe->mp_pos, D.views, fe->mp_H, fe->mp_info, fe->mp_uv, D.upd};
     // keyframe graphs: H / ObsMat / u_proj stay in map order (the local map's
     // point q is map point lmp[q]); the other per-point arrays are gathered
@@ -925,6 +977,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
                   fe->w_nmp);
         GF_HIP(hipGetLastError());
     }
+    FE_RC(fe_tstamp(fe, s, GF_TL_REF_UPDATED));
     // TrackLocalMap -> SearchReferencePointsInFrustum
     if (D.gf) {
         FE_RC(gf::obs_update_gated(ctx, B, D.t_prev, D.Tcw_last, D.t_cur, D.Tcw, fe->Xv, nullptr, D.gate_fi, s));
@@ -961,11 +1014,13 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
         GF_LAUNCH(k_fe_decide, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
+    FE_RC(fe_tstamp(fe, s, GF_TL_FRUSTUM));
     if (D.gf) {
         FE_RC(gf::obs_map_info(ctx, &fe->ocam, B, fe->Xv, fe->mp_pos, D.m_active, M, 0, D.views, D.upd, 1, fe->mp_H,
                                fe->mp_info, fe->mp_uv, fe->mp_updated, rmp, s,
                                mclk ? clock(D.t_mat0, GF_CK_OFF_MI(M, R), GF_CK_SITE_MI) : gf::StageClock{}, D.cap2_mi,
                                fe->mp_info_lt));
+        FE_RC(fe_tstamp(fe, s, GF_TL_MAT_ONLINE));
         gf::ActiveClock ac;
         if (mclk) {
             ac.mat_t0 = D.t_mat0;
@@ -981,9 +1036,11 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
                                    fe->mp_info, fe->mp_H, D.m_active, M, fe->base, fe->level_sigma2,
                                    col(GF_ST_TO_MATCH), 1.f, 0.8f, (gf_rng*)fe->field_ptr[GF_FE_RNG], D.kp2mp, D.score,
                                    D.left, D.nleft, col(GF_ST_LOCAL), col(GF_ST_LDETS), rmp, s, ac, fe->mp_info_lt));
+        FE_RC(fe_tstamp(fe, s, GF_TL_SELECTED));
     }
     FE_RC(gf::match_project_th(ctx, fi, B, D.kps, D.desc, D.nkp, cap, D.views, fe->wdesc, D.m_m2, M, D.th_m2, 0.8f,
                                D.kp2mp, D.score, D.nm2, s));
+    FE_RC(fe_tstamp(fe, s, GF_TL_SEARCHED));
     FE_RC(gf::pose_opt_frames_gated(ctx, B, D.Tcw, D.kps, D.nkp, cap, D.kp2mp, D.map, M, fe->inv_sigma2,
                                     fe->p.nlevels, fi->fx, fi->fy, fi->cx, fi->cy, D.outl, col(GF_ST_INL2),
                                     col(GF_ST_ITER2), col(GF_ST_EDGES2), D.gate_tl, 1, s));
@@ -992,6 +1049,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
         GF_LAUNCH(k_fe_post, B, 256, 0, s, D);
         GF_HIP(hipGetLastError());
     }
+    FE_RC(fe_tstamp(fe, s, GF_TL_OPTIMISED));
     if (D.gf) {
         // predictPWLSVec(dt, 2) + RunMapPointsSelection (MAP_INFO_MATRIX at kinematic[1], check_viz);
         // in a captured step a branch of its own beside SearchAdditionalMatchesInFrame
@@ -1037,6 +1095,10 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
     {
         GF_PROF(ctx, s, "k_fe_end");
         GF_LAUNCH(k_fe_end, B, 256, 0, s, D);
+        GF_HIP(hipGetLastError());
+    }
+    if (D.tl_cap) {
+        GF_LAUNCH(k_fe_tlog, (B + 63) / 64, 64, 0, s, D);
         GF_HIP(hipGetLastError());
     }
     if (fe->ts) {  // join: the context's stream sees the whole step
@@ -1883,6 +1945,51 @@ int gf_frontend_set_test_clock(gf_frontend* fe, const long long* base_slope) {
     }
     GF_HIP(hipMemcpy(fe->d_syn, base_slope, sizeof(long long) * 2 * GF_CK_NSITE, hipMemcpyHostToDevice));
     fe->D.syn = fe->d_syn;
+    return GF_OK;
+}
+
+int gf_frontend_set_time_log(gf_frontend* fe, int steps) {
+    GF_CHECK(fe && steps >= 0, GF_ERR_ARG, "bad arg");
+    GF_CHECK(!fe->exec, GF_ERR_ARG, "set the time log before capturing a graph");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    if (steps > fe->tl_alloc) {
+        void *a, *b;
+        FE_RC(fe_alloc(fe, sizeof(long long) * GF_TL_NSITE * (size_t)steps, &a));
+        FE_RC(fe_alloc(fe, sizeof(gf_time_rec) * (size_t)fe->D.B * steps, &b));
+        fe->D.tl_stamp = (long long*)a;
+        fe->D.tl_rec = (gf_time_rec*)b;
+        fe->tl_alloc = steps;
+    } else if (steps) {
+        GF_HIP(hipMemset(fe->D.tl_stamp, 0, sizeof(long long) * GF_TL_NSITE * (size_t)steps));
+        GF_HIP(hipMemset(fe->D.tl_rec, 0, sizeof(gf_time_rec) * (size_t)fe->D.B * steps));
+    }
+    fe->D.tl_cap = steps;
+    int32_t st = 0;
+    GF_HIP(hipMemcpy(&st, fe->D.step, sizeof(int32_t), hipMemcpyDeviceToHost));
+    fe->tl_first = st;  // the first step the log holds
+    return GF_OK;
+}
+
+int gf_frontend_read_time_log(gf_frontend* fe, long long* stamps, gf_time_rec* recs, int* nsteps) {
+    GF_CHECK(fe && stamps && recs && nsteps, GF_ERR_ARG, "null arg");
+    GF_CHECK(fe->D.tl_cap > 0, GF_ERR_ARG, "the time log is off (gf_frontend_set_time_log)");
+    GF_HIP(hipSetDevice(fe->ctx->device));
+    GF_HIP(hipStreamSynchronize(fe->ctx->stream));
+    int32_t st = 0;
+    GF_HIP(hipMemcpy(&st, fe->D.step, sizeof(int32_t), hipMemcpyDeviceToHost));
+    const int cap = fe->D.tl_cap, B = fe->D.B;
+    const int n = std::min(cap, std::max(0, st - fe->tl_first));
+    std::vector<long long> hs((size_t)cap * GF_TL_NSITE);
+    std::vector<gf_time_rec> hr((size_t)cap * B);
+    GF_HIP(hipMemcpy(hs.data(), fe->D.tl_stamp, sizeof(long long) * hs.size(), hipMemcpyDeviceToHost));
+    GF_HIP(hipMemcpy(hr.data(), fe->D.tl_rec, sizeof(gf_time_rec) * hr.size(), hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; k++) {  // oldest first
+        const int slot = (st - n + k) % cap;
+        memcpy(stamps + (size_t)k * GF_TL_NSITE, hs.data() + (size_t)slot * GF_TL_NSITE, sizeof(long long) * GF_TL_NSITE);
+        memcpy(recs + (size_t)k * B, hr.data() + (size_t)slot * B, sizeof(gf_time_rec) * B);
+    }
+    *nsteps = n;
     return GF_OK;
 }
 

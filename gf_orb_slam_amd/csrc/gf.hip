@@ -604,6 +604,23 @@ __device__ unsigned long long g_am_stamp[8];
 #ifdef GF_AM_GUARD
 __device__ unsigned long long g_am_guard[2];  // [0] corrupted sentinel dwords, [1] frames checked
 #endif
+#ifdef GF_AM_CHECK
+// diagnostic build: [0] commits whose batch-restart RNG history differs from
+// the step-by-step one, [1] out-of-range slot indices at the commit, [2]
+// out-of-range claimed keypoints, [3] sigma^2 copies that differ, [4] commits
+// checked, [8..15] the first RNG mismatch (frame, round, T, nb, b, sz, npop,
+// pass), [16..47] its fast history lanes, [48..79] its step-by-step lanes
+__device__ unsigned long long g_am_check[80];
+#endif
+#ifdef GF_AM_TRACE
+// diagnostic build: one 48-word record per commit of frames 0..7: round, T,
+// nused, nc, nb, used, top, N, oct_b, sigma^2 bits, the round's start
+// history lanes 0..30 would follow at the next record; here the committed
+// history rs (lanes 0..30) at words 16..46
+constexpr int AMT_REC = 48, AMT_MAX = 2048;
+__device__ uint32_t g_am_trace[8][AMT_MAX][AMT_REC];
+__device__ uint32_t g_am_tcnt[8];
+#endif
 
 // Per-round candidate list: the draws of the sequential loop in order (the
 // initial random subset, then one replacement per failed top), produced 64
@@ -611,11 +628,15 @@ __device__ unsigned long long g_am_guard[2];  // [0] corrupted sentinel dwords, 
 // The active matcher is one wave per workgroup: its LDS hand-offs need the
 // wave's LDS operations done and ordered, not a workgroup barrier, whose
 // release fence also waits for the wave's outstanding global stores.
+#ifdef AM_SYNC_BAR  // diagnostic: workgroup barriers instead of the wave-scope hand-offs
+__device__ __forceinline__ void am_sync() { __syncthreads(); }
+#else
 __device__ __forceinline__ void am_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+#endif
 
 struct Cands {
     int16_t* slot;   // pool slot drawn
@@ -1036,6 +1057,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
+#ifdef AM_LSIG  // diagnostic: the level sigma^2 from an LDS copy at the commit
+    __shared__ float s_sig2[16];
+#endif
 #if AM_SLOTS
     __shared__ __align__(16) double s_lsc[64];  // slot_loop: live scores, lane order (-inf past sz)
     __shared__ __align__(16) double s_xsc[64];  // slot_loop: the window's scores (-inf past W)
@@ -1081,6 +1105,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     const int* cell_start = A.grid_cs + (long long)f * (NCELLS + 1);
     const int* items = A.grid_items + (long long)f * A.kp_cap;
     for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
+#ifdef AM_LSIG
+    if (lane < 16) s_sig2[lane] = A.sigma2[lane];
+#endif
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
     // a slot's info / H row: staged at the pool build, or read through the remap
     auto row_of = [&](int sl) -> long long {
@@ -1137,6 +1164,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         return;
     }
     const Pool P{pbits, ppre};
+#ifdef GF_AM_CHECK
+    const int N0 = N;
+#endif
     const int sbits = bits_for(N);  // pool slots are < N (they never move)
     {
         const int lo = lane * 64;
@@ -1720,6 +1750,18 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         const int nused = sz + npop;  // draws that happened
         nld += nused;
         const int T = exh ? exh_at : C.tries[nused - 1];
+#ifdef GF_AM_CHECK
+        {
+            int bad = 0;
+            for (int c = nused + lane; c < nc; c += AW) bad += C.slot[c] < 0 || C.slot[c] >= N0;
+            for (int c = lane; c < nused; c += AW) bad += C.slot[c] < 0 || C.slot[c] >= N0;
+            if (lane == 0 && N != ppre[64]) atomicAdd(&g_am_check[5], 1ull);
+            bad = gfd::warp_sum(bad);
+            if (lane == 0 && bad) atomicAdd(&g_am_check[1], (unsigned long long)bad);
+            if (lane == 0 && !exh && (C.match[top] < 0 || C.match[top] >= n)) atomicAdd(&g_am_check[2], 1ull);
+        }
+        const uint32_t rs_prev = rs;
+#endif
         for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
         used += T;
         if (T > 0 && (T - 1) / 64 >= nb - 2) {  // the batch holding call T is one of the last two
@@ -1728,6 +1770,61 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         } else {
             for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
         }
+#ifdef GF_AM_CHECK
+        {
+            uint32_t rsl = rs_prev;
+            for (int t = T; t > 0; t -= 64) rsl = rng_advance(rsl, rng_word(rsl, rcoef), min(t, 64));
+            const unsigned long long bad = __ballot(lane < 31 && rsl != rs);
+            unsigned long long k = 0;
+            if (lane == 0) {
+                atomicAdd(&g_am_check[4], 1ull);
+                if (bad) k = atomicAdd(&g_am_check[0], 1ull);
+            }
+            k = __shfl(k, 0, 64);
+            if (bad && k == 0) {
+                if (lane < 32) {
+                    g_am_check[16 + lane] = rs;
+                    g_am_check[48 + lane] = rsl;
+                }
+                if (lane == 0) {
+                    g_am_check[8] = f;
+                    g_am_check[9] = round;
+                    g_am_check[10] = T;
+                    g_am_check[11] = nb;
+                    g_am_check[12] = T > 0 ? (T - 1) / 64 : -1;
+                    g_am_check[13] = sz;
+                    g_am_check[14] = npop;
+                    g_am_check[15] = A.pass;
+                }
+            }
+        }
+#endif
+#ifdef GF_AM_TRACE
+        if (f < 8) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&g_am_tcnt[f], 1u);
+            k = __shfl(k, 0, 64);
+            if (k < AMT_MAX) {
+                uint32_t* r = g_am_trace[f][k];
+                if (lane < 31) r[16 + lane] = rs;
+                if (lane == 0) {
+                    r[0] = round;
+                    r[1] = T;
+                    r[2] = nused;
+                    r[3] = nc;
+                    r[4] = nb;
+                    r[5] = used;
+                    r[6] = exh ? 0xffffffffu : (uint32_t)top;
+                    r[7] = N;
+                    r[8] = oct_b;
+                    r[9] = exh ? 0u : (uint32_t)C.match[top];
+                    r[10] = A.pass;
+                    r[11] = npop;
+                    r[12] = sz;
+                }
+            }
+        }
+#endif
         am_sync();
         if (exh) break;
         AM_T(5);
@@ -1739,7 +1836,14 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             A.score[(long long)f * A.kp_cap + b] = C.dist[top];
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
+#ifdef AM_LSIG
+            const double s2 = sqrt((double)s_sig2[oct_b]);
+#ifdef GF_AM_CHECK
+            if (s_sig2[oct_b] != A.sigma2[oct_b]) atomicAdd(&g_am_check[3], 1ull);
+#endif
+#else
             const double s2 = sqrt((double)A.sigma2[oct_b]);
+#endif
             const double w = s2 / (s2 * s2);
             const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
@@ -2691,6 +2795,18 @@ int gf_obs_accumulate_matched_dev(gf_ctx* ctx, int nframes, const int32_t* d_kp2
 #ifdef GF_AM_GUARD
 extern "C" int gf_debug_am_guard(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_guard), sizeof(unsigned long long) * 2) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef GF_AM_TRACE
+extern "C" int gf_debug_am_trace(uint32_t* out, uint32_t* cnt) {
+    if (hipMemcpyFromSymbol(cnt, HIP_SYMBOL(g_am_tcnt), sizeof(uint32_t) * 8) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_trace), sizeof(uint32_t) * 8 * AMT_MAX * AMT_REC) == hipSuccess
+               ? 0 : -1;
+}
+#endif
+#ifdef GF_AM_CHECK
+extern "C" int gf_debug_am_check(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_check), sizeof(unsigned long long) * 80) == hipSuccess ? 0 : -1;
 }
 #endif
 #ifdef GF_AM_STAMP

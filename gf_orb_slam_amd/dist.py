@@ -110,6 +110,12 @@ class GfDist:
         check(lib().gf_dist_init(ctx.handle, rank, world, uid.ctypes.data_as(ctypes.c_void_p),
                                  ctypes.byref(self.handle)))
 
+    def info(self) -> tuple[int, int]:
+        """(rank, world) as the communicator holds them (gf_dist_info)."""
+        r, w = ctypes.c_int(), ctypes.c_int()
+        check(lib().gf_dist_info(self.handle, ctypes.byref(r), ctypes.byref(w)))
+        return r.value, w.value
+
     def transport_kind(self) -> int:
         k = ctypes.c_int()
         check(lib().gf_dist_transport(self.handle, ctypes.byref(k)))

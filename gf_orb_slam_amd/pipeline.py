@@ -79,6 +79,66 @@ PATHS = {0: "motion model", 1: "previous frame after the motion model", 2: "prev
 
 NSTAT = len(STATS)
 
+# per-frame stage log (abi.h GF_TL_*, gf_time_rec): device-clock boundaries of a step
+TL_SITES = ["begin", "extracted", "motion", "init_pose", "ref_updated", "frustum", "mat_online", "selected",
+            "searched", "optimised", "end"]
+TL_NSITE = 12
+TIME_REC_DTYPE = np.dtype([("frame_time_stamp", np.float64), ("path", np.int32), ("branch", np.int32),
+                           ("found", np.int32), ("tpf", np.int32), ("local", np.int32), ("inliers", np.int32),
+                           ("extra", np.int32), ("track_map", np.int32), ("flags", np.int32), ("step", np.int32)])
+# Tracking::SaveTimeLog's columns (Tracking.h:254-280), in its order
+TIME_LOG_COLUMNS = ["frame_time_stamp", "time_ORB_extraction", "time_track_motion", "time_track_frame",
+                    "time_track_map", "time_match", "time_select", "time_optim", "time_mat_pred", "time_mat_online",
+                    "lmk_num_refTrack", "lmk_num_refInlier", "lmk_num_initTrack", "lmk_num_BA"]
+TICK_S = 1e-8  # s_memrealtime: 100 MHz
+
+
+def time_log_columns(stamps: np.ndarray, recs: np.ndarray) -> dict:
+    """logCurrentFrame per step and stream from the device log: stamps
+    [n][TL_NSITE] ticks, recs [n][B] TIME_REC_DTYPE -> {column: [n][B]}.
+    Where the reference's timers sit (Tracking.cc): extraction :528;
+    TrackWithMotionModel / TrackPreviousFrame :605-615 (a motion-model
+    failure logs both); TrackLocalMap :672 (UpdateReference through the
+    statistics); time_match = UpdateReference + SearchReferencePointsInFrustum
+    (:2813); time_optim = PoseOptimization + statistics (:2814);
+    time_mat_online = MAP_INFO_MATRIX (:3339); time_select =
+    runActiveMapMatching (the GF selection; the reference's TrackLocalMap at
+    :2745 leaves it 0, its variants at :2219 / :2705 time the selection
+    there); time_mat_pred = from the motion update to the end of the step
+    (:791, :913: PWLS prediction, RunMapPointsSelection,
+    SearchAdditionalMatchesInFrame). Landmark counts: initTrack = the
+    initial estimate's nmatches (:1635 / :1378, :1400), refTrack =
+    SearchReferencePointsInFrustum's nMatched + nMatchesFound (:3409, :2808),
+    refInlier = mnMatchesInliers, BA = refTrack + the additional matches
+    (:3143). A boundary a stage did not reach reads 0."""
+    st = stamps.astype(np.float64)
+    n, B = recs.shape
+    T = {k: st[:, i][:, None] * np.ones((1, B)) for i, k in enumerate(TL_SITES)}
+
+    def dur(a, b):
+        return np.where((T[a] > 0) & (T[b] > 0), (T[b] - T[a]) * TICK_S, 0.0)
+
+    path, br, tm = recs["path"], recs["branch"], recs["track_map"] != 0
+    motion = (path == 0) | (path == 1)
+    prev = (path == 1) | (path == 2)
+    out = {"frame_time_stamp": recs["frame_time_stamp"].copy(),
+           "time_ORB_extraction": dur("begin", "extracted"),
+           "time_track_motion": np.where(motion, dur("extracted", "motion"), 0.0),
+           "time_track_frame": np.where(prev, dur("motion", "init_pose"), 0.0),
+           "time_track_map": np.where(tm, dur("init_pose", "optimised"), 0.0),
+           "time_match": np.where(tm, dur("init_pose", "searched"), 0.0),
+           "time_select": np.where(tm & (br == 3), dur("mat_online", "selected"), 0.0),
+           "time_optim": np.where(tm, dur("searched", "optimised"), 0.0),
+           "time_mat_pred": dur("optimised", "end"),
+           "time_mat_online": np.where(tm & (br == 3), dur("frustum", "mat_online"), 0.0)}
+    ref = np.where(tm, recs["found"] + recs["local"], 0)
+    out["lmk_num_refTrack"] = ref
+    out["lmk_num_refInlier"] = np.where(tm, recs["inliers"], 0)
+    out["lmk_num_initTrack"] = np.where(path == 0, recs["found"], np.where(prev, recs["tpf"], 0))
+    out["lmk_num_BA"] = np.where(tm, ref + recs["extra"], 0)
+    return out
+
+
 # GF_FE_CLOCK layout (abi.h GF_CK_*): header words, then per-stage elapsed-time
 # arrays; M = map capacity, R = max(gf_budget, 1)
 CK = {"flags": 0, "match": 1, "select": 2, "viz_cut": 3, "viz_time": 4, "mat_online": 5, "am_cut": 6, "sofar": 7,
@@ -337,6 +397,32 @@ class FrontEnd:
         for name, (base, slope) in sites.items():
             a[CK_SITES.index(name)] = (base, slope)
         check(lib().gf_frontend_set_test_clock(self.handle, ptr(a)))
+
+    def set_time_log(self, steps: int) -> None:
+        """gf_frontend_set_time_log: keep the last `steps` steps' stage log (0: off)."""
+        check(lib().gf_frontend_set_time_log(self.handle, int(steps)))
+
+    def time_log(self) -> dict:
+        """The logged steps, oldest first: {"stamps": [n][TL_NSITE] ticks,
+        "recs": [n][B] TIME_REC_DTYPE, column: [n][B] for TIME_LOG_COLUMNS}."""
+        cap = 4096
+        st = np.zeros((cap, TL_NSITE), np.int64)
+        rc = np.zeros((cap, self.B), TIME_REC_DTYPE)
+        n = ctypes.c_int()
+        check(lib().gf_frontend_read_time_log(self.handle, ptr(st), ptr(rc), ctypes.byref(n)))
+        st, rc = st[:n.value], rc[:n.value]
+        return {"stamps": st, "recs": rc, **time_log_columns(st, rc)}
+
+    def save_time_log(self, filename: str, stream: int = 0) -> None:
+        """Tracking::SaveTimeLog's file for one stream (Tracking.h:251-277)."""
+        log = self.time_log()
+        with open(filename, "w") as fh:
+            fh.write("#frame_time_stamp time_ORB_extraction time_track_motion time_track_frame time_track_map "
+                     "time_match ...\n")
+            for k in range(len(log["recs"])):
+                f = [f"{log[c][k, stream]:.6f}" for c in TIME_LOG_COLUMNS[:10]]
+                f += [f"{int(log[c][k, stream]):d}" for c in TIME_LOG_COLUMNS[10:]]
+                fh.write(" ".join(f) + "\n")
 
     # ------------------------------------------------------------ state
     def read(self, name: str) -> np.ndarray:

@@ -66,7 +66,7 @@ int gf_prof_report(gf_ctx* ctx, int idx, char* name, int name_cap, double* total
  * scoreType, fastTh) and operator()(image, mask=empty, keypoints, descriptors).
  * The geometry (width x height) is fixed at creation: the pyramid, cell grids
  * and per-level quotas are planned once. score_type: FAST_SCORE (1) or HARRIS_SCORE (0);
- * HARRIS_SCORE (0) returns GF_ERR_UNSUPPORTED. max_batch bounds nframes of the
+ * any other value returns GF_ERR_ARG. max_batch bounds nframes of the
  * batched device call. */
 int gf_extractor_create(gf_ctx* ctx, int nfeatures, float scale_factor, int nlevels,
                         int score_type, int fast_th, int width, int height, int max_batch,
@@ -1238,6 +1238,49 @@ enum {
     GF_CK_NSITE
 };
 int gf_frontend_set_test_clock(gf_frontend* fe, const long long* base_slope);
+
+/* Per-frame stage log: Tracking::logCurrentFrame / SaveTimeLog
+ * (Tracking.h:254-280, filled at Tracking.cc:528, 605-615, 672, 913,
+ * 2808-2814, 3143, 3339). With a log of `steps` entries on, each step
+ * records the device real-time clock (s_memrealtime, 100 MHz) at its stage
+ * boundaries (one 1-thread launch per boundary on the step's stream) and,
+ * per stream, the counts the reference's landmark columns are made of; the
+ * last `steps` steps are kept in a ring. The stages are batched: a boundary
+ * is where the whole batch crossed it, so a column is the batch's time in
+ * that stage, which every stream of the batch shares. Off (steps = 0) by
+ * default: the step then launches nothing for it. Not while a captured graph
+ * exists (capture again after changing it). */
+enum {
+    GF_TL_BEGIN = 0,     /* the frame's start, after the extraction gate         */
+    GF_TL_EXTRACTED,     /* ORB extraction (+ undistortion) done                 */
+    GF_TL_MOTION,        /* TrackWithMotionModel: SearchByProjection(Cur, Last) + PoseOptimization */
+    GF_TL_INIT_POSE,     /* + TrackPreviousFrame / Relocalisation, outlier discard */
+    GF_TL_REF_UPDATED,   /* TrackLocalMap: UpdateReference                       */
+    GF_TL_FRUSTUM,       /* SearchReferencePointsInFrustum: FRAME_INFO, isInFrustum */
+    GF_TL_MAT_ONLINE,    /* MAP_INFO_MATRIX (runMatrixBuilding, time_Mat_Online) */
+    GF_TL_SELECTED,      /* runActiveMapMatching                                 */
+    GF_TL_SEARCHED,      /* SearchByProjection(F, local) (end of SearchReferencePointsInFrustum) */
+    GF_TL_OPTIMISED,     /* PoseOptimization + statistics (end of TrackLocalMap)  */
+    GF_TL_END,           /* motion update, PWLS prediction, RunMapPointsSelection, SearchAdditionalMatchesInFrame, mLastFrame */
+    GF_TL_NSITE = 12
+};
+typedef struct gf_time_rec {
+    double frame_time_stamp; /* mCurrentFrame.mTimeStamp                          */
+    int32_t path;            /* GF_TR_PATH of the step                             */
+    int32_t branch;          /* GF_ST_BRANCH                                       */
+    int32_t found;           /* GF_ST_FOUND: TrackWithMotionModel's nmatches        */
+    int32_t tpf;             /* GF_ST_TPF: TrackPreviousFrame's nmatches            */
+    int32_t local;           /* GF_ST_LOCAL                                        */
+    int32_t inliers;         /* GF_ST_INL2: mnMatchesInliers                       */
+    int32_t extra;           /* GF_ST_EXTRA                                        */
+    int32_t track_map;       /* 1: TrackLocalMap ran                               */
+    int32_t flags;           /* GF_ST_FLAGS                                        */
+    int32_t step;            /* the front end's step counter of the record         */
+} gf_time_rec;
+int gf_frontend_set_time_log(gf_frontend* fe, int steps);
+/* The ring in step order, oldest first: stamps [n][GF_TL_NSITE] i64 ticks
+ * (0: not reached), recs [n][B]; n (<= steps) returned in *nsteps. */
+int gf_frontend_read_time_log(gf_frontend* fe, long long* stamps, gf_time_rec* recs, int* nsteps);
 
 /* ------------------------------------------------ multi-GPU start-up exchange
  * Config 5: one process per GPU, sequences independent,

@@ -606,3 +606,64 @@ def test_oracle_chain_tracks_sequence():
         assert st["inl2"] >= 50 and st["flags"] == 0
         err = np.abs(ch.read("Tcw").reshape(4, 4) - W.gt_pose(0, k)).max()
         assert err < 0.02, err
+
+
+@pytest.mark.gpu
+def test_time_log_columns():
+    """gf_frontend_set_time_log: Tracking::SaveTimeLog's columns
+    (Tracking.h:254-280) for 12 steps of config 2 with active matching on
+    every frame: device-clock stage boundaries in order within a step and
+    from step to step, durations that add up, the landmark counts taken from
+    the step's own statistics, and the reference's text format. The log does
+    not change the tracking: the same steps without it give the same state."""
+    from gf_orb_slam_amd.pipeline import TIME_LOG_COLUMNS, TL_SITES
+
+    camera, nfeat, B, nmap, budget, gf, stale = CASES["config2_gf"][:7]
+    W, frames, maps, fe, T, V = _setup(camera, nfeat, B, nmap, budget, gf, stale=stale)
+    W2, _, _, fe2, _, _ = _setup(camera, nfeat, B, nmap, budget, gf, stale=stale)
+    fe.set_time_log(16)
+    nsteps = 12
+    stats = []
+    for _ in range(nsteps):
+        fe.step()
+        fe2.step()
+        stats.append(fe.read("stats").copy())
+    log = fe.time_log()
+    for c in TIME_LOG_COLUMNS:
+        assert c in log and log[c].shape == (nsteps, B), c
+    st = log["stamps"][:, :len(TL_SITES)]
+    assert np.all(st > 0), "every boundary of a GF step is reached"
+    assert np.all(np.diff(st, axis=1) >= 0), "boundaries in stage order"
+    assert np.all(st[1:, 0] >= st[:-1, -1]), "a step starts after the previous one ended"
+    assert np.array_equal(log["recs"]["step"][:, 0], np.arange(log["recs"]["step"][0, 0],
+                                                               log["recs"]["step"][0, 0] + nsteps))
+    ts = log["frame_time_stamp"]
+    assert np.all(np.diff(ts, axis=0) > 0), "frame time stamps increase"
+    total = (st[:, -1] - st[:, 0]) * 1e-8
+    parts = (log["time_ORB_extraction"] + log["time_track_motion"] + log["time_track_frame"]
+             + log["time_track_map"] + log["time_mat_pred"])
+    assert np.all(parts <= total[:, None] + 1e-9)
+    assert np.all(log["time_match"] + log["time_optim"] <= log["time_track_map"] + 1e-9)
+    assert np.all(log["time_ORB_extraction"] > 0) and np.all(log["time_track_map"] > 0)
+    idx = {k: i for i, k in enumerate(STATS)}
+    for k in range(nsteps):
+        s = stats[k]
+        assert np.array_equal(log["lmk_num_refInlier"][k], s[idx["inl2"]])
+        assert np.array_equal(log["lmk_num_initTrack"][k], s[idx["found"]])
+        assert np.array_equal(log["lmk_num_refTrack"][k], s[idx["found"]] + s[idx["local"]])
+        assert np.array_equal(log["lmk_num_BA"][k], s[idx["found"]] + s[idx["local"]] + s[idx["extra"]])
+        am = s[idx["branch"]] == 3
+        assert np.all(log["time_select"][k][am] > 0) and np.all(log["time_select"][k][~am] == 0)
+    import os
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, "time_log.txt")
+        fe.save_time_log(fn, 1)
+        lines = open(fn).read().splitlines()
+    assert lines[0].startswith("#frame_time_stamp time_ORB_extraction") and len(lines) == nsteps + 1
+    assert all(len(ln.split()) == len(TIME_LOG_COLUMNS) for ln in lines[1:])
+    for k in ("kp2mp", "rng", "Tcw", "stats"):
+        assert np.array_equal(fe.read(k), fe2.read(k)), f"{k} differs with the time log on"
+    fe.close()
+    fe2.close()
