@@ -44,6 +44,14 @@ struct gf_vocab {
 namespace {
 
 constexpr int BOW_MAX = 4096;
+// dynamic LDS of k_bow_build (bitonic keys and values over pow2(cap)) and
+// k_match_bow (per b-side feature: common node pair, match record, claim, bin)
+static size_t bow_build_lds(int cap) {
+    size_t p2 = 1;
+    while ((int)p2 < cap) p2 <<= 1;
+    return 24 * p2;
+}
+static size_t match_bow_lds(int bcap) { return (8 + 4 + 1 + 1) * (size_t)bcap + 16; }
 
 struct VocabDev {
     const uint8_t* desc;
@@ -143,8 +151,16 @@ __global__ __launch_bounds__(256) void k_bow_build(VocabDev V, int nframes, cons
                                                    int32_t* __restrict__ fv_nodes, int32_t* __restrict__ fv_start,
                                                    int32_t* __restrict__ fv_feats, int32_t* __restrict__ nfv,
                                                    const int32_t* __restrict__ gate) {
-    __shared__ unsigned long long kw[BOW_MAX], kn[BOW_MAX];
-    __shared__ double vals[BOW_MAX];
+    // sized by the launch to the next power of two of cap (bitonic length):
+    // kw, kn (8 B), vals (8 B) per entry. A BOW_MAX-sized static array held
+    // 96 KB per workgroup, so the launch waited for nearly empty CUs beside
+    // the other front ends' extraction even when no stream relocalised
+    extern __shared__ __align__(16) unsigned long long bow_lds[];
+    int p2 = 1;
+    while (p2 < cap) p2 <<= 1;
+    unsigned long long* kw = bow_lds;
+    unsigned long long* kn = kw + p2;
+    double* vals = reinterpret_cast<double*>(kn + p2);
     __shared__ int tmp[4], s_m;
     __shared__ double s_norm;
     const int tid = threadIdx.x;
@@ -299,11 +315,16 @@ __device__ __forceinline__ void top2_merge(int& d1, int& p1, int& d2, int od1, i
 }
 
 __global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ pairs, int npairs, int mode,
-                                                   float nnratio, int check_ori, int32_t* __restrict__ nmatches) {
-    __shared__ uint8_t claimed[BOW_MAX];
-    __shared__ int2 common[BOW_MAX];
-    __shared__ int rec[BOW_MAX];
-    __shared__ uint8_t rbin[BOW_MAX];
+                                                   float nnratio, int check_ori, int32_t* __restrict__ nmatches,
+                                                   int bcap) {
+    // sized by the launch for bcap b-side features (every array's index is
+    // below B.n: common nodes <= B.nfv, matches <= claimed b features):
+    // common (8 B), rec (4 B), claimed, rbin (1 B) per entry
+    extern __shared__ __align__(16) int2 mb_lds[];
+    int2* common = mb_lds;
+    int* rec = reinterpret_cast<int*>(common + bcap);
+    uint8_t* claimed = reinterpret_cast<uint8_t*>(rec + bcap);
+    uint8_t* rbin = claimed + bcap;
     __shared__ int s_nc, s_nm, s_hist[HISTO_LENGTH], s_keep[3];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     // a small grid walks the pairs (the step's pair list is mostly the empty
@@ -312,6 +333,10 @@ __global__ __launch_bounds__(256) void k_match_bow(const BowPair* __restrict__ p
     const BowPair P = pairs[pi];
     const gf_bow_side& A = P.a;
     const gf_bow_side& B = P.b;
+    if (B.n > bcap) {  // the launch's LDS does not hold this pair (the hosts size it: not reached)
+        if (tid == 0) nmatches[pi] = -1;
+        continue;
+    }
     const int nout = mode == 0 ? B.n : A.n;
     for (int i = tid; i < nout; i += 256) P.out[i] = -1;
     if (A.nfv == 0 || B.nfv == 0) {  // no common node: no match
@@ -718,6 +743,12 @@ static int bow_transform_impl(gf_vocab* v, int nframes, const uint8_t* d_desc, c
     int32_t* nid = wid + (size_t)nframes * cap;
     double* wv = (double*)(nid + (size_t)nframes * cap);
     const VocabDev V = vdev(v);
+    static bool lds_attr = false;  // k_bow_build may take up to 96 KB of dynamic LDS (cap 4096)
+    if (!lds_attr) {
+        GF_HIP(hipFuncSetAttribute((const void*)k_bow_build, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)bow_build_lds(BOW_MAX)));
+        lds_attr = true;
+    }
     {
         GF_PROF(v->ctx, s, "k_bow_descend");
         GF_LAUNCH(k_bow_descend, dim3((cap + 255) / 256, nframes), 256, 0, s, V, d_desc, d_n, cap, levelsup, wid, wv, nid,
@@ -726,7 +757,8 @@ static int bow_transform_impl(gf_vocab* v, int nframes, const uint8_t* d_desc, c
     }
     {
         GF_PROF(v->ctx, s, "k_bow_build");
-        GF_LAUNCH(k_bow_build, std::min(nframes, d_gate ? 32 : nframes), 256, 0, s, V, nframes, d_n, cap, wid, wv, nid,
+        GF_LAUNCH(k_bow_build, std::min(nframes, d_gate ? 32 : nframes), 256, bow_build_lds(cap), s, V, nframes, d_n, cap,
+                  wid, wv, nid,
                   d_words, d_values, d_nwords, d_fv_nodes, d_fv_start, d_fv_feats, d_nfv, d_gate);
         GF_HIP(hipGetLastError());
     }
@@ -744,11 +776,13 @@ int gf::bow_transform_gated(gf_vocab* voc, int nframes, const uint8_t* d_desc, c
 }
 
 int gf::match_bow_pairs(gf_ctx* ctx, int mode, float nnratio, int check_ori, int npairs, const gf::BowPairDev* d_pairs,
-                        int32_t* d_nmatches, void* stream) {
+                        int32_t* d_nmatches, int bcap, void* stream) {
     if (npairs <= 0) return GF_OK;
+    GF_CHECK(bcap > 0 && bcap <= BOW_MAX, GF_ERR_UNSUPPORTED, "b side: at most 4096 features");
     hipStream_t s = (hipStream_t)stream;
     GF_PROF(ctx, s, "k_match_bow");
-    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, 0, s, d_pairs, npairs, mode, nnratio, check_ori, d_nmatches);
+    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, match_bow_lds(bcap), s, d_pairs, npairs, mode, nnratio,
+              check_ori, d_nmatches, bcap);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
@@ -819,9 +853,11 @@ int gf_match_bow_dev(gf_ctx* ctx, int mode, float nnratio, int check_ori, int np
     int rc = gf::ws_get(ctx, 52, sizeof(BowPair) * npairs, &dp);
     if (rc) return rc;
     GF_HIP(hipMemcpyAsync(dp, P.data(), sizeof(BowPair) * npairs, hipMemcpyHostToDevice, s));
+    int bcap = 1;
+    for (int p = 0; p < npairs; p++) bcap = std::max(bcap, b[p].n);
     GF_PROF(ctx, s, "k_match_bow");
-    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, 0, s, (const BowPair*)dp, npairs, mode, nnratio, check_ori,
-              d_nmatches);
+    GF_LAUNCH(k_match_bow, std::min(npairs, 256), 256, match_bow_lds(bcap), s, (const BowPair*)dp, npairs, mode,
+              nnratio, check_ori, d_nmatches, bcap);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }

@@ -176,7 +176,7 @@ struct BowPairDev {
     int32_t* out;
 };
 int match_bow_pairs(gf_ctx* ctx, int mode, float nnratio, int check_ori, int npairs, const BowPairDev* d_pairs,
-                    int32_t* d_nmatches, void* stream);
+                    int32_t* d_nmatches, int bcap, void* stream);
 int obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, const gf_keypoint* d_kps,
                      const uint8_t* d_desc, const int32_t* d_n, int kp_cap, const gf_mp_view* d_views,
                      const uint8_t* d_mp_desc, const uint8_t* d_updated, const double* d_info, const double* d_H,

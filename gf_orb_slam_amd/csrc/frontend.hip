@@ -956,7 +956,7 @@ int fe_track_frame(gf_frontend* fe, hipStream_t s) {
                                       (double*)TL.values, (int32_t*)TL.nwords, (int32_t*)TL.fv_nodes,
                                       (int32_t*)TL.fv_start, (int32_t*)TL.fv_feats, (int32_t*)TL.nfv, fe->bow_tmp, s));
         FE_RC(gf::reloc_candidates(ctx, TL, s));
-        FE_RC(gf::match_bow_pairs(ctx, 0, 0.75f, 1, B * TL.ncs, TL.pairs, TL.bow_nm, s));
+        FE_RC(gf::match_bow_pairs(ctx, 0, 0.75f, 1, B * TL.ncs, TL.pairs, TL.bow_nm, cap, s));  // b side: the frame
     }
     // the motion model's outlier discard and failure test, TrackPreviousFrame,
     // the relocalisation loop, and the gates of the TrackLocalMap stages below

@@ -395,9 +395,31 @@ constexpr int AW = 64;
 // o_{n+k} = o_{n+k-3} + o_{n+k-31} (mod 2^32), hence a fixed integer
 // combination sum_j C[k][j] s_j. One wave produces the next 64 words at once
 // (lane k: 31 multiply-adds); rand() = word >> 1.
-__constant__ uint32_t c_rng_coef[64][31];
+// [j][lane]: lane-consecutive, one coalesced 256-B row per history word
+__constant__ uint32_t c_rng_coef[31][64];
 
-__device__ __forceinline__ uint32_t rng_word(uint32_t s, const uint32_t (&coef)[31]) {
+// A lane's row of the recurrence. AM_RCOEF_REG 1 keeps it in 31 VGPRs for the
+// whole kernel; 0 (default) reads it from the table at each 64-word batch (a
+// few batches per round; the 31 registers were a quarter of the budget of a
+// kernel whose register pressure the compiler handled wrongly).
+#ifndef AM_RCOEF_REG
+#define AM_RCOEF_REG 0
+#endif
+struct RCoef {
+#if AM_RCOEF_REG
+    uint32_t c[31];
+    __device__ void load() {
+#pragma unroll
+        for (int j = 0; j < 31; j++) c[j] = c_rng_coef[j][threadIdx.x];
+    }
+    __device__ uint32_t operator[](int j) const { return c[j]; }
+#else
+    __device__ void load() {}
+    __device__ uint32_t operator[](int j) const { return c_rng_coef[j][threadIdx.x]; }
+#endif
+};
+
+__device__ __forceinline__ uint32_t rng_word(uint32_t s, const RCoef& coef) {
     uint32_t acc = 0;
 #pragma unroll
     for (int j = 0; j < 31; j++) acc += coef[j] * (uint32_t)__builtin_amdgcn_readlane((int)s, j);
@@ -674,7 +696,7 @@ __device__ __forceinline__ int bits_for(int n) {  // 2^bits_for(n) >= n
 // commit advances the RNG from the batch holding its last call.
 __device__ int draw_batch(uint32_t& s, uint32_t& s0, uint32_t& o0, int& tries, int& run, int N, int round,
                           const Pool& P, int16_t* vis,
-                          const Cands& C, int nc, int* exh_at, const uint32_t (&coef)[31], int sbits) {
+                          const Cands& C, int nc, int* exh_at, const RCoef& coef, int sbits) {
     const int lane = threadIdx.x;
     const uint32_t o = rng_word(s, coef);
     const int j = (int)((o >> 1) % (uint32_t)N);
@@ -770,7 +792,7 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
 // round's draw state; on return sd is the rand() state after exactly
 // exh_at calls from the round start.
 __device__ void exhaust_draws(uint32_t& sd, int tries, int run, int N, unsigned long long* colvis, int& nacc,
-                              int& exh_at, const uint32_t (&coef)[31]) {
+                              int& exh_at, const RCoef& coef) {
     while (true) {
         const uint32_t o = rng_word(sd, coef);
         const int j = (int)((o >> 1) % (uint32_t)N);
@@ -994,6 +1016,14 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #ifndef AM_SLOTS
 #define AM_SLOTS 1
 #endif
+// AM_SORTED_WIDE: live sets of 65..256 candidates kept sorted in 2 / 4
+// registers per lane (sorted_loop). Off: such rounds (initial subsets above
+// 64: num_to_match small against the pool, not the bench's regime) take the
+// general wave_top loop. Their inlined bodies held the kernel at its register
+// limit, where the compiler misplaced spill copies.
+#ifndef AM_SORTED_WIDE
+#define AM_SORTED_WIDE 0
+#endif
 // LDS hand-over inside the one-wave workgroup
 __device__ __forceinline__ void wave_sync_lds() { am_sync(); }
 
@@ -1115,9 +1145,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         const int q = lmk[sl];
         return rmp ? rmp[q] : q;
     };
-    uint32_t rcoef[31];  // this lane's row of the rand() recurrence, for the whole kernel
-#pragma unroll
-    for (int j = 0; j < 31; j++) rcoef[j] = c_rng_coef[lane][j];
+    RCoef rcoef;  // this lane's row of the rand() recurrence
+    rcoef.load();
     am_sync();
     AM_T(0);
 
@@ -1194,7 +1223,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         const int f0 = A.rng[f].f;
         rs = lane < 31 ? (uint32_t)A.rng[f].state[(f0 + lane) % 31] : 0u;
     }
-    int used = 0, nm = 0, nld = 0;  // nld: logDet calls of the reference (one per draw)
+    // rand() calls, claims, logDet calls of the reference (one per draw): wave
+    // counters, pinned uniform (scalar registers) at every update
+    int used = 0, nm = 0, nld = 0;
     am_sync();
     AM_T(1);
 
@@ -1231,7 +1262,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 // otherwise the draws gave out first (early termination, :1437)
                 const int T = nc >= 1 ? __builtin_amdgcn_readfirstlane(C.tries[0]) : exh_at;
                 for (int t = T; t > 0; t -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(t, 64));
-                used += T;
+                used = __builtin_amdgcn_readfirstlane(used + T);
                 if (nc >= 1) {
                     cut = true;
                     if (lane == 0) rec[GF_CK_AM_CUT] = round;
@@ -1286,8 +1317,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             am_sync();
             int nacc = 0, ex = 0;
             exhaust_draws(sd, 0, 0, N, colvis, nacc, ex, rcoef);
-            nld += nacc;
-            used += ex;
+            nld = __builtin_amdgcn_readfirstlane(nld + nacc);
+            used = __builtin_amdgcn_readfirstlane(used + ex);
             rs = sd;
             AM_T(2);
             break;
@@ -1314,9 +1345,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         AM_T(2);
         if (cabort) break;
         if (nc < sz) {  // the initial subset could not be completed
-            nld += nc;
+            nld = __builtin_amdgcn_readfirstlane(nld + nc);
             for (int c = lane; c < nc; c += AW) vis[C.slot[c]] = -1;
-            used += exh_at;
+            used = __builtin_amdgcn_readfirstlane(used + exh_at);
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
@@ -1690,6 +1721,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         };
         const int kreg = (sz + 63) >> 6;
         int decided = 0;
+        (void)sorted_loop;
 #if AM_SLOTS
         if (kreg == 1)
             decided = slot_loop();
@@ -1697,10 +1729,12 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         if (kreg == 1)
             decided = sorted_loop(std::integral_constant<int, 1>{});
 #endif
+#if AM_SORTED_WIDE
         else if (kreg == 2)
             decided = sorted_loop(std::integral_constant<int, 2>{});
         else if (kreg <= 4)
             decided = sorted_loop(std::integral_constant<int, 4>{});
+#endif
         if (!decided) {
             if (npop == 0) {  // (b) from the start: the initial live set
                 for (int c = lane; c < sz; c += AW) {
@@ -1748,8 +1782,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
-        nld += nused;
-        const int T = exh ? exh_at : C.tries[nused - 1];
+        nld = __builtin_amdgcn_readfirstlane(nld + nused);
+        const int T = __builtin_amdgcn_readfirstlane(exh ? exh_at : C.tries[nused - 1]);
 #ifdef GF_AM_CHECK
         {
             int bad = 0;
@@ -1763,7 +1797,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         const uint32_t rs_prev = rs;
 #endif
         for (int c = nused + lane; c < nc; c += AW) vis[C.slot[c]] = -1;
-        used += T;
+        used = __builtin_amdgcn_readfirstlane(used + T);
         if (T > 0 && (T - 1) / 64 >= nb - 2) {  // the batch holding call T is one of the last two
             const int b = (T - 1) / 64;
             rs = (b & 1) ? rng_advance(bs1, bo1, T - 64 * b) : rng_advance(bs0, bo0, T - 64 * b);
@@ -1848,7 +1882,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
         }
-        nm++;
+        nm = __builtin_amdgcn_readfirstlane(nm + 1);
         (void)success;
         am_sync();
         if (nrem == N) break;  // went through all map points: the pool stays as left-overs
@@ -2218,13 +2252,17 @@ int gf::obs_active_match(gf_ctx* ctx, const gf_frame_info* fi, int nframes, cons
     int rc = gf::ws_get(ctx, 30, sizeof(int32_t) * nframes, &err);
     if (rc) return rc;
     A.err = (int32_t*)err;
-    static unsigned long long mask = 0;
+    static unsigned long long mask = 0;  // devices whose table is set (once per process)
     if (!(mask & (1ull << ctx->device))) {  // rand() as a linear combination of the 31-word history
         uint32_t h[31 + 64][31] = {};
         for (int j = 0; j < 31; j++) h[j][j] = 1u;
         for (int k = 0; k < 64; k++)
             for (int j = 0; j < 31; j++) h[31 + k][j] = h[28 + k][j] + h[k][j];
-        GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_rng_coef), &h[31][0], sizeof(uint32_t) * 64 * 31));
+        uint32_t t[31][64];
+        for (int j = 0; j < 31; j++)
+            for (int k = 0; k < 64; k++) t[j][k] = h[31 + k][j];
+        GF_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_rng_coef), &t[0][0], sizeof(t)));
+        mask |= 1ull << ctx->device;
     }
     void* pre;
     rc = gf::ws_get(ctx, 32, sizeof(OnePre) * (size_t)nframes * mp_cap, &pre);

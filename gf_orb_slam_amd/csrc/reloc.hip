@@ -41,6 +41,9 @@ struct gf_kfdb {
 namespace {
 
 constexpr int TL_T = 64;  // one wave per stream
+#ifndef TL_GRID
+#define TL_GRID 8  // k_track_loss workgroups
+#endif
 
 __device__ __forceinline__ int32_t* stat_of(const gf::TrackLossArgs& A, int which) {
     return A.stats + (size_t)which * A.B;
@@ -995,8 +998,14 @@ int gf::track_loss(gf_ctx* ctx, const TrackLossArgs& A, hipStream_t s) {
         GF_LAUNCH(k_track_gate, A.B, TL_T, 0, s, A);
         GF_HIP(hipGetLastError());
     }
+    // a wave of this kernel takes a whole SIMD's registers (its calls into the
+    // pose LM and the searches make it compile to the 512-register limit): a
+    // small grid, since each workgroup must wait for an idle SIMD beside the
+    // other front ends' extraction even when it finds no stream to track
+    // (64 workgroups: 0.17 ms per launch in the r05 step; a stream that lost
+    // track is walked by one of TL_GRID workgroups)
     GF_PROF(ctx, s, "k_track_loss");
-    GF_LAUNCH(k_track_loss, std::min(A.B, 64), TL_T, 0, s, A);
+    GF_LAUNCH(k_track_loss, std::min(A.B, TL_GRID), TL_T, 0, s, A);
     GF_HIP(hipGetLastError());
     return GF_OK;
 }
