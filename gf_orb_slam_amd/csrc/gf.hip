@@ -1017,12 +1017,16 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #define AM_SLOTS 1
 #endif
 // AM_SORTED_WIDE: live sets of 65..256 candidates kept sorted in 2 / 4
-// registers per lane (sorted_loop). Off: such rounds (initial subsets above
-// 64: num_to_match small against the pool, not the bench's regime) take the
-// general wave_top loop. Their inlined bodies held the kernel at its register
-// limit, where the compiler misplaced spill copies.
+// registers per lane (sorted_loop); off, such rounds (initial subsets above
+// 64: num_to_match small against the pool) take the general wave_top loop.
+// r06: with the loop's match-flag load behind a short-circuit branch, the
+// register allocator put spill copies of live-through values (the rand()-call
+// counter among them) in that branch's join block before its exec restore, so
+// lanes outside the branch kept stale copies. The loads are
+// unconditional now; tests/test_isa_guard.py checks the compiled kernels for
+// the pattern.
 #ifndef AM_SORTED_WIDE
-#define AM_SORTED_WIDE 0
+#define AM_SORTED_WIDE 1
 #endif
 // LDS hand-over inside the one-wave workgroup
 __device__ __forceinline__ void wave_sync_lds() { am_sync(); }
@@ -1549,7 +1553,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             for (int r = 0; r < KR; r++) {
                 const int p = 64 * r + lane;
                 L.c[r] = p < sz ? p : -1;
-                L.s[r] = p < sz ? C.score[p] : -INFINITY;
+                const double sp = C.score[p];  // p < 64 kreg <= PC: in the array (loads unconditional)
+                L.s[r] = p < sz ? sp : -INFINITY;
                 bad |= p < sz && L.s[r] != L.s[r];
             }
             if (__ballot(bad)) return 0;
@@ -1561,7 +1566,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 const double nx = lane < 63 ? nx0 : (r + 1 < KR ? rl0(L.s[r + 1 < KR ? r + 1 : r]) : -INFINITY);
                 const int p = 64 * r + lane;
                 tie |= p + 1 < sz && nx == L.s[r];
-                L.m[r] = L.c[r] >= 0 && C.match[max(L.c[r], 0)] >= 0;
+                const int mt = C.match[max(L.c[r], 0)];
+                L.m[r] = (L.c[r] >= 0) & (mt >= 0);
             }
             if (__ballot(tie)) return 0;
             if constexpr (KR == 1) {
