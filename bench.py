@@ -1011,7 +1011,7 @@ def main():
         top = max(prof, key=lambda k: prof[k][0])
         dom = max(priced, key=lambda k: prof[k][0])
     traffic_src = None
-    for cand in ("r05",):  # PMC traffic measured on this round's build and workload only
+    for cand in ("r06",):  # PMC traffic measured on this round's build and workload only
         try:
             pmc = json.load(open(os.path.join(ROOT, "profiles", cand, "pmc_traffic.json")))
             if pmc.get("batch") == Bg:

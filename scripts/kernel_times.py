@@ -18,7 +18,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 fixed = len(sys.argv) > 4 and sys.argv[4] == "fixed"
 stale = float(sys.argv[3]) if len(sys.argv) > 3 else (0.93 if fixed else 0.82)
-W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=stale)
+W = scene.Workload("euroc", B, n_scenes=32, period=32, seed=0, stale_desc=stale)  # as bench.py: distinct frames
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
 M = 2000 if fixed else 2100
