@@ -1028,6 +1028,9 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #ifndef AM_SORTED_WIDE
 #define AM_SORTED_WIDE 1
 #endif
+#ifndef AM_SB
+#define AM_SB 16  // slot_loop: live / window scores per batch of broadcast reads
+#endif
 // LDS hand-over inside the one-wave workgroup
 __device__ __forceinline__ void wave_sync_lds() { am_sync(); }
 
@@ -1439,35 +1442,35 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 wave_sync_lds();
                 const bool nan = (v0 && lv != lv) || (v1 && xv != xv);
                 // c = #{live > v}, g = {window draws above v}: broadcast LDS
-                // reads, 16 scores per batch in flight, no per-entry branch
+                // reads, AM_SB scores per batch in flight, no per-entry branch
                 int c0 = 0, c1 = 0;
                 uint32_t g0l = 0u, g0h = 0u, g1l = 0u, g1h = 0u;
 #pragma unroll
-                for (int kb = 0; kb < 64; kb += 16) {
+                for (int kb = 0; kb < 64; kb += AM_SB) {
                     if (kb < sz) {
-                        double lk[16];
+                        double lk[AM_SB];
 #pragma unroll
-                        for (int u = 0; u < 16; u += 2) {
+                        for (int u = 0; u < AM_SB; u += 2) {
                             const double2 d2 = *reinterpret_cast<const double2*>(&s_lsc[kb + u]);
                             lk[u] = d2.x;
                             lk[u + 1] = d2.y;
                         }
 #pragma unroll
-                        for (int u = 0; u < 16; u++) {
+                        for (int u = 0; u < AM_SB; u++) {
                             c0 += lk[u] > lv;
                             c1 += lk[u] > xv;
                         }
                     }
                     if (kb < W) {
-                        double xk[16];
+                        double xk[AM_SB];
 #pragma unroll
-                        for (int u = 0; u < 16; u += 2) {
+                        for (int u = 0; u < AM_SB; u += 2) {
                             const double2 d2 = *reinterpret_cast<const double2*>(&s_xsc[kb + u]);
                             xk[u] = d2.x;
                             xk[u + 1] = d2.y;
                         }
 #pragma unroll
-                        for (int u = 0; u < 16; u++) {
+                        for (int u = 0; u < AM_SB; u++) {
                             const int k = kb + u;
                             if (k < 32) {
                                 g0l |= xk[u] > lv ? 1u << k : 0u;
