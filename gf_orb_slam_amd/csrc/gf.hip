@@ -621,7 +621,16 @@ size_t onepoint_pre_lds_bytes(int kp_cap) {
 }
 
 #ifdef GF_AM_STAMP
-__device__ unsigned long long g_am_stamp[8];
+// [0..7] phase cycles; [8] draw batches, [9] eval calls, [10] candidates
+// evaluated, [11] one-point rescans, [12] rounds, [13] pops, [16] max and [17]
+// sum of a frame's cycles
+__device__ unsigned long long g_am_stamp[24];
+#define AM_C(k, v)                                                              \
+    do {                                                                        \
+        if (threadIdx.x == 0) atomicAdd(&g_am_stamp[k], (unsigned long long)(v)); \
+    } while (0)
+#else
+#define AM_C(k, v) (void)0
 #endif
 #ifdef GF_AM_GUARD
 __device__ unsigned long long g_am_guard[2];  // [0] corrupted sentinel dwords, [1] frames checked
@@ -660,6 +669,12 @@ __device__ __forceinline__ void am_sync() {
 }
 #endif
 
+// AM_PREFETCH: each evaluated candidate's claimed-keypoint octave kept in LDS
+// and its H row touched into the caches, so the round's commit (curMat +=
+// H^T H / sigma^2 of the winner) does not wait on two dependent HBM loads
+#ifndef AM_PREFETCH
+#define AM_PREFETCH 1
+#endif
 struct Cands {
     int16_t* slot;   // pool slot drawn
     int32_t* tries;  // rand() calls from the round start up to this acceptance
@@ -667,6 +682,7 @@ struct Cands {
     int16_t* match;  // keypoint OnePoint would claim, -1
     int16_t* dist;
     uint8_t* alive;  // still in the heap
+    int8_t* oct;     // octave of the keypoint OnePoint would claim (the commit's sigma^2)
 };
 
 // True when a lower lane of the wave holds the same value (the earlier try of
@@ -698,6 +714,7 @@ __device__ int draw_batch(uint32_t& s, uint32_t& s0, uint32_t& o0, int& tries, i
                           const Pool& P, int16_t* vis,
                           const Cands& C, int nc, int* exh_at, const RCoef& coef, int sbits) {
     const int lane = threadIdx.x;
+    AM_C(8, 1);
     const uint32_t o = rng_word(s, coef);
     const int j = (int)((o >> 1) % (uint32_t)N);
     const int sl = pool_select(P, j);
@@ -752,6 +769,9 @@ __device__ __forceinline__ int slot_match(const ActiveArgs& A, const FrameConst&
     const int h1 = SM.h1[sl], h2 = SM.h2[sl];
     if ((h1 >= 0 && claim[h1] >= 0) || (h2 >= 0 && claim[h2] >= 0)) {
         int n1, n2;
+#ifdef GF_AM_STAMP
+        atomicAdd(&g_am_stamp[11], 1ull);
+#endif
         one_point_scan(A, fc, f, q, cell_start, items, claim, KpGlobal{K, D}, mi, md, n1, n2);
         if (mi < 0) md = 0;
         SM.match[sl] = (int16_t)mi;
@@ -766,19 +786,34 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
                            const int16_t* lmk, const SlotMatch& SM, const double* cur, const double* info,
                            const double* info_lt,
                            const uint16_t* lq, const int32_t* rmp, const int* cell_start, const int* items,
-                           const int* claim, const gf_keypoint* K, const uint8_t* D) {
+                           const int* claim, const gf_keypoint* K, const uint8_t* D, const double* Hm) {
+    AM_C(9, 1);
+    AM_C(10, c1 - c0);
+    double pf = 0.0;
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
         // the slot's info / H row: staged at the pool build (lq_stage), else through the remap
         const long long qi = A.lq_stage ? (long long)lq[sl] : (rmp ? rmp[q] : q);
+#if AM_PREFETCH
+        // the commit's inputs, fetched while the round is still drawing: the
+        // H row's two cache lines into the caches (read again only if this
+        // candidate wins the round)
+        pf += gfd::ldg(Hm + 14LL * qi) + gfd::ldg(Hm + 14LL * qi + 13);
+#endif
         C.score[c] = logdet_sum_lower_packed(cur, info_lt + 32LL * qi, info + 49LL * qi);
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
         C.dist[c] = (int16_t)md;
         C.alive[c] = 0;
+#if AM_PREFETCH
+        C.oct[c] = (int8_t)(mi >= 0 ? K[mi].octave : 0);  // the claimed keypoint's octave, for the commit
+#endif
     }
+#if AM_PREFETCH
+    if (pf == -1.2345678e-300) A.err[f] = 9;  // keeps the touch loads (a value no H row sums to)
+#endif
     am_sync();
 }
 
@@ -1053,6 +1088,7 @@ __device__ __forceinline__ int kth_bit(unsigned long long m, int k) {
 __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int f) {
 #ifdef GF_AM_STAMP
     unsigned long long am_last_ = __builtin_amdgcn_s_memtime();
+    const unsigned long long am_start_ = am_last_;
 #endif
     extern __shared__ __align__(16) uint8_t smem[];
     // sized for this launch: PC = pool capacity (map-list capacity rounded to 64,
@@ -1090,7 +1126,8 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     int16_t* sm_h2 = sm_h1 + PC;                                           // PC
     int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
     uint8_t* c_alive = (uint8_t*)(alv + PC);                               // CC
-    uint16_t* lq = (uint16_t*)(((uintptr_t)(c_alive + CC) + 1) & ~(uintptr_t)1);  // PC (lq_stage): info / H row of each slot
+    int8_t* c_oct = (int8_t*)(c_alive + CC);                               // CC (AM_PREFETCH)
+    uint16_t* lq = (uint16_t*)(((uintptr_t)(c_oct + (AM_PREFETCH ? CC : 0)) + 1) & ~(uintptr_t)1);  // PC (lq_stage): info / H row of each slot
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
@@ -1236,7 +1273,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     am_sync();
     AM_T(1);
 
-    const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
+    const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive, c_oct};
     const int S = (int)((float)N / (float)num_to_match * 1.0);
     const int nw0 = (N + 63) >> 6;  // pool words (slots never move; only bits clear)
     bool nsucc_valid = true;        // s_nsucc counts the matchable pool slots
@@ -1246,6 +1283,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     const double* Hm = A.H + (long long)f * A.mp_cap * 14;
 
     for (int round = 0; round < num_to_match; ++round) {
+        AM_C(12, 1);
         const int sz = __builtin_amdgcn_readfirstlane(min(S, N));
         if (sz == 0) break;  // empty heap: early termination
         if (clocked) {
@@ -1358,7 +1396,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             for (int T = exh_at; T > 0; T -= 64) rs = rng_advance(rs, rng_word(rs, rcoef), min(T, 64));
             break;
         }
-        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D);
+        eval_cands(A, fc, f, C, 0, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D, Hm);
         evald = nc;
         AM_T(3);
         // -- the sequential heap loop, now over known scores and match results.
@@ -1404,7 +1442,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             }
             if (rep < nc && rep >= evald) {
                 AM_T(4);
-                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D);
+                eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K, D, Hm);
                 evald = nc;
                 AM_T(3);
             }
@@ -1423,7 +1461,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
                 if (evald < nc && !cabort) {
                     AM_T(4);
                     eval_cands(A, fc, f, C, evald, nc, lmk, SM, cur, info, info_lt, lq, rmp, cell_start, items, claim, K,
-                               D);
+                               D, Hm);
                     evald = nc;
                     AM_T(3);
                 }
@@ -1781,13 +1819,18 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         double h_i = 0.0, h_j = 0.0, h_7i = 0.0, h_7j = 0.0;
         int oct_b = 0;
         if (!exh && lane < 49) {
-            const double* Hq = Hm + 14LL * row_of(C.slot[top]);
+            // (top is wave-uniform, so are the row and the octave: scalar bases)
+            const double* Hq = Hm + 14LL * __builtin_amdgcn_readfirstlane((int)row_of(C.slot[top]));
             const int i = lane / 7, jj = lane % 7;
             h_i = Hq[i];
             h_j = Hq[jj];
             h_7i = Hq[7 + i];
             h_7j = Hq[7 + jj];
+#if AM_PREFETCH
+            oct_b = C.oct[top];
+#else
             oct_b = K[C.match[top]].octave;
+#endif
         }
         // -- commit: RNG calls actually made, visited marks of the used draws only
         const int nused = sz + npop;  // draws that happened
@@ -1892,6 +1935,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
         }
         nm = __builtin_amdgcn_readfirstlane(nm + 1);
+        AM_C(13, npop);
         (void)success;
         am_sync();
         if (nrem == N) break;  // went through all map points: the pool stays as left-overs
@@ -1925,6 +1969,13 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     am_sync();
     if (guard[threadIdx.x] != 0xa5a5a5a5u + threadIdx.x) atomicAdd(&g_am_guard[0], 1ull);
     if (threadIdx.x == 0) atomicAdd(&g_am_guard[1], 1ull);
+#endif
+#ifdef GF_AM_STAMP
+    if (threadIdx.x == 0) {
+        const unsigned long long tot_ = __builtin_amdgcn_s_memtime() - am_start_;
+        atomicMax(&g_am_stamp[16], tot_);
+        atomicAdd(&g_am_stamp[17], tot_);
+    }
 #endif
     {  // back to the glibc ring: f advanced by the calls made, oldest word at f
         const int f1 = (A.rng[f].f + used) % 31;
@@ -1977,7 +2028,7 @@ size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap, bool lq_stage = 
 #endif
     return guard + sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) +
            sizeof(int32_t) * cand_cap + sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
-           (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
+           (AM_PREFETCH ? (size_t)cand_cap : 0) + (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
 }
 // dynamic LDS bound of the active matcher's launches: the full-capacity
 // footprint without the staged rows (the static arrays take the rest of 160 KB)
@@ -2859,9 +2910,9 @@ extern "C" int gf_debug_am_check(unsigned long long* out) {
 #ifdef GF_AM_STAMP
 // Diagnostic build only (not in the header): phase cycles of k_active_match.
 extern "C" int gf_debug_am_stamps(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_stamp), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_am_stamp), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0};
+        unsigned long long z[24] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_am_stamp), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

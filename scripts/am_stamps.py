@@ -19,7 +19,7 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 fixed = len(sys.argv) > 3 and sys.argv[3] == "fixed"  # else the bench regime: keyframe maps, UpdateReference
-W = scene.Workload("euroc", B, n_scenes=8, period=32, seed=0, stale_desc=0.93 if fixed else 0.82)
+W = scene.Workload("euroc", B, n_scenes=32, period=32, seed=0, stale_desc=0.93 if fixed else 0.82)  # as bench.py
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
 M = 2000 if fixed else 2100
@@ -42,7 +42,7 @@ for _ in range(3):
 fe.sync()
 f = lib().gf_debug_am_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.c_int]
-st = np.zeros(8, np.uint64)
+st = np.zeros(24, np.uint64)
 f(st.ctypes.data, 1)
 fe.write("hist", np.zeros((B, 8), np.int32))
 fe.prof_enable(True)
@@ -57,6 +57,10 @@ names = ["setup", "pool", "draws", "evals", "heap_pops", "commit_rng", "pool_upd
 per = st[:8].astype(np.float64) / (B * steps)
 out = {"B": B, "steps": steps, "cycles_per_frame": {k: round(float(v)) for k, v in zip(names, per)},
        "logdets_per_frame": float(h[:, 6].sum()) / (B * steps), "matches_per_frame": float(h[:, 7].sum()) / (B * steps),
+       "counts_per_frame": {k: round(float(st[i]) / (B * steps), 2) for i, k in
+                            [(8, "draw_batches"), (9, "eval_calls"), (10, "evaluated"), (11, "rescans"),
+                             (12, "rounds"), (13, "pops")]},
+       "frame_cycles": {"max": int(st[16]), "mean": round(float(st[17]) / (B * steps))},
        "k_active_match_ms": prof["k_active_match"][0] / prof["k_active_match"][1],
        "k_onepoint_pre_ms": prof["k_onepoint_pre"][0] / prof["k_onepoint_pre"][1]}
 print(json.dumps(out))

@@ -16,7 +16,7 @@ from gf_orb_slam_amd.pipeline import FrontEnd  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 fixed = len(sys.argv) > 2 and sys.argv[2] == "fixed"  # default: the bench's keyframe maps + UpdateReference
-W = scene.Workload("euroc", 8, n_scenes=8, period=32, seed=0, stale_desc=0.93 if fixed else 0.82)
+W = scene.Workload("euroc", 8, n_scenes=8, period=32, seed=0, stale_desc=0.93 if fixed else 0.82)  # stream 0 as bench.py's single_stream leg
 frames = W.render_all("cuda").contiguous()
 ex = ORBextractor(1000, 1.2, 8, 1, 20)
 M = 2000 if fixed else 2100
