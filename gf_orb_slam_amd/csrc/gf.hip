@@ -670,10 +670,12 @@ __device__ __forceinline__ void am_sync() {
 #endif
 
 // AM_PREFETCH: each evaluated candidate's claimed-keypoint octave kept in LDS
-// and its H row touched into the caches, so the round's commit (curMat +=
-// H^T H / sigma^2 of the winner) does not wait on two dependent HBM loads
+// (beside its distance) and its H row touched into the caches, so the round's
+// commit (curMat += H^T H / sigma^2 of the winner) does not wait on two
+// dependent HBM loads. Measured r06 (profiles/r06/amab2): k_active_match 0.89 /
+// 0.99 ms against 0.91 without, single sequence 0.967 against 0.961: off.
 #ifndef AM_PREFETCH
-#define AM_PREFETCH 1
+#define AM_PREFETCH 0
 #endif
 struct Cands {
     int16_t* slot;   // pool slot drawn
@@ -682,7 +684,6 @@ struct Cands {
     int16_t* match;  // keypoint OnePoint would claim, -1
     int16_t* dist;
     uint8_t* alive;  // still in the heap
-    int8_t* oct;     // octave of the keypoint OnePoint would claim (the commit's sigma^2)
 };
 
 // True when a lower lane of the wave holds the same value (the earlier try of
@@ -805,11 +806,14 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
         int md;
         const int mi = slot_match(A, fc, f, SM, sl, q, cell_start, items, claim, K, D, md);
         C.match[c] = (int16_t)mi;
-        C.dist[c] = (int16_t)md;
-        C.alive[c] = 0;
 #if AM_PREFETCH
-        C.oct[c] = (int8_t)(mi >= 0 ? K[mi].octave : 0);  // the claimed keypoint's octave, for the commit
+        // the claimed keypoint's octave (the commit's sigma^2, < 16 levels) in
+        // bits 12..15 of the distance (a Hamming distance <= 256)
+        C.dist[c] = (int16_t)(md | (mi >= 0 ? K[mi].octave & 15 : 0) << 12);
+#else
+        C.dist[c] = (int16_t)md;
 #endif
+        C.alive[c] = 0;
     }
 #if AM_PREFETCH
     if (pf == -1.2345678e-300) A.err[f] = 9;  // keeps the touch loads (a value no H row sums to)
@@ -1126,8 +1130,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     int16_t* sm_h2 = sm_h1 + PC;                                           // PC
     int16_t* alv = sm_h2 + PC;                                             // PC: the live candidates (heap set)
     uint8_t* c_alive = (uint8_t*)(alv + PC);                               // CC
-    int8_t* c_oct = (int8_t*)(c_alive + CC);                               // CC (AM_PREFETCH)
-    uint16_t* lq = (uint16_t*)(((uintptr_t)(c_oct + (AM_PREFETCH ? CC : 0)) + 1) & ~(uintptr_t)1);  // PC (lq_stage): info / H row of each slot
+    uint16_t* lq = (uint16_t*)(((uintptr_t)(c_alive + CC) + 1) & ~(uintptr_t)1);  // PC (lq_stage): info / H row of each slot
     __shared__ double cur[49];
     __shared__ unsigned long long colvis[64];  // exhausting round: visited columns
     __shared__ int s_res, s_exh, s_nsucc;  // s_nsucc: 0 = no pool slot can be matched
@@ -1273,7 +1276,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     am_sync();
     AM_T(1);
 
-    const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive, c_oct};
+    const Cands C{c_slot, c_tries, c_score, c_match, c_dist, c_alive};
     const int S = (int)((float)N / (float)num_to_match * 1.0);
     const int nw0 = (N + 63) >> 6;  // pool words (slots never move; only bits clear)
     bool nsucc_valid = true;        // s_nsucc counts the matchable pool slots
@@ -1827,7 +1830,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             h_7i = Hq[7 + i];
             h_7j = Hq[7 + jj];
 #if AM_PREFETCH
-            oct_b = C.oct[top];
+            oct_b = (C.dist[top] >> 12) & 15;
 #else
             oct_b = K[C.match[top]].octave;
 #endif
@@ -1919,7 +1922,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
         const int b = C.match[top];
         if (lane == 0) {  // OnePoint's claim
             claim[b] = q;
-            A.score[(long long)f * A.kp_cap + b] = C.dist[top];
+            A.score[(long long)f * A.kp_cap + b] = C.dist[top] & 0xfff;
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
 #ifdef AM_LSIG
@@ -2028,7 +2031,7 @@ size_t active_lds_bytes(int pool_cap, int cand_cap, int kp_cap, bool lq_stage = 
 #endif
     return guard + sizeof(double) * cand_cap + 8 * 64 + sizeof(int) * ((size_t)kp_cap + 68) +
            sizeof(int32_t) * cand_cap + sizeof(int16_t) * (8 * (size_t)pool_cap + 3 * (size_t)cand_cap) + cand_cap +
-           (AM_PREFETCH ? (size_t)cand_cap : 0) + (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
+           (lq_stage ? 1 + sizeof(uint16_t) * (size_t)pool_cap : 0);
 }
 // dynamic LDS bound of the active matcher's launches: the full-capacity
 // footprint without the staged rows (the static arrays take the rest of 160 KB)
