@@ -790,7 +790,9 @@ __device__ void eval_cands(const ActiveArgs& A, const FrameConst& fc, int f, con
                            const int* claim, const gf_keypoint* K, const uint8_t* D, const double* Hm) {
     AM_C(9, 1);
     AM_C(10, c1 - c0);
+#if AM_PREFETCH
     double pf = 0.0;
+#endif
     for (int c = c0 + threadIdx.x; c < c1; c += AW) {
         const int sl = C.slot[c];
         const int q = lmk[sl];
