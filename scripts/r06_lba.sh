@@ -11,7 +11,8 @@ timeout -k 10 600 python -u -m pytest tests/test_lba_gpu.py -m gpu -x -q --timeo
 echo "lba tests: $(tail -1 $O/pytest.log)"
 for v in ${VARS//,/ }; do
   case $v in product*) lib="";; *) lib=$R/gf_orb_slam_amd/diag/libgfslam_${v}.so;; esac
+  GF_LIB=$lib timeout -k 10 300 python -u -m pytest tests/test_lba_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_$v.log 2>&1 || { tail -30 $O/pytest_$v.log; exit 12; }
   GF_LIB=$lib timeout -k 10 300 python scripts/lba_timing.py > $O/$v.txt 2> $O/$v.err || { tail -20 $O/$v.err; exit 11; }
-  echo "== $v"; grep -E "B=1 |k_ba_solve|B=64" $O/$v.txt | head -6
+  echo "== $v $(tail -1 $O/pytest_$v.log)"; grep -E "B=1 |k_ba_solve|B=64" $O/$v.txt | head -6
 done
 exit 0
