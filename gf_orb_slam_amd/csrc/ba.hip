@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -756,7 +757,9 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     __shared__ double sL[BA_MAXN * (BA_MAXN + 1) / 2];
     __shared__ double sb[BA_MAXN], sbp[BA_MAXN], srinv[BA_MAXN];
     __shared__ uint8_t sact[BA_MAXFREE];
+#ifdef BA_SUBST_BLOCK
     __shared__ double scol6[6];
+#endif
     __shared__ int s_fail;
     const int p = blockIdx.x, tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     const BADesc d = A.desc[p];
@@ -904,6 +907,100 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
 #else
     if (A.tstamp && tid == 0) A.tstamp[(size_t)p * 8 + 5] = __builtin_amdgcn_s_memtime();
 #endif
+#ifndef BA_SUBST_BLOCK
+    if (!fail && w == 0) {
+        // Substitutions on one wave, one unknown per step: lane l holds rows
+        // l, l + 64, l + 128 in registers. Step k takes y_k = r_k / d_k from
+        // its owner lane (the product with 1 / d_k, then two lane reads), and
+        // every row still open subtracts its one term: the forward pass in
+        // ascending k (L_ik from row i), the backward pass in descending k
+        // (L_ki from row k, a contiguous run of the packed triangle). Each
+        // row sees its terms in the oracle's order, so x is the same bits as
+        // the block-wise form (BA_SUBST_BLOCK). The L values of 8 steps are
+        // loaded together (one wait per 8 steps), and the steps of one
+        // owner slot (k in [64 uk, 64 uk + 64)) are a loop of their own, so
+        // the owner's register and the rows a step touches are known at
+        // compile time: the step's chain is a product, two lane reads, a
+        // product and a difference.
+        constexpr int SC = 8;
+        double r[3], ri[3];
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = lane + 64 * u;
+            r[u] = i < n ? sb[i] : 0.0;
+            ri[u] = i < n ? srinv[i] : 0.0;
+        }
+        // forward: SC steps at a time while a whole chunk fits, then single steps
+        auto fwd = [&](auto ukc, auto scc, int k0) {
+            constexpr int uk = decltype(ukc)::value, S = decltype(scc)::value;
+            double Lb[3][S];
+#pragma unroll
+            for (int u = uk; u < 3; u++) {
+                const int i = min(lane + 64 * u, n - 1), base = tri(i);
+#pragma unroll
+                for (int s2 = 0; s2 < S; s2++) Lb[u][s2] = sL[base + min(k0 + s2, i)];
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < S; s2++) {
+                const int k = k0 + s2;
+                const double yk = readlane_d(r[uk] * ri[uk], k & 63);
+                {
+                    const int i = lane + 64 * uk;
+                    const double t = r[uk] - Lb[uk][s2] * yk;
+                    r[uk] = i > k ? t : (i == k ? yk : r[uk]);
+                }
+#pragma unroll
+                for (int u = uk + 1; u < 3; u++) r[u] = r[u] - Lb[u][s2] * yk;
+            }
+        };
+        auto fwd_seg = [&](auto ukc) {
+            constexpr int uk = decltype(ukc)::value;
+            const int ke = min(n, 64 * uk + 64);
+            int k0 = 64 * uk;
+            for (; k0 + SC <= ke; k0 += SC) fwd(ukc, std::integral_constant<int, SC>{}, k0);
+            for (; k0 < ke; k0++) fwd(ukc, std::integral_constant<int, 1>{}, k0);
+        };
+        fwd_seg(std::integral_constant<int, 0>{});
+        fwd_seg(std::integral_constant<int, 1>{});
+        fwd_seg(std::integral_constant<int, 2>{});
+        // backward, the same shape in descending k
+        auto bwd = [&](auto ukc, auto scc, int k1) {
+            constexpr int uk = decltype(ukc)::value, S = decltype(scc)::value;
+            double Lb[3][S];
+#pragma unroll
+            for (int s2 = 0; s2 < S; s2++) {
+                const int base = tri(k1 - s2);
+#pragma unroll
+                for (int u = 0; u <= uk; u++) Lb[u][s2] = sL[base + min(lane + 64 * u, k1 - s2)];
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < S; s2++) {
+                const int k = k1 - s2;
+                const double xk = readlane_d(r[uk] * ri[uk], k & 63);
+                {
+                    const int i = lane + 64 * uk;
+                    const double t = r[uk] - Lb[uk][s2] * xk;
+                    r[uk] = i < k ? t : (i == k ? xk : r[uk]);
+                }
+#pragma unroll
+                for (int u = 0; u < uk; u++) r[u] = r[u] - Lb[u][s2] * xk;
+            }
+        };
+        auto bwd_seg = [&](auto ukc) {
+            constexpr int uk = decltype(ukc)::value;
+            const int kb = 64 * uk;
+            int k1 = min(n, 64 * uk + 64) - 1;
+            for (; k1 - SC + 1 >= kb; k1 -= SC) bwd(ukc, std::integral_constant<int, SC>{}, k1);
+            for (; k1 >= kb; k1--) bwd(ukc, std::integral_constant<int, 1>{}, k1);
+        };
+        bwd_seg(std::integral_constant<int, 2>{});
+        bwd_seg(std::integral_constant<int, 1>{});
+        bwd_seg(std::integral_constant<int, 0>{});
+#pragma unroll
+        for (int u = 0; u < 3; u++)
+            if (lane + 64 * u < n) sb[lane + 64 * u] = r[u];
+    }
+#else
     if (!fail && w == 0) {
         // Substitutions on one wave, one pose block at a time: lane l holds
         // rows l, l + 64, l + 128 in registers; a block's 6 values go through
@@ -980,6 +1077,7 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
         for (int u = 0; u < 3; u++)
             if (lane + 64 * u < n) sb[lane + 64 * u] = r[u];
     }
+#endif
     __syncthreads();
     BA_STAMP(3);
 #ifndef BA_CHOL_PHASES
