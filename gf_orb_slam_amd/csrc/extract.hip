@@ -1430,27 +1430,47 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
     const bool win = live && x >= 18 && x + 18 < w && y >= 18 && y + 18 < h;
 
     {  // one batch: IC rows y-15..y+15 (cols x-15..), window rows y-18..y+18 (cols x-18..)
-        constexpr int NL = (DS_IC * DS_ICW + DS_BL * DS_BLW + 31) / 32;
-        uint32_t v[NL];
+        // Each lane owns one dword column of every third row, so a load's
+        // address is one multiply-add from the lane's column base (the flat
+        // index split by division cost ~13 VALU per load, a third of the
+        // kernel's VALU). IC: lanes (rg, q) = (hl / 9, hl % 9) for hl < 27, rows
+        // rg + 3 k; window: (hl / 10, hl % 10) for hl < 30, rows rg + 3 k.
+        // Lanes past them, and rows past the last, repeat the last lane's
+        // column / the last row: they load and store the same words again.
+        constexpr int NI = (DS_IC + 2) / 3, NB = (DS_BL + 2) / 3;
+        const int hq = min(hl, 3 * DS_ICW - 1), rg = hq / DS_ICW, q = hq - rg * DS_ICW;
+        const int hw = min(hl, 3 * DS_BLW - 1), rg2 = hw / DS_BLW, q2 = hw - rg2 * DS_BLW;
+        uint32_t vi[NI], vb[NB];
+        if (live) {
+            const uint8_t* row0 = Pl + (long long)(y - 15) * stride + x - 15;
+            if ((stride & 3) == 0) {  // every row has row 0's byte shift
+                const uint8_t* c0 = reinterpret_cast<const uint8_t*>(
+                    (reinterpret_cast<uintptr_t>(row0) & ~(uintptr_t)3) + 4 * (uintptr_t)q);
 #pragma unroll
-        for (int t = 0; t < NL; t++) {
-            const int i = hl + 32 * t;
-            v[t] = 0;
-            if (live && i < DS_IC * DS_ICW) {
-                const int r = i / DS_ICW, q = i - r * DS_ICW;
-                const uintptr_t a = (uintptr_t)(Pl + (long long)(y - 15 + r) * stride + x - 15);
-                v[t] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
-            } else if (win && i >= DS_IC * DS_ICW && i < DS_IC * DS_ICW + DS_BL * DS_BLW) {
-                const int j = i - DS_IC * DS_ICW, r = j / DS_BLW, q = j - r * DS_BLW;
-                const uintptr_t a = (uintptr_t)(B + (long long)(y - 18 + r) * pwl + x - 18);
-                v[t] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
+                for (int k = 0; k < NI; k++)
+                    vi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(c0 + (long long)min(rg + 3 * k, DS_IC - 1) * stride));
+            } else {
+#pragma unroll
+                for (int k = 0; k < NI; k++) {
+                    const uintptr_t a = (uintptr_t)(row0 + (long long)min(rg + 3 * k, DS_IC - 1) * stride);
+                    vi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
+                }
             }
         }
+        if (win) {  // blurred rows pitched to 64 B: one byte shift for the window
+            const uint32_t* c0 = reinterpret_cast<const uint32_t*>(
+                                     reinterpret_cast<uintptr_t>(B + (long long)(y - 18) * pwl + x - 18) & ~(uintptr_t)3) +
+                                 q2;
 #pragma unroll
-        for (int t = 0; t < NL; t++) {
-            const int i = hl + 32 * t;
-            if (i < DS_IC * DS_ICW) W.ic[i] = v[t];
-            else if (i < DS_IC * DS_ICW + DS_BL * DS_BLW) W.bl[i - DS_IC * DS_ICW] = v[t];
+            for (int k = 0; k < NB; k++) vb[k] = gfd::ldg(c0 + (long long)min(rg2 + 3 * k, DS_BL - 1) * (pwl >> 2));
+        }
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < NI; k++) W.ic[min(rg + 3 * k, DS_IC - 1) * DS_ICW + q] = vi[k];
+        }
+        if (win) {
+#pragma unroll
+            for (int k = 0; k < NB; k++) W.bl[min(rg2 + 3 * k, DS_BL - 1) * DS_BLW + q2] = vb[k];
         }
         if (hl < DS_IC) W.ic_sh[hl] = (uint8_t)((uintptr_t)(Pl + (long long)(y - 15 + hl) * stride + x - 15) & 3);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1492,33 +1512,49 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
         const float ang = angle * factorPI;
         const float a = gflibm::cosf(ang), b = gflibm::sinf(ang);  // glibc cosf/sinf (ORBextractor.cc:167)
         int val = 0;
+        // the two sample sources in separate loops (a half's keypoint is
+        // either inside or near the border), so the window's loop keeps its
+        // LDS base and the rotation in registers across the 16 tests
+        auto rot = [&](int bit, int q, int& rx, int& ry) {
+            const uint32_t pt = sh_pat[bit * 32 + hl] >> (16 * q);
+            const float px = (float)(int8_t)(pt & 0xff), py = (float)(int8_t)((pt >> 8) & 0xff);
+            ry = __float2int_rn(px * b + py * a);
+            rx = __float2int_rn(px * a - py * b);
+        };
+        if (win) {
+            const uint8_t* ctr = bl8 + bsh + 18 * (4 * DS_BLW) + 18;  // the keypoint's byte in the window
 #pragma unroll
-        for (int bit = 0; bit < 8; bit++) {
-            int t[2];
+            for (int bit = 0; bit < 8; bit++) {
+                int t[2];
 #pragma unroll
-            for (int q = 0; q < 2; q++) {
-                const uint32_t pt = sh_pat[bit * 32 + hl] >> (16 * q);
-                const float px = (float)(int8_t)(pt & 0xff), py = (float)(int8_t)((pt >> 8) & 0xff);
-                const int ry = __float2int_rn(px * b + py * a);
-                const int rx = __float2int_rn(px * a - py * b);
-                if (win) {
-                    const int r = ry + 18;
+                for (int q = 0; q < 2; q++) {
+                    int rx, ry;
+                    rot(bit, q, rx, ry);
 #if DESC_B64
-                    const int a = r * (4 * DS_BLW) + bsh + rx + 18;
-                    const uint64_t w8 = *reinterpret_cast<const uint64_t*>(bl8 + (a & ~7));
-                    t[q] = (int)((w8 >> (8 * (a & 7))) & 0xffu);
+                    const int a8 = (int)(ctr - reinterpret_cast<const uint8_t*>(W.bl)) + ry * (4 * DS_BLW) + rx;
+                    const uint64_t w8 = *reinterpret_cast<const uint64_t*>(bl8 + (a8 & ~7));
+                    t[q] = (int)((w8 >> (8 * (a8 & 7))) & 0xffu);
 #else
-                    t[q] = bl8[r * (4 * DS_BLW) + bsh + rx + 18];
+                    t[q] = ctr[ry * (4 * DS_BLW) + rx];
 #endif
-                } else {
+                }
+                val |= (t[0] < t[1]) << bit;
+            }
+        } else if (live) {
+#pragma unroll
+            for (int bit = 0; bit < 8; bit++) {
+                int t[2];
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    int rx, ry;
+                    rot(bit, q, rx, ry);
                     const int xx = x + rx, yy = y + ry;
                     const bool inside = xx >= 0 && xx < w && yy >= 0 && yy < h;
-                    t[q] = !live ? 0
-                           : inside ? B[(long long)yy * pwl + xx]
-                                    : gfd::ldg(Pl + (long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w));
+                    t[q] = inside ? B[(long long)yy * pwl + xx]
+                                  : gfd::ldg(Pl + (long long)gfd::reflect101(yy, h) * stride + gfd::reflect101(xx, w));
                 }
+                val |= (t[0] < t[1]) << bit;
             }
-            val |= (t[0] < t[1]) << bit;
         }
         if (live) desc[((long long)f * cap + k) * 32 + hl] = (uint8_t)val;
     }

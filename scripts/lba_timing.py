@@ -9,7 +9,7 @@ from gf_orb_slam_amd.synth import synth_lba_problem
 from gf_orb_slam_amd._lib import lib, check
 import oracle_lib as O
 
-for B in [1, 8, 64]:
+for B in [int(b) for b in os.environ.get('LBA_BATCHES', '1,8,64').split(',')]:
     probs = [synth_lba_problem(100 + i, 20, 3000) for i in range(B)]
     plan = LocalBAPlan(probs)
     plan.solve()

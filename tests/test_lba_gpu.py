@@ -40,6 +40,15 @@ def test_local_ba_matches_oracle(seed, nkf, npts):
     _check(local_bundle_adjustment(p), O.local_ba(p))
 
 
+def test_local_ba_max_local_keyframes():
+    """32 local keyframes (the limit, n = 192): k_ba_solve's triangle fills the
+    LDS, so the trailing update reads its panel values from the triangle
+    itself instead of the staged copy."""
+    p = synth_lba_problem(7, 33, 1500, nfixed=0)  # keyframe 0 fixed: 32 free
+    assert int((np.asarray(p["kf_kind"]) == 0).sum()) == 32
+    _check(local_bundle_adjustment(p), O.local_ba(p))
+
+
 def test_local_ba_batch_matches_oracle():
     probs = [synth_lba_problem(20 + i, n, m) for i, (n, m) in enumerate([(8, 500), (20, 3000), (4, 60), (12, 1500)])]
     plan = LocalBAPlan(probs)
