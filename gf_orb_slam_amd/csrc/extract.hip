@@ -541,16 +541,34 @@ __global__ __launch_bounds__(256) void k_blur_fast(Planes P, LevelGeom g, uint8_
             const int o0 = pj[0] - pb, o1 = pj[1] - pb, o2 = pj[2] - pb, o3 = pj[3] - pb;
             const bool two = max(max(o0, o1), max(o2, o3)) >= 4;
             const uint32_t sl = (uint32_t)o0 | (uint32_t)o1 << 8 | (uint32_t)o2 << 16 | (uint32_t)o3 << 24;
+            static_assert(LR * (NI - 1) + LR - 1 < BT_R, "every row of a sweep exists");
+            if (yin) {
+                // interior rows (most tiles): the lane's rows lr + LR k are one
+                // multiply-add from its first row, no reflect per row
+                const uint8_t* row0 = S + (long long)(Y0 + lr - 3) * stride + pb;
+                const long long sweep = (long long)LR * stride;
 #pragma unroll
-            for (int k = 0; k < NI; k++) {
-                const int ry = lr + LR * k;
-                lo[k] = hi[k] = 0u;
-                sel[k] = sl;
-                if (lr < LR && ry < BT_R) {
-                    const int yy = yin ? Y0 + ry - 3 : gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
-                    const uint8_t* row = S + yy * stride + pb;
-                    lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(row));
-                    hi[k] = two ? gfd::ldg(reinterpret_cast<const uint32_t*>(row + 4)) : lo[k];
+                for (int k = 0; k < NI; k++) {
+                    sel[k] = sl;
+                    lo[k] = hi[k] = 0u;
+                    if (lr < LR) {  // both loads unconditional (the second re-reads the first when one dword holds the bytes)
+                        const uint32_t* rp = reinterpret_cast<const uint32_t*>(row0 + k * sweep);
+                        lo[k] = gfd::ldg(rp);
+                        hi[k] = gfd::ldg(rp + (two ? 1 : 0));
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < NI; k++) {
+                    const int ry = lr + LR * k;
+                    lo[k] = hi[k] = 0u;
+                    sel[k] = sl;
+                    if (lr < LR) {
+                        const int yy = gfd::reflect101(min(Y0 + ry - 3, h + 2), h);
+                        const uint8_t* row = S + yy * stride + pb;
+                        lo[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(row));
+                        hi[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(row + (two ? 4 : 0)));
+                    }
                 }
             }
         } else {
