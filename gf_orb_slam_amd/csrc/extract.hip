@@ -1191,13 +1191,34 @@ __device__ __forceinline__ void wave_nth_element(const SelWave<E>& W, int nth, i
     wave_sync();
 }
 
+// dst[0 .. n) = src[0 .. n) by one wave, 8 loads per lane in flight before
+// their stores (a plain strided loop waits for every load before the next)
+template <typename E, typename D>
+__device__ __forceinline__ void wave_copy_in(D* dst, const E* src, int n) {
+    const int lane = threadIdx.x & 63;
+    constexpr int CB = 8;
+    for (int i0 = 0; i0 < n; i0 += 64 * CB) {
+        E v[CB];
+#pragma unroll
+        for (int k = 0; k < CB; k++) {
+            const int i = i0 + 64 * k + lane;
+            v[k] = i < n ? src[i] : (E)0;
+        }
+#pragma unroll
+        for (int k = 0; k < CB; k++) {
+            const int i = i0 + 64 * k + lane;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
 // retainBest(list, keep) + truncation, written to dst[0 .. keep): one wave.
 template <typename E>
 __device__ __forceinline__ void wave_retain_to(const SelWave<E>& W, E* list, int n, int keep, E* dst) {
     const int lane = threadIdx.x & 63;
     if (keep <= 0) return;
     if (n <= keep) {
-        for (int i = lane; i < n; i += 64) dst[i] = list[i];
+        wave_copy_in(dst, list, n);
         return;
     }
     if (n > W.cap) {  // sequential replay on global memory
@@ -1208,7 +1229,7 @@ __device__ __forceinline__ void wave_retain_to(const SelWave<E>& W, E* list, int
         for (int i = lane; i < keep; i += 64) dst[i] = list[i];
         return;
     }
-    for (int i = lane; i < n; i += 64) W.a[i] = list[i];
+    wave_copy_in(W.a, list, n);
     wave_sync();
     wave_nth_element(W, keep - 1, n);
     for (int i = lane; i < keep; i += 64) dst[i] = W.a[i];
@@ -1312,13 +1333,14 @@ __global__ __launch_bounds__(64 * SEL_CW) void k_select_cells(LevelGeom g, const
     int* keep = cnt + maxnc;
     int* off = keep + maxnc;  // maxnc + 1
     uint8_t* flag = reinterpret_cast<uint8_t*>(off + maxnc + 1);
-    const int l = cells[c].level;
+    const CellInfo me = cells[c];  // level and list offset in one load batch (the list address waits on nothing else)
+    const int l = me.level;
     const int cb = g.cell_begin[l], nc = g.cell_begin[l + 1] - cb, ci = c - cb;
     wave_quota(counts + (long long)f * g.ncells + cb, cells + cb, nc, g.nfcell[l], cnt, keep, off, flag);
     E* L = lvl_lists + (long long)f * lvl_stride + g.lvl_off[l];
     if (ci == 0 && lane == 0) lvl_counts[(long long)f * g.nlevels + l] = off[nc];
     if (keep[ci] > 0) {
-        E* a = lists + (long long)f * list_stride + cells[c].cap_off;
+        E* a = lists + (long long)f * list_stride + me.cap_off;
         wave_retain_to(W, a, cnt[ci], keep[ci], L + off[ci]);
     }
 }
@@ -1340,7 +1362,7 @@ __global__ __launch_bounds__(64) void k_select_level(LevelGeom g, E* __restrict_
     int* out = lvl_counts + (long long)f * g.nlevels + l;
     const int total = *out, nd = g.ndesired[l];
     if (nd >= 0 && total > nd && nd > 0 && total <= SEL_BUF) {
-        for (int i = lane; i < total; i += 64) W.a[i] = L[i];
+        wave_copy_in(W.a, L, total);
         wave_sync();
         wave_nth_element(W, nd - 1, total);
         for (int i = lane; i < nd; i += 64) L[i] = W.a[i];
