@@ -849,6 +849,91 @@ __device__ __forceinline__ void fc_sync() {
     }
 }
 
+// k_fast_cells' LDS: the window's score rows realigned to column 0, with a
+// zero row above and below and a zero dword either side (the 3x3 NMS reads
+// its out-of-window neighbours as 0, as FAST's row buffers hold 0 there);
+// survivor bits per window row in whole 32-bit words; the retry's ROI.
+struct FcLayout {
+    int nq, ndw, pitch, wpr, nwords;
+    size_t sc_bytes, bits_bytes, total;
+};
+__host__ __device__ inline FcLayout fc_layout(int dw, int dh, int w, int h) {
+    FcLayout L;
+    L.nq = (dw + 3) / 4;  // dwords of window columns per row
+    L.ndw = L.nq + 2;
+    L.pitch = 4 * L.ndw;
+    L.wpr = (dw + 31) / 32;
+    L.nwords = dh * L.wpr;
+    L.sc_bytes = (size_t)(dh + 2) * L.pitch;
+    L.bits_bytes = 4 * (size_t)((L.nwords + 3) & ~3);
+    L.total = L.sc_bytes + L.bits_bytes + (size_t)w * h;
+    return L;
+}
+
+// 3x3 strict NMS over k_fast_cells' realigned window, four columns per lane
+// (lane L: columns 4L .. 4L + 3) on packed 16-bit lanes: per row the dwords
+// L - 1, L, L + 1 give the even columns E = (4L, 4L + 2), the odd O = (4L + 1,
+// 4L + 3) and their left / right neighbour pairs EL = (4L - 1, 4L + 1), OR =
+// (4L + 2, 4L + 4). The map entries m count only when m > t1 = max(th, 1)
+// (FAST's buffer value at th, see cell_nms_bits): m' = sat(m - t1) keeps their
+// order and sends the others to 0, so "m > every counted neighbour and m
+// counted" is m' > the neighbours' max m'. Wave w takes window rows [w dh / NW,
+// (w + 1) dh / NW); one pass covers 256 columns. Returns the wave's survivors.
+template <int NWV>
+__device__ __forceinline__ int cell_nms4(const uint32_t* sc32, const FcLayout& Ly, uint32_t* bits, int dh, int th) {
+    typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int ya = wv * dh / NWV, yb = (wv + 1) * dh / NWV;
+    const unsigned short t1 = (unsigned short)max(th, 1);
+    const u2 T = {t1, t1}, ONE = {1, 1};
+    auto U = [](uint32_t v) { return __builtin_bit_cast(u2, v); };
+    struct Q {
+        u2 e, o, el, orr;
+    };
+    int cnt = 0;
+    for (int L0 = 0; L0 < Ly.nq; L0 += 64) {
+        const int L = L0 + lane;
+        const bool okq = L < Ly.nq;
+        const uint32_t* col = sc32 + min(L, Ly.nq - 1);  // clamped lanes read the row's last words (dropped)
+        auto rowq = [&](int r) -> Q {  // LDS row r = window row r - 1
+            const uint32_t* q = col + r * Ly.ndw;
+            const uint32_t a = q[0], b = q[1], c = q[2];
+            Q x;
+            x.e = __builtin_elementwise_sub_sat(U(__builtin_amdgcn_perm(0u, b, 0x0c020c00u)), T);
+            x.o = __builtin_elementwise_sub_sat(U(__builtin_amdgcn_perm(0u, b, 0x0c030c01u)), T);
+            x.el = __builtin_elementwise_sub_sat(U(__builtin_amdgcn_perm(a, b, 0x0c010c07u)), T);
+            x.orr = __builtin_elementwise_sub_sat(U(__builtin_amdgcn_perm(c, b, 0x0c040c02u)), T);
+            return x;
+        };
+        uint32_t* brow = bits + ya * Ly.wpr + (L >> 3);
+        const int sh = 4 * (L & 7);
+        // rows y - 1, y, y + 1 in u, c, d; unrolled by three so the roles
+        // rotate by naming
+        auto step = [&](int y, const Q& u, const Q& c, Q& d) {
+            d = rowq(y + 2);
+            const u2 vE = __builtin_elementwise_max(u.e, d.e), vO = __builtin_elementwise_max(u.o, d.o);
+            const u2 vEL = __builtin_elementwise_max(u.el, d.el), vOR = __builtin_elementwise_max(u.orr, d.orr);
+            const u2 mxE = __builtin_elementwise_max(__builtin_elementwise_max(vE, vEL),
+                                                     __builtin_elementwise_max(vO, __builtin_elementwise_max(c.el, c.o)));
+            const u2 mxO = __builtin_elementwise_max(__builtin_elementwise_max(vO, vOR),
+                                                     __builtin_elementwise_max(vE, __builtin_elementwise_max(c.e, c.orr)));
+            const u2 kE = __builtin_elementwise_min(__builtin_elementwise_sub_sat(c.e, mxE), ONE);
+            const u2 kO = __builtin_elementwise_min(__builtin_elementwise_sub_sat(c.o, mxO), ONE);
+            const uint32_t t = __builtin_bit_cast(uint32_t, kE) | (__builtin_bit_cast(uint32_t, kO) << 1);
+            const uint32_t m = okq ? ((t & 3u) | ((t >> 14) & 12u)) : 0u;  // bit i: column 4L + i
+            if (m) atomicOr(brow + (y - ya) * Ly.wpr, m << sh);
+            cnt += __popc(m);
+        };
+        Q q0 = rowq(ya), q1 = rowq(ya + 1), q2;
+        for (int y = ya; y < yb; y += 3) {
+            step(y, q0, q1, q2);
+            if (y + 1 < yb) step(y + 1, q1, q2, q0);
+            if (y + 2 < yb) step(y + 2, q2, q0, q1);
+        }
+    }
+    return gfd::warp_sum(cnt);
+}
+
 template <typename E>
 __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, const uint8_t* __restrict__ score,
                                                     const CellInfo* __restrict__ cells, E* __restrict__ lists,
@@ -868,40 +953,49 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         if (tid == 0) counts[(long long)f * g.ncells + cid] = 0;
         return;
     }
-    const int n = dw * dh, nwords = (n + 31) >> 5;
-    const int ndw = (dw + 6) >> 2, pitch = 4 * ndw;  // dwords per row: dw bytes at any alignment
-    uint8_t* sc = smem;                                                   // (dh + 1) x pitch, row dh zeros
-    uint8_t* rsh = sc + (dh + 1) * pitch;                                  // dh + 1 row shifts
-    uint32_t* bits = reinterpret_cast<uint32_t*>(rsh + ((dh + 16) & ~15));  // survivor bits
+    const FcLayout Ly = fc_layout(dw, dh, ci.w, ci.h);
+    uint8_t* sc = smem;  // window row y, column x at (y + 1) * pitch + 4 + x
+    uint32_t* sc32 = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(smem + Ly.sc_bytes);  // window row y: words y * wpr ..
     const int l = ci.level, lw = g.pw[l];
     const uint8_t* SC = score + (long long)f * g.bslab + g.boff[l] + (long long)(ci.y0 + 3) * lw + ci.x0 + 3;
-    // the window as aligned dwords (a cell window is a few hundred dwords: two
-    // loads per thread in flight before the LDS writes)
-    constexpr int FC_LB = 2;
-    for (int i0 = 0; i0 < dh * ndw; i0 += FC_NT * FC_LB) {
-        uint32_t v[FC_LB];
+    {  // the window realigned: every row of the pitched map has SC's byte shift.
+        // Thread t owns LDS dword column j = t % ndw of rows t / ndw + k rstep,
+        // so a row's address is one step from the last (no index split per load)
+        const uint32_t sh = (uint32_t)((uintptr_t)SC & 3u);
+        const uint32_t* SCa = reinterpret_cast<const uint32_t*>((uintptr_t)SC & ~(uintptr_t)3);
+        const int lw4 = lw >> 2, nrows = dh + 2;
+        const int ndw = Ly.ndw, rstep = max(FC_NT / ndw, 1);
+        const int j = tid % ndw, r0 = tid / ndw;
+        const bool jdata = j >= 1 && j <= Ly.nq;
+        uint32_t bmask = ~0u;  // the window's bytes of this dword column
+        if (jdata && dw - 4 * (j - 1) < 4) bmask = (1u << (8 * (dw - 4 * (j - 1)))) - 1u;
+        constexpr int FC_LB = 8;  // rows per thread in flight
+        for (int rb = r0; rb < nrows; rb += FC_LB * rstep) {  // ndw <= FC_NT (host: wider windows go to k_fast_cells_band)
+            // loads unconditional at clamped (in-window) addresses, the pads
+            // selected after them: a load behind a branch would have its
+            // result merged before the next one issues (a wait per row)
+            uint32_t lo[FC_LB], hi[FC_LB];
+            const int jc = min(max(j, 1), Ly.nq) - 1;
 #pragma unroll
-        for (int k = 0; k < FC_LB; k++) {
-            const int i = i0 + FC_NT * k + tid;
-            const int r = pyr_div(i, 1.0f / (float)ndw), q = i - r * ndw;
-            v[k] = 0;
-            if (r < dh) {
-                const uintptr_t a = (uintptr_t)(SC + (long long)r * lw);
-                if (4 * q < (int)(a & 3) + dw) v[k] = gfd::ldg(reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) + q);
+            for (int k = 0; k < FC_LB; k++) {
+                const int rc = min(max(rb + k * rstep, 1), dh) - 1;
+                const uint32_t* src = SCa + (long long)rc * lw4 + jc;
+                lo[k] = gfd::ldg(src);
+                hi[k] = gfd::ldg(src + 1);
+            }
+#pragma unroll
+            for (int k = 0; k < FC_LB; k++) {
+                const int r = rb + k * rstep;
+                const bool data = jdata && r >= 1 && r <= dh;
+                if (r < nrows && r0 < rstep)
+                    sc32[r * ndw + j] = data ? __builtin_amdgcn_alignbyte(hi[k], lo[k], sh) & bmask : 0u;
             }
         }
-#pragma unroll
-        for (int k = 0; k < FC_LB; k++) {
-            const int i = i0 + FC_NT * k + tid;
-            if (i < dh * ndw) reinterpret_cast<uint32_t*>(sc)[i] = v[k];
-        }
     }
-    for (int r = tid; r < dh; r += FC_NT) rsh[r] = (uint8_t)((uintptr_t)(SC + (long long)r * lw) & 3);
-    if (tid == 0) rsh[dh] = 0;
-    for (int i = tid; i < ndw; i += FC_NT) reinterpret_cast<uint32_t*>(sc + dh * pitch)[i] = 0u;
-    for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
+    for (int i = tid; i < Ly.nwords; i += FC_NT) bits[i] = 0;
     fc_sync();
-    int c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, fast_th);
+    int c = cell_nms4<FC_NW>(sc32, Ly, bits, dh, fast_th);
     if ((tid & 63) == 0) s_cnt[0][tid >> 6] = c;
     fc_sync();
     int total = 0;
@@ -909,7 +1003,7 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     for (int k = 0; k < FC_NW; k++) total += s_cnt[0][k];
     if (total <= 3) {  // ORBextractor.cc:623-628: retry with the minimum threshold
         // the ROI (window + 3-px ring margin) of the unblurred level to LDS
-        uint8_t* roi = reinterpret_cast<uint8_t*>(bits + ((nwords + 3) & ~3));
+        uint8_t* roi = smem + Ly.sc_bytes + Ly.bits_bytes;
         int sstride;
         const uint8_t* Sl = level_plane(P, g, f, l, sstride) + (long long)ci.y0 * sstride + ci.x0;
         for (int i = tid; i < ci.w * ci.h; i += FC_NT) {
@@ -917,16 +1011,16 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
             roi[i] = gfd::ldg(Sl + (long long)r * sstride + (i - r * ci.w));
         }
         fc_sync();
-        for (int i = tid; i < n; i += FC_NT) {
+        for (int i = tid; i < dw * dh; i += FC_NT) {
             const int y = pyr_div(i, 1.0f / (float)dw), x = i - y * dw;
-            int c[16];
-            circle_vals(roi, ci.w, x + 3, y + 3, c);
-            const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], c);
-            sc[y * pitch + rsh[y] + x] = M > min_th ? (uint8_t)M : 0;
+            int cv[16];
+            circle_vals(roi, ci.w, x + 3, y + 3, cv);
+            const int M = fast_max_arc(roi[(y + 3) * ci.w + x + 3], cv);
+            sc[(y + 1) * Ly.pitch + 4 + x] = M > min_th ? (uint8_t)M : 0;
         }
-        for (int i = tid; i < nwords; i += FC_NT) bits[i] = 0;
+        for (int i = tid; i < Ly.nwords; i += FC_NT) bits[i] = 0;
         fc_sync();
-        c = cell_nms_bits<FC_NW>(sc, rsh, pitch, bits, dw, dh, min_th);
+        c = cell_nms4<FC_NW>(sc32, Ly, bits, dh, min_th);
         if ((tid & 63) == 0) s_cnt[1][tid >> 6] = c;
         fc_sync();
         total = 0;
@@ -936,9 +1030,9 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
     E* out = lists + (long long)f * list_stride + ci.cap_off;
     const int X0 = ci.x0 + 3, Y0 = ci.y0 + 3;
     int base = 0;
-    for (int w0 = 0; w0 < nwords; w0 += FC_NT) {
+    for (int w0 = 0; w0 < Ly.nwords; w0 += FC_NT) {  // words in row-major order: the survivors in FAST's order
         const int i = w0 + tid;
-        uint32_t word = i < nwords ? bits[i] : 0u;
+        uint32_t word = i < Ly.nwords ? bits[i] : 0u;
         int tot;
         int off;
         if constexpr (FC_NT == 64) {
@@ -946,11 +1040,14 @@ __global__ __launch_bounds__(FC_NT) void k_fast_cells(Planes P, LevelGeom g, con
         } else {
             off = base + block_scan_nw<FC_NW>(__popc(word), scan_tmp, tot);
         }
-        while (word) {
-            const int p = 32 * i + __ffs(word) - 1;
-            word &= word - 1;
-            const int y = pyr_div(p, 1.0f / (float)dw), x = p - y * dw;
-            out[off++] = cell_entry<E>(sc[y * pitch + rsh[y] + x] - 1, X0 + x, Y0 + y, P, g, f, l);
+        if (word) {
+            const int y = i / Ly.wpr, xw = 32 * (i - y * Ly.wpr);
+            const uint8_t* srow = sc + (y + 1) * Ly.pitch + 4;
+            while (word) {
+                const int x = xw + __ffs(word) - 1;
+                word &= word - 1;
+                out[off++] = cell_entry<E>(srow[x] - 1, X0 + x, Y0 + y, P, g, f, l);
+            }
         }
         base += tot;
     }
@@ -1777,9 +1874,9 @@ static int plan_extractor(gf_extractor* ex) {
                         cap_off += ci.cap;
                         lvl_cap += ci.cap;
                         const size_t pitch = 4 * (size_t)((dw + 6) / 4), bits = 16 * (((size_t)dw * dh + 127) / 128);
-                        size_t lds = ((size_t)dh + 1) * pitch + (((size_t)dh + 16) & ~(size_t)15) + bits +
-                                     (size_t)ci.w * ci.h;
-                        if (lds <= FC_LDS_MAX) {
+                        const FcLayout fl = fc_layout(dw, dh, ci.w, ci.h);
+                        const size_t lds = fl.total;
+                        if (lds <= FC_LDS_MAX && fl.ndw <= FC_NT) {
                             max_lds = std::max(max_lds, lds);
                         } else {  // k_fast_cells_band: bands of BH rows (halo rows, ROI rows of the retry)
                             auto band_lds = [&](size_t bh) {

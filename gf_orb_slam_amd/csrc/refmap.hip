@@ -55,8 +55,11 @@ struct RefArgs {
 // footprint, 74 KB, kept the other stream groups' workgroups off the CU.)
 size_t rm_lds_bytes(int kfc) {
     const size_t a = ((size_t)(kfc + 1) * 4 + 15) & ~(size_t)15, b = ((size_t)kfc * 4 + 15) & ~(size_t)15;
-    return a + b + (size_t)kfc;
+    return a + b + (((size_t)kfc + 15) & ~(size_t)15) + b;  // + the local keyframes' first map-point slots
 }
+
+// map-point slots per thread kept in registers across the three slot passes
+constexpr int RM_SC = 8;
 
 // exclusive scan over the workgroup (16 waves); total returned in `total`
 __device__ int scan_1024(int v, int* tmp, int& total) {
@@ -87,6 +90,7 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     int* cnt = reinterpret_cast<int*>(rm_lds);  // votes, then the slot offsets of the local keyframes
     int* lkf = reinterpret_cast<int*>(rm_lds + (((size_t)(A.kfc + 1) * 4 + 15) & ~(size_t)15));  // local keyframes
     uint8_t* mark = reinterpret_cast<uint8_t*>(lkf) + (((size_t)A.kfc * 4 + 15) & ~(size_t)15);
+    int* kb = reinterpret_cast<int*>(mark + (((size_t)A.kfc + 15) & ~(size_t)15));  // kf_mp_off of local keyframe p
     __shared__ int tmp[RM_T / 64];
     __shared__ unsigned long long s_best;
     __shared__ int s_nl;
@@ -168,11 +172,17 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
         A.n_local_kfs[f] = nl;
         A.ref_kf[f] = s_best ? 0x7fffffff - (int)(unsigned)(s_best & 0xffffffffu) : -1;
     }
-    // 4. map points: slot offsets of the local keyframes (cnt reused)
+    // 4. map points: slot offsets of the local keyframes (cnt reused), their
+    // first kf_mp index in kb
     int total = 0;
     for (int p0 = 0; p0 < nl; p0 += RM_T) {
         const int p = p0 + tid;
-        const int len = p < nl ? M.kf_mp_off[lkf[p] + 1] - M.kf_mp_off[lkf[p]] : 0;
+        int len = 0;
+        if (p < nl) {
+            const int o0 = M.kf_mp_off[lkf[p]];
+            len = M.kf_mp_off[lkf[p] + 1] - o0;
+            kb[p] = o0;
+        }
         int tot;
         const int off = total + scan_1024(len, tmp, tot);
         if (p < nl) cnt[p] = off;
@@ -181,8 +191,8 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     if (tid == 0) cnt[nl] = total;
     __syncthreads();
     int32_t* first = A.first + (size_t)f * A.first_stride;
-    auto slot_mp = [&](int q) -> int {  // map point of sequence position q
-        int lo = 0, hi = nl - 1;        // last p with cnt[p] <= q
+    auto slot_idx = [&](int q) -> int {  // kf_mp index of sequence position q
+        int lo = 0, hi = nl - 1;          // last p with cnt[p] <= q
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (cnt[mid] <= q)
@@ -190,27 +200,70 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
             else
                 hi = mid - 1;
         }
-        return M.kf_mp[M.kf_mp_off[lkf[lo]] + (q - cnt[lo])];
+        return kb[lo] + (q - cnt[lo]);
     };
-    for (int q = tid; q < total; q += RM_T) {
-        const int m = slot_mp(q);
+    auto slot_mp = [&](int q) -> int { return M.kf_mp[slot_idx(q)]; };
+    // the thread's slots q = tid + RM_T k: map point and bad flag loaded once,
+    // all in flight together (the passes below were each a chain of
+    // dependent loads per slot); past RM_SC slots per thread, looked up per pass
+    const int nch = (total + RM_T - 1) / RM_T;
+    int mq[RM_SC];
+    bool bq[RM_SC];
+    if (total > 0) {  // loads at clamped indices, unconditional (a load behind a branch waits before the next)
+        int ix[RM_SC];
+#pragma unroll
+        for (int k = 0; k < RM_SC; k++) ix[k] = slot_idx(min(tid + RM_T * k, total - 1));
+#pragma unroll
+        for (int k = 0; k < RM_SC; k++) mq[k] = M.kf_mp[ix[k]];
+#pragma unroll
+        for (int k = 0; k < RM_SC; k++) bq[k] = M.nmp > 0 ? M.mp_bad[min(max(mq[k], 0), M.nmp - 1)] != 0 : true;
+#pragma unroll
+        for (int k = 0; k < RM_SC; k++)
+            if (tid + RM_T * k >= total) mq[k] = -1;
+    } else {
+#pragma unroll
+        for (int k = 0; k < RM_SC; k++) {
+            mq[k] = -1;
+            bq[k] = true;
+        }
+    }
+    auto slot = [&](int k, int q, int& m, bool& bad) {
+        if (k < RM_SC) {
+#pragma unroll
+            for (int u = 0; u < RM_SC; u++)
+                if (u == k) {
+                    m = mq[u];
+                    bad = bq[u];
+                }
+        } else {
+            m = q < total ? slot_mp(q) : -1;
+            bad = m < 0 || M.mp_bad[m];
+        }
+    };
+    for (int k = 0; k < nch; k++) {
+        int m;
+        bool bad;
+        slot(k, tid + RM_T * k, m, bad);
         if (m >= 0) first[m] = INT_MAX;
     }
     __syncthreads();
-    for (int q = tid; q < total; q += RM_T) {
-        const int m = slot_mp(q);
-        if (m >= 0 && !M.mp_bad[m]) atomicMin(&first[m], q);
+    for (int k = 0; k < nch; k++) {
+        const int q = tid + RM_T * k;
+        int m;
+        bool bad;
+        slot(k, q, m, bad);
+        if (m >= 0 && !bad) atomicMin(&first[m], q);
     }
     __syncthreads();
     int32_t* omp = A.local_mps + (size_t)f * A.mp_cap;
     int nm = 0;
-    for (int q0 = 0; q0 < total; q0 += RM_T) {
-        const int q = q0 + tid;
-        int m = -1;
-        if (q < total) m = slot_mp(q);
+    for (int k = 0; k < nch; k++) {
+        const int q = tid + RM_T * k;
+        int m;
+        bool bad;
+        slot(k, q, m, bad);
         // (an L2-coherent read: the atomics above executed there)
-        const bool keep = m >= 0 && !M.mp_bad[m] &&
-                          __hip_atomic_load(&first[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q;
+        const bool keep = m >= 0 && !bad && __hip_atomic_load(&first[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == q;
         int tot;
         const int pos = nm + scan_1024(keep ? 1 : 0, tmp, tot);
         if (keep && pos < A.mp_cap) omp[pos] = m;
