@@ -1534,17 +1534,19 @@ __global__ __launch_bounds__(256) void k_describe(Planes P, LevelGeom g, const E
     // bit * 32 + i): the 32 lanes of a half read 32 consecutive dwords
     __shared__ uint32_t sh_pat[256];
     __shared__ uint32_t sh_ictab[256];  // IC_Angle's row weights and masks (c_ic_tab)
+    int bx, f;
+    gfd::xcd_block(bx, f);
+    int cnt[GF_MAX_LEVELS];  // all level counts in one batch of loads, in flight with the tables'
+#pragma unroll
+    for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = lvl_counts[(long long)f * g.nlevels + min(i, g.nlevels - 1)];
     sh_pat[(threadIdx.x & 7) * 32 + (threadIdx.x >> 3)] = c_pattern8[threadIdx.x];
     sh_ictab[threadIdx.x] = c_ic_tab[threadIdx.x];
     __syncthreads();
-    int bx, f;
-    gfd::xcd_block(bx, f);
+#pragma unroll
+    for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = i < g.nlevels ? cnt[i] : 0;
     const int lane = threadIdx.x & 63, hl = lane & 31, half = (threadIdx.x >> 5);  // half = slot 0..7
     DescLds& W = sh_all[half];
     const int k = bx * 8 + half;
-    int cnt[GF_MAX_LEVELS];  // all level counts in one batch of loads
-#pragma unroll
-    for (int i = 0; i < GF_MAX_LEVELS; i++) cnt[i] = i < g.nlevels ? lvl_counts[(long long)f * g.nlevels + i] : 0;
     int total = 0, l = -1, idx = 0;
 #pragma unroll
     for (int i = 0; i < GF_MAX_LEVELS; i++) {

@@ -717,34 +717,51 @@ __global__ __launch_bounds__(TL_T) void k_track_gate(gf::TrackLossArgs A) {
 // left (GF_TR_OK = 0): a small grid of one-wave workgroups walks the streams,
 // since each workgroup holds a whole SIMD's registers and most steps have no
 // such stream.
-__global__ __launch_bounds__(TL_T) void k_track_loss(gf::TrackLossArgs A) {
+#ifndef TL_WAVES_PER_EU
+#define TL_WAVES_PER_EU 2
+#endif
+// TL_WAVES_PER_EU 2 caps the kernel at 256 registers (the rest spills to
+// scratch on this rare path), so its no-op waves need half a SIMD's register
+// file instead of all of it to be dispatched beside the other groups' kernels
+__global__ __launch_bounds__(TL_T) __attribute__((amdgpu_waves_per_eu(TL_WAVES_PER_EU))) void k_track_loss(
+    gf::TrackLossArgs A) {
     __shared__ TLShared S;
     const int lane = threadIdx.x, cap = A.cap;
-    for (int b = blockIdx.x; b < A.B; b += gridDim.x) {
-        int32_t* T = A.track + (size_t)b * GF_TR_N;
-        if (T[GF_TR_OK]) continue;
-        const int path = T[GF_TR_PATH];
-        const bool ok = path == 3 ? relocalise(A, b, S) : track_previous_frame(A, b, S);
-        // nMatchesFound / num_to_match of the frame's matches (Tracking.cc:3195-3228)
-        const int n = A.nkp[b];
-        int c = 0;
-        for (int i = lane; i < n; i += TL_T) c += A.kp2mp[(size_t)b * cap + i] >= 0;
-        c = gfd::warp_sum(c);
-        if (lane == 0) {
-            stat_of(A, GF_ST_FOUND)[b] = c;
-            stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
-            T[GF_TR_OK] = ok;
-            int fl = stat_of(A, GF_ST_FLAGS)[b];
-            fl |= path == 3 ? 4096 : 2048;
-            if (!ok) fl |= 8192;
-            if (path == 3 && ok) {
-                fl |= 32768;
-                T[GF_TR_SINCE] = 0;  // mnLastRelocFrameId = mCurrentFrame.mnId
+    // this workgroup's streams (b = blockIdx.x mod gridDim.x): their OK flags
+    // read 64 at a time by the lanes and the ones still open walked in order
+    // (a stream-by-stream scan paid one dependent load per stream when none
+    // is open, the common case)
+    for (int b0 = 0; b0 < A.B; b0 += 64 * (int)gridDim.x) {
+        const int bl = b0 + (int)gridDim.x * lane + (int)blockIdx.x;
+        const bool open = bl < A.B && !A.track[(size_t)bl * GF_TR_N + GF_TR_OK];
+        unsigned long long todo = __ballot(open);
+        while (todo) {
+            const int b = b0 + (int)gridDim.x * (__ffsll((long long)todo) - 1) + (int)blockIdx.x;
+            todo &= todo - 1;
+            int32_t* T = A.track + (size_t)b * GF_TR_N;
+            const int path = T[GF_TR_PATH];
+            const bool ok = path == 3 ? relocalise(A, b, S) : track_previous_frame(A, b, S);
+            // nMatchesFound / num_to_match of the frame's matches (Tracking.cc:3195-3228)
+            const int n = A.nkp[b];
+            int c = 0;
+            for (int i = lane; i < n; i += TL_T) c += A.kp2mp[(size_t)b * cap + i] >= 0;
+            c = gfd::warp_sum(c);
+            if (lane == 0) {
+                stat_of(A, GF_ST_FOUND)[b] = c;
+                stat_of(A, GF_ST_TO_MATCH)[b] = A.budget - c;
+                T[GF_TR_OK] = ok;
+                int fl = stat_of(A, GF_ST_FLAGS)[b];
+                fl |= path == 3 ? 4096 : 2048;
+                if (!ok) fl |= 8192;
+                if (path == 3 && ok) {
+                    fl |= 32768;
+                    T[GF_TR_SINCE] = 0;  // mnLastRelocFrameId = mCurrentFrame.mnId
+                }
+                stat_of(A, GF_ST_FLAGS)[b] = fl;
+                set_gates(A, b, ok, T[GF_TR_SINCE]);
             }
-            stat_of(A, GF_ST_FLAGS)[b] = fl;
-            set_gates(A, b, ok, T[GF_TR_SINCE]);
+            __syncthreads();  // the LDS goes to the next stream
         }
-        __syncthreads();  // the LDS goes to the next stream
     }
 }
 
