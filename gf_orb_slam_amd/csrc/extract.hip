@@ -239,6 +239,31 @@ __global__ __launch_bounds__(PYR_NT) void k_pyramid(Planes P, LevelGeom g, PyrGe
         const uint8_t* S = level_plane(P, g, f, 0, stride) + sx.lo;
         uint32_t* A = reinterpret_cast<uint32_t*>(pyr_lds);
         constexpr int LB = 8;  // dwords per thread per batch, all in flight
+        if ((stride & 3) == 0 && ndw <= PYR_NT) {
+            // rows share one byte shift: thread t owns dword column t % ndw of
+            // rows t / ndw + k rstep, one multiply-add from row to row
+            const int q = tid % ndw, r0 = tid / ndw, rstep = PYR_NT / ndw;
+            // (a column past the span loads the span's last dword and stores 0)
+            const uintptr_t a0 = (uintptr_t)(S + sy.lo * stride) + 4 * min(q, (w0 - 1) >> 2);
+            const uint32_t sh = (uint32_t)(a0 & 3);
+            const bool col = r0 < rstep && 4 * q < w0, two = col && sh != 0 && 4 * q + 4 - (int)sh < w0;
+            const uint32_t* c0 = reinterpret_cast<const uint32_t*>(a0 & ~(uintptr_t)3);
+            const int s4 = stride >> 2;
+            for (int rb = r0; rb < nr; rb += LB * rstep) {
+                uint32_t lo[LB], hi[LB];
+#pragma unroll
+                for (int k = 0; k < LB; k++) {  // unconditional loads at clamped rows
+                    const uint32_t* p = c0 + (long long)min(rb + k * rstep, nr - 1) * s4;
+                    lo[k] = gfd::ldg(p);
+                    hi[k] = gfd::ldg(p + (two ? 1 : 0));
+                }
+#pragma unroll
+                for (int k = 0; k < LB; k++) {
+                    const int r = rb + k * rstep;
+                    if (r0 < rstep && r < nr) A[r * ndw + q] = col ? __builtin_amdgcn_alignbyte(hi[k], lo[k], sh) : 0u;
+                }
+            }
+        } else
         for (int i0 = 0; i0 < nr * ndw; i0 += PYR_NT * LB) {
             uint32_t lo[LB], hi[LB], sh[LB];
 #pragma unroll

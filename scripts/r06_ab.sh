@@ -13,7 +13,7 @@ if [ -n "$TESTS" ]; then
 fi
 ARGS="--no-cpu-baseline --lba-batch 0 --config3-steps 0 --budget-steps 0 --pcie-steps 0 --isolated-steps 0 --time-log-steps 0 ${BENCH_ARGS}"
 for v in ${VARS//,/ }; do
-  case $v in product*) lib="";; *) lib=$R/gf_orb_slam_amd/diag/libgfslam_${v}.so;; esac
+  case $v in product*) lib="";; base*) lib=$R/gf_orb_slam_amd/diag/libgfslam_base.so;; *) lib=$R/gf_orb_slam_amd/diag/libgfslam_${v}.so;; esac
   GF_LIB=$lib timeout -k 10 400 python bench.py $ARGS --detail-out $R/$O/$v.json --kernel-trace-dir $R/$O/kt_$v > $O/$v.line 2> $O/$v.err || { tail -20 $O/$v.err; exit 11; }
   rm -f $O/kt_$v/*kernel_trace.csv
   python - "$O/$v.json" "$v" <<'PY'
