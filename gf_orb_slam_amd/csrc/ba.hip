@@ -1771,8 +1771,14 @@ int gf_ba_plan_solve_stop(gf_ba_plan* P, void* stream, const volatile uint8_t* s
         GF_LAUNCH(k_ba_init, P->nprob, 256, 0, s, P->A);
         GF_HIP(hipGetLastError());
     }
+    // Steps are enqueued blindly in chunks (a finished problem's kernels
+    // return at once) and the state is read back after each chunk. The first
+    // chunk covers the usual optimize(5) + optimize(10) run (15 iterations,
+    // one trial each), the later ones are short; every chunk ends with the
+    // output conversion (idempotent), so the chunk that finishes the last
+    // problem needs no further launch and wait. A host round trip costs about
+    // as much as two no-op steps.
     int n = 0;
-    const int chunk = 4;
     bool done = false;
     while (!done) {
         GF_CHECK(n < BA_MAXSTEPS, GF_ERR_HIP, "local BA did not terminate");
@@ -1781,21 +1787,21 @@ int gf_ba_plan_solve_stop(gf_ba_plan* P, void* stream, const volatile uint8_t* s
             GF_HIP(hipMemcpyAsync(P->d_stop, &one, sizeof(int), hipMemcpyHostToDevice, s));
             stop_sent = true;
         }
+        const int chunk = n == 0 ? 12 : 4;
         for (int c = 0; c < chunk; c++, n++) {
             int rc = ba_launch_step(P, s);
             if (rc) return rc;
+        }
+        {
+            GF_PROF(P->ctx, s, "k_ba_finish");
+            GF_LAUNCH(k_ba_finish, P->nprob, 256, 0, s, P->A);
+            GF_HIP(hipGetLastError());
         }
         GF_HIP(hipMemcpyAsync(P->h_state, P->A.st, sizeof(BAState) * P->nprob, hipMemcpyDeviceToHost, s));
         GF_HIP(hipStreamSynchronize(s));
         done = true;
         for (int p = 0; p < P->nprob; p++) done = done && P->h_state[p].round >= 2;
     }
-    {
-        GF_PROF(P->ctx, s, "k_ba_finish");
-        GF_LAUNCH(k_ba_finish, P->nprob, 256, 0, s, P->A);
-        GF_HIP(hipGetLastError());
-    }
-    GF_HIP(hipStreamSynchronize(s));
     if (steps) *steps = n;
     return GF_OK;
 }
