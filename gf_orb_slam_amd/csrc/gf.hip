@@ -1069,6 +1069,11 @@ __device__ int wave_top(const Cands& C, const int16_t* al, int na, int sz, int n
 #ifndef AM_SORTED_WIDE
 #define AM_SORTED_WIDE 1
 #endif
+// AM_WOCT: the commit's per-octave weight from LDS (made at kernel start)
+// instead of a kernel-argument load, a square root and a division per claim
+#ifndef AM_WOCT
+#define AM_WOCT 1
+#endif
 #ifndef AM_SB
 #define AM_SB 16  // slot_loop: live / window scores per batch of broadcast reads
 #endif
@@ -1139,6 +1144,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
 #ifdef AM_LSIG  // diagnostic: the level sigma^2 from an LDS copy at the commit
     __shared__ float s_sig2[16];
 #endif
+#if AM_WOCT
+    __shared__ double s_woct[16];
+#endif
 #if AM_SLOTS
     __shared__ __align__(16) double s_lsc[64];  // slot_loop: live scores, lane order (-inf past sz)
     __shared__ __align__(16) double s_xsc[64];  // slot_loop: the window's scores (-inf past W)
@@ -1186,6 +1194,12 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
     for (int i = lane; i < n; i += AW) claim[i] = kp2mp[i];
 #ifdef AM_LSIG
     if (lane < 16) s_sig2[lane] = A.sigma2[lane];
+#endif
+#if AM_WOCT
+    if (lane < 16) {  // the commit's weight per octave, s2 / (s2 s2) with s2 = sqrt(sigma^2), made once
+        const double s2 = sqrt((double)A.sigma2[lane]);
+        s_woct[lane] = s2 / (s2 * s2);
+    }
 #endif
     const int32_t* rmp = A.remap ? A.remap + (long long)f * A.mp_cap : nullptr;
     // a slot's info / H row: staged at the pool build, or read through the remap
@@ -1927,6 +1941,9 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             A.score[(long long)f * A.kp_cap + b] = C.dist[top] & 0xfff;
         }
         if (lane < 49) {  // curMat += H_rw^T H_rw (sigma^2 of the matched keypoint octave)
+#if AM_WOCT
+            const double w = s_woct[oct_b];  // the same arithmetic, done at kernel start
+#else
 #ifdef AM_LSIG
             const double s2 = sqrt((double)s_sig2[oct_b]);
 #ifdef GF_AM_CHECK
@@ -1936,6 +1953,7 @@ __device__ __forceinline__ void active_match_body(const ActiveArgs& A, const int
             const double s2 = sqrt((double)A.sigma2[oct_b]);
 #endif
             const double w = s2 / (s2 * s2);
+#endif
             const double a0 = w * h_i, a1 = w * h_j, b0 = w * h_7i, b1 = w * h_7j;
             cur[lane] = cur[lane] + (a0 * a1 + b0 * b1);
         }
