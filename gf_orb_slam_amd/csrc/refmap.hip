@@ -53,9 +53,13 @@ struct RefArgs {
 // offsets [kfc + 1], local keyframes [kfc], marks [kfc]. (Sized per launch:
 // the front end's graphs hold at most 64 keyframes, and a fixed 8192-keyframe
 // footprint, 74 KB, kept the other stream groups' workgroups off the CU.)
+// voted keyframes whose first 10 covisible neighbours are staged in LDS for
+// the neighbour replay (more voted keyframes: the replay reads them from HBM)
+constexpr int RM_NBMAX = 256;
 size_t rm_lds_bytes(int kfc) {
     const size_t a = ((size_t)(kfc + 1) * 4 + 15) & ~(size_t)15, b = ((size_t)kfc * 4 + 15) & ~(size_t)15;
-    return a + b + (((size_t)kfc + 15) & ~(size_t)15) + b;  // + the local keyframes' first map-point slots
+    // + the local keyframes' first map-point slots, + the staged neighbours
+    return a + b + (((size_t)kfc + 15) & ~(size_t)15) + b + 40 * (size_t)std::min(kfc, RM_NBMAX);
 }
 
 // map-point slots per thread kept in registers across the three slot passes
@@ -91,6 +95,7 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     int* lkf = reinterpret_cast<int*>(rm_lds + (((size_t)(A.kfc + 1) * 4 + 15) & ~(size_t)15));  // local keyframes
     uint8_t* mark = reinterpret_cast<uint8_t*>(lkf) + (((size_t)A.kfc * 4 + 15) & ~(size_t)15);
     int* kb = reinterpret_cast<int*>(mark + (((size_t)A.kfc + 15) & ~(size_t)15));  // kf_mp_off of local keyframe p
+    int* snb = kb + ((A.kfc + 3) & ~3);  // [min(kfc, RM_NBMAX)][10]: neighbour index, -1 none, -2 bad
     __shared__ int tmp[RM_T / 64];
     __shared__ unsigned long long s_best;
     __shared__ int s_nl;
@@ -134,18 +139,42 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     }
     __syncthreads();
     const int nk0 = nl;
-    // 3. neighbours (sequential replay on wave 0)
+    // 3. neighbours (sequential replay on wave 0). The voted keyframes' first
+    // 10 covisible neighbours and their bad flags are loaded by every thread
+    // at once into LDS first, so the replay's steps wait on LDS, not on three
+    // dependent HBM loads each
+    const bool staged = nk0 <= min(A.kfc, RM_NBMAX);
+    if (staged) {
+        for (int e = tid; e < 10 * nk0; e += RM_T) {
+            const int p = e / 10, j = e - 10 * p, kf = lkf[p];
+            const int o0 = M.kf_cov_off[kf], deg = min(10, M.kf_cov_off[kf + 1] - o0);
+            int nb = -1;
+            if (j < deg) {
+                nb = M.kf_cov[o0 + j];
+                if (M.kf_bad[nb]) nb = -2;
+            }
+            snb[e] = nb;
+        }
+        __syncthreads();
+    }
     if (tid < 64) {
         int n = nk0;
         for (int p = 0; p < nk0; p++) {
             if (n > 80) break;
-            const int kf = lkf[p];
-            const int o0 = M.kf_cov_off[kf], deg = min(10, M.kf_cov_off[kf + 1] - o0);
             int nb = -1;
             bool ok = false;
-            if (lane < deg) {
-                nb = M.kf_cov[o0 + lane];
-                ok = !M.kf_bad[nb] && !mark[nb];
+            if (staged) {
+                if (lane < 10) {
+                    nb = snb[10 * p + lane];
+                    ok = nb >= 0 && !mark[nb];
+                }
+            } else {
+                const int kf = lkf[p];
+                const int o0 = M.kf_cov_off[kf], deg = min(10, M.kf_cov_off[kf + 1] - o0);
+                if (lane < deg) {
+                    nb = M.kf_cov[o0 + lane];
+                    ok = !M.kf_bad[nb] && !mark[nb];
+                }
             }
             const unsigned long long b = __ballot(ok);
             if (b) {
