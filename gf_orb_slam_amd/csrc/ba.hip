@@ -663,16 +663,17 @@ __global__ __launch_bounds__(64 * BA_SW) void k_ba_spgemm(BAArena A) {
     const int ca = 16 * item.x + cl, cw = 16 * item.y + cl;
     // every k-step's operands in flight at once (an item holds at most
     // BA_KCH k-steps), then the MFMA chain
+    // (loads at clamped k-steps, unconditional: a load behind a branch has its
+    // result merged before the next one issues, one round trip per k-step)
     double a[BA_KCH], w[BA_KCH];
+    int ks[BA_KCH];
+#pragma unroll
+    for (int u = 0; u < BA_KCH; u++) ks[u] = kl[min(item.z + u, item.w - 1)];
 #pragma unroll
     for (int u = 0; u < BA_KCH; u++) {
-        a[u] = 0.0;
-        w[u] = 0.0;
-        if (item.z + u < item.w) {
-            const size_t r = (size_t)(4 * kl[item.z + u] + kr) * d.npad;
-            a[u] = Ht[r + ca];
-            w[u] = Wt[r + cw];
-        }
+        const size_t r = (size_t)(4 * ks[u] + kr) * d.npad;
+        a[u] = Ht[r + ca];
+        w[u] = Wt[r + cw];
     }
     d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -774,19 +775,43 @@ __global__ __launch_bounds__(BA_ST) void k_ba_solve(BAArena A) {
     for (int a = tid; a < d.nfree; a += BA_ST) sact[a] = A.f_act[d.f0 + a];
     __syncthreads();
     const double* Sg = A.Ssum + d.ss0;
-    for (int i = w; i < n; i += BA_ST / 64) {
-        const int a = i / 6;
-        for (int j = lane; j <= i; j += 64) {
-            const int c = j / 6;
-            double v;
-            if (!sact[a] || !sact[c]) {
-                v = (i == j) ? 1.0 : 0.0;
-            } else {
-                v = 0.0;
-                if (a == c) v = A.Hpp[(size_t)(d.f0 + a) * 36 + (i % 6) * 6 + (j % 6)] + (i == j ? lam : 0.0);
-                v = v - Sg[tri(i) + j];
+    // a wave's rows i = w, w + 16, ..., four at a time with their <= 3 column
+    // chunks: the batch's Sg / Hpp values loaded (clamped, unconditional)
+    // before any is used, one round trip per batch instead of one per chunk
+    constexpr int RB = 4, CPR = (BA_MAXN + 63) / 64;
+    for (int i0 = w; i0 < n; i0 += RB * (BA_ST / 64)) {
+        double sgv[RB][CPR], hpv[RB][CPR];
+#pragma unroll
+        for (int ri = 0; ri < RB; ri++) {
+            const int i = min(i0 + ri * (BA_ST / 64), n - 1), a = i / 6;
+#pragma unroll
+            for (int cj = 0; cj < CPR; cj++) {
+                const int j = min(lane + 64 * cj, i);
+                sgv[ri][cj] = Sg[tri(i) + j];
+                const int jc = min(max(j, 6 * a), 6 * a + 5);  // a column of i's own pose block
+                hpv[ri][cj] = A.Hpp[(size_t)(d.f0 + a) * 36 + (i % 6) * 6 + (jc % 6)];
             }
-            sL[tri(i) + j] = v;
+        }
+#pragma unroll
+        for (int ri = 0; ri < RB; ri++) {
+            const int i = i0 + ri * (BA_ST / 64);
+            if (i >= n) break;
+            const int a = i / 6;
+#pragma unroll
+            for (int cj = 0; cj < CPR; cj++) {
+                const int j = lane + 64 * cj;
+                if (j > i) break;
+                const int c = j / 6;
+                double v;
+                if (!sact[a] || !sact[c]) {
+                    v = (i == j) ? 1.0 : 0.0;
+                } else {
+                    v = 0.0;
+                    if (a == c) v = hpv[ri][cj] + (i == j ? lam : 0.0);
+                    v = v - sgv[ri][cj];
+                }
+                sL[tri(i) + j] = v;
+            }
         }
     }
     for (int i = tid; i < n; i += BA_ST) {
