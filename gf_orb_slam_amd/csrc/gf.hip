@@ -514,7 +514,9 @@ struct KpStaged {
 // those two holders alone (the first keypoint at the minimum distance, the
 // first other one at the second smallest), so a result stays exact until one
 // of its two holders is claimed.
-template <class KP>
+// MB > 1: the positions and descriptors of MB candidates are loaded together
+// (clamped indices, unconditional) and then walked in order.
+template <int MB = 1, class KP>
 __device__ void one_point_scan(const ActiveArgs& A, const FrameConst& fc, int f, int mpi, const int* cell_start,
                                const int* items, const int* claim, const KP& kps, int& outIdx, int& outDist,
                                int& holder1, int& holder2) {
@@ -531,27 +533,54 @@ __device__ void one_point_scan(const ActiveArgs& A, const FrameConst& fc, int f,
     if (!grid_window(fc, v.u, v.v, r, cx0, cx1, cy0, cy1)) return;
     const uint8_t* qd = A.mp_desc + ((long long)f * A.mp_cap + mpi) * 32;
     int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1, secondIdx = -1;
+    uint4 qa, qb;
+    if constexpr (MB > 1) {
+        qa = reinterpret_cast<const uint4*>(qd)[0];
+        qb = reinterpret_cast<const uint4*>(qd)[1];
+    }
     for (int ix = cx0; ix <= cx1; ix++) {
         const int s = cell_start[ix * GRID_ROWS + cy0], e = cell_start[ix * GRID_ROWS + cy1 + 1];
-        for (int t = s; t < e; t++) {
-            const int idx = items[t];
-            const float4 kp = kps.xyo(idx);
-            const int oct = __float_as_int(kp.z);
-            if (!level_ok(oct, pl - 1, pl)) continue;
-            if (fabsf(kp.x - v.u) > r || fabsf(kp.y - v.v) > r) continue;
-            if (claim[idx] >= 0) continue;
-            const int dist = hamming32(qd, kps.desc(idx));
-            if (dist < bestDist) {
-                bestDist2 = bestDist;
-                bestDist = dist;
-                bestLevel2 = bestLevel;
-                bestLevel = oct;
-                secondIdx = bestIdx;
-                bestIdx = idx;
-            } else if (dist < bestDist2) {
-                bestLevel2 = oct;
-                bestDist2 = dist;
-                secondIdx = idx;
+        for (int t0 = s; t0 < e; t0 += MB) {
+            int id[MB];
+            float4 kq[MB];
+            uint4 da[MB], db[MB];
+#pragma unroll
+            for (int u = 0; u < MB; u++) id[u] = items[MB > 1 ? min(t0 + u, e - 1) : t0];
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                kq[u] = kps.xyo(id[u]);
+                if constexpr (MB > 1) {
+                    const uint4* pd = reinterpret_cast<const uint4*>(kps.desc(id[u]));
+                    da[u] = pd[0];
+                    db[u] = pd[1];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < MB; u++) {
+                if (MB > 1 && t0 + u >= e) continue;
+                const int idx = id[u];
+                const float4 kp = kq[u];
+                const int oct = __float_as_int(kp.z);
+                if (!level_ok(oct, pl - 1, pl)) continue;
+                if (fabsf(kp.x - v.u) > r || fabsf(kp.y - v.v) > r) continue;
+                if (claim[idx] >= 0) continue;
+                int dist;
+                if constexpr (MB > 1)
+                    dist = hamming_regs(qa, qb, da[u], db[u]);
+                else
+                    dist = hamming32(qd, kps.desc(idx));
+                if (dist < bestDist) {
+                    bestDist2 = bestDist;
+                    bestDist = dist;
+                    bestLevel2 = bestLevel;
+                    bestLevel = oct;
+                    secondIdx = bestIdx;
+                    bestIdx = idx;
+                } else if (dist < bestDist2) {
+                    bestLevel2 = oct;
+                    bestDist2 = dist;
+                    secondIdx = idx;
+                }
             }
         }
     }
@@ -577,6 +606,10 @@ struct OnePre {  // one-point result against the frame's starting claims
 #endif
 // descriptors staged in LDS up to this capacity; 0 since r04 (see
 // SEQ_PRE_DESC_MAX in match.hip)
+// candidates whose loads the precompute's scan issues together
+#ifndef PRE_MB
+#define PRE_MB 2
+#endif
 #ifndef PRE_DESC_LDS_MAX
 #define PRE_DESC_LDS_MAX 0
 #endif
@@ -610,7 +643,7 @@ __global__ __launch_bounds__(PRE_THREADS) void k_onepoint_pre(ActiveArgs A, OneP
     const KpStaged src{X, dl ? (const uint8_t*)Ds : D};
     for (int i = tid; i < m; i += PRE_THREADS) {
         int mi, md, h1, h2;
-        one_point_scan(A, A.fc, f, i, cell_start, items, claim, src, mi, md, h1, h2);
+        one_point_scan<PRE_MB>(A, A.fc, f, i, cell_start, items, claim, src, mi, md, h1, h2);
         out[(long long)f * A.mp_cap + i] = OnePre{(int16_t)mi, (int16_t)(mi >= 0 ? md : 0), (int16_t)h1, (int16_t)h2};
     }
 }

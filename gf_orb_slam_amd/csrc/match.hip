@@ -219,6 +219,14 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
 #define MATCH_STAGE 0
 #endif
 #define MATCH_STAGE_LDS (96 * 1024)
+// candidates whose loads k_match issues together in its window walks
+#ifndef MATCH_MB
+#define MATCH_MB 2
+#endif
+// and their descriptors too (more registers a thread)
+#ifndef MATCH_DESC_AHEAD
+#define MATCH_DESC_AHEAD 0
+#endif
 __host__ __device__ __forceinline__ size_t match_base_lds(int kp_cap, int q_cap) {
     const int kc = kp_cap < KP_MAX ? kp_cap : KP_MAX, qc = q_cap < Q_MAX ? q_cap : Q_MAX;
     return (sizeof(int) * (NCELLS + 1 + 3 * (size_t)kc) + (size_t)qc + 15) & ~(size_t)15;
@@ -314,15 +322,22 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             if (!q.valid) continue;
             for (int ix = q.cx0; ix <= q.cx1; ix++) {
                 const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
-                for (int t = s; t < e; t++) {
-                    const int idx = items[t];
-                    if (claim[idx] >= 0) continue;
-                    float kx, ky;
-                    int ko;
-                    cand(idx, kx, ky, ko);
-                    if (!level_ok(ko, q.minL, q.maxL)) continue;
-                    if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
-                    atomicMin(&minU[idx], k);
+                for (int t0 = s; t0 < e; t0 += MATCH_MB) {
+                    // MATCH_MB candidates' loads issued together (clamped
+                    // indices, unconditional), then tested in order
+                    int id[MATCH_MB], ko[MATCH_MB];
+                    float kx[MATCH_MB], ky[MATCH_MB];
+#pragma unroll
+                    for (int u = 0; u < MATCH_MB; u++) id[u] = items[min(t0 + u, e - 1)];
+#pragma unroll
+                    for (int u = 0; u < MATCH_MB; u++) cand(id[u], kx[u], ky[u], ko[u]);
+#pragma unroll
+                    for (int u = 0; u < MATCH_MB; u++) {
+                        if (t0 + u >= e || claim[id[u]] >= 0) continue;
+                        if (!level_ok(ko[u], q.minL, q.maxL)) continue;
+                        if (fabsf(kx[u] - q.x) > q.r || fabsf(ky[u] - q.y) > q.r) continue;
+                        atomicMin(&minU[id[u]], k);
+                    }
                 }
             }
         }
@@ -334,33 +349,57 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             bool ok = true, near = false;
             int ncq = 0;
             if (q.valid) {
+                const uint4 qa = reinterpret_cast<const uint4*>(q.d)[0], qb = reinterpret_cast<const uint4*>(q.d)[1];
                 for (int ix = q.cx0; ix <= q.cx1 && ok; ix++) {
                     const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
-                    for (int t = s; t < e; t++) {
-                        const int idx = items[t];
-                        float kx, ky;
-                        int ko;
-                        cand(idx, kx, ky, ko);
-                        if (!level_ok(ko, q.minL, q.maxL)) continue;
-                        if (fabsf(kx - q.x) > q.r || fabsf(ky - q.y) > q.r) continue;
-                        near = true;  // GetFeaturesInArea lists it (claimed or not)
-                        ncq++;
-                        if (__hip_atomic_load(&claim[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
-                            continue;
-                        if (minU[idx] != k) {
-                            ok = false;
-                            break;
+                    for (int t0 = s; t0 < e && ok; t0 += MATCH_MB) {
+                        // positions and descriptors of MATCH_MB candidates
+                        // loaded together, then walked in the reference order
+                        int id[MATCH_MB], ko[MATCH_MB];
+                        float kx[MATCH_MB], ky[MATCH_MB];
+#if MATCH_DESC_AHEAD
+                        uint4 da[MATCH_MB], db[MATCH_MB];
+#endif
+#pragma unroll
+                        for (int u = 0; u < MATCH_MB; u++) id[u] = items[min(t0 + u, e - 1)];
+#pragma unroll
+                        for (int u = 0; u < MATCH_MB; u++) {
+                            cand(id[u], kx[u], ky[u], ko[u]);
+#if MATCH_DESC_AHEAD
+                            const uint4* pd = reinterpret_cast<const uint4*>(DD + (long long)id[u] * 32);
+                            da[u] = pd[0];
+                            db[u] = pd[1];
+#endif
                         }
-                        const int dist = hamming32(q.d, DD + (long long)idx * 32);
-                        if (dist < bestDist) {
-                            bestDist2 = bestDist;
-                            bestDist = dist;
-                            bestLevel2 = bestLevel;
-                            bestLevel = ko;
-                            bestIdx = idx;
-                        } else if (dist < bestDist2) {
-                            bestLevel2 = ko;
-                            bestDist2 = dist;
+#pragma unroll
+                        for (int u = 0; u < MATCH_MB; u++) {
+                            if (t0 + u >= e || !ok) continue;
+                            if (!level_ok(ko[u], q.minL, q.maxL)) continue;
+                            if (fabsf(kx[u] - q.x) > q.r || fabsf(ky[u] - q.y) > q.r) continue;
+                            near = true;  // GetFeaturesInArea lists it (claimed or not)
+                            ncq++;
+                            if (__hip_atomic_load(&claim[id[u]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= 0)
+                                continue;
+                            if (minU[id[u]] != k) {
+                                ok = false;
+                                continue;
+                            }
+#if MATCH_DESC_AHEAD
+                            const int dist = hamming_regs(qa, qb, da[u], db[u]);
+#else
+                            const uint4* pd = reinterpret_cast<const uint4*>(DD + (long long)id[u] * 32);
+                            const int dist = hamming_regs(qa, qb, pd[0], pd[1]);
+#endif
+                            if (dist < bestDist) {
+                                bestDist2 = bestDist;
+                                bestDist = dist;
+                                bestLevel2 = bestLevel;
+                                bestLevel = ko[u];
+                                bestIdx = id[u];
+                            } else if (dist < bestDist2) {
+                                bestLevel2 = ko[u];
+                                bestDist2 = dist;
+                            }
                         }
                     }
                 }
@@ -474,6 +513,9 @@ struct SeqPre {
 #define SEQ_PRE_DESC_MAX 0
 #endif
 #define SEQ_PRE_G 4  // lanes per query
+#ifndef SEQ_PRE_MB
+#define SEQ_PRE_MB 1  // candidates a lane loads together (2: 81 VGPRs, no faster in the step)
+#endif
 __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, FrameConst fc,
                                                                    SeqPre* __restrict__ out) {
     gfd::track_prio();
@@ -520,25 +562,45 @@ __global__ __launch_bounds__(SEQ_PRE_THREADS) void k_match_seq_pre(MatchArgs A, 
         unsigned long long key[4] = {NONE, NONE, NONE, NONE};
         int nc = 0;
         if (live && q.valid) {
+            const uint4 qa = reinterpret_cast<const uint4*>(q.d)[0], qb = reinterpret_cast<const uint4*>(q.d)[1];
             int t0 = 0;  // candidate order of the column's first item
             for (int ix = q.cx0; ix <= q.cx1; ix++) {
                 const int s0 = cell_start[ix * GRID_ROWS + q.cy0], s1 = cell_start[ix * GRID_ROWS + q.cy1 + 1];
-                for (int t = s0 + g; t < s1; t += SEQ_PRE_G) {
-                    const int idx = items[t];
-                    const float4 kp = X[idx];
-                    const int oct = __float_as_int(kp.z);
-                    if (!level_ok(oct, q.minL, q.maxL) || fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r) continue;
-                    na++;
-                    if (claim[idx] >= 0) continue;
-                    const int dist = hamming32(q.d, DD + (long long)idx * 32);
-                    nc++;
-                    const unsigned long long kk = ((unsigned long long)dist << 48) |
-                                                  ((unsigned long long)(t0 + t - s0) << 16) | (unsigned)idx;
-                    if (kk < key[3]) {
-                        key[3] = kk;
-                        if (key[3] < key[2]) { const unsigned long long x = key[2]; key[2] = key[3]; key[3] = x; }
-                        if (key[2] < key[1]) { const unsigned long long x = key[1]; key[1] = key[2]; key[2] = x; }
-                        if (key[1] < key[0]) { const unsigned long long x = key[0]; key[0] = key[1]; key[1] = x; }
+                for (int tb = s0 + g; tb < s1; tb += SEQ_PRE_G * SEQ_PRE_MB) {
+                    // SEQ_PRE_MB of this lane's candidates: positions and
+                    // descriptors loaded together (clamped, unconditional)
+                    int id[SEQ_PRE_MB];
+                    float4 kq[SEQ_PRE_MB];
+                    uint4 da[SEQ_PRE_MB], db[SEQ_PRE_MB];
+#pragma unroll
+                    for (int u = 0; u < SEQ_PRE_MB; u++) id[u] = items[min(tb + u * SEQ_PRE_G, s1 - 1)];
+#pragma unroll
+                    for (int u = 0; u < SEQ_PRE_MB; u++) {
+                        kq[u] = X[id[u]];
+                        const uint4* pd = reinterpret_cast<const uint4*>(DD + (long long)id[u] * 32);
+                        da[u] = pd[0];
+                        db[u] = pd[1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < SEQ_PRE_MB; u++) {
+                        const int t = tb + u * SEQ_PRE_G, idx = id[u];
+                        if (t >= s1) continue;
+                        const float4 kp = kq[u];
+                        const int oct = __float_as_int(kp.z);
+                        if (!level_ok(oct, q.minL, q.maxL) || fabsf(kp.x - q.x) > q.r || fabsf(kp.y - q.y) > q.r)
+                            continue;
+                        na++;
+                        if (claim[idx] >= 0) continue;
+                        const int dist = hamming_regs(qa, qb, da[u], db[u]);
+                        nc++;
+                        const unsigned long long kk = ((unsigned long long)dist << 48) |
+                                                      ((unsigned long long)(t0 + t - s0) << 16) | (unsigned)idx;
+                        if (kk < key[3]) {
+                            key[3] = kk;
+                            if (key[3] < key[2]) { const unsigned long long x = key[2]; key[2] = key[3]; key[3] = x; }
+                            if (key[2] < key[1]) { const unsigned long long x = key[1]; key[1] = key[2]; key[2] = x; }
+                            if (key[1] < key[0]) { const unsigned long long x = key[0]; key[0] = key[1]; key[1] = x; }
+                        }
                     }
                 }
                 t0 += s1 - s0;

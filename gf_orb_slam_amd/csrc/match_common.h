@@ -33,6 +33,11 @@ __device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+__device__ __forceinline__ int hamming_regs(uint4 a0, uint4 a1, uint4 b0, uint4 b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
 __device__ __forceinline__ void transform3(const float* T, const float* P, float* Pc) {
 #pragma unroll
     for (int r = 0; r < 3; r++) {
