@@ -479,34 +479,68 @@ __global__ __launch_bounds__(256) void k_fe_viz_exclude(FeDev D) {
     }
 }
 
+constexpr int END_U = 4;
 __global__ __launch_bounds__(256) void k_fe_end(FeDev D) {
     const int b = blockIdx.x, t = threadIdx.x;
     const bool working = D.gate_post[b];  // mState == WORKING (Tracking.cc:854)
     const int n = working ? D.nkp[b] : 0;
     const long long o = (long long)b * D.cap;
-    for (int i = t; i < n; i += 256) {
-        int mp = D.kp2mp[o + i];
-        const uint8_t ou = D.outl[o + i];
-        if (mp >= 0 && ou) mp = -1;  // Tracking.cc:899-905 (mvbOutlier stays set)
-        D.kp2mp[o + i] = mp;
-        D.last_kp2mp[o + i] = mp;
-        D.last_outl[o + i] = ou;
-        D.last_kps[o + i] = D.kps[o + i];
-        float* p = D.last_pos + 3 * (o + i);
-        if (mp >= 0) {
-            const gf_map_point& P = D.gmap[(long long)b * D.M + mp];
-            p[0] = P.pos[0];
-            p[1] = P.pos[1];
-            p[2] = P.pos[2];
-        } else {
-            p[0] = p[1] = p[2] = 0.f;
+    // each loop: END_U elements' loads (clamped, unconditional), then their
+    // stores (the stores may alias the next loads, so a plain loop would wait
+    // on every element)
+    for (int i0 = t; i0 < n; i0 += 256 * END_U) {
+        int mp[END_U];
+        uint8_t ou[END_U];
+        gf_keypoint kp[END_U];
+        float3 pos[END_U];
+#pragma unroll
+        for (int u = 0; u < END_U; u++) {
+            const long long i = o + min(i0 + 256 * u, n - 1);
+            mp[u] = D.kp2mp[i];
+            ou[u] = D.outl[i];
+            kp[u] = D.kps[i];
+        }
+#pragma unroll
+        for (int u = 0; u < END_U; u++) {
+            const gf_map_point& P = D.gmap[(long long)b * D.M + max(mp[u], 0)];
+            pos[u] = make_float3(P.pos[0], P.pos[1], P.pos[2]);
+        }
+#pragma unroll
+        for (int u = 0; u < END_U; u++) {
+            const int i = i0 + 256 * u;
+            if (i >= n) continue;
+            const int m1 = mp[u] >= 0 && ou[u] ? -1 : mp[u];  // Tracking.cc:899-905 (mvbOutlier stays set)
+            D.kp2mp[o + i] = m1;
+            D.last_kp2mp[o + i] = m1;
+            D.last_outl[o + i] = ou[u];
+            D.last_kps[o + i] = kp[u];
+            float* p = D.last_pos + 3 * (o + i);
+            const bool on = m1 >= 0;
+            p[0] = on ? pos[u].x : 0.f;
+            p[1] = on ? pos[u].y : 0.f;
+            p[2] = on ? pos[u].z : 0.f;
         }
     }
     const uint4* ds = (const uint4*)(D.desc + o * 32);
     uint4* dd = (uint4*)(D.last_desc + o * 32);
-    for (int i = t; i < 2 * n; i += 256) dd[i] = ds[i];
+    for (int i0 = t; i0 < 2 * n; i0 += 256 * END_U) {
+        uint4 v[END_U];
+#pragma unroll
+        for (int u = 0; u < END_U; u++) v[u] = ds[min(i0 + 256 * u, 2 * n - 1)];
+#pragma unroll
+        for (int u = 0; u < END_U; u++)
+            if (i0 + 256 * u < 2 * n) dd[i0 + 256 * u] = v[u];
+    }
     const int m = D.gnmp[b];
-    for (int i = t; i < m; i += 256) D.gupd[(long long)b * D.M + i] -= 1;
+    int32_t* gu = D.gupd + (long long)b * D.M;
+    for (int i0 = t; i0 < m; i0 += 256 * END_U) {
+        int v[END_U];
+#pragma unroll
+        for (int u = 0; u < END_U; u++) v[u] = gu[min(i0 + 256 * u, m - 1)];
+#pragma unroll
+        for (int u = 0; u < END_U; u++)
+            if (i0 + 256 * u < m) gu[i0 + 256 * u] = v[u] - 1;
+    }
     if (t == 0) {
         if (working) {  // mLastFrame = Frame(mCurrentFrame) (:910)
             D.last_nkp[b] = n;
@@ -628,42 +662,31 @@ struct MapArrays {
     int32_t* upd;
 };
 
-// Per-point rows of one map array, W 32-bit words per point, for the local
-// points [k0, k0 + np) of a stream: gather (dst local <- src map point lm[k])
-// or scatter (dst map point lm[k] <- src local). Eight independent loads in
-// flight per thread before the stores: a plain per-element loop leaves the
-// copy latency-bound at ~1.3 TB/s.
-template <int W>
-__device__ __forceinline__ void copy_rows(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
-                                          const int32_t* __restrict__ lm, long long o, int k0, int np, bool gather) {
-    constexpr int U = 8;
-    const int t = threadIdx.x, nw = np * W;
-    for (int w0 = t; w0 < nw; w0 += 256 * U) {
-        uint32_t v[U];
-        long long at[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int w = w0 + u * 256;
-            at[u] = -1;
-            if (w < nw) {
-                const int p = w / W, e = w - p * W, k = k0 + p;
-                const long long g = o + lm[k], l = o + k;
-                v[u] = src[(gather ? g : l) * W + e];
-                at[u] = (gather ? l : g) * W + e;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (at[u] >= 0) dst[at[u]] = v[u];
-    }
-}
-
+// Per-point rows of the map arrays for the local points [k0, k0 + np) of a
+// stream (np <= ROWS_PER_BLOCK): gather (dst local <- src map point lm[k]) or
+// scatter (dst map point lm[k] <- src local). Every array's row block fits one
+// word per thread, so a workgroup issues all its arrays' loads (clamped,
+// unconditional) before the first store.
 constexpr int ROWS_PER_BLOCK = 32;
+constexpr int IX_U = 4;  // index conversions: loads in flight per thread
 
+struct RowWord {
+    uint32_t v;
+    long long at;  // destination word, -1: none
+};
 template <int W, typename T>
-__device__ __forceinline__ void rows(T* dst, const T* src, const int32_t* lm, long long o, int k0, int np,
-                                     bool gather) {
-    copy_rows<W>(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src), lm, o, k0, np, gather);
+__device__ __forceinline__ RowWord row_load(const T* src_, const int32_t* lm, long long o, int k0, int np,
+                                            bool gather) {
+    static_assert(W * ROWS_PER_BLOCK <= 256, "one word per thread");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(src_);
+    const int nw = np * W, w0 = threadIdx.x, w = min(w0, nw - 1);
+    const int p = w / W, e = w - p * W, k = k0 + p;
+    const long long g = o + lm[k], l = o + k;
+    return RowWord{src[(gather ? g : l) * W + e], w0 < nw ? (gather ? l : g) * W + e : -1};
+}
+template <typename T>
+__device__ __forceinline__ void row_store(T* dst, const RowWord& r) {
+    if (r.at >= 0) reinterpret_cast<uint32_t*>(dst)[r.at] = r.v;
 }
 
 // Index conversion for the step: g2l of the local points, the frame's matches
@@ -674,7 +697,16 @@ __device__ void gather_index(const FeDev& D, int b, int32_t* lnmp) {
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    for (int k = t; k < n; k += 256) D.g2l[o + lm[k]] = k;
+    // batches of IX_U independent loads, then their stores (the stores may
+    // alias the next loads, so a plain loop waits on every load)
+    for (int k0 = t; k0 < n; k0 += 256 * IX_U) {
+        int v[IX_U];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) v[u] = lm[min(k0 + 256 * u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++)
+            if (k0 + 256 * u < n) D.g2l[o + v[u]] = k0 + 256 * u;
+    }
     if (t == 0) {
         lnmp[b] = n;
         stat(D, GF_ST_NLOCAL)[b] = n;
@@ -682,12 +714,19 @@ __device__ void gather_index(const FeDev& D, int b, int32_t* lnmp) {
     __syncthreads();
     const long long ko = (long long)b * D.cap;
     const int nk = D.nkp_tl[b];
-    for (int i = t; i < nk; i += 256) {
-        const int mp = D.kp2mp[ko + i];
-        if (mp < 0) continue;
-        const int l = D.g2l[o + mp];
-        D.kp2mp[ko + i] = l;
-        if (l < 0) D.score[ko + i] = 999;
+    for (int i0 = t; i0 < nk; i0 += 256 * IX_U) {
+        int mp[IX_U], l[IX_U];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) mp[u] = D.kp2mp[ko + min(i0 + 256 * u, nk - 1)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) l[u] = D.g2l[o + max(mp[u], 0)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) {
+            const int i = i0 + 256 * u;
+            if (i >= nk || mp[u] < 0) continue;
+            D.kp2mp[ko + i] = l[u];
+            if (l[u] < 0) D.score[ko + i] = 999;
+        }
     }
 }
 
@@ -697,15 +736,37 @@ __device__ void scatter_index(const FeDev& D, int b) {
     const int n = D.nlm[b];
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    for (int k = t; k < n; k += 256) D.g2l[o + lm[k]] = -1;
+    for (int k0 = t; k0 < n; k0 += 256 * IX_U) {
+        int v[IX_U];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) v[u] = lm[min(k0 + 256 * u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++)
+            if (k0 + 256 * u < n) D.g2l[o + v[u]] = -1;
+    }
     const long long ko = (long long)b * D.cap;
     const int nk = D.nkp_tl[b];
-    for (int i = t; i < nk; i += 256) {
-        const int l = D.kp2mp[ko + i];
-        if (l >= 0) D.kp2mp[ko + i] = lm[l];
+    for (int i0 = t; i0 < nk; i0 += 256 * IX_U) {
+        int l[IX_U], g[IX_U];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) l[u] = D.kp2mp[ko + min(i0 + 256 * u, nk - 1)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) g[u] = lm[max(l[u], 0)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++)
+            if (i0 + 256 * u < nk && l[u] >= 0) D.kp2mp[ko + i0 + 256 * u] = g[u];
     }
     const int nl = stat(D, GF_ST_NLEFT)[b];
-    for (int j = t; j < nl; j += 256) D.left[o + j] = lm[D.left[o + j]];
+    for (int j0 = t; j0 < nl; j0 += 256 * IX_U) {
+        int l[IX_U], g[IX_U];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) l[u] = D.left[o + min(j0 + 256 * u, nl - 1)];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++) g[u] = lm[l[u]];
+#pragma unroll
+        for (int u = 0; u < IX_U; u++)
+            if (j0 + 256 * u < nl) D.left[o + j0 + 256 * u] = g[u];
+    }
 }
 
 // The local map (grid: 1 + point chunks x streams): workgroup 0 converts the
@@ -722,11 +783,16 @@ __global__ __launch_bounds__(256) void k_fe_gather(FeDev D, MapArrays G, MapArra
     const int np = min(ROWS_PER_BLOCK, n - k0);
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    rows<sizeof(gf_map_point) / 4>((gf_map_point*)L.map, G.map, lm, o, k0, np, true);
-    rows<8>((uint8_t*)L.desc, G.desc, lm, o, k0, np, true);
-    rows<3>((float*)L.pos, G.pos, lm, o, k0, np, true);
-    rows<sizeof(gf_mp_view) / 4>(L.views, G.views, lm, o, k0, np, true);
-    rows<1>(L.upd, G.upd, lm, o, k0, np, true);
+    const RowWord rm = row_load<sizeof(gf_map_point) / 4>(G.map, lm, o, k0, np, true);
+    const RowWord rd = row_load<8>(G.desc, lm, o, k0, np, true);
+    const RowWord rp = row_load<3>(G.pos, lm, o, k0, np, true);
+    const RowWord rv = row_load<sizeof(gf_mp_view) / 4>(G.views, lm, o, k0, np, true);
+    const RowWord ru = row_load<1>(G.upd, lm, o, k0, np, true);
+    row_store((gf_map_point*)L.map, rm);
+    row_store((uint8_t*)L.desc, rd);
+    row_store((float*)L.pos, rp);
+    row_store(L.views, rv);
+    row_store(L.upd, ru);
 }
 
 // Back to the stream's map: workgroup 0 converts the indices, the others
@@ -744,8 +810,10 @@ __global__ __launch_bounds__(256) void k_fe_scatter(FeDev D, MapArrays G, MapArr
     const int np = min(ROWS_PER_BLOCK, n - k0);
     const long long o = (long long)b * D.M;
     const int32_t* lm = D.lmp + o;
-    rows<sizeof(gf_mp_view) / 4>(G.views, L.views, lm, o, k0, np, false);
-    rows<1>(G.upd, L.upd, lm, o, k0, np, false);
+    const RowWord rv = row_load<sizeof(gf_mp_view) / 4>(L.views, lm, o, k0, np, false);
+    const RowWord ru = row_load<1>(L.upd, lm, o, k0, np, false);
+    row_store(G.views, rv);
+    row_store(G.upd, ru);
 }
 
 __global__ void k_fe_boot_begin(FeDev D) {
