@@ -224,6 +224,10 @@ __device__ void rotation_filter(const MatchArgs& A, int f, int nq, const gf_keyp
 #define MATCH_MB 2
 #endif
 // and their descriptors too (more registers a thread)
+// the thread's first query kept in registers over the claim rounds
+#ifndef MATCH_QCACHE
+#define MATCH_QCACHE 0
+#endif
 #ifndef MATCH_DESC_AHEAD
 #define MATCH_DESC_AHEAD 0
 #endif
@@ -309,6 +313,17 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
     __syncthreads();
 
     // ---- claim-resolution rounds
+#if MATCH_QCACHE
+    // the thread's first query, kept in registers over the rounds
+    Query q0;
+    q0.valid = false;
+    q0.cx0 = 1;
+    q0.cx1 = 0;
+    if (tid < nq) q0 = make_query(A, fc, f, tid);
+#define MATCH_Q(k) ((k) == tid ? q0 : make_query(A, fc, f, (k)))
+#else
+#define MATCH_Q(k) make_query(A, fc, f, (k))
+#endif
     int rounds = 0;
     while (true) {
         for (int i = tid; i < n; i += MATCH_THREADS) minU[i] = INT_MAX;
@@ -318,7 +333,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
             if (clocked && rounds == 0)  // per point, from the matcher's start
                 rec[A.ck_off + k] = gfd::ck_elapsed(s_now0, A.ck_syn ? A.ck_syn + 2 : nullptr, k);
             if (done[k]) continue;
-            const Query q = make_query(A, fc, f, k);
+            const Query q = MATCH_Q(k);
             if (!q.valid) continue;
             for (int ix = q.cx0; ix <= q.cx1; ix++) {
                 const int s = cell_start[ix * GRID_ROWS + q.cy0], e = cell_start[ix * GRID_ROWS + q.cy1 + 1];
@@ -344,7 +359,7 @@ __global__ __launch_bounds__(MATCH_THREADS) void k_match(MatchArgs A, FrameConst
         __syncthreads();
         for (int k = tid; k < nq; k += MATCH_THREADS) {
             if (done[k]) continue;
-            const Query q = make_query(A, fc, f, k);
+            const Query q = MATCH_Q(k);
             int bestDist = INT_MAX, bestLevel = -1, bestDist2 = INT_MAX, bestLevel2 = -1, bestIdx = -1;
             bool ok = true, near = false;
             int ncq = 0;

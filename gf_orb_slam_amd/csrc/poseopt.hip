@@ -49,6 +49,9 @@ struct GatherArgs {
     int gate_min;
 };
 
+#ifndef GATHER_U
+#define GATHER_U 4
+#endif
 // Ordered compaction of the matched keypoints of frame f (one wave).
 __device__ __forceinline__ void gather_frame(const GatherArgs& G, int f) {
     const int l = threadIdx.x;
@@ -59,28 +62,48 @@ __device__ __forceinline__ void gather_frame(const GatherArgs& G, int f) {
     const int n = G.nkps[f];
     const size_t kb = (size_t)f * G.kp_stride;
     int cnt = 0;
-    for (int base = 0; base < n; base += 64) {
-        const int i = base + l;
-        int mp = -1;
-        if (i < n) mp = G.kp2mp[kb + i];
-        const bool on = mp >= 0;
-        const unsigned long long m = __ballot(on);
-        const int pos = cnt + __popcll(m & ((1ull << l) - 1ull));
-        if (on) {
-            const gf_keypoint k = G.kps[kb + i];
-            const gf_map_point& P = G.map[(size_t)f * G.map_stride + mp];
-            gf_pose_edge e;
-            e.X[0] = P.pos[0];
-            e.X[1] = P.pos[1];
-            e.X[2] = P.pos[2];
-            e.z[0] = k.x;
-            e.z[1] = k.y;
-            const int oc = min(max(k.octave, 0), G.nlevels - 1);
-            e.inv_sigma2 = G.inv_sigma2[oc];
-            G.edges[kb + pos] = e;
-            G.edge_kp[kb + pos] = i;
+    // GATHER_U rows of 64 keypoints a pass: their loads (clamped,
+    // unconditional) issue together, then the compaction and the stores
+    for (int base = 0; base < n; base += 64 * GATHER_U) {
+        int mp[GATHER_U];
+        float kx[GATHER_U], ky[GATHER_U];
+        int ko[GATHER_U];
+        float X[GATHER_U][3];
+#pragma unroll
+        for (int u = 0; u < GATHER_U; u++) {
+            const size_t i = kb + min(base + 64 * u + l, n - 1);
+            mp[u] = G.kp2mp[i];
+            kx[u] = G.kps[i].x;
+            ky[u] = G.kps[i].y;
+            ko[u] = G.kps[i].octave;
         }
-        cnt += __popcll(m);
+#pragma unroll
+        for (int u = 0; u < GATHER_U; u++) {
+            const gf_map_point& P = G.map[(size_t)f * G.map_stride + max(mp[u], 0)];
+            X[u][0] = P.pos[0];
+            X[u][1] = P.pos[1];
+            X[u][2] = P.pos[2];
+        }
+#pragma unroll
+        for (int u = 0; u < GATHER_U; u++) {
+            const int i = base + 64 * u + l;
+            const bool on = i < n && mp[u] >= 0;
+            const unsigned long long m = __ballot(on);
+            const int pos = cnt + __popcll(m & ((1ull << l) - 1ull));
+            if (on) {
+                gf_pose_edge e;
+                e.X[0] = X[u][0];
+                e.X[1] = X[u][1];
+                e.X[2] = X[u][2];
+                e.z[0] = kx[u];
+                e.z[1] = ky[u];
+                const int oc = min(max(ko[u], 0), G.nlevels - 1);
+                e.inv_sigma2 = G.inv_sigma2[oc];
+                G.edges[kb + pos] = e;
+                G.edge_kp[kb + pos] = i;
+            }
+            cnt += __popcll(m);
+        }
     }
     if (l == 0) G.nedges[f] = cnt;
 }
