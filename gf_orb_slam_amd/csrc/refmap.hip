@@ -88,6 +88,9 @@ __device__ int scan_1024(int v, int* tmp, int& total) {
     return base + x - v;
 }
 
+#ifndef RM_OB
+#define RM_OB 4  // a point's observations loaded together in the votes
+#endif
 __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     gfd::track_prio();
     extern __shared__ __align__(16) uint8_t rm_lds[];
@@ -111,14 +114,27 @@ __global__ __launch_bounds__(RM_T) void k_update_reference(RefArgs A) {
     if (tid == 0) s_best = 0ull;
     __syncthreads();
     // 1. votes
+    // the point's flag and observation range loaded together (clamped,
+    // unconditional), its observations RM_OB at a time
     for (int i = tid; i < nkp; i += RM_T) {
         const int m = fm[i];
+        if (M.nmp <= 0) continue;  // no points: no matches either
+        const int mc = min(max(m, 0), M.nmp - 1);
+        const bool bad = M.mp_bad[mc] != 0;
+        const int o0 = M.mp_obs_off[mc], o1 = M.mp_obs_off[mc + 1];
         if (m < 0) continue;
-        if (M.mp_bad[m]) {
+        if (bad) {
             fm[i] = -1;
             continue;
         }
-        for (int o = M.mp_obs_off[m]; o < M.mp_obs_off[m + 1]; o++) atomicAdd(&cnt[M.mp_obs[o]], 1);
+        for (int o = o0; o < o1; o += RM_OB) {
+            int kq[RM_OB];
+#pragma unroll
+            for (int u = 0; u < RM_OB; u++) kq[u] = M.mp_obs[min(o + u, o1 - 1)];
+#pragma unroll
+            for (int u = 0; u < RM_OB; u++)
+                if (o + u < o1) atomicAdd(&cnt[kq[u]], 1);
+        }
     }
     __syncthreads();
     // 2. voted, non-bad keyframes in index order; pKFmax

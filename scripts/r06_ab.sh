@@ -19,7 +19,7 @@ for v in ${VARS//,/ }; do
   python - "$O/$v.json" "$v" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1])); k = d["kernels"]
-sel = ["k_active_match", "k_blur_fast", "k_match", "k_pose_opt_frames", "k_fast_cells", "k_describe", "k_fe_gather", "k_onepoint_pre"]
+sel = ["k_active_match", "k_blur_fast", "k_match", "k_pose_opt_frames", "k_update_reference", "k_describe", "k_fe_gather", "k_onepoint_pre"]
 print(sys.argv[2], d["value"], d["ms_per_step"], d.get("single_stream", {}).get("ms_per_frame"),
       {n: k[n]["avg_ms"] for n in sel if n in k})
 PY
